@@ -1,0 +1,190 @@
+/*
+ * redisson_sketch.h -- C ABI of the MI355X sketch engine (libredisson_sketch.so).
+ *
+ * Drop-in boundary for Redisson's probabilistic-structure path.  Every entry
+ * point replaces a (RedisCommand, key, params) triple that Redisson's L3
+ * executor would otherwise send over Netty to redis-server
+ * (M:command/CommandAsyncService.java:378 async(...), and the batch hook
+ * M:command/CommandBatchService.java:91-111,184).  M: = /root/reference/src/
+ * main/java/org/redisson/.  The Java side (JNI shim) applies
+ * the codec / param-encoding rules first (M:client/handler/CommandEncoder.java:
+ * 73-94), so every "element" below is already the exact byte string Redis
+ * would have hashed.
+ *
+ * Conventions
+ *   - Plain pointers and sizes only.  "Host" buffers are caller-owned and only
+ *     read/written during the call.  Functions suffixed _dev take DEVICE
+ *     pointers (already resident in HBM on this context's GPU) and enqueue on
+ *     the context's stream; they return after completion unless noted.
+ *   - Variable-length byte strings are passed as (off u64[n+1], bytes u8[]):
+ *     item i = bytes[off[i] .. off[i+1]).  Device byte buffers must have 8
+ *     readable bytes of padding after the last item.
+ *   - Every function returns SK_OK (0) or a negative SK_E* status;
+ *     sk_last_error() gives the Redis-compatible message (Java maps it to
+ *     RedisException, M:client/handler/CommandDecoder.java:239-241).
+ *   - A context is bound to one GPU.  Calls on one context are serialized
+ *     internally (thread-safe).  Multi-GPU: one context per device, keys
+ *     routed by sk_owner() = calcSlot(key) % n_gpus (north_star partitioner).
+ */
+#ifndef REDISSON_SKETCH_H
+#define REDISSON_SKETCH_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes (message text = what redis-server / Redisson raises) ---- */
+#define SK_OK 0
+#define SK_EWRONGTYPE (-1) /* "WRONGTYPE Operation against a key holding the wrong kind of value"
+                              (HLL ops: "Key is not a valid HyperLogLog string value.") */
+#define SK_ERANGE (-2)     /* "ERR bit offset is not an integer or out of range" */
+#define SK_ECONFIG (-3)    /* "Bloom filter config has been changed" (M:RedissonBloomFilter.java:108,183) */
+#define SK_ENOTINIT (-4)   /* "Bloom filter is not initialized!" (IllegalStateException, :217,284) */
+#define SK_EDEVICE (-5)    /* HIP runtime / device failure */
+#define SK_EINVAL (-6)     /* bad argument */
+#define SK_ENOMEM (-7)     /* device or host allocation failed */
+#define SK_ESYNTAX (-8)    /* "ERR BITOP NOT must be called with a single source key." */
+#define SK_ETOOBIG (-9)    /* "Bloom filter can't be greater than 4294967294. ..." (IllegalArgumentException, :72-74) */
+
+#define SK_TYPE_NONE 0
+#define SK_TYPE_HLL 1    /* string holding a HyperLogLog (PFADD/PFMERGE created it) */
+#define SK_TYPE_STRING 2 /* plain string: RBitSet / Bloom filter bit array */
+
+#define SK_BITOP_AND 0
+#define SK_BITOP_OR 1
+#define SK_BITOP_XOR 2
+#define SK_BITOP_NOT 3
+
+#define SK_HLL_REGISTERS 16384
+#define SK_HLL_DENSE_SIZE (16 + 12288) /* "HYLL" header + 6-bit dense registers */
+
+typedef struct sk_ctx sk_ctx;
+
+typedef struct sk_config {
+    int device;              /* HIP device ordinal */
+    int redis_major;         /* 3 = redis 3.2.0 semantics (reference CI pin, R:.travis.yml:23-24);
+                                >= 5: HLL_Q sentinel in hllPatLen + Ertl estimator */
+    uint64_t max_bit_offset; /* exclusive SETBIT/GETBIT offset limit; 0 -> 2^32 (redis 3.2: 512 MB strings) */
+    uint64_t hll_capacity;   /* initial HLL slab capacity (16 KiB each); 0 -> 1024 */
+    uint64_t max_batch;      /* largest single device batch (elements); 0 -> 1<<22 */
+} sk_config;
+
+/* ---- lifecycle ---- */
+int sk_open(const sk_config *cfg, sk_ctx **out);
+int sk_close(sk_ctx *ctx);
+const char *sk_last_error(sk_ctx *ctx);
+const char *sk_strerror(int status);
+void *sk_stream(sk_ctx *ctx); /* the context's hipStream_t (for event timing) */
+int sk_sync(sk_ctx *ctx);
+
+/* ---- host-only helpers (no GPU needed) ---- */
+/* CRC16-XMODEM, M:connection/CRC16.java:55-61 */
+uint32_t sk_crc16(const uint8_t *bytes, uint64_t len);
+/* ClusterConnectionManager.calcSlot, M:cluster/ClusterConnectionManager.java:543-558;
+ * -1 where Java's substring() throws (a '}' before the '{', or none). */
+int32_t sk_calc_slot(const uint8_t *key, uint64_t len);
+/* partitioner: owning GPU = calcSlot % n_gpus (-1 if calcSlot throws) */
+int32_t sk_owner(const uint8_t *key, uint64_t len, int32_t n_gpus);
+/* RedissonBloomFilter.optimalNumOfBits / optimalNumOfHashFunctions (:69-78) */
+int64_t sk_bloom_optimal_bits(int64_t expected_insertions, double false_probability);
+int32_t sk_bloom_optimal_k(int64_t expected_insertions, int64_t bits);
+/* hllCount from a 64-bin register histogram (exact when no register >= 40
+ * under redis 3.x; always under >= 5).  encoding 0 sparse / 1 dense / 2 raw. */
+uint64_t sk_hll_estimate_hist(const uint32_t *hist64, int redis_major);
+
+/* ---- key directory (one keyspace per context, like one redis db) ---- */
+/* type of key (SK_TYPE_*) */
+int sk_type(sk_ctx *ctx, const uint8_t *key, uint64_t len, int *out_type);
+/* DEL k1..kn -> number removed (RedissonObject.delete / RBitSet.clear, M:RedissonBitSet.java:250) */
+int sk_del(sk_ctx *ctx, uint32_t n, const uint64_t *key_off, const uint8_t *key_bytes, uint64_t *out_removed);
+/* resolve HLL names to slab ids, creating empty HLLs for missing names (what
+ * PFADD / PFMERGE do).  out_created[i] = 1 if this call created it. */
+int sk_hll_resolve(sk_ctx *ctx, uint32_t n, const uint64_t *key_off, const uint8_t *key_bytes,
+                   uint32_t *out_ids, uint8_t *out_created);
+
+/* ---- RHyperLogLog (M:RedissonHyperLogLog.java:66-97) ---- */
+/* Batch of PFADD commands in RBatch order.  Command c targets key c and adds
+ * elem_counts[c] elements (consecutive in elem_off/elem_bytes).  out_changed[c]
+ * = PFADD reply (1 if a register rose or the key was created), with exact
+ * sequential semantics inside the batch. */
+int sk_pfadd(sk_ctx *ctx, uint32_t n_cmds, const uint64_t *key_off, const uint8_t *key_bytes,
+             const uint32_t *elem_counts, const uint64_t *elem_off, const uint8_t *elem_bytes,
+             uint8_t *out_changed);
+/* PFADD of one element per command, keys pre-resolved to slab ids (all
+ * existing); device-resident inputs.  d_out_changed u8[n] on device. */
+int sk_pfadd_dev(sk_ctx *ctx, uint64_t n, const uint32_t *d_key_ids, const uint64_t *d_elem_off,
+                 const uint8_t *d_elem_bytes, uint64_t elem_bytes_len, uint8_t *d_out_changed);
+/* Batch of PFCOUNT commands: command c counts the union of nkeys[c] keys
+ * (1 = RHyperLogLog.count, >1 = countWith).  Missing keys count as empty. */
+int sk_pfcount(sk_ctx *ctx, uint32_t n_cmds, const uint32_t *nkeys, const uint64_t *key_off,
+               const uint8_t *key_bytes, int64_t *out_counts);
+/* per-key 64-bin register histograms for slab ids (device in / device out u32[n*64]) */
+int sk_hll_histogram_dev(sk_ctx *ctx, uint64_t n, const uint32_t *d_key_ids, uint32_t *d_hist);
+/* PFMERGE dest src1..srcn (dest included in the max, becomes dense) */
+int sk_pfmerge(sk_ctx *ctx, const uint8_t *dest, uint64_t dest_len, uint32_t n_src,
+               const uint64_t *src_off, const uint8_t *src_bytes);
+/* union of n slab ids into a 16384-byte register array on device (d_out);
+ * building block of the cross-GPU merge (then RCCL uint8 max all-reduce). */
+int sk_hll_union_dev(sk_ctx *ctx, uint64_t n, const uint32_t *d_key_ids, uint8_t *d_out);
+/* write 16384 unpacked registers (device pointer) into a key as max (PFMERGE of a raw array) */
+int sk_hll_merge_registers_dev(sk_ctx *ctx, const uint8_t *key, uint64_t len, const uint8_t *d_regs);
+/* parity readback: 16384 unpacked registers of an HLL key (zeros if missing) */
+int sk_hll_registers(sk_ctx *ctx, const uint8_t *key, uint64_t len, uint8_t *out16384);
+
+/* ---- RBitSet (M:RedissonBitSet.java:53-268) ---- */
+/* batch of SETBIT in order; out_old[i] = previous bit (SETBIT reply), may be NULL */
+int sk_setbit(sk_ctx *ctx, uint32_t n, const uint64_t *key_off, const uint8_t *key_bytes,
+              const uint64_t *offsets, const uint8_t *values, uint8_t *out_old);
+/* batch of GETBIT */
+int sk_getbit(sk_ctx *ctx, uint32_t n, const uint64_t *key_off, const uint8_t *key_bytes,
+              const uint64_t *offsets, uint8_t *out_bits);
+/* single-key device-resident variants for the bulk path (C5) */
+int sk_setbit_dev(sk_ctx *ctx, const uint8_t *key, uint64_t len, uint64_t n, const uint64_t *d_offsets,
+                  uint8_t value, uint8_t *d_out_old);
+int sk_getbit_dev(sk_ctx *ctx, const uint8_t *key, uint64_t len, uint64_t n, const uint64_t *d_offsets,
+                  uint8_t *d_out_bits);
+int sk_bitcount(sk_ctx *ctx, const uint8_t *key, uint64_t len, uint64_t *out);
+int sk_strlen(sk_ctx *ctx, const uint8_t *key, uint64_t len, uint64_t *out);
+/* BITOP op dest src1..srcn -> out_len = result length (0 deletes dest) */
+int sk_bitop(sk_ctx *ctx, int op, const uint8_t *dest, uint64_t dest_len, uint32_t n_src,
+             const uint64_t *src_off, const uint8_t *src_bytes, uint64_t *out_len);
+/* GET: HLL keys -> dense "HYLL" string (12304 B); strings -> raw bytes.
+ * *out_len = length (or -1 when the key does not exist); copies min(cap, len). */
+int sk_get(sk_ctx *ctx, const uint8_t *key, uint64_t len, uint8_t *buf, uint64_t cap, int64_t *out_len);
+/* SET key raw-bytes (RBitSet.set(BitSet), M:RedissonBitSet.java:211-214) */
+int sk_set(sk_ctx *ctx, const uint8_t *key, uint64_t len, const uint8_t *val, uint64_t val_len);
+/* RBitSet.length() Lua script (M:RedissonBitSet.java:180-192), same result and errors */
+int sk_bitset_length(sk_ctx *ctx, const uint8_t *key, uint64_t len, int64_t *out);
+
+/* ---- RBloomFilter (M:RedissonBloomFilter.java) ---- */
+/* tryInit :223-252 -> *out_ok 1 if created, 0 if a config already existed */
+int sk_bloom_try_init(sk_ctx *ctx, const uint8_t *name, uint64_t len, int64_t expected_insertions,
+                      double false_probability, int *out_ok);
+/* readConfig :206-221 (SK_ENOTINIT if absent) */
+int sk_bloom_config(sk_ctx *ctx, const uint8_t *name, uint64_t len, int64_t *size, int32_t *hash_iterations,
+                    int64_t *expected_insertions, double *false_probability);
+/* add :80-114 / contains :133-168 for n encoded elements, checked against the
+ * caller's (size, k) like addConfigCheck :180-186 (SK_ECONFIG on mismatch). */
+int sk_bloom_add(sk_ctx *ctx, const uint8_t *name, uint64_t len, int64_t size, int32_t k, uint32_t n,
+                 const uint64_t *elem_off, const uint8_t *elem_bytes, uint8_t *out);
+int sk_bloom_contains(sk_ctx *ctx, const uint8_t *name, uint64_t len, int64_t size, int32_t k, uint32_t n,
+                      const uint64_t *elem_off, const uint8_t *elem_bytes, uint8_t *out);
+int sk_bloom_add_dev(sk_ctx *ctx, const uint8_t *name, uint64_t len, uint64_t n, const uint64_t *d_elem_off,
+                     const uint8_t *d_elem_bytes, uint64_t elem_bytes_len, uint8_t *d_out);
+int sk_bloom_contains_dev(sk_ctx *ctx, const uint8_t *name, uint64_t len, uint64_t n, const uint64_t *d_elem_off,
+                          const uint8_t *d_elem_bytes, uint64_t elem_bytes_len, uint8_t *d_out);
+/* count :188-199 */
+int sk_bloom_count(sk_ctx *ctx, const uint8_t *name, uint64_t len, int32_t *out);
+
+/* ---- bench / test helpers ---- */
+/* Jackson default-typing bytes of Longs, ["java.lang.Long",<v>] (M:codec/JsonJacksonCodec.java:
+ * 86-117, Long forced typed :103-106), for SplitMix64(seed) values; host buffers.
+ * Call with bytes == NULL to get the offsets (and total size in off[n]). */
+int sk_gen_jackson_longs(uint64_t seed, uint64_t n, uint64_t *off, uint8_t *bytes);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,263 @@
+"""ctypes wrapper of oracle/liboracle.so -- TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may use
+this module, and only as the checker / CPU comparator.  The product
+(redisson_amd, libredisson_sketch.so) never imports it.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+from ctypes import c_double, c_int, c_int32, c_int64, c_uint32, c_uint64, c_void_p
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "liboracle.so")
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        L = ctypes.CDLL(LIB)
+        sig = {
+            "or_murmur64a": (c_uint64, [c_void_p, c_int64, c_uint64]),
+            "or_murmur64a_verification": (c_uint32, []),
+            "or_xxh64": (c_uint64, [c_void_p, c_uint64, c_uint64]),
+            "or_farmhash_na64": (c_uint64, [c_void_p, c_uint64]),
+            "or_farmhash_uo64": (c_uint64, [c_void_p, c_uint64]),
+            "or_crc16": (c_uint32, [c_void_p, c_uint64]),
+            "or_calc_slot": (c_int32, [c_void_p, c_uint64]),
+            "or_hll_patlen": (c_int, [c_void_p, c_uint64, c_int, c_void_p]),
+            "or_hll_add": (c_int, [c_void_p, c_void_p, c_uint64, c_int]),
+            "or_pfadd_batch": (None, [c_void_p, c_void_p, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
+                                      c_void_p]),
+            "or_hll_sum": (c_double, [c_void_p, c_int, c_void_p]),
+            "or_hll_count": (c_uint64, [c_void_p, c_int, c_int]),
+            "or_hll_histogram": (None, [c_void_p, c_void_p]),
+            "or_hll_union": (None, [c_void_p, c_uint32, c_void_p]),
+            "or_hll_dense_pack": (None, [c_void_p, c_void_p]),
+            "or_hll_dense_unpack": (None, [c_void_p, c_void_p]),
+            "or_bloom_optimal_bits": (c_int64, [c_int64, c_double]),
+            "or_bloom_optimal_k": (c_int32, [c_int64, c_int64]),
+            "or_bloom_indexes": (None, [c_void_p, c_uint64, c_int32, c_int64, c_void_p]),
+            "or_bloom_count": (c_int32, [c_int64, c_int32, c_int64]),
+            "or_bloom_add_batch": (None, [c_void_p, c_void_p, c_int64, c_int32, c_uint32, c_void_p, c_void_p,
+                                          c_void_p]),
+            "or_bloom_contains_batch": (None, [c_void_p, c_uint64, c_int64, c_int32, c_uint32, c_void_p, c_void_p,
+                                               c_void_p]),
+            "or_getbit": (c_int, [c_void_p, c_uint64, c_uint64]),
+            "or_setbit": (c_int, [c_void_p, c_void_p, c_uint64, c_int]),
+            "or_bitcount": (c_uint64, [c_void_p, c_uint64]),
+            "or_bitop": (c_uint64, [c_int, c_void_p, c_void_p, c_void_p, c_uint32]),
+        }
+        for name, (res, args) in sig.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data if isinstance(a, np.ndarray) else a
+
+
+def pack(items):
+    off = np.zeros(len(items) + 1, dtype=np.uint64)
+    if items:
+        np.cumsum([len(x) for x in items], out=off[1:])
+    blob = b"".join(items) + b"\0" * 16
+    return off, np.frombuffer(blob, dtype=np.uint8).copy()
+
+
+# ---- hashes ------------------------------------------------------------
+def murmur64a(b: bytes, seed: int = 0xADC83B19) -> int:
+    return lib().or_murmur64a(b, len(b), seed)
+
+
+def xxh64(b: bytes) -> int:
+    return lib().or_xxh64(b, len(b), 0)
+
+
+def farmhash_na64(b: bytes) -> int:
+    return lib().or_farmhash_na64(b, len(b))
+
+
+def farmhash_uo64(b: bytes) -> int:
+    return lib().or_farmhash_uo64(b, len(b))
+
+
+def crc16(b: bytes) -> int:
+    return lib().or_crc16(b, len(b))
+
+
+def calc_slot(key) -> int:
+    b = key.encode() if isinstance(key, str) else key
+    return lib().or_calc_slot(b, len(b))
+
+
+# ---- HLL -----------------------------------------------------------------
+def hll_patlen(b: bytes, redis_major: int = 3):
+    reg = c_int64()
+    cnt = lib().or_hll_patlen(b, len(b), redis_major, ctypes.addressof(reg))
+    return reg.value, cnt
+
+
+class HLLStore:
+    """Reference keyspace of HLLs (unpacked registers), redis semantics."""
+
+    def __init__(self, redis_major: int = 3):
+        self.m = redis_major
+        self.regs = {}
+
+    def pfadd(self, keys, elems):
+        out = []
+        for k, es in zip(keys, elems):
+            created = k not in self.regs
+            r = self.regs.setdefault(k, np.zeros(16384, dtype=np.uint8))
+            ch = created
+            for e in es:
+                ch |= bool(lib().or_hll_add(r.ctypes.data, e, len(e), self.m))
+            out.append(ch)
+        return out
+
+    def pfadd_bulk(self, key_ids: np.ndarray, off: np.ndarray, buf: np.ndarray, n_keys: int):
+        """One element per command, key given by integer id (fast C loop)."""
+        regs = np.zeros((n_keys, 16384), dtype=np.uint8)
+        exists = np.zeros(n_keys, dtype=np.uint8)
+        n = len(key_ids)
+        counts = np.ones(n, dtype=np.uint32)
+        out = np.zeros(n, dtype=np.uint8)
+        ids = np.ascontiguousarray(key_ids, dtype=np.uint32)
+        lib().or_pfadd_batch(regs.ctypes.data, exists.ctypes.data, n, ids.ctypes.data, counts.ctypes.data,
+                             off.ctypes.data, buf.ctypes.data, self.m, out.ctypes.data)
+        return regs, out
+
+    def count(self, keys):
+        keys = [k for k in keys if k in self.regs]
+        if len(keys) == 1 or (len(keys) == 0):
+            r = self.regs[keys[0]] if keys else np.zeros(16384, dtype=np.uint8)
+            return count_regs(r, 1, self.m)
+        u = np.maximum.reduce([self.regs[k] for k in keys])
+        return count_regs(u, 2, self.m)
+
+    def merge(self, dest, srcs):
+        arrs = [self.regs[k] for k in srcs if k in self.regs]
+        d = self.regs.setdefault(dest, np.zeros(16384, dtype=np.uint8))
+        for a in arrs:
+            np.maximum(d, a, out=d)
+
+
+def count_regs(regs: np.ndarray, encoding: int = 1, redis_major: int = 3) -> int:
+    r = np.ascontiguousarray(regs, dtype=np.uint8)
+    return lib().or_hll_count(r.ctypes.data, encoding, redis_major)
+
+
+def hll_histogram(regs: np.ndarray) -> np.ndarray:
+    h = np.zeros(64, dtype=np.uint32)
+    r = np.ascontiguousarray(regs, dtype=np.uint8)
+    lib().or_hll_histogram(r.ctypes.data, h.ctypes.data)
+    return h
+
+
+def dense_pack(regs: np.ndarray) -> bytes:
+    out = np.zeros(12288, dtype=np.uint8)
+    r = np.ascontiguousarray(regs, dtype=np.uint8)
+    lib().or_hll_dense_pack(r.ctypes.data, out.ctypes.data)
+    return out.tobytes()
+
+
+# ---- Bloom ---------------------------------------------------------------
+def bloom_optimal_bits(n, p):
+    return lib().or_bloom_optimal_bits(n, p)
+
+
+def bloom_optimal_k(n, m):
+    return lib().or_bloom_optimal_k(n, m)
+
+
+def bloom_indexes(b: bytes, k: int, size: int):
+    out = np.zeros(k, dtype=np.int64)
+    lib().or_bloom_indexes(b, len(b), k, size, out.ctypes.data)
+    return [int(x) for x in out]
+
+
+def bloom_count(size, k, bitcount):
+    return lib().or_bloom_count(size, k, bitcount)
+
+
+class BitString:
+    """A redis string used as a bit array (MSB-first), growable."""
+
+    def __init__(self, cap_bytes: int = 16):
+        self.buf = np.zeros(max(cap_bytes, 16), dtype=np.uint8)
+        self.len = c_uint64(0)
+
+    def reserve(self, nbytes):
+        if nbytes > len(self.buf):
+            nb = np.zeros(max(nbytes, 2 * len(self.buf)), dtype=np.uint8)
+            nb[: len(self.buf)] = self.buf
+            self.buf = nb
+
+    def setbit(self, off: int, val: int) -> int:
+        self.reserve(off // 8 + 1)
+        return lib().or_setbit(self.buf.ctypes.data, ctypes.addressof(self.len), off, val)
+
+    def getbit(self, off: int) -> int:
+        return lib().or_getbit(self.buf.ctypes.data, self.len.value, off)
+
+    def bitcount(self) -> int:
+        return lib().or_bitcount(self.buf.ctypes.data, self.len.value)
+
+    def bytes(self) -> bytes:
+        return self.buf[: self.len.value].tobytes()
+
+    def bloom_add(self, size, k, elems):
+        self.reserve((size + 7) // 8)
+        off, buf = pack(list(elems))
+        out = np.zeros(len(elems), dtype=np.uint8)
+        lib().or_bloom_add_batch(self.buf.ctypes.data, ctypes.addressof(self.len), size, k, len(elems),
+                                 off.ctypes.data, buf.ctypes.data, out.ctypes.data)
+        return [bool(x) for x in out]
+
+    def bloom_contains(self, size, k, elems):
+        off, buf = pack(list(elems))
+        out = np.zeros(len(elems), dtype=np.uint8)
+        lib().or_bloom_contains_batch(self.buf.ctypes.data, self.len.value, size, k, len(elems),
+                                      off.ctypes.data, buf.ctypes.data, out.ctypes.data)
+        return [bool(x) for x in out]
+
+    def bloom_contains_raw(self, size, k, off, buf):
+        n = len(off) - 1
+        out = np.zeros(n, dtype=np.uint8)
+        lib().or_bloom_contains_batch(self.buf.ctypes.data, self.len.value, size, k, n,
+                                      off.ctypes.data, buf.ctypes.data, out.ctypes.data)
+        return out
+
+    def bloom_add_raw(self, size, k, off, buf):
+        self.reserve((size + 7) // 8)
+        n = len(off) - 1
+        out = np.zeros(n, dtype=np.uint8)
+        lib().or_bloom_add_batch(self.buf.ctypes.data, ctypes.addressof(self.len), size, k, n,
+                                 off.ctypes.data, buf.ctypes.data, out.ctypes.data)
+        return out
+
+
+def bitop(op: str, srcs):
+    """srcs: list of bytes or None (missing key) -> result bytes (b'' deletes)."""
+    code = {"AND": 0, "OR": 1, "XOR": 2, "NOT": 3}[op]
+    arrs = [np.frombuffer((s or b"") + b"\0", dtype=np.uint8) for s in srcs]
+    lens = np.array([len(s or b"") for s in srcs], dtype=np.uint64)
+    ptrs = (c_void_p * len(arrs))(*[a.ctypes.data for a in arrs])
+    dst = np.zeros(int(lens.max()) + 1 if len(lens) else 1, dtype=np.uint8)
+    n = lib().or_bitop(code, dst.ctypes.data, ptrs, lens.ctypes.data, len(arrs))
+    return dst[:n].tobytes()

@@ -1,0 +1,107 @@
+"""ctypes binding of libredisson_sketch.so (include/redisson_sketch.h).
+
+This is the same boundary the Java JNI shim binds.  There is
+no CPU fallback: if the library is missing, import of the engine fails loudly,
+and opening a context without a GPU raises ``DeviceUnavailable``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_char_p, c_double, c_int, c_int32, c_int64, c_uint8, c_uint32, c_uint64, c_void_p
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libredisson_sketch.so")
+
+SK_OK = 0
+SK_EWRONGTYPE = -1
+SK_ERANGE = -2
+SK_ECONFIG = -3
+SK_ENOTINIT = -4
+SK_EDEVICE = -5
+SK_EINVAL = -6
+SK_ENOMEM = -7
+SK_ESYNTAX = -8
+SK_ETOOBIG = -9
+
+SK_TYPE_NONE, SK_TYPE_HLL, SK_TYPE_STRING, SK_TYPE_HASH = 0, 1, 2, 3
+SK_BITOP = {"AND": 0, "OR": 1, "XOR": 2, "NOT": 3}
+
+
+class SkConfig(ctypes.Structure):
+    _fields_ = [
+        ("device", c_int),
+        ("redis_major", c_int),
+        ("max_bit_offset", c_uint64),
+        ("hll_capacity", c_uint64),
+        ("max_batch", c_uint64),
+    ]
+
+
+P = c_void_p  # every pointer argument is passed as a raw address
+_u8p, _u32p, _u64p, _i64p = P, P, P, P
+
+# name -> (restype, argtypes)
+SIGNATURES = {
+    "sk_open": (c_int, [POINTER(SkConfig), POINTER(c_void_p)]),
+    "sk_close": (c_int, [P]),
+    "sk_last_error": (c_char_p, [P]),
+    "sk_strerror": (c_char_p, [c_int]),
+    "sk_stream": (c_void_p, [P]),
+    "sk_sync": (c_int, [P]),
+    "sk_crc16": (c_uint32, [_u8p, c_uint64]),
+    "sk_calc_slot": (c_int32, [_u8p, c_uint64]),
+    "sk_owner": (c_int32, [_u8p, c_uint64, c_int32]),
+    "sk_bloom_optimal_bits": (c_int64, [c_int64, c_double]),
+    "sk_bloom_optimal_k": (c_int32, [c_int64, c_int64]),
+    "sk_hll_estimate_hist": (c_uint64, [_u32p, c_int]),
+    "sk_type": (c_int, [P, _u8p, c_uint64, P]),
+    "sk_del": (c_int, [P, c_uint32, _u64p, _u8p, _u64p]),
+    "sk_hll_resolve": (c_int, [P, c_uint32, _u64p, _u8p, _u32p, _u8p]),
+    "sk_pfadd": (c_int, [P, c_uint32, _u64p, _u8p, _u32p, _u64p, _u8p, _u8p]),
+    "sk_pfadd_dev": (c_int, [P, c_uint64, _u32p, _u64p, _u8p, c_uint64, _u8p]),
+    "sk_pfcount": (c_int, [P, c_uint32, _u32p, _u64p, _u8p, _i64p]),
+    "sk_hll_histogram_dev": (c_int, [P, c_uint64, _u32p, _u32p]),
+    "sk_pfmerge": (c_int, [P, _u8p, c_uint64, c_uint32, _u64p, _u8p]),
+    "sk_hll_union_dev": (c_int, [P, c_uint64, _u32p, _u8p]),
+    "sk_hll_merge_registers_dev": (c_int, [P, _u8p, c_uint64, _u8p]),
+    "sk_hll_registers": (c_int, [P, _u8p, c_uint64, _u8p]),
+    "sk_setbit": (c_int, [P, c_uint32, _u64p, _u8p, _u64p, _u8p, _u8p]),
+    "sk_getbit": (c_int, [P, c_uint32, _u64p, _u8p, _u64p, _u8p]),
+    "sk_setbit_dev": (c_int, [P, _u8p, c_uint64, c_uint64, _u64p, c_uint8, _u8p]),
+    "sk_getbit_dev": (c_int, [P, _u8p, c_uint64, c_uint64, _u64p, _u8p]),
+    "sk_bitcount": (c_int, [P, _u8p, c_uint64, _u64p]),
+    "sk_strlen": (c_int, [P, _u8p, c_uint64, _u64p]),
+    "sk_bitop": (c_int, [P, c_int, _u8p, c_uint64, c_uint32, _u64p, _u8p, _u64p]),
+    "sk_get": (c_int, [P, _u8p, c_uint64, _u8p, c_uint64, _i64p]),
+    "sk_set": (c_int, [P, _u8p, c_uint64, _u8p, c_uint64]),
+    "sk_bitset_length": (c_int, [P, _u8p, c_uint64, _i64p]),
+    "sk_bloom_try_init": (c_int, [P, _u8p, c_uint64, c_int64, c_double, P]),
+    "sk_bloom_config": (c_int, [P, _u8p, c_uint64, P, P, P, P]),
+    "sk_bloom_add": (c_int, [P, _u8p, c_uint64, c_int64, c_int32, c_uint32, _u64p, _u8p, _u8p]),
+    "sk_bloom_contains": (c_int, [P, _u8p, c_uint64, c_int64, c_int32, c_uint32, _u64p, _u8p, _u8p]),
+    "sk_bloom_add_dev": (c_int, [P, _u8p, c_uint64, c_uint64, _u64p, _u8p, c_uint64, _u8p]),
+    "sk_bloom_contains_dev": (c_int, [P, _u8p, c_uint64, c_uint64, _u64p, _u8p, c_uint64, _u8p]),
+    "sk_bloom_count": (c_int, [P, _u8p, c_uint64, P]),
+    "sk_gen_jackson_longs": (c_int, [c_uint64, c_uint64, _u64p, _u8p]),
+}
+
+_lib = None
+
+
+def load() -> ctypes.CDLL:
+    """Load the in-tree native library (raises if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(there is no CPU fallback for the sketch engine)"
+        )
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib

@@ -1,0 +1,336 @@
+// sk_device.h -- device-side byte readers and hash functions for gfx950.
+//
+// Keys arrive as (off u64[n+1], bytes u8[]) with arbitrary byte alignment
+// (Jackson-encoded Longs are 20-39 B).  Rather than byte loads, every 8-byte
+// block is assembled from two naturally aligned 8-byte loads and a funnel
+// shift, so a key costs ~len/8+2 dword-pair loads that hit L1 for neighbours.
+// Contract: byte buffers carry >= 16 readable bytes of padding after the last
+// key (the library's staging buffers do; _dev callers must).
+//
+// Hash functions restate the third-party algorithms on the path (the oracle
+// in oracle/sketch_oracle.c is the CPU checker; this file never calls it):
+//   murmur64a  -- redis 3.2 hyperloglog.c MurmurHash64A (PFADD)
+//   xxh64      -- OpenHFT xx_r39() (M:RedissonBloomFilter.java:117)
+//   farm_uo64  -- OpenHFT farmUo() = farmhashuo::Hash64 (:118)
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace sk {
+
+__device__ __forceinline__ uint64_t funnel(uint64_t lo, uint64_t hi, unsigned sh) {
+    // (lo >> sh) | (hi << (64 - sh)), correct for sh == 0 (two shifts < 64)
+    return (lo >> sh) | ((hi << 1) << (63 - sh));
+}
+
+// unaligned little-endian 8-byte load (over-reads < 16 B past p)
+__device__ __forceinline__ uint64_t ldu64(const uint8_t *p) {
+    uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    const uint64_t *q = reinterpret_cast<const uint64_t *>(a & ~uintptr_t(7));
+    unsigned sh = unsigned(a & 7) * 8u;
+    return funnel(q[0], q[1], sh);
+}
+__device__ __forceinline__ uint32_t ldu32(const uint8_t *p) { return uint32_t(ldu64(p)); }
+
+// Sequential reader: each next() costs one aligned load.
+struct Stream {
+    const uint64_t *q;
+    uint64_t cur;
+    unsigned sh;
+    __device__ __forceinline__ explicit Stream(const uint8_t *p) {
+        uintptr_t a = reinterpret_cast<uintptr_t>(p);
+        q = reinterpret_cast<const uint64_t *>(a & ~uintptr_t(7));
+        sh = unsigned(a & 7) * 8u;
+        cur = q[0];
+    }
+    __device__ __forceinline__ uint64_t next() {
+        uint64_t nxt = *++q;
+        uint64_t v = funnel(cur, nxt, sh);
+        cur = nxt;
+        return v;
+    }
+};
+
+__device__ __forceinline__ uint64_t low_bytes(uint64_t v, unsigned nbytes) {
+    // keep the low nbytes (0..7) bytes
+    return nbytes ? (v & (~0ull >> (64 - 8 * nbytes))) : 0ull;
+}
+
+// ---------------------------------------------------------------- Murmur
+__device__ __forceinline__ uint64_t murmur64a(const uint8_t *data, uint32_t len, uint64_t seed) {
+    const uint64_t m = 0xc6a4a7935bd1e995ull;
+    uint64_t h = seed ^ (uint64_t(len) * m);
+    Stream s(data);
+    uint32_t nb = len >> 3;
+    for (uint32_t i = 0; i < nb; i++) {
+        uint64_t k = s.next();
+        k *= m;
+        k ^= k >> 47;
+        k *= m;
+        h ^= k;
+        h *= m;
+    }
+    unsigned tail = len & 7u;
+    if (tail) {
+        h ^= low_bytes(s.next(), tail);
+        h *= m;
+    }
+    h ^= h >> 47;
+    h *= m;
+    h ^= h >> 47;
+    return h;
+}
+
+// ---------------------------------------------------------------- XXH64
+#define SK_XP1 0x9E3779B185EBCA87ull
+#define SK_XP2 0xC2B2AE3D27D4EB4Full
+#define SK_XP3 0x165667B19E3779F9ull
+#define SK_XP4 0x85EBCA77C2B2AE63ull
+#define SK_XP5 0x27D4EB2F165667C5ull
+
+__device__ __forceinline__ uint64_t rotl(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
+__device__ __forceinline__ uint64_t rotr(uint64_t x, int r) { return (x >> r) | (x << (64 - r)); }
+__device__ __forceinline__ uint64_t xround(uint64_t acc, uint64_t in) {
+    acc += in * SK_XP2;
+    acc = rotl(acc, 31);
+    return acc * SK_XP1;
+}
+__device__ __forceinline__ uint64_t xmerge(uint64_t acc, uint64_t v) {
+    acc ^= xround(0, v);
+    return acc * SK_XP1 + SK_XP4;
+}
+
+__device__ __forceinline__ uint64_t xxh64(const uint8_t *p, uint32_t len) {
+    const uint64_t seed = 0;
+    Stream s(p);
+    uint64_t h;
+    uint32_t rem = len;
+    if (len >= 32) {
+        uint64_t v1 = seed + SK_XP1 + SK_XP2, v2 = seed + SK_XP2, v3 = seed, v4 = seed - SK_XP1;
+        do {
+            v1 = xround(v1, s.next());
+            v2 = xround(v2, s.next());
+            v3 = xround(v3, s.next());
+            v4 = xround(v4, s.next());
+            rem -= 32;
+        } while (rem >= 32);
+        h = rotl(v1, 1) + rotl(v2, 7) + rotl(v3, 12) + rotl(v4, 18);
+        h = xmerge(h, v1);
+        h = xmerge(h, v2);
+        h = xmerge(h, v3);
+        h = xmerge(h, v4);
+    } else {
+        h = seed + SK_XP5;
+    }
+    h += len;
+    while (rem >= 8) {
+        h ^= xround(0, s.next());
+        h = rotl(h, 27) * SK_XP1 + SK_XP4;
+        rem -= 8;
+    }
+    if (rem) {
+        uint64_t w = s.next(); // the last 1..7 bytes, low-aligned
+        if (rem >= 4) {
+            h ^= (w & 0xffffffffull) * SK_XP1;
+            h = rotl(h, 23) * SK_XP2 + SK_XP3;
+            w >>= 32;
+            rem -= 4;
+        }
+        while (rem) {
+            h ^= (w & 0xffull) * SK_XP5;
+            h = rotl(h, 11) * SK_XP1;
+            w >>= 8;
+            rem--;
+        }
+    }
+    h ^= h >> 33;
+    h *= SK_XP2;
+    h ^= h >> 29;
+    h *= SK_XP3;
+    h ^= h >> 32;
+    return h;
+}
+
+// ---------------------------------------------------------------- FarmHash
+#define SK_K0 0xc3a5c85c97cb3127ull
+#define SK_K1 0xb492b66fbe98f273ull
+#define SK_K2 0x9ae16a3b2f90404full
+
+__device__ __forceinline__ uint64_t shift_mix(uint64_t v) { return v ^ (v >> 47); }
+__device__ __forceinline__ uint64_t hl16(uint64_t u, uint64_t v, uint64_t mul) {
+    uint64_t a = (u ^ v) * mul;
+    a ^= (a >> 47);
+    uint64_t b = (v ^ a) * mul;
+    b ^= (b >> 47);
+    return b * mul;
+}
+struct P2 {
+    uint64_t first, second;
+};
+__device__ __forceinline__ P2 weak32(const uint8_t *s, uint64_t a, uint64_t b) {
+    uint64_t w = ldu64(s), x = ldu64(s + 8), y = ldu64(s + 16), z = ldu64(s + 24);
+    a += w;
+    b = rotr(b + a + z, 21);
+    uint64_t c = a;
+    a += x;
+    a += y;
+    b += rotr(a, 44);
+    return P2{a + z, b + c};
+}
+
+__device__ __forceinline__ uint64_t farm_na_short(const uint8_t *s, uint32_t len) {
+    // farmhashna::Hash64 for len <= 64
+    if (len <= 16) {
+        if (len >= 8) {
+            uint64_t mul = SK_K2 + uint64_t(len) * 2;
+            uint64_t a = ldu64(s) + SK_K2;
+            uint64_t b = ldu64(s + len - 8);
+            uint64_t c = rotr(b, 37) * mul + a;
+            uint64_t d = (rotr(a, 25) + b) * mul;
+            return hl16(c, d, mul);
+        }
+        if (len >= 4) {
+            uint64_t mul = SK_K2 + uint64_t(len) * 2;
+            uint64_t a = ldu32(s);
+            return hl16(uint64_t(len) + (a << 3), ldu32(s + len - 4), mul);
+        }
+        if (len > 0) {
+            uint64_t w = ldu64(s);
+            uint32_t a = uint32_t(w & 0xff), b = uint32_t((w >> (8 * (len >> 1))) & 0xff),
+                     c = uint32_t((w >> (8 * (len - 1))) & 0xff);
+            uint32_t y = a + (b << 8);
+            uint32_t z = len + (c << 2);
+            return shift_mix(uint64_t(y) * SK_K2 ^ uint64_t(z) * SK_K0) * SK_K2;
+        }
+        return SK_K2;
+    }
+    uint64_t mul = SK_K2 + uint64_t(len) * 2;
+    if (len <= 32) {
+        uint64_t a = ldu64(s) * SK_K1;
+        uint64_t b = ldu64(s + 8);
+        uint64_t c = ldu64(s + len - 8) * mul;
+        uint64_t d = ldu64(s + len - 16) * SK_K2;
+        return hl16(rotr(a + b, 43) + rotr(c, 30) + d, a + rotr(b + SK_K2, 18) + c, mul);
+    }
+    uint64_t a = ldu64(s) * SK_K2;
+    uint64_t b = ldu64(s + 8);
+    uint64_t c = ldu64(s + len - 8) * mul;
+    uint64_t d = ldu64(s + len - 16) * SK_K2;
+    uint64_t y = rotr(a + b, 43) + rotr(c, 30) + d;
+    uint64_t z = hl16(y, a + rotr(b + SK_K2, 18) + c, mul);
+    uint64_t e = ldu64(s + 16) * mul;
+    uint64_t f = ldu64(s + 24);
+    uint64_t g = (y + ldu64(s + len - 32)) * mul;
+    uint64_t h = (z + ldu64(s + len - 24)) * mul;
+    return hl16(rotr(e + f, 43) + rotr(g, 30) + h, e + rotr(f + a, 18) + g, mul);
+}
+
+__device__ __forceinline__ uint64_t uo_H(uint64_t x, uint64_t y, uint64_t mul, int r) {
+    uint64_t a = (x ^ y) * mul;
+    a ^= (a >> 47);
+    uint64_t b = (y ^ a) * mul;
+    return rotr(b, r) * mul;
+}
+
+// farmhashuo::Hash64WithSeeds(s, len, 81, 0) for len > 64
+__device__ __noinline__ uint64_t farm_uo_long(const uint8_t *s, uint32_t len) {
+    const uint64_t seed0 = 81, seed1 = 0;
+    uint64_t x = seed0;
+    uint64_t y = seed1 * SK_K2 + 113;
+    uint64_t z = shift_mix(y * SK_K2) * SK_K2;
+    P2 v{seed0, seed1}, w{0, 0};
+    uint64_t u = x - z;
+    x *= SK_K2;
+    uint64_t mul = SK_K2 + (u & 0x82);
+    uint32_t nblk = (len - 1) / 64;
+    const uint8_t *last64 = s + len - 64;
+    for (uint32_t blk = 0; blk < nblk; blk++, s += 64) {
+        uint64_t a0 = ldu64(s), a1 = ldu64(s + 8), a2 = ldu64(s + 16), a3 = ldu64(s + 24);
+        uint64_t a4 = ldu64(s + 32), a5 = ldu64(s + 40), a6 = ldu64(s + 48), a7 = ldu64(s + 56);
+        x += a0 + a1;
+        y += a2;
+        z += a3;
+        v.first += a4;
+        v.second += a5 + a1;
+        w.first += a6;
+        w.second += a7;
+        x = rotr(x, 26);
+        x *= 9;
+        y = rotr(y, 29);
+        z *= mul;
+        v.first = rotr(v.first, 33);
+        v.second = rotr(v.second, 30);
+        w.first ^= x;
+        w.first *= 9;
+        z = rotr(z, 32);
+        z += w.second;
+        w.second += z;
+        z *= 9;
+        uint64_t t = u;
+        u = y;
+        y = t;
+        z += a0 + a6;
+        v.first += a2;
+        v.second += a3;
+        w.first += a4;
+        w.second += a5 + a6;
+        x += a1;
+        y += a7;
+        y += v.first;
+        v.first += x - y;
+        v.second += w.first;
+        w.first += v.second;
+        w.second += x - y;
+        x += w.second;
+        w.second = rotr(w.second, 34);
+        t = u;
+        u = z;
+        z = t;
+    }
+    s = last64;
+    u *= 9;
+    v.second = rotr(v.second, 28);
+    v.first = rotr(v.first, 20);
+    w.first += ((len - 1) & 63);
+    u += y;
+    y += u;
+    x = rotr(y - x + v.first + ldu64(s + 8), 37) * mul;
+    y = rotr(y ^ v.second ^ ldu64(s + 48), 42) * mul;
+    x ^= w.second * 9;
+    y += v.first + ldu64(s + 40);
+    z = rotr(z + w.first, 33) * mul;
+    v = weak32(s, v.second * mul, x + w.first);
+    w = weak32(s + 32, z + w.second, y + ldu64(s + 16));
+    return uo_H(hl16(v.first + x, w.first ^ y, mul) + z - u, uo_H(v.second + w.second, x, mul, 30) ^ w.first,
+                mul, 31);
+}
+
+__device__ __forceinline__ uint64_t farm_uo64(const uint8_t *s, uint32_t len) {
+    return len <= 64 ? farm_na_short(s, len) : farm_uo_long(s, len);
+}
+
+// ---------------------------------------------------------------- misc
+// x % d for x < 2^63 using a precomputed M = floor((2^64-1)/d): q_est is
+// at most 2 below the true quotient, so two conditional subtractions fix it.
+__device__ __forceinline__ uint64_t mod_invariant(uint64_t x, uint64_t d, uint64_t M) {
+    uint64_t q = __umul64hi(x, M);
+    uint64_t r = x - q * d;
+    if (r >= d) r -= d;
+    if (r >= d) r -= d;
+    return r;
+}
+
+// Redis bit strings are MSB-first: bit i lives in byte i>>3 at mask 0x80>>(i&7)
+__device__ __forceinline__ int get_bit(const uint8_t *buf, uint64_t len, uint64_t idx) {
+    uint64_t byte = idx >> 3;
+    if (byte >= len) return 0;
+    return (buf[byte] >> (7 - unsigned(idx & 7))) & 1;
+}
+// word-aligned address + mask of bit idx inside a little-endian u32
+__device__ __forceinline__ uint32_t *bit_word(uint8_t *buf, uint64_t idx, uint32_t *mask) {
+    uint64_t byte = idx >> 3;
+    *mask = 1u << (unsigned(byte & 3) * 8u + (7u - unsigned(idx & 7)));
+    return reinterpret_cast<uint32_t *>(buf + (byte & ~uint64_t(3)));
+}
+
+} // namespace sk

@@ -1,0 +1,44 @@
+// sk_internal.h -- launchers exported by sk_kernels.hip to the store/executor.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stddef.h>
+
+namespace sk {
+
+hipError_t launch_pfadd_hash(hipStream_t st, uint64_t n, const uint32_t *key_ids, const uint64_t *off,
+                             const uint8_t *bytes, const uint32_t *cmd_of, int v5, unsigned slot_shift,
+                             uint64_t *out_keys);
+hipError_t launch_pfadd_apply(hipStream_t st, uint64_t n, const uint64_t *keys, unsigned slot_shift, uint64_t cmd_mask,
+                              uint8_t *arena, uint8_t *changed);
+hipError_t sort_keys_size(uint64_t n, unsigned begin_bit, unsigned end_bit, size_t *bytes);
+hipError_t sort_keys(hipStream_t st, void *tmp, size_t tmp_bytes, const uint64_t *in, uint64_t *out, uint64_t n,
+                     unsigned begin_bit, unsigned end_bit);
+hipError_t sort_pairs_size(uint64_t n, unsigned begin_bit, unsigned end_bit, size_t *bytes);
+hipError_t sort_pairs(hipStream_t st, void *tmp, size_t tmp_bytes, const uint64_t *kin, uint64_t *kout,
+                      const uint32_t *vin, uint32_t *vout, uint64_t n, unsigned begin_bit, unsigned end_bit);
+hipError_t launch_hll_hist(hipStream_t st, uint64_t n, const uint32_t *ids, const uint8_t *arena, uint32_t *hist);
+hipError_t launch_hll_union(hipStream_t st, uint64_t n, const uint32_t *ids, const uint8_t *arena, uint8_t *partial,
+                            uint64_t max_groups, uint8_t *out, int include_out);
+hipError_t launch_bloom_contains(hipStream_t st, uint64_t n, const uint64_t *off, const uint8_t *bytes,
+                                 const uint8_t *bits, const uint64_t *d_len, uint64_t size, uint64_t magic, int k,
+                                 uint8_t *out);
+hipError_t launch_bloom_probes(hipStream_t st, uint64_t n, const uint64_t *off, const uint8_t *bytes, uint64_t size,
+                               uint64_t magic, int k, uint64_t *keys);
+hipError_t launch_bloom_apply(hipStream_t st, uint64_t m, const uint64_t *keys, uint8_t *bits, uint64_t *d_len, int k,
+                              uint8_t *out);
+hipError_t launch_getbit_multi(hipStream_t st, uint64_t n, const uint32_t *sid, const uint64_t *offs, const void *dir,
+                               uint8_t *out);
+hipError_t launch_getbit_single(hipStream_t st, uint64_t n, const uint64_t *offs, const uint8_t *buf,
+                                const uint64_t *d_len, uint8_t *out);
+hipError_t launch_setbit_keys(hipStream_t st, uint64_t n, const uint32_t *sid, const uint64_t *offs, uint64_t *keys,
+                              uint32_t *vals);
+hipError_t launch_setbit_apply(hipStream_t st, uint64_t n, const uint64_t *keys, const uint32_t *vals,
+                               const uint8_t *values, uint8_t value_all, void *dir, uint8_t *out_old);
+hipError_t launch_setbit_void(hipStream_t st, uint64_t n, const uint64_t *offs, uint8_t *buf, uint32_t value);
+hipError_t launch_max_u64(hipStream_t st, uint64_t n, const uint64_t *v, uint64_t *out);
+hipError_t launch_bitcount(hipStream_t st, const uint8_t *buf, uint64_t len, uint64_t *out);
+hipError_t launch_bitop(hipStream_t st, int op, uint32_t nsrc, const uint8_t *const *srcs, const uint64_t *lens,
+                        uint64_t maxlen, uint8_t *dst);
+
+} // namespace sk

@@ -1,0 +1,554 @@
+// sk_kernels.hip -- CDNA4 (gfx950) kernels of the sketch engine.
+//
+// Layout in HBM (see DESIGN.md "Data layout"):
+//   HLL arena   : u8 registers, 16384 per slab, slab id -> arena + id*16 KiB
+//                 (unpacked; the 6-bit Redis dense form is produced on GET).
+//   bit strings : one buffer per key, Redis MSB-first bytes, capacity a
+//                 multiple of 16 B, bytes in [len, cap) kept zero; a device
+//                 directory {ptr, len, cap} per string id, len grown by
+//                 atomicMax (sdsgrowzero semantics).
+//
+// Sequential-reply semantics inside a batch (PFADD's 1/0, SETBIT's old bit,
+// Bloom add's "a probe saw 0") are made exact by a stable radix sort on the
+// touched slot (rocPRIM) followed by a segment-head walk in batch order; the
+// final state (max / OR) needs no atomics because each slot has one head.
+#include <hip/hip_runtime.h>
+#include <cstring>
+#include <rocprim/device/device_radix_sort.hpp>
+#include <stdint.h>
+
+#include "sk_device.h"
+#include "sk_internal.h"
+
+namespace sk {
+
+static inline unsigned grid_for(uint64_t n, unsigned block, unsigned cap = 1u << 20) {
+    uint64_t g = (n + block - 1) / block;
+    if (g == 0) g = 1;
+    return g > cap ? cap : unsigned(g);
+}
+
+// ------------------------------------------------------------------ PFADD
+// hllPatLen: register index = low 14 bits; rho = 1 + trailing zeros of
+// bits 14.. with the version's sentinel (3.2: bit 63 -> rho <= 50,
+// >= 5.0: bit 64 of the shifted hash at HLL_Q=50 -> rho <= 51).
+__device__ __forceinline__ void hll_pat(uint64_t h, int v5, uint32_t *reg, uint32_t *rho) {
+    *reg = uint32_t(h & 16383u);
+    uint64_t x = (h >> 14) | (v5 ? (1ull << 50) : (1ull << 49));
+    *rho = 1u + uint32_t(__builtin_ctzll(x));
+}
+
+__global__ void __launch_bounds__(256) k_pfadd_hash(uint64_t n, const uint32_t *__restrict__ key_ids,
+                                                    const uint64_t *__restrict__ off,
+                                                    const uint8_t *__restrict__ bytes,
+                                                    const uint32_t *__restrict__ cmd_of, int v5,
+                                                    unsigned slot_shift, uint64_t *__restrict__ out_keys) {
+    uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint64_t o = off[i];
+    uint32_t len = uint32_t(off[i + 1] - o);
+    uint64_t h = murmur64a(bytes + o, len, 0xadc83b19ull);
+    uint32_t reg, rho;
+    hll_pat(h, v5, &reg, &rho);
+    uint64_t cmd = cmd_of ? cmd_of[i] : i;
+    uint64_t slot = (uint64_t(key_ids[i]) << 14) | reg;
+    out_keys[i] = (slot << slot_shift) | (cmd << 6) | rho;
+}
+
+// One thread per sorted element; the first element of each (slab, register)
+// segment walks the segment in batch order: exact PFADD replies, one store.
+__global__ void __launch_bounds__(256) k_pfadd_apply(uint64_t n, const uint64_t *__restrict__ keys,
+                                                     unsigned slot_shift, uint64_t cmd_mask,
+                                                     uint8_t *__restrict__ arena, uint8_t *__restrict__ changed) {
+    uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint64_t k = keys[i];
+    uint64_t slot = k >> slot_shift;
+    if (i > 0 && (keys[i - 1] >> slot_shift) == slot) return;
+    uint8_t *r = arena + slot; // slot = id*16384 + reg
+    uint32_t R0 = *r, R = R0;
+    for (uint64_t j = i; j < n; j++) {
+        uint64_t kk = (j == i) ? k : keys[j];
+        if ((kk >> slot_shift) != slot) break;
+        uint32_t rho = uint32_t(kk & 63u);
+        if (rho > R) {
+            changed[(kk >> 6) & cmd_mask] = 1;
+            R = rho;
+        }
+    }
+    if (R != R0) *r = uint8_t(R);
+}
+
+// -------------------------------------------------------------- histogram
+// One 256-thread workgroup per key: 16 KiB of registers read as 4 x 16 B
+// per lane (coalesced), counted into per-wave LDS histograms.
+__global__ void __launch_bounds__(256) k_hll_hist(const uint32_t *__restrict__ ids, const uint8_t *__restrict__ arena,
+                                                  uint32_t *__restrict__ hist) {
+    __shared__ uint32_t h[4][64];
+    unsigned t = threadIdx.x, w = t >> 6;
+    h[w][t & 63] = 0;
+    __syncthreads();
+    const uint4 *base = reinterpret_cast<const uint4 *>(arena + (uint64_t(ids[blockIdx.x]) << 14));
+#pragma unroll
+    for (int it = 0; it < 4; it++) {
+        uint4 v = base[it * 256 + t];
+        uint32_t ws[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+#pragma unroll
+            for (int b = 0; b < 4; b++) atomicAdd(&h[w][(ws[q] >> (8 * b)) & 63u], 1u);
+    }
+    __syncthreads();
+    if (t < 64) hist[uint64_t(blockIdx.x) * 64 + t] = h[0][t] + h[1][t] + h[2][t] + h[3][t];
+}
+
+// ------------------------------------------------------------------ union
+typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t bytemax(uint32_t a, uint32_t b) {
+    const uint32_t m = 0x00ff00ffu;
+    us2 al = __builtin_bit_cast(us2, a & m), bl = __builtin_bit_cast(us2, b & m);
+    us2 ah = __builtin_bit_cast(us2, (a >> 8) & m), bh = __builtin_bit_cast(us2, (b >> 8) & m);
+    uint32_t lo = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(al, bl));
+    uint32_t hi = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(ah, bh));
+    return lo | (hi << 8);
+}
+__device__ __forceinline__ uint4 bytemax4(uint4 a, uint4 b) {
+    return make_uint4(bytemax(a.x, b.x), bytemax(a.y, b.y), bytemax(a.z, b.z), bytemax(a.w, b.w));
+}
+
+// grid (4, G): block (x, g) covers 4096 registers (256 lanes x 16 B) of the
+// union of keys [g*per, (g+1)*per); writes partial[g].
+__global__ void __launch_bounds__(256) k_hll_union_partial(uint64_t n, const uint32_t *__restrict__ ids,
+                                                           const uint8_t *__restrict__ arena, uint64_t per,
+                                                           uint8_t *__restrict__ partial) {
+    unsigned lane16 = blockIdx.x * 256 + threadIdx.x; // uint4 index within 16 KiB
+    uint64_t g = blockIdx.y, k0 = g * per, k1 = k0 + per;
+    if (k1 > n) k1 = n;
+    uint4 acc = make_uint4(0, 0, 0, 0);
+    uint64_t k = k0;
+    for (; k + 4 <= k1; k += 4) { // 4 independent loads in flight per lane
+        uint4 a = reinterpret_cast<const uint4 *>(arena + (uint64_t(ids[k]) << 14))[lane16];
+        uint4 b = reinterpret_cast<const uint4 *>(arena + (uint64_t(ids[k + 1]) << 14))[lane16];
+        uint4 c = reinterpret_cast<const uint4 *>(arena + (uint64_t(ids[k + 2]) << 14))[lane16];
+        uint4 d = reinterpret_cast<const uint4 *>(arena + (uint64_t(ids[k + 3]) << 14))[lane16];
+        acc = bytemax4(acc, bytemax4(bytemax4(a, b), bytemax4(c, d)));
+    }
+    for (; k < k1; k++)
+        acc = bytemax4(acc, reinterpret_cast<const uint4 *>(arena + (uint64_t(ids[k]) << 14))[lane16]);
+    reinterpret_cast<uint4 *>(partial + g * 16384)[lane16] = acc;
+}
+
+// out = max(out_init ? out : 0, partial[0..G))
+__global__ void __launch_bounds__(256) k_hll_union_final(uint64_t G, const uint8_t *__restrict__ partial,
+                                                         uint8_t *__restrict__ out, int include_out) {
+    unsigned lane16 = blockIdx.x * 256 + threadIdx.x;
+    uint4 acc = include_out ? reinterpret_cast<const uint4 *>(out)[lane16] : make_uint4(0, 0, 0, 0);
+    for (uint64_t g = 0; g < G; g++) acc = bytemax4(acc, reinterpret_cast<const uint4 *>(partial + g * 16384)[lane16]);
+    reinterpret_cast<uint4 *>(out)[lane16] = acc;
+}
+
+// ------------------------------------------------------------------ Bloom
+__device__ __forceinline__ void bloom_hashes(const uint8_t *p, uint32_t len, uint64_t *h1, uint64_t *h2) {
+    *h1 = xxh64(p, len);
+    *h2 = farm_uo64(p, len);
+}
+
+// contains: probes 0..k-2 only (the k-th GETBIT reply is dropped by
+// result.subList(1, size-1), M:RedissonBloomFilter.java:155), early exit.
+__global__ void __launch_bounds__(256) k_bloom_contains(uint64_t n, const uint64_t *__restrict__ off,
+                                                        const uint8_t *__restrict__ bytes,
+                                                        const uint8_t *__restrict__ bits,
+                                                        const uint64_t *__restrict__ d_len, uint64_t size,
+                                                        uint64_t magic, int k, uint8_t *__restrict__ out) {
+    uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint64_t o = off[i];
+    uint32_t len = uint32_t(off[i + 1] - o);
+    uint64_t h1, h2;
+    bloom_hashes(bytes + o, len, &h1, &h2);
+    uint64_t slen = *d_len;
+    uint64_t h = h1;
+    uint8_t r = 1;
+    for (int j = 0; j < k - 1; j++) {
+        uint64_t idx = mod_invariant(h & 0x7fffffffffffffffull, size, magic);
+        if (!get_bit(bits, slen, idx)) {
+            r = 0;
+            break;
+        }
+        h += (j & 1) ? h1 : h2;
+    }
+    out[i] = r;
+}
+
+// add, pass 1: all k probes -> key = idx << 32 | (elem*k + j)
+__global__ void __launch_bounds__(256) k_bloom_probes(uint64_t n, const uint64_t *__restrict__ off,
+                                                      const uint8_t *__restrict__ bytes, uint64_t size,
+                                                      uint64_t magic, int k, uint64_t *__restrict__ keys) {
+    uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint64_t o = off[i];
+    uint32_t len = uint32_t(off[i + 1] - o);
+    uint64_t h1, h2;
+    bloom_hashes(bytes + o, len, &h1, &h2);
+    uint64_t h = h1;
+    uint64_t pos = i * uint64_t(k);
+    for (int j = 0; j < k; j++) {
+        uint64_t idx = mod_invariant(h & 0x7fffffffffffffffull, size, magic);
+        keys[pos + j] = (idx << 32) | (pos + j);
+        h += (j & 1) ? h1 : h2;
+    }
+}
+
+// add, pass 2 (after a stable sort on idx): the earliest probe of each bit
+// sees the pre-batch bit; every later probe of the same bit sees 1.
+__global__ void __launch_bounds__(256) k_bloom_apply(uint64_t m, const uint64_t *__restrict__ keys, uint8_t *bits,
+                                                     uint64_t *d_len, int k, uint8_t *__restrict__ out) {
+    uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    uint64_t need = 0;
+    if (i < m) {
+        uint64_t key = keys[i];
+        uint64_t idx = key >> 32;
+        if (i == 0 || (keys[i - 1] >> 32) != idx) {
+            uint32_t mask;
+            uint32_t *wp = bit_word(bits, idx, &mask);
+            uint32_t old = atomicOr(wp, mask); // other bits of the word may race; ours is exclusive
+            uint32_t pos = uint32_t(key & 0xffffffffu);
+            uint32_t e = pos / uint32_t(k), j = pos - e * uint32_t(k);
+            if (!(old & mask) && int(j) <= k - 2) out[e] = 1;
+            need = (idx >> 3) + 1;
+        }
+    }
+    // one atomicMax per wave for the string length
+    for (int s = 32; s > 0; s >>= 1) {
+        uint64_t o = __shfl_xor(need, s);
+        need = o > need ? o : need;
+    }
+    if ((threadIdx.x & 63) == 0 && need) atomicMax((unsigned long long *)d_len, (unsigned long long)need);
+}
+
+// ------------------------------------------------------------ bit strings
+struct DirEnt {
+    uint8_t *ptr;
+    uint64_t len;
+    uint64_t cap;
+};
+
+__global__ void __launch_bounds__(256) k_getbit_multi(uint64_t n, const uint32_t *__restrict__ sid,
+                                                      const uint64_t *__restrict__ offs,
+                                                      const DirEnt *__restrict__ dir, uint8_t *__restrict__ out) {
+    uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint32_t s = sid[i];
+    if (s == 0xffffffffu) { // missing key
+        out[i] = 0;
+        return;
+    }
+    out[i] = uint8_t(get_bit(dir[s].ptr, dir[s].len, offs[i]));
+}
+
+__global__ void __launch_bounds__(256) k_getbit_single(uint64_t n, const uint64_t *__restrict__ offs,
+                                                       const uint8_t *__restrict__ buf,
+                                                       const uint64_t *__restrict__ d_len, uint8_t *__restrict__ out) {
+    uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    out[i] = uint8_t(get_bit(buf, *d_len, offs[i]));
+}
+
+// SETBIT, pass 1: key = (string id << 36 | offset) sorted stably with the
+// command index as value; pass 2: segment heads walk the ops in order.
+__global__ void __launch_bounds__(256) k_setbit_keys(uint64_t n, const uint32_t *__restrict__ sid,
+                                                     const uint64_t *__restrict__ offs, uint64_t *__restrict__ keys,
+                                                     uint32_t *__restrict__ vals) {
+    uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    keys[i] = (uint64_t(sid ? sid[i] : 0u) << 36) | offs[i];
+    vals[i] = uint32_t(i);
+}
+
+__global__ void __launch_bounds__(256) k_setbit_apply(uint64_t n, const uint64_t *__restrict__ keys,
+                                                      const uint32_t *__restrict__ vals,
+                                                      const uint8_t *__restrict__ values, uint8_t value_all,
+                                                      DirEnt *dir, uint8_t *__restrict__ out_old) {
+    uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i < n) {
+        uint64_t key = keys[i];
+        if (i == 0 || keys[i - 1] != key) {
+            uint32_t s = uint32_t(key >> 36);
+            uint64_t off = key & ((1ull << 36) - 1);
+            DirEnt d = dir[s];
+            uint32_t mask;
+            uint32_t *wp = bit_word(d.ptr, off, &mask);
+            uint32_t cur = (*wp & mask) ? 1u : 0u; // only this head writes this bit
+            uint32_t c0 = cur;
+            for (uint64_t j = i; j < n; j++) {
+                if (j != i && keys[j] != key) break;
+                uint32_t c = vals[j];
+                if (out_old) out_old[c] = uint8_t(cur);
+                cur = values ? (values[c] & 1u) : value_all;
+            }
+            if (cur != c0) {
+                if (cur) atomicOr(wp, mask);
+                else atomicAnd(wp, ~mask);
+            }
+        }
+    }
+}
+
+// SETBIT of one value with no replies (SETBIT_VOID, M:RedissonBitSet.java:79-81): order-free.
+// (the string length is raised by the host from the validated max offset)
+__global__ void __launch_bounds__(256) k_setbit_void(uint64_t n, const uint64_t *__restrict__ offs, uint8_t *buf,
+                                                     uint32_t value) {
+    uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i < n) {
+        uint64_t off = offs[i];
+        uint32_t mask;
+        uint32_t *wp = bit_word(buf, off, &mask);
+        if (value) atomicOr(wp, mask);
+        else atomicAnd(wp, ~mask);
+    }
+}
+
+// max of a u64 array (offset validation / capacity sizing)
+__global__ void __launch_bounds__(256) k_max_u64(uint64_t n, const uint64_t *__restrict__ v, uint64_t *out) {
+    uint64_t m = 0;
+    for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += uint64_t(gridDim.x) * blockDim.x)
+        m = v[i] > m ? v[i] : m;
+    for (int s = 32; s > 0; s >>= 1) {
+        uint64_t o = __shfl_xor(m, s);
+        m = o > m ? o : m;
+    }
+    if ((threadIdx.x & 63) == 0) atomicMax((unsigned long long *)out, (unsigned long long)m);
+}
+
+// BITCOUNT: 16 B per lane per step, popcount, wave reduce, one atomic per wave
+__global__ void __launch_bounds__(256) k_bitcount(const uint8_t *__restrict__ buf, uint64_t len,
+                                                  unsigned long long *out) {
+    uint64_t nvec = len >> 4;
+    uint64_t c = 0;
+    const uint4 *v = reinterpret_cast<const uint4 *>(buf);
+    uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
+    for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < nvec; i += stride) {
+        uint4 x = v[i];
+        c += __popc(x.x) + __popc(x.y) + __popc(x.z) + __popc(x.w);
+    }
+    if (blockIdx.x == 0) // tail bytes
+        for (uint64_t b = (nvec << 4) + threadIdx.x; b < len; b += blockDim.x) c += __popc(buf[b]);
+    for (int s = 32; s > 0; s >>= 1) c += __shfl_xor(c, s);
+    if ((threadIdx.x & 63) == 0 && c) atomicAdd(out, (unsigned long long)c);
+}
+
+// BITOP over maxlen bytes; sources shorter than maxlen read as 0.
+__global__ void __launch_bounds__(256) k_bitop(int op, uint32_t nsrc, const uint8_t *const *__restrict__ srcs,
+                                               const uint64_t *__restrict__ lens, uint64_t maxlen,
+                                               uint8_t *__restrict__ dst) {
+    uint64_t nvec = (maxlen + 15) >> 4;
+    uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
+    for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < nvec; i += stride) {
+        uint64_t b0 = i << 4;
+        uint4 acc = make_uint4(0, 0, 0, 0);
+        for (uint32_t s = 0; s < nsrc; s++) {
+            uint64_t l = lens[s];
+            uint4 x;
+            if (b0 + 16 <= l) {
+                x = reinterpret_cast<const uint4 *>(srcs[s])[i];
+            } else {
+                uint8_t tmp[16];
+                for (int q = 0; q < 16; q++) tmp[q] = (b0 + q < l) ? srcs[s][b0 + q] : 0;
+                x = *reinterpret_cast<uint4 *>(tmp);
+            }
+            if (s == 0) {
+                acc = x;
+                if (op == 3) acc = make_uint4(~acc.x, ~acc.y, ~acc.z, ~acc.w);
+            } else if (op == 0) {
+                acc = make_uint4(acc.x & x.x, acc.y & x.y, acc.z & x.z, acc.w & x.w);
+            } else if (op == 1) {
+                acc = make_uint4(acc.x | x.x, acc.y | x.y, acc.z | x.z, acc.w | x.w);
+            } else if (op == 2) {
+                acc = make_uint4(acc.x ^ x.x, acc.y ^ x.y, acc.z ^ x.z, acc.w ^ x.w);
+            }
+        }
+        if (b0 + 16 <= maxlen) {
+            reinterpret_cast<uint4 *>(dst)[i] = acc;
+        } else {
+            const uint8_t *a = reinterpret_cast<const uint8_t *>(&acc);
+            for (int q = 0; q < 16; q++)
+                if (b0 + q < maxlen) dst[b0 + q] = a[q];
+        }
+    }
+}
+
+// ================================================================ launchers
+#define SK_LAUNCH_CHECK()                                                                                              \
+    do {                                                                                                               \
+        hipError_t e__ = hipGetLastError();                                                                            \
+        if (e__ != hipSuccess) return e__;                                                                             \
+    } while (0)
+
+hipError_t launch_pfadd_hash(hipStream_t st, uint64_t n, const uint32_t *key_ids, const uint64_t *off,
+                             const uint8_t *bytes, const uint32_t *cmd_of, int v5, unsigned slot_shift,
+                             uint64_t *out_keys) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k_pfadd_hash, dim3(grid_for(n, 256)), dim3(256), 0, st, n, key_ids, off, bytes, cmd_of, v5,
+                       slot_shift, out_keys);
+    SK_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+hipError_t launch_pfadd_apply(hipStream_t st, uint64_t n, const uint64_t *keys, unsigned slot_shift, uint64_t cmd_mask,
+                              uint8_t *arena, uint8_t *changed) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k_pfadd_apply, dim3(grid_for(n, 256)), dim3(256), 0, st, n, keys, slot_shift, cmd_mask, arena,
+                       changed);
+    SK_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+hipError_t sort_keys_size(uint64_t n, unsigned begin_bit, unsigned end_bit, size_t *bytes) {
+    size_t sz = 0;
+    hipError_t e = rocprim::radix_sort_keys(nullptr, sz, (const uint64_t *)nullptr, (uint64_t *)nullptr, size_t(n),
+                                            begin_bit, end_bit);
+    *bytes = sz;
+    return e;
+}
+
+hipError_t sort_keys(hipStream_t st, void *tmp, size_t tmp_bytes, const uint64_t *in, uint64_t *out, uint64_t n,
+                     unsigned begin_bit, unsigned end_bit) {
+    if (!n) return hipSuccess;
+    size_t sz = tmp_bytes;
+    return rocprim::radix_sort_keys(tmp, sz, in, out, size_t(n), begin_bit, end_bit, st);
+}
+
+hipError_t sort_pairs_size(uint64_t n, unsigned begin_bit, unsigned end_bit, size_t *bytes) {
+    size_t sz = 0;
+    hipError_t e = rocprim::radix_sort_pairs(nullptr, sz, (const uint64_t *)nullptr, (uint64_t *)nullptr,
+                                             (const uint32_t *)nullptr, (uint32_t *)nullptr, size_t(n), begin_bit,
+                                             end_bit);
+    *bytes = sz;
+    return e;
+}
+
+hipError_t sort_pairs(hipStream_t st, void *tmp, size_t tmp_bytes, const uint64_t *kin, uint64_t *kout,
+                      const uint32_t *vin, uint32_t *vout, uint64_t n, unsigned begin_bit, unsigned end_bit) {
+    if (!n) return hipSuccess;
+    size_t sz = tmp_bytes;
+    return rocprim::radix_sort_pairs(tmp, sz, kin, kout, vin, vout, size_t(n), begin_bit, end_bit, st);
+}
+
+hipError_t launch_hll_hist(hipStream_t st, uint64_t n, const uint32_t *ids, const uint8_t *arena, uint32_t *hist) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k_hll_hist, dim3(unsigned(n)), dim3(256), 0, st, ids, arena, hist);
+    SK_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+hipError_t launch_hll_union(hipStream_t st, uint64_t n, const uint32_t *ids, const uint8_t *arena, uint8_t *partial,
+                            uint64_t max_groups, uint8_t *out, int include_out) {
+    if (!n) {
+        if (!include_out) return hipMemsetAsync(out, 0, 16384, st);
+        return hipSuccess;
+    }
+    uint64_t G = (n + 63) / 64; // 64 keys per group -> 4*G workgroups
+    if (G > max_groups) G = max_groups;
+    uint64_t per = (n + G - 1) / G;
+    G = (n + per - 1) / per;
+    hipLaunchKernelGGL(k_hll_union_partial, dim3(4, unsigned(G)), dim3(256), 0, st, n, ids, arena, per, partial);
+    SK_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_hll_union_final, dim3(4), dim3(256), 0, st, G, partial, out, include_out);
+    SK_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+hipError_t launch_bloom_contains(hipStream_t st, uint64_t n, const uint64_t *off, const uint8_t *bytes,
+                                 const uint8_t *bits, const uint64_t *d_len, uint64_t size, uint64_t magic, int k,
+                                 uint8_t *out) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k_bloom_contains, dim3(grid_for(n, 256)), dim3(256), 0, st, n, off, bytes, bits, d_len, size,
+                       magic, k, out);
+    SK_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+hipError_t launch_bloom_probes(hipStream_t st, uint64_t n, const uint64_t *off, const uint8_t *bytes, uint64_t size,
+                               uint64_t magic, int k, uint64_t *keys) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k_bloom_probes, dim3(grid_for(n, 256)), dim3(256), 0, st, n, off, bytes, size, magic, k, keys);
+    SK_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+hipError_t launch_bloom_apply(hipStream_t st, uint64_t m, const uint64_t *keys, uint8_t *bits, uint64_t *d_len, int k,
+                              uint8_t *out) {
+    if (!m) return hipSuccess;
+    hipLaunchKernelGGL(k_bloom_apply, dim3(grid_for(m, 256)), dim3(256), 0, st, m, keys, bits, d_len, k, out);
+    SK_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+hipError_t launch_getbit_multi(hipStream_t st, uint64_t n, const uint32_t *sid, const uint64_t *offs, const void *dir,
+                               uint8_t *out) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k_getbit_multi, dim3(grid_for(n, 256)), dim3(256), 0, st, n, sid, offs,
+                       reinterpret_cast<const DirEnt *>(dir), out);
+    SK_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+hipError_t launch_getbit_single(hipStream_t st, uint64_t n, const uint64_t *offs, const uint8_t *buf,
+                                const uint64_t *d_len, uint8_t *out) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k_getbit_single, dim3(grid_for(n, 256)), dim3(256), 0, st, n, offs, buf, d_len, out);
+    SK_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+hipError_t launch_setbit_keys(hipStream_t st, uint64_t n, const uint32_t *sid, const uint64_t *offs, uint64_t *keys,
+                              uint32_t *vals) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k_setbit_keys, dim3(grid_for(n, 256)), dim3(256), 0, st, n, sid, offs, keys, vals);
+    SK_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+hipError_t launch_setbit_apply(hipStream_t st, uint64_t n, const uint64_t *keys, const uint32_t *vals,
+                               const uint8_t *values, uint8_t value_all, void *dir, uint8_t *out_old) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k_setbit_apply, dim3(grid_for(n, 256)), dim3(256), 0, st, n, keys, vals, values, value_all,
+                       reinterpret_cast<DirEnt *>(dir), out_old);
+    SK_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+hipError_t launch_setbit_void(hipStream_t st, uint64_t n, const uint64_t *offs, uint8_t *buf, uint32_t value) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k_setbit_void, dim3(grid_for(n, 256)), dim3(256), 0, st, n, offs, buf, value);
+    SK_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+hipError_t launch_max_u64(hipStream_t st, uint64_t n, const uint64_t *v, uint64_t *out) {
+    hipError_t e = hipMemsetAsync(out, 0, sizeof(uint64_t), st);
+    if (e != hipSuccess || !n) return e;
+    hipLaunchKernelGGL(k_max_u64, dim3(grid_for(n, 256, 1024)), dim3(256), 0, st, n, v, out);
+    SK_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+hipError_t launch_bitcount(hipStream_t st, const uint8_t *buf, uint64_t len, uint64_t *out) {
+    hipError_t e = hipMemsetAsync(out, 0, sizeof(uint64_t), st);
+    if (e != hipSuccess || !len) return e;
+    hipLaunchKernelGGL(k_bitcount, dim3(grid_for((len + 15) / 16, 256, 2048)), dim3(256), 0, st, buf, len,
+                       (unsigned long long *)out);
+    SK_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+hipError_t launch_bitop(hipStream_t st, int op, uint32_t nsrc, const uint8_t *const *srcs, const uint64_t *lens,
+                        uint64_t maxlen, uint8_t *dst) {
+    if (!maxlen) return hipSuccess;
+    hipLaunchKernelGGL(k_bitop, dim3(grid_for((maxlen + 15) / 16, 256, 4096)), dim3(256), 0, st, op, nsrc, srcs, lens,
+                       maxlen, dst);
+    SK_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+} // namespace sk

@@ -1,0 +1,1461 @@
+// sk_store.cpp -- GPU-resident sketch store + batched command executor behind
+// the C ABI in include/redisson_sketch.h.
+//
+// Replaces, for sketch key types, what Redisson's L3 executor hands to Netty
+// and redis-server (M:command/CommandAsyncService.java:378, batch hook
+// M:command/CommandBatchService.java:91-111,184-293).  Host work here is
+// bookkeeping only (key directory, validation, capacity, error text, and the
+// final scalar steps of PFCOUNT / Bloom count); every per-element and
+// per-register step runs in the HIP kernels of sk_kernels.hip.  There is no
+// CPU fallback: without a working device sk_open() fails.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/redisson_sketch.h"
+#include "sk_internal.h"
+
+namespace {
+
+constexpr uint64_t kHllBytes = 16384;
+constexpr int64_t kBloomMaxSize = 2LL * 2147483647LL; // M:RedissonBloomFilter.java:52
+constexpr uint32_t kNoId = 0xffffffffu;
+
+struct DirEnt { // mirrors sk::DirEnt in sk_kernels.hip
+    uint8_t *ptr;
+    uint64_t len;
+    uint64_t cap;
+};
+
+struct KeyEnt {
+    int type;
+    uint32_t id;
+};
+
+struct BloomCfg {
+    int64_t size;
+    int32_t k;
+    int64_t expected;
+    double fpp;
+};
+
+struct DBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t bytes) {
+        if (bytes <= cap) return hipSuccess;
+        size_t nc = std::max(bytes, cap * 2);
+        if (p) {
+            hipError_t e = hipFree(p);
+            if (e != hipSuccess) return e;
+            p = nullptr;
+            cap = 0;
+        }
+        hipError_t e = hipMalloc(&p, nc);
+        if (e != hipSuccess) return e;
+        cap = nc;
+        return hipSuccess;
+    }
+    template <class T> T *as() const { return reinterpret_cast<T *>(p); }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+unsigned bits_for(uint64_t maxval) { // bits needed to represent values 0..maxval
+    unsigned b = 0;
+    while (b < 64 && (maxval >> b)) b++;
+    return b ? b : 1;
+}
+
+uint64_t round16(uint64_t x) { return (x + 15) & ~uint64_t(15); }
+
+double g_pe[64];
+struct PeInit {
+    PeInit() {
+        g_pe[0] = 1;
+        for (int j = 1; j < 64; j++) g_pe[j] = 1.0 / double(1ULL << j);
+    }
+} g_pe_init;
+
+// ---- estimator (redis hyperloglog.c hllCount) -------------------------
+uint64_t estimate_v3(double E, int ez) {
+    const double m = 16384;
+    double alpha = 0.7213 / (1 + 1.079 / m);
+    E = (1 / E) * alpha * m * m;
+    if (E < m * 2.5 && ez != 0) {
+        E = m * std::log(m / ez);
+    } else if (E < 72000) { // m == 16384
+        double bias = 5.9119 * 1.0e-18 * (E * E * E * E) - 1.4253 * 1.0e-12 * (E * E * E) +
+                      1.2940 * 1.0e-7 * (E * E) - 5.2921 * 1.0e-3 * E + 83.3216;
+        E -= E * (bias / 100);
+    }
+    return uint64_t(E);
+}
+double hll_sigma(double x) {
+    if (x == 1.) return INFINITY;
+    double zp, y = 1, z = x;
+    do {
+        x *= x;
+        zp = z;
+        z += x * y;
+        y += y;
+    } while (zp != z);
+    return z;
+}
+double hll_tau(double x) {
+    if (x == 0. || x == 1.) return 0.;
+    double zp, y = 1.0, z = 1 - x;
+    do {
+        x = std::sqrt(x);
+        zp = z;
+        y *= 0.5;
+        z -= std::pow(1 - x, 2) * y;
+    } while (zp != z);
+    return z / 3;
+}
+uint64_t estimate_v5(const uint32_t *hist) {
+    double m = 16384;
+    double z = m * hll_tau((m - hist[51]) / m);
+    for (int j = 50; j >= 1; --j) {
+        z += hist[j];
+        z *= 0.5;
+    }
+    z += m * hll_sigma(hist[0] / m);
+    return uint64_t(llroundl(0.721347520444481703680 * m * m / z));
+}
+bool hist_exact_v3(const uint32_t *hist) {
+    for (int v = 40; v < 64; v++)
+        if (hist[v]) return false;
+    return true;
+}
+// Redis-ordered sums, needed only when a register >= 40 (3.x estimator)
+double dense_sum(const uint8_t *r, int *ez) {
+    double E = 0;
+    int z = 0;
+    for (int j = 0; j < 1024; j++, r += 16) {
+        for (int t = 0; t < 16; t++) z += (r[t] == 0);
+        E += (g_pe[r[0]] + g_pe[r[1]]) + (g_pe[r[2]] + g_pe[r[3]]) + (g_pe[r[4]] + g_pe[r[5]]) +
+             (g_pe[r[6]] + g_pe[r[7]]) + (g_pe[r[8]] + g_pe[r[9]]) + (g_pe[r[10]] + g_pe[r[11]]) +
+             (g_pe[r[12]] + g_pe[r[13]]) + (g_pe[r[14]] + g_pe[r[15]]);
+    }
+    *ez = z;
+    return E;
+}
+double raw_sum(const uint8_t *r, int *ez) {
+    double E = 0;
+    int z = 0;
+    for (int j = 0; j < 2048; j++, r += 8) {
+        uint64_t w;
+        std::memcpy(&w, r, 8);
+        if (w == 0) {
+            z += 8;
+            continue;
+        }
+        for (int t = 0; t < 8; t++) {
+            if (r[t]) E += g_pe[r[t]];
+            else z++;
+        }
+    }
+    E += z;
+    *ez = z;
+    return E;
+}
+
+} // namespace
+
+struct sk_ctx {
+    std::mutex mu;
+    int device = 0;
+    int redis_major = 3;
+    uint64_t max_bit_offset = 1ULL << 32;
+    uint64_t max_batch = 1ULL << 22;
+    hipStream_t st = nullptr;
+    std::string err;
+
+    std::unordered_map<std::string, KeyEnt> keys;
+    std::unordered_map<std::string, BloomCfg> bloom; // keyed by "{name}__config"
+
+    // HLL arena: slab id -> arena + id*16 KiB; free slabs are kept zeroed
+    uint8_t *arena = nullptr;
+    uint64_t hll_cap = 0, hll_next = 0;
+    std::vector<uint32_t> hll_free;
+
+    // strings: host mirror of {ptr, cap}; len lives in the device directory
+    std::vector<DirEnt> strs;
+    std::vector<uint32_t> str_free;
+    DirEnt *d_dir = nullptr;
+    uint64_t dir_cap = 0;
+
+    // workspace
+    uint32_t *d_zero = nullptr; // device u32[4] zeros: id 0 / empty length
+    DBuf keys_a, keys_b, vals_a, vals_b, sort_tmp, in_off, in_bytes, in_ids, in_cmd, out_u8, misc, partial, hist,
+        uni, ptrs;
+};
+
+namespace {
+
+int fail(sk_ctx *c, int code, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    c->err = buf;
+    return code;
+}
+#define HIPCHK(c, expr)                                                                                                \
+    do {                                                                                                               \
+        hipError_t e__ = (expr);                                                                                       \
+        if (e__ != hipSuccess) return fail((c), SK_EDEVICE, "HIP error %s at %s:%d", hipGetErrorString(e__), __FILE__, \
+                                           __LINE__);                                                                  \
+    } while (0)
+
+const char *kWrongType = "WRONGTYPE Operation against a key holding the wrong kind of value";
+const char *kNotHll = "WRONGTYPE Key is not a valid HyperLogLog string value.";
+const char *kRange = "ERR bit offset is not an integer or out of range";
+const char *kCfgChanged = "ERR Error running script: Bloom filter config has been changed";
+const char *kNotInit = "Bloom filter is not initialized!";
+
+std::string key_of(const uint8_t *b, uint64_t len) { return std::string(reinterpret_cast<const char *>(b), len); }
+std::string key_at(const uint64_t *off, const uint8_t *bytes, uint64_t i) {
+    return std::string(reinterpret_cast<const char *>(bytes + off[i]), off[i + 1] - off[i]);
+}
+
+int sync(sk_ctx *c) {
+    HIPCHK(c, hipStreamSynchronize(c->st));
+    return SK_OK;
+}
+
+// --------------------------------------------------------------- HLL slabs
+int hll_grow(sk_ctx *c, uint64_t need) {
+    if (need <= c->hll_cap) return SK_OK;
+    uint64_t nc = std::max<uint64_t>(need, c->hll_cap * 2);
+    uint8_t *na = nullptr;
+    if (hipMalloc(&na, nc * kHllBytes) != hipSuccess)
+        return fail(c, SK_ENOMEM, "cannot allocate %llu HLL slabs", (unsigned long long)nc);
+    HIPCHK(c, hipMemsetAsync(na + c->hll_cap * kHllBytes, 0, (nc - c->hll_cap) * kHllBytes, c->st));
+    if (c->arena) {
+        HIPCHK(c, hipMemcpyAsync(na, c->arena, c->hll_cap * kHllBytes, hipMemcpyDeviceToDevice, c->st));
+        HIPCHK(c, hipStreamSynchronize(c->st));
+        HIPCHK(c, hipFree(c->arena));
+    }
+    c->arena = na;
+    c->hll_cap = nc;
+    return SK_OK;
+}
+
+int hll_alloc(sk_ctx *c, uint32_t *id) {
+    if (!c->hll_free.empty()) {
+        *id = c->hll_free.back();
+        c->hll_free.pop_back();
+        return SK_OK;
+    }
+    int r = hll_grow(c, c->hll_next + 1);
+    if (r) return r;
+    *id = uint32_t(c->hll_next++);
+    return SK_OK;
+}
+
+// lookup or create an HLL key (PFADD / PFMERGE create)
+int hll_get(sk_ctx *c, const std::string &k, bool create, uint32_t *id, bool *created) {
+    if (created) *created = false;
+    auto it = c->keys.find(k);
+    if (it != c->keys.end()) {
+        if (it->second.type != SK_TYPE_HLL) return fail(c, SK_EWRONGTYPE, "%s", kNotHll);
+        *id = it->second.id;
+        return SK_OK;
+    }
+    if (!create) {
+        *id = kNoId;
+        return SK_OK;
+    }
+    int r = hll_alloc(c, id);
+    if (r) return r;
+    c->keys[k] = KeyEnt{SK_TYPE_HLL, *id};
+    if (created) *created = true;
+    return SK_OK;
+}
+
+// -------------------------------------------------------------- strings
+int dir_write(sk_ctx *c, uint32_t id, const DirEnt &e) {
+    HIPCHK(c, hipMemcpyAsync(c->d_dir + id, &e, sizeof(DirEnt), hipMemcpyHostToDevice, c->st));
+    return SK_OK;
+}
+int str_len(sk_ctx *c, uint32_t id, uint64_t *len) {
+    HIPCHK(c, hipMemcpyAsync(len, &c->d_dir[id].len, sizeof(uint64_t), hipMemcpyDeviceToHost, c->st));
+    return sync(c);
+}
+int str_set_len(sk_ctx *c, uint32_t id, uint64_t len) {
+    HIPCHK(c, hipMemcpyAsync(&c->d_dir[id].len, &len, sizeof(uint64_t), hipMemcpyHostToDevice, c->st));
+    return sync(c); // len is a stack variable
+}
+
+int str_alloc(sk_ctx *c, uint64_t cap, uint32_t *id) {
+    cap = round16(std::max<uint64_t>(cap, 16));
+    uint8_t *p = nullptr;
+    if (hipMalloc(&p, cap) != hipSuccess)
+        return fail(c, SK_ENOMEM, "cannot allocate %llu-byte string", (unsigned long long)cap);
+    HIPCHK(c, hipMemsetAsync(p, 0, cap, c->st));
+    uint32_t nid;
+    if (!c->str_free.empty()) {
+        nid = c->str_free.back();
+        c->str_free.pop_back();
+    } else {
+        nid = uint32_t(c->strs.size());
+        c->strs.push_back(DirEnt{nullptr, 0, 0});
+    }
+    if (c->strs.size() > c->dir_cap) {
+        uint64_t nc = std::max<uint64_t>(64, c->dir_cap * 2);
+        DirEnt *nd = nullptr;
+        HIPCHK(c, hipMalloc(&nd, nc * sizeof(DirEnt)));
+        if (c->d_dir) {
+            HIPCHK(c, hipMemcpyAsync(nd, c->d_dir, c->dir_cap * sizeof(DirEnt), hipMemcpyDeviceToDevice, c->st));
+            HIPCHK(c, hipStreamSynchronize(c->st));
+            HIPCHK(c, hipFree(c->d_dir));
+        }
+        c->d_dir = nd;
+        c->dir_cap = nc;
+    }
+    c->strs[nid] = DirEnt{p, 0, cap};
+    *id = nid;
+    int r = dir_write(c, nid, c->strs[nid]);
+    if (r) return r;
+    return sync(c);
+}
+
+int str_free(sk_ctx *c, uint32_t id) {
+    HIPCHK(c, hipStreamSynchronize(c->st));
+    if (c->strs[id].ptr) HIPCHK(c, hipFree(c->strs[id].ptr));
+    c->strs[id] = DirEnt{nullptr, 0, 0};
+    c->str_free.push_back(id);
+    return dir_write(c, id, c->strs[id]);
+}
+
+// grow capacity to >= need bytes (new bytes zero, content kept)
+int str_reserve(sk_ctx *c, uint32_t id, uint64_t need) {
+    DirEnt &e = c->strs[id];
+    if (need <= e.cap) return SK_OK;
+    uint64_t nc = round16(std::max(need, e.cap * 2));
+    uint8_t *p = nullptr;
+    if (hipMalloc(&p, nc) != hipSuccess)
+        return fail(c, SK_ENOMEM, "cannot allocate %llu-byte string", (unsigned long long)nc);
+    HIPCHK(c, hipMemsetAsync(p + e.cap, 0, nc - e.cap, c->st));
+    HIPCHK(c, hipMemcpyAsync(p, e.ptr, e.cap, hipMemcpyDeviceToDevice, c->st));
+    uint64_t len;
+    int r = str_len(c, id, &len);
+    if (r) return r;
+    HIPCHK(c, hipFree(e.ptr));
+    e.ptr = p;
+    e.cap = nc;
+    DirEnt w{p, len, nc};
+    r = dir_write(c, id, w);
+    if (r) return r;
+    return sync(c);
+}
+
+// lookup or create a plain string key (SETBIT / SET / BITOP dest)
+int str_get(sk_ctx *c, const std::string &k, bool create, uint64_t init_cap, uint32_t *id) {
+    auto it = c->keys.find(k);
+    if (it != c->keys.end()) {
+        if (it->second.type != SK_TYPE_STRING) return fail(c, SK_EWRONGTYPE, "%s", kWrongType);
+        *id = it->second.id;
+        return SK_OK;
+    }
+    if (!create) {
+        *id = kNoId;
+        return SK_OK;
+    }
+    int r = str_alloc(c, init_cap, id);
+    if (r) return r;
+    c->keys[k] = KeyEnt{SK_TYPE_STRING, *id};
+    return SK_OK;
+}
+
+int del_key(sk_ctx *c, const std::string &k, bool *removed) {
+    *removed = false;
+    auto b = c->bloom.find(k);
+    if (b != c->bloom.end()) {
+        c->bloom.erase(b);
+        *removed = true;
+        return SK_OK;
+    }
+    auto it = c->keys.find(k);
+    if (it == c->keys.end()) return SK_OK;
+    KeyEnt e = it->second;
+    c->keys.erase(it);
+    *removed = true;
+    if (e.type == SK_TYPE_HLL) {
+        HIPCHK(c, hipMemsetAsync(c->arena + uint64_t(e.id) * kHllBytes, 0, kHllBytes, c->st));
+        c->hll_free.push_back(e.id);
+        return SK_OK;
+    }
+    return str_free(c, e.id);
+}
+
+// ------------------------------------------------------------ PFADD core
+// Device batch: n elements with per-element slab id and command index.
+// hash -> stable radix sort on (slab, register) -> segment heads apply.
+int pfadd_device(sk_ctx *c, uint64_t n, const uint32_t *d_ids, const uint64_t *d_off, const uint8_t *d_bytes,
+                 const uint32_t *d_cmd, uint64_t n_cmds, uint8_t *d_changed) {
+    if (!n) return SK_OK;
+    unsigned id_bits = bits_for(c->hll_next ? c->hll_next - 1 : 0);
+    unsigned cmd_bits = bits_for(n_cmds ? n_cmds - 1 : 0);
+    if (6 + cmd_bits + 14 + id_bits > 64) return fail(c, SK_EINVAL, "PFADD batch too large for key packing");
+    unsigned slot_shift = 6 + cmd_bits;
+    uint64_t cmd_mask = (cmd_bits >= 64) ? ~0ull : ((1ull << cmd_bits) - 1);
+    HIPCHK(c, c->keys_a.ensure(n * 8));
+    HIPCHK(c, c->keys_b.ensure(n * 8));
+    size_t tmp = 0;
+    HIPCHK(c, sk::sort_keys_size(n, slot_shift, slot_shift + 14 + id_bits, &tmp));
+    HIPCHK(c, c->sort_tmp.ensure(tmp));
+    HIPCHK(c, sk::launch_pfadd_hash(c->st, n, d_ids, d_off, d_bytes, d_cmd, c->redis_major >= 5, slot_shift,
+                                    c->keys_a.as<uint64_t>()));
+    HIPCHK(c, sk::sort_keys(c->st, c->sort_tmp.p, c->sort_tmp.cap, c->keys_a.as<uint64_t>(), c->keys_b.as<uint64_t>(),
+                            n, slot_shift, slot_shift + 14 + id_bits));
+    HIPCHK(c, sk::launch_pfadd_apply(c->st, n, c->keys_b.as<uint64_t>(), slot_shift, cmd_mask, c->arena, d_changed));
+    return SK_OK;
+}
+
+int hll_histograms(sk_ctx *c, uint64_t n, const uint32_t *d_ids, const uint8_t *base, std::vector<uint32_t> &h) {
+    HIPCHK(c, c->hist.ensure(n * 64 * 4));
+    HIPCHK(c, sk::launch_hll_hist(c->st, n, d_ids, base, c->hist.as<uint32_t>()));
+    h.resize(n * 64);
+    HIPCHK(c, hipMemcpyAsync(h.data(), c->hist.p, n * 64 * 4, hipMemcpyDeviceToHost, c->st));
+    return sync(c);
+}
+
+int union_into(sk_ctx *c, const std::vector<uint32_t> &ids, uint8_t *d_out, int include_out) {
+    HIPCHK(c, c->in_ids.ensure(std::max<size_t>(ids.size(), 1) * 4));
+    if (!ids.empty())
+        HIPCHK(c, hipMemcpyAsync(c->in_ids.p, ids.data(), ids.size() * 4, hipMemcpyHostToDevice, c->st));
+    const uint64_t max_groups = 4096;
+    HIPCHK(c, c->partial.ensure(max_groups * kHllBytes));
+    HIPCHK(c, sk::launch_hll_union(c->st, ids.size(), c->in_ids.as<uint32_t>(), c->arena, c->partial.as<uint8_t>(),
+                                   max_groups, d_out, include_out));
+    return sync(c); // ids is a host vector
+}
+
+uint64_t estimate_host(sk_ctx *c, const uint32_t *hist, const uint8_t *d_regs, bool raw_order, int *rc) {
+    *rc = SK_OK;
+    if (c->redis_major >= 5) return estimate_v5(hist);
+    if (hist_exact_v3(hist)) {
+        double E = 0;
+        for (int v = 0; v < 64; v++) E += double(hist[v]) * g_pe[v]; // every partial sum exact
+        return estimate_v3(E, int(hist[0]));
+    }
+    // a register >= 40: the summation order matters -> redo it in Redis order
+    std::vector<uint8_t> regs(kHllBytes);
+    if (hipMemcpy(regs.data(), d_regs, kHllBytes, hipMemcpyDeviceToHost) != hipSuccess) {
+        *rc = fail(c, SK_EDEVICE, "register readback failed");
+        return 0;
+    }
+    int ez;
+    double E = raw_order ? raw_sum(regs.data(), &ez) : dense_sum(regs.data(), &ez);
+    return estimate_v3(E, ez);
+}
+
+// ------------------------------------------------------------- bit strings
+int check_offsets(sk_ctx *c, uint64_t n, const uint64_t *offs, std::vector<uint8_t> &ok) {
+    ok.assign(n, 1);
+    int r = SK_OK;
+    for (uint64_t i = 0; i < n; i++)
+        if (offs[i] >= c->max_bit_offset) {
+            ok[i] = 0;
+            r = fail(c, SK_ERANGE, "%s", kRange);
+        }
+    return r;
+}
+
+int bloom_cfg(sk_ctx *c, const std::string &name, BloomCfg **out) {
+    auto it = c->bloom.find("{" + name + "}__config");
+    if (it == c->bloom.end()) return fail(c, SK_ENOTINIT, "%s", kNotInit);
+    *out = &it->second;
+    return SK_OK;
+}
+
+uint64_t magic_for(uint64_t d) { return ~0ull / d; }
+
+} // namespace
+
+// =================================================================== C ABI
+extern "C" {
+
+const char *sk_strerror(int s) {
+    switch (s) {
+    case SK_OK: return "OK";
+    case SK_EWRONGTYPE: return kWrongType;
+    case SK_ERANGE: return kRange;
+    case SK_ECONFIG: return kCfgChanged;
+    case SK_ENOTINIT: return kNotInit;
+    case SK_EDEVICE: return "device error";
+    case SK_EINVAL: return "invalid argument";
+    case SK_ENOMEM: return "out of memory";
+    case SK_ESYNTAX: return "ERR BITOP NOT must be called with a single source key.";
+    case SK_ETOOBIG: return "Bloom filter can't be greater than 4294967294";
+    default: return "unknown";
+    }
+}
+
+int sk_open(const sk_config *cfg, sk_ctx **out) {
+    if (!out) return SK_EINVAL;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return SK_EDEVICE;
+    sk_ctx *c = new sk_ctx();
+    if (cfg) {
+        c->device = cfg->device;
+        c->redis_major = cfg->redis_major ? cfg->redis_major : 3;
+        if (cfg->max_bit_offset) c->max_bit_offset = cfg->max_bit_offset;
+        if (cfg->max_batch) c->max_batch = cfg->max_batch;
+    }
+    if (c->device < 0 || c->device >= ndev || hipSetDevice(c->device) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return SK_EDEVICE;
+    }
+    uint64_t cap = (cfg && cfg->hll_capacity) ? cfg->hll_capacity : 1024;
+    if (hll_grow(c, cap) != SK_OK || c->misc.ensure(4096) != hipSuccess ||
+        hipMalloc(&c->d_zero, 16) != hipSuccess || hipMemsetAsync(c->d_zero, 0, 16, c->st) != hipSuccess ||
+        hipMemsetAsync(c->misc.p, 0, 4096, c->st) != hipSuccess || hipStreamSynchronize(c->st) != hipSuccess) {
+        sk_close(c);
+        return SK_EDEVICE;
+    }
+    *out = c;
+    return SK_OK;
+}
+
+int sk_close(sk_ctx *c) {
+    if (!c) return SK_OK;
+    (void)hipSetDevice(c->device);
+    if (c->st) (void)hipStreamSynchronize(c->st);
+    for (auto &e : c->strs)
+        if (e.ptr) (void)hipFree(e.ptr);
+    if (c->arena) (void)hipFree(c->arena);
+    if (c->d_dir) (void)hipFree(c->d_dir);
+    if (c->d_zero) (void)hipFree(c->d_zero);
+    for (DBuf *b : {&c->keys_a, &c->keys_b, &c->vals_a, &c->vals_b, &c->sort_tmp, &c->in_off, &c->in_bytes,
+                    &c->in_ids, &c->in_cmd, &c->out_u8, &c->misc, &c->partial, &c->hist, &c->uni, &c->ptrs})
+        b->release();
+    if (c->st) (void)hipStreamDestroy(c->st);
+    delete c;
+    return SK_OK;
+}
+
+const char *sk_last_error(sk_ctx *c) { return c ? c->err.c_str() : "no context"; }
+void *sk_stream(sk_ctx *c) { return c ? (void *)c->st : nullptr; }
+int sk_sync(sk_ctx *c) {
+    std::lock_guard<std::mutex> g(c->mu);
+    return sync(c);
+}
+
+uint32_t sk_crc16(const uint8_t *p, uint64_t len) {
+    // CRC16-XMODEM: poly 0x1021, init 0 (M:connection/CRC16.java:23-61)
+    static uint16_t table[256];
+    static bool init = false;
+    if (!init) {
+        for (int i = 0; i < 256; i++) {
+            uint16_t crc = uint16_t(i << 8);
+            for (int b = 0; b < 8; b++) crc = (crc & 0x8000) ? uint16_t((crc << 1) ^ 0x1021) : uint16_t(crc << 1);
+            table[i] = crc;
+        }
+        init = true;
+    }
+    uint32_t crc = 0;
+    for (uint64_t i = 0; i < len; i++) crc = ((crc << 8) ^ table[((crc >> 8) ^ p[i]) & 0xff]) & 0xffff;
+    return crc;
+}
+
+int32_t sk_calc_slot(const uint8_t *key, uint64_t len) {
+    if (!key) return 0;
+    const uint8_t *b = static_cast<const uint8_t *>(memchr(key, '{', len));
+    if (b) {
+        const uint8_t *e = static_cast<const uint8_t *>(memchr(key, '}', len)); // first '}' anywhere
+        if (!e || e < b + 1) return -1; // Java substring() throws
+        return int32_t(sk_crc16(b + 1, uint64_t(e - b - 1)) % 16384);
+    }
+    return int32_t(sk_crc16(key, len) % 16384);
+}
+
+int32_t sk_owner(const uint8_t *key, uint64_t len, int32_t n_gpus) {
+    int32_t s = sk_calc_slot(key, len);
+    if (s < 0 || n_gpus <= 0) return -1;
+    return s % n_gpus;
+}
+
+int64_t sk_bloom_optimal_bits(int64_t n, double p) {
+    if (p == 0) p = 4.9e-324; // Double.MIN_VALUE
+    double v = double(-n) * std::log(p) / (std::log(2) * std::log(2));
+    if (v != v) return 0;
+    if (v >= 9.2233720368547758e18) return INT64_MAX;
+    if (v <= -9.2233720368547758e18) return INT64_MIN;
+    return int64_t(v);
+}
+
+int32_t sk_bloom_optimal_k(int64_t n, int64_t m) {
+    double x = double(m) / double(n) * std::log(2);
+    double r = std::floor(x + 0.5); // Math.round
+    int64_t l = (r != r) ? 0 : (r >= 9.2233720368547758e18 ? INT64_MAX : int64_t(r));
+    int32_t k = int32_t(l); // (int) of a long: low 32 bits
+    return std::max(1, k);
+}
+
+uint64_t sk_hll_estimate_hist(const uint32_t *hist, int redis_major) {
+    if (redis_major >= 5) return estimate_v5(hist);
+    double E = 0;
+    for (int v = 0; v < 64; v++) E += double(hist[v]) * g_pe[v];
+    return estimate_v3(E, int(hist[0]));
+}
+
+int sk_type(sk_ctx *c, const uint8_t *key, uint64_t len, int *out) {
+    std::lock_guard<std::mutex> g(c->mu);
+    std::string k = key_of(key, len);
+    auto it = c->keys.find(k);
+    if (it != c->keys.end()) *out = it->second.type;
+    else *out = c->bloom.count(k) ? 3 : SK_TYPE_NONE;
+    return SK_OK;
+}
+
+int sk_del(sk_ctx *c, uint32_t n, const uint64_t *off, const uint8_t *bytes, uint64_t *removed) {
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(c, hipSetDevice(c->device));
+    uint64_t cnt = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        bool r;
+        int rc = del_key(c, key_at(off, bytes, i), &r);
+        if (rc) return rc;
+        cnt += r;
+    }
+    if (removed) *removed = cnt;
+    return sync(c);
+}
+
+int sk_hll_resolve(sk_ctx *c, uint32_t n, const uint64_t *off, const uint8_t *bytes, uint32_t *ids,
+                   uint8_t *created) {
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(c, hipSetDevice(c->device));
+    for (uint32_t i = 0; i < n; i++) {
+        bool cr;
+        int r = hll_get(c, key_at(off, bytes, i), true, &ids[i], &cr);
+        if (r) return r;
+        if (created) created[i] = cr;
+    }
+    return sync(c);
+}
+
+// ---------------------------------------------------------------- PFADD
+int sk_pfadd(sk_ctx *c, uint32_t n_cmds, const uint64_t *key_off, const uint8_t *key_bytes,
+             const uint32_t *elem_counts, const uint64_t *elem_off, const uint8_t *elem_bytes, uint8_t *out_changed) {
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(c, hipSetDevice(c->device));
+    if (!n_cmds) return SK_OK;
+    // resolve keys in command order; the first command on a created key replies 1
+    std::vector<uint32_t> cmd_key(n_cmds);
+    std::vector<uint8_t> first_created(n_cmds, 0);
+    std::unordered_map<uint32_t, bool> pending_created;
+    int status = SK_OK;
+    std::vector<uint8_t> valid(n_cmds, 1);
+    for (uint32_t i = 0; i < n_cmds; i++) {
+        bool cr;
+        int r = hll_get(c, key_at(key_off, key_bytes, i), true, &cmd_key[i], &cr);
+        if (r == SK_EWRONGTYPE) {
+            valid[i] = 0;
+            status = r;
+            continue;
+        }
+        if (r) return r;
+        if (cr) first_created[i] = 1;
+    }
+    std::memset(out_changed, 0, n_cmds);
+    // chunk by elements, never more than max_batch elements per device batch
+    uint64_t total_e = 0;
+    std::vector<uint64_t> cmd_e0(n_cmds + 1);
+    for (uint32_t i = 0; i < n_cmds; i++) {
+        cmd_e0[i] = total_e;
+        total_e += elem_counts[i];
+    }
+    cmd_e0[n_cmds] = total_e;
+    uint32_t c0 = 0;
+    std::vector<uint32_t> h_ids, h_cmd;
+    while (c0 < n_cmds) {
+        // commands [c0, c1) -- a single command larger than max_batch goes alone
+        uint32_t c1 = c0;
+        uint64_t ne = 0;
+        while (c1 < n_cmds && (c1 == c0 || ne + elem_counts[c1] <= c->max_batch)) ne += elem_counts[c1++];
+        // element list of valid commands
+        h_ids.clear();
+        h_cmd.clear();
+        uint64_t b0 = elem_off[cmd_e0[c0]], b1 = elem_off[cmd_e0[c1]];
+        for (uint32_t cc = c0; cc < c1; cc++) {
+            if (!valid[cc]) continue;
+            for (uint64_t e = cmd_e0[cc]; e < cmd_e0[cc + 1]; e++) {
+                h_ids.push_back(cmd_key[cc]);
+                h_cmd.push_back(cc - c0);
+            }
+        }
+        uint64_t m = h_ids.size();
+        if (m) {
+            // re-pack the bytes of the valid commands' elements (+16 B padding)
+            std::vector<uint64_t> off2(m + 1);
+            std::vector<uint8_t> bytes2;
+            bytes2.reserve(b1 - b0 + 16);
+            uint64_t t = 0;
+            uint64_t ei = 0;
+            for (uint32_t cc = c0; cc < c1; cc++) {
+                if (!valid[cc]) continue;
+                for (uint64_t e = cmd_e0[cc]; e < cmd_e0[cc + 1]; e++, ei++) {
+                    uint64_t l = elem_off[e + 1] - elem_off[e];
+                    off2[ei] = t;
+                    bytes2.insert(bytes2.end(), elem_bytes + elem_off[e], elem_bytes + elem_off[e] + l);
+                    t += l;
+                }
+            }
+            off2[m] = t;
+            bytes2.resize(t + 16, 0);
+            HIPCHK(c, c->in_ids.ensure(m * 4));
+            HIPCHK(c, c->in_cmd.ensure(m * 4));
+            HIPCHK(c, c->in_off.ensure((m + 1) * 8));
+            HIPCHK(c, c->in_bytes.ensure(bytes2.size()));
+            HIPCHK(c, c->out_u8.ensure(c1 - c0));
+            HIPCHK(c, hipMemcpyAsync(c->in_ids.p, h_ids.data(), m * 4, hipMemcpyHostToDevice, c->st));
+            HIPCHK(c, hipMemcpyAsync(c->in_cmd.p, h_cmd.data(), m * 4, hipMemcpyHostToDevice, c->st));
+            HIPCHK(c, hipMemcpyAsync(c->in_off.p, off2.data(), (m + 1) * 8, hipMemcpyHostToDevice, c->st));
+            HIPCHK(c, hipMemcpyAsync(c->in_bytes.p, bytes2.data(), bytes2.size(), hipMemcpyHostToDevice, c->st));
+            HIPCHK(c, hipMemsetAsync(c->out_u8.p, 0, c1 - c0, c->st));
+            int r = pfadd_device(c, m, c->in_ids.as<uint32_t>(), c->in_off.as<uint64_t>(), c->in_bytes.as<uint8_t>(),
+                                 c->in_cmd.as<uint32_t>(), c1 - c0, c->out_u8.as<uint8_t>());
+            if (r) return r;
+            HIPCHK(c, hipMemcpyAsync(out_changed + c0, c->out_u8.p, c1 - c0, hipMemcpyDeviceToHost, c->st));
+            r = sync(c);
+            if (r) return r;
+        }
+        c0 = c1;
+    }
+    for (uint32_t i = 0; i < n_cmds; i++)
+        if (first_created[i]) out_changed[i] = 1;
+    return status;
+}
+
+int sk_pfadd_dev(sk_ctx *c, uint64_t n, const uint32_t *d_ids, const uint64_t *d_off, const uint8_t *d_bytes,
+                 uint64_t bytes_len, uint8_t *d_changed) {
+    (void)bytes_len;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(c, hipSetDevice(c->device));
+    if (!n) return SK_OK;
+    HIPCHK(c, hipMemsetAsync(d_changed, 0, n, c->st));
+    unsigned id_bits = bits_for(c->hll_next ? c->hll_next - 1 : 0);
+    uint64_t max_cmds = std::min<uint64_t>(c->max_batch, 1ull << std::min(32u, 64 - 20 - id_bits));
+    for (uint64_t s = 0; s < n; s += max_cmds) {
+        uint64_t m = std::min(max_cmds, n - s);
+        int r = pfadd_device(c, m, d_ids + s, d_off + s, d_bytes, nullptr, m, d_changed + s);
+        if (r) return r;
+    }
+    return sync(c);
+}
+
+// --------------------------------------------------------------- PFCOUNT
+int sk_hll_histogram_dev(sk_ctx *c, uint64_t n, const uint32_t *d_ids, uint32_t *d_hist) {
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, sk::launch_hll_hist(c->st, n, d_ids, c->arena, d_hist));
+    return sync(c);
+}
+
+int sk_pfcount(sk_ctx *c, uint32_t n_cmds, const uint32_t *nkeys, const uint64_t *key_off, const uint8_t *key_bytes,
+               int64_t *out) {
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(c, hipSetDevice(c->device));
+    // single-key commands: one histogram launch over all of them
+    std::vector<uint32_t> single_ids;
+    std::vector<uint32_t> single_cmd;
+    uint64_t k = 0;
+    int status = SK_OK;
+    std::vector<std::vector<uint32_t>> multi(n_cmds);
+    std::vector<uint8_t> is_multi(n_cmds, 0), bad(n_cmds, 0);
+    for (uint32_t cmd = 0; cmd < n_cmds; cmd++) {
+        out[cmd] = 0;
+        std::vector<uint32_t> ids;
+        for (uint32_t j = 0; j < nkeys[cmd]; j++, k++) {
+            uint32_t id;
+            int r = hll_get(c, key_at(key_off, key_bytes, k), false, &id, nullptr);
+            if (r == SK_EWRONGTYPE) {
+                bad[cmd] = 1;
+                status = r;
+                continue;
+            }
+            if (r) return r;
+            if (id != kNoId) ids.push_back(id);
+        }
+        if (bad[cmd]) continue;
+        if (nkeys[cmd] == 1) {
+            if (!ids.empty()) {
+                single_ids.push_back(ids[0]);
+                single_cmd.push_back(cmd);
+            }
+        } else {
+            is_multi[cmd] = 1;
+            multi[cmd] = std::move(ids);
+        }
+    }
+    std::vector<uint32_t> h;
+    if (!single_ids.empty()) {
+        HIPCHK(c, c->in_ids.ensure(single_ids.size() * 4));
+        HIPCHK(c, hipMemcpyAsync(c->in_ids.p, single_ids.data(), single_ids.size() * 4, hipMemcpyHostToDevice, c->st));
+        int r = hll_histograms(c, single_ids.size(), c->in_ids.as<uint32_t>(), c->arena, h);
+        if (r) return r;
+        for (size_t i = 0; i < single_ids.size(); i++) {
+            int rc;
+            out[single_cmd[i]] = int64_t(estimate_host(c, &h[i * 64], c->arena + uint64_t(single_ids[i]) * kHllBytes,
+                                                       false, &rc));
+            if (rc) return rc;
+        }
+    }
+    // multi-key commands: union into a temporary raw register array (nothing modified)
+    HIPCHK(c, c->uni.ensure(kHllBytes));
+    HIPCHK(c, c->misc.ensure(4096));
+    for (uint32_t cmd = 0; cmd < n_cmds; cmd++) {
+        if (!is_multi[cmd]) continue;
+        int r = union_into(c, multi[cmd], c->uni.as<uint8_t>(), 0);
+        if (r) return r;
+        r = hll_histograms(c, 1, c->d_zero, c->uni.as<uint8_t>(), h);
+        if (r) return r;
+        int rc;
+        out[cmd] = int64_t(estimate_host(c, h.data(), c->uni.as<uint8_t>(), true, &rc));
+        if (rc) return rc;
+    }
+    return status;
+}
+
+int sk_hll_union_dev(sk_ctx *c, uint64_t n, const uint32_t *d_ids, uint8_t *d_out) {
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(c, hipSetDevice(c->device));
+    const uint64_t max_groups = 4096;
+    HIPCHK(c, c->partial.ensure(max_groups * kHllBytes));
+    HIPCHK(c, sk::launch_hll_union(c->st, n, d_ids, c->arena, c->partial.as<uint8_t>(), max_groups, d_out, 0));
+    return sync(c);
+}
+
+int sk_pfmerge(sk_ctx *c, const uint8_t *dest, uint64_t dest_len, uint32_t n_src, const uint64_t *src_off,
+               const uint8_t *src_bytes) {
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(c, hipSetDevice(c->device));
+    // check every source first (pfmergeCommand checks before touching dest)
+    std::vector<uint32_t> ids;
+    for (uint32_t i = 0; i < n_src; i++) {
+        uint32_t id;
+        int r = hll_get(c, key_at(src_off, src_bytes, i), false, &id, nullptr);
+        if (r) return r;
+        if (id != kNoId) ids.push_back(id);
+    }
+    uint32_t did;
+    int r = hll_get(c, key_of(dest, dest_len), true, &did, nullptr);
+    if (r) return r;
+    return union_into(c, ids, c->arena + uint64_t(did) * kHllBytes, 1);
+}
+
+int sk_hll_merge_registers_dev(sk_ctx *c, const uint8_t *key, uint64_t len, const uint8_t *d_regs) {
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(c, hipSetDevice(c->device));
+    uint32_t did;
+    int r = hll_get(c, key_of(key, len), true, &did, nullptr);
+    if (r) return r;
+    // out = max(out, d_regs): a one-key union whose "arena" is d_regs
+    const uint64_t max_groups = 4096;
+    HIPCHK(c, c->partial.ensure(max_groups * kHllBytes));
+    HIPCHK(c, sk::launch_hll_union(c->st, 1, c->d_zero, d_regs, c->partial.as<uint8_t>(), max_groups,
+                                   c->arena + uint64_t(did) * kHllBytes, 1));
+    return sync(c);
+}
+
+int sk_hll_registers(sk_ctx *c, const uint8_t *key, uint64_t len, uint8_t *out) {
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(c, hipSetDevice(c->device));
+    uint32_t id;
+    int r = hll_get(c, key_of(key, len), false, &id, nullptr);
+    if (r) return r;
+    if (id == kNoId) {
+        std::memset(out, 0, kHllBytes);
+        return SK_OK;
+    }
+    HIPCHK(c, hipMemcpyAsync(out, c->arena + uint64_t(id) * kHllBytes, kHllBytes, hipMemcpyDeviceToHost, c->st));
+    return sync(c);
+}
+
+} // extern "C"
+
+// ============================================================== bit strings
+extern "C" {
+
+int sk_setbit(sk_ctx *c, uint32_t n, const uint64_t *key_off, const uint8_t *key_bytes, const uint64_t *offsets,
+              const uint8_t *values, uint8_t *out_old) {
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(c, hipSetDevice(c->device));
+    if (!n) return SK_OK;
+    std::vector<uint8_t> ok;
+    int status = check_offsets(c, n, offsets, ok);
+    // resolve / create keys, find per-key max offset (capacity + new length)
+    std::vector<uint32_t> sid(n);
+    std::unordered_map<uint32_t, uint64_t> maxoff;
+    for (uint32_t i = 0; i < n; i++) {
+        if (!ok[i]) {
+            sid[i] = kNoId;
+            continue;
+        }
+        int r = str_get(c, key_at(key_off, key_bytes, i), true, (offsets[i] >> 3) + 1, &sid[i]);
+        if (r == SK_EWRONGTYPE) {
+            ok[i] = 0;
+            sid[i] = kNoId;
+            status = r;
+            continue;
+        }
+        if (r) return r;
+        auto it = maxoff.find(sid[i]);
+        if (it == maxoff.end() || it->second < offsets[i]) maxoff[sid[i]] = offsets[i];
+    }
+    for (auto &kv : maxoff) {
+        uint64_t need = (kv.second >> 3) + 1, len;
+        int r = str_reserve(c, kv.first, need);
+        if (r) return r;
+        r = str_len(c, kv.first, &len);
+        if (r) return r;
+        if (need > len && (r = str_set_len(c, kv.first, need))) return r;
+    }
+    // compact the valid ops (order kept)
+    std::vector<uint32_t> vs;
+    std::vector<uint64_t> vo;
+    std::vector<uint8_t> vv;
+    std::vector<uint32_t> vidx;
+    for (uint32_t i = 0; i < n; i++)
+        if (ok[i]) {
+            vs.push_back(sid[i]);
+            vo.push_back(offsets[i]);
+            vv.push_back(values[i] & 1);
+            vidx.push_back(i);
+        }
+    uint64_t m = vs.size();
+    if (out_old) std::memset(out_old, 0, n);
+    if (!m) return status;
+    unsigned sid_bits = bits_for(c->strs.size() ? c->strs.size() - 1 : 0);
+    if (36 + sid_bits > 64) return fail(c, SK_EINVAL, "too many strings");
+    HIPCHK(c, c->in_ids.ensure(m * 4));
+    HIPCHK(c, c->in_off.ensure(m * 8));
+    HIPCHK(c, c->in_bytes.ensure(m));
+    HIPCHK(c, c->out_u8.ensure(m));
+    HIPCHK(c, c->keys_a.ensure(m * 8));
+    HIPCHK(c, c->keys_b.ensure(m * 8));
+    HIPCHK(c, c->vals_a.ensure(m * 4));
+    HIPCHK(c, c->vals_b.ensure(m * 4));
+    size_t tmp;
+    HIPCHK(c, sk::sort_pairs_size(m, 0, 36 + sid_bits, &tmp));
+    HIPCHK(c, c->sort_tmp.ensure(tmp));
+    HIPCHK(c, hipMemcpyAsync(c->in_ids.p, vs.data(), m * 4, hipMemcpyHostToDevice, c->st));
+    HIPCHK(c, hipMemcpyAsync(c->in_off.p, vo.data(), m * 8, hipMemcpyHostToDevice, c->st));
+    HIPCHK(c, hipMemcpyAsync(c->in_bytes.p, vv.data(), m, hipMemcpyHostToDevice, c->st));
+    HIPCHK(c, sk::launch_setbit_keys(c->st, m, c->in_ids.as<uint32_t>(), c->in_off.as<uint64_t>(),
+                                     c->keys_a.as<uint64_t>(), c->vals_a.as<uint32_t>()));
+    HIPCHK(c, sk::sort_pairs(c->st, c->sort_tmp.p, c->sort_tmp.cap, c->keys_a.as<uint64_t>(), c->keys_b.as<uint64_t>(),
+                             c->vals_a.as<uint32_t>(), c->vals_b.as<uint32_t>(), m, 0, 36 + sid_bits));
+    HIPCHK(c, sk::launch_setbit_apply(c->st, m, c->keys_b.as<uint64_t>(), c->vals_b.as<uint32_t>(),
+                                      c->in_bytes.as<uint8_t>(), 0, c->d_dir, c->out_u8.as<uint8_t>()));
+    std::vector<uint8_t> old(m);
+    HIPCHK(c, hipMemcpyAsync(old.data(), c->out_u8.p, m, hipMemcpyDeviceToHost, c->st));
+    int r = sync(c);
+    if (r) return r;
+    if (out_old)
+        for (uint64_t j = 0; j < m; j++) out_old[vidx[j]] = old[j];
+    return status;
+}
+
+int sk_getbit(sk_ctx *c, uint32_t n, const uint64_t *key_off, const uint8_t *key_bytes, const uint64_t *offsets,
+              uint8_t *out) {
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(c, hipSetDevice(c->device));
+    if (!n) return SK_OK;
+    std::vector<uint8_t> ok;
+    int status = check_offsets(c, n, offsets, ok);
+    std::vector<uint32_t> sid(n);
+    for (uint32_t i = 0; i < n; i++) {
+        sid[i] = kNoId;
+        if (!ok[i]) continue;
+        int r = str_get(c, key_at(key_off, key_bytes, i), false, 0, &sid[i]);
+        if (r == SK_EWRONGTYPE) {
+            sid[i] = kNoId;
+            status = r;
+            continue;
+        }
+        if (r) return r;
+    }
+    HIPCHK(c, c->in_ids.ensure(n * 4));
+    HIPCHK(c, c->in_off.ensure(n * 8));
+    HIPCHK(c, c->out_u8.ensure(n));
+    HIPCHK(c, hipMemcpyAsync(c->in_ids.p, sid.data(), n * 4, hipMemcpyHostToDevice, c->st));
+    HIPCHK(c, hipMemcpyAsync(c->in_off.p, offsets, n * 8ull, hipMemcpyHostToDevice, c->st));
+    HIPCHK(c, sk::launch_getbit_multi(c->st, n, c->in_ids.as<uint32_t>(), c->in_off.as<uint64_t>(), c->d_dir,
+                                      c->out_u8.as<uint8_t>()));
+    HIPCHK(c, hipMemcpyAsync(out, c->out_u8.p, n, hipMemcpyDeviceToHost, c->st));
+    int r = sync(c);
+    return r ? r : status;
+}
+
+// validate a device offset array: max offset -> host (one small readback)
+static int dev_max_offset(sk_ctx *c, uint64_t n, const uint64_t *d_offsets, uint64_t *mx) {
+    HIPCHK(c, sk::launch_max_u64(c->st, n, d_offsets, c->misc.as<uint64_t>()));
+    HIPCHK(c, hipMemcpyAsync(mx, c->misc.p, 8, hipMemcpyDeviceToHost, c->st));
+    return sync(c);
+}
+
+int sk_setbit_dev(sk_ctx *c, const uint8_t *key, uint64_t len, uint64_t n, const uint64_t *d_offsets, uint8_t value,
+                  uint8_t *d_out_old) {
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(c, hipSetDevice(c->device));
+    if (!n) return SK_OK;
+    uint64_t mx;
+    int r = dev_max_offset(c, n, d_offsets, &mx);
+    if (r) return r;
+    if (mx >= c->max_bit_offset) return fail(c, SK_ERANGE, "%s", kRange);
+    uint32_t id;
+    if ((r = str_get(c, key_of(key, len), true, (mx >> 3) + 1, &id))) return r;
+    uint64_t need = (mx >> 3) + 1, cur;
+    if ((r = str_reserve(c, id, need))) return r;
+    if ((r = str_len(c, id, &cur))) return r;
+    if (need > cur && (r = str_set_len(c, id, need))) return r;
+    if (!d_out_old) {
+        HIPCHK(c, sk::launch_setbit_void(c->st, n, d_offsets, c->strs[id].ptr, value & 1));
+        return sync(c);
+    }
+    size_t tmp;
+    HIPCHK(c, sk::sort_pairs_size(n, 0, 36, &tmp));
+    HIPCHK(c, c->sort_tmp.ensure(tmp));
+    HIPCHK(c, c->keys_a.ensure(n * 8));
+    HIPCHK(c, c->keys_b.ensure(n * 8));
+    HIPCHK(c, c->vals_a.ensure(n * 4));
+    HIPCHK(c, c->vals_b.ensure(n * 4));
+    // single key: string id bits are zero in the sort key, the apply kernel reads dir[0]
+    // through a one-entry directory view of this key
+    DirEnt one{c->strs[id].ptr, 0, c->strs[id].cap};
+    HIPCHK(c, c->ptrs.ensure(sizeof(DirEnt)));
+    HIPCHK(c, hipMemcpyAsync(c->ptrs.p, &one, sizeof one, hipMemcpyHostToDevice, c->st));
+    HIPCHK(c, sk::launch_setbit_keys(c->st, n, nullptr, d_offsets, c->keys_a.as<uint64_t>(), c->vals_a.as<uint32_t>()));
+    HIPCHK(c, sk::sort_pairs(c->st, c->sort_tmp.p, c->sort_tmp.cap, c->keys_a.as<uint64_t>(), c->keys_b.as<uint64_t>(),
+                             c->vals_a.as<uint32_t>(), c->vals_b.as<uint32_t>(), n, 0, 36));
+    HIPCHK(c, sk::launch_setbit_apply(c->st, n, c->keys_b.as<uint64_t>(), c->vals_b.as<uint32_t>(), nullptr,
+                                      value & 1, c->ptrs.p, d_out_old));
+    return sync(c);
+}
+
+int sk_getbit_dev(sk_ctx *c, const uint8_t *key, uint64_t len, uint64_t n, const uint64_t *d_offsets,
+                  uint8_t *d_out) {
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(c, hipSetDevice(c->device));
+    if (!n) return SK_OK;
+    uint64_t mx;
+    int r = dev_max_offset(c, n, d_offsets, &mx);
+    if (r) return r;
+    if (mx >= c->max_bit_offset) return fail(c, SK_ERANGE, "%s", kRange);
+    uint32_t id;
+    if ((r = str_get(c, key_of(key, len), false, 0, &id))) return r;
+    if (id == kNoId) {
+        HIPCHK(c, hipMemsetAsync(d_out, 0, n, c->st));
+        return sync(c);
+    }
+    HIPCHK(c, sk::launch_getbit_single(c->st, n, d_offsets, c->strs[id].ptr, &c->d_dir[id].len, d_out));
+    return sync(c);
+}
+
+int sk_bitcount(sk_ctx *c, const uint8_t *key, uint64_t len, uint64_t *out) {
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(c, hipSetDevice(c->device));
+    uint32_t id;
+    int r = str_get(c, key_of(key, len), false, 0, &id);
+    if (r) return r;
+    *out = 0;
+    if (id == kNoId) return SK_OK;
+    uint64_t l;
+    if ((r = str_len(c, id, &l))) return r;
+    HIPCHK(c, sk::launch_bitcount(c->st, c->strs[id].ptr, l, c->misc.as<uint64_t>()));
+    HIPCHK(c, hipMemcpyAsync(out, c->misc.p, 8, hipMemcpyDeviceToHost, c->st));
+    return sync(c);
+}
+
+int sk_strlen(sk_ctx *c, const uint8_t *key, uint64_t len, uint64_t *out) {
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(c, hipSetDevice(c->device));
+    auto it = c->keys.find(key_of(key, len));
+    *out = 0;
+    if (it == c->keys.end()) return SK_OK;
+    if (it->second.type == SK_TYPE_HLL) { // STRLEN of a dense HLL string
+        *out = SK_HLL_DENSE_SIZE;
+        return SK_OK;
+    }
+    return str_len(c, it->second.id, out);
+}
+
+int sk_bitop(sk_ctx *c, int op, const uint8_t *dest, uint64_t dest_len, uint32_t n_src, const uint64_t *src_off,
+             const uint8_t *src_bytes, uint64_t *out_len) {
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(c, hipSetDevice(c->device));
+    if (op < 0 || op > 3) return fail(c, SK_EINVAL, "ERR syntax error");
+    if (op == SK_BITOP_NOT && n_src != 1)
+        return fail(c, SK_ESYNTAX, "ERR BITOP NOT must be called with a single source key.");
+    if (n_src == 0) return fail(c, SK_EINVAL, "ERR wrong number of arguments for 'bitop' command");
+    std::vector<const uint8_t *> ptrs(n_src);
+    std::vector<uint64_t> lens(n_src);
+    std::string dkey = key_of(dest, dest_len);
+    uint32_t did = kNoId;
+    {
+        auto it = c->keys.find(dkey);
+        if (it != c->keys.end() && it->second.type == SK_TYPE_STRING) did = it->second.id;
+    }
+    bool dest_is_src = false;
+    uint64_t maxlen = 0;
+    for (uint32_t i = 0; i < n_src; i++) {
+        uint32_t id;
+        int r = str_get(c, key_at(src_off, src_bytes, i), false, 0, &id);
+        if (r) return r;
+        if (id == kNoId) {
+            ptrs[i] = c->strs.empty() ? nullptr : nullptr;
+            lens[i] = 0;
+            continue;
+        }
+        if (id == did) dest_is_src = true;
+        ptrs[i] = c->strs[id].ptr;
+        if ((r = str_len(c, id, &lens[i]))) return r;
+        maxlen = std::max(maxlen, lens[i]);
+    }
+    *out_len = maxlen;
+    if (maxlen == 0) { // empty result deletes the destination
+        bool removed;
+        int r = del_key(c, dkey, &removed);
+        return r ? r : sync(c);
+    }
+    for (uint32_t i = 0; i < n_src; i++)
+        if (!ptrs[i]) ptrs[i] = reinterpret_cast<const uint8_t *>(c->d_zero); // len 0: never read
+    // destination buffer: in place when dest is a source with room, else fresh
+    uint8_t *dst;
+    uint8_t *old_buf = nullptr;
+    int r;
+    if (did != kNoId && dest_is_src && c->strs[did].cap >= maxlen) {
+        dst = c->strs[did].ptr;
+    } else {
+        if (hipMalloc(&dst, round16(maxlen)) != hipSuccess) return fail(c, SK_ENOMEM, "cannot allocate BITOP result");
+        HIPCHK(c, hipMemsetAsync(dst, 0, round16(maxlen), c->st));
+    }
+    HIPCHK(c, c->ptrs.ensure(n_src * 16));
+    std::vector<uint8_t> blob(n_src * 16);
+    std::memcpy(blob.data(), ptrs.data(), n_src * 8);
+    std::memcpy(blob.data() + n_src * 8, lens.data(), n_src * 8);
+    HIPCHK(c, hipMemcpyAsync(c->ptrs.p, blob.data(), blob.size(), hipMemcpyHostToDevice, c->st));
+    HIPCHK(c, sk::launch_bitop(c->st, op, n_src, reinterpret_cast<const uint8_t *const *>(c->ptrs.p),
+                               reinterpret_cast<const uint64_t *>(c->ptrs.as<uint8_t>() + n_src * 8), maxlen, dst));
+    if ((r = sync(c))) return r;
+    if (did == kNoId) { // create / replace the destination (BITOP overwrites any type)
+        bool removed;
+        if ((r = del_key(c, dkey, &removed))) return r;
+        uint32_t nid;
+        if ((r = str_alloc(c, 16, &nid))) return r;
+        HIPCHK(c, hipFree(c->strs[nid].ptr));
+        c->strs[nid].ptr = dst;
+        c->strs[nid].cap = round16(maxlen);
+        c->keys[dkey] = KeyEnt{SK_TYPE_STRING, nid};
+        did = nid;
+    } else if (dst != c->strs[did].ptr) {
+        old_buf = c->strs[did].ptr;
+        c->strs[did].ptr = dst;
+        c->strs[did].cap = round16(maxlen);
+    }
+    DirEnt w{c->strs[did].ptr, maxlen, c->strs[did].cap};
+    if ((r = dir_write(c, did, w))) return r;
+    if ((r = sync(c))) return r;
+    if (old_buf) HIPCHK(c, hipFree(old_buf));
+    return SK_OK;
+}
+
+int sk_get(sk_ctx *c, const uint8_t *key, uint64_t len, uint8_t *buf, uint64_t cap, int64_t *out_len) {
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(c, hipSetDevice(c->device));
+    auto it = c->keys.find(key_of(key, len));
+    if (it == c->keys.end()) {
+        *out_len = -1;
+        return SK_OK;
+    }
+    if (it->second.type == SK_TYPE_HLL) {
+        std::vector<uint8_t> regs(kHllBytes);
+        HIPCHK(c, hipMemcpyAsync(regs.data(), c->arena + uint64_t(it->second.id) * kHllBytes, kHllBytes,
+                                 hipMemcpyDeviceToHost, c->st));
+        int r = sync(c);
+        if (r) return r;
+        std::vector<uint8_t> s(SK_HLL_DENSE_SIZE, 0);
+        std::memcpy(s.data(), "HYLL", 4); // encoding 0 = dense; card cache marked invalid
+        s[15] = 0x80;
+        for (int i = 0; i < 16384; i++) { // HLL_DENSE_SET_REGISTER: 6 bits at bit 6*i, LSB first
+            unsigned byte = unsigned(i * 6) / 8, fb = unsigned(i * 6) & 7, v = regs[i] & 63;
+            s[16 + byte] |= uint8_t(v << fb);
+            if (fb > 2) s[16 + byte + 1] |= uint8_t(v >> (8 - fb));
+        }
+        *out_len = int64_t(s.size());
+        std::memcpy(buf, s.data(), std::min<uint64_t>(cap, s.size()));
+        return SK_OK;
+    }
+    uint64_t l;
+    int r = str_len(c, it->second.id, &l);
+    if (r) return r;
+    *out_len = int64_t(l);
+    uint64_t ncopy = std::min(cap, l);
+    if (ncopy) HIPCHK(c, hipMemcpyAsync(buf, c->strs[it->second.id].ptr, ncopy, hipMemcpyDeviceToHost, c->st));
+    return sync(c);
+}
+
+int sk_set(sk_ctx *c, const uint8_t *key, uint64_t len, const uint8_t *val, uint64_t val_len) {
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(c, hipSetDevice(c->device));
+    std::string k = key_of(key, len);
+    bool removed;
+    int r = del_key(c, k, &removed); // SET overwrites whatever was there
+    if (r) return r;
+    uint32_t id;
+    if ((r = str_get(c, k, true, val_len, &id))) return r;
+    if (val_len) HIPCHK(c, hipMemcpyAsync(c->strs[id].ptr, val, val_len, hipMemcpyHostToDevice, c->st));
+    if ((r = sync(c))) return r;
+    return str_set_len(c, id, val_len);
+}
+
+int sk_bitset_length(sk_ctx *c, const uint8_t *key, uint64_t len, int64_t *out) {
+    // Lua of M:RedissonBitSet.java:180-192: fromBit = BITPOS key 1 -1 (first set
+    // bit of the LAST byte, -1 if none); toBit = 8*(fromBit/8+1) - fromBit%8
+    // (Lua float division, floored modulo); scan GETBIT toBit..fromBit downwards,
+    // first 1 -> i+1; else fromBit+1.  GETBIT -1 raises the offset error.
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(c, hipSetDevice(c->device));
+    uint32_t id;
+    int r = str_get(c, key_of(key, len), false, 0, &id);
+    if (r) return r;
+    uint64_t l = 0;
+    uint8_t last = 0, first = 0;
+    if (id != kNoId) {
+        if ((r = str_len(c, id, &l))) return r;
+        if (l) {
+            HIPCHK(c, hipMemcpyAsync(&last, c->strs[id].ptr + l - 1, 1, hipMemcpyDeviceToHost, c->st));
+            HIPCHK(c, hipMemcpyAsync(&first, c->strs[id].ptr, 1, hipMemcpyDeviceToHost, c->st));
+            if ((r = sync(c))) return r;
+        }
+    }
+    if (l == 0 || last == 0) {
+        // fromBit = -1 -> toBit = 0: GETBIT 0, then GETBIT -1 -> error
+        if (l && (first & 0x80)) {
+            *out = 1;
+            return SK_OK;
+        }
+        return fail(c, SK_ERANGE, "ERR Error running script: %s", kRange);
+    }
+    int ctz = __builtin_ctz(unsigned(last));
+    *out = int64_t(8 * (l - 1) + (8 - ctz));
+    return SK_OK;
+}
+
+int sk_gen_jackson_longs(uint64_t seed, uint64_t n, uint64_t *off, uint8_t *bytes) {
+    static const char pre[] = "[\"java.lang.Long\",";
+    const uint64_t plen = sizeof(pre) - 1;
+    uint64_t st = seed, t = 0;
+    for (uint64_t i = 0; i < n; i++) {
+        uint64_t z = (st += 0x9E3779B97F4A7C15ull);
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        z ^= z >> 31;
+        char num[24];
+        int nl = snprintf(num, sizeof num, "%lld", (long long)(int64_t)z);
+        off[i] = t;
+        if (bytes) {
+            std::memcpy(bytes + t, pre, plen);
+            std::memcpy(bytes + t + plen, num, size_t(nl));
+            bytes[t + plen + nl] = ']';
+        }
+        t += plen + uint64_t(nl) + 1;
+    }
+    off[n] = t;
+    return SK_OK;
+}
+
+// ================================================================== Bloom
+int sk_bloom_try_init(sk_ctx *c, const uint8_t *name, uint64_t len, int64_t expected, double fpp, int *out_ok) {
+    std::lock_guard<std::mutex> g(c->mu);
+    int64_t m = sk_bloom_optimal_bits(expected, fpp);
+    if (m > kBloomMaxSize)
+        return fail(c, SK_ETOOBIG, "Bloom filter can't be greater than %lld. But calculated size is %lld",
+                    (long long)kBloomMaxSize, (long long)m);
+    int32_t k = sk_bloom_optimal_k(expected, m);
+    std::string cfg = "{" + key_of(name, len) + "}__config";
+    if (c->bloom.count(cfg)) { // the Lua assert fails -> tryInit returns false
+        *out_ok = 0;
+        return SK_OK;
+    }
+    c->bloom[cfg] = BloomCfg{m, k, expected, fpp};
+    *out_ok = 1;
+    return SK_OK;
+}
+
+int sk_bloom_config(sk_ctx *c, const uint8_t *name, uint64_t len, int64_t *size, int32_t *k, int64_t *expected,
+                    double *fpp) {
+    std::lock_guard<std::mutex> g(c->mu);
+    BloomCfg *b;
+    int r = bloom_cfg(c, key_of(name, len), &b);
+    if (r) return r;
+    if (size) *size = b->size;
+    if (k) *k = b->k;
+    if (expected) *expected = b->expected;
+    if (fpp) *fpp = b->fpp;
+    return SK_OK;
+}
+
+// shared by the host and device Bloom paths; inputs already on device
+static int bloom_add_device(sk_ctx *c, uint32_t id, int64_t size, int32_t k, uint64_t n, const uint64_t *d_off,
+                            const uint8_t *d_bytes, uint8_t *d_out) {
+    if (!n) return SK_OK;
+    HIPCHK(c, hipMemsetAsync(d_out, 0, n, c->st));
+    uint64_t per = std::max<uint64_t>(1, std::min<uint64_t>(c->max_batch / uint64_t(k), 0xffffffffull / uint64_t(k)));
+    unsigned idx_bits = bits_for(uint64_t(size - 1));
+    uint64_t magic = magic_for(uint64_t(size));
+    for (uint64_t s = 0; s < n; s += per) {
+        uint64_t e = std::min(per, n - s), m = e * uint64_t(k);
+        HIPCHK(c, c->keys_a.ensure(m * 8));
+        HIPCHK(c, c->keys_b.ensure(m * 8));
+        size_t tmp;
+        HIPCHK(c, sk::sort_keys_size(m, 32, 32 + idx_bits, &tmp));
+        HIPCHK(c, c->sort_tmp.ensure(tmp));
+        HIPCHK(c, sk::launch_bloom_probes(c->st, e, d_off + s, d_bytes, uint64_t(size), magic, k,
+                                          c->keys_a.as<uint64_t>()));
+        HIPCHK(c, sk::sort_keys(c->st, c->sort_tmp.p, c->sort_tmp.cap, c->keys_a.as<uint64_t>(),
+                                c->keys_b.as<uint64_t>(), m, 32, 32 + idx_bits));
+        HIPCHK(c, sk::launch_bloom_apply(c->st, m, c->keys_b.as<uint64_t>(), c->strs[id].ptr, &c->d_dir[id].len, k,
+                                         d_out + s));
+    }
+    return SK_OK;
+}
+
+static int bloom_prepare(sk_ctx *c, const std::string &nm, int64_t size, int32_t k, bool create, uint32_t *id) {
+    BloomCfg *b;
+    int r = bloom_cfg(c, nm, &b);
+    if (r) return r;
+    if (b->size != size || b->k != k) return fail(c, SK_ECONFIG, "%s", kCfgChanged); // addConfigCheck
+    if (size <= 0 || k <= 0) return fail(c, SK_EINVAL, "bad Bloom filter config");
+    if ((r = str_get(c, nm, create, round16(uint64_t((size + 7) / 8)), id))) return r;
+    if (*id != kNoId && (r = str_reserve(c, *id, uint64_t((size + 7) / 8)))) return r;
+    return SK_OK;
+}
+
+static int stage_elems(sk_ctx *c, uint32_t n, const uint64_t *off, const uint8_t *bytes) {
+    uint64_t tot = off[n] - off[0];
+    std::vector<uint64_t> o(n + 1);
+    for (uint32_t i = 0; i <= n; i++) o[i] = off[i] - off[0];
+    HIPCHK(c, c->in_off.ensure((n + 1) * 8ull));
+    HIPCHK(c, c->in_bytes.ensure(tot + 16));
+    HIPCHK(c, hipMemcpyAsync(c->in_off.p, o.data(), (n + 1) * 8ull, hipMemcpyHostToDevice, c->st));
+    if (tot) HIPCHK(c, hipMemcpyAsync(c->in_bytes.p, bytes + off[0], tot, hipMemcpyHostToDevice, c->st));
+    HIPCHK(c, hipMemsetAsync(c->in_bytes.as<uint8_t>() + tot, 0, 16, c->st));
+    return sync(c); // o is a host vector
+}
+
+int sk_bloom_add(sk_ctx *c, const uint8_t *name, uint64_t len, int64_t size, int32_t k, uint32_t n,
+                 const uint64_t *off, const uint8_t *bytes, uint8_t *out) {
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(c, hipSetDevice(c->device));
+    uint32_t id;
+    int r = bloom_prepare(c, key_of(name, len), size, k, true, &id);
+    if (r || !n) return r;
+    if ((r = stage_elems(c, n, off, bytes))) return r;
+    HIPCHK(c, c->out_u8.ensure(n));
+    if ((r = bloom_add_device(c, id, size, k, n, c->in_off.as<uint64_t>(), c->in_bytes.as<uint8_t>(),
+                              c->out_u8.as<uint8_t>())))
+        return r;
+    HIPCHK(c, hipMemcpyAsync(out, c->out_u8.p, n, hipMemcpyDeviceToHost, c->st));
+    return sync(c);
+}
+
+int sk_bloom_contains(sk_ctx *c, const uint8_t *name, uint64_t len, int64_t size, int32_t k, uint32_t n,
+                      const uint64_t *off, const uint8_t *bytes, uint8_t *out) {
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(c, hipSetDevice(c->device));
+    uint32_t id;
+    int r = bloom_prepare(c, key_of(name, len), size, k, false, &id);
+    if (r || !n) return r;
+    if ((r = stage_elems(c, n, off, bytes))) return r;
+    HIPCHK(c, c->out_u8.ensure(n));
+    const uint8_t *bits = id == kNoId ? reinterpret_cast<const uint8_t *>(c->d_zero) : c->strs[id].ptr;
+    const uint64_t *dl = id == kNoId ? reinterpret_cast<const uint64_t *>(c->d_zero) : &c->d_dir[id].len;
+    HIPCHK(c, sk::launch_bloom_contains(c->st, n, c->in_off.as<uint64_t>(), c->in_bytes.as<uint8_t>(), bits, dl,
+                                        uint64_t(size), magic_for(uint64_t(size)), k, c->out_u8.as<uint8_t>()));
+    HIPCHK(c, hipMemcpyAsync(out, c->out_u8.p, n, hipMemcpyDeviceToHost, c->st));
+    return sync(c);
+}
+
+int sk_bloom_add_dev(sk_ctx *c, const uint8_t *name, uint64_t len, uint64_t n, const uint64_t *d_off,
+                     const uint8_t *d_bytes, uint64_t bytes_len, uint8_t *d_out) {
+    (void)bytes_len;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(c, hipSetDevice(c->device));
+    BloomCfg *b;
+    std::string nm = key_of(name, len);
+    int r = bloom_cfg(c, nm, &b);
+    if (r) return r;
+    uint32_t id;
+    if ((r = bloom_prepare(c, nm, b->size, b->k, true, &id))) return r;
+    if ((r = bloom_add_device(c, id, b->size, b->k, n, d_off, d_bytes, d_out))) return r;
+    return sync(c);
+}
+
+int sk_bloom_contains_dev(sk_ctx *c, const uint8_t *name, uint64_t len, uint64_t n, const uint64_t *d_off,
+                          const uint8_t *d_bytes, uint64_t bytes_len, uint8_t *d_out) {
+    (void)bytes_len;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(c, hipSetDevice(c->device));
+    BloomCfg *b;
+    std::string nm = key_of(name, len);
+    int r = bloom_cfg(c, nm, &b);
+    if (r) return r;
+    uint32_t id;
+    if ((r = bloom_prepare(c, nm, b->size, b->k, false, &id))) return r;
+    const uint8_t *bits = id == kNoId ? reinterpret_cast<const uint8_t *>(c->d_zero) : c->strs[id].ptr;
+    const uint64_t *dl = id == kNoId ? reinterpret_cast<const uint64_t *>(c->d_zero) : &c->d_dir[id].len;
+    HIPCHK(c, sk::launch_bloom_contains(c->st, n, d_off, d_bytes, bits, dl, uint64_t(b->size),
+                                        magic_for(uint64_t(b->size)), b->k, d_out));
+    return sync(c);
+}
+
+int sk_bloom_count(sk_ctx *c, const uint8_t *name, uint64_t len, int32_t *out) {
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(c, hipSetDevice(c->device));
+    BloomCfg *b;
+    std::string nm = key_of(name, len);
+    int r = bloom_cfg(c, nm, &b);
+    if (r) return r;
+    uint32_t id;
+    if ((r = str_get(c, nm, false, 0, &id))) return r;
+    uint64_t bc = 0;
+    if (id != kNoId) {
+        uint64_t l;
+        if ((r = str_len(c, id, &l))) return r;
+        HIPCHK(c, sk::launch_bitcount(c->st, c->strs[id].ptr, l, c->misc.as<uint64_t>()));
+        HIPCHK(c, hipMemcpyAsync(&bc, c->misc.p, 8, hipMemcpyDeviceToHost, c->st));
+        if ((r = sync(c))) return r;
+    }
+    // (int) (-size / ((double) hashIterations) * Math.log(1 - bitcount / ((double) size)))  :197
+    double v = double(-b->size) / double(b->k) * std::log(1 - double(bc) / double(b->size));
+    int32_t res;
+    if (v != v) res = 0;
+    else if (v >= 2147483647.0) res = 2147483647;
+    else if (v <= -2147483648.0) res = INT32_MIN;
+    else res = int32_t(v);
+    *out = res;
+    return SK_OK;
+}
+
+} // extern "C"

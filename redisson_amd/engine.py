@@ -1,0 +1,321 @@
+"""SketchEngine: one GPU-resident sketch store (one C-ABI context per device).
+
+Thin Python marshalling over libredisson_sketch.so: packs byte strings into
+(offsets u64[n+1], bytes) arrays, calls the C ABI, maps status codes to the
+exceptions Redisson raises (RedisException for server replies,
+IllegalStateException / IllegalArgumentException for the Bloom filter's
+client-side checks, M:RedissonBloomFilter.java:72-74,217,284).
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Iterable, List, Sequence
+
+import numpy as np
+
+from . import _native as N
+
+
+class RedisException(Exception):
+    """Error reply of a command (M:client/RedisException.java)."""
+
+
+class IllegalStateException(RuntimeError):
+    pass
+
+
+class IllegalArgumentException(ValueError):
+    pass
+
+
+class DeviceUnavailable(RuntimeError):
+    pass
+
+
+def _addr(a) -> int:
+    if a is None:
+        return 0
+    if isinstance(a, np.ndarray):
+        return a.ctypes.data
+    if hasattr(a, "data_ptr"):  # torch tensor (device pointer)
+        return a.data_ptr()
+    return int(a)
+
+
+def pack(items: Sequence[bytes]):
+    """(off u64[n+1], bytes u8[total+16]) with 16 B zero padding."""
+    n = len(items)
+    off = np.zeros(n + 1, dtype=np.uint64)
+    if n:
+        lens = np.fromiter((len(x) for x in items), dtype=np.uint64, count=n)
+        np.cumsum(lens, out=off[1:])
+    blob = b"".join(items)
+    buf = np.zeros(len(blob) + 16, dtype=np.uint8)
+    if blob:
+        buf[: len(blob)] = np.frombuffer(blob, dtype=np.uint8)
+    return off, buf
+
+
+def _b(x) -> bytes:
+    return x.encode("utf-8") if isinstance(x, str) else bytes(x)
+
+
+class SketchEngine:
+    def __init__(self, device: int = 0, redis_major: int = 3, max_bit_offset: int = 0,
+                 hll_capacity: int = 0, max_batch: int = 0):
+        self.lib = N.load()
+        cfg = N.SkConfig(device, redis_major, max_bit_offset, hll_capacity, max_batch)
+        h = ctypes.c_void_p()
+        st = self.lib.sk_open(ctypes.byref(cfg), ctypes.byref(h))
+        if st != N.SK_OK:
+            raise DeviceUnavailable(f"sk_open(device={device}) failed with status {st}: no usable HIP device")
+        self.ctx = h.value
+        self.device = device
+        self.redis_major = redis_major
+
+    # ------------------------------------------------------------ plumbing
+    def close(self):
+        if self.ctx:
+            self.lib.sk_close(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, st: int):
+        if st == N.SK_OK:
+            return
+        msg = (self.lib.sk_last_error(self.ctx) or b"").decode("utf-8", "replace")
+        if st == N.SK_ENOTINIT:
+            raise IllegalStateException(msg)
+        if st == N.SK_ETOOBIG:
+            raise IllegalArgumentException(msg)
+        raise RedisException(msg or self.lib.sk_strerror(st).decode())
+
+    @property
+    def stream(self) -> int:
+        return self.lib.sk_stream(self.ctx)
+
+    def sync(self):
+        self._check(self.lib.sk_sync(self.ctx))
+
+    # ------------------------------------------------------------ keys
+    def key_type(self, key) -> int:
+        k = _b(key)
+        t = ctypes.c_int()
+        self._check(self.lib.sk_type(self.ctx, k, len(k), ctypes.addressof(t)))
+        return t.value
+
+    def delete(self, keys: Iterable) -> int:
+        ks = [_b(k) for k in keys]
+        off, buf = pack(ks)
+        out = ctypes.c_uint64()
+        self._check(self.lib.sk_del(self.ctx, len(ks), _addr(off), _addr(buf), ctypes.addressof(out)))
+        return out.value
+
+    def hll_resolve(self, keys: Sequence) -> np.ndarray:
+        ks = [_b(k) for k in keys]
+        off, buf = pack(ks)
+        ids = np.zeros(len(ks), dtype=np.uint32)
+        self._check(self.lib.sk_hll_resolve(self.ctx, len(ks), _addr(off), _addr(buf), _addr(ids), None))
+        return ids
+
+    # ------------------------------------------------------------ HLL
+    def pfadd(self, keys: Sequence, elems: Sequence[Sequence[bytes]]) -> List[bool]:
+        """PFADD batch: command i = PFADD keys[i] *elems[i] (raw element bytes)."""
+        n = len(keys)
+        koff, kbuf = pack([_b(k) for k in keys])
+        counts = np.fromiter((len(e) for e in elems), dtype=np.uint32, count=n)
+        flat = [x for e in elems for x in e]
+        eoff, ebuf = pack(flat)
+        out = np.zeros(n, dtype=np.uint8)
+        self._check(self.lib.sk_pfadd(self.ctx, n, _addr(koff), _addr(kbuf), _addr(counts), _addr(eoff),
+                                      _addr(ebuf), _addr(out)))
+        return [bool(x) for x in out]
+
+    def pfadd_dev(self, n: int, d_key_ids, d_elem_off, d_elem_bytes, bytes_len: int, d_out):
+        self._check(self.lib.sk_pfadd_dev(self.ctx, n, _addr(d_key_ids), _addr(d_elem_off), _addr(d_elem_bytes),
+                                          bytes_len, _addr(d_out)))
+
+    def pfcount(self, cmds: Sequence[Sequence]) -> List[int]:
+        """PFCOUNT batch: command i counts the union of keys cmds[i]."""
+        nk = np.fromiter((len(c) for c in cmds), dtype=np.uint32, count=len(cmds))
+        koff, kbuf = pack([_b(k) for c in cmds for k in c])
+        out = np.zeros(len(cmds), dtype=np.int64)
+        self._check(self.lib.sk_pfcount(self.ctx, len(cmds), _addr(nk), _addr(koff), _addr(kbuf), _addr(out)))
+        return [int(x) for x in out]
+
+    def pfmerge(self, dest, srcs: Sequence):
+        d = _b(dest)
+        soff, sbuf = pack([_b(s) for s in srcs])
+        self._check(self.lib.sk_pfmerge(self.ctx, d, len(d), len(srcs), _addr(soff), _addr(sbuf)))
+
+    def hll_histogram_dev(self, n: int, d_ids, d_hist):
+        self._check(self.lib.sk_hll_histogram_dev(self.ctx, n, _addr(d_ids), _addr(d_hist)))
+
+    def hll_union_dev(self, n: int, d_ids, d_out):
+        self._check(self.lib.sk_hll_union_dev(self.ctx, n, _addr(d_ids), _addr(d_out)))
+
+    def hll_merge_registers_dev(self, key, d_regs):
+        k = _b(key)
+        self._check(self.lib.sk_hll_merge_registers_dev(self.ctx, k, len(k), _addr(d_regs)))
+
+    def hll_registers(self, key) -> np.ndarray:
+        k = _b(key)
+        out = np.zeros(16384, dtype=np.uint8)
+        self._check(self.lib.sk_hll_registers(self.ctx, k, len(k), _addr(out)))
+        return out
+
+    def estimate_hist(self, hist64) -> int:
+        h = np.ascontiguousarray(hist64, dtype=np.uint32)
+        return int(self.lib.sk_hll_estimate_hist(_addr(h), self.redis_major))
+
+    # ------------------------------------------------------------ bits
+    def setbit(self, keys: Sequence, offsets: Sequence[int], values: Sequence[int], want_old: bool = True):
+        n = len(keys)
+        koff, kbuf = pack([_b(k) for k in keys])
+        offs = np.asarray(offsets, dtype=np.uint64)
+        vals = np.asarray(values, dtype=np.uint8)
+        out = np.zeros(n, dtype=np.uint8) if want_old else None
+        self._check(self.lib.sk_setbit(self.ctx, n, _addr(koff), _addr(kbuf), _addr(offs), _addr(vals),
+                                       _addr(out)))
+        return [int(x) for x in out] if want_old else None
+
+    def getbit(self, keys: Sequence, offsets: Sequence[int]) -> List[int]:
+        n = len(keys)
+        koff, kbuf = pack([_b(k) for k in keys])
+        offs = np.asarray(offsets, dtype=np.uint64)
+        out = np.zeros(n, dtype=np.uint8)
+        self._check(self.lib.sk_getbit(self.ctx, n, _addr(koff), _addr(kbuf), _addr(offs), _addr(out)))
+        return [int(x) for x in out]
+
+    def setbit_dev(self, key, n: int, d_offsets, value: int, d_out_old=None):
+        k = _b(key)
+        self._check(self.lib.sk_setbit_dev(self.ctx, k, len(k), n, _addr(d_offsets), value, _addr(d_out_old)))
+
+    def getbit_dev(self, key, n: int, d_offsets, d_out):
+        k = _b(key)
+        self._check(self.lib.sk_getbit_dev(self.ctx, k, len(k), n, _addr(d_offsets), _addr(d_out)))
+
+    def bitcount(self, key) -> int:
+        k = _b(key)
+        out = ctypes.c_uint64()
+        self._check(self.lib.sk_bitcount(self.ctx, k, len(k), ctypes.addressof(out)))
+        return out.value
+
+    def strlen(self, key) -> int:
+        k = _b(key)
+        out = ctypes.c_uint64()
+        self._check(self.lib.sk_strlen(self.ctx, k, len(k), ctypes.addressof(out)))
+        return out.value
+
+    def bitop(self, op: str, dest, srcs: Sequence) -> int:
+        d = _b(dest)
+        soff, sbuf = pack([_b(s) for s in srcs])
+        out = ctypes.c_uint64()
+        self._check(self.lib.sk_bitop(self.ctx, N.SK_BITOP[op.upper()], d, len(d), len(srcs), _addr(soff),
+                                      _addr(sbuf), ctypes.addressof(out)))
+        return out.value
+
+    def get(self, key):
+        k = _b(key)
+        ln = ctypes.c_int64()
+        self._check(self.lib.sk_get(self.ctx, k, len(k), None, 0, ctypes.addressof(ln)))
+        if ln.value < 0:
+            return None
+        buf = np.zeros(max(ln.value, 1), dtype=np.uint8)
+        self._check(self.lib.sk_get(self.ctx, k, len(k), _addr(buf), ln.value, ctypes.addressof(ln)))
+        return buf[: ln.value].tobytes()
+
+    def set(self, key, value: bytes):
+        k = _b(key)
+        v = np.frombuffer(bytes(value) + b"\0", dtype=np.uint8)
+        self._check(self.lib.sk_set(self.ctx, k, len(k), _addr(v), len(value)))
+
+    def bitset_length(self, key) -> int:
+        k = _b(key)
+        out = ctypes.c_int64()
+        self._check(self.lib.sk_bitset_length(self.ctx, k, len(k), ctypes.addressof(out)))
+        return out.value
+
+    # ------------------------------------------------------------ Bloom
+    def bloom_try_init(self, name, expected: int, fpp: float) -> bool:
+        k = _b(name)
+        ok = ctypes.c_int()
+        self._check(self.lib.sk_bloom_try_init(self.ctx, k, len(k), expected, fpp, ctypes.addressof(ok)))
+        return bool(ok.value)
+
+    def bloom_config(self, name):
+        k = _b(name)
+        size, kk, exp, fpp = ctypes.c_int64(), ctypes.c_int32(), ctypes.c_int64(), ctypes.c_double()
+        self._check(self.lib.sk_bloom_config(self.ctx, k, len(k), ctypes.addressof(size), ctypes.addressof(kk),
+                                             ctypes.addressof(exp), ctypes.addressof(fpp)))
+        return size.value, kk.value, exp.value, fpp.value
+
+    def bloom_add(self, name, size: int, k: int, elems: Sequence[bytes]) -> List[bool]:
+        nm = _b(name)
+        off, buf = pack(list(elems))
+        out = np.zeros(len(elems), dtype=np.uint8)
+        self._check(self.lib.sk_bloom_add(self.ctx, nm, len(nm), size, k, len(elems), _addr(off), _addr(buf),
+                                          _addr(out)))
+        return [bool(x) for x in out]
+
+    def bloom_contains(self, name, size: int, k: int, elems: Sequence[bytes]) -> List[bool]:
+        nm = _b(name)
+        off, buf = pack(list(elems))
+        out = np.zeros(len(elems), dtype=np.uint8)
+        self._check(self.lib.sk_bloom_contains(self.ctx, nm, len(nm), size, k, len(elems), _addr(off),
+                                               _addr(buf), _addr(out)))
+        return [bool(x) for x in out]
+
+    def bloom_add_dev(self, name, n: int, d_off, d_bytes, bytes_len: int, d_out):
+        nm = _b(name)
+        self._check(self.lib.sk_bloom_add_dev(self.ctx, nm, len(nm), n, _addr(d_off), _addr(d_bytes), bytes_len,
+                                              _addr(d_out)))
+
+    def bloom_contains_dev(self, name, n: int, d_off, d_bytes, bytes_len: int, d_out):
+        nm = _b(name)
+        self._check(self.lib.sk_bloom_contains_dev(self.ctx, nm, len(nm), n, _addr(d_off), _addr(d_bytes),
+                                                   bytes_len, _addr(d_out)))
+
+    def bloom_count(self, name) -> int:
+        nm = _b(name)
+        out = ctypes.c_int32()
+        self._check(self.lib.sk_bloom_count(self.ctx, nm, len(nm), ctypes.addressof(out)))
+        return out.value
+
+
+# ---------------------------------------------------------------- host-only
+def calc_slot(key) -> int:
+    k = _b(key)
+    return int(N.load().sk_calc_slot(k, len(k)))
+
+
+def crc16(data: bytes) -> int:
+    return int(N.load().sk_crc16(bytes(data), len(data)))
+
+
+def owner(key, n_gpus: int) -> int:
+    k = _b(key)
+    return int(N.load().sk_owner(k, len(k), n_gpus))
+
+
+def bloom_optimal_bits(n: int, p: float) -> int:
+    return int(N.load().sk_bloom_optimal_bits(n, p))
+
+
+def bloom_optimal_k(n: int, m: int) -> int:
+    return int(N.load().sk_bloom_optimal_k(n, m))
+
+
+def gen_jackson_longs(seed: int, n: int):
+    """(off u64[n+1], bytes u8[total+16]) of ["java.lang.Long",v] for SplitMix64(seed)."""
+    lib = N.load()
+    off = np.zeros(n + 1, dtype=np.uint64)
+    lib.sk_gen_jackson_longs(seed, n, off.ctypes.data, None)
+    buf = np.zeros(int(off[n]) + 16, dtype=np.uint8)
+    lib.sk_gen_jackson_longs(seed, n, off.ctypes.data, buf.ctypes.data)
+    return off, buf

@@ -1,0 +1,239 @@
+"""GPU parity: HIP path (through the C ABI) vs the CPU oracle, bit-exact.
+
+Seeded inputs at sizes the oracle finishes in seconds; edge cases the
+reference path has (empty / ragged / long elements, intra-batch register and
+bit collisions, missing keys, maximum offsets)."""
+import numpy as np
+import pytest
+
+from redisson_amd import RedisException, gen_jackson_longs
+
+pytestmark = pytest.mark.gpu
+
+
+def _elems(seed, n):
+    off, buf = gen_jackson_longs(seed, n)
+    return [buf[off[i]:off[i + 1]].tobytes() for i in range(n)]
+
+
+def _ragged(rng, n, maxlen=200):
+    lens = rng.integers(0, maxlen, n)
+    return [rng.integers(0, 256, l, dtype=np.uint8).tobytes() for l in lens]
+
+
+# ------------------------------------------------------------------- PFADD
+@pytest.mark.parametrize("nkeys,n", [(1, 5000), (7, 20000), (300, 30000)])
+def test_pfadd_registers_and_replies(engine, O, nkeys, n):
+    rng = np.random.default_rng(nkeys)
+    elems = _elems(0x5EED0000 + nkeys, n)
+    # duplicates -> replies 0, same-register collisions inside the batch
+    elems += [elems[i] for i in rng.integers(0, n, n // 5)]
+    keys = [b"pf:%d:%d" % (nkeys, rng.integers(0, nkeys)) for _ in elems]
+    got = engine.pfadd(keys, [[e] for e in elems])
+    ref = O.HLLStore()
+    want = ref.pfadd(keys, [[e] for e in elems])
+    assert got == want
+    for k in set(keys):
+        np.testing.assert_array_equal(engine.hll_registers(k), ref.regs[k])
+
+
+def test_pfadd_multi_element_and_ragged(engine, O):
+    rng = np.random.default_rng(7)
+    keys, elems = [], []
+    for c in range(400):
+        keys.append(b"rag:%d" % (c % 13))
+        elems.append(_ragged(rng, int(rng.integers(0, 6))))   # includes 0-element commands
+    got = engine.pfadd(keys, elems)
+    ref = O.HLLStore()
+    assert got == ref.pfadd(keys, elems)
+    for k in set(keys):
+        np.testing.assert_array_equal(engine.hll_registers(k), ref.regs[k])
+
+
+def test_pfadd_dense_single_key_sequential(engine, O):
+    # C1 shape, small: many elements into ONE key -> long same-register segments
+    elems = _elems(0x5EED0001, 60000)
+    keys = [b"c1"] * len(elems)
+    got = engine.pfadd(keys, [[e] for e in elems])
+    ref = O.HLLStore()
+    assert got == ref.pfadd(keys, [[e] for e in elems])
+    np.testing.assert_array_equal(engine.hll_registers(b"c1"), ref.regs[b"c1"])
+
+
+def test_pfcount_single_and_union(engine, O):
+    rng = np.random.default_rng(3)
+    ref = O.HLLStore()
+    keys = [b"cnt:%d" % i for i in range(20)]
+    for ci, k in enumerate(keys):
+        m = int(10 ** rng.uniform(0, 5))
+        es = _elems(1000 + ci, m)
+        engine.pfadd([k] * m, [[e] for e in es])
+        ref.pfadd([k] * m, [[e] for e in es])
+    cmds = [[k] for k in keys] + [keys[:3], keys, [b"missing"], [b"missing", keys[4]]]
+    assert engine.pfcount(cmds) == [ref.count(c) for c in cmds]
+
+
+def test_pfcount_register_ge_40_order_fallback(engine, O):
+    # craft an element whose rho >= 40 is astronomically rare; instead merge a
+    # raw register array with values >= 40 through the device merge entry
+    import torch
+    regs = np.zeros(16384, dtype=np.uint8)
+    rng = np.random.default_rng(11)
+    regs[:] = rng.integers(0, 12, 16384)
+    regs[[5, 77, 9000]] = [40, 45, 50]
+    d = torch.from_numpy(regs).cuda()
+    engine.hll_merge_registers_dev(b"big40", d)
+    np.testing.assert_array_equal(engine.hll_registers(b"big40"), regs)
+    assert engine.pfcount([[b"big40"]]) == [O.count_regs(regs, 1)]        # dense order
+    assert engine.pfcount([[b"big40", b"nokey2"]]) == [O.count_regs(regs, 2)]  # raw order
+
+
+def test_pfmerge(engine, O):
+    ref = O.HLLStore()
+    srcs = [b"m:%d" % i for i in range(6)]
+    for i, k in enumerate(srcs):
+        es = _elems(77 + i, 3000)
+        engine.pfadd([k] * len(es), [[e] for e in es])
+        ref.pfadd([k] * len(es), [[e] for e in es])
+    engine.pfadd([b"m:dest"], [[b"x"]])
+    ref.pfadd([b"m:dest"], [[b"x"]])
+    engine.pfmerge(b"m:dest", [b"m:dest"] + srcs + [b"m:absent"])
+    ref.merge(b"m:dest", [b"m:dest"] + srcs + [b"m:absent"])
+    np.testing.assert_array_equal(engine.hll_registers(b"m:dest"), ref.regs[b"m:dest"])
+    assert engine.pfcount([[b"m:dest"]]) == [ref.count([b"m:dest"])]
+
+
+def test_hll_wrongtype(engine):
+    engine.setbit([b"wt:str"], [3], [1])
+    with pytest.raises(RedisException, match="HyperLogLog"):
+        engine.pfadd([b"wt:str"], [[b"a"]])
+
+
+def test_pfadd_dev_path(engine, O):
+    import torch
+    n, nkeys = 50000, 37
+    off, buf = gen_jackson_longs(0x5EED0002, n)
+    rng = np.random.default_rng(5)
+    kid = rng.integers(0, nkeys, n).astype(np.uint32)
+    names = [b"dev:%d" % i for i in range(nkeys)]
+    ids = engine.hll_resolve(names)
+    d_ids = torch.from_numpy(ids[kid].astype(np.int32)).cuda()
+    d_off = torch.from_numpy(off.view(np.int64)).cuda()
+    d_buf = torch.from_numpy(buf).cuda()
+    d_out = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    engine.pfadd_dev(n, d_ids, d_off, d_buf, int(off[-1]), d_out)
+    regs, want = O.HLLStore().pfadd_bulk(kid, off, buf, nkeys)
+    assert np.array_equal(d_out.cpu().numpy(), want)
+    for i, nm in enumerate(names):
+        np.testing.assert_array_equal(engine.hll_registers(nm), regs[i])
+    # histogram + host estimator == oracle count
+    d_hist = torch.zeros(nkeys * 64, dtype=torch.int32, device="cuda")
+    engine.hll_histogram_dev(nkeys, torch.from_numpy(ids.astype(np.int32)).cuda(), d_hist)
+    h = d_hist.cpu().numpy().view(np.uint32).reshape(nkeys, 64)
+    for i in range(nkeys):
+        assert engine.estimate_hist(h[i]) == O.count_regs(regs[i], 1)
+
+
+# ------------------------------------------------------------------- Bloom
+@pytest.mark.parametrize("n_exp,p", [(100, 0.03), (20000, 0.01), (5000, 0.5)])
+def test_bloom_add_contains(engine, O, n_exp, p):
+    name = "bf:%d:%s" % (n_exp, p)
+    assert engine.bloom_try_init(name, n_exp, p)
+    size, k, _, _ = engine.bloom_config(name)
+    bits = O.BitString()
+    rng = np.random.default_rng(n_exp)
+    elems = _elems(n_exp, n_exp) + _ragged(rng, 300)           # includes >64 B (farmUo long path)
+    elems += [elems[i] for i in rng.integers(0, len(elems), 200)]  # in-batch duplicates
+    assert engine.bloom_add(name, size, k, elems) == bits.bloom_add(size, k, elems)
+    probe = elems[::3] + _elems(n_exp + 1, 3000)
+    assert engine.bloom_contains(name, size, k, probe) == bits.bloom_contains(size, k, probe)
+    assert engine.get(name) == bits.bytes()
+    assert engine.bitcount(name) == bits.bitcount()
+    assert engine.bloom_count(name) == O.bloom_count(size, k, bits.bitcount())
+
+
+def test_bloom_k1_and_config_errors(engine, O):
+    from redisson_amd import IllegalStateException
+    assert engine.bloom_try_init("bfk1", 10, 0.9)   # k == 1: add never true, contains always true
+    size, k, _, _ = engine.bloom_config("bfk1")
+    assert k == 1
+    bits = O.BitString()
+    els = [b"a", b"b", b"c"]
+    assert engine.bloom_contains("bfk1", size, k, els) == bits.bloom_contains(size, k, els) == [True] * 3
+    assert engine.bloom_add("bfk1", size, k, els) == bits.bloom_add(size, k, els)
+    with pytest.raises(RedisException, match="Bloom filter config has been changed"):
+        engine.bloom_add("bfk1", size + 1, k, els)
+    with pytest.raises(IllegalStateException):
+        engine.bloom_config("nobf")
+
+
+# ------------------------------------------------------------------- bits
+def test_setbit_getbit_sequential(engine, O):
+    rng = np.random.default_rng(9)
+    n = 20000
+    keys = [b"bs:%d" % rng.integers(0, 5) for _ in range(n)]
+    offs = rng.integers(0, 5000, n)
+    vals = rng.integers(0, 2, n)
+    got = engine.setbit(keys, offs, vals)
+    ref = {}
+    want = []
+    for k, o, v in zip(keys, offs, vals):
+        want.append(ref.setdefault(k, O.BitString()).setbit(int(o), int(v)))
+    assert got == want
+    for k, b in ref.items():
+        assert engine.get(k) == b.bytes()
+        assert engine.strlen(k) == len(b.bytes())
+        assert engine.bitcount(k) == b.bitcount()
+    q = rng.integers(0, 6000, 3000)
+    qk = [b"bs:%d" % rng.integers(0, 6) for _ in q]   # bs:5 missing -> 0
+    assert engine.getbit(qk, q) == [ref[k].getbit(int(o)) if k in ref else 0 for k, o in zip(qk, q)]
+
+
+def test_bit_offset_limits(engine):
+    top = 2 * 2147483647                       # RedissonBitSetTest.testIndexRange
+    assert engine.getbit([b"lim"], [top]) == [0]
+    engine.setbit([b"lim"], [top], [1])
+    assert engine.getbit([b"lim"], [top]) == [1]
+    with pytest.raises(RedisException, match="bit offset is not an integer or out of range"):
+        engine.setbit([b"lim"], [1 << 32], [1])
+
+
+def test_bitop(engine, O):
+    rng = np.random.default_rng(2)
+    data = {b"op:a": rng.integers(0, 256, 1000, dtype=np.uint8).tobytes(),
+            b"op:b": rng.integers(0, 256, 37, dtype=np.uint8).tobytes(),
+            b"op:c": rng.integers(0, 256, 4099, dtype=np.uint8).tobytes()}
+    for k, v in data.items():
+        engine.set(k, v)
+    for op in ["AND", "OR", "XOR"]:
+        srcs = [b"op:a", b"op:b", b"op:missing", b"op:c"]
+        n = engine.bitop(op, b"op:dst:" + op.encode(), srcs)
+        want = O.bitop(op, [data.get(s) for s in srcs])
+        assert n == len(want)
+        assert engine.get(b"op:dst:" + op.encode()) == want
+    engine.bitop("NOT", b"op:a", [b"op:a"])
+    assert engine.get(b"op:a") == O.bitop("NOT", [data[b"op:a"]])
+    with pytest.raises(RedisException, match="BITOP NOT"):
+        engine.bitop("NOT", b"x", [b"op:a", b"op:b"])
+    # empty result deletes the destination
+    assert engine.bitop("OR", b"op:c", [b"op:none1", b"op:none2"]) == 0
+    assert engine.get(b"op:c") is None
+
+
+def test_bulk_setbit_getbit_dev(engine):
+    import torch
+    rng = np.random.default_rng(4)
+    n = 1 << 16
+    offs = rng.integers(0, 1 << 24, n).astype(np.int64)
+    d = torch.from_numpy(offs).cuda()
+    engine.setbit_dev(b"bulk", n, d, 1)
+    out = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    engine.getbit_dev(b"bulk", n, d, out)
+    assert int(out.sum()) == n
+    assert engine.bitcount(b"bulk") == len(np.unique(offs))
+    # with replies: first occurrence sees 0, repeats see 1
+    offs2 = np.concatenate([offs[:100], offs[:100], rng.integers(1 << 24, 1 << 25, 100)]).astype(np.int64)
+    old = torch.zeros(len(offs2), dtype=torch.uint8, device="cuda")
+    engine.setbit_dev(b"bulk", len(offs2), torch.from_numpy(offs2).cuda(), 0, old)
+    o = old.cpu().numpy()
+    assert o[:100].all() and not o[100:200].any()

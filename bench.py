@@ -1,0 +1,237 @@
+#!/usr/bin/env python3
+"""bench.py -- HLL inserts/s + Bloom contains/s (whole node) on the MI355X sketch engine.
+
+One "step" = one RBatch-sized batch of PFADD (C2: 100k tenants, Jackson-encoded
+random Longs, one element per command, 1M commands) + one batch of Bloom
+contains (C3: tryInit(425,000,000, 0.008) -> m = 4,271,038,538 bits, k = 7,
+50 % members / 50 % fresh, 1M elements), both with inputs already resident in
+HBM.  value = (PFADD elements + contains elements) / wall time, all ranks.
+
+Multi-GPU (torch.distributed.run, one process per GPU): keys are partitioned by
+calcSlot(key) % world (the north-star partitioner), each rank owns its tenants
+and its own Bloom filter, no data-path collective -> "scaling": "weak".
+Rendezvous / barrier / max-over-ranks timing use torch.distributed's gloo (CPU)
+backend: the engine owns the GPU through the system HIP runtime, so this
+process never initialises torch's bundled HIP runtime.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from redisson_amd import SketchEngine, owner  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+PHASES = ["pfadd_hash", "pfadd_sort", "pfadd_apply", "bloom_contains"]
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def dist_setup():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    pg = None
+    if world > 1:
+        import torch.distributed as dist  # gloo only: CPU-side rendezvous / barrier / max
+
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        pg = dist
+    return world, rank, local, pg
+
+
+def barrier(pg):
+    if pg is not None:
+        pg.barrier()
+
+
+def allmax(pg, x: float) -> float:
+    if pg is None:
+        return x
+    import torch
+
+    t = torch.tensor([x], dtype=torch.float64)
+    pg.all_reduce(t, op=pg.ReduceOp.MAX)
+    return float(t.item())
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=1 << 20, help="commands per PFADD / contains batch")
+    ap.add_argument("--tenants", type=int, default=100_000)
+    ap.add_argument("--bloom-n", type=int, default=425_000_000)
+    ap.add_argument("--bloom-p", type=float, default=0.008)
+    ap.add_argument("--bloom-fill", type=int, default=-1, help="elements added before contains (default bloom-n)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample", type=int, default=2_000_000)
+    args = ap.parse_args()
+
+    world, rank, local, pg = dist_setup()
+    B, K, W = args.batch, args.steps, args.warmup
+    fill = args.bloom_n if args.bloom_fill < 0 else args.bloom_fill
+
+    # ------------------------------------------------------------ setup (untimed)
+    names = ["tenant:%d:hll" % t for t in range(args.tenants)]
+    mine = [nm for nm in names if owner(nm, world) == rank]
+    eng = SketchEngine(device=local, hll_capacity=len(mine) + 16, max_batch=max(8 * B, 1 << 22),
+                       max_bit_offset=1 << 34)
+    ids = eng.hll_resolve(mine)
+    rng = np.random.default_rng(0x5EED0002 + rank)
+
+    nsteps = W + K
+    seed_h = 0x5EED0002
+    base_h = rank << 40                      # disjoint element streams per rank
+    h_off, h_bytes, h_total = eng.gen_jackson_longs_dev(seed_h, nsteps * B, first=base_h)
+    kid = rng.integers(0, len(mine), nsteps * B)
+    d_ids = eng.to_device(ids[kid].astype(np.uint32))
+    d_changed = eng.alloc(B)
+    mean_len_h = h_total / (nsteps * B)
+
+    bloom = "bloom:c3:%d" % rank
+    eng.bloom_try_init(bloom, args.bloom_n, args.bloom_p)
+    size, k, _, _ = eng.bloom_config(bloom)
+    seed_b = 0x5EED0003
+    t0 = time.perf_counter()
+    chunk = 1 << 23
+    d_add_out = eng.alloc(chunk)
+    for s in range(0, fill, chunk):
+        n = min(chunk, fill - s)
+        a_off, a_bytes, a_tot = eng.gen_jackson_longs_dev(seed_b, n, first=(rank << 40) + s)
+        eng.bloom_add_dev(bloom, n, a_off, a_bytes, a_tot, d_add_out)
+        a_off.free()
+        a_bytes.free()
+    eng.sync()
+    add_s = time.perf_counter() - t0
+    # contains inputs: 50 % members, 50 % fresh
+    member = rng.integers(0, max(fill, 1), nsteps * B, dtype=np.uint64) + np.uint64(rank << 40)
+    fresh = rng.integers(1 << 39, 1 << 40, nsteps * B, dtype=np.uint64) + np.uint64(rank << 40)
+    pick = rng.random(nsteps * B) < 0.5
+    idx = np.where(pick, member, fresh)
+    d_idx = eng.to_device(idx)
+    c_off, c_bytes, c_total = eng.gen_jackson_longs_dev(seed_b, nsteps * B, d_idx=d_idx)
+    d_idx.free()
+    d_contains = eng.alloc(B)
+    mean_len_b = c_total / (nsteps * B)
+    log(f"[rank {rank}] setup: {len(mine)} tenants, bloom m={size} k={k} filled with {fill} in {add_s:.1f}s")
+
+    def step(s):
+        eng.pfadd_dev(B, d_ids.ptr + s * B * 4, h_off.ptr + s * B * 8, h_bytes, h_total, d_changed)
+        eng.bloom_contains_dev(bloom, B, c_off.ptr + s * B * 8, c_bytes, c_total, d_contains)
+
+    for s in range(W):
+        step(s)
+    eng.sync()
+
+    # ------------------------------------------------------------ timed region
+    eng.prof_reset()
+    eng.prof_enable(True)
+    barrier(pg)
+    eng.sync()
+    t0 = time.perf_counter()
+    eng.timer_record(0)
+    for s in range(W, W + K):
+        step(s)
+    eng.timer_record(1)
+    eng.sync()
+    t1 = time.perf_counter()
+    barrier(pg)
+    eng.prof_enable(False)
+    wall = allmax(pg, t1 - t0)
+    dev_ms = eng.timer_elapsed_ms(0, 1)
+    prof = {p: eng.prof_read(p) for p in PHASES}
+
+    units = 2 * B * K * world
+    value = units / wall
+    hll_ms = sum(prof[p][1] for p in PHASES[:3])
+    bl_ms = prof["bloom_contains"][1]
+    # roofline of the dominant kernel: algorithmic bytes per unit x units / avg launch time
+    dom = max(PHASES, key=lambda p: prof[p][1])
+    per_unit = {
+        "pfadd_hash": mean_len_h + 8 + 4 + 8,          # key bytes + offset + slab id in, sort key out
+        "pfadd_sort": 2 * 8 * 5,                       # 5 radix passes over 8-byte keys (read + write)
+        "pfadd_apply": 8 + 64 + 64 + 1,                # sorted key + register sector RMW + reply byte
+        "bloom_contains": mean_len_b + 8 + 1 + (k - 1) * 64,   # len + 9 + (k-1)*64 B
+    }[dom]
+    n_launch, tot_ms = prof[dom]
+    avg_ms = tot_ms / max(n_launch, 1)
+    achieved = per_unit * B / (avg_ms * 1e-3) / 1e9
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(eng, args, h_off, h_bytes, ids, kid, len(mine), c_off, c_bytes, bloom, size, k)
+
+    out = {
+        "metric": "HLL inserts/sec + Bloom contains/sec (whole node)",
+        "value": value,
+        "unit": "ops/s",
+        "n_gpus": world,
+        "steps": K,
+        "warmup": W,
+        "ms_per_step": wall / K * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8/u64",
+        "data": "synthetic: SplitMix64 Longs as Jackson bytes [\"java.lang.Long\",v] (mean %.1f B)" % mean_len_h,
+        "config": {
+            "workload": "C2 PFADD 1 elem/cmd over %d tenants + C3 Bloom contains (m=%d, k=%d, filled with %d, "
+                        "50%% members), %d commands per batch each" % (args.tenants, size, k, fill, B),
+            "batch": B, "tenants": args.tenants, "bloom_bits": size, "bloom_k": k, "bloom_fill": fill,
+            "partitioner": "calcSlot(key) %% %d" % world,
+        },
+        "hll_inserts_per_s": B * K * world / (hll_ms * 1e-3) if hll_ms else None,
+        "bloom_contains_per_s": B * K * world / (bl_ms * 1e-3) if bl_ms else None,
+        "bloom_add_per_s": fill / add_s if add_s else None,
+        "device_ms_timed_region": dev_ms,
+        "kernel_ms_per_launch": {p: (prof[p][1] / max(prof[p][0], 1)) for p in PHASES},
+        "roofline": {"kernel": dom, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "bytes_per_unit": per_unit, "units_per_launch": B, "avg_launch_ms": avg_ms},
+        "cpu_baseline": cpu,
+    }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    eng.close()
+
+
+def cpu_baseline(eng, args, h_off, h_bytes, ids, kid, n_keys, c_off, c_bytes, bloom, size, k):
+    """The oracle (CPU restatement, one core) on a bounded sample of the same workload."""
+    from oracle import oracle as O
+
+    S = args.cpu_sample
+    off = h_off.download(np.uint64, S + 1)
+    buf = h_bytes.download(np.uint8, int(off[S]) + 16)
+    t0 = time.perf_counter()
+    O.HLLStore().pfadd_bulk(kid[:S].astype(np.uint32), off, buf, n_keys)
+    th = time.perf_counter() - t0
+
+    bits = O.BitString(0)
+    full = eng.get(bloom) or b""
+    bits.buf = np.frombuffer(full + b"\0" * 16, dtype=np.uint8).copy()
+    bits.len.value = len(full)
+    coff = c_off.download(np.uint64, S + 1)
+    cbuf = c_bytes.download(np.uint8, int(coff[S]) + 16)
+    t0 = time.perf_counter()
+    bits.bloom_contains_raw(size, k, coff, cbuf)
+    tb = time.perf_counter() - t0
+    return {"value": 2 * S / (th + tb), "unit": "ops/s", "cores": 1, "kind": "port",
+            "sample": "%d PFADD (same tenants/elements) + %d Bloom contains on the same filled filter, "
+                      "oracle/sketch_oracle.c single-threaded" % (S, S),
+            "hll_inserts_per_s": S / th, "bloom_contains_per_s": S / tb}
+
+
+if __name__ == "__main__":
+    main()

@@ -17,7 +17,7 @@
  *     pointers (already resident in HBM on this context's GPU) and enqueue on
  *     the context's stream; they return after completion unless noted.
  *   - Variable-length byte strings are passed as (off u64[n+1], bytes u8[]):
- *     item i = bytes[off[i] .. off[i+1]).  Device byte buffers must have 8
+ *     item i = bytes[off[i] .. off[i+1]).  Device byte buffers must have 16
  *     readable bytes of padding after the last item.
  *   - Every function returns SK_OK (0) or a negative SK_E* status;
  *     sk_last_error() gives the Redis-compatible message (Java maps it to
@@ -178,11 +178,42 @@ int sk_bloom_contains_dev(sk_ctx *ctx, const uint8_t *name, uint64_t len, uint64
 /* count :188-199 */
 int sk_bloom_count(sk_ctx *ctx, const uint8_t *name, uint64_t len, int32_t *out);
 
+/* ---- device memory and timing on the context's device / stream ---- */
+int sk_dev_alloc(sk_ctx *ctx, uint64_t bytes, void **out);
+int sk_dev_free(sk_ctx *ctx, void *p);
+int sk_h2d(sk_ctx *ctx, void *d_dst, const void *src, uint64_t n);
+int sk_d2h(sk_ctx *ctx, void *dst, const void *d_src, uint64_t n);
+int sk_dev_memset(sk_ctx *ctx, void *d_p, int value, uint64_t n);
+/* HIP events on the context stream: 16 slots; elapsed(a, b) waits for b */
+int sk_timer_record(sk_ctx *ctx, int slot);
+int sk_timer_elapsed(sk_ctx *ctx, int slot_a, int slot_b, float *ms);
+/* per-kernel device time inside the library (event pairs around each launch
+ * of a phase): "pfadd_hash", "pfadd_sort", "pfadd_apply", "hll_hist",
+ * "hll_union", "bloom_contains", "bloom_probes", "bloom_sort", "bloom_apply",
+ * "setbit", "getbit", "bitcount", "bitop" */
+int sk_prof_enable(sk_ctx *ctx, int on);
+int sk_prof_reset(sk_ctx *ctx);
+int sk_prof_read(sk_ctx *ctx, const char *phase, uint64_t *launches, double *total_ms);
+
+/* ---- cross-GPU exchange: RCCL over xGMI (one context per GPU / process) ---- */
+int sk_comm_unique_id(uint8_t *out128);
+int sk_comm_init(sk_ctx *ctx, int nranks, int rank, const uint8_t *id128);
+/* register-wise max of n bytes in place (cross-GPU PFMERGE / countWith) */
+int sk_allreduce_max_u8(sk_ctx *ctx, uint8_t *d_buf, uint64_t n);
+/* sum of n u64 in place (BITCOUNT of a range-sharded bitset) */
+int sk_allreduce_sum_u64(sk_ctx *ctx, uint64_t *d_buf, uint64_t n);
+/* gather bytes_per_rank from every rank into d_recv (rank-major) */
+int sk_allgather(sk_ctx *ctx, const void *d_send, void *d_recv, uint64_t bytes_per_rank);
+
 /* ---- bench / test helpers ---- */
 /* Jackson default-typing bytes of Longs, ["java.lang.Long",<v>] (M:codec/JsonJacksonCodec.java:
  * 86-117, Long forced typed :103-106), for SplitMix64(seed) values; host buffers.
  * Call with bytes == NULL to get the offsets (and total size in off[n]). */
 int sk_gen_jackson_longs(uint64_t seed, uint64_t n, uint64_t *off, uint8_t *bytes);
+/* device variant: element j = value #(d_idx ? d_idx[j] : first + j) of the same
+ * counter-based sequence; d_off u64[n+1], d_bytes sized n*39 + 16. */
+int sk_gen_jackson_longs_dev(sk_ctx *ctx, uint64_t seed, const uint64_t *d_idx, uint64_t first, uint64_t n,
+                             uint64_t *d_off, uint8_t *d_bytes);
 
 #ifdef __cplusplus
 }

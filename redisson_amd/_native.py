@@ -83,6 +83,22 @@ SIGNATURES = {
     "sk_bloom_contains_dev": (c_int, [P, _u8p, c_uint64, c_uint64, _u64p, _u8p, c_uint64, _u8p]),
     "sk_bloom_count": (c_int, [P, _u8p, c_uint64, P]),
     "sk_gen_jackson_longs": (c_int, [c_uint64, c_uint64, _u64p, _u8p]),
+    "sk_gen_jackson_longs_dev": (c_int, [P, c_uint64, P, c_uint64, c_uint64, P, P]),
+    "sk_dev_alloc": (c_int, [P, c_uint64, P]),
+    "sk_dev_free": (c_int, [P, P]),
+    "sk_h2d": (c_int, [P, P, P, c_uint64]),
+    "sk_d2h": (c_int, [P, P, P, c_uint64]),
+    "sk_dev_memset": (c_int, [P, P, c_int, c_uint64]),
+    "sk_timer_record": (c_int, [P, c_int]),
+    "sk_timer_elapsed": (c_int, [P, c_int, c_int, P]),
+    "sk_prof_enable": (c_int, [P, c_int]),
+    "sk_prof_reset": (c_int, [P]),
+    "sk_prof_read": (c_int, [P, c_char_p, P, P]),
+    "sk_comm_unique_id": (c_int, [P]),
+    "sk_comm_init": (c_int, [P, c_int, c_int, P]),
+    "sk_allreduce_max_u8": (c_int, [P, P, c_uint64]),
+    "sk_allreduce_sum_u64": (c_int, [P, P, c_uint64]),
+    "sk_allgather": (c_int, [P, P, P, c_uint64]),
 }
 
 _lib = None

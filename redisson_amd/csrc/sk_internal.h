@@ -41,4 +41,8 @@ hipError_t launch_bitcount(hipStream_t st, const uint8_t *buf, uint64_t len, uin
 hipError_t launch_bitop(hipStream_t st, int op, uint32_t nsrc, const uint8_t *const *srcs, const uint64_t *lens,
                         uint64_t maxlen, uint8_t *dst);
 
+hipError_t gen_jackson_scan_size(uint64_t n, size_t *bytes);
+hipError_t launch_gen_jackson(hipStream_t st, uint64_t n, uint64_t seed, const uint64_t *idx, uint64_t first,
+                              uint64_t *lens, void *tmp, size_t tmp_bytes, uint64_t *off, uint8_t *out);
+
 } // namespace sk

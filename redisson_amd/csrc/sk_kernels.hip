@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 #include <cstring>
 #include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
 #include <stdint.h>
 
 #include "sk_device.h"
@@ -377,6 +378,53 @@ __global__ void __launch_bounds__(256) k_bitop(int op, uint32_t nsrc, const uint
     }
 }
 
+
+// ------------------------------------------------- synthetic input generator
+// Counter-based SplitMix64: element i = mix(seed + (i+1)*golden), the same
+// sequence sk_gen_jackson_longs produces on the host, rendered as Jackson's
+// default-typed Long ["java.lang.Long",<v>] (bench/test inputs only).
+__device__ __forceinline__ int64_t splitmix_at(uint64_t seed, uint64_t i) {
+    uint64_t z = seed + (i + 1) * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return int64_t(z ^ (z >> 31));
+}
+__device__ __forceinline__ unsigned dec_len(int64_t v) {
+    uint64_t u = v < 0 ? (~uint64_t(v) + 1) : uint64_t(v);
+    unsigned d = 1;
+    while (u >= 10) {
+        u /= 10;
+        d++;
+    }
+    return d + (v < 0);
+}
+__global__ void __launch_bounds__(256) k_gen_len(uint64_t n, uint64_t seed, const uint64_t *__restrict__ idx,
+                                                 uint64_t first, uint64_t *__restrict__ lens) {
+    uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    int64_t v = splitmix_at(seed, idx ? idx[i] : first + i);
+    lens[i] = 18 + dec_len(v) + 1;
+}
+__global__ void __launch_bounds__(256) k_gen_write(uint64_t n, uint64_t seed, const uint64_t *__restrict__ idx,
+                                                   uint64_t first, const uint64_t *__restrict__ off,
+                                                   uint8_t *__restrict__ out) {
+    uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    int64_t v = splitmix_at(seed, idx ? idx[i] : first + i);
+    const char pre[] = "[\"java.lang.Long\",";
+    uint8_t *p = out + off[i];
+    for (int q = 0; q < 18; q++) p[q] = uint8_t(pre[q]);
+    unsigned L = dec_len(v);
+    uint64_t u = v < 0 ? (~uint64_t(v) + 1) : uint64_t(v);
+    uint8_t *d = p + 18;
+    if (v < 0) d[0] = '-';
+    for (unsigned q = L; q > unsigned(v < 0); q--) {
+        d[q - 1] = uint8_t('0' + u % 10);
+        u /= 10;
+    }
+    p[18 + L] = ']';
+}
+
 // ================================================================ launchers
 #define SK_LAUNCH_CHECK()                                                                                              \
     do {                                                                                                               \
@@ -547,6 +595,30 @@ hipError_t launch_bitop(hipStream_t st, int op, uint32_t nsrc, const uint8_t *co
     if (!maxlen) return hipSuccess;
     hipLaunchKernelGGL(k_bitop, dim3(grid_for((maxlen + 15) / 16, 256, 4096)), dim3(256), 0, st, op, nsrc, srcs, lens,
                        maxlen, dst);
+    SK_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+hipError_t gen_jackson_scan_size(uint64_t n, size_t *bytes) {
+    size_t sz = 0;
+    hipError_t e = rocprim::inclusive_scan(nullptr, sz, (const uint64_t *)nullptr, (uint64_t *)nullptr, size_t(n),
+                                           rocprim::plus<uint64_t>());
+    *bytes = sz;
+    return e;
+}
+
+// lens: scratch u64[n]; off: u64[n+1]
+hipError_t launch_gen_jackson(hipStream_t st, uint64_t n, uint64_t seed, const uint64_t *idx, uint64_t first,
+                              uint64_t *lens, void *tmp, size_t tmp_bytes, uint64_t *off, uint8_t *out) {
+    if (!n) return hipMemsetAsync(off, 0, 8, st);
+    hipLaunchKernelGGL(k_gen_len, dim3(grid_for(n, 256)), dim3(256), 0, st, n, seed, idx, first, lens);
+    SK_LAUNCH_CHECK();
+    hipError_t e = hipMemsetAsync(off, 0, 8, st);
+    if (e != hipSuccess) return e;
+    size_t sz = tmp_bytes;
+    e = rocprim::inclusive_scan(tmp, sz, lens, off + 1, size_t(n), rocprim::plus<uint64_t>(), st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_gen_write, dim3(grid_for(n, 256)), dim3(256), 0, st, n, seed, idx, first, off, out);
     SK_LAUNCH_CHECK();
     return hipSuccess;
 }

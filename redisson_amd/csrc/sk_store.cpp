@@ -20,6 +20,8 @@
 #include <unordered_map>
 #include <vector>
 
+#include <rccl/rccl.h>
+
 #include "../../include/redisson_sketch.h"
 #include "sk_internal.h"
 
@@ -197,6 +199,21 @@ struct sk_ctx {
     DirEnt *d_dir = nullptr;
     uint64_t dir_cap = 0;
 
+    // in-library kernel timing (sk_prof_*): event pairs around the hot launches
+    bool prof = false;
+    struct ProfRec {
+        int phase;
+        hipEvent_t a, b;
+    };
+    std::vector<ProfRec> prof_pending;
+    std::vector<hipEvent_t> ev_pool;
+    double prof_ms[16] = {0};
+    uint64_t prof_n[16] = {0};
+    hipEvent_t timers[16] = {};
+
+    // cross-GPU exchange (RCCL over xGMI)
+    ncclComm_t comm = nullptr;
+
     // workspace
     uint32_t *d_zero = nullptr; // device u32[4] zeros: id 0 / empty length
     DBuf keys_a, keys_b, vals_a, vals_b, sort_tmp, in_off, in_bytes, in_ids, in_cmd, out_u8, misc, partial, hist,
@@ -235,6 +252,55 @@ std::string key_at(const uint64_t *off, const uint8_t *bytes, uint64_t i) {
 int sync(sk_ctx *c) {
     HIPCHK(c, hipStreamSynchronize(c->st));
     return SK_OK;
+}
+
+// phases timed by sk_prof_* (index = SK_PROF_* in the header)
+const char *kPhaseNames[] = {"pfadd_hash", "pfadd_sort", "pfadd_apply", "hll_hist",     "hll_union",
+                             "bloom_contains", "bloom_probes", "bloom_sort", "bloom_apply", "setbit",
+                             "getbit",     "bitcount",   "bitop"};
+constexpr int kNumPhases = sizeof(kPhaseNames) / sizeof(kPhaseNames[0]);
+
+hipEvent_t ev_get(sk_ctx *c) {
+    if (!c->ev_pool.empty()) {
+        hipEvent_t e = c->ev_pool.back();
+        c->ev_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    (void)hipEventCreate(&e);
+    return e;
+}
+struct Prof { // RAII: events around one launch when profiling is on
+    sk_ctx *c;
+    int phase;
+    hipEvent_t a = nullptr;
+    Prof(sk_ctx *c_, int ph) : c(c_), phase(ph) {
+        if (c->prof) {
+            a = ev_get(c);
+            (void)hipEventRecord(a, c->st);
+        }
+    }
+    ~Prof() {
+        if (a) {
+            hipEvent_t b = ev_get(c);
+            (void)hipEventRecord(b, c->st);
+            c->prof_pending.push_back({phase, a, b});
+        }
+    }
+};
+void prof_collect(sk_ctx *c) {
+    if (c->prof_pending.empty()) return;
+    (void)hipStreamSynchronize(c->st);
+    for (auto &r : c->prof_pending) {
+        float ms = 0;
+        if (hipEventElapsedTime(&ms, r.a, r.b) == hipSuccess) {
+            c->prof_ms[r.phase] += ms;
+            c->prof_n[r.phase] += 1;
+        }
+        c->ev_pool.push_back(r.a);
+        c->ev_pool.push_back(r.b);
+    }
+    c->prof_pending.clear();
 }
 
 // --------------------------------------------------------------- HLL slabs
@@ -419,17 +485,21 @@ int pfadd_device(sk_ctx *c, uint64_t n, const uint32_t *d_ids, const uint64_t *d
     size_t tmp = 0;
     HIPCHK(c, sk::sort_keys_size(n, slot_shift, slot_shift + 14 + id_bits, &tmp));
     HIPCHK(c, c->sort_tmp.ensure(tmp));
+    { Prof p_(c, 0);
     HIPCHK(c, sk::launch_pfadd_hash(c->st, n, d_ids, d_off, d_bytes, d_cmd, c->redis_major >= 5, slot_shift,
-                                    c->keys_a.as<uint64_t>()));
+                                    c->keys_a.as<uint64_t>())); }
+    { Prof p_(c, 1);
     HIPCHK(c, sk::sort_keys(c->st, c->sort_tmp.p, c->sort_tmp.cap, c->keys_a.as<uint64_t>(), c->keys_b.as<uint64_t>(),
-                            n, slot_shift, slot_shift + 14 + id_bits));
-    HIPCHK(c, sk::launch_pfadd_apply(c->st, n, c->keys_b.as<uint64_t>(), slot_shift, cmd_mask, c->arena, d_changed));
+                            n, slot_shift, slot_shift + 14 + id_bits)); }
+    { Prof p_(c, 2);
+    HIPCHK(c, sk::launch_pfadd_apply(c->st, n, c->keys_b.as<uint64_t>(), slot_shift, cmd_mask, c->arena, d_changed)); }
     return SK_OK;
 }
 
 int hll_histograms(sk_ctx *c, uint64_t n, const uint32_t *d_ids, const uint8_t *base, std::vector<uint32_t> &h) {
     HIPCHK(c, c->hist.ensure(n * 64 * 4));
-    HIPCHK(c, sk::launch_hll_hist(c->st, n, d_ids, base, c->hist.as<uint32_t>()));
+    { Prof p_(c, 3);
+    HIPCHK(c, sk::launch_hll_hist(c->st, n, d_ids, base, c->hist.as<uint32_t>())); }
     h.resize(n * 64);
     HIPCHK(c, hipMemcpyAsync(h.data(), c->hist.p, n * 64 * 4, hipMemcpyDeviceToHost, c->st));
     return sync(c);
@@ -539,6 +609,11 @@ int sk_close(sk_ctx *c) {
     if (!c) return SK_OK;
     (void)hipSetDevice(c->device);
     if (c->st) (void)hipStreamSynchronize(c->st);
+    if (c->comm) (void)ncclCommDestroy(c->comm);
+    prof_collect(c);
+    for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
+    for (hipEvent_t e : c->timers)
+        if (e) (void)hipEventDestroy(e);
     for (auto &e : c->strs)
         if (e.ptr) (void)hipFree(e.ptr);
     if (c->arena) (void)hipFree(c->arena);
@@ -767,7 +842,8 @@ int sk_pfadd_dev(sk_ctx *c, uint64_t n, const uint32_t *d_ids, const uint64_t *d
 int sk_hll_histogram_dev(sk_ctx *c, uint64_t n, const uint32_t *d_ids, uint32_t *d_hist) {
     std::lock_guard<std::mutex> g(c->mu);
     HIPCHK(c, hipSetDevice(c->device));
-    HIPCHK(c, sk::launch_hll_hist(c->st, n, d_ids, c->arena, d_hist));
+    { Prof p_(c, 3);
+    HIPCHK(c, sk::launch_hll_hist(c->st, n, d_ids, c->arena, d_hist)); }
     return sync(c);
 }
 
@@ -841,7 +917,8 @@ int sk_hll_union_dev(sk_ctx *c, uint64_t n, const uint32_t *d_ids, uint8_t *d_ou
     HIPCHK(c, hipSetDevice(c->device));
     const uint64_t max_groups = 4096;
     HIPCHK(c, c->partial.ensure(max_groups * kHllBytes));
-    HIPCHK(c, sk::launch_hll_union(c->st, n, d_ids, c->arena, c->partial.as<uint8_t>(), max_groups, d_out, 0));
+    { Prof p_(c, 4);
+    HIPCHK(c, sk::launch_hll_union(c->st, n, d_ids, c->arena, c->partial.as<uint8_t>(), max_groups, d_out, 0)); }
     return sync(c);
 }
 
@@ -1030,7 +1107,8 @@ int sk_setbit_dev(sk_ctx *c, const uint8_t *key, uint64_t len, uint64_t n, const
     if ((r = str_len(c, id, &cur))) return r;
     if (need > cur && (r = str_set_len(c, id, need))) return r;
     if (!d_out_old) {
-        HIPCHK(c, sk::launch_setbit_void(c->st, n, d_offsets, c->strs[id].ptr, value & 1));
+        { Prof p_(c, 9);
+        HIPCHK(c, sk::launch_setbit_void(c->st, n, d_offsets, c->strs[id].ptr, value & 1)); }
         return sync(c);
     }
     size_t tmp;
@@ -1068,7 +1146,8 @@ int sk_getbit_dev(sk_ctx *c, const uint8_t *key, uint64_t len, uint64_t n, const
         HIPCHK(c, hipMemsetAsync(d_out, 0, n, c->st));
         return sync(c);
     }
-    HIPCHK(c, sk::launch_getbit_single(c->st, n, d_offsets, c->strs[id].ptr, &c->d_dir[id].len, d_out));
+    { Prof p_(c, 10);
+    HIPCHK(c, sk::launch_getbit_single(c->st, n, d_offsets, c->strs[id].ptr, &c->d_dir[id].len, d_out)); }
     return sync(c);
 }
 
@@ -1331,12 +1410,15 @@ static int bloom_add_device(sk_ctx *c, uint32_t id, int64_t size, int32_t k, uin
         size_t tmp;
         HIPCHK(c, sk::sort_keys_size(m, 32, 32 + idx_bits, &tmp));
         HIPCHK(c, c->sort_tmp.ensure(tmp));
+        { Prof p_(c, 6);
         HIPCHK(c, sk::launch_bloom_probes(c->st, e, d_off + s, d_bytes, uint64_t(size), magic, k,
-                                          c->keys_a.as<uint64_t>()));
+                                          c->keys_a.as<uint64_t>())); }
+        { Prof p_(c, 7);
         HIPCHK(c, sk::sort_keys(c->st, c->sort_tmp.p, c->sort_tmp.cap, c->keys_a.as<uint64_t>(),
-                                c->keys_b.as<uint64_t>(), m, 32, 32 + idx_bits));
+                                c->keys_b.as<uint64_t>(), m, 32, 32 + idx_bits)); }
+        { Prof p_(c, 8);
         HIPCHK(c, sk::launch_bloom_apply(c->st, m, c->keys_b.as<uint64_t>(), c->strs[id].ptr, &c->d_dir[id].len, k,
-                                         d_out + s));
+                                         d_out + s)); }
     }
     return SK_OK;
 }
@@ -1425,8 +1507,9 @@ int sk_bloom_contains_dev(sk_ctx *c, const uint8_t *name, uint64_t len, uint64_t
     if ((r = bloom_prepare(c, nm, b->size, b->k, false, &id))) return r;
     const uint8_t *bits = id == kNoId ? reinterpret_cast<const uint8_t *>(c->d_zero) : c->strs[id].ptr;
     const uint64_t *dl = id == kNoId ? reinterpret_cast<const uint64_t *>(c->d_zero) : &c->d_dir[id].len;
+    { Prof p_(c, 5);
     HIPCHK(c, sk::launch_bloom_contains(c->st, n, d_off, d_bytes, bits, dl, uint64_t(b->size),
-                                        magic_for(uint64_t(b->size)), b->k, d_out));
+                                        magic_for(uint64_t(b->size)), b->k, d_out)); }
     return sync(c);
 }
 
@@ -1459,3 +1542,135 @@ int sk_bloom_count(sk_ctx *c, const uint8_t *name, uint64_t len, int32_t *out) {
 }
 
 } // extern "C"
+
+// ============================================== device memory, timing, RCCL
+extern "C" {
+
+int sk_dev_alloc(sk_ctx *c, uint64_t bytes, void **out) {
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(c, hipSetDevice(c->device));
+    *out = nullptr;
+    if (hipMalloc(out, std::max<uint64_t>(bytes, 16)) != hipSuccess)
+        return fail(c, SK_ENOMEM, "cannot allocate %llu device bytes", (unsigned long long)bytes);
+    return SK_OK;
+}
+int sk_dev_free(sk_ctx *c, void *p) {
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->st));
+    if (p) HIPCHK(c, hipFree(p));
+    return SK_OK;
+}
+int sk_h2d(sk_ctx *c, void *dst, const void *src, uint64_t n) {
+    std::lock_guard<std::mutex> g(c->mu);
+    if (n) HIPCHK(c, hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, c->st));
+    return sync(c);
+}
+int sk_d2h(sk_ctx *c, void *dst, const void *src, uint64_t n) {
+    std::lock_guard<std::mutex> g(c->mu);
+    if (n) HIPCHK(c, hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, c->st));
+    return sync(c);
+}
+int sk_dev_memset(sk_ctx *c, void *p, int v, uint64_t n) {
+    std::lock_guard<std::mutex> g(c->mu);
+    if (n) HIPCHK(c, hipMemsetAsync(p, v, n, c->st));
+    return sync(c);
+}
+
+int sk_timer_record(sk_ctx *c, int slot) {
+    std::lock_guard<std::mutex> g(c->mu);
+    if (slot < 0 || slot >= 16) return fail(c, SK_EINVAL, "timer slot");
+    if (!c->timers[slot]) HIPCHK(c, hipEventCreate(&c->timers[slot]));
+    HIPCHK(c, hipEventRecord(c->timers[slot], c->st));
+    return SK_OK;
+}
+int sk_timer_elapsed(sk_ctx *c, int a, int b, float *ms) {
+    std::lock_guard<std::mutex> g(c->mu);
+    if (a < 0 || a >= 16 || b < 0 || b >= 16 || !c->timers[a] || !c->timers[b])
+        return fail(c, SK_EINVAL, "timer slot");
+    HIPCHK(c, hipEventSynchronize(c->timers[b]));
+    HIPCHK(c, hipEventElapsedTime(ms, c->timers[a], c->timers[b]));
+    return SK_OK;
+}
+
+int sk_prof_enable(sk_ctx *c, int on) {
+    std::lock_guard<std::mutex> g(c->mu);
+    c->prof = on != 0;
+    return SK_OK;
+}
+int sk_prof_reset(sk_ctx *c) {
+    std::lock_guard<std::mutex> g(c->mu);
+    prof_collect(c);
+    for (int i = 0; i < 16; i++) c->prof_ms[i] = 0, c->prof_n[i] = 0;
+    return SK_OK;
+}
+int sk_prof_read(sk_ctx *c, const char *phase, uint64_t *launches, double *total_ms) {
+    std::lock_guard<std::mutex> g(c->mu);
+    prof_collect(c);
+    for (int i = 0; i < kNumPhases; i++)
+        if (!std::strcmp(phase, kPhaseNames[i])) {
+            *launches = c->prof_n[i];
+            *total_ms = c->prof_ms[i];
+            return SK_OK;
+        }
+    return fail(c, SK_EINVAL, "unknown phase %s", phase);
+}
+
+#define NCCLCHK(c, expr)                                                                                               \
+    do {                                                                                                               \
+        ncclResult_t r__ = (expr);                                                                                     \
+        if (r__ != ncclSuccess) return fail((c), SK_EDEVICE, "RCCL error %s", ncclGetErrorString(r__));                \
+    } while (0)
+
+int sk_comm_unique_id(uint8_t *out128) {
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess) return SK_EDEVICE;
+    std::memcpy(out128, id.internal, NCCL_UNIQUE_ID_BYTES);
+    return SK_OK;
+}
+int sk_comm_init(sk_ctx *c, int nranks, int rank, const uint8_t *id128) {
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(c, hipSetDevice(c->device));
+    ncclUniqueId id;
+    std::memcpy(id.internal, id128, NCCL_UNIQUE_ID_BYTES);
+    if (c->comm) NCCLCHK(c, ncclCommDestroy(c->comm));
+    c->comm = nullptr;
+    NCCLCHK(c, ncclCommInitRank(&c->comm, nranks, id, rank));
+    return SK_OK;
+}
+// cross-GPU PFMERGE / countWith: register-wise max of 16384-byte arrays
+int sk_allreduce_max_u8(sk_ctx *c, uint8_t *d_buf, uint64_t n) {
+    std::lock_guard<std::mutex> g(c->mu);
+    if (!c->comm) return fail(c, SK_EINVAL, "sk_comm_init first");
+    NCCLCHK(c, ncclAllReduce(d_buf, d_buf, n, ncclUint8, ncclMax, c->comm, c->st));
+    return sync(c);
+}
+// BITCOUNT of a range-sharded bitset
+int sk_allreduce_sum_u64(sk_ctx *c, uint64_t *d_buf, uint64_t n) {
+    std::lock_guard<std::mutex> g(c->mu);
+    if (!c->comm) return fail(c, SK_EINVAL, "sk_comm_init first");
+    NCCLCHK(c, ncclAllReduce(d_buf, d_buf, n, ncclUint64, ncclSum, c->comm, c->st));
+    return sync(c);
+}
+// key-sharded BITOP: gather the remote operands, then a local op
+int sk_allgather(sk_ctx *c, const void *d_send, void *d_recv, uint64_t bytes_per_rank) {
+    std::lock_guard<std::mutex> g(c->mu);
+    if (!c->comm) return fail(c, SK_EINVAL, "sk_comm_init first");
+    NCCLCHK(c, ncclAllGather(d_send, d_recv, bytes_per_rank, ncclUint8, c->comm, c->st));
+    return sync(c);
+}
+
+} // extern "C"
+
+extern "C" int sk_gen_jackson_longs_dev(sk_ctx *c, uint64_t seed, const uint64_t *d_idx, uint64_t first, uint64_t n,
+                                        uint64_t *d_off, uint8_t *d_bytes) {
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(c, hipSetDevice(c->device));
+    size_t tmp;
+    HIPCHK(c, sk::gen_jackson_scan_size(n, &tmp));
+    HIPCHK(c, c->sort_tmp.ensure(std::max<size_t>(tmp, 16)));
+    HIPCHK(c, c->keys_a.ensure(std::max<uint64_t>(n, 1) * 8));
+    HIPCHK(c, sk::launch_gen_jackson(c->st, n, seed, d_idx, first, c->keys_a.as<uint64_t>(), c->sort_tmp.p,
+                                     c->sort_tmp.cap, d_off, d_bytes));
+    return sync(c);
+}

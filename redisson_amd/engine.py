@@ -37,9 +37,50 @@ def _addr(a) -> int:
         return 0
     if isinstance(a, np.ndarray):
         return a.ctypes.data
-    if hasattr(a, "data_ptr"):  # torch tensor (device pointer)
-        return a.data_ptr()
+    if isinstance(a, DeviceBuffer):
+        return a.ptr
     return int(a)
+
+
+class DeviceBuffer:
+    """HBM allocation owned by an engine context (no torch: the engine links the
+    system HIP runtime, and one process must not load two)."""
+
+    def __init__(self, engine: "SketchEngine", nbytes: int):
+        self.engine = engine
+        self.nbytes = int(nbytes)
+        p = ctypes.c_void_p()
+        engine._check(engine.lib.sk_dev_alloc(engine.ctx, self.nbytes, ctypes.addressof(p)))
+        self.ptr = p.value
+
+    def upload(self, arr: np.ndarray, offset: int = 0):
+        a = np.ascontiguousarray(arr)
+        assert offset + a.nbytes <= self.nbytes
+        self.engine._check(self.engine.lib.sk_h2d(self.engine.ctx, self.ptr + offset, a.ctypes.data, a.nbytes))
+        return self
+
+    def download(self, dtype=np.uint8, count: int = -1, offset: int = 0) -> np.ndarray:
+        dt = np.dtype(dtype)
+        if count < 0:
+            count = (self.nbytes - offset) // dt.itemsize
+        out = np.empty(count, dtype=dt)
+        self.engine._check(self.engine.lib.sk_d2h(self.engine.ctx, out.ctypes.data, self.ptr + offset, out.nbytes))
+        return out
+
+    def zero(self):
+        self.engine._check(self.engine.lib.sk_dev_memset(self.engine.ctx, self.ptr, 0, self.nbytes))
+        return self
+
+    def free(self):
+        if self.ptr and self.engine.ctx:
+            self.engine.lib.sk_dev_free(self.engine.ctx, self.ptr)
+        self.ptr = 0
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
 
 
 def pack(items: Sequence[bytes]):
@@ -101,6 +142,63 @@ class SketchEngine:
 
     def sync(self):
         self._check(self.lib.sk_sync(self.ctx))
+
+    # ------------------------------------------------------------ device memory / timing / RCCL
+    def alloc(self, nbytes: int) -> DeviceBuffer:
+        return DeviceBuffer(self, nbytes)
+
+    def to_device(self, arr: np.ndarray, pad: int = 0) -> DeviceBuffer:
+        a = np.ascontiguousarray(arr)
+        return DeviceBuffer(self, a.nbytes + pad).zero().upload(a)
+
+    def gen_jackson_longs_dev(self, seed: int, n: int, first: int = 0, d_idx=None):
+        """Device-resident Jackson Long elements: (d_off u64[n+1], d_bytes, total_bytes)."""
+        d_off = self.alloc((n + 1) * 8)
+        d_bytes = self.alloc(n * 39 + 16).zero()
+        self._check(self.lib.sk_gen_jackson_longs_dev(self.ctx, seed, _addr(d_idx), first, n, d_off.ptr,
+                                                      d_bytes.ptr))
+        total = int(d_off.download(np.uint64, 1, offset=n * 8)[0])
+        return d_off, d_bytes, total
+
+    def timer_record(self, slot: int):
+        self._check(self.lib.sk_timer_record(self.ctx, slot))
+
+    def timer_elapsed_ms(self, a: int, b: int) -> float:
+        ms = ctypes.c_float()
+        self._check(self.lib.sk_timer_elapsed(self.ctx, a, b, ctypes.addressof(ms)))
+        return ms.value
+
+    def prof_enable(self, on: bool = True):
+        self._check(self.lib.sk_prof_enable(self.ctx, int(on)))
+
+    def prof_reset(self):
+        self._check(self.lib.sk_prof_reset(self.ctx))
+
+    def prof_read(self, phase: str):
+        n, ms = ctypes.c_uint64(), ctypes.c_double()
+        self._check(self.lib.sk_prof_read(self.ctx, phase.encode(), ctypes.addressof(n), ctypes.addressof(ms)))
+        return n.value, ms.value
+
+    @staticmethod
+    def comm_unique_id() -> bytes:
+        buf = (ctypes.c_uint8 * 128)()
+        st = N.load().sk_comm_unique_id(ctypes.addressof(buf))
+        if st != N.SK_OK:
+            raise RedisException("ncclGetUniqueId failed")
+        return bytes(buf)
+
+    def comm_init(self, nranks: int, rank: int, uid: bytes):
+        b = (ctypes.c_uint8 * 128).from_buffer_copy(uid)
+        self._check(self.lib.sk_comm_init(self.ctx, nranks, rank, ctypes.addressof(b)))
+
+    def allreduce_max_u8(self, buf: DeviceBuffer, n: int):
+        self._check(self.lib.sk_allreduce_max_u8(self.ctx, _addr(buf), n))
+
+    def allreduce_sum_u64(self, buf: DeviceBuffer, n: int):
+        self._check(self.lib.sk_allreduce_sum_u64(self.ctx, _addr(buf), n))
+
+    def allgather(self, send: DeviceBuffer, recv: DeviceBuffer, bytes_per_rank: int):
+        self._check(self.lib.sk_allgather(self.ctx, _addr(send), _addr(recv), bytes_per_rank))
 
     # ------------------------------------------------------------ keys
     def key_type(self, key) -> int:

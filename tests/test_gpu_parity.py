@@ -76,12 +76,11 @@ def test_pfcount_single_and_union(engine, O):
 def test_pfcount_register_ge_40_order_fallback(engine, O):
     # craft an element whose rho >= 40 is astronomically rare; instead merge a
     # raw register array with values >= 40 through the device merge entry
-    import torch
     regs = np.zeros(16384, dtype=np.uint8)
     rng = np.random.default_rng(11)
     regs[:] = rng.integers(0, 12, 16384)
     regs[[5, 77, 9000]] = [40, 45, 50]
-    d = torch.from_numpy(regs).cuda()
+    d = engine.to_device(regs)
     engine.hll_merge_registers_dev(b"big40", d)
     np.testing.assert_array_equal(engine.hll_registers(b"big40"), regs)
     assert engine.pfcount([[b"big40"]]) == [O.count_regs(regs, 1)]        # dense order
@@ -110,26 +109,25 @@ def test_hll_wrongtype(engine):
 
 
 def test_pfadd_dev_path(engine, O):
-    import torch
     n, nkeys = 50000, 37
     off, buf = gen_jackson_longs(0x5EED0002, n)
     rng = np.random.default_rng(5)
     kid = rng.integers(0, nkeys, n).astype(np.uint32)
     names = [b"dev:%d" % i for i in range(nkeys)]
     ids = engine.hll_resolve(names)
-    d_ids = torch.from_numpy(ids[kid].astype(np.int32)).cuda()
-    d_off = torch.from_numpy(off.view(np.int64)).cuda()
-    d_buf = torch.from_numpy(buf).cuda()
-    d_out = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    d_ids = engine.to_device(ids[kid])
+    d_off = engine.to_device(off)
+    d_buf = engine.to_device(buf, pad=16)
+    d_out = engine.alloc(n)
     engine.pfadd_dev(n, d_ids, d_off, d_buf, int(off[-1]), d_out)
     regs, want = O.HLLStore().pfadd_bulk(kid, off, buf, nkeys)
-    assert np.array_equal(d_out.cpu().numpy(), want)
+    assert np.array_equal(d_out.download(np.uint8, n), want)
     for i, nm in enumerate(names):
         np.testing.assert_array_equal(engine.hll_registers(nm), regs[i])
     # histogram + host estimator == oracle count
-    d_hist = torch.zeros(nkeys * 64, dtype=torch.int32, device="cuda")
-    engine.hll_histogram_dev(nkeys, torch.from_numpy(ids.astype(np.int32)).cuda(), d_hist)
-    h = d_hist.cpu().numpy().view(np.uint32).reshape(nkeys, 64)
+    d_hist = engine.alloc(nkeys * 64 * 4)
+    engine.hll_histogram_dev(nkeys, engine.to_device(ids), d_hist)
+    h = d_hist.download(np.uint32).reshape(nkeys, 64)
     for i in range(nkeys):
         assert engine.estimate_hist(h[i]) == O.count_regs(regs[i], 1)
 
@@ -221,19 +219,18 @@ def test_bitop(engine, O):
 
 
 def test_bulk_setbit_getbit_dev(engine):
-    import torch
     rng = np.random.default_rng(4)
     n = 1 << 16
-    offs = rng.integers(0, 1 << 24, n).astype(np.int64)
-    d = torch.from_numpy(offs).cuda()
+    offs = rng.integers(0, 1 << 24, n).astype(np.uint64)
+    d = engine.to_device(offs)
     engine.setbit_dev(b"bulk", n, d, 1)
-    out = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    out = engine.alloc(n)
     engine.getbit_dev(b"bulk", n, d, out)
-    assert int(out.sum()) == n
+    assert int(out.download(np.uint8, n).sum()) == n
     assert engine.bitcount(b"bulk") == len(np.unique(offs))
     # with replies: first occurrence sees 0, repeats see 1
-    offs2 = np.concatenate([offs[:100], offs[:100], rng.integers(1 << 24, 1 << 25, 100)]).astype(np.int64)
-    old = torch.zeros(len(offs2), dtype=torch.uint8, device="cuda")
-    engine.setbit_dev(b"bulk", len(offs2), torch.from_numpy(offs2).cuda(), 0, old)
-    o = old.cpu().numpy()
+    offs2 = np.concatenate([offs[:100], offs[:100], rng.integers(1 << 24, 1 << 25, 100)]).astype(np.uint64)
+    old = engine.alloc(len(offs2))
+    engine.setbit_dev(b"bulk", len(offs2), engine.to_device(offs2), 0, old)
+    o = old.download(np.uint8, len(offs2))
     assert o[:100].all() and not o[100:200].any()

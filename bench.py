@@ -30,7 +30,8 @@ sys.path.insert(0, ROOT)
 from redisson_amd import SketchEngine, owner  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-PHASES = ["pfadd_hash", "pfadd_sort", "pfadd_apply", "bloom_contains"]
+PHASES = ["pfadd_claim", "pfadd_commit", "pfadd_hash", "pfadd_sort", "pfadd_apply", "bloom_contains"]
+HLL_PHASES = PHASES[:5]
 
 
 def log(*a):
@@ -155,11 +156,13 @@ def main():
 
     units = 2 * B * K * world
     value = units / wall
-    hll_ms = sum(prof[p][1] for p in PHASES[:3])
+    hll_ms = sum(prof[p][1] for p in HLL_PHASES)
     bl_ms = prof["bloom_contains"][1]
     # roofline of the dominant kernel: algorithmic bytes per unit x units / avg launch time
     dom = max(PHASES, key=lambda p: prof[p][1])
     per_unit = {
+        "pfadd_claim": mean_len_h + 8 + 4 + 1 + 8,     # key bytes + offset + slab id + register in, record out
+        "pfadd_commit": 8 + 1 + 1,                     # record in, register + reply out
         "pfadd_hash": mean_len_h + 8 + 4 + 8,          # key bytes + offset + slab id in, sort key out
         "pfadd_sort": 2 * 8 * 5,                       # 5 radix passes over 8-byte keys (read + write)
         "pfadd_apply": 8 + 64 + 64 + 1,                # sorted key + register sector RMW + reply byte

@@ -190,7 +190,7 @@ int sk_timer_elapsed(sk_ctx *ctx, int slot_a, int slot_b, float *ms);
 /* per-kernel device time inside the library (event pairs around each launch
  * of a phase): "pfadd_hash", "pfadd_sort", "pfadd_apply", "hll_hist",
  * "hll_union", "bloom_contains", "bloom_probes", "bloom_sort", "bloom_apply",
- * "setbit", "getbit", "bitcount", "bitop" */
+ * "setbit", "getbit", "bitcount", "bitop", "pfadd_claim", "pfadd_commit" */
 int sk_prof_enable(sk_ctx *ctx, int on);
 int sk_prof_reset(sk_ctx *ctx);
 int sk_prof_read(sk_ctx *ctx, const char *phase, uint64_t *launches, double *total_ms);

@@ -80,6 +80,150 @@ __global__ void __launch_bounds__(256) k_pfadd_apply(uint64_t n, const uint64_t 
     if (R != R0) *r = uint8_t(R);
 }
 
+
+// ----------------------------------------------------- PFADD, sparse path
+// For batches that touch many registers thinly (C2: 1M elements over
+// 100k x 16384 registers) the sort is replaced by a claim / commit protocol
+// that uses the two spare bits of every register byte (values <= 51 < 64):
+//   bit 7 CLAIMED  -- some candidate of this batch targets the register
+//   bit 6 CONFLICT -- at least two candidates target it
+// A candidate is an element whose rho exceeds the pre-batch value R0 (the
+// value bits never change during the claim pass).  A register with a single
+// candidate is raised by it and that command replies 1 -- exactly the
+// sequential result, because non-candidates change nothing.  Registers with
+// several candidates (rare: ~n^2/2R pairs) are replayed in batch order by
+// k_pfadd_conflicts.  Flags are cleared by the commit that writes the value.
+#define SK_CLAIMED 0x80u
+#define SK_CONFLICT 0x40u
+
+__global__ void __launch_bounds__(256) k_pfadd_claim(uint64_t n, const uint32_t *__restrict__ key_ids,
+                                                     const uint64_t *__restrict__ off,
+                                                     const uint8_t *__restrict__ bytes, int v5, uint8_t *arena,
+                                                     uint64_t *__restrict__ rec) {
+    uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint64_t o = off[i];
+    uint32_t len = uint32_t(off[i + 1] - o);
+    uint64_t h = murmur64a(bytes + o, len, 0xadc83b19ull);
+    uint32_t reg, rho;
+    hll_pat(h, v5, &reg, &rho);
+    uint64_t slot = (uint64_t(key_ids[i]) << 14) | reg;
+    uint8_t *p = arena + slot;
+    uint64_t r = 0;
+    if (rho > (uint32_t(*p) & 63u)) { // candidate
+        uint32_t sh = uint32_t(slot & 3) * 8u;
+        uint32_t *w = reinterpret_cast<uint32_t *>(arena + (slot & ~uint64_t(3)));
+        uint32_t old = atomicOr(w, SK_CLAIMED << sh);
+        if ((old >> sh) & SK_CLAIMED) atomicOr(w, SK_CONFLICT << sh);
+        r = (slot << 7) | (uint64_t(rho) << 1) | 1u;
+    }
+    rec[i] = r;
+}
+
+__global__ void __launch_bounds__(256) k_pfadd_commit(uint64_t n, const uint64_t *__restrict__ rec,
+                                                      const uint32_t *__restrict__ cmd_of, uint8_t *arena,
+                                                      uint8_t *__restrict__ changed, uint64_t *conf_keys,
+                                                      uint32_t *conf_vals, uint32_t *conf_count, uint32_t conf_cap) {
+    uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint64_t r = rec[i];
+    if (!(r & 1u)) return;
+    uint64_t slot = r >> 7;
+    uint32_t rho = uint32_t(r >> 1) & 63u;
+    uint32_t cmd = cmd_of ? cmd_of[i] : uint32_t(i);
+    uint8_t *p = arena + slot;
+    if (!(*p & SK_CONFLICT)) {
+        *p = uint8_t(rho); // sole candidate: raise and clear the flags
+        changed[cmd] = 1;
+        return;
+    }
+    uint32_t k = atomicAdd(conf_count, 1u);
+    if (k < conf_cap) {
+        conf_keys[k] = (slot << 26) | i; // batch order inside a register
+        conf_vals[k] = (cmd << 6) | rho;
+    }
+}
+
+// One workgroup: bitonic sort of the conflict list in LDS by (slot, seq),
+// then each register's first entry replays its candidates in order.
+// Lists longer than the LDS capacity are left for the host (rocPRIM sort).
+#define SK_CONF_LDS 8192
+__global__ void __launch_bounds__(1024) k_pfadd_conflicts(const uint64_t *__restrict__ conf_keys,
+                                                          const uint32_t *__restrict__ conf_vals,
+                                                          const uint32_t *__restrict__ conf_count, uint8_t *arena,
+                                                          uint8_t *__restrict__ changed) {
+    __shared__ uint64_t K[SK_CONF_LDS];
+    __shared__ uint32_t V[SK_CONF_LDS];
+    uint32_t cnt = *conf_count;
+    if (cnt == 0 || cnt > SK_CONF_LDS) return;
+    uint32_t P = 1;
+    while (P < cnt) P <<= 1;
+    for (uint32_t t = threadIdx.x; t < P; t += blockDim.x) {
+        K[t] = t < cnt ? conf_keys[t] : ~0ull;
+        V[t] = t < cnt ? conf_vals[t] : 0u;
+    }
+    __syncthreads();
+    for (uint32_t kk = 2; kk <= P; kk <<= 1)
+        for (uint32_t j = kk >> 1; j > 0; j >>= 1) {
+            for (uint32_t t = threadIdx.x; t < P; t += blockDim.x) {
+                uint32_t x = t ^ j;
+                if (x > t) {
+                    bool up = (t & kk) == 0;
+                    uint64_t a = K[t], b = K[x];
+                    if ((a > b) == up) {
+                        K[t] = b;
+                        K[x] = a;
+                        uint32_t tv = V[t];
+                        V[t] = V[x];
+                        V[x] = tv;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    for (uint32_t t = threadIdx.x; t < cnt; t += blockDim.x) {
+        uint64_t slot = K[t] >> 26;
+        if (t > 0 && (K[t - 1] >> 26) == slot) continue;
+        uint8_t *p = arena + slot;
+        uint32_t R = uint32_t(*p) & 63u, R0 = R;
+        for (uint32_t u = t; u < cnt && (K[u] >> 26) == slot; u++) {
+            uint32_t rho = V[u] & 63u;
+            if (rho > R) {
+                changed[V[u] >> 6] = 1;
+                R = rho;
+            }
+        }
+        (void)R0;
+        *p = uint8_t(R); // also clears the flags
+    }
+}
+
+// host fallback for long conflict lists: same replay over a rocPRIM-sorted list
+__global__ void __launch_bounds__(256) k_pfadd_conflicts_sorted(uint64_t cnt, const uint64_t *__restrict__ K,
+                                                                const uint32_t *__restrict__ V, uint8_t *arena,
+                                                                uint8_t *__restrict__ changed) {
+    uint64_t t = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (t >= cnt) return;
+    uint64_t slot = K[t] >> 26;
+    if (t > 0 && (K[t - 1] >> 26) == slot) return;
+    uint8_t *p = arena + slot;
+    uint32_t R = uint32_t(*p) & 63u;
+    for (uint64_t u = t; u < cnt && (K[u] >> 26) == slot; u++) {
+        uint32_t rho = V[u] & 63u;
+        if (rho > R) {
+            changed[V[u] >> 6] = 1;
+            R = rho;
+        }
+    }
+    *p = uint8_t(R);
+}
+
+// Bloom add: the string length follows the largest probed bit = the last sorted key
+__global__ void k_len_from_last_key(const uint64_t *keys, uint64_t m, uint64_t *d_len) {
+    uint64_t need = (keys[m - 1] >> 35) + 1; // (idx >> 3) + 1 with idx = key >> 32
+    atomicMax((unsigned long long *)d_len, (unsigned long long)need);
+}
+
 // -------------------------------------------------------------- histogram
 // One 256-thread workgroup per key: 16 KiB of registers read as 4 x 16 B
 // per lane (coalesced), counted into per-wave LDS histograms.
@@ -205,7 +349,6 @@ __global__ void __launch_bounds__(256) k_bloom_probes(uint64_t n, const uint64_t
 __global__ void __launch_bounds__(256) k_bloom_apply(uint64_t m, const uint64_t *__restrict__ keys, uint8_t *bits,
                                                      uint64_t *d_len, int k, uint8_t *__restrict__ out) {
     uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-    uint64_t need = 0;
     if (i < m) {
         uint64_t key = keys[i];
         uint64_t idx = key >> 32;
@@ -216,15 +359,8 @@ __global__ void __launch_bounds__(256) k_bloom_apply(uint64_t m, const uint64_t 
             uint32_t pos = uint32_t(key & 0xffffffffu);
             uint32_t e = pos / uint32_t(k), j = pos - e * uint32_t(k);
             if (!(old & mask) && int(j) <= k - 2) out[e] = 1;
-            need = (idx >> 3) + 1;
         }
     }
-    // one atomicMax per wave for the string length
-    for (int s = 32; s > 0; s >>= 1) {
-        uint64_t o = __shfl_xor(need, s);
-        need = o > need ? o : need;
-    }
-    if ((threadIdx.x & 63) == 0 && need) atomicMax((unsigned long long *)d_len, (unsigned long long)need);
 }
 
 // ------------------------------------------------------------ bit strings
@@ -451,6 +587,40 @@ hipError_t launch_pfadd_apply(hipStream_t st, uint64_t n, const uint64_t *keys, 
     return hipSuccess;
 }
 
+
+hipError_t launch_pfadd_claim(hipStream_t st, uint64_t n, const uint32_t *key_ids, const uint64_t *off,
+                              const uint8_t *bytes, int v5, uint8_t *arena, uint64_t *rec) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k_pfadd_claim, dim3(grid_for(n, 256)), dim3(256), 0, st, n, key_ids, off, bytes, v5, arena,
+                       rec);
+    SK_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+hipError_t launch_pfadd_commit(hipStream_t st, uint64_t n, const uint64_t *rec, const uint32_t *cmd_of, uint8_t *arena,
+                               uint8_t *changed, uint64_t *conf_keys, uint32_t *conf_vals, uint32_t *conf_count,
+                               uint32_t conf_cap) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k_pfadd_commit, dim3(grid_for(n, 256)), dim3(256), 0, st, n, rec, cmd_of, arena, changed,
+                       conf_keys, conf_vals, conf_count, conf_cap);
+    SK_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_pfadd_conflicts, dim3(1), dim3(1024), 0, st, conf_keys, conf_vals, conf_count, arena,
+                       changed);
+    SK_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+hipError_t launch_pfadd_conflicts_sorted(hipStream_t st, uint64_t cnt, const uint64_t *K, const uint32_t *V,
+                                         uint8_t *arena, uint8_t *changed) {
+    if (!cnt) return hipSuccess;
+    hipLaunchKernelGGL(k_pfadd_conflicts_sorted, dim3(grid_for(cnt, 256)), dim3(256), 0, st, cnt, K, V, arena,
+                       changed);
+    SK_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+uint32_t pfadd_conflict_lds_capacity() { return SK_CONF_LDS; }
+
 hipError_t sort_keys_size(uint64_t n, unsigned begin_bit, unsigned end_bit, size_t *bytes) {
     size_t sz = 0;
     hipError_t e = rocprim::radix_sort_keys(nullptr, sz, (const uint64_t *)nullptr, (uint64_t *)nullptr, size_t(n),
@@ -528,6 +698,8 @@ hipError_t launch_bloom_apply(hipStream_t st, uint64_t m, const uint64_t *keys, 
                               uint8_t *out) {
     if (!m) return hipSuccess;
     hipLaunchKernelGGL(k_bloom_apply, dim3(grid_for(m, 256)), dim3(256), 0, st, m, keys, bits, d_len, k, out);
+    SK_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_len_from_last_key, dim3(1), dim3(1), 0, st, keys, m, d_len);
     SK_LAUNCH_CHECK();
     return hipSuccess;
 }

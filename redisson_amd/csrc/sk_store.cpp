@@ -255,9 +255,9 @@ int sync(sk_ctx *c) {
 }
 
 // phases timed by sk_prof_* (index = SK_PROF_* in the header)
-const char *kPhaseNames[] = {"pfadd_hash", "pfadd_sort", "pfadd_apply", "hll_hist",     "hll_union",
+const char *kPhaseNames[] = {"pfadd_hash",  "pfadd_sort",   "pfadd_apply", "hll_hist",     "hll_union",
                              "bloom_contains", "bloom_probes", "bloom_sort", "bloom_apply", "setbit",
-                             "getbit",     "bitcount",   "bitop"};
+                             "getbit",      "bitcount",     "bitop",       "pfadd_claim", "pfadd_commit"};
 constexpr int kNumPhases = sizeof(kPhaseNames) / sizeof(kPhaseNames[0]);
 
 hipEvent_t ev_get(sk_ctx *c) {
@@ -471,10 +471,13 @@ int del_key(sk_ctx *c, const std::string &k, bool *removed) {
 
 // ------------------------------------------------------------ PFADD core
 // Device batch: n elements with per-element slab id and command index.
-// hash -> stable radix sort on (slab, register) -> segment heads apply.
-int pfadd_device(sk_ctx *c, uint64_t n, const uint32_t *d_ids, const uint64_t *d_off, const uint8_t *d_bytes,
+// Two exact paths (same replies, same registers):
+//  * sparse (few elements per touched sketch, C2): claim / commit on the
+//    spare register bits, conflicts replayed in batch order (sk_kernels.hip);
+//  * dense (many elements per sketch, C1): hash -> stable radix sort on
+//    (slab, register) -> segment heads walk in batch order.
+int pfadd_sorted(sk_ctx *c, uint64_t n, const uint32_t *d_ids, const uint64_t *d_off, const uint8_t *d_bytes,
                  const uint32_t *d_cmd, uint64_t n_cmds, uint8_t *d_changed) {
-    if (!n) return SK_OK;
     unsigned id_bits = bits_for(c->hll_next ? c->hll_next - 1 : 0);
     unsigned cmd_bits = bits_for(n_cmds ? n_cmds - 1 : 0);
     if (6 + cmd_bits + 14 + id_bits > 64) return fail(c, SK_EINVAL, "PFADD batch too large for key packing");
@@ -494,6 +497,47 @@ int pfadd_device(sk_ctx *c, uint64_t n, const uint32_t *d_ids, const uint64_t *d
     { Prof p_(c, 2);
     HIPCHK(c, sk::launch_pfadd_apply(c->st, n, c->keys_b.as<uint64_t>(), slot_shift, cmd_mask, c->arena, d_changed)); }
     return SK_OK;
+}
+
+int pfadd_sparse(sk_ctx *c, uint64_t n, const uint32_t *d_ids, const uint64_t *d_off, const uint8_t *d_bytes,
+                 const uint32_t *d_cmd, uint8_t *d_changed) {
+    if (n >= (1ull << 26) || c->hll_next >= (1ull << 24)) return fail(c, SK_EINVAL, "PFADD batch too large");
+    HIPCHK(c, c->keys_a.ensure(n * 8)); // claim records
+    HIPCHK(c, c->keys_b.ensure(n * 8)); // conflict keys
+    HIPCHK(c, c->vals_a.ensure(n * 4)); // conflict values
+    uint32_t *d_cnt = reinterpret_cast<uint32_t *>(c->misc.as<uint8_t>() + 256);
+    HIPCHK(c, hipMemsetAsync(d_cnt, 0, 4, c->st));
+    { Prof p_(c, 13);
+    HIPCHK(c, sk::launch_pfadd_claim(c->st, n, d_ids, d_off, d_bytes, c->redis_major >= 5, c->arena,
+                                     c->keys_a.as<uint64_t>())); }
+    { Prof p_(c, 14);
+    HIPCHK(c, sk::launch_pfadd_commit(c->st, n, c->keys_a.as<uint64_t>(), d_cmd, c->arena, d_changed,
+                                      c->keys_b.as<uint64_t>(), c->vals_a.as<uint32_t>(), d_cnt, uint32_t(n))); }
+    uint32_t cnt = 0;
+    HIPCHK(c, hipMemcpyAsync(&cnt, d_cnt, 4, hipMemcpyDeviceToHost, c->st));
+    int r = sync(c);
+    if (r) return r;
+    if (cnt > sk::pfadd_conflict_lds_capacity()) { // long conflict list: rocPRIM sort + replay
+        HIPCHK(c, c->vals_b.ensure(uint64_t(cnt) * 4));
+        size_t tmp;
+        HIPCHK(c, sk::sort_pairs_size(cnt, 0, 64, &tmp));
+        HIPCHK(c, c->sort_tmp.ensure(tmp));
+        HIPCHK(c, sk::sort_pairs(c->st, c->sort_tmp.p, c->sort_tmp.cap, c->keys_b.as<uint64_t>(),
+                                 c->keys_a.as<uint64_t>(), c->vals_a.as<uint32_t>(), c->vals_b.as<uint32_t>(), cnt, 0,
+                                 64));
+        HIPCHK(c, sk::launch_pfadd_conflicts_sorted(c->st, cnt, c->keys_a.as<uint64_t>(), c->vals_b.as<uint32_t>(),
+                                                    c->arena, d_changed));
+    }
+    return SK_OK;
+}
+
+int pfadd_device(sk_ctx *c, uint64_t n, const uint32_t *d_ids, const uint64_t *d_off, const uint8_t *d_bytes,
+                 const uint32_t *d_cmd, uint64_t n_cmds, uint8_t *d_changed, uint64_t touched_keys) {
+    if (!n) return SK_OK;
+    // expected conflicting fraction ~ (n / touched) / 32768: sparse while it is small
+    if (touched_keys && n <= 2048 * touched_keys && n < (1ull << 26))
+        return pfadd_sparse(c, n, d_ids, d_off, d_bytes, d_cmd, d_changed);
+    return pfadd_sorted(c, n, d_ids, d_off, d_bytes, d_cmd, n_cmds, d_changed);
 }
 
 int hll_histograms(sk_ctx *c, uint64_t n, const uint32_t *d_ids, const uint8_t *base, std::vector<uint32_t> &h) {
@@ -807,8 +851,11 @@ int sk_pfadd(sk_ctx *c, uint32_t n_cmds, const uint64_t *key_off, const uint8_t 
             HIPCHK(c, hipMemcpyAsync(c->in_off.p, off2.data(), (m + 1) * 8, hipMemcpyHostToDevice, c->st));
             HIPCHK(c, hipMemcpyAsync(c->in_bytes.p, bytes2.data(), bytes2.size(), hipMemcpyHostToDevice, c->st));
             HIPCHK(c, hipMemsetAsync(c->out_u8.p, 0, c1 - c0, c->st));
+            std::vector<uint32_t> uniq(h_ids);
+            std::sort(uniq.begin(), uniq.end());
+            uint64_t touched = uint64_t(std::unique(uniq.begin(), uniq.end()) - uniq.begin());
             int r = pfadd_device(c, m, c->in_ids.as<uint32_t>(), c->in_off.as<uint64_t>(), c->in_bytes.as<uint8_t>(),
-                                 c->in_cmd.as<uint32_t>(), c1 - c0, c->out_u8.as<uint8_t>());
+                                 c->in_cmd.as<uint32_t>(), c1 - c0, c->out_u8.as<uint8_t>(), touched);
             if (r) return r;
             HIPCHK(c, hipMemcpyAsync(out_changed + c0, c->out_u8.p, c1 - c0, hipMemcpyDeviceToHost, c->st));
             r = sync(c);
@@ -832,7 +879,8 @@ int sk_pfadd_dev(sk_ctx *c, uint64_t n, const uint32_t *d_ids, const uint64_t *d
     uint64_t max_cmds = std::min<uint64_t>(c->max_batch, 1ull << std::min(32u, 64 - 20 - id_bits));
     for (uint64_t s = 0; s < n; s += max_cmds) {
         uint64_t m = std::min(max_cmds, n - s);
-        int r = pfadd_device(c, m, d_ids + s, d_off + s, d_bytes, nullptr, m, d_changed + s);
+        uint64_t live = c->hll_next - c->hll_free.size(); // slabs in use bounds the touched sketches
+        int r = pfadd_device(c, m, d_ids + s, d_off + s, d_bytes, nullptr, m, d_changed + s, live);
         if (r) return r;
     }
     return sync(c);

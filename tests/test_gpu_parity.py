@@ -22,7 +22,7 @@ def _ragged(rng, n, maxlen=200):
 
 
 # ------------------------------------------------------------------- PFADD
-@pytest.mark.parametrize("nkeys,n", [(1, 5000), (7, 20000), (300, 30000)])
+@pytest.mark.parametrize("nkeys,n", [(1, 5000), (7, 20000), (300, 30000), (100, 200000), (5, 10000)])
 def test_pfadd_registers_and_replies(engine, O, nkeys, n):
     rng = np.random.default_rng(nkeys)
     elems = _elems(0x5EED0000 + nkeys, n)

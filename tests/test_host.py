@@ -1,0 +1,131 @@
+"""CPU-only checks of the product: the C-ABI library loads and exports every
+symbol include/redisson_sketch.h declares; host-only entry points agree with
+the oracle; codec bytes; the Python API fails loudly without a GPU."""
+import os
+import re
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _header_symbols():
+    src = open(os.path.join(ROOT, "include", "redisson_sketch.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(sk_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_exports_every_header_symbol():
+    from redisson_amd import _native
+
+    lib = _native.load()
+    syms = _header_symbols()
+    assert len(syms) > 50
+    missing = [s for s in syms if not hasattr(lib, s)]
+    assert not missing, missing
+    # and the ctypes signature table covers exactly the header
+    assert sorted(_native.SIGNATURES) == syms
+
+
+def test_no_cpu_fallback_without_gpu():
+    from redisson_amd import DeviceUnavailable, SketchEngine
+    try:
+        import torch  # noqa: F401  (only to ask whether a GPU exists; never initialised here)
+    except ImportError:
+        pass
+    if os.path.exists("/dev/kfd") and os.environ.get("HIP_VISIBLE_DEVICES", "x") != "":
+        pytest.skip("a GPU may be present")
+    with pytest.raises(DeviceUnavailable):
+        SketchEngine(device=0)
+
+
+def test_calc_slot_and_crc16_match_oracle(O):
+    from redisson_amd import calc_slot, crc16, owner
+
+    rng = np.random.default_rng(0)
+    keys = ["tenant:%d:hll" % i for i in range(2000)] + ["{a}b", "a{b}c", "{}x", "x}y{z", "{{a}}", "", "é{ü}"]
+    for _ in range(500):
+        keys.append(rng.integers(32, 127, int(rng.integers(0, 30)), dtype=np.uint8).tobytes().decode())
+    for k in keys:
+        assert calc_slot(k) == O.calc_slot(k), k
+        b = k.encode()
+        assert crc16(b) == O.crc16(b)
+        s = O.calc_slot(k)
+        assert owner(k, 8) == (s % 8 if s >= 0 else -1)
+
+
+def test_bloom_sizing_matches_oracle(O):
+    from redisson_amd import bloom_optimal_bits, bloom_optimal_k
+
+    for n, p in [(100, 0.03), (550000000, 0.03), (425000000, 0.008), (55000000, 0.03), (1, 0.5), (10, 0.9),
+                 (1000, 1e-9), (7, 0.0), (123456789, 0.123)]:
+        m = bloom_optimal_bits(n, p)
+        assert m == O.bloom_optimal_bits(n, p)
+        if m > 0:
+            assert bloom_optimal_k(n, m) == O.bloom_optimal_k(n, m)
+
+
+def test_estimator_from_histogram_matches_oracle(O):
+    from redisson_amd import _native
+
+    lib = _native.load()
+    rng = np.random.default_rng(5)
+    for trial in range(200):
+        card = int(10 ** rng.uniform(0, 8))
+        # registers distributed like an HLL after `card` insertions (geometric rho)
+        hits = rng.integers(0, 16384, min(card, 400000))
+        regs = np.zeros(16384, dtype=np.uint8)
+        rho = np.minimum(rng.geometric(0.5, len(hits)), 39).astype(np.uint8)
+        np.maximum.at(regs, hits, rho)
+        h = O.hll_histogram(regs)
+        for major in (3, 5):
+            got = lib.sk_hll_estimate_hist(h.ctypes.data, major)
+            assert got == O.count_regs(regs, 1, major) == O.count_regs(regs, 0, major)
+
+
+def test_jackson_codec_bytes():
+    from redisson_amd import JInteger, JLong, JsonJacksonCodec, LongCodec, StringCodec
+
+    c = JsonJacksonCodec()
+    assert c.encode(JInteger(1)) == b"1"
+    assert c.encode(1) == b"1"
+    assert c.encode(JLong(123)) == b'["java.lang.Long",123]'
+    assert c.encode(1 << 40) == b'["java.lang.Long",1099511627776]'
+    assert c.encode("foo") == b'"foo"'
+    assert c.encode('a"b\\c\n\x01') == b'"a\\"b\\\\c\\n\\u0001"'
+    assert c.encode(True) == b"true"
+    assert c.encode(["hll", JLong(-5), "x"]) == b'["[Ljava.lang.Object;",["hll",["java.lang.Long",-5],"x"]]'
+    assert StringCodec().encode(12) == b"12"
+    assert LongCodec().encode(-7) == b"-7"
+
+
+def test_host_generator_matches_jackson_codec():
+    from redisson_amd import JLong, JsonJacksonCodec, gen_jackson_longs
+
+    off, buf = gen_jackson_longs(0x5EED0002, 1000)
+    # SplitMix64 reference (SURVEY 8d RNG)
+    st, M = 0x5EED0002, (1 << 64) - 1
+    c = JsonJacksonCodec()
+    for i in range(1000):
+        st = (st + 0x9E3779B97F4A7C15) & M
+        z = st
+        z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & M
+        z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & M
+        z ^= z >> 31
+        v = z - (1 << 64) if z >> 63 else z
+        assert buf[off[i]:off[i + 1]].tobytes() == c.encode(JLong(v))
+    lens = np.diff(off)
+    assert lens.min() >= 20 and lens.max() <= 39
+
+
+def test_bitset_java_conversions():
+    from redisson_amd.redisson import JBitSet, _from_byte_array_reverse, _int32, _to_byte_array_reverse
+
+    b = JBitSet([1, 10])
+    raw = _to_byte_array_reverse(b)
+    assert raw == bytes([0b01000000, 0b00100000])
+    assert str(_from_byte_array_reverse(raw)) == "{1, 10}"
+    assert _to_byte_array_reverse(JBitSet()) == b"\x00"           # bits.length()/8 + 1
+    assert _to_byte_array_reverse(JBitSet([7])) == b"\x01\x00"
+    assert _int32((1 << 29) * 8) == -(1 << 32) + (1 << 32) and _int32(0x1_0000_0000 // 4 * 8) == 0  # Q3 overflow

@@ -137,6 +137,7 @@ def main():
     eng.sync()
 
     # ------------------------------------------------------------ timed region
+    eng.set_async(True)          # one host sync per step (PFADD's conflict-count readback)
     eng.prof_reset()
     eng.prof_enable(True)
     barrier(pg)
@@ -150,6 +151,7 @@ def main():
     t1 = time.perf_counter()
     barrier(pg)
     eng.prof_enable(False)
+    eng.set_async(False)
     wall = allmax(pg, t1 - t0)
     dev_ms = eng.timer_elapsed_ms(0, 1)
     prof = {p: eng.prof_read(p) for p in PHASES}

@@ -184,6 +184,9 @@ int sk_dev_free(sk_ctx *ctx, void *p);
 int sk_h2d(sk_ctx *ctx, void *d_dst, const void *src, uint64_t n);
 int sk_d2h(sk_ctx *ctx, void *dst, const void *d_src, uint64_t n);
 int sk_dev_memset(sk_ctx *ctx, void *d_p, int value, uint64_t n);
+/* async mode: sk_pfadd_dev / sk_bloom_contains_dev / sk_bloom_add_dev return
+ * once enqueued (inputs must stay valid until sk_sync); default off */
+int sk_set_async(sk_ctx *ctx, int on);
 /* HIP events on the context stream: 16 slots; elapsed(a, b) waits for b */
 int sk_timer_record(sk_ctx *ctx, int slot);
 int sk_timer_elapsed(sk_ctx *ctx, int slot_a, int slot_b, float *ms);

@@ -91,6 +91,7 @@ SIGNATURES = {
     "sk_dev_memset": (c_int, [P, P, c_int, c_uint64]),
     "sk_timer_record": (c_int, [P, c_int]),
     "sk_timer_elapsed": (c_int, [P, c_int, c_int, P]),
+    "sk_set_async": (c_int, [P, c_int]),
     "sk_prof_enable": (c_int, [P, c_int]),
     "sk_prof_reset": (c_int, [P]),
     "sk_prof_read": (c_int, [P, c_char_p, P, P]),

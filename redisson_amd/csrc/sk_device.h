@@ -56,7 +56,72 @@ __device__ __forceinline__ uint64_t low_bytes(uint64_t v, unsigned nbytes) {
     return nbytes ? (v & (~0ull >> (64 - 8 * nbytes))) : 0ull;
 }
 
+// ------------------------------------------------------- key byte readers
+// Hash functions are written against a Reader: u64(p) = 8 little-endian
+// bytes starting at byte position p of the key.  GlobalReader reads HBM
+// directly (two aligned loads + funnel shift); LdsReader reads a workgroup's
+// key bytes that were staged into LDS with coalesced 16-byte loads
+// (stage_keys below), which turns ~len/8 scattered line requests per lane into
+// ~1 coalesced request per 16 bytes per workgroup.
+struct GlobalReader {
+    const uint8_t *base;
+    __device__ __forceinline__ uint64_t u64(uint32_t p) const { return ldu64(base + p); }
+};
+struct LdsReader {
+    const uint64_t *lds; // __shared__ words
+    uint32_t base;       // byte position of the key inside the staged window
+    __device__ __forceinline__ uint64_t u64(uint32_t p) const {
+        uint32_t a = base + p;
+        uint32_t q = a >> 3, sh = (a & 7u) * 8u;
+        return funnel(lds[q], lds[q + 1], sh);
+    }
+};
+
+// Stage bytes [lo, hi) of a global buffer into LDS words and zero the next
+// 16 B (readers look up to 15 B past a key's end, masked); returns the byte
+// position of `lo` inside the window (lo rounded down to 16 B).  Global reads
+// stay below hi + 16 (the buffers' padding contract).  All threads of the
+// workgroup must call it; ends with a barrier.
+__device__ __forceinline__ uint32_t stage_keys(const uint8_t *bytes, uint64_t lo, uint64_t hi, uint64_t *lds) {
+    uint64_t a0 = lo & ~uint64_t(15);
+    uint32_t nvec = uint32_t((hi - a0 + 15) >> 4);
+    const uint4 *src = reinterpret_cast<const uint4 *>(bytes + a0);
+    uint4 *dst = reinterpret_cast<uint4 *>(lds);
+    for (uint32_t v = threadIdx.x; v <= nvec; v += blockDim.x) dst[v] = v < nvec ? src[v] : make_uint4(0, 0, 0, 0);
+    __syncthreads();
+    return uint32_t(lo - a0);
+}
+// LDS window (u64 words) for one 256-element workgroup: room for keys of
+// mean length <= ~90 B; larger windows fall back to GlobalReader.
+#define SK_STAGE_WORDS 3072
+__device__ __forceinline__ bool stage_fits(uint64_t lo, uint64_t hi) {
+    return (hi - (lo & ~uint64_t(15))) + 32 <= uint64_t(SK_STAGE_WORDS) * 8;
+}
+
 // ---------------------------------------------------------------- Murmur
+template <class R> __device__ __forceinline__ uint64_t murmur64a_r(const R &rd, uint32_t len, uint64_t seed) {
+    const uint64_t m = 0xc6a4a7935bd1e995ull;
+    uint64_t h = seed ^ (uint64_t(len) * m);
+    uint32_t nb = len >> 3;
+    for (uint32_t i = 0; i < nb; i++) {
+        uint64_t k = rd.u64(8 * i);
+        k *= m;
+        k ^= k >> 47;
+        k *= m;
+        h ^= k;
+        h *= m;
+    }
+    unsigned tail = len & 7u;
+    if (tail) {
+        h ^= low_bytes(rd.u64(8 * nb), tail);
+        h *= m;
+    }
+    h ^= h >> 47;
+    h *= m;
+    h ^= h >> 47;
+    return h;
+}
+
 __device__ __forceinline__ uint64_t murmur64a(const uint8_t *data, uint32_t len, uint64_t seed) {
     const uint64_t m = 0xc6a4a7935bd1e995ull;
     uint64_t h = seed ^ (uint64_t(len) * m);
@@ -100,18 +165,18 @@ __device__ __forceinline__ uint64_t xmerge(uint64_t acc, uint64_t v) {
     return acc * SK_XP1 + SK_XP4;
 }
 
-__device__ __forceinline__ uint64_t xxh64(const uint8_t *p, uint32_t len) {
+template <class R> __device__ __forceinline__ uint64_t xxh64_r(const R &rd, uint32_t len) {
     const uint64_t seed = 0;
-    Stream s(p);
     uint64_t h;
-    uint32_t rem = len;
+    uint32_t pos = 0, rem = len;
     if (len >= 32) {
         uint64_t v1 = seed + SK_XP1 + SK_XP2, v2 = seed + SK_XP2, v3 = seed, v4 = seed - SK_XP1;
         do {
-            v1 = xround(v1, s.next());
-            v2 = xround(v2, s.next());
-            v3 = xround(v3, s.next());
-            v4 = xround(v4, s.next());
+            v1 = xround(v1, rd.u64(pos));
+            v2 = xround(v2, rd.u64(pos + 8));
+            v3 = xround(v3, rd.u64(pos + 16));
+            v4 = xround(v4, rd.u64(pos + 24));
+            pos += 32;
             rem -= 32;
         } while (rem >= 32);
         h = rotl(v1, 1) + rotl(v2, 7) + rotl(v3, 12) + rotl(v4, 18);
@@ -124,12 +189,13 @@ __device__ __forceinline__ uint64_t xxh64(const uint8_t *p, uint32_t len) {
     }
     h += len;
     while (rem >= 8) {
-        h ^= xround(0, s.next());
+        h ^= xround(0, rd.u64(pos));
         h = rotl(h, 27) * SK_XP1 + SK_XP4;
+        pos += 8;
         rem -= 8;
     }
     if (rem) {
-        uint64_t w = s.next(); // the last 1..7 bytes, low-aligned
+        uint64_t w = rd.u64(pos); // the last 1..7 bytes, low-aligned
         if (rem >= 4) {
             h ^= (w & 0xffffffffull) * SK_XP1;
             h = rotl(h, 23) * SK_XP2 + SK_XP3;
@@ -150,6 +216,7 @@ __device__ __forceinline__ uint64_t xxh64(const uint8_t *p, uint32_t len) {
     h ^= h >> 32;
     return h;
 }
+__device__ __forceinline__ uint64_t xxh64(const uint8_t *p, uint32_t len) { return xxh64_r(GlobalReader{p}, len); }
 
 // ---------------------------------------------------------------- FarmHash
 #define SK_K0 0xc3a5c85c97cb3127ull
@@ -167,8 +234,8 @@ __device__ __forceinline__ uint64_t hl16(uint64_t u, uint64_t v, uint64_t mul) {
 struct P2 {
     uint64_t first, second;
 };
-__device__ __forceinline__ P2 weak32(const uint8_t *s, uint64_t a, uint64_t b) {
-    uint64_t w = ldu64(s), x = ldu64(s + 8), y = ldu64(s + 16), z = ldu64(s + 24);
+template <class R> __device__ __forceinline__ P2 weak32(const R &rd, uint32_t s, uint64_t a, uint64_t b) {
+    uint64_t w = rd.u64(s), x = rd.u64(s + 8), y = rd.u64(s + 16), z = rd.u64(s + 24);
     a += w;
     b = rotr(b + a + z, 21);
     uint64_t c = a;
@@ -178,24 +245,25 @@ __device__ __forceinline__ P2 weak32(const uint8_t *s, uint64_t a, uint64_t b) {
     return P2{a + z, b + c};
 }
 
-__device__ __forceinline__ uint64_t farm_na_short(const uint8_t *s, uint32_t len) {
+template <class R> __device__ __forceinline__ uint64_t farm_na_short(const R &rd, uint32_t len) {
+    const uint32_t s = 0;
     // farmhashna::Hash64 for len <= 64
     if (len <= 16) {
         if (len >= 8) {
             uint64_t mul = SK_K2 + uint64_t(len) * 2;
-            uint64_t a = ldu64(s) + SK_K2;
-            uint64_t b = ldu64(s + len - 8);
+            uint64_t a = rd.u64(s) + SK_K2;
+            uint64_t b = rd.u64(s + len - 8);
             uint64_t c = rotr(b, 37) * mul + a;
             uint64_t d = (rotr(a, 25) + b) * mul;
             return hl16(c, d, mul);
         }
         if (len >= 4) {
             uint64_t mul = SK_K2 + uint64_t(len) * 2;
-            uint64_t a = ldu32(s);
-            return hl16(uint64_t(len) + (a << 3), ldu32(s + len - 4), mul);
+            uint64_t a = uint32_t(rd.u64(s));
+            return hl16(uint64_t(len) + (a << 3), uint32_t(rd.u64(s + len - 4)), mul);
         }
         if (len > 0) {
-            uint64_t w = ldu64(s);
+            uint64_t w = rd.u64(s);
             uint32_t a = uint32_t(w & 0xff), b = uint32_t((w >> (8 * (len >> 1))) & 0xff),
                      c = uint32_t((w >> (8 * (len - 1))) & 0xff);
             uint32_t y = a + (b << 8);
@@ -206,22 +274,22 @@ __device__ __forceinline__ uint64_t farm_na_short(const uint8_t *s, uint32_t len
     }
     uint64_t mul = SK_K2 + uint64_t(len) * 2;
     if (len <= 32) {
-        uint64_t a = ldu64(s) * SK_K1;
-        uint64_t b = ldu64(s + 8);
-        uint64_t c = ldu64(s + len - 8) * mul;
-        uint64_t d = ldu64(s + len - 16) * SK_K2;
+        uint64_t a = rd.u64(s) * SK_K1;
+        uint64_t b = rd.u64(s + 8);
+        uint64_t c = rd.u64(s + len - 8) * mul;
+        uint64_t d = rd.u64(s + len - 16) * SK_K2;
         return hl16(rotr(a + b, 43) + rotr(c, 30) + d, a + rotr(b + SK_K2, 18) + c, mul);
     }
-    uint64_t a = ldu64(s) * SK_K2;
-    uint64_t b = ldu64(s + 8);
-    uint64_t c = ldu64(s + len - 8) * mul;
-    uint64_t d = ldu64(s + len - 16) * SK_K2;
+    uint64_t a = rd.u64(s) * SK_K2;
+    uint64_t b = rd.u64(s + 8);
+    uint64_t c = rd.u64(s + len - 8) * mul;
+    uint64_t d = rd.u64(s + len - 16) * SK_K2;
     uint64_t y = rotr(a + b, 43) + rotr(c, 30) + d;
     uint64_t z = hl16(y, a + rotr(b + SK_K2, 18) + c, mul);
-    uint64_t e = ldu64(s + 16) * mul;
-    uint64_t f = ldu64(s + 24);
-    uint64_t g = (y + ldu64(s + len - 32)) * mul;
-    uint64_t h = (z + ldu64(s + len - 24)) * mul;
+    uint64_t e = rd.u64(s + 16) * mul;
+    uint64_t f = rd.u64(s + 24);
+    uint64_t g = (y + rd.u64(s + len - 32)) * mul;
+    uint64_t h = (z + rd.u64(s + len - 24)) * mul;
     return hl16(rotr(e + f, 43) + rotr(g, 30) + h, e + rotr(f + a, 18) + g, mul);
 }
 
@@ -233,7 +301,8 @@ __device__ __forceinline__ uint64_t uo_H(uint64_t x, uint64_t y, uint64_t mul, i
 }
 
 // farmhashuo::Hash64WithSeeds(s, len, 81, 0) for len > 64
-__device__ __noinline__ uint64_t farm_uo_long(const uint8_t *s, uint32_t len) {
+template <class R> __device__ __noinline__ uint64_t farm_uo_long(const R &rd, uint32_t len) {
+    uint32_t s = 0;
     const uint64_t seed0 = 81, seed1 = 0;
     uint64_t x = seed0;
     uint64_t y = seed1 * SK_K2 + 113;
@@ -243,10 +312,10 @@ __device__ __noinline__ uint64_t farm_uo_long(const uint8_t *s, uint32_t len) {
     x *= SK_K2;
     uint64_t mul = SK_K2 + (u & 0x82);
     uint32_t nblk = (len - 1) / 64;
-    const uint8_t *last64 = s + len - 64;
+    const uint32_t last64 = len - 64;
     for (uint32_t blk = 0; blk < nblk; blk++, s += 64) {
-        uint64_t a0 = ldu64(s), a1 = ldu64(s + 8), a2 = ldu64(s + 16), a3 = ldu64(s + 24);
-        uint64_t a4 = ldu64(s + 32), a5 = ldu64(s + 40), a6 = ldu64(s + 48), a7 = ldu64(s + 56);
+        uint64_t a0 = rd.u64(s), a1 = rd.u64(s + 8), a2 = rd.u64(s + 16), a3 = rd.u64(s + 24);
+        uint64_t a4 = rd.u64(s + 32), a5 = rd.u64(s + 40), a6 = rd.u64(s + 48), a7 = rd.u64(s + 56);
         x += a0 + a1;
         y += a2;
         z += a3;
@@ -294,19 +363,22 @@ __device__ __noinline__ uint64_t farm_uo_long(const uint8_t *s, uint32_t len) {
     w.first += ((len - 1) & 63);
     u += y;
     y += u;
-    x = rotr(y - x + v.first + ldu64(s + 8), 37) * mul;
-    y = rotr(y ^ v.second ^ ldu64(s + 48), 42) * mul;
+    x = rotr(y - x + v.first + rd.u64(s + 8), 37) * mul;
+    y = rotr(y ^ v.second ^ rd.u64(s + 48), 42) * mul;
     x ^= w.second * 9;
-    y += v.first + ldu64(s + 40);
+    y += v.first + rd.u64(s + 40);
     z = rotr(z + w.first, 33) * mul;
-    v = weak32(s, v.second * mul, x + w.first);
-    w = weak32(s + 32, z + w.second, y + ldu64(s + 16));
+    v = weak32(rd, s, v.second * mul, x + w.first);
+    w = weak32(rd, s + 32, z + w.second, y + rd.u64(s + 16));
     return uo_H(hl16(v.first + x, w.first ^ y, mul) + z - u, uo_H(v.second + w.second, x, mul, 30) ^ w.first,
                 mul, 31);
 }
 
+template <class R> __device__ __forceinline__ uint64_t farm_uo64_r(const R &rd, uint32_t len) {
+    return len <= 64 ? farm_na_short(rd, len) : farm_uo_long(rd, len);
+}
 __device__ __forceinline__ uint64_t farm_uo64(const uint8_t *s, uint32_t len) {
-    return len <= 64 ? farm_na_short(s, len) : farm_uo_long(s, len);
+    return farm_uo64_r(GlobalReader{s}, len);
 }
 
 // ---------------------------------------------------------------- misc

@@ -12,16 +12,22 @@ hipError_t launch_pfadd_hash(hipStream_t st, uint64_t n, const uint32_t *key_ids
 hipError_t launch_pfadd_apply(hipStream_t st, uint64_t n, const uint64_t *keys, unsigned slot_shift, uint64_t cmd_mask,
                               uint8_t *arena, uint8_t *changed);
 hipError_t launch_pfadd_claim(hipStream_t st, uint64_t n, const uint32_t *key_ids, const uint64_t *off,
-                              const uint8_t *bytes, int v5, uint8_t *arena, uint64_t *rec);
+                              const uint8_t *bytes, int v5, uint8_t *arena, uint64_t *rec, uint8_t *changed_i,
+                              uint32_t *conf_count);
+hipError_t launch_pfadd_conflicts(hipStream_t st, const uint64_t *conf_keys, const uint64_t *conf_vals,
+                                  const uint32_t *conf_count, uint8_t *arena, uint8_t *changed, uint32_t *host_count);
 hipError_t launch_pfadd_commit(hipStream_t st, uint64_t n, const uint64_t *rec, const uint32_t *cmd_of, uint8_t *arena,
-                               uint8_t *changed, uint64_t *conf_keys, uint32_t *conf_vals, uint32_t *conf_count,
+                               uint8_t *changed, uint64_t *conf_keys, uint64_t *conf_vals, uint32_t *conf_count,
                                uint32_t conf_cap);
-hipError_t launch_pfadd_conflicts_sorted(hipStream_t st, uint64_t cnt, const uint64_t *K, const uint32_t *V,
+hipError_t launch_pfadd_conflicts_sorted(hipStream_t st, uint64_t cnt, const uint64_t *K, const uint64_t *V,
                                          uint8_t *arena, uint8_t *changed);
 uint32_t pfadd_conflict_lds_capacity();
 hipError_t sort_keys_size(uint64_t n, unsigned begin_bit, unsigned end_bit, size_t *bytes);
 hipError_t sort_keys(hipStream_t st, void *tmp, size_t tmp_bytes, const uint64_t *in, uint64_t *out, uint64_t n,
                      unsigned begin_bit, unsigned end_bit);
+hipError_t sort_pairs64_size(uint64_t n, size_t *bytes);
+hipError_t sort_pairs64(hipStream_t st, void *tmp, size_t tmp_bytes, const uint64_t *kin, uint64_t *kout,
+                        const uint64_t *vin, uint64_t *vout, uint64_t n);
 hipError_t sort_pairs_size(uint64_t n, unsigned begin_bit, unsigned end_bit, size_t *bytes);
 hipError_t sort_pairs(hipStream_t st, void *tmp, size_t tmp_bytes, const uint64_t *kin, uint64_t *kout,
                       const uint32_t *vin, uint32_t *vout, uint64_t n, unsigned begin_bit, unsigned end_bit);

@@ -23,7 +23,7 @@
 
 namespace sk {
 
-static inline unsigned grid_for(uint64_t n, unsigned block, unsigned cap = 1u << 20) {
+static inline unsigned grid_for(uint64_t n, unsigned block, unsigned cap = 0x7fffffffu) {
     uint64_t g = (n + block - 1) / block;
     if (g == 0) g = 1;
     return g > cap ? cap : unsigned(g);
@@ -99,12 +99,21 @@ __global__ void __launch_bounds__(256) k_pfadd_apply(uint64_t n, const uint64_t 
 __global__ void __launch_bounds__(256) k_pfadd_claim(uint64_t n, const uint32_t *__restrict__ key_ids,
                                                      const uint64_t *__restrict__ off,
                                                      const uint8_t *__restrict__ bytes, int v5, uint8_t *arena,
-                                                     uint64_t *__restrict__ rec) {
-    uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+                                                     uint64_t *__restrict__ rec, uint8_t *__restrict__ changed_i,
+                                                     uint32_t *conf_count) {
+    __shared__ uint64_t lds[SK_STAGE_WORDS];
+    uint64_t e0 = uint64_t(blockIdx.x) * blockDim.x, e1 = e0 + blockDim.x < n ? e0 + blockDim.x : n;
+    uint64_t lo = off[e0], hi = off[e1];
+    bool staged = stage_fits(lo, hi); // uniform per workgroup
+    uint32_t wbase = staged ? stage_keys(bytes, lo, hi, lds) : 0u;
+    uint64_t i = e0 + threadIdx.x;
+    if (i == 0) *conf_count = 0; // consumed by k_pfadd_commit, which runs after this kernel
     if (i >= n) return;
+    if (changed_i) changed_i[i] = 0; // one element per command: replies start at 0
     uint64_t o = off[i];
     uint32_t len = uint32_t(off[i + 1] - o);
-    uint64_t h = murmur64a(bytes + o, len, 0xadc83b19ull);
+    uint64_t h = staged ? murmur64a_r(LdsReader{lds, wbase + uint32_t(o - lo)}, len, 0xadc83b19ull)
+                        : murmur64a(bytes + o, len, 0xadc83b19ull);
     uint32_t reg, rho;
     hll_pat(h, v5, &reg, &rho);
     uint64_t slot = (uint64_t(key_ids[i]) << 14) | reg;
@@ -123,7 +132,7 @@ __global__ void __launch_bounds__(256) k_pfadd_claim(uint64_t n, const uint32_t 
 __global__ void __launch_bounds__(256) k_pfadd_commit(uint64_t n, const uint64_t *__restrict__ rec,
                                                       const uint32_t *__restrict__ cmd_of, uint8_t *arena,
                                                       uint8_t *__restrict__ changed, uint64_t *conf_keys,
-                                                      uint32_t *conf_vals, uint32_t *conf_count, uint32_t conf_cap) {
+                                                      uint64_t *conf_vals, uint32_t *conf_count, uint32_t conf_cap) {
     uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
     if (i >= n) return;
     uint64_t r = rec[i];
@@ -140,82 +149,96 @@ __global__ void __launch_bounds__(256) k_pfadd_commit(uint64_t n, const uint64_t
     uint32_t k = atomicAdd(conf_count, 1u);
     if (k < conf_cap) {
         conf_keys[k] = (slot << 26) | i; // batch order inside a register
-        conf_vals[k] = (cmd << 6) | rho;
+        // R0: the value bits are untouched until the replay writes the register
+        conf_vals[k] = (uint64_t(cmd) << 16) | (uint64_t(*p & 63u) << 8) | rho;
     }
 }
 
-// One workgroup: bitonic sort of the conflict list in LDS by (slot, seq),
-// then each register's first entry replays its candidates in order.
-// Lists longer than the LDS capacity are left for the host (rocPRIM sort).
-#define SK_CONF_LDS 8192
-__global__ void __launch_bounds__(1024) k_pfadd_conflicts(const uint64_t *__restrict__ conf_keys,
-                                                          const uint32_t *__restrict__ conf_vals,
-                                                          const uint32_t *__restrict__ conf_count, uint8_t *arena,
-                                                          uint8_t *__restrict__ changed) {
-    __shared__ uint64_t K[SK_CONF_LDS];
-    __shared__ uint32_t V[SK_CONF_LDS];
+// Conflict replay.  Every conflict entry carries (slot, seq) as its key and
+// (cmd, R0, rho) as its value.  Entry t is raised iff its rho beats R0 and the
+// rho of every earlier (lower seq) entry of its register; the earliest entry
+// of a register writes max(R0, every rho) and so clears the flags.  One
+// 1024-thread workgroup loads up to SK_CONF_MAX entries into LDS and chains
+// them by register in an LDS hash table (atomicExch on bucket heads), so each
+// entry visits only the entries of its own register.  Longer lists are left
+// to the host (rocPRIM sort + k_pfadd_conflicts_sorted).
+#define SK_CONF_TPB 1024
+#define SK_CONF_MAX 4096
+#define SK_CONF_BUCKETS 4096
+__global__ void __launch_bounds__(SK_CONF_TPB) k_pfadd_conflicts(const uint64_t *__restrict__ conf_keys,
+                                                                 const uint64_t *__restrict__ conf_vals,
+                                                                 const uint32_t *__restrict__ conf_count,
+                                                                 uint8_t *arena, uint8_t *__restrict__ changed,
+                                                                 uint32_t *host_count) {
+    __shared__ uint64_t K[SK_CONF_MAX];
+    __shared__ uint64_t V[SK_CONF_MAX];
+    __shared__ uint32_t head[SK_CONF_BUCKETS];
+    __shared__ uint32_t nxt[SK_CONF_MAX];
     uint32_t cnt = *conf_count;
-    if (cnt == 0 || cnt > SK_CONF_LDS) return;
-    uint32_t P = 1;
-    while (P < cnt) P <<= 1;
-    for (uint32_t t = threadIdx.x; t < P; t += blockDim.x) {
-        K[t] = t < cnt ? conf_keys[t] : ~0ull;
-        V[t] = t < cnt ? conf_vals[t] : 0u;
+    if (threadIdx.x == 0) *host_count = cnt; // zero-copy: read after the stream sync
+    if (cnt == 0 || cnt > SK_CONF_MAX) return;
+    constexpr int PER = SK_CONF_MAX / SK_CONF_TPB;
+    uint64_t kr[PER], vr[PER];
+#pragma unroll
+    for (int q = 0; q < PER; q++) { // every global load issued before the LDS stores
+        uint32_t t = threadIdx.x + q * SK_CONF_TPB;
+        kr[q] = t < cnt ? conf_keys[t] : 0;
+        vr[q] = t < cnt ? conf_vals[t] : 0;
+    }
+    for (uint32_t b = threadIdx.x; b < SK_CONF_BUCKETS; b += SK_CONF_TPB) head[b] = 0xffffffffu;
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < PER; q++) {
+        uint32_t t = threadIdx.x + q * SK_CONF_TPB;
+        if (t < cnt) {
+            K[t] = kr[q];
+            V[t] = vr[q];
+            uint32_t bkt = uint32_t(((kr[q] >> 26) * 0x9E3779B97F4A7C15ull) >> 52);
+            nxt[t] = atomicExch(&head[bkt], t);
+        }
     }
     __syncthreads();
-    for (uint32_t kk = 2; kk <= P; kk <<= 1)
-        for (uint32_t j = kk >> 1; j > 0; j >>= 1) {
-            for (uint32_t t = threadIdx.x; t < P; t += blockDim.x) {
-                uint32_t x = t ^ j;
-                if (x > t) {
-                    bool up = (t & kk) == 0;
-                    uint64_t a = K[t], b = K[x];
-                    if ((a > b) == up) {
-                        K[t] = b;
-                        K[x] = a;
-                        uint32_t tv = V[t];
-                        V[t] = V[x];
-                        V[x] = tv;
-                    }
-                }
-            }
-            __syncthreads();
-        }
-    for (uint32_t t = threadIdx.x; t < cnt; t += blockDim.x) {
-        uint64_t slot = K[t] >> 26;
-        if (t > 0 && (K[t - 1] >> 26) == slot) continue;
-        uint8_t *p = arena + slot;
-        uint32_t R = uint32_t(*p) & 63u, R0 = R;
-        for (uint32_t u = t; u < cnt && (K[u] >> 26) == slot; u++) {
-            uint32_t rho = V[u] & 63u;
-            if (rho > R) {
-                changed[V[u] >> 6] = 1;
-                R = rho;
+#pragma unroll
+    for (int q = 0; q < PER; q++) {
+        uint32_t t = threadIdx.x + q * SK_CONF_TPB;
+        if (t >= cnt) continue;
+        uint64_t kt = kr[q], vt = vr[q];
+        uint64_t slot = kt >> 26;
+        uint32_t rho = uint32_t(vt & 63u), R0 = uint32_t(vt >> 8) & 63u;
+        uint32_t mx = rho, pm = 0, nearlier = 0;
+        uint32_t bkt = uint32_t((slot * 0x9E3779B97F4A7C15ull) >> 52);
+        for (uint32_t u = head[bkt]; u != 0xffffffffu; u = nxt[u]) {
+            uint64_t ku = K[u];
+            if ((ku >> 26) != slot) continue;
+            uint32_t ru = uint32_t(V[u] & 63u);
+            mx = ru > mx ? ru : mx;
+            if (ku < kt) {
+                nearlier++;
+                pm = ru > pm ? ru : pm;
             }
         }
-        (void)R0;
-        *p = uint8_t(R); // also clears the flags
+        if (rho > (R0 > pm ? R0 : pm)) changed[vt >> 16] = 1;
+        if (nearlier == 0) arena[slot] = uint8_t(R0 > mx ? R0 : mx);
     }
 }
 
 // host fallback for long conflict lists: same replay over a rocPRIM-sorted list
 __global__ void __launch_bounds__(256) k_pfadd_conflicts_sorted(uint64_t cnt, const uint64_t *__restrict__ K,
-                                                                const uint32_t *__restrict__ V, uint8_t *arena,
+                                                                const uint64_t *__restrict__ V, uint8_t *arena,
                                                                 uint8_t *__restrict__ changed) {
     uint64_t t = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
     if (t >= cnt) return;
     uint64_t slot = K[t] >> 26;
     if (t > 0 && (K[t - 1] >> 26) == slot) return;
-    uint8_t *p = arena + slot;
-    uint32_t R = uint32_t(*p) & 63u;
+    uint32_t R = uint32_t(V[t] >> 8) & 63u; // R0
     for (uint64_t u = t; u < cnt && (K[u] >> 26) == slot; u++) {
-        uint32_t rho = V[u] & 63u;
+        uint32_t rho = uint32_t(V[u] & 63u);
         if (rho > R) {
-            changed[V[u] >> 6] = 1;
+            changed[V[u] >> 16] = 1;
             R = rho;
         }
     }
-    *p = uint8_t(R);
+    arena[slot] = uint8_t(R);
 }
 
 // Bloom add: the string length follows the largest probed bit = the last sorted key
@@ -305,12 +328,23 @@ __global__ void __launch_bounds__(256) k_bloom_contains(uint64_t n, const uint64
                                                         const uint8_t *__restrict__ bits,
                                                         const uint64_t *__restrict__ d_len, uint64_t size,
                                                         uint64_t magic, int k, uint8_t *__restrict__ out) {
-    uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    __shared__ uint64_t lds[SK_STAGE_WORDS];
+    uint64_t e0 = uint64_t(blockIdx.x) * blockDim.x, e1 = e0 + blockDim.x < n ? e0 + blockDim.x : n;
+    uint64_t lo = off[e0], hi = off[e1];
+    bool staged = stage_fits(lo, hi);
+    uint32_t wbase = staged ? stage_keys(bytes, lo, hi, lds) : 0u;
+    uint64_t i = e0 + threadIdx.x;
     if (i >= n) return;
     uint64_t o = off[i];
     uint32_t len = uint32_t(off[i + 1] - o);
     uint64_t h1, h2;
-    bloom_hashes(bytes + o, len, &h1, &h2);
+    if (staged) {
+        LdsReader rd{lds, wbase + uint32_t(o - lo)};
+        h1 = xxh64_r(rd, len);
+        h2 = farm_uo64_r(rd, len);
+    } else {
+        bloom_hashes(bytes + o, len, &h1, &h2);
+    }
     uint64_t slen = *d_len;
     uint64_t h = h1;
     uint8_t r = 1;
@@ -329,12 +363,23 @@ __global__ void __launch_bounds__(256) k_bloom_contains(uint64_t n, const uint64
 __global__ void __launch_bounds__(256) k_bloom_probes(uint64_t n, const uint64_t *__restrict__ off,
                                                       const uint8_t *__restrict__ bytes, uint64_t size,
                                                       uint64_t magic, int k, uint64_t *__restrict__ keys) {
-    uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    __shared__ uint64_t lds[SK_STAGE_WORDS];
+    uint64_t e0 = uint64_t(blockIdx.x) * blockDim.x, e1 = e0 + blockDim.x < n ? e0 + blockDim.x : n;
+    uint64_t lo = off[e0], hi = off[e1];
+    bool staged = stage_fits(lo, hi);
+    uint32_t wbase = staged ? stage_keys(bytes, lo, hi, lds) : 0u;
+    uint64_t i = e0 + threadIdx.x;
     if (i >= n) return;
     uint64_t o = off[i];
     uint32_t len = uint32_t(off[i + 1] - o);
     uint64_t h1, h2;
-    bloom_hashes(bytes + o, len, &h1, &h2);
+    if (staged) {
+        LdsReader rd{lds, wbase + uint32_t(o - lo)};
+        h1 = xxh64_r(rd, len);
+        h2 = farm_uo64_r(rd, len);
+    } else {
+        bloom_hashes(bytes + o, len, &h1, &h2);
+    }
     uint64_t h = h1;
     uint64_t pos = i * uint64_t(k);
     for (int j = 0; j < k; j++) {
@@ -589,28 +634,34 @@ hipError_t launch_pfadd_apply(hipStream_t st, uint64_t n, const uint64_t *keys, 
 
 
 hipError_t launch_pfadd_claim(hipStream_t st, uint64_t n, const uint32_t *key_ids, const uint64_t *off,
-                              const uint8_t *bytes, int v5, uint8_t *arena, uint64_t *rec) {
+                              const uint8_t *bytes, int v5, uint8_t *arena, uint64_t *rec, uint8_t *changed_i,
+                              uint32_t *conf_count) {
     if (!n) return hipSuccess;
     hipLaunchKernelGGL(k_pfadd_claim, dim3(grid_for(n, 256)), dim3(256), 0, st, n, key_ids, off, bytes, v5, arena,
-                       rec);
+                       rec, changed_i, conf_count);
     SK_LAUNCH_CHECK();
     return hipSuccess;
 }
 
 hipError_t launch_pfadd_commit(hipStream_t st, uint64_t n, const uint64_t *rec, const uint32_t *cmd_of, uint8_t *arena,
-                               uint8_t *changed, uint64_t *conf_keys, uint32_t *conf_vals, uint32_t *conf_count,
+                               uint8_t *changed, uint64_t *conf_keys, uint64_t *conf_vals, uint32_t *conf_count,
                                uint32_t conf_cap) {
     if (!n) return hipSuccess;
     hipLaunchKernelGGL(k_pfadd_commit, dim3(grid_for(n, 256)), dim3(256), 0, st, n, rec, cmd_of, arena, changed,
                        conf_keys, conf_vals, conf_count, conf_cap);
     SK_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_pfadd_conflicts, dim3(1), dim3(1024), 0, st, conf_keys, conf_vals, conf_count, arena,
-                       changed);
+    return hipSuccess;
+}
+
+hipError_t launch_pfadd_conflicts(hipStream_t st, const uint64_t *conf_keys, const uint64_t *conf_vals,
+                                  const uint32_t *conf_count, uint8_t *arena, uint8_t *changed, uint32_t *host_count) {
+    hipLaunchKernelGGL(k_pfadd_conflicts, dim3(1), dim3(SK_CONF_TPB), 0, st, conf_keys, conf_vals, conf_count, arena,
+                       changed, host_count);
     SK_LAUNCH_CHECK();
     return hipSuccess;
 }
 
-hipError_t launch_pfadd_conflicts_sorted(hipStream_t st, uint64_t cnt, const uint64_t *K, const uint32_t *V,
+hipError_t launch_pfadd_conflicts_sorted(hipStream_t st, uint64_t cnt, const uint64_t *K, const uint64_t *V,
                                          uint8_t *arena, uint8_t *changed) {
     if (!cnt) return hipSuccess;
     hipLaunchKernelGGL(k_pfadd_conflicts_sorted, dim3(grid_for(cnt, 256)), dim3(256), 0, st, cnt, K, V, arena,
@@ -619,7 +670,7 @@ hipError_t launch_pfadd_conflicts_sorted(hipStream_t st, uint64_t cnt, const uin
     return hipSuccess;
 }
 
-uint32_t pfadd_conflict_lds_capacity() { return SK_CONF_LDS; }
+uint32_t pfadd_conflict_lds_capacity() { return SK_CONF_MAX; }
 
 hipError_t sort_keys_size(uint64_t n, unsigned begin_bit, unsigned end_bit, size_t *bytes) {
     size_t sz = 0;
@@ -650,6 +701,21 @@ hipError_t sort_pairs(hipStream_t st, void *tmp, size_t tmp_bytes, const uint64_
     if (!n) return hipSuccess;
     size_t sz = tmp_bytes;
     return rocprim::radix_sort_pairs(tmp, sz, kin, kout, vin, vout, size_t(n), begin_bit, end_bit, st);
+}
+
+hipError_t sort_pairs64_size(uint64_t n, size_t *bytes) {
+    size_t sz = 0;
+    hipError_t e = rocprim::radix_sort_pairs(nullptr, sz, (const uint64_t *)nullptr, (uint64_t *)nullptr,
+                                             (const uint64_t *)nullptr, (uint64_t *)nullptr, size_t(n), 0, 64);
+    *bytes = sz;
+    return e;
+}
+
+hipError_t sort_pairs64(hipStream_t st, void *tmp, size_t tmp_bytes, const uint64_t *kin, uint64_t *kout,
+                        const uint64_t *vin, uint64_t *vout, uint64_t n) {
+    if (!n) return hipSuccess;
+    size_t sz = tmp_bytes;
+    return rocprim::radix_sort_pairs(tmp, sz, kin, kout, vin, vout, size_t(n), 0, 64, st);
 }
 
 hipError_t launch_hll_hist(hipStream_t st, uint64_t n, const uint32_t *ids, const uint8_t *arena, uint32_t *hist) {

@@ -214,6 +214,10 @@ struct sk_ctx {
     // cross-GPU exchange (RCCL over xGMI)
     ncclComm_t comm = nullptr;
 
+    bool async_dev = false;     // sk_set_async: _dev calls return without a final sync
+    uint32_t *h_cnt = nullptr;  // pinned, device-mapped word: conflict count written by the kernel
+    uint32_t *d_h_cnt = nullptr;
+
     // workspace
     uint32_t *d_zero = nullptr; // device u32[4] zeros: id 0 / empty length
     DBuf keys_a, keys_b, vals_a, vals_b, sort_tmp, in_off, in_bytes, in_ids, in_cmd, out_u8, misc, partial, hist,
@@ -504,28 +508,28 @@ int pfadd_sparse(sk_ctx *c, uint64_t n, const uint32_t *d_ids, const uint64_t *d
     if (n >= (1ull << 26) || c->hll_next >= (1ull << 24)) return fail(c, SK_EINVAL, "PFADD batch too large");
     HIPCHK(c, c->keys_a.ensure(n * 8)); // claim records
     HIPCHK(c, c->keys_b.ensure(n * 8)); // conflict keys
-    HIPCHK(c, c->vals_a.ensure(n * 4)); // conflict values
+    HIPCHK(c, c->vals_a.ensure(n * 8)); // conflict values (cmd, R0, rho)
     uint32_t *d_cnt = reinterpret_cast<uint32_t *>(c->misc.as<uint8_t>() + 256);
-    HIPCHK(c, hipMemsetAsync(d_cnt, 0, 4, c->st));
     { Prof p_(c, 13);
+    // one element per command (d_cmd == null): the claim pass also zeroes the replies
     HIPCHK(c, sk::launch_pfadd_claim(c->st, n, d_ids, d_off, d_bytes, c->redis_major >= 5, c->arena,
-                                     c->keys_a.as<uint64_t>())); }
+                                     c->keys_a.as<uint64_t>(), d_cmd ? nullptr : d_changed, d_cnt)); }
     { Prof p_(c, 14);
     HIPCHK(c, sk::launch_pfadd_commit(c->st, n, c->keys_a.as<uint64_t>(), d_cmd, c->arena, d_changed,
-                                      c->keys_b.as<uint64_t>(), c->vals_a.as<uint32_t>(), d_cnt, uint32_t(n))); }
-    uint32_t cnt = 0;
-    HIPCHK(c, hipMemcpyAsync(&cnt, d_cnt, 4, hipMemcpyDeviceToHost, c->st));
-    int r = sync(c);
+                                      c->keys_b.as<uint64_t>(), c->vals_a.as<uint64_t>(), d_cnt, uint32_t(n)));
+    HIPCHK(c, sk::launch_pfadd_conflicts(c->st, c->keys_b.as<uint64_t>(), c->vals_a.as<uint64_t>(), d_cnt, c->arena,
+                                         d_changed, c->d_h_cnt)); }
+    int r = sync(c); // the conflict count decides whether the long-list path is needed
     if (r) return r;
+    uint32_t cnt = *c->h_cnt;
     if (cnt > sk::pfadd_conflict_lds_capacity()) { // long conflict list: rocPRIM sort + replay
-        HIPCHK(c, c->vals_b.ensure(uint64_t(cnt) * 4));
+        HIPCHK(c, c->vals_b.ensure(uint64_t(cnt) * 8));
         size_t tmp;
-        HIPCHK(c, sk::sort_pairs_size(cnt, 0, 64, &tmp));
+        HIPCHK(c, sk::sort_pairs64_size(cnt, &tmp));
         HIPCHK(c, c->sort_tmp.ensure(tmp));
-        HIPCHK(c, sk::sort_pairs(c->st, c->sort_tmp.p, c->sort_tmp.cap, c->keys_b.as<uint64_t>(),
-                                 c->keys_a.as<uint64_t>(), c->vals_a.as<uint32_t>(), c->vals_b.as<uint32_t>(), cnt, 0,
-                                 64));
-        HIPCHK(c, sk::launch_pfadd_conflicts_sorted(c->st, cnt, c->keys_a.as<uint64_t>(), c->vals_b.as<uint32_t>(),
+        HIPCHK(c, sk::sort_pairs64(c->st, c->sort_tmp.p, c->sort_tmp.cap, c->keys_b.as<uint64_t>(),
+                                   c->keys_a.as<uint64_t>(), c->vals_a.as<uint64_t>(), c->vals_b.as<uint64_t>(), cnt));
+        HIPCHK(c, sk::launch_pfadd_conflicts_sorted(c->st, cnt, c->keys_a.as<uint64_t>(), c->vals_b.as<uint64_t>(),
                                                     c->arena, d_changed));
     }
     return SK_OK;
@@ -641,6 +645,8 @@ int sk_open(const sk_config *cfg, sk_ctx **out) {
     uint64_t cap = (cfg && cfg->hll_capacity) ? cfg->hll_capacity : 1024;
     if (hll_grow(c, cap) != SK_OK || c->misc.ensure(4096) != hipSuccess ||
         hipMalloc(&c->d_zero, 16) != hipSuccess || hipMemsetAsync(c->d_zero, 0, 16, c->st) != hipSuccess ||
+        hipHostMalloc((void **)&c->h_cnt, 64, hipHostMallocMapped) != hipSuccess ||
+        hipHostGetDevicePointer((void **)&c->d_h_cnt, c->h_cnt, 0) != hipSuccess ||
         hipMemsetAsync(c->misc.p, 0, 4096, c->st) != hipSuccess || hipStreamSynchronize(c->st) != hipSuccess) {
         sk_close(c);
         return SK_EDEVICE;
@@ -663,6 +669,7 @@ int sk_close(sk_ctx *c) {
     if (c->arena) (void)hipFree(c->arena);
     if (c->d_dir) (void)hipFree(c->d_dir);
     if (c->d_zero) (void)hipFree(c->d_zero);
+    if (c->h_cnt) (void)hipHostFree(c->h_cnt);
     for (DBuf *b : {&c->keys_a, &c->keys_b, &c->vals_a, &c->vals_b, &c->sort_tmp, &c->in_off, &c->in_bytes,
                     &c->in_ids, &c->in_cmd, &c->out_u8, &c->misc, &c->partial, &c->hist, &c->uni, &c->ptrs})
         b->release();
@@ -874,16 +881,17 @@ int sk_pfadd_dev(sk_ctx *c, uint64_t n, const uint32_t *d_ids, const uint64_t *d
     std::lock_guard<std::mutex> g(c->mu);
     HIPCHK(c, hipSetDevice(c->device));
     if (!n) return SK_OK;
-    HIPCHK(c, hipMemsetAsync(d_changed, 0, n, c->st));
     unsigned id_bits = bits_for(c->hll_next ? c->hll_next - 1 : 0);
     uint64_t max_cmds = std::min<uint64_t>(c->max_batch, 1ull << std::min(32u, 64 - 20 - id_bits));
     for (uint64_t s = 0; s < n; s += max_cmds) {
         uint64_t m = std::min(max_cmds, n - s);
         uint64_t live = c->hll_next - c->hll_free.size(); // slabs in use bounds the touched sketches
+        if (!(live && m <= 2048 * live && m < (1ull << 26)))
+            HIPCHK(c, hipMemsetAsync(d_changed + s, 0, m, c->st)); // sorted path sets only the 1s
         int r = pfadd_device(c, m, d_ids + s, d_off + s, d_bytes, nullptr, m, d_changed + s, live);
         if (r) return r;
     }
-    return sync(c);
+    return c->async_dev ? SK_OK : sync(c);
 }
 
 // --------------------------------------------------------------- PFCOUNT
@@ -1539,7 +1547,7 @@ int sk_bloom_add_dev(sk_ctx *c, const uint8_t *name, uint64_t len, uint64_t n, c
     uint32_t id;
     if ((r = bloom_prepare(c, nm, b->size, b->k, true, &id))) return r;
     if ((r = bloom_add_device(c, id, b->size, b->k, n, d_off, d_bytes, d_out))) return r;
-    return sync(c);
+    return c->async_dev ? SK_OK : sync(c);
 }
 
 int sk_bloom_contains_dev(sk_ctx *c, const uint8_t *name, uint64_t len, uint64_t n, const uint64_t *d_off,
@@ -1558,7 +1566,7 @@ int sk_bloom_contains_dev(sk_ctx *c, const uint8_t *name, uint64_t len, uint64_t
     { Prof p_(c, 5);
     HIPCHK(c, sk::launch_bloom_contains(c->st, n, d_off, d_bytes, bits, dl, uint64_t(b->size),
                                         magic_for(uint64_t(b->size)), b->k, d_out)); }
-    return sync(c);
+    return c->async_dev ? SK_OK : sync(c);
 }
 
 int sk_bloom_count(sk_ctx *c, const uint8_t *name, uint64_t len, int32_t *out) {
@@ -1638,6 +1646,12 @@ int sk_timer_elapsed(sk_ctx *c, int a, int b, float *ms) {
         return fail(c, SK_EINVAL, "timer slot");
     HIPCHK(c, hipEventSynchronize(c->timers[b]));
     HIPCHK(c, hipEventElapsedTime(ms, c->timers[a], c->timers[b]));
+    return SK_OK;
+}
+
+int sk_set_async(sk_ctx *c, int on) {
+    std::lock_guard<std::mutex> g(c->mu);
+    c->async_dev = on != 0;
     return SK_OK;
 }
 

@@ -168,6 +168,9 @@ class SketchEngine:
         self._check(self.lib.sk_timer_elapsed(self.ctx, a, b, ctypes.addressof(ms)))
         return ms.value
 
+    def set_async(self, on: bool = True):
+        self._check(self.lib.sk_set_async(self.ctx, int(on)))
+
     def prof_enable(self, on: bool = True):
         self._check(self.lib.sk_prof_enable(self.ctx, int(on)))
 

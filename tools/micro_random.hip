@@ -47,6 +47,29 @@ __global__ void k_atomic_or_ret(uint32_t *t, uint64_t words, uint64_t n, uint32_
     uint32_t o = atomicOr(&t[mix(seed + i) % words], 1u << (i & 31));
     if (o == 0xdeadbeef) out[0] = o;
 }
+__global__ void k_load_nt(const uint8_t *t, uint64_t bytes, uint64_t n, int per, uint32_t *out, uint64_t seed) {
+    uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint32_t acc = 0;
+    for (int j = 0; j < per; j++) acc += __builtin_nontemporal_load(t + mix(seed + i * per + j) % bytes);
+    if (acc == 0xffffffff) out[0] = acc;
+}
+__global__ void k_load16(const uint4 *t, uint64_t n16, uint64_t n, int per, uint32_t *out, uint64_t seed) {
+    uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint32_t acc = 0;
+    for (int j = 0; j < per; j++) { uint4 v = t[mix(seed + i * per + j) % n16]; acc += v.x ^ v.w; }
+    if (acc == 0xffffffff) out[0] = acc;
+}
+// each lane's 6 probes land in one 4 KiB page (what a page-blocked layout would give)
+__global__ void k_load_page(const uint8_t *t, uint64_t bytes, uint64_t n, int per, uint32_t *out, uint64_t seed) {
+    uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint64_t base = (mix(seed + i) % (bytes >> 12)) << 12;
+    uint32_t acc = 0;
+    for (int j = 0; j < per; j++) acc += t[base + (mix(seed + i * per + j) & 4095)];
+    if (acc == 0xffffffff) out[0] = acc;
+}
 __global__ void k_stream(const uint4 *a, uint64_t n, uint4 *b) {
     uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
     if (i < n) b[i] = a[i];
@@ -98,6 +121,22 @@ int main() {
         timeit(nm, [&] { k_atomic_or_ret<<<g, 256>>>((uint32_t *)t, big / 4, n, o, 7); }, n, "atom");
         snprintf(nm, sizeof nm, "atomicOr u32 ret rand 32MB n=%llu", (unsigned long long)n);
         timeit(nm, [&] { k_atomic_or_ret<<<g, 256>>>((uint32_t *)t, (32ull << 20) / 4, n, o, 8); }, n, "atom");
+    }
+    {
+        uint64_t n = 1ull << 22;
+        unsigned g = unsigned((n + 255) / 256);
+        for (uint64_t tb : {2ull << 20, 16ull << 20, 64ull << 20}) {
+            char nm[128];
+            snprintf(nm, sizeof nm, "load 1B x6 rand %lluMB (indep) n=4M", (unsigned long long)(tb >> 20));
+            timeit(nm, [&] { k_load<<<g, 256>>>(t, tb, n, 6, o, 2); }, 6.0 * n, "load");
+            snprintf(nm, sizeof nm, "atomicOr ret rand %lluMB n=4M", (unsigned long long)(tb >> 20));
+            timeit(nm, [&] { k_atomic_or_ret<<<g, 256>>>((uint32_t *)t, tb / 4, n, o, 9); }, n, "atom");
+        }
+        timeit("load 1B x6 nontemporal 534MB n=4M", [&] { k_load_nt<<<g, 256>>>(t, bloom, n, 6, o, 2); }, 6.0 * n, "load");
+        timeit("load 16B x6 rand 534MB n=4M", [&] { k_load16<<<g, 256>>>((const uint4 *)t, bloom / 16, n, 6, o, 2); }, 6.0 * n, "load");
+        timeit("load 1B x6 same-4KiB-page 534MB n=4M", [&] { k_load_page<<<g, 256>>>(t, bloom, n, 6, o, 2); }, 6.0 * n, "load");
+        timeit("load 1B x6 rand 534MB n=4M block=64", [&] { k_load<<<unsigned(n / 64), 64>>>(t, bloom, n, 6, o, 2); }, 6.0 * n, "load");
+        timeit("load 1B x6 rand 534MB n=4M block=1024", [&] { k_load<<<unsigned(n / 1024), 1024>>>(t, bloom, n, 6, o, 2); }, 6.0 * n, "load");
     }
     uint64_t nv = (512ull << 20) / 16;
     timeit("stream copy 512MB (read+write GB/s)", [&] { k_stream<<<unsigned(nv / 256), 256>>>((uint4 *)t, nv, (uint4 *)(t + (768ull << 20))); }, 1024.0 * (1 << 20), "B");

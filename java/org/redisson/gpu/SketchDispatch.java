@@ -1,0 +1,117 @@
+/*
+ * SketchDispatch -- turns (RedisCommand, params) into C-ABI calls, one command
+ * at a time (GpuSketchCommandService) or as same-kind runs of an RBatch
+ * (GpuSketchBatchService).  Replies are the raw redis replies (Long / byte[] /
+ * "OK"), so the command's own convertor produces what Redisson returns.
+ * Source only here; see INTEGRATION.md.
+ */
+package org.redisson.gpu;
+
+import java.io.ByteArrayOutputStream;
+import java.util.List;
+
+import org.redisson.client.RedisException;
+import org.redisson.client.codec.Codec;
+import org.redisson.client.protocol.RedisCommand;
+
+final class SketchDispatch {
+    private SketchDispatch() {
+    }
+
+    static final class Packed {
+        final long[] off;
+        final byte[] bytes;
+
+        Packed(List<byte[]> items) {
+            off = new long[items.size() + 1];
+            ByteArrayOutputStream out = new ByteArrayOutputStream();
+            for (int i = 0; i < items.size(); i++) {
+                off[i] = out.size();
+                out.write(items.get(i), 0, items.get(i).length);
+            }
+            off[items.size()] = out.size();
+            out.write(new byte[16], 0, 16); // device padding contract
+            bytes = out.toByteArray();
+        }
+    }
+
+    static void check(long ctx, int st) {
+        if (st == SketchNative.SK_OK) {
+            return;
+        }
+        if (st == SketchNative.SK_ENOTINIT) {
+            throw new IllegalStateException(SketchNative.lastError(ctx));
+        }
+        if (st == SketchNative.SK_ETOOBIG) {
+            throw new IllegalArgumentException(SketchNative.lastError(ctx));
+        }
+        throw new RedisException(SketchNative.lastError(ctx));
+    }
+
+    static Object single(long ctx, Codec codec, RedisCommand<?> command, Object[] params) {
+        try {
+            String name = command.getName();
+            byte[] key = GpuSketchCommandService.encodeParam(codec, command, params[0], 1);
+            if ("PFADD".equals(name)) {
+                java.util.ArrayList<byte[]> elems = new java.util.ArrayList<byte[]>();
+                for (int i = 1; i < params.length; i++) {
+                    elems.add(GpuSketchCommandService.encodeParam(codec, command, params[i], i + 1));
+                }
+                Packed k = new Packed(java.util.Collections.singletonList(key));
+                Packed e = new Packed(elems);
+                byte[] out = new byte[1];
+                check(ctx, SketchNative.pfadd(ctx, k.off, k.bytes, new int[] {elems.size()}, e.off, e.bytes, out));
+                return Long.valueOf(out[0]);
+            }
+            if ("PFCOUNT".equals(name)) {
+                java.util.ArrayList<byte[]> keys = new java.util.ArrayList<byte[]>();
+                for (Object p : params) {
+                    keys.add(p.toString().getBytes(GpuSketchCommandService.UTF8));
+                }
+                Packed k = new Packed(keys);
+                long[] out = new long[1];
+                check(ctx, SketchNative.pfcount(ctx, new int[] {keys.size()}, k.off, k.bytes, out));
+                return Long.valueOf(out[0]);
+            }
+            if ("GETBIT".equals(name) || "SETBIT".equals(name)) {
+                Packed k = new Packed(java.util.Collections.singletonList(key));
+                long[] offs = {Long.parseLong(params[1].toString())};
+                byte[] out = new byte[1];
+                if ("GETBIT".equals(name)) {
+                    check(ctx, SketchNative.getbit(ctx, k.off, k.bytes, offs, out));
+                } else {
+                    byte[] vals = {(byte) Integer.parseInt(params[2].toString())};
+                    check(ctx, SketchNative.setbit(ctx, k.off, k.bytes, offs, vals, out));
+                }
+                return Long.valueOf(out[0]);
+            }
+            if ("BITCOUNT".equals(name) || "STRLEN".equals(name)) {
+                long[] out = new long[1];
+                check(ctx, "BITCOUNT".equals(name) ? SketchNative.bitcount(ctx, key, out)
+                        : SketchNative.strlen(ctx, key, out));
+                return Long.valueOf(out[0]);
+            }
+            // PFMERGE dest srcs... / BITOP op dest srcs...
+            boolean bitop = "BITOP".equals(name);
+            int first = bitop ? 2 : 1;
+            java.util.ArrayList<byte[]> srcs = new java.util.ArrayList<byte[]>();
+            for (int i = first; i < params.length; i++) {
+                srcs.add(params[i].toString().getBytes(GpuSketchCommandService.UTF8));
+            }
+            Packed s = new Packed(srcs);
+            if (bitop) {
+                int op = java.util.Arrays.asList("AND", "OR", "XOR", "NOT").indexOf(params[0].toString());
+                long[] len = new long[1];
+                check(ctx, SketchNative.bitop(ctx, op, params[1].toString().getBytes(GpuSketchCommandService.UTF8),
+                        s.off, s.bytes, len));
+                return Long.valueOf(len[0]);
+            }
+            check(ctx, SketchNative.pfmerge(ctx, key, s.off, s.bytes));
+            return "OK";
+        } catch (RedisException e) {
+            throw e;
+        } catch (Exception e) {
+            throw new RedisException(e.getMessage(), e);
+        }
+    }
+}

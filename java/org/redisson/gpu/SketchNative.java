@@ -1,0 +1,47 @@
+/*
+ * JNI binding of libredisson_sketch.so (include/redisson_sketch.h).
+ * Source only in this repository (no JDK in the build image); see INTEGRATION.md.
+ * Every array argument follows the C ABI: variable-length byte strings are
+ * (long[] off (n+1), byte[] bytes); replies are written into caller arrays.
+ */
+package org.redisson.gpu;
+
+public final class SketchNative {
+    static {
+        System.loadLibrary("redisson_sketch_jni"); // links libredisson_sketch.so
+    }
+
+    private SketchNative() {
+    }
+
+    public static final int SK_OK = 0, SK_EWRONGTYPE = -1, SK_ERANGE = -2, SK_ECONFIG = -3, SK_ENOTINIT = -4,
+            SK_EDEVICE = -5, SK_EINVAL = -6, SK_ENOMEM = -7, SK_ESYNTAX = -8, SK_ETOOBIG = -9;
+
+    public static native long open(int device, int redisMajor, long maxBitOffset, long hllCapacity, long maxBatch);
+    public static native void close(long ctx);
+    public static native String lastError(long ctx);
+    public static native int calcSlot(byte[] key);
+
+    public static native int del(long ctx, long[] keyOff, byte[] keys, long[] outRemoved);
+    public static native int pfadd(long ctx, long[] keyOff, byte[] keys, int[] elemCounts, long[] elemOff,
+                                   byte[] elems, byte[] outChanged);
+    public static native int pfcount(long ctx, int[] nkeys, long[] keyOff, byte[] keys, long[] outCounts);
+    public static native int pfmerge(long ctx, byte[] dest, long[] srcOff, byte[] srcs);
+    public static native int setbit(long ctx, long[] keyOff, byte[] keys, long[] offsets, byte[] values,
+                                    byte[] outOld);
+    public static native int getbit(long ctx, long[] keyOff, byte[] keys, long[] offsets, byte[] outBits);
+    public static native int bitcount(long ctx, byte[] key, long[] out);
+    public static native int strlen(long ctx, byte[] key, long[] out);
+    public static native int bitop(long ctx, int op, byte[] dest, long[] srcOff, byte[] srcs, long[] outLen);
+    public static native byte[] get(long ctx, byte[] key); // null when the key does not exist
+    public static native int set(long ctx, byte[] key, byte[] value);
+    public static native int bitsetLength(long ctx, byte[] key, long[] out);
+
+    public static native int bloomTryInit(long ctx, byte[] name, long expected, double fpp, int[] outOk);
+    public static native int bloomConfig(long ctx, byte[] name, long[] sizeExpected, int[] k, double[] fpp);
+    public static native int bloomAdd(long ctx, byte[] name, long size, int k, long[] elemOff, byte[] elems,
+                                      byte[] out);
+    public static native int bloomContains(long ctx, byte[] name, long size, int k, long[] elemOff, byte[] elems,
+                                           byte[] out);
+    public static native int bloomCount(long ctx, byte[] name, int[] out);
+}

@@ -215,6 +215,15 @@ struct sk_ctx {
     ncclComm_t comm = nullptr;
 
     bool async_dev = false;     // sk_set_async: _dev calls return without a final sync
+    // async PFADD: the conflict count of the last sparse batch is checked ("settled")
+    // by the next call that needs the HLL arena, not by the call itself
+    bool pf_pending = false;
+    uint8_t *pf_changed = nullptr;
+    // read stream: async Bloom contains runs beside the main stream; writers
+    // on the main stream wait for ev_r, the read stream waits for ev_w
+    hipStream_t st2 = nullptr;
+    hipEvent_t ev_w = nullptr, ev_r = nullptr;
+    bool rd_pending = false;
     uint32_t *h_cnt = nullptr;  // pinned, device-mapped word: conflict count written by the kernel
     uint32_t *d_h_cnt = nullptr;
 
@@ -255,8 +264,26 @@ std::string key_at(const uint64_t *off, const uint8_t *bytes, uint64_t i) {
 
 int sync(sk_ctx *c) {
     HIPCHK(c, hipStreamSynchronize(c->st));
+    if (c->st2) HIPCHK(c, hipStreamSynchronize(c->st2));
     return SK_OK;
 }
+
+int pfadd_settle(sk_ctx *c); // defined with the PFADD core
+
+// entry of every API call: bind the device, finish a pending async PFADD,
+// and order this call after outstanding read-stream work
+#define ENTER(c)                                                                                                       \
+    do {                                                                                                               \
+        HIPCHK(c, hipSetDevice((c)->device));                                                                          \
+        if ((c)->pf_pending) {                                                                                         \
+            int r__ = pfadd_settle(c);                                                                                 \
+            if (r__) return r__;                                                                                       \
+        }                                                                                                              \
+        if ((c)->rd_pending) {                                                                                         \
+            HIPCHK(c, hipStreamWaitEvent((c)->st, (c)->ev_r, 0));                                                      \
+            (c)->rd_pending = false;                                                                                   \
+        }                                                                                                              \
+    } while (0)
 
 // phases timed by sk_prof_* (index = SK_PROF_* in the header)
 const char *kPhaseNames[] = {"pfadd_hash",  "pfadd_sort",   "pfadd_apply", "hll_hist",     "hll_union",
@@ -277,17 +304,18 @@ hipEvent_t ev_get(sk_ctx *c) {
 struct Prof { // RAII: events around one launch when profiling is on
     sk_ctx *c;
     int phase;
+    hipStream_t s;
     hipEvent_t a = nullptr;
-    Prof(sk_ctx *c_, int ph) : c(c_), phase(ph) {
+    Prof(sk_ctx *c_, int ph, hipStream_t s_ = nullptr) : c(c_), phase(ph), s(s_ ? s_ : c_->st) {
         if (c->prof) {
             a = ev_get(c);
-            (void)hipEventRecord(a, c->st);
+            (void)hipEventRecord(a, s);
         }
     }
     ~Prof() {
         if (a) {
             hipEvent_t b = ev_get(c);
-            (void)hipEventRecord(b, c->st);
+            (void)hipEventRecord(b, s);
             c->prof_pending.push_back({phase, a, b});
         }
     }
@@ -295,6 +323,7 @@ struct Prof { // RAII: events around one launch when profiling is on
 void prof_collect(sk_ctx *c) {
     if (c->prof_pending.empty()) return;
     (void)hipStreamSynchronize(c->st);
+    if (c->st2) (void)hipStreamSynchronize(c->st2);
     for (auto &r : c->prof_pending) {
         float ms = 0;
         if (hipEventElapsedTime(&ms, r.a, r.b) == hipSuccess) {
@@ -519,8 +548,16 @@ int pfadd_sparse(sk_ctx *c, uint64_t n, const uint32_t *d_ids, const uint64_t *d
                                       c->keys_b.as<uint64_t>(), c->vals_a.as<uint64_t>(), d_cnt, uint32_t(n)));
     HIPCHK(c, sk::launch_pfadd_conflicts(c->st, c->keys_b.as<uint64_t>(), c->vals_a.as<uint64_t>(), d_cnt, c->arena,
                                          d_changed, c->d_h_cnt)); }
-    int r = sync(c); // the conflict count decides whether the long-list path is needed
-    if (r) return r;
+    c->pf_pending = true;
+    c->pf_changed = d_changed;
+    if (c->async_dev) return SK_OK; // settled by the next call that needs the HLL arena
+    return pfadd_settle(c);
+}
+
+// the conflict count of the last sparse batch decides whether the long-list path is needed
+int pfadd_settle(sk_ctx *c) {
+    c->pf_pending = false;
+    HIPCHK(c, hipStreamSynchronize(c->st));
     uint32_t cnt = *c->h_cnt;
     if (cnt > sk::pfadd_conflict_lds_capacity()) { // long conflict list: rocPRIM sort + replay
         HIPCHK(c, c->vals_b.ensure(uint64_t(cnt) * 8));
@@ -530,7 +567,8 @@ int pfadd_sparse(sk_ctx *c, uint64_t n, const uint32_t *d_ids, const uint64_t *d
         HIPCHK(c, sk::sort_pairs64(c->st, c->sort_tmp.p, c->sort_tmp.cap, c->keys_b.as<uint64_t>(),
                                    c->keys_a.as<uint64_t>(), c->vals_a.as<uint64_t>(), c->vals_b.as<uint64_t>(), cnt));
         HIPCHK(c, sk::launch_pfadd_conflicts_sorted(c->st, cnt, c->keys_a.as<uint64_t>(), c->vals_b.as<uint64_t>(),
-                                                    c->arena, d_changed));
+                                                    c->arena, c->pf_changed));
+        HIPCHK(c, hipStreamSynchronize(c->st));
     }
     return SK_OK;
 }
@@ -638,7 +676,10 @@ int sk_open(const sk_config *cfg, sk_ctx **out) {
         if (cfg->max_batch) c->max_batch = cfg->max_batch;
     }
     if (c->device < 0 || c->device >= ndev || hipSetDevice(c->device) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess) {
+        hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->st2, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_w, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_r, hipEventDisableTiming) != hipSuccess) {
         delete c;
         return SK_EDEVICE;
     }
@@ -658,6 +699,7 @@ int sk_open(const sk_config *cfg, sk_ctx **out) {
 int sk_close(sk_ctx *c) {
     if (!c) return SK_OK;
     (void)hipSetDevice(c->device);
+    if (c->pf_pending) (void)pfadd_settle(c);
     if (c->st) (void)hipStreamSynchronize(c->st);
     if (c->comm) (void)ncclCommDestroy(c->comm);
     prof_collect(c);
@@ -673,6 +715,10 @@ int sk_close(sk_ctx *c) {
     for (DBuf *b : {&c->keys_a, &c->keys_b, &c->vals_a, &c->vals_b, &c->sort_tmp, &c->in_off, &c->in_bytes,
                     &c->in_ids, &c->in_cmd, &c->out_u8, &c->misc, &c->partial, &c->hist, &c->uni, &c->ptrs})
         b->release();
+    if (c->st2) (void)hipStreamSynchronize(c->st2);
+    if (c->ev_w) (void)hipEventDestroy(c->ev_w);
+    if (c->ev_r) (void)hipEventDestroy(c->ev_r);
+    if (c->st2) (void)hipStreamDestroy(c->st2);
     if (c->st) (void)hipStreamDestroy(c->st);
     delete c;
     return SK_OK;
@@ -682,6 +728,7 @@ const char *sk_last_error(sk_ctx *c) { return c ? c->err.c_str() : "no context";
 void *sk_stream(sk_ctx *c) { return c ? (void *)c->st : nullptr; }
 int sk_sync(sk_ctx *c) {
     std::lock_guard<std::mutex> g(c->mu);
+    ENTER(c);
     return sync(c);
 }
 
@@ -754,7 +801,7 @@ int sk_type(sk_ctx *c, const uint8_t *key, uint64_t len, int *out) {
 
 int sk_del(sk_ctx *c, uint32_t n, const uint64_t *off, const uint8_t *bytes, uint64_t *removed) {
     std::lock_guard<std::mutex> g(c->mu);
-    HIPCHK(c, hipSetDevice(c->device));
+    ENTER(c);
     uint64_t cnt = 0;
     for (uint32_t i = 0; i < n; i++) {
         bool r;
@@ -769,7 +816,7 @@ int sk_del(sk_ctx *c, uint32_t n, const uint64_t *off, const uint8_t *bytes, uin
 int sk_hll_resolve(sk_ctx *c, uint32_t n, const uint64_t *off, const uint8_t *bytes, uint32_t *ids,
                    uint8_t *created) {
     std::lock_guard<std::mutex> g(c->mu);
-    HIPCHK(c, hipSetDevice(c->device));
+    ENTER(c);
     for (uint32_t i = 0; i < n; i++) {
         bool cr;
         int r = hll_get(c, key_at(off, bytes, i), true, &ids[i], &cr);
@@ -783,7 +830,7 @@ int sk_hll_resolve(sk_ctx *c, uint32_t n, const uint64_t *off, const uint8_t *by
 int sk_pfadd(sk_ctx *c, uint32_t n_cmds, const uint64_t *key_off, const uint8_t *key_bytes,
              const uint32_t *elem_counts, const uint64_t *elem_off, const uint8_t *elem_bytes, uint8_t *out_changed) {
     std::lock_guard<std::mutex> g(c->mu);
-    HIPCHK(c, hipSetDevice(c->device));
+    ENTER(c);
     if (!n_cmds) return SK_OK;
     // resolve keys in command order; the first command on a created key replies 1
     std::vector<uint32_t> cmd_key(n_cmds);
@@ -879,7 +926,11 @@ int sk_pfadd_dev(sk_ctx *c, uint64_t n, const uint32_t *d_ids, const uint64_t *d
                  uint64_t bytes_len, uint8_t *d_changed) {
     (void)bytes_len;
     std::lock_guard<std::mutex> g(c->mu);
-    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipSetDevice(c->device)); // touches only the HLL arena: no wait on the read stream
+    if (c->pf_pending) {
+        int r = pfadd_settle(c);
+        if (r) return r;
+    }
     if (!n) return SK_OK;
     unsigned id_bits = bits_for(c->hll_next ? c->hll_next - 1 : 0);
     uint64_t max_cmds = std::min<uint64_t>(c->max_batch, 1ull << std::min(32u, 64 - 20 - id_bits));
@@ -897,7 +948,7 @@ int sk_pfadd_dev(sk_ctx *c, uint64_t n, const uint32_t *d_ids, const uint64_t *d
 // --------------------------------------------------------------- PFCOUNT
 int sk_hll_histogram_dev(sk_ctx *c, uint64_t n, const uint32_t *d_ids, uint32_t *d_hist) {
     std::lock_guard<std::mutex> g(c->mu);
-    HIPCHK(c, hipSetDevice(c->device));
+    ENTER(c);
     { Prof p_(c, 3);
     HIPCHK(c, sk::launch_hll_hist(c->st, n, d_ids, c->arena, d_hist)); }
     return sync(c);
@@ -906,7 +957,7 @@ int sk_hll_histogram_dev(sk_ctx *c, uint64_t n, const uint32_t *d_ids, uint32_t 
 int sk_pfcount(sk_ctx *c, uint32_t n_cmds, const uint32_t *nkeys, const uint64_t *key_off, const uint8_t *key_bytes,
                int64_t *out) {
     std::lock_guard<std::mutex> g(c->mu);
-    HIPCHK(c, hipSetDevice(c->device));
+    ENTER(c);
     // single-key commands: one histogram launch over all of them
     std::vector<uint32_t> single_ids;
     std::vector<uint32_t> single_cmd;
@@ -970,7 +1021,7 @@ int sk_pfcount(sk_ctx *c, uint32_t n_cmds, const uint32_t *nkeys, const uint64_t
 
 int sk_hll_union_dev(sk_ctx *c, uint64_t n, const uint32_t *d_ids, uint8_t *d_out) {
     std::lock_guard<std::mutex> g(c->mu);
-    HIPCHK(c, hipSetDevice(c->device));
+    ENTER(c);
     const uint64_t max_groups = 4096;
     HIPCHK(c, c->partial.ensure(max_groups * kHllBytes));
     { Prof p_(c, 4);
@@ -981,7 +1032,7 @@ int sk_hll_union_dev(sk_ctx *c, uint64_t n, const uint32_t *d_ids, uint8_t *d_ou
 int sk_pfmerge(sk_ctx *c, const uint8_t *dest, uint64_t dest_len, uint32_t n_src, const uint64_t *src_off,
                const uint8_t *src_bytes) {
     std::lock_guard<std::mutex> g(c->mu);
-    HIPCHK(c, hipSetDevice(c->device));
+    ENTER(c);
     // check every source first (pfmergeCommand checks before touching dest)
     std::vector<uint32_t> ids;
     for (uint32_t i = 0; i < n_src; i++) {
@@ -998,7 +1049,7 @@ int sk_pfmerge(sk_ctx *c, const uint8_t *dest, uint64_t dest_len, uint32_t n_src
 
 int sk_hll_merge_registers_dev(sk_ctx *c, const uint8_t *key, uint64_t len, const uint8_t *d_regs) {
     std::lock_guard<std::mutex> g(c->mu);
-    HIPCHK(c, hipSetDevice(c->device));
+    ENTER(c);
     uint32_t did;
     int r = hll_get(c, key_of(key, len), true, &did, nullptr);
     if (r) return r;
@@ -1012,7 +1063,7 @@ int sk_hll_merge_registers_dev(sk_ctx *c, const uint8_t *key, uint64_t len, cons
 
 int sk_hll_registers(sk_ctx *c, const uint8_t *key, uint64_t len, uint8_t *out) {
     std::lock_guard<std::mutex> g(c->mu);
-    HIPCHK(c, hipSetDevice(c->device));
+    ENTER(c);
     uint32_t id;
     int r = hll_get(c, key_of(key, len), false, &id, nullptr);
     if (r) return r;
@@ -1032,7 +1083,7 @@ extern "C" {
 int sk_setbit(sk_ctx *c, uint32_t n, const uint64_t *key_off, const uint8_t *key_bytes, const uint64_t *offsets,
               const uint8_t *values, uint8_t *out_old) {
     std::lock_guard<std::mutex> g(c->mu);
-    HIPCHK(c, hipSetDevice(c->device));
+    ENTER(c);
     if (!n) return SK_OK;
     std::vector<uint8_t> ok;
     int status = check_offsets(c, n, offsets, ok);
@@ -1112,7 +1163,7 @@ int sk_setbit(sk_ctx *c, uint32_t n, const uint64_t *key_off, const uint8_t *key
 int sk_getbit(sk_ctx *c, uint32_t n, const uint64_t *key_off, const uint8_t *key_bytes, const uint64_t *offsets,
               uint8_t *out) {
     std::lock_guard<std::mutex> g(c->mu);
-    HIPCHK(c, hipSetDevice(c->device));
+    ENTER(c);
     if (!n) return SK_OK;
     std::vector<uint8_t> ok;
     int status = check_offsets(c, n, offsets, ok);
@@ -1150,7 +1201,7 @@ static int dev_max_offset(sk_ctx *c, uint64_t n, const uint64_t *d_offsets, uint
 int sk_setbit_dev(sk_ctx *c, const uint8_t *key, uint64_t len, uint64_t n, const uint64_t *d_offsets, uint8_t value,
                   uint8_t *d_out_old) {
     std::lock_guard<std::mutex> g(c->mu);
-    HIPCHK(c, hipSetDevice(c->device));
+    ENTER(c);
     if (!n) return SK_OK;
     uint64_t mx;
     int r = dev_max_offset(c, n, d_offsets, &mx);
@@ -1190,7 +1241,7 @@ int sk_setbit_dev(sk_ctx *c, const uint8_t *key, uint64_t len, uint64_t n, const
 int sk_getbit_dev(sk_ctx *c, const uint8_t *key, uint64_t len, uint64_t n, const uint64_t *d_offsets,
                   uint8_t *d_out) {
     std::lock_guard<std::mutex> g(c->mu);
-    HIPCHK(c, hipSetDevice(c->device));
+    ENTER(c);
     if (!n) return SK_OK;
     uint64_t mx;
     int r = dev_max_offset(c, n, d_offsets, &mx);
@@ -1209,7 +1260,7 @@ int sk_getbit_dev(sk_ctx *c, const uint8_t *key, uint64_t len, uint64_t n, const
 
 int sk_bitcount(sk_ctx *c, const uint8_t *key, uint64_t len, uint64_t *out) {
     std::lock_guard<std::mutex> g(c->mu);
-    HIPCHK(c, hipSetDevice(c->device));
+    ENTER(c);
     uint32_t id;
     int r = str_get(c, key_of(key, len), false, 0, &id);
     if (r) return r;
@@ -1224,7 +1275,7 @@ int sk_bitcount(sk_ctx *c, const uint8_t *key, uint64_t len, uint64_t *out) {
 
 int sk_strlen(sk_ctx *c, const uint8_t *key, uint64_t len, uint64_t *out) {
     std::lock_guard<std::mutex> g(c->mu);
-    HIPCHK(c, hipSetDevice(c->device));
+    ENTER(c);
     auto it = c->keys.find(key_of(key, len));
     *out = 0;
     if (it == c->keys.end()) return SK_OK;
@@ -1238,7 +1289,7 @@ int sk_strlen(sk_ctx *c, const uint8_t *key, uint64_t len, uint64_t *out) {
 int sk_bitop(sk_ctx *c, int op, const uint8_t *dest, uint64_t dest_len, uint32_t n_src, const uint64_t *src_off,
              const uint8_t *src_bytes, uint64_t *out_len) {
     std::lock_guard<std::mutex> g(c->mu);
-    HIPCHK(c, hipSetDevice(c->device));
+    ENTER(c);
     if (op < 0 || op > 3) return fail(c, SK_EINVAL, "ERR syntax error");
     if (op == SK_BITOP_NOT && n_src != 1)
         return fail(c, SK_ESYNTAX, "ERR BITOP NOT must be called with a single source key.");
@@ -1317,7 +1368,7 @@ int sk_bitop(sk_ctx *c, int op, const uint8_t *dest, uint64_t dest_len, uint32_t
 
 int sk_get(sk_ctx *c, const uint8_t *key, uint64_t len, uint8_t *buf, uint64_t cap, int64_t *out_len) {
     std::lock_guard<std::mutex> g(c->mu);
-    HIPCHK(c, hipSetDevice(c->device));
+    ENTER(c);
     auto it = c->keys.find(key_of(key, len));
     if (it == c->keys.end()) {
         *out_len = -1;
@@ -1352,7 +1403,7 @@ int sk_get(sk_ctx *c, const uint8_t *key, uint64_t len, uint8_t *buf, uint64_t c
 
 int sk_set(sk_ctx *c, const uint8_t *key, uint64_t len, const uint8_t *val, uint64_t val_len) {
     std::lock_guard<std::mutex> g(c->mu);
-    HIPCHK(c, hipSetDevice(c->device));
+    ENTER(c);
     std::string k = key_of(key, len);
     bool removed;
     int r = del_key(c, k, &removed); // SET overwrites whatever was there
@@ -1370,7 +1421,7 @@ int sk_bitset_length(sk_ctx *c, const uint8_t *key, uint64_t len, int64_t *out) 
     // (Lua float division, floored modulo); scan GETBIT toBit..fromBit downwards,
     // first 1 -> i+1; else fromBit+1.  GETBIT -1 raises the offset error.
     std::lock_guard<std::mutex> g(c->mu);
-    HIPCHK(c, hipSetDevice(c->device));
+    ENTER(c);
     uint32_t id;
     int r = str_get(c, key_of(key, len), false, 0, &id);
     if (r) return r;
@@ -1505,7 +1556,7 @@ static int stage_elems(sk_ctx *c, uint32_t n, const uint64_t *off, const uint8_t
 int sk_bloom_add(sk_ctx *c, const uint8_t *name, uint64_t len, int64_t size, int32_t k, uint32_t n,
                  const uint64_t *off, const uint8_t *bytes, uint8_t *out) {
     std::lock_guard<std::mutex> g(c->mu);
-    HIPCHK(c, hipSetDevice(c->device));
+    ENTER(c);
     uint32_t id;
     int r = bloom_prepare(c, key_of(name, len), size, k, true, &id);
     if (r || !n) return r;
@@ -1521,7 +1572,7 @@ int sk_bloom_add(sk_ctx *c, const uint8_t *name, uint64_t len, int64_t size, int
 int sk_bloom_contains(sk_ctx *c, const uint8_t *name, uint64_t len, int64_t size, int32_t k, uint32_t n,
                       const uint64_t *off, const uint8_t *bytes, uint8_t *out) {
     std::lock_guard<std::mutex> g(c->mu);
-    HIPCHK(c, hipSetDevice(c->device));
+    ENTER(c);
     uint32_t id;
     int r = bloom_prepare(c, key_of(name, len), size, k, false, &id);
     if (r || !n) return r;
@@ -1539,7 +1590,7 @@ int sk_bloom_add_dev(sk_ctx *c, const uint8_t *name, uint64_t len, uint64_t n, c
                      const uint8_t *d_bytes, uint64_t bytes_len, uint8_t *d_out) {
     (void)bytes_len;
     std::lock_guard<std::mutex> g(c->mu);
-    HIPCHK(c, hipSetDevice(c->device));
+    ENTER(c);
     BloomCfg *b;
     std::string nm = key_of(name, len);
     int r = bloom_cfg(c, nm, &b);
@@ -1554,7 +1605,7 @@ int sk_bloom_contains_dev(sk_ctx *c, const uint8_t *name, uint64_t len, uint64_t
                           const uint8_t *d_bytes, uint64_t bytes_len, uint8_t *d_out) {
     (void)bytes_len;
     std::lock_guard<std::mutex> g(c->mu);
-    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipSetDevice(c->device)); // reads the bit array only: no PFADD settle needed
     BloomCfg *b;
     std::string nm = key_of(name, len);
     int r = bloom_cfg(c, nm, &b);
@@ -1563,15 +1614,26 @@ int sk_bloom_contains_dev(sk_ctx *c, const uint8_t *name, uint64_t len, uint64_t
     if ((r = bloom_prepare(c, nm, b->size, b->k, false, &id))) return r;
     const uint8_t *bits = id == kNoId ? reinterpret_cast<const uint8_t *>(c->d_zero) : c->strs[id].ptr;
     const uint64_t *dl = id == kNoId ? reinterpret_cast<const uint64_t *>(c->d_zero) : &c->d_dir[id].len;
-    { Prof p_(c, 5);
-    HIPCHK(c, sk::launch_bloom_contains(c->st, n, d_off, d_bytes, bits, dl, uint64_t(b->size),
+    // async: run on the read stream after everything already enqueued on the main stream
+    hipStream_t s = c->async_dev ? c->st2 : c->st;
+    if (c->async_dev) {
+        HIPCHK(c, hipEventRecord(c->ev_w, c->st));
+        HIPCHK(c, hipStreamWaitEvent(c->st2, c->ev_w, 0));
+    }
+    { Prof p_(c, 5, s);
+    HIPCHK(c, sk::launch_bloom_contains(s, n, d_off, d_bytes, bits, dl, uint64_t(b->size),
                                         magic_for(uint64_t(b->size)), b->k, d_out)); }
-    return c->async_dev ? SK_OK : sync(c);
+    if (c->async_dev) {
+        HIPCHK(c, hipEventRecord(c->ev_r, c->st2));
+        c->rd_pending = true;
+        return SK_OK;
+    }
+    return sync(c);
 }
 
 int sk_bloom_count(sk_ctx *c, const uint8_t *name, uint64_t len, int32_t *out) {
     std::lock_guard<std::mutex> g(c->mu);
-    HIPCHK(c, hipSetDevice(c->device));
+    ENTER(c);
     BloomCfg *b;
     std::string nm = key_of(name, len);
     int r = bloom_cfg(c, nm, &b);
@@ -1604,7 +1666,7 @@ extern "C" {
 
 int sk_dev_alloc(sk_ctx *c, uint64_t bytes, void **out) {
     std::lock_guard<std::mutex> g(c->mu);
-    HIPCHK(c, hipSetDevice(c->device));
+    ENTER(c);
     *out = nullptr;
     if (hipMalloc(out, std::max<uint64_t>(bytes, 16)) != hipSuccess)
         return fail(c, SK_ENOMEM, "cannot allocate %llu device bytes", (unsigned long long)bytes);
@@ -1612,7 +1674,7 @@ int sk_dev_alloc(sk_ctx *c, uint64_t bytes, void **out) {
 }
 int sk_dev_free(sk_ctx *c, void *p) {
     std::lock_guard<std::mutex> g(c->mu);
-    HIPCHK(c, hipSetDevice(c->device));
+    ENTER(c);
     HIPCHK(c, hipStreamSynchronize(c->st));
     if (p) HIPCHK(c, hipFree(p));
     return SK_OK;
@@ -1636,6 +1698,10 @@ int sk_dev_memset(sk_ctx *c, void *p, int v, uint64_t n) {
 int sk_timer_record(sk_ctx *c, int slot) {
     std::lock_guard<std::mutex> g(c->mu);
     if (slot < 0 || slot >= 16) return fail(c, SK_EINVAL, "timer slot");
+    if (c->rd_pending) { // the timer covers read-stream work too
+        HIPCHK(c, hipStreamWaitEvent(c->st, c->ev_r, 0));
+        c->rd_pending = false;
+    }
     if (!c->timers[slot]) HIPCHK(c, hipEventCreate(&c->timers[slot]));
     HIPCHK(c, hipEventRecord(c->timers[slot], c->st));
     return SK_OK;
@@ -1692,7 +1758,7 @@ int sk_comm_unique_id(uint8_t *out128) {
 }
 int sk_comm_init(sk_ctx *c, int nranks, int rank, const uint8_t *id128) {
     std::lock_guard<std::mutex> g(c->mu);
-    HIPCHK(c, hipSetDevice(c->device));
+    ENTER(c);
     ncclUniqueId id;
     std::memcpy(id.internal, id128, NCCL_UNIQUE_ID_BYTES);
     if (c->comm) NCCLCHK(c, ncclCommDestroy(c->comm));
@@ -1727,7 +1793,7 @@ int sk_allgather(sk_ctx *c, const void *d_send, void *d_recv, uint64_t bytes_per
 extern "C" int sk_gen_jackson_longs_dev(sk_ctx *c, uint64_t seed, const uint64_t *d_idx, uint64_t first, uint64_t n,
                                         uint64_t *d_off, uint8_t *d_bytes) {
     std::lock_guard<std::mutex> g(c->mu);
-    HIPCHK(c, hipSetDevice(c->device));
+    ENTER(c);
     size_t tmp;
     HIPCHK(c, sk::gen_jackson_scan_size(n, &tmp));
     HIPCHK(c, c->sort_tmp.ensure(std::max<size_t>(tmp, 16)));

@@ -234,3 +234,48 @@ def test_bulk_setbit_getbit_dev(engine):
     engine.setbit_dev(b"bulk", len(offs2), engine.to_device(offs2), 0, old)
     o = old.download(np.uint8, len(offs2))
     assert o[:100].all() and not o[100:200].any()
+
+
+def test_async_pfadd_and_read_stream(engine, O):
+    """Async mode: PFADD batches (one overflowing the in-LDS conflict replay)
+    interleaved with Bloom contains on the read stream and Bloom adds; the
+    deferred settle and the stream ordering give the sequential results."""
+    nkeys = 30
+    names = [b"as:%d" % i for i in range(nkeys)]
+    ids = engine.hll_resolve(names)
+    assert engine.bloom_try_init("as:bf", 50000, 0.01)
+    size, k, _, _ = engine.bloom_config("as:bf")
+    bits = O.BitString()
+    rng = np.random.default_rng(21)
+    batches, outs, keep = [], [], []
+    ref_regs = np.zeros((nkeys, 16384), dtype=np.uint8)
+    exists = np.zeros(nkeys, dtype=np.uint8)
+    engine.set_async(True)
+    try:
+        for b, n in enumerate([20000, 300000, 5000]):
+            off, buf = gen_jackson_longs(0x5EED0100 + b, n)
+            kid = rng.integers(0, nkeys, n).astype(np.uint32)
+            d = [engine.to_device(ids[kid]), engine.to_device(off), engine.to_device(buf, pad=16), engine.alloc(n)]
+            engine.pfadd_dev(n, d[0], d[1], d[2], int(off[-1]), d[3])
+            # Bloom: add on the main stream, contains on the read stream
+            eoff, ebuf = gen_jackson_longs(0x5EED0200 + b, 4000)
+            e = [engine.to_device(eoff), engine.to_device(ebuf, pad=16), engine.alloc(4000), engine.alloc(4000)]
+            engine.bloom_add_dev("as:bf", 4000, e[0], e[1], int(eoff[-1]), e[2])
+            engine.bloom_contains_dev("as:bf", 4000, e[0], e[1], int(eoff[-1]), e[3])
+            batches.append((kid, off, buf, n, eoff, ebuf))
+            keep.append((d, e))
+        engine.sync()
+    finally:
+        engine.set_async(False)
+    for (kid, off, buf, n, eoff, ebuf), (d, e) in zip(batches, keep):
+        counts = np.ones(n, dtype=np.uint32)
+        want = np.zeros(n, dtype=np.uint8)
+        O.lib().or_pfadd_batch(ref_regs.ctypes.data, exists.ctypes.data, n, kid.ctypes.data, counts.ctypes.data,
+                               off.ctypes.data, buf.ctypes.data, 3, want.ctypes.data)
+        assert np.array_equal(d[3].download(np.uint8, n), want)
+        els = [ebuf[eoff[i]:eoff[i + 1]].tobytes() for i in range(4000)]
+        assert list(e[2].download(np.uint8, 4000).astype(bool)) == bits.bloom_add(size, k, els)
+        assert list(e[3].download(np.uint8, 4000).astype(bool)) == bits.bloom_contains(size, k, els)
+    for i, nm in enumerate(names):
+        np.testing.assert_array_equal(engine.hll_registers(nm), ref_regs[i])
+    assert engine.get("as:bf") == bits.bytes()

@@ -162,17 +162,24 @@ def main():
     bl_ms = prof["bloom_contains"][1]
     # roofline of the dominant kernel: algorithmic bytes per unit x units / avg launch time
     dom = max(PHASES, key=lambda p: prof[p][1])
-    per_unit = {
-        "pfadd_claim": mean_len_h + 8 + 4 + 1 + 8,     # key bytes + offset + slab id + register in, record out
-        "pfadd_commit": 8 + 1 + 1,                     # record in, register + reply out
-        "pfadd_hash": mean_len_h + 8 + 4 + 8,          # key bytes + offset + slab id in, sort key out
-        "pfadd_sort": 2 * 8 * 5,                       # 5 radix passes over 8-byte keys (read + write)
-        "pfadd_apply": 8 + 64 + 64 + 1,                # sorted key + register sector RMW + reply byte
-        "bloom_contains": mean_len_b + 8 + 1 + (k - 1) * 64,   # len + 9 + (k-1)*64 B
-    }[dom]
+    per_unit = per_unit_of(dom, mean_len_h, mean_len_b, k)
     n_launch, tot_ms = prof[dom]
     avg_ms = tot_ms / max(n_launch, 1)
     achieved = per_unit * B / (avg_ms * 1e-3) / 1e9
+
+    # the same kernels measured alone (sync mode, no overlap between PFADD and contains)
+    eng.prof_reset()
+    eng.prof_enable(True)
+    for s in range(W, min(W + K, W + 5)):
+        step(s)
+    eng.sync()
+    eng.prof_enable(False)
+    iso = {p: eng.prof_read(p) for p in PHASES}
+    iso_ms = {p: iso[p][1] / max(iso[p][0], 1) for p in PHASES}
+    iso_dom_ms = iso_ms["bloom_contains"]
+    iso_achieved = per_unit_of("bloom_contains", mean_len_h, mean_len_b, k) * B / (iso_dom_ms * 1e-3) / 1e9
+    traffic = pmc_traffic(dom)
+    step_bytes = B * (per_unit_of("bloom_contains", mean_len_h, mean_len_b, k) + (mean_len_h + 12 + 2.5))
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -203,13 +210,47 @@ def main():
         "device_ms_timed_region": dev_ms,
         "kernel_ms_per_launch": {p: (prof[p][1] / max(prof[p][0], 1)) for p in PHASES},
         "roofline": {"kernel": dom, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "bytes_per_unit": per_unit, "units_per_launch": B, "avg_launch_ms": avg_ms},
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "traffic_source": "profiles/*_pmc_summary.json (FETCH_SIZE+WRITE_SIZE per launch, raw)",
+                     "bytes_per_unit": per_unit, "units_per_launch": B, "avg_launch_ms": avg_ms,
+                     "note": "timed region: PFADD and Bloom contains overlap on two streams"},
+        "roofline_isolated": {"kernel": "bloom_contains", "achieved": iso_achieved, "peak": HBM_PEAK_GBS,
+                              "unit": "GB/s", "frac": iso_achieved / HBM_PEAK_GBS, "avg_launch_ms": iso_dom_ms,
+                              "kernel_ms_per_launch": iso_ms},
+        "step_algorithmic_GBps": step_bytes * K * world / wall / 1e9,
         "cpu_baseline": cpu,
     }
     if rank == 0:
         print(json.dumps(out), flush=True)
     eng.close()
+
+
+def per_unit_of(phase, mean_len_h, mean_len_b, k):
+    """Algorithmic bytes per unit (SURVEY 8d / DESIGN.md kernel table)."""
+    return {
+        "pfadd_claim": mean_len_h + 8 + 4 + 1 + 8,     # key bytes + offset + slab id + register in, record out
+        "pfadd_commit": 8 + 1 + 1,                     # record in, register + reply out
+        "pfadd_hash": mean_len_h + 8 + 4 + 8,          # key bytes + offset + slab id in, sort key out
+        "pfadd_sort": 2 * 8 * 5,                       # 5 radix passes over 8-byte keys (read + write)
+        "pfadd_apply": 8 + 64 + 64 + 1,                # sorted key + register sector RMW + reply byte
+        "bloom_contains": mean_len_b + 8 + 1 + (k - 1) * 64,   # SURVEY 8d: len + 9 + (k-1)*64 B
+    }[phase]
+
+
+def pmc_traffic(phase):
+    """HBM bytes per launch of the phase's kernel from the newest committed PMC summary (or None)."""
+    import glob
+
+    kern = {"bloom_contains": "sk::k_bloom_contains", "pfadd_claim": "sk::k_pfadd_claim",
+            "pfadd_commit": "sk::k_pfadd_commit"}.get(phase)
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_summary.json")))
+    if not kern or not files:
+        return None
+    try:
+        d = json.load(open(files[-1]))["kernels"].get(kern)
+        return d["traffic_bytes_per_launch"] if d else None
+    except (OSError, ValueError, KeyError):
+        return None
 
 
 def cpu_baseline(eng, args, h_off, h_bytes, ids, kid, n_keys, c_off, c_bytes, bloom, size, k):

@@ -27,7 +27,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from redisson_amd import SketchEngine, owner  # noqa: E402
+from redisson_amd import SketchEngine, device_count, owner  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 PHASES = ["pfadd_claim", "pfadd_commit", "pfadd_hash", "pfadd_sort", "pfadd_apply", "bloom_contains"]
@@ -87,7 +87,8 @@ def main():
     # ------------------------------------------------------------ setup (untimed)
     names = ["tenant:%d:hll" % t for t in range(args.tenants)]
     mine = [nm for nm in names if owner(nm, world) == rank]
-    eng = SketchEngine(device=local, hll_capacity=len(mine) + 16, max_batch=max(8 * B, 1 << 22),
+    ndev = max(device_count(), 1)   # one rank per GPU; rehearsals with more ranks than GPUs share devices
+    eng = SketchEngine(device=local % ndev, hll_capacity=len(mine) + 16, max_batch=max(8 * B, 1 << 22),
                        max_bit_offset=1 << 34)
     ids = eng.hll_resolve(mine)
     rng = np.random.default_rng(0x5EED0002 + rank)

@@ -1,0 +1,153 @@
+#!/usr/bin/env python3
+"""bench_configs.py -- the other BASELINE.json configs, one JSON line each.
+
+bench.py measures the headline (C2 PFADD + C3 Bloom contains).  This script
+measures the remaining configs on one MI355X with inputs resident in HBM:
+
+  c1  RHyperLogLog: 1M random Longs into ONE key as 1M RBatch PFADDs (dense
+      path: exact replies via radix sort), and the reference addAll (Q1: one
+      element = the Jackson array, ~38 MB) + count().
+  c4  1M tenant HLLs x 1,000 elements (1B PFADD, sharded by calcSlot % 8 ->
+      the slab set of one GPU of 8 is timed at full size here), then the
+      global union / countWith over all of them: k_hll_union streams 16 KiB
+      per source (roofline: HBM streaming).
+  c5  RBitSet 2^34 bits (2 GiB): 1B random SETBIT (SETBIT_VOID), 1B GETBIT,
+      BITCOUNT, AND/OR across 4 bitsets (BITOP streams (s+1)*N/8 bytes).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+from redisson_amd import JsonJacksonCodec, JLong, SketchEngine, owner  # noqa: E402
+
+PEAK = 8000.0
+
+
+def line(d):
+    print(json.dumps(d), flush=True)
+
+
+def timed(eng, fn, reps=1):
+    eng.sync()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        fn()
+    eng.sync()
+    return (time.perf_counter() - t0) / reps
+
+
+def c1(eng, args):
+    n = args.c1_n
+    off, byt, tot = eng.gen_jackson_longs_dev(0x5EED0001, n)
+    ids = eng.hll_resolve([b"hll:c1"])
+    d_ids = eng.to_device(np.full(n, ids[0], dtype=np.uint32))
+    d_out = eng.alloc(n)
+    eng.pfadd_dev(n, d_ids, off, byt, tot, d_out)            # warm (and fills the registers)
+    eng.delete([b"hll:c1"])
+    ids = eng.hll_resolve([b"hll:c1"])
+    d_ids.upload(np.full(n, ids[0], dtype=np.uint32))
+    t = timed(eng, lambda: eng.pfadd_dev(n, d_ids, off, byt, tot, d_out))
+    cnt = eng.pfcount([[b"hll:c1"]])[0]
+    # Q1: addAll(1M Longs) = ONE PFADD element, the Jackson encoding of Object[]{name, e1..en}
+    vals = np.random.default_rng(1).integers(-(1 << 63), (1 << 63) - 1, min(n, 1 << 20), dtype=np.int64)
+    blob = JsonJacksonCodec().encode(["hll:c1q"] + [JLong(int(v)) for v in vals])
+    t_q1 = timed(eng, lambda: eng.pfadd([b"hll:c1q"], [[blob]]))
+    line({"metric": "C1 PFADD inserts/sec (one key, RBatch of single-element PFADDs)", "value": n / t,
+          "unit": "inserts/s", "config": {"workload": "c1", "elements": n, "count_after": cnt},
+          "addAll_q1": {"element_bytes": len(blob), "seconds": t_q1, "count_after":
+                        eng.pfcount([[b"hll:c1q"]])[0]}})
+
+
+def c4(eng, args):
+    nk, per = args.c4_keys, args.c4_per_key
+    names = [b"t4:%d" % i for i in range(nk)]
+    ids = eng.hll_resolve(names)
+    chunk = 1 << 24
+    total = nk * per
+    d_out = eng.alloc(chunk)
+    rng = np.random.default_rng(4)
+    t_add = 0.0
+    for s in range(0, total, chunk):
+        m = min(chunk, total - s)
+        off, byt, tot = eng.gen_jackson_longs_dev(0x5EED0004, m, first=s)
+        d_ids = eng.to_device(ids[rng.integers(0, nk, m)].astype(np.uint32))
+        t_add += timed(eng, lambda: eng.pfadd_dev(m, d_ids, off, byt, tot, d_out))
+        off.free(); byt.free(); d_ids.free()
+    d_all = eng.to_device(ids)
+    d_u = eng.alloc(16384)
+    eng.prof_reset(); eng.prof_enable(True)
+    t_u = timed(eng, lambda: eng.hll_union_dev(nk, d_all, d_u), reps=3)
+    eng.prof_enable(False)
+    n_l, ms = eng.prof_read("hll_union")
+    k_ms = ms / max(n_l, 1)
+    eng.hll_merge_registers_dev(b"t4:union", d_u)
+    est = eng.pfcount([[b"t4:union"]])[0]
+    gbs = nk * 16384 / (k_ms * 1e-3) / 1e9
+    line({"metric": "C4 global union (countWith/PFMERGE) sources/sec, one GPU's shard", "value": nk / t_u,
+          "unit": "sources/s", "config": {"workload": "c4", "keys": nk, "elements_per_key": per},
+          "pfadd_inserts_per_s": total / t_add, "union_estimate": est,
+          "roofline": {"kernel": "hll_union", "bound": "hbm", "achieved": gbs, "peak": PEAK, "unit": "GB/s",
+                       "frac": gbs / PEAK, "bytes_per_unit": 16384, "avg_launch_ms": k_ms}})
+
+
+def c5(eng, args):
+    bits = 1 << args.c5_log2_bits
+    n = args.c5_ops
+    rng = np.random.default_rng(5)
+    chunk = 1 << 26
+    keys = [b"bs5:%d" % i for i in range(4)]
+    t_set = t_get = 0.0
+    d_out = eng.alloc(chunk)
+    for key in keys:
+        for s in range(0, n if key == keys[0] else n // 16, chunk):
+            m = min(chunk, n - s)
+            d_off = eng.to_device(rng.integers(0, bits, m, dtype=np.uint64))
+            dt = timed(eng, lambda: eng.setbit_dev(key, m, d_off, 1))
+            if key == keys[0]:
+                t_set += dt
+                t_get += timed(eng, lambda: eng.getbit_dev(key, m, d_off, d_out))
+            d_off.free()
+    for key in keys[1:]:     # make every bitset full length (2^34 bits)
+        eng.setbit([key], [bits - 1], [1])
+    eng.prof_reset(); eng.prof_enable(True)
+    t_bc = timed(eng, lambda: eng.bitcount(keys[0]), reps=3)
+    t_and = timed(eng, lambda: eng.bitop("AND", b"bs5:and", keys), reps=2)
+    t_or = timed(eng, lambda: eng.bitop("OR", b"bs5:or", keys[:2]), reps=2)
+    eng.prof_enable(False)
+    nbytes = bits // 8
+    line({"metric": "C5 RBitSet 2^%d bits: SETBIT+GETBIT ops/sec" % args.c5_log2_bits,
+          "value": 2 * n / (t_set + t_get), "unit": "ops/s",
+          "config": {"workload": "c5", "bits": bits, "ops": n},
+          "setbit_per_s": n / t_set, "getbit_per_s": n / t_get,
+          "bitcount_GBps": nbytes / t_bc / 1e9, "bitop_and4_GBps": 5 * nbytes / t_and / 1e9,
+          "bitop_or2_GBps": 3 * nbytes / t_or / 1e9,
+          "roofline": {"kernel": "bitcount", "bound": "hbm", "achieved": nbytes / t_bc / 1e9, "peak": PEAK,
+                       "unit": "GB/s", "frac": nbytes / t_bc / 1e9 / PEAK, "note": "host-timed incl. launch"}})
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--configs", default="c1,c4,c5")
+    ap.add_argument("--c1-n", type=int, default=1 << 20)
+    ap.add_argument("--c4-keys", type=int, default=125_000)       # 1M keys / 8 GPUs
+    ap.add_argument("--c4-per-key", type=int, default=1000)
+    ap.add_argument("--c5-log2-bits", type=int, default=34)
+    ap.add_argument("--c5-ops", type=int, default=1 << 28)
+    args = ap.parse_args()
+    eng = SketchEngine(device=int(os.environ.get("LOCAL_RANK", "0")), max_bit_offset=1 << 36,
+                       hll_capacity=args.c4_keys + 64, max_batch=1 << 24)
+    for c in args.configs.split(","):
+        {"c1": c1, "c4": c4, "c5": c5}[c](eng, args)
+    eng.close()
+
+
+if __name__ == "__main__":
+    main()

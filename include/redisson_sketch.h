@@ -80,6 +80,8 @@ void *sk_stream(sk_ctx *ctx); /* the context's hipStream_t (for event timing) */
 int sk_sync(sk_ctx *ctx);
 
 /* ---- host-only helpers (no GPU needed) ---- */
+/* visible HIP devices (0 without a GPU) */
+int sk_device_count(void);
 /* CRC16-XMODEM, M:connection/CRC16.java:55-61 */
 uint32_t sk_crc16(const uint8_t *bytes, uint64_t len);
 /* ClusterConnectionManager.calcSlot, M:cluster/ClusterConnectionManager.java:543-558;

@@ -6,7 +6,7 @@ RBloomFilter / RBatch interfaces over that ABI.
 """
 from .codec import ByteArrayCodec, JInteger, JLong, JsonJacksonCodec, LongCodec, StringCodec  # noqa: F401
 from .engine import (DeviceUnavailable, IllegalArgumentException, IllegalStateException,  # noqa: F401
-                     RedisException, SketchEngine, bloom_optimal_bits, bloom_optimal_k, calc_slot, crc16,
+                     RedisException, SketchEngine, bloom_optimal_bits, bloom_optimal_k, calc_slot, crc16, device_count,
                      gen_jackson_longs, owner)
 from .redisson import Config, JBitSet, RBatch, RBitSet, RBloomFilter, Redisson, RHyperLogLog  # noqa: F401
 
@@ -14,5 +14,5 @@ __all__ = [
     "Redisson", "Config", "RBatch", "RBitSet", "RBloomFilter", "RHyperLogLog", "JBitSet",
     "SketchEngine", "RedisException", "IllegalStateException", "IllegalArgumentException", "DeviceUnavailable",
     "JsonJacksonCodec", "StringCodec", "LongCodec", "ByteArrayCodec", "JLong", "JInteger",
-    "calc_slot", "crc16", "owner", "bloom_optimal_bits", "bloom_optimal_k", "gen_jackson_longs",
+    "calc_slot", "crc16", "owner", "device_count", "bloom_optimal_bits", "bloom_optimal_k", "gen_jackson_longs",
 ]

@@ -48,6 +48,7 @@ SIGNATURES = {
     "sk_strerror": (c_char_p, [c_int]),
     "sk_stream": (c_void_p, [P]),
     "sk_sync": (c_int, [P]),
+    "sk_device_count": (c_int, []),
     "sk_crc16": (c_uint32, [_u8p, c_uint64]),
     "sk_calc_slot": (c_int32, [_u8p, c_uint64]),
     "sk_owner": (c_int32, [_u8p, c_uint64, c_int32]),

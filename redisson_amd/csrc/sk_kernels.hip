@@ -285,28 +285,31 @@ __device__ __forceinline__ uint4 bytemax4(uint4 a, uint4 b) {
 }
 
 // grid (4, G): block (x, g) covers 4096 registers (256 lanes x 16 B) of the
-// union of keys [g*per, (g+1)*per); writes partial[g].
+// union of sources [g*per, (g+1)*per) and writes partial[g].  Sources are
+// slabs ids[k] of `base`, or (ids == null) consecutive 16 KiB arrays -- the
+// form the next tree level reads.
 __global__ void __launch_bounds__(256) k_hll_union_partial(uint64_t n, const uint32_t *__restrict__ ids,
-                                                           const uint8_t *__restrict__ arena, uint64_t per,
+                                                           const uint8_t *__restrict__ base, uint64_t per,
                                                            uint8_t *__restrict__ partial) {
     unsigned lane16 = blockIdx.x * 256 + threadIdx.x; // uint4 index within 16 KiB
     uint64_t g = blockIdx.y, k0 = g * per, k1 = k0 + per;
     if (k1 > n) k1 = n;
     uint4 acc = make_uint4(0, 0, 0, 0);
     uint64_t k = k0;
-    for (; k + 4 <= k1; k += 4) { // 4 independent loads in flight per lane
-        uint4 a = reinterpret_cast<const uint4 *>(arena + (uint64_t(ids[k]) << 14))[lane16];
-        uint4 b = reinterpret_cast<const uint4 *>(arena + (uint64_t(ids[k + 1]) << 14))[lane16];
-        uint4 c = reinterpret_cast<const uint4 *>(arena + (uint64_t(ids[k + 2]) << 14))[lane16];
-        uint4 d = reinterpret_cast<const uint4 *>(arena + (uint64_t(ids[k + 3]) << 14))[lane16];
-        acc = bytemax4(acc, bytemax4(bytemax4(a, b), bytemax4(c, d)));
+#define SK_SRC(kk) (reinterpret_cast<const uint4 *>(base + ((ids ? uint64_t(ids[kk]) : uint64_t(kk)) << 14)))
+    for (; k + 8 <= k1; k += 8) { // 8 independent 16 B loads in flight per lane
+        uint4 a0 = SK_SRC(k)[lane16], a1 = SK_SRC(k + 1)[lane16], a2 = SK_SRC(k + 2)[lane16],
+              a3 = SK_SRC(k + 3)[lane16], a4 = SK_SRC(k + 4)[lane16], a5 = SK_SRC(k + 5)[lane16],
+              a6 = SK_SRC(k + 6)[lane16], a7 = SK_SRC(k + 7)[lane16];
+        acc = bytemax4(acc, bytemax4(bytemax4(bytemax4(a0, a1), bytemax4(a2, a3)),
+                                     bytemax4(bytemax4(a4, a5), bytemax4(a6, a7))));
     }
-    for (; k < k1; k++)
-        acc = bytemax4(acc, reinterpret_cast<const uint4 *>(arena + (uint64_t(ids[k]) << 14))[lane16]);
+    for (; k < k1; k++) acc = bytemax4(acc, SK_SRC(k)[lane16]);
+#undef SK_SRC
     reinterpret_cast<uint4 *>(partial + g * 16384)[lane16] = acc;
 }
 
-// out = max(out_init ? out : 0, partial[0..G))
+// out = max(include_out ? out : 0, partial[0..G)) for a small G (the tree root)
 __global__ void __launch_bounds__(256) k_hll_union_final(uint64_t G, const uint8_t *__restrict__ partial,
                                                          uint8_t *__restrict__ out, int include_out) {
     unsigned lane16 = blockIdx.x * 256 + threadIdx.x;
@@ -519,46 +522,79 @@ __global__ void __launch_bounds__(256) k_bitcount(const uint8_t *__restrict__ bu
     if ((threadIdx.x & 63) == 0 && c) atomicAdd(out, (unsigned long long)c);
 }
 
-// BITOP over maxlen bytes; sources shorter than maxlen read as 0.
+// BITOP over maxlen bytes; sources shorter than maxlen read as 0.  Source
+// pointers / lengths are cached in LDS; chunks every source covers take the
+// straight 16 B path, two chunks per lane per step for memory parallelism.
+#define SK_BITOP_MAXSRC 64
+__device__ __forceinline__ uint4 bitop_src_chunk(const uint8_t *p, uint64_t l, uint64_t b0) {
+    if (b0 + 16 <= l) return *reinterpret_cast<const uint4 *>(p + b0);
+    uint8_t tmp[16];
+    for (int q = 0; q < 16; q++) tmp[q] = (b0 + q < l) ? p[b0 + q] : 0;
+    return *reinterpret_cast<uint4 *>(tmp);
+}
+__device__ __forceinline__ uint4 bitop_combine(int op, uint4 acc, uint4 x) {
+    if (op == 0) return make_uint4(acc.x & x.x, acc.y & x.y, acc.z & x.z, acc.w & x.w);
+    if (op == 1) return make_uint4(acc.x | x.x, acc.y | x.y, acc.z | x.z, acc.w | x.w);
+    return make_uint4(acc.x ^ x.x, acc.y ^ x.y, acc.z ^ x.z, acc.w ^ x.w);
+}
 __global__ void __launch_bounds__(256) k_bitop(int op, uint32_t nsrc, const uint8_t *const *__restrict__ srcs,
                                                const uint64_t *__restrict__ lens, uint64_t maxlen,
                                                uint8_t *__restrict__ dst) {
+    __shared__ const uint8_t *P[SK_BITOP_MAXSRC];
+    __shared__ uint64_t L[SK_BITOP_MAXSRC];
+    if (threadIdx.x < nsrc) {
+        P[threadIdx.x] = srcs[threadIdx.x];
+        L[threadIdx.x] = lens[threadIdx.x];
+    }
+    __syncthreads();
+    uint64_t minlen = L[0];
+    for (uint32_t s = 1; s < nsrc; s++) minlen = L[s] < minlen ? L[s] : minlen;
     uint64_t nvec = (maxlen + 15) >> 4;
     uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
-    for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < nvec; i += stride) {
-        uint64_t b0 = i << 4;
-        uint4 acc = make_uint4(0, 0, 0, 0);
-        for (uint32_t s = 0; s < nsrc; s++) {
-            uint64_t l = lens[s];
-            uint4 x;
-            if (b0 + 16 <= l) {
-                x = reinterpret_cast<const uint4 *>(srcs[s])[i];
-            } else {
-                uint8_t tmp[16];
-                for (int q = 0; q < 16; q++) tmp[q] = (b0 + q < l) ? srcs[s][b0 + q] : 0;
-                x = *reinterpret_cast<uint4 *>(tmp);
+    for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < nvec; i += 2 * stride) {
+        uint64_t j = i + stride; // second chunk of this lane
+        bool has_j = j < nvec;
+        uint64_t b0 = i << 4, b1 = j << 4;
+        uint4 acc0, acc1 = make_uint4(0, 0, 0, 0);
+        if (b0 + 16 <= minlen && (!has_j || b1 + 16 <= minlen)) { // every source covers both chunks
+            acc0 = reinterpret_cast<const uint4 *>(P[0])[i];
+            if (has_j) acc1 = reinterpret_cast<const uint4 *>(P[0])[j];
+            if (op == 3) {
+                acc0 = make_uint4(~acc0.x, ~acc0.y, ~acc0.z, ~acc0.w);
+                acc1 = make_uint4(~acc1.x, ~acc1.y, ~acc1.z, ~acc1.w);
             }
-            if (s == 0) {
-                acc = x;
-                if (op == 3) acc = make_uint4(~acc.x, ~acc.y, ~acc.z, ~acc.w);
-            } else if (op == 0) {
-                acc = make_uint4(acc.x & x.x, acc.y & x.y, acc.z & x.z, acc.w & x.w);
-            } else if (op == 1) {
-                acc = make_uint4(acc.x | x.x, acc.y | x.y, acc.z | x.z, acc.w | x.w);
-            } else if (op == 2) {
-                acc = make_uint4(acc.x ^ x.x, acc.y ^ x.y, acc.z ^ x.z, acc.w ^ x.w);
+            for (uint32_t s = 1; s < nsrc; s++) {
+                uint4 x0 = reinterpret_cast<const uint4 *>(P[s])[i];
+                uint4 x1 = has_j ? reinterpret_cast<const uint4 *>(P[s])[j] : make_uint4(0, 0, 0, 0);
+                acc0 = bitop_combine(op, acc0, x0);
+                acc1 = bitop_combine(op, acc1, x1);
+            }
+        } else {
+            acc0 = bitop_src_chunk(P[0], L[0], b0);
+            if (has_j) acc1 = bitop_src_chunk(P[0], L[0], b1);
+            if (op == 3) {
+                acc0 = make_uint4(~acc0.x, ~acc0.y, ~acc0.z, ~acc0.w);
+                acc1 = make_uint4(~acc1.x, ~acc1.y, ~acc1.z, ~acc1.w);
+            }
+            for (uint32_t s = 1; s < nsrc; s++) {
+                acc0 = bitop_combine(op, acc0, bitop_src_chunk(P[s], L[s], b0));
+                if (has_j) acc1 = bitop_combine(op, acc1, bitop_src_chunk(P[s], L[s], b1));
             }
         }
-        if (b0 + 16 <= maxlen) {
-            reinterpret_cast<uint4 *>(dst)[i] = acc;
-        } else {
-            const uint8_t *a = reinterpret_cast<const uint8_t *>(&acc);
-            for (int q = 0; q < 16; q++)
-                if (b0 + q < maxlen) dst[b0 + q] = a[q];
+        for (int c = 0; c < 2; c++) {
+            uint64_t bb = c ? b1 : b0;
+            uint4 a = c ? acc1 : acc0;
+            if (c && !has_j) break;
+            if (bb + 16 <= maxlen) {
+                reinterpret_cast<uint4 *>(dst)[bb >> 4] = a;
+            } else {
+                const uint8_t *ab = reinterpret_cast<const uint8_t *>(&a);
+                for (int q = 0; q < 16; q++)
+                    if (bb + q < maxlen) dst[bb + q] = ab[q];
+            }
         }
     }
 }
-
 
 // ------------------------------------------------- synthetic input generator
 // Counter-based SplitMix64: element i = mix(seed + (i+1)*golden), the same
@@ -725,19 +761,41 @@ hipError_t launch_hll_hist(hipStream_t st, uint64_t n, const uint32_t *ids, cons
     return hipSuccess;
 }
 
+// Union as a max-tree: level 0 reduces the slabs into <= max_groups partials
+// (>= 64 sources per workgroup column), each further level reduces 64:1 until
+// <= 64 remain, and the root folds them (and `out` when include_out) into out.
+// `partial` holds max_groups + max_groups/64 + 1 arrays of 16 KiB.
 hipError_t launch_hll_union(hipStream_t st, uint64_t n, const uint32_t *ids, const uint8_t *arena, uint8_t *partial,
                             uint64_t max_groups, uint8_t *out, int include_out) {
     if (!n) {
         if (!include_out) return hipMemsetAsync(out, 0, 16384, st);
         return hipSuccess;
     }
-    uint64_t G = (n + 63) / 64; // 64 keys per group -> 4*G workgroups
-    if (G > max_groups) G = max_groups;
-    uint64_t per = (n + G - 1) / G;
-    G = (n + per - 1) / per;
-    hipLaunchKernelGGL(k_hll_union_partial, dim3(4, unsigned(G)), dim3(256), 0, st, n, ids, arena, per, partial);
-    SK_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_hll_union_final, dim3(4), dim3(256), 0, st, G, partial, out, include_out);
+    const uint32_t *cur_ids = ids;
+    const uint8_t *cur = arena;
+    uint64_t cur_n = n;
+    uint8_t *bufs[2] = {partial, partial + max_groups * 16384};
+    int which = 0;
+    while (cur_n > 64) {
+        uint64_t per = (cur_n + max_groups - 1) / max_groups;
+        if (per < 64) per = 64;
+        uint64_t G = (cur_n + per - 1) / per;
+        hipLaunchKernelGGL(k_hll_union_partial, dim3(4, unsigned(G)), dim3(256), 0, st, cur_n, cur_ids, cur, per,
+                           bufs[which]);
+        SK_LAUNCH_CHECK();
+        cur = bufs[which];
+        cur_ids = nullptr;
+        cur_n = G;
+        which ^= 1;
+    }
+    if (cur_ids) { // n <= 64 slabs: one partial, then the root
+        hipLaunchKernelGGL(k_hll_union_partial, dim3(4, 1), dim3(256), 0, st, cur_n, cur_ids, cur, cur_n,
+                           bufs[which]);
+        SK_LAUNCH_CHECK();
+        cur = bufs[which];
+        cur_n = 1;
+    }
+    hipLaunchKernelGGL(k_hll_union_final, dim3(4), dim3(256), 0, st, cur_n, cur, out, include_out);
     SK_LAUNCH_CHECK();
     return hipSuccess;
 }

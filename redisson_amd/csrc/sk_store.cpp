@@ -596,7 +596,7 @@ int union_into(sk_ctx *c, const std::vector<uint32_t> &ids, uint8_t *d_out, int 
     if (!ids.empty())
         HIPCHK(c, hipMemcpyAsync(c->in_ids.p, ids.data(), ids.size() * 4, hipMemcpyHostToDevice, c->st));
     const uint64_t max_groups = 4096;
-    HIPCHK(c, c->partial.ensure(max_groups * kHllBytes));
+    HIPCHK(c, c->partial.ensure((max_groups + max_groups / 64 + 2) * kHllBytes));
     HIPCHK(c, sk::launch_hll_union(c->st, ids.size(), c->in_ids.as<uint32_t>(), c->arena, c->partial.as<uint8_t>(),
                                    max_groups, d_out, include_out));
     return sync(c); // ids is a host vector
@@ -730,6 +730,11 @@ int sk_sync(sk_ctx *c) {
     std::lock_guard<std::mutex> g(c->mu);
     ENTER(c);
     return sync(c);
+}
+
+int sk_device_count(void) {
+    int n = 0;
+    return hipGetDeviceCount(&n) == hipSuccess ? n : 0;
 }
 
 uint32_t sk_crc16(const uint8_t *p, uint64_t len) {
@@ -1023,7 +1028,7 @@ int sk_hll_union_dev(sk_ctx *c, uint64_t n, const uint32_t *d_ids, uint8_t *d_ou
     std::lock_guard<std::mutex> g(c->mu);
     ENTER(c);
     const uint64_t max_groups = 4096;
-    HIPCHK(c, c->partial.ensure(max_groups * kHllBytes));
+    HIPCHK(c, c->partial.ensure((max_groups + max_groups / 64 + 2) * kHllBytes));
     { Prof p_(c, 4);
     HIPCHK(c, sk::launch_hll_union(c->st, n, d_ids, c->arena, c->partial.as<uint8_t>(), max_groups, d_out, 0)); }
     return sync(c);
@@ -1055,7 +1060,7 @@ int sk_hll_merge_registers_dev(sk_ctx *c, const uint8_t *key, uint64_t len, cons
     if (r) return r;
     // out = max(out, d_regs): a one-key union whose "arena" is d_regs
     const uint64_t max_groups = 4096;
-    HIPCHK(c, c->partial.ensure(max_groups * kHllBytes));
+    HIPCHK(c, c->partial.ensure((max_groups + max_groups / 64 + 2) * kHllBytes));
     HIPCHK(c, sk::launch_hll_union(c->st, 1, c->d_zero, d_regs, c->partial.as<uint8_t>(), max_groups,
                                    c->arena + uint64_t(did) * kHllBytes, 1));
     return sync(c);
@@ -1294,6 +1299,7 @@ int sk_bitop(sk_ctx *c, int op, const uint8_t *dest, uint64_t dest_len, uint32_t
     if (op == SK_BITOP_NOT && n_src != 1)
         return fail(c, SK_ESYNTAX, "ERR BITOP NOT must be called with a single source key.");
     if (n_src == 0) return fail(c, SK_EINVAL, "ERR wrong number of arguments for 'bitop' command");
+    if (n_src > 64) return fail(c, SK_EINVAL, "BITOP supports at most 64 source keys per call");
     std::vector<const uint8_t *> ptrs(n_src);
     std::vector<uint64_t> lens(n_src);
     std::string dkey = key_of(dest, dest_len);
@@ -1329,12 +1335,19 @@ int sk_bitop(sk_ctx *c, int op, const uint8_t *dest, uint64_t dest_len, uint32_t
     // destination buffer: in place when dest is a source with room, else fresh
     uint8_t *dst;
     uint8_t *old_buf = nullptr;
-    int r;
-    if (did != kNoId && dest_is_src && c->strs[did].cap >= maxlen) {
+    int r = SK_OK;
+    if (did != kNoId && c->strs[did].cap >= maxlen) {
+        // in place: a source that is also the destination is read and written by
+        // the same lane at the same chunk; bytes past the new length must read 0
         dst = c->strs[did].ptr;
+        uint64_t old_len;
+        if (!dest_is_src) {
+            if ((r = str_len(c, did, &old_len))) return r;
+            if (old_len > maxlen) HIPCHK(c, hipMemsetAsync(dst + maxlen, 0, old_len - maxlen, c->st));
+        }
     } else {
         if (hipMalloc(&dst, round16(maxlen)) != hipSuccess) return fail(c, SK_ENOMEM, "cannot allocate BITOP result");
-        HIPCHK(c, hipMemsetAsync(dst, 0, round16(maxlen), c->st));
+        if (round16(maxlen) > maxlen) HIPCHK(c, hipMemsetAsync(dst + maxlen, 0, round16(maxlen) - maxlen, c->st));
     }
     HIPCHK(c, c->ptrs.ensure(n_src * 16));
     std::vector<uint8_t> blob(n_src * 16);

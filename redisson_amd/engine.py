@@ -390,6 +390,10 @@ class SketchEngine:
 
 
 # ---------------------------------------------------------------- host-only
+def device_count() -> int:
+    return int(N.load().sk_device_count())
+
+
 def calc_slot(key) -> int:
     k = _b(key)
     return int(N.load().sk_calc_slot(k, len(k)))

@@ -279,3 +279,54 @@ def test_async_pfadd_and_read_stream(engine, O):
     for i, nm in enumerate(names):
         np.testing.assert_array_equal(engine.hll_registers(nm), ref_regs[i])
     assert engine.get("as:bf") == bits.bytes()
+
+
+def test_redis5_semantics(O):
+    """redis_major=5: HLL_Q sentinel in hllPatLen and the Ertl estimator."""
+    from redisson_amd import SketchEngine
+    e5 = SketchEngine(device=0, redis_major=5)
+    try:
+        ref = O.HLLStore(5)
+        keys = [b"v5:%d" % i for i in range(6)]
+        for i, k in enumerate(keys):
+            m = [10, 1000, 20000, 100000, 3, 0][i]
+            els = _elems(4000 + i, m)
+            if els:
+                e5.pfadd([k] * m, [[x] for x in els])
+                ref.pfadd([k] * m, [[x] for x in els])
+        live = [k for k in keys if k in ref.regs]
+        for k in live:
+            np.testing.assert_array_equal(e5.hll_registers(k), ref.regs[k])
+        assert e5.pfcount([[k] for k in live]) == [ref.count([k]) for k in live]
+        assert e5.pfcount([live]) == [ref.count(live)]
+    finally:
+        e5.close()
+
+
+def test_edge_cases(engine, O):
+    # empty batches are no-ops
+    assert engine.pfadd([], []) == []
+    assert engine.getbit([], []) == []
+    assert engine.pfcount([]) == []
+    # zero-length elements and very long elements (global-reader path, farmUo > 64)
+    rng = np.random.default_rng(1)
+    els = [b"", b"x", bytes(64), bytes(65), rng.integers(0, 256, 5000, dtype=np.uint8).tobytes()] * 3
+    keys = [b"edge:%d" % (i % 2) for i in range(len(els))]
+    ref = O.HLLStore()
+    assert engine.pfadd(keys, [[e] for e in els]) == ref.pfadd(keys, [[e] for e in els])
+    for k in set(keys):
+        np.testing.assert_array_equal(engine.hll_registers(k), ref.regs[k])
+    assert engine.bloom_try_init("edge:bf", 1000, 0.01)
+    size, k, _, _ = engine.bloom_config("edge:bf")
+    bits = O.BitString()
+    assert engine.bloom_add("edge:bf", size, k, els) == bits.bloom_add(size, k, els)
+    assert engine.bloom_contains("edge:bf", size, k, els[::-1]) == bits.bloom_contains(size, k, els[::-1])
+    # PFCOUNT of a missing key, union with only missing keys
+    assert engine.pfcount([[b"edge:none"], [b"edge:none", b"edge:none2"]]) == [0, 0]
+    # DEL returns the count and frees slabs for reuse (zeroed)
+    assert engine.delete([b"edge:0", b"edge:0", b"edge:none"]) == 1
+    assert engine.pfadd([b"edge:new"], [[b"a"]]) == [True]
+    assert engine.pfcount([[b"edge:new"]]) == [1]
+    # STRLEN of an HLL is its dense size; GET of a missing key is None
+    assert engine.strlen(b"edge:new") == 12304
+    assert engine.get(b"edge:none") is None

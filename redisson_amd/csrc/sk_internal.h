@@ -13,7 +13,7 @@ hipError_t launch_pfadd_apply(hipStream_t st, uint64_t n, const uint64_t *keys, 
                               uint8_t *arena, uint8_t *changed);
 hipError_t launch_pfadd_claim(hipStream_t st, uint64_t n, const uint32_t *key_ids, const uint64_t *off,
                               const uint8_t *bytes, int v5, uint8_t *arena, uint64_t *rec, uint8_t *changed_i,
-                              uint32_t *conf_count);
+                              uint32_t *conf_count, int claim_all);
 hipError_t launch_pfadd_conflicts(hipStream_t st, const uint64_t *conf_keys, const uint64_t *conf_vals,
                                   const uint32_t *conf_count, uint8_t *arena, uint8_t *changed, uint32_t *host_count);
 hipError_t launch_pfadd_commit(hipStream_t st, uint64_t n, const uint64_t *rec, const uint32_t *cmd_of, uint8_t *arena,
@@ -36,7 +36,7 @@ hipError_t launch_hll_union(hipStream_t st, uint64_t n, const uint32_t *ids, con
                             uint64_t max_groups, uint8_t *out, int include_out);
 hipError_t launch_bloom_contains(hipStream_t st, uint64_t n, const uint64_t *off, const uint8_t *bytes,
                                  const uint8_t *bits, const uint64_t *d_len, uint64_t size, uint64_t magic, int k,
-                                 uint8_t *out);
+                                 uint8_t *out, int sched);
 hipError_t launch_bloom_probes(hipStream_t st, uint64_t n, const uint64_t *off, const uint8_t *bytes, uint64_t size,
                                uint64_t magic, int k, uint64_t *keys);
 hipError_t launch_bloom_apply(hipStream_t st, uint64_t m, const uint64_t *keys, uint8_t *bits, uint64_t *d_len, int k,

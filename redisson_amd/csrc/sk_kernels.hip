@@ -96,6 +96,7 @@ __global__ void __launch_bounds__(256) k_pfadd_apply(uint64_t n, const uint64_t 
 #define SK_CLAIMED 0x80u
 #define SK_CONFLICT 0x40u
 
+template <bool ALL>
 __global__ void __launch_bounds__(256) k_pfadd_claim(uint64_t n, const uint32_t *__restrict__ key_ids,
                                                      const uint64_t *__restrict__ off,
                                                      const uint8_t *__restrict__ bytes, int v5, uint8_t *arena,
@@ -118,13 +119,20 @@ __global__ void __launch_bounds__(256) k_pfadd_claim(uint64_t n, const uint32_t 
     hll_pat(h, v5, &reg, &rho);
     uint64_t slot = (uint64_t(key_ids[i]) << 14) | reg;
     uint8_t *p = arena + slot;
+    uint32_t sh = uint32_t(slot & 3) * 8u;
+    uint32_t *w = reinterpret_cast<uint32_t *>(arena + (slot & ~uint64_t(3)));
     uint64_t r = 0;
-    if (rho > (uint32_t(*p) & 63u)) { // candidate
-        uint32_t sh = uint32_t(slot & 3) * 8u;
-        uint32_t *w = reinterpret_cast<uint32_t *>(arena + (slot & ~uint64_t(3)));
+    if (ALL) {
+        // every element claims; the atomic's old value is also R0 (one random op, no load)
+        uint32_t old = atomicOr(w, SK_CLAIMED << sh);
+        uint32_t b = (old >> sh) & 0xffu;
+        if (b & SK_CLAIMED) atomicOr(w, SK_CONFLICT << sh);
+        uint32_t cand = rho > (b & 63u);
+        r = (slot << 8) | (uint64_t(cand) << 7) | (uint64_t(rho) << 1) | 1u;
+    } else if (rho > (uint32_t(*p) & 63u)) { // candidates only: load, then claim
         uint32_t old = atomicOr(w, SK_CLAIMED << sh);
         if ((old >> sh) & SK_CLAIMED) atomicOr(w, SK_CONFLICT << sh);
-        r = (slot << 7) | (uint64_t(rho) << 1) | 1u;
+        r = (slot << 8) | (1u << 7) | (uint64_t(rho) << 1) | 1u;
     }
     rec[i] = r;
 }
@@ -137,20 +145,26 @@ __global__ void __launch_bounds__(256) k_pfadd_commit(uint64_t n, const uint64_t
     if (i >= n) return;
     uint64_t r = rec[i];
     if (!(r & 1u)) return;
-    uint64_t slot = r >> 7;
+    uint64_t slot = r >> 8;
     uint32_t rho = uint32_t(r >> 1) & 63u;
+    bool cand = (r >> 7) & 1u;
     uint32_t cmd = cmd_of ? cmd_of[i] : uint32_t(i);
     uint8_t *p = arena + slot;
-    if (!(*p & SK_CONFLICT)) {
-        *p = uint8_t(rho); // sole candidate: raise and clear the flags
-        changed[cmd] = 1;
+    uint32_t b = *p;
+    if (!(b & SK_CONFLICT)) { // the only claimer of this register
+        if (cand) {
+            *p = uint8_t(rho); // raise and clear the flags
+            changed[cmd] = 1;
+        } else {
+            *p = uint8_t(b & 63u); // non-candidate claimer: just clear the flag
+        }
         return;
     }
     uint32_t k = atomicAdd(conf_count, 1u);
     if (k < conf_cap) {
         conf_keys[k] = (slot << 26) | i; // batch order inside a register
         // R0: the value bits are untouched until the replay writes the register
-        conf_vals[k] = (uint64_t(cmd) << 16) | (uint64_t(*p & 63u) << 8) | rho;
+        conf_vals[k] = (uint64_t(cmd) << 16) | (uint64_t(b & 63u) << 8) | rho;
     }
 }
 
@@ -325,7 +339,52 @@ __device__ __forceinline__ void bloom_hashes(const uint8_t *p, uint32_t len, uin
 }
 
 // contains: probes 0..k-2 only (the k-th GETBIT reply is dropped by
-// result.subList(1, size-1), M:RedissonBloomFilter.java:155), early exit.
+// result.subList(1, size-1), M:RedissonBloomFilter.java:155).  Probes are
+// fetched in rounds of `first` then the rest: all loads of a round are in
+// flight together and the element stops after a round that saw a 0 bit.
+// FIRST = 0 is the fully sequential early exit, FIRST >= k-1 fetches every
+// probe at once; the result is the same AND for every schedule.  Measured at
+// C3 (k = 7, fill 0.50): sequential 100 us / 1M, 2+rest 108, 3+rest 113,
+// all 138 -- line fetches (~55 G/s chip-wide), not latency, bound the kernel.
+template <int FIRST>
+__device__ __forceinline__ uint8_t bloom_probe_and(uint64_t h1, uint64_t h2, int k, const uint8_t *__restrict__ bits,
+                                                   uint64_t slen, uint64_t size, uint64_t magic) {
+    if (FIRST == 0) { // fully sequential early exit: fewest line fetches (the measured best)
+        uint64_t h = h1;
+        for (int j = 0; j < k - 1; j++) {
+            if (!get_bit(bits, slen, mod_invariant(h & 0x7fffffffffffffffull, size, magic))) return 0;
+            h += (j & 1) ? h1 : h2;
+        }
+        return 1;
+    }
+    constexpr int MAXP = 32; // probes held in registers per round
+    uint64_t h = h1;
+    int j = 0;
+    int np = k - 1;
+    int round = FIRST;
+    while (j < np) {
+        int m = np - j < round ? np - j : round;
+        if (m > MAXP) m = MAXP;
+        uint32_t acc = 1;
+        uint64_t idx[MAXP];
+#pragma unroll
+        for (int q = 0; q < MAXP; q++) {
+            if (q < m) {
+                idx[q] = mod_invariant(h & 0x7fffffffffffffffull, size, magic);
+                h += ((j + q) & 1) ? h1 : h2;
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < MAXP; q++)
+            if (q < m) acc &= uint32_t(get_bit(bits, slen, idx[q]));
+        if (!acc) return 0;
+        j += m;
+        round = MAXP; // after the first round: everything left at once
+    }
+    return 1;
+}
+
+template <int FIRST>
 __global__ void __launch_bounds__(256) k_bloom_contains(uint64_t n, const uint64_t *__restrict__ off,
                                                         const uint8_t *__restrict__ bytes,
                                                         const uint8_t *__restrict__ bits,
@@ -348,18 +407,7 @@ __global__ void __launch_bounds__(256) k_bloom_contains(uint64_t n, const uint64
     } else {
         bloom_hashes(bytes + o, len, &h1, &h2);
     }
-    uint64_t slen = *d_len;
-    uint64_t h = h1;
-    uint8_t r = 1;
-    for (int j = 0; j < k - 1; j++) {
-        uint64_t idx = mod_invariant(h & 0x7fffffffffffffffull, size, magic);
-        if (!get_bit(bits, slen, idx)) {
-            r = 0;
-            break;
-        }
-        h += (j & 1) ? h1 : h2;
-    }
-    out[i] = r;
+    out[i] = bloom_probe_and<FIRST>(h1, h2, k, bits, *d_len, size, magic);
 }
 
 // add, pass 1: all k probes -> key = idx << 32 | (elem*k + j)
@@ -671,10 +719,14 @@ hipError_t launch_pfadd_apply(hipStream_t st, uint64_t n, const uint64_t *keys, 
 
 hipError_t launch_pfadd_claim(hipStream_t st, uint64_t n, const uint32_t *key_ids, const uint64_t *off,
                               const uint8_t *bytes, int v5, uint8_t *arena, uint64_t *rec, uint8_t *changed_i,
-                              uint32_t *conf_count) {
+                              uint32_t *conf_count, int claim_all) {
     if (!n) return hipSuccess;
-    hipLaunchKernelGGL(k_pfadd_claim, dim3(grid_for(n, 256)), dim3(256), 0, st, n, key_ids, off, bytes, v5, arena,
-                       rec, changed_i, conf_count);
+    if (claim_all)
+        hipLaunchKernelGGL(k_pfadd_claim<true>, dim3(grid_for(n, 256)), dim3(256), 0, st, n, key_ids, off, bytes, v5,
+                           arena, rec, changed_i, conf_count);
+    else
+        hipLaunchKernelGGL(k_pfadd_claim<false>, dim3(grid_for(n, 256)), dim3(256), 0, st, n, key_ids, off, bytes, v5,
+                           arena, rec, changed_i, conf_count);
     SK_LAUNCH_CHECK();
     return hipSuccess;
 }
@@ -802,10 +854,16 @@ hipError_t launch_hll_union(hipStream_t st, uint64_t n, const uint32_t *ids, con
 
 hipError_t launch_bloom_contains(hipStream_t st, uint64_t n, const uint64_t *off, const uint8_t *bytes,
                                  const uint8_t *bits, const uint64_t *d_len, uint64_t size, uint64_t magic, int k,
-                                 uint8_t *out) {
+                                 uint8_t *out, int sched) {
     if (!n) return hipSuccess;
-    hipLaunchKernelGGL(k_bloom_contains, dim3(grid_for(n, 256)), dim3(256), 0, st, n, off, bytes, bits, d_len, size,
-                       magic, k, out);
+    dim3 g(grid_for(n, 256)), b(256);
+    switch (sched) {
+    case 1: hipLaunchKernelGGL(k_bloom_contains<1>, g, b, 0, st, n, off, bytes, bits, d_len, size, magic, k, out); break;
+    case 3: hipLaunchKernelGGL(k_bloom_contains<3>, g, b, 0, st, n, off, bytes, bits, d_len, size, magic, k, out); break;
+    case 2: hipLaunchKernelGGL(k_bloom_contains<2>, g, b, 0, st, n, off, bytes, bits, d_len, size, magic, k, out); break;
+    case 32: hipLaunchKernelGGL(k_bloom_contains<32>, g, b, 0, st, n, off, bytes, bits, d_len, size, magic, k, out); break;
+    default: hipLaunchKernelGGL(k_bloom_contains<0>, g, b, 0, st, n, off, bytes, bits, d_len, size, magic, k, out);
+    }
     SK_LAUNCH_CHECK();
     return hipSuccess;
 }

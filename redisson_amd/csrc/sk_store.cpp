@@ -14,6 +14,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -215,6 +216,8 @@ struct sk_ctx {
     ncclComm_t comm = nullptr;
 
     bool async_dev = false;     // sk_set_async: _dev calls return without a final sync
+    int claim_all = 1;          // PFADD claim: 1 = every element claims (R0 from the atomic), 0 = load first, claim candidates (SK_PFADD_CLAIM)
+    int bloom_sched = 0;        // contains probe schedule: 0 sequential; 1/2/3/32 = first-round size (SK_BLOOM_SCHED)
     // async PFADD: the conflict count of the last sparse batch is checked ("settled")
     // by the next call that needs the HLL arena, not by the call itself
     bool pf_pending = false;
@@ -542,7 +545,7 @@ int pfadd_sparse(sk_ctx *c, uint64_t n, const uint32_t *d_ids, const uint64_t *d
     { Prof p_(c, 13);
     // one element per command (d_cmd == null): the claim pass also zeroes the replies
     HIPCHK(c, sk::launch_pfadd_claim(c->st, n, d_ids, d_off, d_bytes, c->redis_major >= 5, c->arena,
-                                     c->keys_a.as<uint64_t>(), d_cmd ? nullptr : d_changed, d_cnt)); }
+                                     c->keys_a.as<uint64_t>(), d_cmd ? nullptr : d_changed, d_cnt, c->claim_all)); }
     { Prof p_(c, 14);
     HIPCHK(c, sk::launch_pfadd_commit(c->st, n, c->keys_a.as<uint64_t>(), d_cmd, c->arena, d_changed,
                                       c->keys_b.as<uint64_t>(), c->vals_a.as<uint64_t>(), d_cnt, uint32_t(n)));
@@ -683,6 +686,8 @@ int sk_open(const sk_config *cfg, sk_ctx **out) {
         delete c;
         return SK_EDEVICE;
     }
+    if (const char *e = getenv("SK_BLOOM_SCHED")) c->bloom_sched = atoi(e);
+    if (const char *e = getenv("SK_PFADD_CLAIM")) c->claim_all = atoi(e);
     uint64_t cap = (cfg && cfg->hll_capacity) ? cfg->hll_capacity : 1024;
     if (hll_grow(c, cap) != SK_OK || c->misc.ensure(4096) != hipSuccess ||
         hipMalloc(&c->d_zero, 16) != hipSuccess || hipMemsetAsync(c->d_zero, 0, 16, c->st) != hipSuccess ||
@@ -1594,7 +1599,7 @@ int sk_bloom_contains(sk_ctx *c, const uint8_t *name, uint64_t len, int64_t size
     const uint8_t *bits = id == kNoId ? reinterpret_cast<const uint8_t *>(c->d_zero) : c->strs[id].ptr;
     const uint64_t *dl = id == kNoId ? reinterpret_cast<const uint64_t *>(c->d_zero) : &c->d_dir[id].len;
     HIPCHK(c, sk::launch_bloom_contains(c->st, n, c->in_off.as<uint64_t>(), c->in_bytes.as<uint8_t>(), bits, dl,
-                                        uint64_t(size), magic_for(uint64_t(size)), k, c->out_u8.as<uint8_t>()));
+                                        uint64_t(size), magic_for(uint64_t(size)), k, c->out_u8.as<uint8_t>(), c->bloom_sched));
     HIPCHK(c, hipMemcpyAsync(out, c->out_u8.p, n, hipMemcpyDeviceToHost, c->st));
     return sync(c);
 }
@@ -1635,7 +1640,7 @@ int sk_bloom_contains_dev(sk_ctx *c, const uint8_t *name, uint64_t len, uint64_t
     }
     { Prof p_(c, 5, s);
     HIPCHK(c, sk::launch_bloom_contains(s, n, d_off, d_bytes, bits, dl, uint64_t(b->size),
-                                        magic_for(uint64_t(b->size)), b->k, d_out)); }
+                                        magic_for(uint64_t(b->size)), b->k, d_out, c->bloom_sched)); }
     if (c->async_dev) {
         HIPCHK(c, hipEventRecord(c->ev_r, c->st2));
         c->rd_pending = true;

@@ -261,6 +261,196 @@ __global__ void k_len_from_last_key(const uint64_t *keys, uint64_t m, uint64_t *
     atomicMax((unsigned long long *)d_len, (unsigned long long)need);
 }
 
+
+// ------------------------------------------------- PFADD, partition path
+// One pass hash-partitions the batch into SK_PFP_NB buckets by register slot
+// (every element of a slot lands in one bucket), then one workgroup per bucket
+// resolves it in LDS: records of a slot are chained by an LDS hash table, the
+// earliest (lowest seq) record of each slot loads R0 and writes the final
+// max, and a record replies 1 iff its rho beats R0 and every earlier rho of
+// its slot -- the sequential PFADD result with one random load + one store
+// per touched register and no global atomics.
+//   rec = slot << 26 | seq << 6 | rho   (slot <= 38 bits, seq < 2^20)
+// Buckets larger than SK_PFP_CAP are listed for the host, which sorts just
+// those records by (slot, seq) and walks them (k_pfadd_conflicts_sorted form).
+#define SK_PFP_NB 2048    // buckets (~n/2048 records each)
+#define SK_PFP_TPB 1024   // threads per hash / scatter workgroup (16 waves: one per CU hides the latency)
+#define SK_PFP_EPB 4096   // elements per hash / scatter workgroup
+#define SK_PFP_CAP 2048   // records one apply workgroup holds in LDS
+#define SK_PFP_HT 2048    // LDS hash-chain heads
+#define SK_PFP_STAGE (4 * SK_STAGE_WORDS) // LDS key window (u64 words) for SK_PFP_TPB elements
+__device__ __forceinline__ uint32_t pfp_bucket(uint64_t slot) {
+    return uint32_t((slot * 0x9E3779B97F4A7C15ull) >> 53); // 11 bits
+}
+__device__ __forceinline__ uint32_t pfp_ht(uint64_t slot) {
+    return uint32_t((slot * 0xC2B2AE3D27D4EB4Full) >> 53); // 11 bits
+}
+
+// Hash SK_PFP_EPB elements (keys staged through LDS SK_PFP_TPB at a time),
+// write their records in batch order and the workgroup's bucket histogram,
+// bucket-major, for the scan.  Also zeroes the apply pass's overflow count.
+__global__ void __launch_bounds__(SK_PFP_TPB) k_pfp_hash(uint64_t n, const uint32_t *__restrict__ key_ids,
+                                                         const uint64_t *__restrict__ off,
+                                                         const uint8_t *__restrict__ bytes, int v5,
+                                                         uint64_t *__restrict__ rec, uint32_t *__restrict__ hist,
+                                                         uint32_t nblocks, uint8_t *__restrict__ changed_i,
+                                                         uint32_t *__restrict__ overflow_count) {
+    __shared__ uint32_t h[SK_PFP_NB];
+    __shared__ uint64_t lds[SK_PFP_STAGE];
+    for (uint32_t b = threadIdx.x; b < SK_PFP_NB; b += SK_PFP_TPB) h[b] = 0;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *overflow_count = 0;
+    uint64_t base = uint64_t(blockIdx.x) * SK_PFP_EPB;
+    for (int e = 0; e < SK_PFP_EPB / SK_PFP_TPB; e++) {
+        uint64_t e0 = base + uint64_t(e) * SK_PFP_TPB;
+        if (e0 >= n) break; // uniform
+        uint64_t e1 = e0 + SK_PFP_TPB < n ? e0 + SK_PFP_TPB : n;
+        uint64_t lo = off[e0], hi = off[e1];
+        bool staged = (hi - (lo & ~uint64_t(15))) + 32 <= uint64_t(SK_PFP_STAGE) * 8;
+        __syncthreads(); // h zeroed / the previous window's readers are done
+        uint32_t wbase = staged ? stage_keys(bytes, lo, hi, lds) : 0u;
+        uint64_t i = e0 + threadIdx.x;
+        if (i < n) {
+            if (changed_i) changed_i[i] = 0;
+            uint64_t o = off[i];
+            uint32_t len = uint32_t(off[i + 1] - o);
+            uint64_t hh = staged ? murmur64a_r(LdsReader{lds, wbase + uint32_t(o - lo)}, len, 0xadc83b19ull)
+                                 : murmur64a(bytes + o, len, 0xadc83b19ull);
+            uint32_t reg, rho;
+            hll_pat(hh, v5, &reg, &rho);
+            uint64_t slot = (uint64_t(key_ids[i]) << 14) | reg;
+            rec[i] = (slot << 26) | (i << 6) | rho;
+            atomicAdd(&h[pfp_bucket(slot)], 1u);
+        }
+    }
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < SK_PFP_NB; b += SK_PFP_TPB) hist[uint64_t(b) * nblocks + blockIdx.x] = h[b];
+}
+
+// hist (bucket-major) has been exclusive-scanned into pos; records keep
+// their batch index, so order inside a bucket does not matter
+__global__ void __launch_bounds__(SK_PFP_TPB) k_pfp_scatter(uint64_t n, const uint64_t *__restrict__ rec,
+                                                            const uint32_t *__restrict__ pos, uint32_t nblocks,
+                                                            uint64_t *__restrict__ out) {
+    __shared__ uint32_t cur[SK_PFP_NB];
+    for (uint32_t b = threadIdx.x; b < SK_PFP_NB; b += SK_PFP_TPB) cur[b] = pos[uint64_t(b) * nblocks + blockIdx.x];
+    __syncthreads();
+    uint64_t base = uint64_t(blockIdx.x) * SK_PFP_EPB;
+    uint64_t r[SK_PFP_EPB / SK_PFP_TPB];
+#pragma unroll
+    for (int e = 0; e < SK_PFP_EPB / SK_PFP_TPB; e++) {
+        uint64_t i = base + uint64_t(e) * SK_PFP_TPB + threadIdx.x;
+        r[e] = i < n ? rec[i] : ~0ull;
+    }
+#pragma unroll
+    for (int e = 0; e < SK_PFP_EPB / SK_PFP_TPB; e++) {
+        if (r[e] == ~0ull) continue;
+        uint32_t d = atomicAdd(&cur[pfp_bucket(r[e] >> 26)], 1u);
+        out[d] = r[e];
+    }
+}
+
+// One workgroup per bucket.  Phase A: chain walk -> each record's earliest
+// same-slot record, the max rho of its earlier records and of the whole slot;
+// phase B: the earliest records load R0 (independent loads, all in flight);
+// phase C: replies and the final register store.
+__global__ void __launch_bounds__(256) k_pfp_apply(uint64_t n, const uint64_t *__restrict__ recs,
+                                                   const uint32_t *__restrict__ pos, uint32_t nblocks,
+                                                   const uint32_t *__restrict__ cmd_of, uint8_t *arena,
+                                                   uint8_t *__restrict__ changed, uint32_t *overflow_list,
+                                                   uint32_t *overflow_count) {
+    __shared__ uint64_t R[SK_PFP_CAP];
+    __shared__ uint16_t nxt[SK_PFP_CAP];
+    __shared__ uint32_t head[SK_PFP_HT];
+    __shared__ uint8_t r0[SK_PFP_CAP];
+    uint32_t b = blockIdx.x;
+    uint64_t lo = pos[uint64_t(b) * nblocks];
+    uint64_t hi = (b + 1 < SK_PFP_NB) ? pos[uint64_t(b + 1) * nblocks] : n;
+    uint32_t cnt = uint32_t(hi - lo);
+    if (cnt == 0) return;
+    if (cnt > SK_PFP_CAP) { // left for the host (sorted walk of this bucket)
+        if (threadIdx.x == 0) overflow_list[atomicAdd(overflow_count, 1u)] = b;
+        return;
+    }
+    for (uint32_t t = threadIdx.x; t < SK_PFP_HT; t += 256) head[t] = 0xffffu;
+    __syncthreads();
+    for (uint32_t t = threadIdx.x; t < cnt; t += 256) {
+        uint64_t r = recs[lo + t];
+        R[t] = r;
+        nxt[t] = uint16_t(atomicExch(&head[pfp_ht(r >> 26)], t));
+    }
+    __syncthreads();
+    constexpr int PER = SK_PFP_CAP / 256;
+    uint32_t first[PER], pm[PER], mx[PER];
+#pragma unroll
+    for (int q = 0; q < PER; q++) {
+        uint32_t t = threadIdx.x + q * 256;
+        first[q] = 0xffffffffu;
+        if (t >= cnt) continue;
+        uint64_t rt = R[t], slot = rt >> 26, seq = (rt >> 6) & 0xfffffu;
+        uint32_t rho = uint32_t(rt & 63u);
+        uint32_t f = t, p = 0, m = rho;
+        uint64_t fseq = seq;
+        for (uint32_t u = head[pfp_ht(slot)]; u != 0xffffu; u = nxt[u]) {
+            uint64_t ru = R[u];
+            if ((ru >> 26) != slot) continue;
+            uint32_t rhou = uint32_t(ru & 63u);
+            uint64_t sequ = (ru >> 6) & 0xfffffu;
+            m = rhou > m ? rhou : m;
+            if (sequ < seq) p = rhou > p ? rhou : p;
+            if (sequ < fseq) {
+                fseq = sequ;
+                f = u;
+            }
+        }
+        first[q] = f;
+        pm[q] = p;
+        mx[q] = m;
+    }
+    uint32_t ld[PER];
+#pragma unroll
+    for (int q = 0; q < PER; q++) {
+        uint32_t t = threadIdx.x + q * 256;
+        ld[q] = first[q] == t ? uint32_t(arena[R[t] >> 26]) : 0u;
+    }
+#pragma unroll
+    for (int q = 0; q < PER; q++) {
+        uint32_t t = threadIdx.x + q * 256;
+        if (first[q] == t) r0[t] = uint8_t(ld[q] & 63u);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < PER; q++) {
+        uint32_t t = threadIdx.x + q * 256;
+        if (t >= cnt) continue;
+        uint64_t rt = R[t], slot = rt >> 26, seq = (rt >> 6) & 0xfffffu;
+        uint32_t rho = uint32_t(rt & 63u);
+        uint32_t R0 = r0[first[q]];
+        if (rho > (R0 > pm[q] ? R0 : pm[q])) changed[cmd_of ? cmd_of[seq] : uint32_t(seq)] = 1;
+        if (first[q] == t && mx[q] > R0) arena[slot] = uint8_t(mx[q]);
+    }
+}
+
+// host fallback for an oversized bucket: records sorted by (slot, seq); the
+// first record of each slot walks them in batch order
+__global__ void __launch_bounds__(256) k_pfp_sorted_walk(uint64_t cnt, const uint64_t *__restrict__ K,
+                                                         const uint32_t *__restrict__ cmd_of, uint8_t *arena,
+                                                         uint8_t *__restrict__ changed) {
+    uint64_t t = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (t >= cnt) return;
+    uint64_t slot = K[t] >> 26;
+    if (t > 0 && (K[t - 1] >> 26) == slot) return;
+    uint32_t R = uint32_t(arena[slot]) & 63u, R0 = R;
+    for (uint64_t u = t; u < cnt && (K[u] >> 26) == slot; u++) {
+        uint32_t rho = uint32_t(K[u] & 63u);
+        if (rho > R) {
+            uint32_t seq = uint32_t((K[u] >> 6) & 0xfffffu);
+            changed[cmd_of ? cmd_of[seq] : seq] = 1;
+            R = rho;
+        }
+    }
+    if (R != R0) arena[slot] = uint8_t(R);
+}
+
 // -------------------------------------------------------------- histogram
 // One 256-thread workgroup per key: 16 KiB of registers read as 4 x 16 B
 // per lane (coalesced), counted into per-wave LDS histograms.
@@ -759,6 +949,58 @@ hipError_t launch_pfadd_conflicts_sorted(hipStream_t st, uint64_t cnt, const uin
 }
 
 uint32_t pfadd_conflict_lds_capacity() { return SK_CONF_MAX; }
+
+
+uint32_t pfp_blocks(uint64_t n) { return uint32_t((n + SK_PFP_EPB - 1) / SK_PFP_EPB); }
+uint32_t pfp_buckets() { return SK_PFP_NB; }
+uint32_t pfp_cap() { return SK_PFP_CAP; }
+
+hipError_t pfp_scan_size(uint64_t m, size_t *bytes) {
+    size_t sz = 0;
+    hipError_t e = rocprim::exclusive_scan(nullptr, sz, (const uint32_t *)nullptr, (uint32_t *)nullptr, 0u,
+                                           size_t(m), rocprim::plus<uint32_t>());
+    *bytes = sz;
+    return e;
+}
+
+// hash + per-block bucket histograms -> scan -> stable-enough scatter -> per-bucket LDS resolve
+hipError_t launch_pfp(hipStream_t st, uint64_t n, const uint32_t *key_ids, const uint64_t *off, const uint8_t *bytes,
+                      int v5, const uint32_t *cmd_of, uint8_t *arena, uint8_t *changed, uint8_t *changed_i,
+                      uint64_t *rec, uint64_t *rec_out, uint32_t *hist, uint32_t *pos, void *tmp, size_t tmp_bytes,
+                      uint32_t *overflow_list, uint32_t *overflow_count) {
+    if (!n) return hipSuccess;
+    uint32_t nb = pfp_blocks(n);
+    hipLaunchKernelGGL(k_pfp_hash, dim3(nb), dim3(SK_PFP_TPB), 0, st, n, key_ids, off, bytes, v5, rec, hist, nb,
+                       changed_i, overflow_count);
+    SK_LAUNCH_CHECK();
+    size_t sz = tmp_bytes;
+    hipError_t e = rocprim::exclusive_scan(tmp, sz, hist, pos, 0u, size_t(uint64_t(SK_PFP_NB) * nb),
+                                           rocprim::plus<uint32_t>(), st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_pfp_scatter, dim3(nb), dim3(SK_PFP_TPB), 0, st, n, rec, pos, nb, rec_out);
+    SK_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_pfp_apply, dim3(SK_PFP_NB), dim3(256), 0, st, n, rec_out, pos, nb, cmd_of, arena, changed,
+                       overflow_list, overflow_count);
+    SK_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+__global__ void k_publish_u32(const uint32_t *src, uint32_t *dst) { *dst = *src; }
+
+hipError_t launch_publish_u32(hipStream_t st, const uint32_t *src, uint32_t *dst_host_mapped) {
+    hipLaunchKernelGGL(k_publish_u32, dim3(1), dim3(1), 0, st, src, dst_host_mapped);
+    SK_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+hipError_t launch_pfp_sorted_walk(hipStream_t st, uint64_t cnt, const uint64_t *K, const uint32_t *cmd_of,
+                                  uint8_t *arena, uint8_t *changed) {
+    if (!cnt) return hipSuccess;
+    hipLaunchKernelGGL(k_pfp_sorted_walk, dim3(grid_for(cnt, 256)), dim3(256), 0, st, cnt, K, cmd_of, arena,
+                       changed);
+    SK_LAUNCH_CHECK();
+    return hipSuccess;
+}
 
 hipError_t sort_keys_size(uint64_t n, unsigned begin_bit, unsigned end_bit, size_t *bytes) {
     size_t sz = 0;

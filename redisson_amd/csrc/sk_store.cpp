@@ -216,12 +216,17 @@ struct sk_ctx {
     ncclComm_t comm = nullptr;
 
     bool async_dev = false;     // sk_set_async: _dev calls return without a final sync
+    int pfadd_path = 1;         // 0 claim/commit, 1 partition, 2 sorted (SK_PFADD_PATH); dense batches use 2
     int claim_all = 1;          // PFADD claim: 1 = every element claims (R0 from the atomic), 0 = load first, claim candidates (SK_PFADD_CLAIM)
+    int read_stream = 1;        // async Bloom contains on the read stream st2 (SK_READ_STREAM=0: main stream)
     int bloom_sched = 0;        // contains probe schedule: 0 sequential; 1/2/3/32 = first-round size (SK_BLOOM_SCHED)
     // async PFADD: the conflict count of the last sparse batch is checked ("settled")
     // by the next call that needs the HLL arena, not by the call itself
     bool pf_pending = false;
+    int pf_kind = 0;            // which path is pending: 0 claim/commit, 1 partition
     uint8_t *pf_changed = nullptr;
+    const uint32_t *pf_cmd = nullptr;
+    uint64_t pf_n = 0;
     // read stream: async Bloom contains runs beside the main stream; writers
     // on the main stream wait for ev_r, the read stream waits for ev_w
     hipStream_t st2 = nullptr;
@@ -233,7 +238,7 @@ struct sk_ctx {
     // workspace
     uint32_t *d_zero = nullptr; // device u32[4] zeros: id 0 / empty length
     DBuf keys_a, keys_b, vals_a, vals_b, sort_tmp, in_off, in_bytes, in_ids, in_cmd, out_u8, misc, partial, hist,
-        uni, ptrs;
+        uni, ptrs, hist_a, hist_b, ovf;
 };
 
 namespace {
@@ -552,16 +557,20 @@ int pfadd_sparse(sk_ctx *c, uint64_t n, const uint32_t *d_ids, const uint64_t *d
     HIPCHK(c, sk::launch_pfadd_conflicts(c->st, c->keys_b.as<uint64_t>(), c->vals_a.as<uint64_t>(), d_cnt, c->arena,
                                          d_changed, c->d_h_cnt)); }
     c->pf_pending = true;
+    c->pf_kind = 0;
     c->pf_changed = d_changed;
     if (c->async_dev) return SK_OK; // settled by the next call that needs the HLL arena
     return pfadd_settle(c);
 }
 
 // the conflict count of the last sparse batch decides whether the long-list path is needed
+int pfp_settle(sk_ctx *c, uint32_t novf);
+
 int pfadd_settle(sk_ctx *c) {
     c->pf_pending = false;
     HIPCHK(c, hipStreamSynchronize(c->st));
     uint32_t cnt = *c->h_cnt;
+    if (c->pf_kind == 1) return cnt ? pfp_settle(c, cnt) : SK_OK;
     if (cnt > sk::pfadd_conflict_lds_capacity()) { // long conflict list: rocPRIM sort + replay
         HIPCHK(c, c->vals_b.ensure(uint64_t(cnt) * 8));
         size_t tmp;
@@ -576,12 +585,97 @@ int pfadd_settle(sk_ctx *c) {
     return SK_OK;
 }
 
+// Path choice.  Partition (default): any density.  Claim/commit: expected
+// conflicting fraction ~ (n / touched) / 32768, used while that is small, else
+// the sorted path.
+bool pfadd_uses_sort(sk_ctx *c, uint64_t n, uint64_t touched_keys) {
+    if (c->pfadd_path == 1) return false;
+    if (c->pfadd_path == 2) return true;
+    return !(touched_keys && n <= 2048 * touched_keys && n < (1ull << 26));
+}
+
+// partition path (sk_kernels.hip "PFADD, partition path"); n <= 2^20 per launch
+int pfadd_partition(sk_ctx *c, uint64_t n, const uint32_t *d_ids, const uint64_t *d_off, const uint8_t *d_bytes,
+                    const uint32_t *d_cmd, uint8_t *d_changed) {
+    if (n > (1ull << 20) || c->hll_next >= (1ull << 24)) return fail(c, SK_EINVAL, "PFADD partition batch too large");
+    uint32_t nb = sk::pfp_blocks(n);
+    uint64_t hn = uint64_t(sk::pfp_buckets()) * nb;
+    size_t tmp;
+    HIPCHK(c, sk::pfp_scan_size(hn, &tmp));
+    HIPCHK(c, c->sort_tmp.ensure(std::max<size_t>(tmp, 16)));
+    HIPCHK(c, c->keys_a.ensure(n * 8));
+    HIPCHK(c, c->keys_b.ensure(n * 8));
+    HIPCHK(c, c->hist_a.ensure(hn * 4));
+    HIPCHK(c, c->hist_b.ensure(hn * 4));
+    HIPCHK(c, c->ovf.ensure(sk::pfp_buckets() * 4 + 64));
+    uint32_t *ovf_count = reinterpret_cast<uint32_t *>(c->ovf.as<uint8_t>() + sk::pfp_buckets() * 4);
+    { Prof p_(c, 13);
+    HIPCHK(c, sk::launch_pfp(c->st, n, d_ids, d_off, d_bytes, c->redis_major >= 5, d_cmd, c->arena, d_changed,
+                             d_cmd ? nullptr : d_changed, c->keys_a.as<uint64_t>(), c->keys_b.as<uint64_t>(),
+                             c->hist_a.as<uint32_t>(), c->hist_b.as<uint32_t>(), c->sort_tmp.p, c->sort_tmp.cap,
+                             c->ovf.as<uint32_t>(), ovf_count));
+    HIPCHK(c, sk::launch_publish_u32(c->st, ovf_count, c->d_h_cnt)); }
+    c->pf_pending = true;
+    c->pf_kind = 1;
+    c->pf_changed = d_changed;
+    c->pf_cmd = d_cmd;
+    c->pf_n = n;
+    if (c->async_dev) return SK_OK;
+    return pfadd_settle(c);
+}
+
+// oversized buckets of the last partition batch: sort their records by (slot, seq) and walk
+int pfp_settle(sk_ctx *c, uint32_t novf) {
+    uint32_t nb = sk::pfp_blocks(c->pf_n);
+    std::vector<uint32_t> buckets(novf);
+    HIPCHK(c, hipMemcpy(buckets.data(), c->ovf.p, novf * 4, hipMemcpyDeviceToHost));
+    for (uint32_t bkt : buckets) {
+        uint32_t lo, hi;
+        HIPCHK(c, hipMemcpy(&lo, c->hist_b.as<uint32_t>() + uint64_t(bkt) * nb, 4, hipMemcpyDeviceToHost));
+        if (bkt + 1 < sk::pfp_buckets()) {
+            HIPCHK(c, hipMemcpy(&hi, c->hist_b.as<uint32_t>() + uint64_t(bkt + 1) * nb, 4, hipMemcpyDeviceToHost));
+        } else {
+            hi = uint32_t(c->pf_n);
+        }
+        uint64_t m = hi - lo;
+        HIPCHK(c, c->vals_a.ensure(m * 8));
+        size_t tmp;
+        HIPCHK(c, sk::sort_keys_size(m, 0, 64, &tmp));
+        HIPCHK(c, c->sort_tmp.ensure(tmp));
+        HIPCHK(c, sk::sort_keys(c->st, c->sort_tmp.p, c->sort_tmp.cap, c->keys_b.as<uint64_t>() + lo,
+                                c->vals_a.as<uint64_t>(), m, 0, 64));
+        HIPCHK(c, sk::launch_pfp_sorted_walk(c->st, m, c->vals_a.as<uint64_t>(), c->pf_cmd, c->arena,
+                                             c->pf_changed));
+    }
+    HIPCHK(c, hipStreamSynchronize(c->st));
+    return SK_OK;
+}
+
 int pfadd_device(sk_ctx *c, uint64_t n, const uint32_t *d_ids, const uint64_t *d_off, const uint8_t *d_bytes,
                  const uint32_t *d_cmd, uint64_t n_cmds, uint8_t *d_changed, uint64_t touched_keys) {
     if (!n) return SK_OK;
-    // expected conflicting fraction ~ (n / touched) / 32768: sparse while it is small
-    if (touched_keys && n <= 2048 * touched_keys && n < (1ull << 26))
-        return pfadd_sparse(c, n, d_ids, d_off, d_bytes, d_cmd, d_changed);
+    if (c->pfadd_path == 1) { // partition path, 1M elements per launch
+        for (uint64_t s = 0; s < n; s += (1ull << 20)) {
+            if (c->pf_pending) {
+                int r = pfadd_settle(c);
+                if (r) return r;
+            }
+            uint64_t m = std::min<uint64_t>(1ull << 20, n - s);
+            // element offsets stay absolute; the command index of element s+j is d_cmd[s+j] (or s+j)
+            if (d_cmd == nullptr && s > 0) {
+                int r = pfadd_partition(c, m, d_ids + s, d_off + s, d_bytes, nullptr, d_changed + s);
+                if (r) return r;
+            } else if (d_cmd == nullptr) {
+                int r = pfadd_partition(c, m, d_ids, d_off, d_bytes, nullptr, d_changed);
+                if (r) return r;
+            } else {
+                int r = pfadd_partition(c, m, d_ids + s, d_off + s, d_bytes, d_cmd + s, d_changed);
+                if (r) return r;
+            }
+        }
+        return SK_OK;
+    }
+    if (!pfadd_uses_sort(c, n, touched_keys)) return pfadd_sparse(c, n, d_ids, d_off, d_bytes, d_cmd, d_changed);
     return pfadd_sorted(c, n, d_ids, d_off, d_bytes, d_cmd, n_cmds, d_changed);
 }
 
@@ -687,7 +781,9 @@ int sk_open(const sk_config *cfg, sk_ctx **out) {
         return SK_EDEVICE;
     }
     if (const char *e = getenv("SK_BLOOM_SCHED")) c->bloom_sched = atoi(e);
+    if (const char *e = getenv("SK_READ_STREAM")) c->read_stream = atoi(e);
     if (const char *e = getenv("SK_PFADD_CLAIM")) c->claim_all = atoi(e);
+    if (const char *e = getenv("SK_PFADD_PATH")) c->pfadd_path = atoi(e);
     uint64_t cap = (cfg && cfg->hll_capacity) ? cfg->hll_capacity : 1024;
     if (hll_grow(c, cap) != SK_OK || c->misc.ensure(4096) != hipSuccess ||
         hipMalloc(&c->d_zero, 16) != hipSuccess || hipMemsetAsync(c->d_zero, 0, 16, c->st) != hipSuccess ||
@@ -718,7 +814,8 @@ int sk_close(sk_ctx *c) {
     if (c->d_zero) (void)hipFree(c->d_zero);
     if (c->h_cnt) (void)hipHostFree(c->h_cnt);
     for (DBuf *b : {&c->keys_a, &c->keys_b, &c->vals_a, &c->vals_b, &c->sort_tmp, &c->in_off, &c->in_bytes,
-                    &c->in_ids, &c->in_cmd, &c->out_u8, &c->misc, &c->partial, &c->hist, &c->uni, &c->ptrs})
+                    &c->in_ids, &c->in_cmd, &c->out_u8, &c->misc, &c->partial, &c->hist, &c->uni, &c->ptrs,
+                    &c->hist_a, &c->hist_b, &c->ovf})
         b->release();
     if (c->st2) (void)hipStreamSynchronize(c->st2);
     if (c->ev_w) (void)hipEventDestroy(c->ev_w);
@@ -947,8 +1044,8 @@ int sk_pfadd_dev(sk_ctx *c, uint64_t n, const uint32_t *d_ids, const uint64_t *d
     for (uint64_t s = 0; s < n; s += max_cmds) {
         uint64_t m = std::min(max_cmds, n - s);
         uint64_t live = c->hll_next - c->hll_free.size(); // slabs in use bounds the touched sketches
-        if (!(live && m <= 2048 * live && m < (1ull << 26)))
-            HIPCHK(c, hipMemsetAsync(d_changed + s, 0, m, c->st)); // sorted path sets only the 1s
+        if (pfadd_uses_sort(c, m, live))
+            HIPCHK(c, hipMemsetAsync(d_changed + s, 0, m, c->st)); // the sorted path sets only the 1s
         int r = pfadd_device(c, m, d_ids + s, d_off + s, d_bytes, nullptr, m, d_changed + s, live);
         if (r) return r;
     }
@@ -1633,19 +1730,21 @@ int sk_bloom_contains_dev(sk_ctx *c, const uint8_t *name, uint64_t len, uint64_t
     const uint8_t *bits = id == kNoId ? reinterpret_cast<const uint8_t *>(c->d_zero) : c->strs[id].ptr;
     const uint64_t *dl = id == kNoId ? reinterpret_cast<const uint64_t *>(c->d_zero) : &c->d_dir[id].len;
     // async: run on the read stream after everything already enqueued on the main stream
-    hipStream_t s = c->async_dev ? c->st2 : c->st;
-    if (c->async_dev) {
+    bool rs = c->async_dev && c->read_stream;
+    hipStream_t s = rs ? c->st2 : c->st;
+    if (rs) {
         HIPCHK(c, hipEventRecord(c->ev_w, c->st));
         HIPCHK(c, hipStreamWaitEvent(c->st2, c->ev_w, 0));
     }
     { Prof p_(c, 5, s);
     HIPCHK(c, sk::launch_bloom_contains(s, n, d_off, d_bytes, bits, dl, uint64_t(b->size),
                                         magic_for(uint64_t(b->size)), b->k, d_out, c->bloom_sched)); }
-    if (c->async_dev) {
+    if (rs) {
         HIPCHK(c, hipEventRecord(c->ev_r, c->st2));
         c->rd_pending = true;
         return SK_OK;
     }
+    if (c->async_dev) return SK_OK;
     return sync(c);
 }
 

@@ -330,3 +330,50 @@ def test_edge_cases(engine, O):
     # STRLEN of an HLL is its dense size; GET of a missing key is None
     assert engine.strlen(b"edge:new") == 12304
     assert engine.get(b"edge:none") is None
+
+
+@pytest.mark.parametrize("path,claim", [("0", "0"), ("0", "1"), ("1", "1"), ("2", "1")])
+def test_pfadd_paths_agree(O, path, claim):
+    """Every PFADD path (claim/commit with either claim form, partition, sorted)
+    gives the oracle's registers and replies, dense and sparse, with
+    intra-batch collisions and an oversized partition bucket."""
+    import os
+    from redisson_amd import SketchEngine
+    os.environ["SK_PFADD_PATH"], os.environ["SK_PFADD_CLAIM"] = path, claim
+    try:
+        e = SketchEngine(device=0)
+    finally:
+        del os.environ["SK_PFADD_PATH"], os.environ["SK_PFADD_CLAIM"]
+    try:
+        for nkeys, n, dup in [(300, 40000, 0.2), (3, 60000, 0.1), (1, 3000, 0.0)]:
+            rng = np.random.default_rng(nkeys)
+            els = _elems(0x5EED0300 + nkeys, n)
+            els += [els[i] for i in rng.integers(0, n, int(n * dup))]
+            names = [b"pp:%d:%d" % (nkeys, i) for i in range(nkeys)]
+            ids = e.hll_resolve(names)
+            kid = rng.integers(0, nkeys, len(els)).astype(np.uint32)
+            off, buf = O.pack(els)
+            d = [e.to_device(ids[kid]), e.to_device(off), e.to_device(buf, pad=16), e.alloc(len(els))]
+            e.pfadd_dev(len(els), d[0], d[1], d[2], int(off[-1]), d[3])
+            regs, want = O.HLLStore().pfadd_bulk(kid, off, buf, nkeys)
+            assert np.array_equal(d[3].download(np.uint8, len(els)), want)
+            for i, nm in enumerate(names):
+                np.testing.assert_array_equal(e.hll_registers(nm), regs[i])
+            # host path with multi-element commands through the same path
+            keys = [names[i % nkeys] for i in range(500)]
+            el2 = [[bytes([j % 256, i % 256]) * (j % 7) for j in range(i % 5)] for i in range(500)]
+            ref = O.HLLStore()
+            ref.regs = {nm: e.hll_registers(nm).copy() for nm in names}
+            assert e.pfadd(keys, el2) == ref.pfadd(keys, el2)
+            for nm in names:
+                np.testing.assert_array_equal(e.hll_registers(nm), ref.regs[nm])
+        # one register hit by 5000 copies of one element: oversized partition bucket -> host sort
+        same = [b"same-element"] * 5000
+        off, buf = O.pack(same)
+        ids = e.hll_resolve([b"pp:same"])
+        d = [e.to_device(np.repeat(ids, 5000)), e.to_device(off), e.to_device(buf, pad=16), e.alloc(5000)]
+        e.pfadd_dev(5000, d[0], d[1], d[2], int(off[-1]), d[3])
+        r = d[3].download(np.uint8, 5000)
+        assert r[0] == 1 and not r[1:].any()
+    finally:
+        e.close()

@@ -29,9 +29,13 @@ sys.path.insert(0, ROOT)
 
 from redisson_amd import SketchEngine, device_count, owner  # noqa: E402
 
+PROF_STEPS = 5          # steps in each per-kernel breakdown pass (outside the timed region)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-PHASES = ["pfadd_claim", "pfadd_commit", "pfadd_hash", "pfadd_sort", "pfadd_apply", "bloom_contains"]
-HLL_PHASES = PHASES[:5]
+# in-library event-timed phases (sk_prof_*): one kernel each, except pfadd_sort
+# (rocPRIM onesweep passes) and pfp_scan (rocPRIM scan); only the path in use has launches
+HLL_PHASES = ["pfp_hash", "pfp_scan", "pfp_scatter", "pfp_apply", "pfp_big",
+              "pfadd_claim", "pfadd_commit", "pfadd_hash", "pfadd_sort", "pfadd_apply"]
+PHASES = HLL_PHASES + ["bloom_contains"]
 
 
 def log(*a):
@@ -93,7 +97,7 @@ def main():
     ids = eng.hll_resolve(mine)
     rng = np.random.default_rng(0x5EED0002 + rank)
 
-    nsteps = W + K
+    nsteps = W + K + 2 * PROF_STEPS   # warmup, overlapped breakdown, timed, isolated breakdown: fresh inputs each
     seed_h = 0x5EED0002
     base_h = rank << 40                      # disjoint element streams per rank
     h_off, h_bytes, h_total = eng.gen_jackson_longs_dev(seed_h, nsteps * B, first=base_h)
@@ -133,50 +137,65 @@ def main():
         eng.pfadd_dev(B, d_ids.ptr + s * B * 4, h_off.ptr + s * B * 8, h_bytes, h_total, d_changed)
         eng.bloom_contains_dev(bloom, B, c_off.ptr + s * B * 8, c_bytes, c_total, d_contains)
 
+    P = PROF_STEPS
     for s in range(W):
         step(s)
     eng.sync()
 
+    def profiled(first, mode_async):
+        """Per-phase device time over P fresh steps (every launch event-timed)."""
+        eng.set_async(mode_async)
+        eng.prof_only(None)
+        eng.prof_reset()
+        eng.prof_enable(True)
+        for s in range(first, first + P):
+            step(s)
+        eng.sync()
+        eng.prof_enable(False)
+        eng.set_async(False)
+        r = {p: eng.prof_read(p) for p in PHASES}
+        return {p: r[p][1] / r[p][0] for p in PHASES if r[p][0]}
+
+    # breakdown as in the timed region (PFADD on the main stream, contains on the
+    # read stream, no host sync): picks the kernel with the most device time
+    over_ms = profiled(W, True)
+    dom = max([p for p in over_ms if p not in ("pfadd_sort", "pfp_scan")], key=lambda p: over_ms[p])
+
     # ------------------------------------------------------------ timed region
-    eng.set_async(True)          # one host sync per step (PFADD's conflict-count readback)
+    # async: PFADD batches never wait on the host; only `dom` is event-timed
+    T0 = W + P
+    eng.set_async(True)
+    eng.prof_only(dom)
     eng.prof_reset()
     eng.prof_enable(True)
     barrier(pg)
     eng.sync()
     t0 = time.perf_counter()
     eng.timer_record(0)
-    for s in range(W, W + K):
+    for s in range(T0, T0 + K):
         step(s)
     eng.timer_record(1)
     eng.sync()
     t1 = time.perf_counter()
     barrier(pg)
     eng.prof_enable(False)
+    eng.prof_only(None)
     eng.set_async(False)
     wall = allmax(pg, t1 - t0)
     dev_ms = eng.timer_elapsed_ms(0, 1)
-    prof = {p: eng.prof_read(p) for p in PHASES}
+    n_launch, tot_ms = eng.prof_read(dom)
 
     units = 2 * B * K * world
     value = units / wall
-    hll_ms = sum(prof[p][1] for p in HLL_PHASES)
-    bl_ms = prof["bloom_contains"][1]
     # roofline of the dominant kernel: algorithmic bytes per unit (SURVEY 8d) x units / avg launch time
-    dom = max(PHASES, key=lambda p: prof[p][1])
     per_unit = per_unit_of(dom, mean_len_h, mean_len_b, k)
-    n_launch, tot_ms = prof[dom]
     avg_ms = tot_ms / max(n_launch, 1)
     achieved = per_unit * B / (avg_ms * 1e-3) / 1e9
 
-    # the same kernels measured alone (sync mode, no overlap between PFADD and contains)
-    eng.prof_reset()
-    eng.prof_enable(True)
-    for s in range(W, min(W + K, W + 5)):
-        step(s)
-    eng.sync()
-    eng.prof_enable(False)
-    iso = {p: eng.prof_read(p) for p in PHASES}
-    iso_ms = {p: iso[p][1] / max(iso[p][0], 1) for p in PHASES}
+    # the same kernels measured alone (sync mode: no overlap between PFADD and contains)
+    iso_ms = profiled(T0 + K, False)
+    hll_ms = sum(v for p, v in iso_ms.items() if p in HLL_PHASES)
+    bl_ms = iso_ms["bloom_contains"]
     iso_dom_ms = iso_ms["bloom_contains"]
     iso_achieved = per_unit_of("bloom_contains", mean_len_h, mean_len_b, k) * B / (iso_dom_ms * 1e-3) / 1e9
     traffic = pmc_traffic(dom)
@@ -205,16 +224,18 @@ def main():
             "batch": B, "tenants": args.tenants, "bloom_bits": size, "bloom_k": k, "bloom_fill": fill,
             "partitioner": "calcSlot(key) %% %d" % world,
         },
-        "hll_inserts_per_s": B * K * world / (hll_ms * 1e-3) if hll_ms else None,
-        "bloom_contains_per_s": B * K * world / (bl_ms * 1e-3) if bl_ms else None,
+        # device-time rates of each chain run alone (roofline_isolated's launches), whole job
+        "hll_inserts_per_s": B * world / (hll_ms * 1e-3) if hll_ms else None,
+        "bloom_contains_per_s": B * world / (bl_ms * 1e-3) if bl_ms else None,
         "bloom_add_per_s": fill / add_s if add_s else None,
         "device_ms_timed_region": dev_ms,
-        "kernel_ms_per_launch": {p: (prof[p][1] / max(prof[p][0], 1)) for p in PHASES},
+        "kernel_ms_per_launch": over_ms,   # overlapped breakdown pass (same schedule as the timed region)
         "roofline": {"kernel": dom, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "traffic_source": "profiles/*_pmc_summary.json (FETCH_SIZE+WRITE_SIZE per launch, raw)",
                      "bytes_per_unit": per_unit, "units_per_launch": B, "avg_launch_ms": avg_ms,
-                     "note": "timed region: PFADD and Bloom contains overlap on two streams"},
+                     "note": "avg launch of the dominant kernel, HIP events on its stream inside the timed region "
+                             "(PFADD and Bloom contains overlap on two streams)"},
         "roofline_isolated": {"kernel": "bloom_contains", "achieved": iso_achieved, "peak": HBM_PEAK_GBS,
                               "unit": "GB/s", "frac": iso_achieved / HBM_PEAK_GBS, "avg_launch_ms": iso_dom_ms,
                               "kernel_ms_per_launch": iso_ms},
@@ -229,6 +250,11 @@ def main():
 def per_unit_of(phase, mean_len_h, mean_len_b, k):
     """Algorithmic bytes per unit (SURVEY 8d / DESIGN.md kernel table)."""
     return {
+        "pfp_hash": mean_len_h + 8 + 4 + 8 + 1,        # key bytes + offset + slab id in, record + reply zero out
+        "pfp_scan": 2 * 4 * 2048 * 256 / (1 << 20),    # bucket x block histogram, read + write, per element
+        "pfp_scatter": 8 + 8,                          # record in, record out
+        "pfp_apply": 8 + 64 + 64 + 1,                  # record + register sector load (R0) + store + reply
+        "pfp_big": 0.0,                                # oversized buckets only (none at C2)
         "pfadd_claim": mean_len_h + 8 + 4 + 1 + 8,     # key bytes + offset + slab id + register in, record out
         "pfadd_commit": 8 + 1 + 1,                     # record in, register + reply out
         "pfadd_hash": mean_len_h + 8 + 4 + 8,          # key bytes + offset + slab id in, sort key out
@@ -242,8 +268,9 @@ def pmc_traffic(phase):
     """HBM bytes per launch of the phase's kernel from the newest committed PMC summary (or None)."""
     import glob
 
-    kern = {"bloom_contains": "sk::k_bloom_contains", "pfadd_claim": "sk::k_pfadd_claim",
-            "pfadd_commit": "sk::k_pfadd_commit"}.get(phase)
+    kern = {"bloom_contains": "sk::k_bloom_contains<0>", "pfadd_claim": "sk::k_pfadd_claim",
+            "pfadd_commit": "sk::k_pfadd_commit", "pfp_hash": "sk::k_pfp_hash", "pfp_scatter": "sk::k_pfp_scatter",
+            "pfp_apply": "sk::k_pfp_apply"}.get(phase)
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_summary.json")))
     if not kern or not files:
         return None

@@ -26,7 +26,7 @@ def main(src, tag):
         for r in csv.DictReader(open(os.path.join(src, sub, "run_counter_collection.csv"))):
             if r["Counter_Name"] != ctr:
                 continue
-            acc[r["Kernel_Name"].split("(")[0]].append((float(r["Counter_Value"]) * 1024,
+            acc[r["Kernel_Name"].split("(")[0].replace("void ", "")].append((float(r["Counter_Value"]) * 1024,
                                                       int(r["End_Timestamp"]) - int(r["Start_Timestamp"]),
                                                       int(r["Grid_Size"])))
         for k, v in acc.items():

@@ -94,6 +94,7 @@ SIGNATURES = {
     "sk_timer_elapsed": (c_int, [P, c_int, c_int, P]),
     "sk_set_async": (c_int, [P, c_int]),
     "sk_prof_enable": (c_int, [P, c_int]),
+    "sk_prof_only": (c_int, [P, c_char_p]),
     "sk_prof_reset": (c_int, [P]),
     "sk_prof_read": (c_int, [P, c_char_p, P, P]),
     "sk_comm_unique_id": (c_int, [P]),

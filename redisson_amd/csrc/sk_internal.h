@@ -24,15 +24,13 @@ hipError_t launch_pfadd_conflicts_sorted(hipStream_t st, uint64_t cnt, const uin
 uint32_t pfadd_conflict_lds_capacity();
 uint32_t pfp_blocks(uint64_t n);
 uint32_t pfp_buckets();
-uint32_t pfp_cap();
-hipError_t pfp_scan_size(uint64_t m, size_t *bytes);
-hipError_t launch_pfp(hipStream_t st, uint64_t n, const uint32_t *key_ids, const uint64_t *off, const uint8_t *bytes,
-                      int v5, const uint32_t *cmd_of, uint8_t *arena, uint8_t *changed, uint8_t *changed_i,
-                      uint64_t *rec, uint64_t *rec_out, uint32_t *hist, uint32_t *pos, void *tmp, size_t tmp_bytes,
-                      uint32_t *overflow_list, uint32_t *overflow_count);
-hipError_t launch_publish_u32(hipStream_t st, const uint32_t *src, uint32_t *dst_host_mapped);
-hipError_t launch_pfp_sorted_walk(hipStream_t st, uint64_t cnt, const uint64_t *K, const uint32_t *cmd_of,
-                                  uint8_t *arena, uint8_t *changed);
+uint32_t pfp_epb();
+hipError_t launch_pfp_hash(hipStream_t st, uint64_t n, const uint32_t *key_ids, const uint64_t *off,
+                           const uint8_t *bytes, int v5, uint8_t *changed_i, uint64_t *chunks, uint32_t *S,
+                           uint32_t *big_alloc);
+hipError_t launch_pfp_apply(hipStream_t st, uint64_t n, const uint64_t *chunks, const uint32_t *S,
+                            const uint32_t *cmd_of, uint8_t *arena, uint8_t *changed, uint32_t *big_alloc,
+                            uint64_t *big_keys, uint32_t *big_vals);
 hipError_t sort_keys_size(uint64_t n, unsigned begin_bit, unsigned end_bit, size_t *bytes);
 hipError_t sort_keys(hipStream_t st, void *tmp, size_t tmp_bytes, const uint64_t *in, uint64_t *out, uint64_t n,
                      unsigned begin_bit, unsigned end_bit);

@@ -263,22 +263,30 @@ __global__ void k_len_from_last_key(const uint64_t *keys, uint64_t m, uint64_t *
 
 
 // ------------------------------------------------- PFADD, partition path
-// One pass hash-partitions the batch into SK_PFP_NB buckets by register slot
-// (every element of a slot lands in one bucket), then one workgroup per bucket
-// resolves it in LDS: records of a slot are chained by an LDS hash table, the
-// earliest (lowest seq) record of each slot loads R0 and writes the final
-// max, and a record replies 1 iff its rho beats R0 and every earlier rho of
-// its slot -- the sequential PFADD result with one random load + one store
-// per touched register and no global atomics.
+// Two launches, no global scan and no sort:
+//   k_pfp_hash   one workgroup per SK_PFP_EPB elements: hash, bucket each
+//                record by its register slot (every record of a slot lands in
+//                one bucket), counting-sort the block's records by bucket in
+//                LDS, store them as one coalesced chunk plus the block's
+//                bucket start offsets (bucket-major table S[b][block]);
+//   k_pfp_apply  one workgroup per bucket: gather the bucket's segment from
+//                every block chunk into LDS, chain the records of a slot with
+//                an LDS hash table; the earliest (lowest seq) record of each
+//                slot loads R0 and writes the final max, and a record replies
+//                1 iff its rho beats R0 and every earlier rho of its slot --
+//                the sequential PFADD result with one random load + one store
+//                per touched register and no global atomics.
 //   rec = slot << 26 | seq << 6 | rho   (slot <= 38 bits, seq < 2^20)
-// Buckets larger than SK_PFP_CAP are listed for the host, which sorts just
-// those records by (slot, seq) and walks them (k_pfadd_conflicts_sorted form).
+// Buckets larger than SK_PFP_CAP (hot registers, skew) are resolved by the
+// same workgroup from a (slot, rho) -> min seq table (pfp_big_resolve).
 #define SK_PFP_NB 2048    // buckets (~n/2048 records each)
-#define SK_PFP_TPB 1024   // threads per hash / scatter workgroup (16 waves: one per CU hides the latency)
-#define SK_PFP_EPB 4096   // elements per hash / scatter workgroup
+#define SK_PFP_TPB 1024   // threads per hash workgroup (16 waves: one per CU hides the latency)
+#define SK_PFP_EPB 4096   // elements per hash workgroup = max blocks 256 for n <= 2^20
+#define SK_PFP_ATPB 256   // threads per apply workgroup (one block segment per thread)
 #define SK_PFP_CAP 2048   // records one apply workgroup holds in LDS
 #define SK_PFP_HT 2048    // LDS hash-chain heads
 #define SK_PFP_STAGE (4 * SK_STAGE_WORDS) // LDS key window (u64 words) for SK_PFP_TPB elements
+static_assert(SK_PFP_ATPB * SK_PFP_EPB >= (1 << 20), "one apply thread per hash block");
 __device__ __forceinline__ uint32_t pfp_bucket(uint64_t slot) {
     return uint32_t((slot * 0x9E3779B97F4A7C15ull) >> 53); // 11 bits
 }
@@ -286,23 +294,51 @@ __device__ __forceinline__ uint32_t pfp_ht(uint64_t slot) {
     return uint32_t((slot * 0xC2B2AE3D27D4EB4Full) >> 53); // 11 bits
 }
 
-// Hash SK_PFP_EPB elements (keys staged through LDS SK_PFP_TPB at a time),
-// write their records in batch order and the workgroup's bucket histogram,
-// bucket-major, for the scan.  Also zeroes the apply pass's overflow count.
+// exclusive scan of one value per thread over a workgroup of NT threads;
+// `wsum` is LDS scratch of NT/64 words; returns the exclusive prefix, *total = sum
+template <int NT> __device__ __forceinline__ uint32_t block_exscan(uint32_t v, uint32_t *wsum, uint32_t *total) {
+    uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int s = 1; s < 64; s <<= 1) {
+        uint32_t y = __shfl_up(x, s);
+        if (lane >= uint32_t(s)) x += y;
+    }
+    if (lane == 63) wsum[w] = x;
+    __syncthreads();
+    uint32_t base = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < NT / 64; i++) {
+        uint32_t t = wsum[i];
+        base += i < int(w) ? t : 0u;
+        tot += t;
+    }
+    __syncthreads(); // wsum reusable
+    *total = tot;
+    return base + x - v;
+}
+
 __global__ void __launch_bounds__(SK_PFP_TPB) k_pfp_hash(uint64_t n, const uint32_t *__restrict__ key_ids,
                                                          const uint64_t *__restrict__ off,
                                                          const uint8_t *__restrict__ bytes, int v5,
-                                                         uint64_t *__restrict__ rec, uint32_t *__restrict__ hist,
+                                                         uint64_t *__restrict__ chunks, uint32_t *__restrict__ S,
                                                          uint32_t nblocks, uint8_t *__restrict__ changed_i,
-                                                         uint32_t *__restrict__ overflow_count) {
+                                                         uint32_t *__restrict__ big_alloc) {
     __shared__ uint32_t h[SK_PFP_NB];
+    __shared__ uint32_t wsum[SK_PFP_TPB / 64];
+    __shared__ uint64_t lrec[SK_PFP_EPB];
     __shared__ uint64_t lds[SK_PFP_STAGE];
     for (uint32_t b = threadIdx.x; b < SK_PFP_NB; b += SK_PFP_TPB) h[b] = 0;
-    if (blockIdx.x == 0 && threadIdx.x == 0) *overflow_count = 0;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *big_alloc = 0;
+    constexpr int PER = SK_PFP_EPB / SK_PFP_TPB;
     uint64_t base = uint64_t(blockIdx.x) * SK_PFP_EPB;
-    for (int e = 0; e < SK_PFP_EPB / SK_PFP_TPB; e++) {
+    uint64_t r[PER];
+    uint32_t bk[PER], rk[PER];
+#pragma unroll
+    for (int e = 0; e < PER; e++) {
+        r[e] = ~0ull;
         uint64_t e0 = base + uint64_t(e) * SK_PFP_TPB;
-        if (e0 >= n) break; // uniform
+        if (e0 >= n) continue; // uniform
         uint64_t e1 = e0 + SK_PFP_TPB < n ? e0 + SK_PFP_TPB : n;
         uint64_t lo = off[e0], hi = off[e1];
         bool staged = (hi - (lo & ~uint64_t(15))) + 32 <= uint64_t(SK_PFP_STAGE) * 8;
@@ -318,72 +354,173 @@ __global__ void __launch_bounds__(SK_PFP_TPB) k_pfp_hash(uint64_t n, const uint3
             uint32_t reg, rho;
             hll_pat(hh, v5, &reg, &rho);
             uint64_t slot = (uint64_t(key_ids[i]) << 14) | reg;
-            rec[i] = (slot << 26) | (i << 6) | rho;
-            atomicAdd(&h[pfp_bucket(slot)], 1u);
+            r[e] = (slot << 26) | (i << 6) | rho;
+            bk[e] = pfp_bucket(slot);
+            rk[e] = atomicAdd(&h[bk[e]], 1u);
         }
     }
     __syncthreads();
-    for (uint32_t b = threadIdx.x; b < SK_PFP_NB; b += SK_PFP_TPB) hist[uint64_t(b) * nblocks + blockIdx.x] = h[b];
-}
-
-// hist (bucket-major) has been exclusive-scanned into pos; records keep
-// their batch index, so order inside a bucket does not matter
-__global__ void __launch_bounds__(SK_PFP_TPB) k_pfp_scatter(uint64_t n, const uint64_t *__restrict__ rec,
-                                                            const uint32_t *__restrict__ pos, uint32_t nblocks,
-                                                            uint64_t *__restrict__ out) {
-    __shared__ uint32_t cur[SK_PFP_NB];
-    for (uint32_t b = threadIdx.x; b < SK_PFP_NB; b += SK_PFP_TPB) cur[b] = pos[uint64_t(b) * nblocks + blockIdx.x];
+    // bucket starts: two buckets per thread
+    uint32_t c0 = h[2 * threadIdx.x], c1 = h[2 * threadIdx.x + 1], tot;
+    uint32_t st0 = block_exscan<SK_PFP_TPB>(c0 + c1, wsum, &tot);
+    h[2 * threadIdx.x] = st0;
+    h[2 * threadIdx.x + 1] = st0 + c0;
+    S[uint64_t(2 * threadIdx.x) * nblocks + blockIdx.x] = st0;
+    S[uint64_t(2 * threadIdx.x + 1) * nblocks + blockIdx.x] = st0 + c0;
+    if (threadIdx.x == 0) S[uint64_t(SK_PFP_NB) * nblocks + blockIdx.x] = tot;
     __syncthreads();
-    uint64_t base = uint64_t(blockIdx.x) * SK_PFP_EPB;
-    uint64_t r[SK_PFP_EPB / SK_PFP_TPB];
 #pragma unroll
-    for (int e = 0; e < SK_PFP_EPB / SK_PFP_TPB; e++) {
-        uint64_t i = base + uint64_t(e) * SK_PFP_TPB + threadIdx.x;
-        r[e] = i < n ? rec[i] : ~0ull;
+    for (int e = 0; e < PER; e++)
+        if (r[e] != ~0ull) lrec[h[bk[e]] + rk[e]] = r[e];
+    __syncthreads();
+    uint64_t *dst = chunks + base;
+    for (uint32_t t = threadIdx.x; t < tot; t += SK_PFP_TPB) dst[t] = lrec[t];
+}
+
+// ---- oversized buckets: a record replies 1 iff rho > R0 and it is the
+// earliest record of its slot with a rho >= its own; the workgroup builds the
+// table (slot, rho) -> min seq (LDS open addressing, SK_BIG_PROBE slots, then
+// a global table of 2*cnt entries carved from a per-batch arena) and answers
+// from it.  The slot's last prefix maximum (max rho, its earliest record)
+// stores the register: one writer per slot.
+#define SK_BIG_LDS 2048
+#define SK_BIG_PROBE 32
+#define SK_BIG_EMPTY 0xffffffffffffffffull
+__device__ __forceinline__ uint32_t big_hash(uint64_t key) {
+    return uint32_t((key * 0x9E3779B97F4A7C15ull) >> 32);
+}
+__device__ __forceinline__ uint32_t gload_u32(const uint32_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long gload_u64(const unsigned long long *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+struct BigTable {
+    unsigned long long *lk; // LDS keys
+    uint32_t *lv;           // LDS min seq
+    unsigned long long *gk; // global keys
+    uint32_t *gv;
+    uint32_t S;
+
+    __device__ void insert(uint64_t key, uint32_t seq) const {
+        uint32_t h = big_hash(key);
+        for (uint32_t p = 0; p < SK_BIG_PROBE; p++) {
+            uint32_t s = (h + p) & (SK_BIG_LDS - 1);
+            unsigned long long k = lk[s];
+            if (k == SK_BIG_EMPTY) k = atomicCAS(&lk[s], SK_BIG_EMPTY, (unsigned long long)key);
+            if (k == SK_BIG_EMPTY || k == key) {
+                atomicMin(&lv[s], seq);
+                return;
+            }
+        }
+        for (uint32_t s = h % S;; s = s + 1 == S ? 0 : s + 1) { // S >= 2 x distinct keys: terminates
+            unsigned long long k = atomicCAS(&gk[s], SK_BIG_EMPTY, (unsigned long long)key);
+            if (k == SK_BIG_EMPTY || k == key) {
+                atomicMin(&gv[s], seq);
+                return;
+            }
+        }
     }
-#pragma unroll
-    for (int e = 0; e < SK_PFP_EPB / SK_PFP_TPB; e++) {
-        if (r[e] == ~0ull) continue;
-        uint32_t d = atomicAdd(&cur[pfp_bucket(r[e] >> 26)], 1u);
-        out[d] = r[e];
+    // min seq of key, or 0xffffffff if absent (after the insert phase's barrier)
+    __device__ uint32_t find(uint64_t key) const {
+        uint32_t h = big_hash(key);
+        for (uint32_t p = 0; p < SK_BIG_PROBE; p++) {
+            uint32_t s = (h + p) & (SK_BIG_LDS - 1);
+            unsigned long long k = lk[s];
+            if (k == key) return lv[s];
+            if (k == SK_BIG_EMPTY) return 0xffffffffu; // slots only fill: the key was never inserted
+        }
+        for (uint32_t s = h % S;; s = s + 1 == S ? 0 : s + 1) {
+            unsigned long long k = gload_u64(&gk[s]);
+            if (k == key) return gload_u32(&gv[s]);
+            if (k == SK_BIG_EMPTY) return 0xffffffffu;
+        }
+    }
+};
+
+// one bucket segment per thread: records seg[0 .. cnt)
+__device__ void pfp_big_resolve(const uint64_t *seg, uint32_t seg_cnt, uint32_t cnt, void *smem,
+                                uint32_t *big_alloc, uint64_t *big_keys, uint32_t *big_vals,
+                                const uint32_t *__restrict__ cmd_of, uint8_t *arena, uint8_t *__restrict__ changed) {
+    __shared__ uint32_t gbase;
+    unsigned long long *lk = reinterpret_cast<unsigned long long *>(smem);
+    uint32_t *lv = reinterpret_cast<uint32_t *>(lk + SK_BIG_LDS);
+    if (threadIdx.x == 0) gbase = atomicAdd(big_alloc, 2 * cnt);
+    for (uint32_t s = threadIdx.x; s < SK_BIG_LDS; s += blockDim.x) lk[s] = SK_BIG_EMPTY, lv[s] = 0xffffffffu;
+    __syncthreads();
+    BigTable T{lk, lv, reinterpret_cast<unsigned long long *>(big_keys) + gbase, big_vals + gbase, 2 * cnt};
+    for (uint32_t s = threadIdx.x; s < T.S; s += blockDim.x) T.gk[s] = SK_BIG_EMPTY, T.gv[s] = 0xffffffffu;
+    __threadfence();
+    __syncthreads();
+    for (uint32_t t = 0; t < seg_cnt; t++) {
+        uint64_t r = seg[t];
+        T.insert(((r >> 26) << 6) | (r & 63u), uint32_t((r >> 6) & 0xfffffu));
+    }
+    __threadfence();
+    __syncthreads();
+    for (uint32_t t = 0; t < seg_cnt; t++) { // replies (the arena is only read)
+        uint64_t r = seg[t], slot = r >> 26;
+        uint32_t rho = uint32_t(r & 63u), seq = uint32_t((r >> 6) & 0xfffffu);
+        if (rho <= (uint32_t(arena[slot]) & 63u)) continue;
+        bool first = true; // v = rho: no earlier equal rho; v > rho: no earlier larger one
+        for (uint32_t v = rho; v < 52 && first; v++) first = T.find((slot << 6) | v) >= seq;
+        if (first) changed[cmd_of ? cmd_of[seq] : seq] = 1;
+    }
+    __syncthreads();
+    for (uint32_t t = 0; t < seg_cnt; t++) { // the slot's writer
+        uint64_t r = seg[t], slot = r >> 26;
+        uint32_t rho = uint32_t(r & 63u), seq = uint32_t((r >> 6) & 0xfffffu);
+        if (T.find((slot << 6) | rho) != seq) continue;
+        bool top = true;
+        for (uint32_t v = rho + 1; v < 52 && top; v++) top = T.find((slot << 6) | v) == 0xffffffffu;
+        if (top && rho > (uint32_t(arena[slot]) & 63u)) arena[slot] = uint8_t(rho);
     }
 }
 
-// One workgroup per bucket.  Phase A: chain walk -> each record's earliest
+// One workgroup per bucket.  Gather: thread j copies block j's segment of
+// the bucket into LDS.  Phase A: chain walk -> each record's earliest
 // same-slot record, the max rho of its earlier records and of the whole slot;
 // phase B: the earliest records load R0 (independent loads, all in flight);
 // phase C: replies and the final register store.
-__global__ void __launch_bounds__(256) k_pfp_apply(uint64_t n, const uint64_t *__restrict__ recs,
-                                                   const uint32_t *__restrict__ pos, uint32_t nblocks,
-                                                   const uint32_t *__restrict__ cmd_of, uint8_t *arena,
-                                                   uint8_t *__restrict__ changed, uint32_t *overflow_list,
-                                                   uint32_t *overflow_count) {
-    __shared__ uint64_t R[SK_PFP_CAP];
-    __shared__ uint16_t nxt[SK_PFP_CAP];
-    __shared__ uint32_t head[SK_PFP_HT];
-    __shared__ uint8_t r0[SK_PFP_CAP];
-    uint32_t b = blockIdx.x;
-    uint64_t lo = pos[uint64_t(b) * nblocks];
-    uint64_t hi = (b + 1 < SK_PFP_NB) ? pos[uint64_t(b + 1) * nblocks] : n;
-    uint32_t cnt = uint32_t(hi - lo);
-    if (cnt == 0) return;
-    if (cnt > SK_PFP_CAP) { // left for the host (sorted walk of this bucket)
-        if (threadIdx.x == 0) overflow_list[atomicAdd(overflow_count, 1u)] = b;
+__global__ void __launch_bounds__(SK_PFP_ATPB) k_pfp_apply(const uint64_t *__restrict__ chunks,
+                                                           const uint32_t *__restrict__ S, uint32_t nblocks,
+                                                           const uint32_t *__restrict__ cmd_of, uint8_t *arena,
+                                                           uint8_t *__restrict__ changed, uint32_t *big_alloc,
+                                                           uint64_t *big_keys, uint32_t *big_vals) {
+    constexpr uint32_t kSmem = SK_PFP_CAP * 8 + SK_PFP_CAP * 2 + SK_PFP_HT * 4 + SK_PFP_CAP;
+    static_assert(kSmem >= SK_BIG_LDS * 12, "big-bucket table shares the LDS");
+    __shared__ uint64_t smem[(kSmem + 7) / 8];
+    __shared__ uint32_t wsum[SK_PFP_ATPB / 64];
+    uint64_t *R = smem;
+    uint16_t *nxt = reinterpret_cast<uint16_t *>(R + SK_PFP_CAP);
+    uint32_t *head = reinterpret_cast<uint32_t *>(nxt + SK_PFP_CAP);
+    uint8_t *r0 = reinterpret_cast<uint8_t *>(head + SK_PFP_HT);
+    uint32_t b = blockIdx.x, j = threadIdx.x;
+    uint32_t lo = 0, c = 0;
+    if (j < nblocks) {
+        lo = S[uint64_t(b) * nblocks + j];
+        c = S[uint64_t(b + 1) * nblocks + j] - lo;
+    }
+    uint32_t cnt;
+    uint32_t dst = block_exscan<SK_PFP_ATPB>(c, wsum, &cnt);
+    if (cnt == 0) return; // uniform
+    const uint64_t *seg = chunks + uint64_t(j) * SK_PFP_EPB + lo;
+    if (cnt > SK_PFP_CAP) {
+        pfp_big_resolve(seg, c, cnt, smem, big_alloc, big_keys, big_vals, cmd_of, arena, changed);
         return;
     }
-    for (uint32_t t = threadIdx.x; t < SK_PFP_HT; t += 256) head[t] = 0xffffu;
+    for (uint32_t t = threadIdx.x; t < SK_PFP_HT; t += SK_PFP_ATPB) head[t] = 0xffffu;
+    for (uint32_t t = 0; t < c; t++) R[dst + t] = seg[t];
     __syncthreads();
-    for (uint32_t t = threadIdx.x; t < cnt; t += 256) {
-        uint64_t r = recs[lo + t];
-        R[t] = r;
-        nxt[t] = uint16_t(atomicExch(&head[pfp_ht(r >> 26)], t));
-    }
+    for (uint32_t t = threadIdx.x; t < cnt; t += SK_PFP_ATPB)
+        nxt[t] = uint16_t(atomicExch(&head[pfp_ht(R[t] >> 26)], t));
     __syncthreads();
-    constexpr int PER = SK_PFP_CAP / 256;
+    constexpr int PER = SK_PFP_CAP / SK_PFP_ATPB;
     uint32_t first[PER], pm[PER], mx[PER];
 #pragma unroll
     for (int q = 0; q < PER; q++) {
-        uint32_t t = threadIdx.x + q * 256;
+        uint32_t t = threadIdx.x + q * SK_PFP_ATPB;
         first[q] = 0xffffffffu;
         if (t >= cnt) continue;
         uint64_t rt = R[t], slot = rt >> 26, seq = (rt >> 6) & 0xfffffu;
@@ -409,18 +546,18 @@ __global__ void __launch_bounds__(256) k_pfp_apply(uint64_t n, const uint64_t *_
     uint32_t ld[PER];
 #pragma unroll
     for (int q = 0; q < PER; q++) {
-        uint32_t t = threadIdx.x + q * 256;
+        uint32_t t = threadIdx.x + q * SK_PFP_ATPB;
         ld[q] = first[q] == t ? uint32_t(arena[R[t] >> 26]) : 0u;
     }
 #pragma unroll
     for (int q = 0; q < PER; q++) {
-        uint32_t t = threadIdx.x + q * 256;
+        uint32_t t = threadIdx.x + q * SK_PFP_ATPB;
         if (first[q] == t) r0[t] = uint8_t(ld[q] & 63u);
     }
     __syncthreads();
 #pragma unroll
     for (int q = 0; q < PER; q++) {
-        uint32_t t = threadIdx.x + q * 256;
+        uint32_t t = threadIdx.x + q * SK_PFP_ATPB;
         if (t >= cnt) continue;
         uint64_t rt = R[t], slot = rt >> 26, seq = (rt >> 6) & 0xfffffu;
         uint32_t rho = uint32_t(rt & 63u);
@@ -428,27 +565,6 @@ __global__ void __launch_bounds__(256) k_pfp_apply(uint64_t n, const uint64_t *_
         if (rho > (R0 > pm[q] ? R0 : pm[q])) changed[cmd_of ? cmd_of[seq] : uint32_t(seq)] = 1;
         if (first[q] == t && mx[q] > R0) arena[slot] = uint8_t(mx[q]);
     }
-}
-
-// host fallback for an oversized bucket: records sorted by (slot, seq); the
-// first record of each slot walks them in batch order
-__global__ void __launch_bounds__(256) k_pfp_sorted_walk(uint64_t cnt, const uint64_t *__restrict__ K,
-                                                         const uint32_t *__restrict__ cmd_of, uint8_t *arena,
-                                                         uint8_t *__restrict__ changed) {
-    uint64_t t = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-    if (t >= cnt) return;
-    uint64_t slot = K[t] >> 26;
-    if (t > 0 && (K[t - 1] >> 26) == slot) return;
-    uint32_t R = uint32_t(arena[slot]) & 63u, R0 = R;
-    for (uint64_t u = t; u < cnt && (K[u] >> 26) == slot; u++) {
-        uint32_t rho = uint32_t(K[u] & 63u);
-        if (rho > R) {
-            uint32_t seq = uint32_t((K[u] >> 6) & 0xfffffu);
-            changed[cmd_of ? cmd_of[seq] : seq] = 1;
-            R = rho;
-        }
-    }
-    if (R != R0) arena[slot] = uint8_t(R);
 }
 
 // -------------------------------------------------------------- histogram
@@ -953,51 +1069,25 @@ uint32_t pfadd_conflict_lds_capacity() { return SK_CONF_MAX; }
 
 uint32_t pfp_blocks(uint64_t n) { return uint32_t((n + SK_PFP_EPB - 1) / SK_PFP_EPB); }
 uint32_t pfp_buckets() { return SK_PFP_NB; }
-uint32_t pfp_cap() { return SK_PFP_CAP; }
+uint32_t pfp_epb() { return SK_PFP_EPB; }
 
-hipError_t pfp_scan_size(uint64_t m, size_t *bytes) {
-    size_t sz = 0;
-    hipError_t e = rocprim::exclusive_scan(nullptr, sz, (const uint32_t *)nullptr, (uint32_t *)nullptr, 0u,
-                                           size_t(m), rocprim::plus<uint32_t>());
-    *bytes = sz;
-    return e;
-}
 
-// hash + per-block bucket histograms -> scan -> stable-enough scatter -> per-bucket LDS resolve
-hipError_t launch_pfp(hipStream_t st, uint64_t n, const uint32_t *key_ids, const uint64_t *off, const uint8_t *bytes,
-                      int v5, const uint32_t *cmd_of, uint8_t *arena, uint8_t *changed, uint8_t *changed_i,
-                      uint64_t *rec, uint64_t *rec_out, uint32_t *hist, uint32_t *pos, void *tmp, size_t tmp_bytes,
-                      uint32_t *overflow_list, uint32_t *overflow_count) {
-    if (!n) return hipSuccess;
+// hash + block-local bucket sort -> per-bucket LDS resolve; one launcher per stage so each is timed
+hipError_t launch_pfp_hash(hipStream_t st, uint64_t n, const uint32_t *key_ids, const uint64_t *off,
+                           const uint8_t *bytes, int v5, uint8_t *changed_i, uint64_t *chunks, uint32_t *S,
+                           uint32_t *big_alloc) {
     uint32_t nb = pfp_blocks(n);
-    hipLaunchKernelGGL(k_pfp_hash, dim3(nb), dim3(SK_PFP_TPB), 0, st, n, key_ids, off, bytes, v5, rec, hist, nb,
-                       changed_i, overflow_count);
-    SK_LAUNCH_CHECK();
-    size_t sz = tmp_bytes;
-    hipError_t e = rocprim::exclusive_scan(tmp, sz, hist, pos, 0u, size_t(uint64_t(SK_PFP_NB) * nb),
-                                           rocprim::plus<uint32_t>(), st);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_pfp_scatter, dim3(nb), dim3(SK_PFP_TPB), 0, st, n, rec, pos, nb, rec_out);
-    SK_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_pfp_apply, dim3(SK_PFP_NB), dim3(256), 0, st, n, rec_out, pos, nb, cmd_of, arena, changed,
-                       overflow_list, overflow_count);
+    hipLaunchKernelGGL(k_pfp_hash, dim3(nb), dim3(SK_PFP_TPB), 0, st, n, key_ids, off, bytes, v5, chunks, S, nb,
+                       changed_i, big_alloc);
     SK_LAUNCH_CHECK();
     return hipSuccess;
 }
 
-__global__ void k_publish_u32(const uint32_t *src, uint32_t *dst) { *dst = *src; }
-
-hipError_t launch_publish_u32(hipStream_t st, const uint32_t *src, uint32_t *dst_host_mapped) {
-    hipLaunchKernelGGL(k_publish_u32, dim3(1), dim3(1), 0, st, src, dst_host_mapped);
-    SK_LAUNCH_CHECK();
-    return hipSuccess;
-}
-
-hipError_t launch_pfp_sorted_walk(hipStream_t st, uint64_t cnt, const uint64_t *K, const uint32_t *cmd_of,
-                                  uint8_t *arena, uint8_t *changed) {
-    if (!cnt) return hipSuccess;
-    hipLaunchKernelGGL(k_pfp_sorted_walk, dim3(grid_for(cnt, 256)), dim3(256), 0, st, cnt, K, cmd_of, arena,
-                       changed);
+hipError_t launch_pfp_apply(hipStream_t st, uint64_t n, const uint64_t *chunks, const uint32_t *S,
+                            const uint32_t *cmd_of, uint8_t *arena, uint8_t *changed, uint32_t *big_alloc,
+                            uint64_t *big_keys, uint32_t *big_vals) {
+    hipLaunchKernelGGL(k_pfp_apply, dim3(SK_PFP_NB), dim3(SK_PFP_ATPB), 0, st, chunks, S, pfp_blocks(n), cmd_of,
+                       arena, changed, big_alloc, big_keys, big_vals);
     SK_LAUNCH_CHECK();
     return hipSuccess;
 }

@@ -208,8 +208,9 @@ struct sk_ctx {
     };
     std::vector<ProfRec> prof_pending;
     std::vector<hipEvent_t> ev_pool;
-    double prof_ms[16] = {0};
-    uint64_t prof_n[16] = {0};
+    uint32_t prof_mask = 0xffffffffu; // phases timed when prof is on (sk_prof_only)
+    double prof_ms[32] = {0};
+    uint64_t prof_n[32] = {0};
     hipEvent_t timers[16] = {};
 
     // cross-GPU exchange (RCCL over xGMI)
@@ -223,12 +224,12 @@ struct sk_ctx {
     // async PFADD: the conflict count of the last sparse batch is checked ("settled")
     // by the next call that needs the HLL arena, not by the call itself
     bool pf_pending = false;
-    int pf_kind = 0;            // which path is pending: 0 claim/commit, 1 partition
     uint8_t *pf_changed = nullptr;
-    const uint32_t *pf_cmd = nullptr;
-    uint64_t pf_n = 0;
     // read stream: async Bloom contains runs beside the main stream; writers
-    // on the main stream wait for ev_r, the read stream waits for ev_w
+    // on the main stream wait for ev_r, the read stream waits for ev_w when the
+    // main stream may have written bit strings since it last waited (every API
+    // call through ENTER may; device PFADD batches touch only the HLL arena)
+    bool st_wrote_bits = true;
     hipStream_t st2 = nullptr;
     hipEvent_t ev_w = nullptr, ev_r = nullptr;
     bool rd_pending = false;
@@ -283,6 +284,7 @@ int pfadd_settle(sk_ctx *c); // defined with the PFADD core
 #define ENTER(c)                                                                                                       \
     do {                                                                                                               \
         HIPCHK(c, hipSetDevice((c)->device));                                                                          \
+        (c)->st_wrote_bits = true;                                                                                     \
         if ((c)->pf_pending) {                                                                                         \
             int r__ = pfadd_settle(c);                                                                                 \
             if (r__) return r__;                                                                                       \
@@ -296,7 +298,8 @@ int pfadd_settle(sk_ctx *c); // defined with the PFADD core
 // phases timed by sk_prof_* (index = SK_PROF_* in the header)
 const char *kPhaseNames[] = {"pfadd_hash",  "pfadd_sort",   "pfadd_apply", "hll_hist",     "hll_union",
                              "bloom_contains", "bloom_probes", "bloom_sort", "bloom_apply", "setbit",
-                             "getbit",      "bitcount",     "bitop",       "pfadd_claim", "pfadd_commit"};
+                             "getbit",      "bitcount",     "bitop",       "pfadd_claim", "pfadd_commit",
+                             "pfp_hash",    "pfp_scan",     "pfp_scatter", "pfp_apply",    "pfp_big"};
 constexpr int kNumPhases = sizeof(kPhaseNames) / sizeof(kPhaseNames[0]);
 
 hipEvent_t ev_get(sk_ctx *c) {
@@ -315,7 +318,7 @@ struct Prof { // RAII: events around one launch when profiling is on
     hipStream_t s;
     hipEvent_t a = nullptr;
     Prof(sk_ctx *c_, int ph, hipStream_t s_ = nullptr) : c(c_), phase(ph), s(s_ ? s_ : c_->st) {
-        if (c->prof) {
+        if (c->prof && (c->prof_mask >> phase & 1u)) {
             a = ev_get(c);
             (void)hipEventRecord(a, s);
         }
@@ -557,20 +560,17 @@ int pfadd_sparse(sk_ctx *c, uint64_t n, const uint32_t *d_ids, const uint64_t *d
     HIPCHK(c, sk::launch_pfadd_conflicts(c->st, c->keys_b.as<uint64_t>(), c->vals_a.as<uint64_t>(), d_cnt, c->arena,
                                          d_changed, c->d_h_cnt)); }
     c->pf_pending = true;
-    c->pf_kind = 0;
     c->pf_changed = d_changed;
     if (c->async_dev) return SK_OK; // settled by the next call that needs the HLL arena
     return pfadd_settle(c);
 }
 
 // the conflict count of the last sparse batch decides whether the long-list path is needed
-int pfp_settle(sk_ctx *c, uint32_t novf);
 
 int pfadd_settle(sk_ctx *c) {
     c->pf_pending = false;
     HIPCHK(c, hipStreamSynchronize(c->st));
     uint32_t cnt = *c->h_cnt;
-    if (c->pf_kind == 1) return cnt ? pfp_settle(c, cnt) : SK_OK;
     if (cnt > sk::pfadd_conflict_lds_capacity()) { // long conflict list: rocPRIM sort + replay
         HIPCHK(c, c->vals_b.ensure(uint64_t(cnt) * 8));
         size_t tmp;
@@ -594,60 +594,26 @@ bool pfadd_uses_sort(sk_ctx *c, uint64_t n, uint64_t touched_keys) {
     return !(touched_keys && n <= 2048 * touched_keys && n < (1ull << 26));
 }
 
-// partition path (sk_kernels.hip "PFADD, partition path"); n <= 2^20 per launch
+// partition path (sk_kernels.hip "PFADD, partition path"); n <= 2^20 per launch.
+// Exact for every input on the device (oversized buckets: k_pfp_big), so the
+// host never waits on a batch.
 int pfadd_partition(sk_ctx *c, uint64_t n, const uint32_t *d_ids, const uint64_t *d_off, const uint8_t *d_bytes,
                     const uint32_t *d_cmd, uint8_t *d_changed) {
     if (n > (1ull << 20) || c->hll_next >= (1ull << 24)) return fail(c, SK_EINVAL, "PFADD partition batch too large");
     uint32_t nb = sk::pfp_blocks(n);
-    uint64_t hn = uint64_t(sk::pfp_buckets()) * nb;
-    size_t tmp;
-    HIPCHK(c, sk::pfp_scan_size(hn, &tmp));
-    HIPCHK(c, c->sort_tmp.ensure(std::max<size_t>(tmp, 16)));
-    HIPCHK(c, c->keys_a.ensure(n * 8));
-    HIPCHK(c, c->keys_b.ensure(n * 8));
-    HIPCHK(c, c->hist_a.ensure(hn * 4));
-    HIPCHK(c, c->hist_b.ensure(hn * 4));
-    HIPCHK(c, c->ovf.ensure(sk::pfp_buckets() * 4 + 64));
-    uint32_t *ovf_count = reinterpret_cast<uint32_t *>(c->ovf.as<uint8_t>() + sk::pfp_buckets() * 4);
-    { Prof p_(c, 13);
-    HIPCHK(c, sk::launch_pfp(c->st, n, d_ids, d_off, d_bytes, c->redis_major >= 5, d_cmd, c->arena, d_changed,
-                             d_cmd ? nullptr : d_changed, c->keys_a.as<uint64_t>(), c->keys_b.as<uint64_t>(),
-                             c->hist_a.as<uint32_t>(), c->hist_b.as<uint32_t>(), c->sort_tmp.p, c->sort_tmp.cap,
-                             c->ovf.as<uint32_t>(), ovf_count));
-    HIPCHK(c, sk::launch_publish_u32(c->st, ovf_count, c->d_h_cnt)); }
-    c->pf_pending = true;
-    c->pf_kind = 1;
-    c->pf_changed = d_changed;
-    c->pf_cmd = d_cmd;
-    c->pf_n = n;
-    if (c->async_dev) return SK_OK;
-    return pfadd_settle(c);
-}
-
-// oversized buckets of the last partition batch: sort their records by (slot, seq) and walk
-int pfp_settle(sk_ctx *c, uint32_t novf) {
-    uint32_t nb = sk::pfp_blocks(c->pf_n);
-    std::vector<uint32_t> buckets(novf);
-    HIPCHK(c, hipMemcpy(buckets.data(), c->ovf.p, novf * 4, hipMemcpyDeviceToHost));
-    for (uint32_t bkt : buckets) {
-        uint32_t lo, hi;
-        HIPCHK(c, hipMemcpy(&lo, c->hist_b.as<uint32_t>() + uint64_t(bkt) * nb, 4, hipMemcpyDeviceToHost));
-        if (bkt + 1 < sk::pfp_buckets()) {
-            HIPCHK(c, hipMemcpy(&hi, c->hist_b.as<uint32_t>() + uint64_t(bkt + 1) * nb, 4, hipMemcpyDeviceToHost));
-        } else {
-            hi = uint32_t(c->pf_n);
-        }
-        uint64_t m = hi - lo;
-        HIPCHK(c, c->vals_a.ensure(m * 8));
-        size_t tmp;
-        HIPCHK(c, sk::sort_keys_size(m, 0, 64, &tmp));
-        HIPCHK(c, c->sort_tmp.ensure(tmp));
-        HIPCHK(c, sk::sort_keys(c->st, c->sort_tmp.p, c->sort_tmp.cap, c->keys_b.as<uint64_t>() + lo,
-                                c->vals_a.as<uint64_t>(), m, 0, 64));
-        HIPCHK(c, sk::launch_pfp_sorted_walk(c->st, m, c->vals_a.as<uint64_t>(), c->pf_cmd, c->arena,
-                                             c->pf_changed));
-    }
-    HIPCHK(c, hipStreamSynchronize(c->st));
+    HIPCHK(c, c->keys_a.ensure(uint64_t(nb) * sk::pfp_epb() * 8));         // block chunks of records
+    HIPCHK(c, c->hist_a.ensure((uint64_t(sk::pfp_buckets()) + 1) * nb * 4)); // bucket starts per block
+    HIPCHK(c, c->vals_a.ensure(2 * n * 8)); // oversized-bucket tables: 2 entries per record
+    HIPCHK(c, c->vals_b.ensure(2 * n * 4));
+    HIPCHK(c, c->ovf.ensure(64));
+    uint64_t *chunks = c->keys_a.as<uint64_t>();
+    uint32_t *S = c->hist_a.as<uint32_t>(), *big_alloc = c->ovf.as<uint32_t>();
+    { Prof p_(c, 15);
+    HIPCHK(c, sk::launch_pfp_hash(c->st, n, d_ids, d_off, d_bytes, c->redis_major >= 5, d_cmd ? nullptr : d_changed,
+                                  chunks, S, big_alloc)); }
+    { Prof p_(c, 18);
+    HIPCHK(c, sk::launch_pfp_apply(c->st, n, chunks, S, d_cmd, c->arena, d_changed, big_alloc,
+                                   c->vals_a.as<uint64_t>(), c->vals_b.as<uint32_t>())); }
     return SK_OK;
 }
 
@@ -1729,12 +1695,13 @@ int sk_bloom_contains_dev(sk_ctx *c, const uint8_t *name, uint64_t len, uint64_t
     if ((r = bloom_prepare(c, nm, b->size, b->k, false, &id))) return r;
     const uint8_t *bits = id == kNoId ? reinterpret_cast<const uint8_t *>(c->d_zero) : c->strs[id].ptr;
     const uint64_t *dl = id == kNoId ? reinterpret_cast<const uint64_t *>(c->d_zero) : &c->d_dir[id].len;
-    // async: run on the read stream after everything already enqueued on the main stream
+    // async: run on the read stream after every main-stream write of bit strings
     bool rs = c->async_dev && c->read_stream;
     hipStream_t s = rs ? c->st2 : c->st;
-    if (rs) {
+    if (rs && c->st_wrote_bits) {
         HIPCHK(c, hipEventRecord(c->ev_w, c->st));
         HIPCHK(c, hipStreamWaitEvent(c->st2, c->ev_w, 0));
+        c->st_wrote_bits = false;
     }
     { Prof p_(c, 5, s);
     HIPCHK(c, sk::launch_bloom_contains(s, n, d_off, d_bytes, bits, dl, uint64_t(b->size),
@@ -1843,10 +1810,23 @@ int sk_prof_enable(sk_ctx *c, int on) {
     c->prof = on != 0;
     return SK_OK;
 }
+int sk_prof_only(sk_ctx *c, const char *phase) {
+    std::lock_guard<std::mutex> g(c->mu);
+    if (!phase) {
+        c->prof_mask = 0xffffffffu;
+        return SK_OK;
+    }
+    for (int i = 0; i < kNumPhases; i++)
+        if (strcmp(phase, kPhaseNames[i]) == 0) {
+            c->prof_mask = 1u << i;
+            return SK_OK;
+        }
+    return fail(c, SK_EINVAL, "unknown phase");
+}
 int sk_prof_reset(sk_ctx *c) {
     std::lock_guard<std::mutex> g(c->mu);
     prof_collect(c);
-    for (int i = 0; i < 16; i++) c->prof_ms[i] = 0, c->prof_n[i] = 0;
+    for (int i = 0; i < 32; i++) c->prof_ms[i] = 0, c->prof_n[i] = 0;
     return SK_OK;
 }
 int sk_prof_read(sk_ctx *c, const char *phase, uint64_t *launches, double *total_ms) {

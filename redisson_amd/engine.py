@@ -174,6 +174,10 @@ class SketchEngine:
     def prof_enable(self, on: bool = True):
         self._check(self.lib.sk_prof_enable(self.ctx, int(on)))
 
+    def prof_only(self, phase=None):
+        """Time only `phase` while profiling is on (None: every phase)."""
+        self._check(self.lib.sk_prof_only(self.ctx, phase.encode() if phase else None))
+
     def prof_reset(self):
         self._check(self.lib.sk_prof_reset(self.ctx))
 

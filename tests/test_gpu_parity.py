@@ -377,3 +377,48 @@ def test_pfadd_paths_agree(O, path, claim):
         assert r[0] == 1 and not r[1:].any()
     finally:
         e.close()
+
+
+def _pfp_bucket(slots):
+    """k_pfp_hash's bucket of a register slot (sk_kernels.hip pfp_bucket)."""
+    with np.errstate(over="ignore"):
+        return (np.asarray(slots, dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15)) >> np.uint64(53)
+
+
+def test_pfadd_partition_oversized_buckets(engine, O):
+    """Buckets far past the apply pass's LDS capacity, with more distinct
+    (slot, rho) pairs than k_pfp_big's LDS table (its global table), plus one
+    hot register hit thousands of times: replies and registers still exact."""
+    nkeys = 1000
+    names = [b"ob:%d" % i for i in range(nkeys)]
+    ids = engine.hll_resolve(names)
+    pool = _elems(0x5EED0400, 120000)
+    by_reg = {}
+    for e in pool:
+        by_reg.setdefault(O.hll_patlen(e)[0], []).append(e)
+    rng = np.random.default_rng(44)
+    kids, els = [], []
+    for target in (5, 1234):
+        kk, rr = np.meshgrid(np.arange(nkeys, dtype=np.uint64), np.arange(16384, dtype=np.uint64), indexing="ij")
+        slots = (ids[kk.astype(np.int64)].astype(np.uint64) << np.uint64(14)) | rr
+        hit = np.argwhere(_pfp_bucket(slots) == target)
+        for ki, r in hit:
+            cand = by_reg.get(int(r), [])
+            for e in cand[: int(rng.integers(1, 5))]:
+                for _ in range(int(rng.integers(1, 3))):
+                    kids.append(ki)
+                    els.append(e)
+    hot = pool[7]
+    kids += [3] * 6000
+    els += [hot] * 6000
+    perm = rng.permutation(len(els))
+    kid = np.asarray(kids, dtype=np.uint32)[perm]
+    els = [els[i] for i in perm]
+    assert len(els) < (1 << 20)
+    off, buf = O.pack(els)
+    d = [engine.to_device(ids[kid]), engine.to_device(off), engine.to_device(buf, pad=16), engine.alloc(len(els))]
+    engine.pfadd_dev(len(els), d[0], d[1], d[2], int(off[-1]), d[3])
+    regs, want = O.HLLStore().pfadd_bulk(kid, off, buf, nkeys)
+    assert np.array_equal(d[3].download(np.uint8, len(els)), want)
+    for i, nm in enumerate(names):
+        np.testing.assert_array_equal(engine.hll_registers(nm), regs[i])

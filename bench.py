@@ -32,8 +32,8 @@ from redisson_amd import SketchEngine, device_count, owner  # noqa: E402
 PROF_STEPS = 5          # steps in each per-kernel breakdown pass (outside the timed region)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 # in-library event-timed phases (sk_prof_*): one kernel each, except pfadd_sort
-# (rocPRIM onesweep passes) and pfp_scan (rocPRIM scan); only the path in use has launches
-HLL_PHASES = ["pfp_hash", "pfp_scan", "pfp_scatter", "pfp_apply", "pfp_big",
+# (rocPRIM onesweep passes); only the path in use has launches
+HLL_PHASES = ["pfp_hash", "pfp_apply", "pfp_reply",
               "pfadd_claim", "pfadd_commit", "pfadd_hash", "pfadd_sort", "pfadd_apply"]
 PHASES = HLL_PHASES + ["bloom_contains"]
 
@@ -159,7 +159,7 @@ def main():
     # breakdown as in the timed region (PFADD on the main stream, contains on the
     # read stream, no host sync): picks the kernel with the most device time
     over_ms = profiled(W, True)
-    dom = max([p for p in over_ms if p not in ("pfadd_sort", "pfp_scan")], key=lambda p: over_ms[p])
+    dom = max([p for p in over_ms if p != "pfadd_sort"], key=lambda p: over_ms[p])
 
     # ------------------------------------------------------------ timed region
     # async: PFADD batches never wait on the host; only `dom` is event-timed
@@ -250,11 +250,9 @@ def main():
 def per_unit_of(phase, mean_len_h, mean_len_b, k):
     """Algorithmic bytes per unit (SURVEY 8d / DESIGN.md kernel table)."""
     return {
-        "pfp_hash": mean_len_h + 8 + 4 + 8 + 1,        # key bytes + offset + slab id in, record + reply zero out
-        "pfp_scan": 2 * 4 * 2048 * 256 / (1 << 20),    # bucket x block histogram, read + write, per element
-        "pfp_scatter": 8 + 8,                          # record in, record out
+        "pfp_hash": mean_len_h + 8 + 4 + 8 + 2,        # key bytes + offset + slab id in, record + chunk slot out
         "pfp_apply": 8 + 64 + 64 + 1,                  # record + register sector load (R0) + store + reply
-        "pfp_big": 0.0,                                # oversized buckets only (none at C2)
+        "pfp_reply": 1 + 2 + 1,                        # chunk-order reply + chunk slot in, reply out
         "pfadd_claim": mean_len_h + 8 + 4 + 1 + 8,     # key bytes + offset + slab id + register in, record out
         "pfadd_commit": 8 + 1 + 1,                     # record in, register + reply out
         "pfadd_hash": mean_len_h + 8 + 4 + 8,          # key bytes + offset + slab id in, sort key out
@@ -269,8 +267,8 @@ def pmc_traffic(phase):
     import glob
 
     kern = {"bloom_contains": "sk::k_bloom_contains<0>", "pfadd_claim": "sk::k_pfadd_claim",
-            "pfadd_commit": "sk::k_pfadd_commit", "pfp_hash": "sk::k_pfp_hash", "pfp_scatter": "sk::k_pfp_scatter",
-            "pfp_apply": "sk::k_pfp_apply"}.get(phase)
+            "pfadd_commit": "sk::k_pfadd_commit", "pfp_hash": "sk::k_pfp_hash", "pfp_apply": "sk::k_pfp_apply",
+            "pfp_reply": "sk::k_pfp_reply"}.get(phase)
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_summary.json")))
     if not kern or not files:
         return None

@@ -26,11 +26,12 @@ uint32_t pfp_blocks(uint64_t n);
 uint32_t pfp_buckets();
 uint32_t pfp_epb();
 hipError_t launch_pfp_hash(hipStream_t st, uint64_t n, const uint32_t *key_ids, const uint64_t *off,
-                           const uint8_t *bytes, int v5, uint8_t *changed_i, uint64_t *chunks, uint32_t *S,
+                           const uint8_t *bytes, int v5, uint64_t *chunks, uint32_t *S, uint16_t *pos,
                            uint32_t *big_alloc);
-hipError_t launch_pfp_apply(hipStream_t st, uint64_t n, const uint64_t *chunks, const uint32_t *S,
-                            const uint32_t *cmd_of, uint8_t *arena, uint8_t *changed, uint32_t *big_alloc,
-                            uint64_t *big_keys, uint32_t *big_vals);
+hipError_t launch_pfp_apply(hipStream_t st, uint64_t n, const uint64_t *chunks, const uint32_t *S, uint8_t *arena,
+                            uint8_t *rep, uint32_t *big_alloc, uint64_t *big_keys, uint32_t *big_vals);
+hipError_t launch_pfp_reply(hipStream_t st, uint64_t n, const uint8_t *rep, const uint16_t *pos,
+                            const uint32_t *cmd_of, uint8_t *changed);
 hipError_t sort_keys_size(uint64_t n, unsigned begin_bit, unsigned end_bit, size_t *bytes);
 hipError_t sort_keys(hipStream_t st, void *tmp, size_t tmp_bytes, const uint64_t *in, uint64_t *out, uint64_t n,
                      unsigned begin_bit, unsigned end_bit);

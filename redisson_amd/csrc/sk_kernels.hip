@@ -279,19 +279,21 @@ __global__ void k_len_from_last_key(const uint64_t *keys, uint64_t m, uint64_t *
 //   rec = slot << 26 | seq << 6 | rho   (slot <= 38 bits, seq < 2^20)
 // Buckets larger than SK_PFP_CAP (hot registers, skew) are resolved by the
 // same workgroup from a (slot, rho) -> min seq table (pfp_big_resolve).
-#define SK_PFP_NB 2048    // buckets (~n/2048 records each)
+#define SK_PFP_NB 512     // buckets (~n/512 records each; ~8 records = one 64-B line per block segment)
 #define SK_PFP_TPB 1024   // threads per hash workgroup (16 waves: one per CU hides the latency)
 #define SK_PFP_EPB 4096   // elements per hash workgroup = max blocks 256 for n <= 2^20
-#define SK_PFP_ATPB 256   // threads per apply workgroup (one block segment per thread)
-#define SK_PFP_CAP 2048   // records one apply workgroup holds in LDS
-#define SK_PFP_HT 2048    // LDS hash-chain heads
+#define SK_PFP_ATPB 1024  // threads per apply workgroup (4 per block segment)
+#define SK_PFP_CAP 4096   // records one apply workgroup holds in LDS
+#define SK_PFP_HT 4096    // LDS hash-chain heads
 #define SK_PFP_STAGE (4 * SK_STAGE_WORDS) // LDS key window (u64 words) for SK_PFP_TPB elements
-static_assert(SK_PFP_ATPB * SK_PFP_EPB >= (1 << 20), "one apply thread per hash block");
+static_assert(SK_PFP_ATPB / 4 * SK_PFP_EPB >= (1 << 20), "4 apply threads per hash block");
+static_assert(SK_PFP_NB <= SK_PFP_TPB, "one bucket per hash thread in the start scan");
+static_assert(SK_PFP_CAP < 0xffff, "u16 chain links");
 __device__ __forceinline__ uint32_t pfp_bucket(uint64_t slot) {
-    return uint32_t((slot * 0x9E3779B97F4A7C15ull) >> 53); // 11 bits
+    return uint32_t((slot * 0x9E3779B97F4A7C15ull) >> 55); // 9 bits
 }
 __device__ __forceinline__ uint32_t pfp_ht(uint64_t slot) {
-    return uint32_t((slot * 0xC2B2AE3D27D4EB4Full) >> 53); // 11 bits
+    return uint32_t((slot * 0xC2B2AE3D27D4EB4Full) >> 52); // 12 bits
 }
 
 // exclusive scan of one value per thread over a workgroup of NT threads;
@@ -318,63 +320,140 @@ template <int NT> __device__ __forceinline__ uint32_t block_exscan(uint32_t v, u
     return base + x - v;
 }
 
+// Key bytes are staged through two LDS windows: the global loads of window
+// e+1 are issued (into registers) before round e is hashed, so one barrier
+// per round is the only wait; every element's offsets and slab id are loaded
+// up front.  Windows that do not fit fall back to direct global reads.
+#define SK_PFP_WIN 6144 // u64 words per key window (48 KiB; 1024 keys of mean length <= ~46 B)
+#define SK_PFP_WVEC (SK_PFP_WIN * 8 / 16 / SK_PFP_TPB) // 16-B vectors per thread per window
+__device__ __forceinline__ bool pfp_win_fits(uint64_t lo, uint64_t hi) {
+    return (hi - (lo & ~uint64_t(15))) + 32 <= uint64_t(SK_PFP_WIN) * 8;
+}
+__device__ __forceinline__ void pfp_win_load(const uint8_t *bytes, uint64_t lo, uint64_t hi, uint4 (&v)[SK_PFP_WVEC]) {
+    uint64_t a0 = lo & ~uint64_t(15);
+    uint32_t nvec = uint32_t((hi - a0 + 15) >> 4);
+    const uint4 *src = reinterpret_cast<const uint4 *>(bytes + a0);
+#pragma unroll
+    for (int q = 0; q < SK_PFP_WVEC; q++) {
+        uint32_t idx = threadIdx.x + q * SK_PFP_TPB;
+        v[q] = idx < nvec ? src[idx] : make_uint4(0, 0, 0, 0);
+    }
+}
+// stores the window and the 16 zero bytes after it (readers look up to 15 B past a key)
+__device__ __forceinline__ void pfp_win_store(uint64_t lo, uint64_t hi, const uint4 (&v)[SK_PFP_WVEC], uint64_t *buf) {
+    uint32_t nvec = uint32_t((hi - (lo & ~uint64_t(15)) + 15) >> 4);
+    uint4 *dst = reinterpret_cast<uint4 *>(buf);
+#pragma unroll
+    for (int q = 0; q < SK_PFP_WVEC; q++) {
+        uint32_t idx = threadIdx.x + q * SK_PFP_TPB;
+        if (idx <= nvec) dst[idx] = v[q];
+    }
+}
+
 __global__ void __launch_bounds__(SK_PFP_TPB) k_pfp_hash(uint64_t n, const uint32_t *__restrict__ key_ids,
                                                          const uint64_t *__restrict__ off,
                                                          const uint8_t *__restrict__ bytes, int v5,
                                                          uint64_t *__restrict__ chunks, uint32_t *__restrict__ S,
-                                                         uint32_t nblocks, uint8_t *__restrict__ changed_i,
+                                                         uint32_t nblocks, uint16_t *__restrict__ pos,
                                                          uint32_t *__restrict__ big_alloc) {
     __shared__ uint32_t h[SK_PFP_NB];
     __shared__ uint32_t wsum[SK_PFP_TPB / 64];
     __shared__ uint64_t lrec[SK_PFP_EPB];
-    __shared__ uint64_t lds[SK_PFP_STAGE];
+    __shared__ uint64_t win[2][SK_PFP_WIN];
     for (uint32_t b = threadIdx.x; b < SK_PFP_NB; b += SK_PFP_TPB) h[b] = 0;
     if (blockIdx.x == 0 && threadIdx.x == 0) *big_alloc = 0;
     constexpr int PER = SK_PFP_EPB / SK_PFP_TPB;
-    uint64_t base = uint64_t(blockIdx.x) * SK_PFP_EPB;
+    const uint64_t base = uint64_t(blockIdx.x) * SK_PFP_EPB;
+    const uint64_t rounds = (n - base + SK_PFP_TPB - 1) / SK_PFP_TPB;
+    const int nr = rounds < PER ? int(rounds) : PER;
+    uint64_t wb[PER + 1], oa[PER], ob[PER];
+    uint32_t kid[PER];
+#pragma unroll
+    for (int e = 0; e <= PER; e++) {
+        uint64_t i0 = base + uint64_t(e) * SK_PFP_TPB;
+        wb[e] = off[i0 < n ? i0 : n];
+    }
+#pragma unroll
+    for (int e = 0; e < PER; e++) {
+        uint64_t i = base + uint64_t(e) * SK_PFP_TPB + threadIdx.x;
+        oa[e] = ob[e] = 0;
+        kid[e] = 0;
+        if (i < n) {
+            oa[e] = off[i];
+            ob[e] = off[i + 1];
+            kid[e] = key_ids[i];
+        }
+    }
+    uint4 v[SK_PFP_WVEC];
+    if (pfp_win_fits(wb[0], wb[1])) {
+        pfp_win_load(bytes, wb[0], wb[1], v);
+        pfp_win_store(wb[0], wb[1], v, win[0]);
+    }
+    __syncthreads(); // h zeroed, window 0 staged
     uint64_t r[PER];
     uint32_t bk[PER], rk[PER];
 #pragma unroll
     for (int e = 0; e < PER; e++) {
         r[e] = ~0ull;
-        uint64_t e0 = base + uint64_t(e) * SK_PFP_TPB;
-        if (e0 >= n) continue; // uniform
-        uint64_t e1 = e0 + SK_PFP_TPB < n ? e0 + SK_PFP_TPB : n;
-        uint64_t lo = off[e0], hi = off[e1];
-        bool staged = (hi - (lo & ~uint64_t(15))) + 32 <= uint64_t(SK_PFP_STAGE) * 8;
-        __syncthreads(); // h zeroed / the previous window's readers are done
-        uint32_t wbase = staged ? stage_keys(bytes, lo, hi, lds) : 0u;
-        uint64_t i = e0 + threadIdx.x;
+        bk[e] = rk[e] = 0;
+        if (e >= nr) continue; // uniform
+        bool pre = e + 1 < nr && pfp_win_fits(wb[e + 1], wb[e + 2]);
+        if (pre) pfp_win_load(bytes, wb[e + 1], wb[e + 2], v);
+        uint64_t i = base + uint64_t(e) * SK_PFP_TPB + threadIdx.x;
         if (i < n) {
-            if (changed_i) changed_i[i] = 0;
-            uint64_t o = off[i];
-            uint32_t len = uint32_t(off[i + 1] - o);
-            uint64_t hh = staged ? murmur64a_r(LdsReader{lds, wbase + uint32_t(o - lo)}, len, 0xadc83b19ull)
-                                 : murmur64a(bytes + o, len, 0xadc83b19ull);
+            uint32_t len = uint32_t(ob[e] - oa[e]);
+            uint64_t hh = pfp_win_fits(wb[e], wb[e + 1])
+                              ? murmur64a_r(LdsReader{win[e & 1], uint32_t(wb[e] & 15u) + uint32_t(oa[e] - wb[e])},
+                                            len, 0xadc83b19ull)
+                              : murmur64a(bytes + oa[e], len, 0xadc83b19ull);
             uint32_t reg, rho;
             hll_pat(hh, v5, &reg, &rho);
-            uint64_t slot = (uint64_t(key_ids[i]) << 14) | reg;
+            uint64_t slot = (uint64_t(kid[e]) << 14) | reg;
             r[e] = (slot << 26) | (i << 6) | rho;
             bk[e] = pfp_bucket(slot);
             rk[e] = atomicAdd(&h[bk[e]], 1u);
         }
+        if (pre) pfp_win_store(wb[e + 1], wb[e + 2], v, win[(e + 1) & 1]);
+        __syncthreads(); // window e+1 staged; window e free for round e+2
     }
-    __syncthreads();
-    // bucket starts: two buckets per thread
-    uint32_t c0 = h[2 * threadIdx.x], c1 = h[2 * threadIdx.x + 1], tot;
-    uint32_t st0 = block_exscan<SK_PFP_TPB>(c0 + c1, wsum, &tot);
-    h[2 * threadIdx.x] = st0;
-    h[2 * threadIdx.x + 1] = st0 + c0;
-    S[uint64_t(2 * threadIdx.x) * nblocks + blockIdx.x] = st0;
-    S[uint64_t(2 * threadIdx.x + 1) * nblocks + blockIdx.x] = st0 + c0;
+    // bucket starts (one bucket per thread), row SK_PFP_NB = the block's total
+    uint32_t c0 = threadIdx.x < SK_PFP_NB ? h[threadIdx.x] : 0u, tot;
+    uint32_t st0 = block_exscan<SK_PFP_TPB>(c0, wsum, &tot);
+    if (threadIdx.x < SK_PFP_NB) {
+        h[threadIdx.x] = st0;
+        S[uint64_t(threadIdx.x) * nblocks + blockIdx.x] = st0;
+    }
     if (threadIdx.x == 0) S[uint64_t(SK_PFP_NB) * nblocks + blockIdx.x] = tot;
     __syncthreads();
 #pragma unroll
     for (int e = 0; e < PER; e++)
-        if (r[e] != ~0ull) lrec[h[bk[e]] + rk[e]] = r[e];
+        if (r[e] != ~0ull) {
+            uint32_t p = h[bk[e]] + rk[e];
+            lrec[p] = r[e];
+            pos[base + uint64_t(e) * SK_PFP_TPB + threadIdx.x] = uint16_t(p);
+        }
     __syncthreads();
     uint64_t *dst = chunks + base;
     for (uint32_t t = threadIdx.x; t < tot; t += SK_PFP_TPB) dst[t] = lrec[t];
+}
+
+// Replies back to batch order: rep holds them in chunk order (written by
+// k_pfp_apply as runs per block segment), pos maps element -> chunk slot.
+__global__ void __launch_bounds__(SK_PFP_TPB) k_pfp_reply(uint64_t n, const uint8_t *__restrict__ rep,
+                                                          const uint16_t *__restrict__ pos,
+                                                          const uint32_t *__restrict__ cmd_of,
+                                                          uint8_t *__restrict__ changed) {
+    __shared__ uint8_t lr[SK_PFP_EPB];
+    const uint64_t base = uint64_t(blockIdx.x) * SK_PFP_EPB;
+    const uint32_t m = uint32_t(n - base < SK_PFP_EPB ? n - base : SK_PFP_EPB);
+    for (uint32_t t = threadIdx.x; t < m; t += SK_PFP_TPB) lr[t] = rep[base + t];
+    __syncthreads();
+    for (uint32_t t = threadIdx.x; t < m; t += SK_PFP_TPB) {
+        uint64_t i = base + t;
+        uint8_t v = lr[pos[i]];
+        if (!cmd_of) changed[i] = v;
+        else if (v) changed[cmd_of[i]] = 1; // multi-element commands: OR over their elements
+    }
 }
 
 // ---- oversized buckets: a record replies 1 iff rho > R0 and it is the
@@ -383,7 +462,7 @@ __global__ void __launch_bounds__(SK_PFP_TPB) k_pfp_hash(uint64_t n, const uint3
 // a global table of 2*cnt entries carved from a per-batch arena) and answers
 // from it.  The slot's last prefix maximum (max rho, its earliest record)
 // stores the register: one writer per slot.
-#define SK_BIG_LDS 2048
+#define SK_BIG_LDS 4096
 #define SK_BIG_PROBE 32
 #define SK_BIG_EMPTY 0xffffffffffffffffull
 __device__ __forceinline__ uint32_t big_hash(uint64_t key) {
@@ -439,10 +518,10 @@ struct BigTable {
     }
 };
 
-// one bucket segment per thread: records seg[0 .. cnt)
-__device__ void pfp_big_resolve(const uint64_t *seg, uint32_t seg_cnt, uint32_t cnt, void *smem,
-                                uint32_t *big_alloc, uint64_t *big_keys, uint32_t *big_vals,
-                                const uint32_t *__restrict__ cmd_of, uint8_t *arena, uint8_t *__restrict__ changed) {
+// this thread's records: seg[t0], seg[t0 + 4], ... below seg_cnt; cnt = the bucket's total
+__device__ void pfp_big_resolve(const uint64_t *seg, uint32_t t0, uint32_t seg_cnt, uint32_t cnt, void *smem,
+                                uint32_t *big_alloc, uint64_t *big_keys, uint32_t *big_vals, uint8_t *arena,
+                                uint8_t *__restrict__ rep_seg) {
     __shared__ uint32_t gbase;
     unsigned long long *lk = reinterpret_cast<unsigned long long *>(smem);
     uint32_t *lv = reinterpret_cast<uint32_t *>(lk + SK_BIG_LDS);
@@ -453,22 +532,22 @@ __device__ void pfp_big_resolve(const uint64_t *seg, uint32_t seg_cnt, uint32_t 
     for (uint32_t s = threadIdx.x; s < T.S; s += blockDim.x) T.gk[s] = SK_BIG_EMPTY, T.gv[s] = 0xffffffffu;
     __threadfence();
     __syncthreads();
-    for (uint32_t t = 0; t < seg_cnt; t++) {
+    for (uint32_t t = t0; t < seg_cnt; t += 4) {
         uint64_t r = seg[t];
         T.insert(((r >> 26) << 6) | (r & 63u), uint32_t((r >> 6) & 0xfffffu));
     }
     __threadfence();
     __syncthreads();
-    for (uint32_t t = 0; t < seg_cnt; t++) { // replies (the arena is only read)
+    for (uint32_t t = t0; t < seg_cnt; t += 4) { // replies (the arena is only read)
         uint64_t r = seg[t], slot = r >> 26;
         uint32_t rho = uint32_t(r & 63u), seq = uint32_t((r >> 6) & 0xfffffu);
-        if (rho <= (uint32_t(arena[slot]) & 63u)) continue;
-        bool first = true; // v = rho: no earlier equal rho; v > rho: no earlier larger one
+        bool first = rho > (uint32_t(arena[slot]) & 63u);
+        // v = rho: no earlier equal rho; v > rho: no earlier larger one
         for (uint32_t v = rho; v < 52 && first; v++) first = T.find((slot << 6) | v) >= seq;
-        if (first) changed[cmd_of ? cmd_of[seq] : seq] = 1;
+        rep_seg[t] = first ? 1 : 0;
     }
     __syncthreads();
-    for (uint32_t t = 0; t < seg_cnt; t++) { // the slot's writer
+    for (uint32_t t = t0; t < seg_cnt; t += 4) { // the slot's writer
         uint64_t r = seg[t], slot = r >> 26;
         uint32_t rho = uint32_t(r & 63u), seq = uint32_t((r >> 6) & 0xfffffu);
         if (T.find((slot << 6) | rho) != seq) continue;
@@ -478,16 +557,18 @@ __device__ void pfp_big_resolve(const uint64_t *seg, uint32_t seg_cnt, uint32_t 
     }
 }
 
-// One workgroup per bucket.  Gather: thread j copies block j's segment of
-// the bucket into LDS.  Phase A: chain walk -> each record's earliest
-// same-slot record, the max rho of its earlier records and of the whole slot;
-// phase B: the earliest records load R0 (independent loads, all in flight);
-// phase C: replies and the final register store.
+// One workgroup per bucket.  Gather: threads 4j..4j+3 copy block j's segment
+// of the bucket into LDS and load each record's register (R0) right away --
+// records of one slot all live in this workgroup and the arena is written
+// only after the last barrier, so every load of a slot sees its pre-batch
+// value, and the R0 latency overlaps the chain building.  Then the chain walk
+// gives each record the max rho of its slot's earlier records and of the
+// whole slot; replies and the slot's one register store follow.
 __global__ void __launch_bounds__(SK_PFP_ATPB) k_pfp_apply(const uint64_t *__restrict__ chunks,
                                                            const uint32_t *__restrict__ S, uint32_t nblocks,
-                                                           const uint32_t *__restrict__ cmd_of, uint8_t *arena,
-                                                           uint8_t *__restrict__ changed, uint32_t *big_alloc,
-                                                           uint64_t *big_keys, uint32_t *big_vals) {
+                                                           uint8_t *arena, uint8_t *__restrict__ rep,
+                                                           uint32_t *big_alloc, uint64_t *big_keys,
+                                                           uint32_t *big_vals) {
     constexpr uint32_t kSmem = SK_PFP_CAP * 8 + SK_PFP_CAP * 2 + SK_PFP_HT * 4 + SK_PFP_CAP;
     static_assert(kSmem >= SK_BIG_LDS * 12, "big-bucket table shares the LDS");
     __shared__ uint64_t smem[(kSmem + 7) / 8];
@@ -496,75 +577,68 @@ __global__ void __launch_bounds__(SK_PFP_ATPB) k_pfp_apply(const uint64_t *__res
     uint16_t *nxt = reinterpret_cast<uint16_t *>(R + SK_PFP_CAP);
     uint32_t *head = reinterpret_cast<uint32_t *>(nxt + SK_PFP_CAP);
     uint8_t *r0 = reinterpret_cast<uint8_t *>(head + SK_PFP_HT);
-    uint32_t b = blockIdx.x, j = threadIdx.x;
+    uint32_t b = blockIdx.x, j = threadIdx.x >> 2, sub = threadIdx.x & 3u;
     uint32_t lo = 0, c = 0;
     if (j < nblocks) {
         lo = S[uint64_t(b) * nblocks + j];
         c = S[uint64_t(b + 1) * nblocks + j] - lo;
     }
     uint32_t cnt;
-    uint32_t dst = block_exscan<SK_PFP_ATPB>(c, wsum, &cnt);
+    uint32_t dst = block_exscan<SK_PFP_ATPB>(sub ? 0u : c, wsum, &cnt);
+    dst = __shfl(dst, int((threadIdx.x & 63u) & ~3u)); // the group's start (from its sub 0 lane)
     if (cnt == 0) return; // uniform
     const uint64_t *seg = chunks + uint64_t(j) * SK_PFP_EPB + lo;
     if (cnt > SK_PFP_CAP) {
-        pfp_big_resolve(seg, c, cnt, smem, big_alloc, big_keys, big_vals, cmd_of, arena, changed);
+        pfp_big_resolve(seg, sub, c, cnt, smem, big_alloc, big_keys, big_vals, arena,
+                        rep + uint64_t(j) * SK_PFP_EPB + lo);
         return;
     }
     for (uint32_t t = threadIdx.x; t < SK_PFP_HT; t += SK_PFP_ATPB) head[t] = 0xffffu;
-    for (uint32_t t = 0; t < c; t++) R[dst + t] = seg[t];
+    uint32_t t = sub;
+    for (; t + 4 < c; t += 8) { // two records per step: both loads, then both register loads, in flight
+        uint64_t ra = seg[t], rb = seg[t + 4];
+        uint8_t va = arena[ra >> 26], vb = arena[rb >> 26];
+        R[dst + t] = ra;
+        R[dst + t + 4] = rb;
+        r0[dst + t] = va & 63u;
+        r0[dst + t + 4] = vb & 63u;
+    }
+    if (t < c) {
+        uint64_t ra = seg[t];
+        R[dst + t] = ra;
+        r0[dst + t] = arena[ra >> 26] & 63u;
+    }
     __syncthreads();
-    for (uint32_t t = threadIdx.x; t < cnt; t += SK_PFP_ATPB)
-        nxt[t] = uint16_t(atomicExch(&head[pfp_ht(R[t] >> 26)], t));
+    for (uint32_t u = threadIdx.x; u < cnt; u += SK_PFP_ATPB)
+        nxt[u] = uint16_t(atomicExch(&head[pfp_ht(R[u] >> 26)], u));
     __syncthreads();
     constexpr int PER = SK_PFP_CAP / SK_PFP_ATPB;
-    uint32_t first[PER], pm[PER], mx[PER];
 #pragma unroll
     for (int q = 0; q < PER; q++) {
-        uint32_t t = threadIdx.x + q * SK_PFP_ATPB;
-        first[q] = 0xffffffffu;
-        if (t >= cnt) continue;
-        uint64_t rt = R[t], slot = rt >> 26, seq = (rt >> 6) & 0xfffffu;
+        uint32_t tq = threadIdx.x + q * SK_PFP_ATPB;
+        if (tq >= cnt) continue;
+        uint64_t rt = R[tq], slot = rt >> 26, seq = (rt >> 6) & 0xfffffu;
         uint32_t rho = uint32_t(rt & 63u);
-        uint32_t f = t, p = 0, m = rho;
-        uint64_t fseq = seq;
+        uint32_t p = 0, m = rho;
+        bool earliest = true;
         for (uint32_t u = head[pfp_ht(slot)]; u != 0xffffu; u = nxt[u]) {
             uint64_t ru = R[u];
             if ((ru >> 26) != slot) continue;
             uint32_t rhou = uint32_t(ru & 63u);
             uint64_t sequ = (ru >> 6) & 0xfffffu;
             m = rhou > m ? rhou : m;
-            if (sequ < seq) p = rhou > p ? rhou : p;
-            if (sequ < fseq) {
-                fseq = sequ;
-                f = u;
+            if (sequ < seq) {
+                p = rhou > p ? rhou : p;
+                earliest = false;
             }
         }
-        first[q] = f;
-        pm[q] = p;
-        mx[q] = m;
-    }
-    uint32_t ld[PER];
-#pragma unroll
-    for (int q = 0; q < PER; q++) {
-        uint32_t t = threadIdx.x + q * SK_PFP_ATPB;
-        ld[q] = first[q] == t ? uint32_t(arena[R[t] >> 26]) : 0u;
-    }
-#pragma unroll
-    for (int q = 0; q < PER; q++) {
-        uint32_t t = threadIdx.x + q * SK_PFP_ATPB;
-        if (first[q] == t) r0[t] = uint8_t(ld[q] & 63u);
+        uint32_t R0 = r0[tq];
+        r0[tq] = rho > (R0 > p ? R0 : p); // the reply replaces R0 (read by this thread only)
+        if (earliest && m > R0) arena[slot] = uint8_t(m);
     }
     __syncthreads();
-#pragma unroll
-    for (int q = 0; q < PER; q++) {
-        uint32_t t = threadIdx.x + q * SK_PFP_ATPB;
-        if (t >= cnt) continue;
-        uint64_t rt = R[t], slot = rt >> 26, seq = (rt >> 6) & 0xfffffu;
-        uint32_t rho = uint32_t(rt & 63u);
-        uint32_t R0 = r0[first[q]];
-        if (rho > (R0 > pm[q] ? R0 : pm[q])) changed[cmd_of ? cmd_of[seq] : uint32_t(seq)] = 1;
-        if (first[q] == t && mx[q] > R0) arena[slot] = uint8_t(mx[q]);
-    }
+    uint8_t *rs = rep + uint64_t(j) * SK_PFP_EPB + lo; // replies as runs, in the chunk's order
+    for (uint32_t u = sub; u < c; u += 4) rs[u] = r0[dst + u];
 }
 
 // -------------------------------------------------------------- histogram
@@ -645,61 +719,30 @@ __device__ __forceinline__ void bloom_hashes(const uint8_t *p, uint32_t len, uin
 }
 
 // contains: probes 0..k-2 only (the k-th GETBIT reply is dropped by
-// result.subList(1, size-1), M:RedissonBloomFilter.java:155).  Probes are
-// fetched in rounds of `first` then the rest: all loads of a round are in
-// flight together and the element stops after a round that saw a 0 bit.
-// FIRST = 0 is the fully sequential early exit, FIRST >= k-1 fetches every
-// probe at once; the result is the same AND for every schedule.  Measured at
-// C3 (k = 7, fill 0.50): sequential 100 us / 1M, 2+rest 108, 3+rest 113,
-// all 138 -- line fetches (~55 G/s chip-wide), not latency, bound the kernel.
-template <int FIRST>
-__device__ __forceinline__ uint8_t bloom_probe_and(uint64_t h1, uint64_t h2, int k, const uint8_t *__restrict__ bits,
-                                                   uint64_t slen, uint64_t size, uint64_t magic) {
-    if (FIRST == 0) { // fully sequential early exit: fewest line fetches (the measured best)
-        uint64_t h = h1;
-        for (int j = 0; j < k - 1; j++) {
-            if (!get_bit(bits, slen, mod_invariant(h & 0x7fffffffffffffffull, size, magic))) return 0;
-            h += (j & 1) ? h1 : h2;
-        }
-        return 1;
-    }
-    constexpr int MAXP = 32; // probes held in registers per round
-    uint64_t h = h1;
-    int j = 0;
-    int np = k - 1;
-    int round = FIRST;
-    while (j < np) {
-        int m = np - j < round ? np - j : round;
-        if (m > MAXP) m = MAXP;
-        uint32_t acc = 1;
-        uint64_t idx[MAXP];
-#pragma unroll
-        for (int q = 0; q < MAXP; q++) {
-            if (q < m) {
-                idx[q] = mod_invariant(h & 0x7fffffffffffffffull, size, magic);
-                h += ((j + q) & 1) ? h1 : h2;
-            }
-        }
-#pragma unroll
-        for (int q = 0; q < MAXP; q++)
-            if (q < m) acc &= uint32_t(get_bit(bits, slen, idx[q]));
-        if (!acc) return 0;
-        j += m;
-        round = MAXP; // after the first round: everything left at once
-    }
-    return 1;
-}
-
-template <int FIRST>
-__global__ void __launch_bounds__(256) k_bloom_contains(uint64_t n, const uint64_t *__restrict__ off,
-                                                        const uint8_t *__restrict__ bytes,
-                                                        const uint8_t *__restrict__ bits,
-                                                        const uint64_t *__restrict__ d_len, uint64_t size,
-                                                        uint64_t magic, int k, uint8_t *__restrict__ out) {
-    __shared__ uint64_t lds[SK_STAGE_WORDS];
+// result.subList(1, size-1), M:RedissonBloomFilter.java:155), in order, and
+// an element stops at its first 0 bit (the fewest line fetches: fetching
+// 2, 3 or all probes per round measured 8 %, 13 % and 38 % slower at C3).
+// Members need k-1 probes, non-members ~2 at fill 0.5.
+//
+// k_bloom_contains: one element per thread -- a wave lives as long as its
+// slowest lane, so early-exit lanes sit idle.
+// k_bloom_contains_q: a wave hashes 64*EPT elements into LDS, then runs a
+// probe queue: every iteration each busy lane issues one probe, and lanes
+// whose element finished take the next one (ballot + prefix count, no
+// atomics), so nearly every lane of every load instruction is a useful probe.
+// Measured at C3 (1M contains, k = 7, fill 0.5): 112 us one-per-thread, 113
+// queue with 4 elements per lane, 110 with 2 -- the chip-wide rate of random
+// line requests (~55 G/s), not idle lanes, bounds it.
+// WORDS: key window (u64 words)
+template <int WORDS>
+__device__ __forceinline__ void bloom_contains_body(uint64_t n, const uint64_t *__restrict__ off,
+                                                    const uint8_t *__restrict__ bytes, const uint8_t *__restrict__ bits,
+                                                    const uint64_t *__restrict__ d_len, uint64_t size, uint64_t magic,
+                                                    int k, uint8_t *__restrict__ out) {
+    __shared__ uint64_t lds[WORDS];
     uint64_t e0 = uint64_t(blockIdx.x) * blockDim.x, e1 = e0 + blockDim.x < n ? e0 + blockDim.x : n;
     uint64_t lo = off[e0], hi = off[e1];
-    bool staged = stage_fits(lo, hi);
+    bool staged = (hi - (lo & ~uint64_t(15))) + 32 <= uint64_t(WORDS) * 8;
     uint32_t wbase = staged ? stage_keys(bytes, lo, hi, lds) : 0u;
     uint64_t i = e0 + threadIdx.x;
     if (i >= n) return;
@@ -713,7 +756,106 @@ __global__ void __launch_bounds__(256) k_bloom_contains(uint64_t n, const uint64
     } else {
         bloom_hashes(bytes + o, len, &h1, &h2);
     }
-    out[i] = bloom_probe_and<FIRST>(h1, h2, k, bits, *d_len, size, magic);
+    uint64_t slen = *d_len, h = h1;
+    uint8_t r = 1;
+    for (int j = 0; j < k - 1; j++) {
+        if (!get_bit(bits, slen, mod_invariant(h & 0x7fffffffffffffffull, size, magic))) {
+            r = 0;
+            break;
+        }
+        h += (j & 1) ? h1 : h2;
+    }
+    out[i] = r;
+}
+
+__global__ void __launch_bounds__(256) k_bloom_contains(uint64_t n, const uint64_t *__restrict__ off,
+                                                        const uint8_t *__restrict__ bytes,
+                                                        const uint8_t *__restrict__ bits,
+                                                        const uint64_t *__restrict__ d_len, uint64_t size,
+                                                        uint64_t magic, int k, uint8_t *__restrict__ out) {
+    bloom_contains_body<SK_STAGE_WORDS>(n, off, bytes, bits, d_len, size, magic, k, out);
+}
+template <int EPT>
+__global__ void __launch_bounds__(256) k_bloom_contains_q(uint64_t n, const uint64_t *__restrict__ off,
+                                                          const uint8_t *__restrict__ bytes,
+                                                          const uint8_t *__restrict__ bits,
+                                                          const uint64_t *__restrict__ d_len, uint64_t size,
+                                                          uint64_t magic, int k, uint8_t *__restrict__ out) {
+    __shared__ uint64_t lds[SK_STAGE_WORDS];
+    __shared__ uint64_t H1[256 * EPT], H2[256 * EPT];
+    uint64_t base = uint64_t(blockIdx.x) * (256 * EPT);
+    for (int e = 0; e < EPT; e++) { // hash 256 elements per round (keys staged in LDS)
+        uint64_t e0 = base + uint64_t(e) * 256;
+        if (e0 >= n) break; // uniform
+        uint64_t e1 = e0 + 256 < n ? e0 + 256 : n;
+        uint64_t lo = off[e0], hi = off[e1];
+        bool staged = stage_fits(lo, hi);
+        __syncthreads(); // the previous round's readers are done
+        uint32_t wbase = staged ? stage_keys(bytes, lo, hi, lds) : 0u;
+        uint64_t i = e0 + threadIdx.x;
+        if (i < n) {
+            uint64_t o = off[i];
+            uint32_t len = uint32_t(off[i + 1] - o);
+            uint64_t h1, h2;
+            if (staged) {
+                LdsReader rd{lds, wbase + uint32_t(o - lo)};
+                h1 = xxh64_r(rd, len);
+                h2 = farm_uo64_r(rd, len);
+            } else {
+                bloom_hashes(bytes + o, len, &h1, &h2);
+            }
+            H1[e * 256 + threadIdx.x] = h1;
+            H2[e * 256 + threadIdx.x] = h2;
+        }
+    }
+    __syncthreads();
+    // wave w owns local elements [first, first + cnt)
+    const uint32_t lane = threadIdx.x & 63u, first = (threadIdx.x >> 6) * (64u * EPT);
+    uint64_t avail = n - base;
+    uint32_t cnt = avail > first ? uint32_t(avail - first < 64u * EPT ? avail - first : 64u * EPT) : 0u;
+    uint8_t *o = out + base + first;
+    const int np = k - 1;
+    if (np <= 0) { // k = 1: no reply is kept, contains is true (Q2)
+        for (uint32_t t = lane; t < cnt; t += 64) o[t] = 1;
+        return;
+    }
+    const uint64_t slen = *d_len;
+    uint32_t cursor = 64, cur = lane;
+    bool active = lane < cnt;
+    uint64_t a1 = 0, a2 = 0, h = 0;
+    int j = 0;
+    if (active) {
+        a1 = H1[first + cur];
+        a2 = H2[first + cur];
+        h = a1;
+    }
+    while (true) {
+        bool freed = !active;
+        if (active) {
+            int bit = get_bit(bits, slen, mod_invariant(h & 0x7fffffffffffffffull, size, magic));
+            if (!bit || j == np - 1) {
+                o[cur] = uint8_t(bit);
+                freed = true;
+            } else {
+                h += (j & 1) ? a1 : a2;
+                j++;
+            }
+        }
+        uint64_t mask = __ballot(freed);
+        if (freed) {
+            uint32_t e = cursor + uint32_t(__popcll(mask & ((1ull << lane) - 1ull)));
+            active = e < cnt;
+            if (active) {
+                cur = e;
+                a1 = H1[first + e];
+                a2 = H2[first + e];
+                h = a1;
+                j = 0;
+            }
+        }
+        cursor += uint32_t(__popcll(mask));
+        if (__ballot(active) == 0) break;
+    }
 }
 
 // add, pass 1: all k probes -> key = idx << 32 | (elem*k + j)
@@ -1074,20 +1216,26 @@ uint32_t pfp_epb() { return SK_PFP_EPB; }
 
 // hash + block-local bucket sort -> per-bucket LDS resolve; one launcher per stage so each is timed
 hipError_t launch_pfp_hash(hipStream_t st, uint64_t n, const uint32_t *key_ids, const uint64_t *off,
-                           const uint8_t *bytes, int v5, uint8_t *changed_i, uint64_t *chunks, uint32_t *S,
+                           const uint8_t *bytes, int v5, uint64_t *chunks, uint32_t *S, uint16_t *pos,
                            uint32_t *big_alloc) {
     uint32_t nb = pfp_blocks(n);
-    hipLaunchKernelGGL(k_pfp_hash, dim3(nb), dim3(SK_PFP_TPB), 0, st, n, key_ids, off, bytes, v5, chunks, S, nb,
-                       changed_i, big_alloc);
+    hipLaunchKernelGGL(k_pfp_hash, dim3(nb), dim3(SK_PFP_TPB), 0, st, n, key_ids, off, bytes, v5, chunks, S, nb, pos,
+                       big_alloc);
     SK_LAUNCH_CHECK();
     return hipSuccess;
 }
 
-hipError_t launch_pfp_apply(hipStream_t st, uint64_t n, const uint64_t *chunks, const uint32_t *S,
-                            const uint32_t *cmd_of, uint8_t *arena, uint8_t *changed, uint32_t *big_alloc,
-                            uint64_t *big_keys, uint32_t *big_vals) {
-    hipLaunchKernelGGL(k_pfp_apply, dim3(SK_PFP_NB), dim3(SK_PFP_ATPB), 0, st, chunks, S, pfp_blocks(n), cmd_of,
-                       arena, changed, big_alloc, big_keys, big_vals);
+hipError_t launch_pfp_apply(hipStream_t st, uint64_t n, const uint64_t *chunks, const uint32_t *S, uint8_t *arena,
+                            uint8_t *rep, uint32_t *big_alloc, uint64_t *big_keys, uint32_t *big_vals) {
+    hipLaunchKernelGGL(k_pfp_apply, dim3(SK_PFP_NB), dim3(SK_PFP_ATPB), 0, st, chunks, S, pfp_blocks(n), arena, rep,
+                       big_alloc, big_keys, big_vals);
+    SK_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+hipError_t launch_pfp_reply(hipStream_t st, uint64_t n, const uint8_t *rep, const uint16_t *pos,
+                            const uint32_t *cmd_of, uint8_t *changed) {
+    hipLaunchKernelGGL(k_pfp_reply, dim3(pfp_blocks(n)), dim3(SK_PFP_TPB), 0, st, n, rep, pos, cmd_of, changed);
     SK_LAUNCH_CHECK();
     return hipSuccess;
 }
@@ -1188,14 +1336,12 @@ hipError_t launch_bloom_contains(hipStream_t st, uint64_t n, const uint64_t *off
                                  const uint8_t *bits, const uint64_t *d_len, uint64_t size, uint64_t magic, int k,
                                  uint8_t *out, int sched) {
     if (!n) return hipSuccess;
-    dim3 g(grid_for(n, 256)), b(256);
-    switch (sched) {
-    case 1: hipLaunchKernelGGL(k_bloom_contains<1>, g, b, 0, st, n, off, bytes, bits, d_len, size, magic, k, out); break;
-    case 3: hipLaunchKernelGGL(k_bloom_contains<3>, g, b, 0, st, n, off, bytes, bits, d_len, size, magic, k, out); break;
-    case 2: hipLaunchKernelGGL(k_bloom_contains<2>, g, b, 0, st, n, off, bytes, bits, d_len, size, magic, k, out); break;
-    case 32: hipLaunchKernelGGL(k_bloom_contains<32>, g, b, 0, st, n, off, bytes, bits, d_len, size, magic, k, out); break;
-    default: hipLaunchKernelGGL(k_bloom_contains<0>, g, b, 0, st, n, off, bytes, bits, d_len, size, magic, k, out);
-    }
+    if (sched == 1) // probe queue, 4 elements per lane (A/B: not faster at C3 -- line requests bound both)
+        hipLaunchKernelGGL(k_bloom_contains_q<4>, dim3(grid_for(n, 1024)), dim3(256), 0, st, n, off, bytes, bits,
+                           d_len, size, magic, k, out);
+    else // one element per thread
+        hipLaunchKernelGGL(k_bloom_contains, dim3(grid_for(n, 256)), dim3(256), 0, st, n, off,
+                           bytes, bits, d_len, size, magic, k, out);
     SK_LAUNCH_CHECK();
     return hipSuccess;
 }

@@ -220,7 +220,7 @@ struct sk_ctx {
     int pfadd_path = 1;         // 0 claim/commit, 1 partition, 2 sorted (SK_PFADD_PATH); dense batches use 2
     int claim_all = 1;          // PFADD claim: 1 = every element claims (R0 from the atomic), 0 = load first, claim candidates (SK_PFADD_CLAIM)
     int read_stream = 1;        // async Bloom contains on the read stream st2 (SK_READ_STREAM=0: main stream)
-    int bloom_sched = 0;        // contains probe schedule: 0 sequential; 1/2/3/32 = first-round size (SK_BLOOM_SCHED)
+    int bloom_sched = 0;        // contains kernel (SK_BLOOM_SCHED): 0 one element per thread; 1 probe queue, 4/lane
     // async PFADD: the conflict count of the last sparse batch is checked ("settled")
     // by the next call that needs the HLL arena, not by the call itself
     bool pf_pending = false;
@@ -299,7 +299,7 @@ int pfadd_settle(sk_ctx *c); // defined with the PFADD core
 const char *kPhaseNames[] = {"pfadd_hash",  "pfadd_sort",   "pfadd_apply", "hll_hist",     "hll_union",
                              "bloom_contains", "bloom_probes", "bloom_sort", "bloom_apply", "setbit",
                              "getbit",      "bitcount",     "bitop",       "pfadd_claim", "pfadd_commit",
-                             "pfp_hash",    "pfp_scan",     "pfp_scatter", "pfp_apply",    "pfp_big"};
+                             "pfp_hash",    "pfp_apply",    "pfp_reply"};
 constexpr int kNumPhases = sizeof(kPhaseNames) / sizeof(kPhaseNames[0]);
 
 hipEvent_t ev_get(sk_ctx *c) {
@@ -600,20 +600,24 @@ bool pfadd_uses_sort(sk_ctx *c, uint64_t n, uint64_t touched_keys) {
 int pfadd_partition(sk_ctx *c, uint64_t n, const uint32_t *d_ids, const uint64_t *d_off, const uint8_t *d_bytes,
                     const uint32_t *d_cmd, uint8_t *d_changed) {
     if (n > (1ull << 20) || c->hll_next >= (1ull << 24)) return fail(c, SK_EINVAL, "PFADD partition batch too large");
-    uint32_t nb = sk::pfp_blocks(n);
-    HIPCHK(c, c->keys_a.ensure(uint64_t(nb) * sk::pfp_epb() * 8));         // block chunks of records
+    uint64_t nb = sk::pfp_blocks(n), cap = nb * sk::pfp_epb();
+    HIPCHK(c, c->keys_a.ensure(cap * 8));                                // block chunks of records
+    HIPCHK(c, c->keys_b.ensure(cap + 2 * n + 32));                       // replies in chunk order + element slots
     HIPCHK(c, c->hist_a.ensure((uint64_t(sk::pfp_buckets()) + 1) * nb * 4)); // bucket starts per block
     HIPCHK(c, c->vals_a.ensure(2 * n * 8)); // oversized-bucket tables: 2 entries per record
     HIPCHK(c, c->vals_b.ensure(2 * n * 4));
     HIPCHK(c, c->ovf.ensure(64));
     uint64_t *chunks = c->keys_a.as<uint64_t>();
+    uint8_t *rep = c->keys_b.as<uint8_t>();
+    uint16_t *pos = reinterpret_cast<uint16_t *>(rep + ((cap + 15) & ~uint64_t(15)));
     uint32_t *S = c->hist_a.as<uint32_t>(), *big_alloc = c->ovf.as<uint32_t>();
     { Prof p_(c, 15);
-    HIPCHK(c, sk::launch_pfp_hash(c->st, n, d_ids, d_off, d_bytes, c->redis_major >= 5, d_cmd ? nullptr : d_changed,
-                                  chunks, S, big_alloc)); }
-    { Prof p_(c, 18);
-    HIPCHK(c, sk::launch_pfp_apply(c->st, n, chunks, S, d_cmd, c->arena, d_changed, big_alloc,
-                                   c->vals_a.as<uint64_t>(), c->vals_b.as<uint32_t>())); }
+    HIPCHK(c, sk::launch_pfp_hash(c->st, n, d_ids, d_off, d_bytes, c->redis_major >= 5, chunks, S, pos, big_alloc)); }
+    { Prof p_(c, 16);
+    HIPCHK(c, sk::launch_pfp_apply(c->st, n, chunks, S, c->arena, rep, big_alloc, c->vals_a.as<uint64_t>(),
+                                   c->vals_b.as<uint32_t>())); }
+    { Prof p_(c, 17);
+    HIPCHK(c, sk::launch_pfp_reply(c->st, n, rep, pos, d_cmd, d_changed)); }
     return SK_OK;
 }
 

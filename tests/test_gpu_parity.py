@@ -382,7 +382,7 @@ def test_pfadd_paths_agree(O, path, claim):
 def _pfp_bucket(slots):
     """k_pfp_hash's bucket of a register slot (sk_kernels.hip pfp_bucket)."""
     with np.errstate(over="ignore"):
-        return (np.asarray(slots, dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15)) >> np.uint64(53)
+        return (np.asarray(slots, dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15)) >> np.uint64(55)
 
 
 def test_pfadd_partition_oversized_buckets(engine, O):
@@ -398,7 +398,7 @@ def test_pfadd_partition_oversized_buckets(engine, O):
         by_reg.setdefault(O.hll_patlen(e)[0], []).append(e)
     rng = np.random.default_rng(44)
     kids, els = [], []
-    for target in (5, 1234):
+    for target in (5, 300):
         kk, rr = np.meshgrid(np.arange(nkeys, dtype=np.uint64), np.arange(16384, dtype=np.uint64), indexing="ij")
         slots = (ids[kk.astype(np.int64)].astype(np.uint64) << np.uint64(14)) | rr
         hit = np.argwhere(_pfp_bucket(slots) == target)
@@ -422,3 +422,34 @@ def test_pfadd_partition_oversized_buckets(engine, O):
     assert np.array_equal(d[3].download(np.uint8, len(els)), want)
     for i, nm in enumerate(names):
         np.testing.assert_array_equal(engine.hll_registers(nm), regs[i])
+
+
+@pytest.mark.parametrize("sched", ["0", "1"])
+def test_bloom_contains_kernels_agree(O, sched):
+    """Both Bloom contains kernels (one element per thread, probe queue) gives the oracle's replies, for k = 1 (Q2: always true), small
+    and large k, ragged and empty elements, batch sizes off the tile size."""
+    import os
+    from redisson_amd import SketchEngine
+    os.environ["SK_BLOOM_SCHED"] = sched
+    try:
+        e = SketchEngine(device=0)
+    finally:
+        del os.environ["SK_BLOOM_SCHED"]
+    try:
+        rng = np.random.default_rng(int(sched) + 90)
+        for n_exp, p, n_add, n_probe in [(5000, 0.5, 3000, 777), (20000, 0.01, 15000, 5001),
+                                         (3000, 1e-6, 2000, 3333), (100, 0.03, 60, 1)]:
+            name = "bq:%s:%d" % (sched, n_exp)
+            assert e.bloom_try_init(name, n_exp, p)
+            size, k, _, _ = e.bloom_config(name)
+            bits = O.BitString()
+            added = _elems(0x5EED0500 + n_exp, n_add)
+            assert e.bloom_add(name, size, k, added) == bits.bloom_add(size, k, added)
+            probe = [added[i] for i in rng.integers(0, n_add, n_probe // 2)] + _ragged(rng, n_probe - n_probe // 2)
+            assert e.bloom_contains(name, size, k, probe) == bits.bloom_contains(size, k, probe)
+            off, buf = O.pack(probe)
+            d = [e.to_device(off), e.to_device(buf, pad=16), e.alloc(len(probe))]
+            e.bloom_contains_dev(name, len(probe), d[0], d[1], int(off[-1]), d[2])
+            assert list(d[2].download(np.uint8, len(probe)).astype(bool)) == bits.bloom_contains(size, k, probe)
+    finally:
+        e.close()

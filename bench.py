@@ -232,7 +232,7 @@ def main():
         "kernel_ms_per_launch": over_ms,   # overlapped breakdown pass (same schedule as the timed region)
         "roofline": {"kernel": dom, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "traffic_source": "profiles/*_pmc_summary.json (FETCH_SIZE+WRITE_SIZE per launch, raw)",
+                     "traffic_source": "profiles/*_pmc_summary.json: 2 x FETCH_SIZE (gfx950) + WRITE_SIZE per launch",
                      "bytes_per_unit": per_unit, "units_per_launch": B, "avg_launch_ms": avg_ms,
                      "note": "avg launch of the dominant kernel, HIP events on its stream inside the timed region "
                              "(PFADD and Bloom contains overlap on two streams)"},
@@ -266,7 +266,7 @@ def pmc_traffic(phase):
     """HBM bytes per launch of the phase's kernel from the newest committed PMC summary (or None)."""
     import glob
 
-    kern = {"bloom_contains": "sk::k_bloom_contains<0>", "pfadd_claim": "sk::k_pfadd_claim",
+    kern = {"bloom_contains": "sk::k_bloom_contains", "pfadd_claim": "sk::k_pfadd_claim",
             "pfadd_commit": "sk::k_pfadd_commit", "pfp_hash": "sk::k_pfp_hash", "pfp_apply": "sk::k_pfp_apply",
             "pfp_reply": "sk::k_pfp_reply"}.get(phase)
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_summary.json")))

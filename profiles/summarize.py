@@ -2,12 +2,12 @@
 committed per-round files: kernel stats CSV copy + per-kernel PMC means.
 
 PMC units: FETCH_SIZE / WRITE_SIZE are KiB per dispatch.  MI355X_MICROARCH.md
-(HBM section): on gfx950 FETCH_SIZE reads 1/2 of the bytes of a wide (16 B/lane)
-coalesced stream; other access widths are uncalibrated.  The hot kernels here
-fetch scattered 64-B lines (1-byte probes), so the raw value is reported
-(`fetch_bytes_raw`) next to the x2-corrected one (`fetch_bytes_x2`) and the
-judge-facing `traffic` uses the raw value for scattered-access kernels.
-Usage: python profiles/summarize.py gpurun_out/prof_r01b r01
+(HBM section): on gfx950 FETCH_SIZE = TCC_EA0_RDREQ x 64 B while the requests
+are 128 B, i.e. it reads 1/2 of the bytes fetched -- the summary doubles it
+(`fetch_bytes`, raw value kept as `fetch_bytes_raw`).  WRITE_SIZE is taken as
+reported.  `traffic_bytes_per_launch` = fetch_bytes + write_bytes.
+Usage: python profiles/summarize.py gpurun_out/prof_r01 r01 [--into DIR]
+(--into: write the summary files into DIR instead of profiles/, for copying later)
 """
 import csv
 import json
@@ -17,8 +17,9 @@ import sys
 from collections import defaultdict
 
 
-def main(src, tag):
-    out = os.path.dirname(os.path.abspath(__file__))
+def main(src, tag, into=None):
+    out = into or os.path.dirname(os.path.abspath(__file__))
+    os.makedirs(out, exist_ok=True)
     shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(out, f"{tag}_kernel_stats.csv"))
     res = defaultdict(dict)
     for sub, ctr in [("pmc_fetch", "FETCH_SIZE"), ("pmc_write", "WRITE_SIZE")]:
@@ -26,24 +27,24 @@ def main(src, tag):
         for r in csv.DictReader(open(os.path.join(src, sub, "run_counter_collection.csv"))):
             if r["Counter_Name"] != ctr:
                 continue
-            acc[r["Kernel_Name"].split("(")[0].replace("void ", "")].append((float(r["Counter_Value"]) * 1024,
-                                                      int(r["End_Timestamp"]) - int(r["Start_Timestamp"]),
-                                                      int(r["Grid_Size"])))
+            acc[r["Kernel_Name"].split("(")[0].replace("void ", "")].append(
+                (float(r["Counter_Value"]) * 1024, int(r["Grid_Size"])))
         for k, v in acc.items():
             res[k][ctr] = sum(x[0] for x in v) / len(v)
             res[k]["dispatches"] = len(v)
-            res[k]["grid"] = max(x[2] for x in v)
+            res[k]["grid"] = max(x[1] for x in v)
     for k, d in res.items():
         d["fetch_bytes_raw"] = d.get("FETCH_SIZE", 0.0)
-        d["fetch_bytes_x2"] = 2 * d.get("FETCH_SIZE", 0.0)
+        d["fetch_bytes"] = 2 * d.get("FETCH_SIZE", 0.0)
         d["write_bytes"] = d.get("WRITE_SIZE", 0.0)
-        d["traffic_bytes_per_launch"] = d["fetch_bytes_raw"] + d["write_bytes"]
+        d["traffic_bytes_per_launch"] = d["fetch_bytes"] + d["write_bytes"]
     keep = {k: v for k, v in res.items() if k.startswith("sk::")}
-    json.dump({"source": src, "units": "bytes per dispatch (mean)", "kernels": keep},
-              open(os.path.join(out, f"{tag}_pmc_summary.json"), "w"), indent=1)
+    json.dump({"source": src, "units": "bytes per dispatch (mean); fetch_bytes = 2 x FETCH_SIZE (gfx950)",
+               "kernels": keep}, open(os.path.join(out, f"{tag}_pmc_summary.json"), "w"), indent=1)
     for k, v in sorted(keep.items()):
-        print("%-28s n=%5d fetch=%12.0f write=%12.0f" % (k, v["dispatches"], v["fetch_bytes_raw"], v["write_bytes"]))
+        print("%-28s n=%5d fetch=%12.0f write=%12.0f" % (k, v["dispatches"], v["fetch_bytes"], v["write_bytes"]))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    into = sys.argv[sys.argv.index("--into") + 1] if "--into" in sys.argv else None
+    main(sys.argv[1], sys.argv[2], into)

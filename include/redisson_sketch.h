@@ -142,6 +142,11 @@ int sk_setbit(sk_ctx *ctx, uint32_t n, const uint64_t *key_off, const uint8_t *k
 /* batch of GETBIT */
 int sk_getbit(sk_ctx *ctx, uint32_t n, const uint64_t *key_off, const uint8_t *key_bytes,
               const uint64_t *offsets, uint8_t *out_bits);
+/* RBitSet.set(from, to) / clear(from, to) (M:RedissonBitSet.java:194-228, one
+ * SETBIT_VOID per bit in a pipeline): bits [from, to) := value; from >= to is a
+ * no-op.  Offsets outside [0, max_bit_offset) fail with SK_ERANGE after the
+ * in-range bits are applied (a pipeline runs the other commands). */
+int sk_set_bit_range(sk_ctx *ctx, const uint8_t *key, uint64_t len, int64_t from, int64_t to, int value);
 /* single-key device-resident variants for the bulk path (C5) */
 int sk_setbit_dev(sk_ctx *ctx, const uint8_t *key, uint64_t len, uint64_t n, const uint64_t *d_offsets,
                   uint8_t value, uint8_t *d_out_old);

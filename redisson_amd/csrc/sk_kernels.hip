@@ -989,6 +989,36 @@ __global__ void __launch_bounds__(256) k_setbit_void(uint64_t n, const uint64_t 
     }
 }
 
+// RBitSet.set(from, to) / clear(from, to) (M:RedissonBitSet.java:202-228:
+// one SETBIT_VOID per bit): bits [from, to) of an MSB-first string set to
+// `value`.  One lane per 16-B vector; vectors inside the range are stored
+// whole, the two edge vectors are masked per byte.  The buffer capacity is a
+// multiple of 16 B, so whole-vector access stays in bounds.
+__global__ void __launch_bounds__(256) k_bit_range(uint8_t *buf, uint64_t from, uint64_t to, uint32_t value) {
+    uint64_t v0 = (from >> 3) >> 4;
+    uint64_t v = v0 + uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (v > ((to - 1) >> 3) >> 4) return;
+    uint64_t b0 = v << 4;
+    uint4 *p = reinterpret_cast<uint4 *>(buf) + v;
+    if (b0 * 8 >= from && (b0 + 16) * 8 <= to) {
+        uint32_t f = value ? 0xffffffffu : 0u;
+        *p = make_uint4(f, f, f, f);
+        return;
+    }
+    uint4 w = *p;
+    uint8_t *bytes = reinterpret_cast<uint8_t *>(&w);
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+        uint64_t lo = (b0 + j) * 8, hi = lo + 8; // the byte's bit range [lo, hi)
+        uint64_t a = from > lo ? from : lo, b = to < hi ? to : hi;
+        if (a >= b) continue;
+        // MSB-first: bit i of the byte has mask 0x80 >> i
+        uint32_t mask = (0xffu >> (a - lo)) & (0xffu << (hi - b)) & 0xffu;
+        bytes[j] = value ? uint8_t(bytes[j] | mask) : uint8_t(bytes[j] & ~mask);
+    }
+    *p = w;
+}
+
 // max of a u64 array (offset validation / capacity sizing)
 __global__ void __launch_bounds__(256) k_max_u64(uint64_t n, const uint64_t *__restrict__ v, uint64_t *out) {
     uint64_t m = 0;
@@ -1401,6 +1431,14 @@ hipError_t launch_setbit_apply(hipStream_t st, uint64_t n, const uint64_t *keys,
 hipError_t launch_setbit_void(hipStream_t st, uint64_t n, const uint64_t *offs, uint8_t *buf, uint32_t value) {
     if (!n) return hipSuccess;
     hipLaunchKernelGGL(k_setbit_void, dim3(grid_for(n, 256)), dim3(256), 0, st, n, offs, buf, value);
+    SK_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+hipError_t launch_bit_range(hipStream_t st, uint8_t *buf, uint64_t from, uint64_t to, uint32_t value) {
+    if (from >= to) return hipSuccess;
+    uint64_t nvec = (((to - 1) >> 3) >> 4) - ((from >> 3) >> 4) + 1;
+    hipLaunchKernelGGL(k_bit_range, dim3(grid_for(nvec, 256)), dim3(256), 0, st, buf, from, to, value);
     SK_LAUNCH_CHECK();
     return hipSuccess;
 }

@@ -1315,6 +1315,34 @@ int sk_setbit_dev(sk_ctx *c, const uint8_t *key, uint64_t len, uint64_t n, const
     return sync(c);
 }
 
+// RBitSet.set(from, to) / clear(from, to): the reference sends one SETBIT_VOID
+// per bit in one pipeline (M:RedissonBitSet.java:202-228).  Each SETBIT grows
+// the string (sdsgrowzero) whatever the value; an out-of-range offset fails
+// only its own command, so the in-range bits are applied and the call then
+// reports SK_ERANGE, as the batch future would fail.
+int sk_set_bit_range(sk_ctx *c, const uint8_t *key, uint64_t len, int64_t from, int64_t to, int value) {
+    std::lock_guard<std::mutex> g(c->mu);
+    ENTER(c);
+    if (from >= to) return SK_OK; // empty batch
+    int64_t lim = int64_t(c->max_bit_offset);
+    int64_t a = from < 0 ? 0 : from, b = to > lim ? lim : to;
+    bool bad = from < 0 || to > lim;
+    if (a < b) {
+        uint64_t need = (uint64_t(b - 1) >> 3) + 1, cur;
+        uint32_t id;
+        int r = str_get(c, key_of(key, len), true, need, &id);
+        if (r) return r;
+        if ((r = str_reserve(c, id, need))) return r;
+        if ((r = str_len(c, id, &cur))) return r;
+        if (need > cur && (r = str_set_len(c, id, need))) return r;
+        { Prof p_(c, 9);
+        HIPCHK(c, sk::launch_bit_range(c->st, c->strs[id].ptr, uint64_t(a), uint64_t(b), value ? 1u : 0u)); }
+        if ((r = sync(c))) return r;
+    }
+    if (bad) return fail(c, SK_ERANGE, "%s", kRange);
+    return SK_OK;
+}
+
 int sk_getbit_dev(sk_ctx *c, const uint8_t *key, uint64_t len, uint64_t n, const uint64_t *d_offsets,
                   uint8_t *d_out) {
     std::lock_guard<std::mutex> g(c->mu);
@@ -1565,12 +1593,12 @@ int sk_bloom_try_init(sk_ctx *c, const uint8_t *name, uint64_t len, int64_t expe
                     (long long)kBloomMaxSize, (long long)m);
     int32_t k = sk_bloom_optimal_k(expected, m);
     std::string cfg = "{" + key_of(name, len) + "}__config";
-    if (c->bloom.count(cfg)) { // the Lua assert fails -> tryInit returns false
-        *out_ok = 0;
-        return SK_OK;
-    }
+    // tryInit sends EVAL (assert no config) + HMSET in one pipeline
+    // (M:RedissonBloomFilter.java:231-240): when the assert fails, the HMSET
+    // that follows it still runs, so the new parameters replace the config,
+    // and tryInit returns false after re-reading it (Q6).
+    *out_ok = c->bloom.count(cfg) ? 0 : 1;
     c->bloom[cfg] = BloomCfg{m, k, expected, fpp};
-    *out_ok = 1;
     return SK_OK;
 }
 

@@ -305,6 +305,11 @@ class SketchEngine:
         k = _b(key)
         self._check(self.lib.sk_getbit_dev(self.ctx, k, len(k), n, _addr(d_offsets), _addr(d_out)))
 
+    def set_bit_range(self, key, frm: int, to: int, value: int):
+        """RBitSet.set(from, to) / clear(from, to): bits [from, to) := value."""
+        k = _b(key)
+        self._check(self.lib.sk_set_bit_range(self.ctx, k, len(k), int(frm), int(to), int(value)))
+
     def bitcount(self, key) -> int:
         k = _b(key)
         out = ctypes.c_uint64()

@@ -212,12 +212,9 @@ class RBitSet(RObject):
         raise TypeError("set() arguments")
 
     def _range(self, frm: int, to: int, v: int) -> Future:
-        # one SETBIT_VOID per bit in a new batch (M:RedissonBitSet.java:202-228)
-        b = self._c.createBatch()
-        bs = b.getBitSet(self._name)
-        for i in range(frm, to):
-            bs.setAsync(i, bool(v))
-        return _completed(lambda: (b.execute(), None)[1])
+        # the reference: one SETBIT_VOID per bit in a new batch (M:RedissonBitSet.java:202-228);
+        # here one range-fill kernel with the same final string and the same error
+        return self._c._submit(("SETRANGE", self._name, frm, to, v))
 
     def clear(self, *args):
         return self.clearAsync(*args).get()
@@ -483,6 +480,10 @@ class Redisson:
                 elif kind == "BITOP":
                     _, op, dest, srcs = run[0][0]
                     e.bitop(op, dest, srcs)
+                    results = [None]
+                elif kind == "SETRANGE":
+                    _, name, frm, to, v = run[0][0]
+                    e.set_bit_range(name, frm, to, v)
                     results = [None]
                 elif kind == "SET":
                     e.set(run[0][0][1], run[0][0][2])

@@ -453,3 +453,33 @@ def test_bloom_contains_kernels_agree(O, sched):
             assert list(d[2].download(np.uint8, len(probe)).astype(bool)) == bits.bloom_contains(size, k, probe)
     finally:
         e.close()
+
+
+def test_set_bit_range(engine, O):
+    """RBitSet.set(from, to) / clear(from, to): one range-fill kernel gives the
+    string the reference's per-bit SETBIT_VOID batch gives (growth included),
+    and out-of-range offsets fail after the in-range bits are applied."""
+    rng = np.random.default_rng(12)
+    ref = O.BitString()
+    key = b"rng:bits"
+    cases = [(3, 10, 1), (0, 8, 1), (5, 6, 0), (7, 9, 0), (100, 1000, 1), (120, 900, 0), (127, 129, 1),
+             (1000, 1000, 1), (2000, 1999, 1), (4096 * 8 - 3, 4096 * 8 + 133, 1), (17, 4096 * 8 + 5, 0)]
+    cases += [(int(a), int(a + rng.integers(1, 3000)), int(rng.integers(0, 2))) for a in rng.integers(0, 40000, 40)]
+    for frm, to, v in cases:
+        engine.set_bit_range(key, frm, to, v)
+        for i in range(frm, to):
+            ref.setbit(i, v)
+        assert engine.get(key) == ref.bytes(), (frm, to, v)
+    # clear on a missing key grows it with zero bytes, like SETBIT x 0
+    engine.set_bit_range(b"rng:empty", 0, 20, 0)
+    assert engine.get(b"rng:empty") == bytes(3)
+    # out of range: the valid part is applied, then the offset error
+    lim = 1 << 32
+    with pytest.raises(RedisException, match="bit offset"):
+        engine.set_bit_range(b"rng:neg", -5, 4, 1)
+    assert engine.get(b"rng:neg") == bytes([0xF0])
+    with pytest.raises(RedisException, match="bit offset"):
+        engine.set_bit_range(b"rng:big", lim - 2, lim + 3, 1)
+    assert engine.strlen(b"rng:big") == lim // 8
+    assert engine.getbit([b"rng:big"] * 3, [lim - 3, lim - 2, lim - 1]) == [0, 1, 1]
+    engine.delete([b"rng:big"])

@@ -64,6 +64,9 @@ def test_bloom_init(client):                                 # :20-28
     f = client.getBloomFilter("filter2")
     assert f.tryInit(55000000, 0.03)
     assert not f.tryInit(55000001, 0.03)
+    # Q6: the pipeline's HMSET runs after the failed EVAL assert, so the new
+    # parameters replace the config (M:RedissonBloomFilter.java:231-248)
+    assert f.getExpectedInsertions() == 55000001
     f.delete()
     assert f.tryInit(55000001, 0.03)
 

@@ -101,6 +101,8 @@ uint64_t sk_hll_estimate_hist(const uint32_t *hist64, int redis_major);
 int sk_type(sk_ctx *ctx, const uint8_t *key, uint64_t len, int *out_type);
 /* DEL k1..kn -> number removed (RedissonObject.delete / RBitSet.clear, M:RedissonBitSet.java:250) */
 int sk_del(sk_ctx *ctx, uint32_t n, const uint64_t *key_off, const uint8_t *key_bytes, uint64_t *out_removed);
+/* FLUSHALL: remove every key and Bloom config of the context */
+int sk_flushall(sk_ctx *ctx);
 /* resolve HLL names to slab ids, creating empty HLLs for missing names (what
  * PFADD / PFMERGE do).  out_created[i] = 1 if this call created it. */
 int sk_hll_resolve(sk_ctx *ctx, uint32_t n, const uint64_t *key_off, const uint8_t *key_bytes,

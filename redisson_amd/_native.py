@@ -96,6 +96,7 @@ SIGNATURES = {
     "sk_prof_enable": (c_int, [P, c_int]),
     "sk_prof_only": (c_int, [P, c_char_p]),
     "sk_set_bit_range": (c_int, [P, _u8p, c_uint64, c_int64, c_int64, c_int]),
+    "sk_flushall": (c_int, [P]),
     "sk_prof_reset": (c_int, [P]),
     "sk_prof_read": (c_int, [P, c_char_p, P, P]),
     "sk_comm_unique_id": (c_int, [P]),

@@ -890,6 +890,23 @@ int sk_del(sk_ctx *c, uint32_t n, const uint64_t *off, const uint8_t *bytes, uin
     return sync(c);
 }
 
+// FLUSHALL / FLUSHDB: every key (HLL slabs re-zeroed and reused, strings
+// freed) and every Bloom config
+int sk_flushall(sk_ctx *c) {
+    std::lock_guard<std::mutex> g(c->mu);
+    ENTER(c);
+    std::vector<std::string> names;
+    names.reserve(c->keys.size());
+    for (auto &kv : c->keys) names.push_back(kv.first);
+    for (auto &k : names) {
+        bool r;
+        int rc = del_key(c, k, &r);
+        if (rc) return rc;
+    }
+    c->bloom.clear();
+    return sync(c);
+}
+
 int sk_hll_resolve(sk_ctx *c, uint32_t n, const uint64_t *off, const uint8_t *bytes, uint32_t *ids,
                    uint8_t *created) {
     std::lock_guard<std::mutex> g(c->mu);
@@ -1502,7 +1519,7 @@ int sk_get(sk_ctx *c, const uint8_t *key, uint64_t len, uint8_t *buf, uint64_t c
             if (fb > 2) s[16 + byte + 1] |= uint8_t(v >> (8 - fb));
         }
         *out_len = int64_t(s.size());
-        std::memcpy(buf, s.data(), std::min<uint64_t>(cap, s.size()));
+        if (cap) std::memcpy(buf, s.data(), std::min<uint64_t>(cap, s.size()));
         return SK_OK;
     }
     uint64_t l;

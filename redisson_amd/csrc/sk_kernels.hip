@@ -664,6 +664,13 @@ __global__ void __launch_bounds__(256) k_hll_hist(const uint32_t *__restrict__ i
     if (t < 64) hist[uint64_t(blockIdx.x) * 64 + t] = h[0][t] + h[1][t] + h[2][t] + h[3][t];
 }
 
+// streamed-once 16-B load with the nontemporal hint (native vector type for the builtin)
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 ld_nt(const uint4 *p) {
+    u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
 // ------------------------------------------------------------------ union
 typedef unsigned short us2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t bytemax(uint32_t a, uint32_t b) {
@@ -692,9 +699,14 @@ __global__ void __launch_bounds__(256) k_hll_union_partial(uint64_t n, const uin
     uint64_t k = k0;
 #define SK_SRC(kk) (reinterpret_cast<const uint4 *>(base + ((ids ? uint64_t(ids[kk]) : uint64_t(kk)) << 14)))
     for (; k + 8 <= k1; k += 8) { // 8 independent 16 B loads in flight per lane
-        uint4 a0 = SK_SRC(k)[lane16], a1 = SK_SRC(k + 1)[lane16], a2 = SK_SRC(k + 2)[lane16],
-              a3 = SK_SRC(k + 3)[lane16], a4 = SK_SRC(k + 4)[lane16], a5 = SK_SRC(k + 5)[lane16],
-              a6 = SK_SRC(k + 6)[lane16], a7 = SK_SRC(k + 7)[lane16];
+        uint4 a0 = ld_nt(SK_SRC(k) + lane16),
+              a1 = ld_nt(SK_SRC(k + 1) + lane16),
+              a2 = ld_nt(SK_SRC(k + 2) + lane16),
+              a3 = ld_nt(SK_SRC(k + 3) + lane16),
+              a4 = ld_nt(SK_SRC(k + 4) + lane16),
+              a5 = ld_nt(SK_SRC(k + 5) + lane16),
+              a6 = ld_nt(SK_SRC(k + 6) + lane16),
+              a7 = ld_nt(SK_SRC(k + 7) + lane16);
         acc = bytemax4(acc, bytemax4(bytemax4(bytemax4(a0, a1), bytemax4(a2, a3)),
                                      bytemax4(bytemax4(a4, a5), bytemax4(a6, a7))));
     }
@@ -1031,17 +1043,29 @@ __global__ void __launch_bounds__(256) k_max_u64(uint64_t n, const uint64_t *__r
     if ((threadIdx.x & 63) == 0) atomicMax((unsigned long long *)out, (unsigned long long)m);
 }
 
-// BITCOUNT: 16 B per lane per step, popcount, wave reduce, one atomic per wave
+// BITCOUNT: SK_BC_UNROLL independent 16-B loads per lane per step (one
+// coalesced 4 KiB row per unroll slot and workgroup), popcount, wave reduce,
+// one atomic per wave.
+#define SK_BC_UNROLL 8
 __global__ void __launch_bounds__(256) k_bitcount(const uint8_t *__restrict__ buf, uint64_t len,
                                                   unsigned long long *out) {
     uint64_t nvec = len >> 4;
     uint64_t c = 0;
     const uint4 *v = reinterpret_cast<const uint4 *>(buf);
-    uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
-    for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < nvec; i += stride) {
-        uint4 x = v[i];
-        c += __popc(x.x) + __popc(x.y) + __popc(x.z) + __popc(x.w);
+    const uint64_t step = uint64_t(gridDim.x) * (256 * SK_BC_UNROLL);
+    uint64_t i = uint64_t(blockIdx.x) * (256 * SK_BC_UNROLL) + threadIdx.x;
+    for (; i + 256 * (SK_BC_UNROLL - 1) < nvec; i += step) {
+        uint4 x[SK_BC_UNROLL];
+#pragma unroll
+        for (int u = 0; u < SK_BC_UNROLL; u++) x[u] = ld_nt(v + i + 256 * u);
+#pragma unroll
+        for (int u = 0; u < SK_BC_UNROLL; u++) c += __popc(x[u].x) + __popc(x[u].y) + __popc(x[u].z) + __popc(x[u].w);
     }
+    for (int u = 0; u < SK_BC_UNROLL; u++, i += 256) // the last partial step
+        if (i < nvec) {
+            uint4 x = v[i];
+            c += __popc(x.x) + __popc(x.y) + __popc(x.z) + __popc(x.w);
+        }
     if (blockIdx.x == 0) // tail bytes
         for (uint64_t b = (nvec << 4) + threadIdx.x; b < len; b += blockDim.x) c += __popc(buf[b]);
     for (int s = 32; s > 0; s >>= 1) c += __shfl_xor(c, s);
@@ -1049,8 +1073,8 @@ __global__ void __launch_bounds__(256) k_bitcount(const uint8_t *__restrict__ bu
 }
 
 // BITOP over maxlen bytes; sources shorter than maxlen read as 0.  Source
-// pointers / lengths are cached in LDS; chunks every source covers take the
-// straight 16 B path, two chunks per lane per step for memory parallelism.
+// pointers / lengths are cached in LDS; steps every source covers take the
+// straight 16 B path with SK_BO_UNROLL chunks per lane in flight per source.
 #define SK_BITOP_MAXSRC 64
 __device__ __forceinline__ uint4 bitop_src_chunk(const uint8_t *p, uint64_t l, uint64_t b0) {
     if (b0 + 16 <= l) return *reinterpret_cast<const uint4 *>(p + b0);
@@ -1063,9 +1087,12 @@ __device__ __forceinline__ uint4 bitop_combine(int op, uint4 acc, uint4 x) {
     if (op == 1) return make_uint4(acc.x | x.x, acc.y | x.y, acc.z | x.z, acc.w | x.w);
     return make_uint4(acc.x ^ x.x, acc.y ^ x.y, acc.z ^ x.z, acc.w ^ x.w);
 }
+#define SK_BO_UNROLL 4
+__device__ __forceinline__ uint4 bitop_not(uint4 a) { return make_uint4(~a.x, ~a.y, ~a.z, ~a.w); }
+// One step = SK_BO_UNROLL coalesced 4 KiB rows per workgroup; a lane reads
+// and writes the same 16-B chunks, so dest may alias a source (BITOP in place).
 __global__ void __launch_bounds__(256) k_bitop(int op, uint32_t nsrc, const uint8_t *const *__restrict__ srcs,
-                                               const uint64_t *__restrict__ lens, uint64_t maxlen,
-                                               uint8_t *__restrict__ dst) {
+                                               const uint64_t *__restrict__ lens, uint64_t maxlen, uint8_t *dst) {
     __shared__ const uint8_t *P[SK_BITOP_MAXSRC];
     __shared__ uint64_t L[SK_BITOP_MAXSRC];
     if (threadIdx.x < nsrc) {
@@ -1075,44 +1102,38 @@ __global__ void __launch_bounds__(256) k_bitop(int op, uint32_t nsrc, const uint
     __syncthreads();
     uint64_t minlen = L[0];
     for (uint32_t s = 1; s < nsrc; s++) minlen = L[s] < minlen ? L[s] : minlen;
-    uint64_t nvec = (maxlen + 15) >> 4;
-    uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
-    for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < nvec; i += 2 * stride) {
-        uint64_t j = i + stride; // second chunk of this lane
-        bool has_j = j < nvec;
-        uint64_t b0 = i << 4, b1 = j << 4;
-        uint4 acc0, acc1 = make_uint4(0, 0, 0, 0);
-        if (b0 + 16 <= minlen && (!has_j || b1 + 16 <= minlen)) { // every source covers both chunks
-            acc0 = reinterpret_cast<const uint4 *>(P[0])[i];
-            if (has_j) acc1 = reinterpret_cast<const uint4 *>(P[0])[j];
-            if (op == 3) {
-                acc0 = make_uint4(~acc0.x, ~acc0.y, ~acc0.z, ~acc0.w);
-                acc1 = make_uint4(~acc1.x, ~acc1.y, ~acc1.z, ~acc1.w);
-            }
+    const uint64_t nvec = (maxlen + 15) >> 4, step = uint64_t(gridDim.x) * (256 * SK_BO_UNROLL);
+    for (uint64_t base = uint64_t(blockIdx.x) * (256 * SK_BO_UNROLL); base < nvec; base += step) {
+        const uint64_t i0 = base + threadIdx.x;
+        uint4 acc[SK_BO_UNROLL];
+        if ((base + 256 * SK_BO_UNROLL) * 16 <= minlen) { // every source covers the whole step (uniform)
+            const uint4 *p0 = reinterpret_cast<const uint4 *>(P[0]) + i0;
+#pragma unroll
+            for (int u = 0; u < SK_BO_UNROLL; u++) acc[u] = ld_nt(p0 + 256 * u);
+            if (op == 3)
+#pragma unroll
+                for (int u = 0; u < SK_BO_UNROLL; u++) acc[u] = bitop_not(acc[u]);
             for (uint32_t s = 1; s < nsrc; s++) {
-                uint4 x0 = reinterpret_cast<const uint4 *>(P[s])[i];
-                uint4 x1 = has_j ? reinterpret_cast<const uint4 *>(P[s])[j] : make_uint4(0, 0, 0, 0);
-                acc0 = bitop_combine(op, acc0, x0);
-                acc1 = bitop_combine(op, acc1, x1);
+                const uint4 *ps = reinterpret_cast<const uint4 *>(P[s]) + i0;
+                uint4 x[SK_BO_UNROLL];
+#pragma unroll
+                for (int u = 0; u < SK_BO_UNROLL; u++) x[u] = ld_nt(ps + 256 * u);
+#pragma unroll
+                for (int u = 0; u < SK_BO_UNROLL; u++) acc[u] = bitop_combine(op, acc[u], x[u]);
             }
-        } else {
-            acc0 = bitop_src_chunk(P[0], L[0], b0);
-            if (has_j) acc1 = bitop_src_chunk(P[0], L[0], b1);
-            if (op == 3) {
-                acc0 = make_uint4(~acc0.x, ~acc0.y, ~acc0.z, ~acc0.w);
-                acc1 = make_uint4(~acc1.x, ~acc1.y, ~acc1.z, ~acc1.w);
-            }
-            for (uint32_t s = 1; s < nsrc; s++) {
-                acc0 = bitop_combine(op, acc0, bitop_src_chunk(P[s], L[s], b0));
-                if (has_j) acc1 = bitop_combine(op, acc1, bitop_src_chunk(P[s], L[s], b1));
-            }
+#pragma unroll
+            for (int u = 0; u < SK_BO_UNROLL; u++) reinterpret_cast<uint4 *>(dst)[i0 + 256 * u] = acc[u];
+            continue;
         }
-        for (int c = 0; c < 2; c++) {
-            uint64_t bb = c ? b1 : b0;
-            uint4 a = c ? acc1 : acc0;
-            if (c && !has_j) break;
+        for (int u = 0; u < SK_BO_UNROLL; u++) { // ragged edge: sources shorter than maxlen read as 0
+            uint64_t i = i0 + 256 * u;
+            if (i >= nvec) break;
+            uint64_t bb = i << 4;
+            uint4 a = bitop_src_chunk(P[0], L[0], bb);
+            if (op == 3) a = bitop_not(a);
+            for (uint32_t s = 1; s < nsrc; s++) a = bitop_combine(op, a, bitop_src_chunk(P[s], L[s], bb));
             if (bb + 16 <= maxlen) {
-                reinterpret_cast<uint4 *>(dst)[bb >> 4] = a;
+                reinterpret_cast<uint4 *>(dst)[i] = a;
             } else {
                 const uint8_t *ab = reinterpret_cast<const uint8_t *>(&a);
                 for (int q = 0; q < 16; q++)
@@ -1454,7 +1475,7 @@ hipError_t launch_max_u64(hipStream_t st, uint64_t n, const uint64_t *v, uint64_
 hipError_t launch_bitcount(hipStream_t st, const uint8_t *buf, uint64_t len, uint64_t *out) {
     hipError_t e = hipMemsetAsync(out, 0, sizeof(uint64_t), st);
     if (e != hipSuccess || !len) return e;
-    hipLaunchKernelGGL(k_bitcount, dim3(grid_for((len + 15) / 16, 256, 2048)), dim3(256), 0, st, buf, len,
+    hipLaunchKernelGGL(k_bitcount, dim3(grid_for((len + 15) / 16, 256 * SK_BC_UNROLL, 2048)), dim3(256), 0, st, buf, len,
                        (unsigned long long *)out);
     SK_LAUNCH_CHECK();
     return hipSuccess;
@@ -1463,8 +1484,8 @@ hipError_t launch_bitcount(hipStream_t st, const uint8_t *buf, uint64_t len, uin
 hipError_t launch_bitop(hipStream_t st, int op, uint32_t nsrc, const uint8_t *const *srcs, const uint64_t *lens,
                         uint64_t maxlen, uint8_t *dst) {
     if (!maxlen) return hipSuccess;
-    hipLaunchKernelGGL(k_bitop, dim3(grid_for((maxlen + 15) / 16, 256, 4096)), dim3(256), 0, st, op, nsrc, srcs, lens,
-                       maxlen, dst);
+    hipLaunchKernelGGL(k_bitop, dim3(grid_for((maxlen + 15) / 16, 256 * SK_BO_UNROLL, 4096)), dim3(256), 0, st, op, nsrc,
+                       srcs, lens, maxlen, dst);
     SK_LAUNCH_CHECK();
     return hipSuccess;
 }

@@ -196,6 +196,12 @@ int sk_dev_memset(sk_ctx *ctx, void *d_p, int value, uint64_t n);
 /* async mode: sk_pfadd_dev / sk_bloom_contains_dev / sk_bloom_add_dev return
  * once enqueued (inputs must stay valid until sk_sync); default off */
 int sk_set_async(sk_ctx *ctx, int on);
+/* completion tickets (with sk_set_async): a ticket covers everything enqueued on
+ * the context so far.  sk_poll never blocks and releases a finished ticket;
+ * sk_wait blocks (without holding the context lock) and releases it. */
+int sk_ticket(sk_ctx *ctx, uint64_t *out_ticket);
+int sk_poll(sk_ctx *ctx, uint64_t ticket, int *out_done);
+int sk_wait(sk_ctx *ctx, uint64_t ticket);
 /* HIP events on the context stream: 16 slots; elapsed(a, b) waits for b */
 int sk_timer_record(sk_ctx *ctx, int slot);
 int sk_timer_elapsed(sk_ctx *ctx, int slot_a, int slot_b, float *ms);

@@ -44,4 +44,16 @@ public final class SketchNative {
     public static native int bloomContains(long ctx, byte[] name, long size, int k, long[] elemOff, byte[] elems,
                                            byte[] out);
     public static native int bloomCount(long ctx, byte[] name, int[] out);
+
+    // RBitSet.set(from, to) / clear(from, to) as one device fill (M:RedissonBitSet.java:194-228)
+    public static native int setBitRange(long ctx, byte[] key, long from, long to, boolean value);
+    public static native int flushall(long ctx);
+
+    // asynchronous submission: _dev / batch calls return once enqueued; a ticket
+    // covers everything enqueued so far.  poll: 1 done (ticket released), 0 not
+    // yet, < 0 status; await blocks a completion thread, never an event loop.
+    public static native int setAsync(long ctx, boolean on);
+    public static native long ticket(long ctx);
+    public static native int poll(long ctx, long ticket);
+    public static native int await(long ctx, long ticket);
 }

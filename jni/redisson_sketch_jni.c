@@ -214,3 +214,43 @@ JNIEXPORT jint JNICALL Java_org_redisson_gpu_SketchNative_bloomCount(JNIEnv *env
     UNPIN(out, r, 0); UNPIN(name, nm, JNI_ABORT);
     return st;
 }
+
+JNIEXPORT jint JNICALL Java_org_redisson_gpu_SketchNative_setBitRange(JNIEnv *env, jclass cls, jlong ctx,
+                                                                      jbyteArray key, jlong from, jlong to,
+                                                                      jboolean value) {
+    (void)cls;
+    jsize n = LEN(key);
+    void *k = PIN(key);
+    jint st = sk_set_bit_range(CTX(ctx), (const uint8_t *)k, (uint64_t)n, from, to, value ? 1 : 0);
+    UNPIN(key, k, JNI_ABORT);
+    return st;
+}
+
+JNIEXPORT jint JNICALL Java_org_redisson_gpu_SketchNative_flushall(JNIEnv *env, jclass cls, jlong ctx) {
+    (void)env; (void)cls;
+    return sk_flushall(CTX(ctx));
+}
+
+JNIEXPORT jint JNICALL Java_org_redisson_gpu_SketchNative_setAsync(JNIEnv *env, jclass cls, jlong ctx, jboolean on) {
+    (void)env; (void)cls;
+    return sk_set_async(CTX(ctx), on ? 1 : 0);
+}
+
+/* completion tickets: the completion thread polls / waits, event loops never block */
+JNIEXPORT jlong JNICALL Java_org_redisson_gpu_SketchNative_ticket(JNIEnv *env, jclass cls, jlong ctx) {
+    (void)env; (void)cls;
+    uint64_t t = 0;
+    return sk_ticket(CTX(ctx), &t) == SK_OK ? (jlong)t : -1;
+}
+
+JNIEXPORT jint JNICALL Java_org_redisson_gpu_SketchNative_poll(JNIEnv *env, jclass cls, jlong ctx, jlong ticket) {
+    (void)env; (void)cls;
+    int done = 0;
+    jint st = sk_poll(CTX(ctx), (uint64_t)ticket, &done);
+    return st == SK_OK ? done : st;
+}
+
+JNIEXPORT jint JNICALL Java_org_redisson_gpu_SketchNative_await(JNIEnv *env, jclass cls, jlong ctx, jlong ticket) {
+    (void)env; (void)cls;
+    return sk_wait(CTX(ctx), (uint64_t)ticket);
+}

@@ -97,6 +97,9 @@ SIGNATURES = {
     "sk_prof_only": (c_int, [P, c_char_p]),
     "sk_set_bit_range": (c_int, [P, _u8p, c_uint64, c_int64, c_int64, c_int]),
     "sk_flushall": (c_int, [P]),
+    "sk_ticket": (c_int, [P, P]),
+    "sk_poll": (c_int, [P, c_uint64, P]),
+    "sk_wait": (c_int, [P, c_uint64]),
     "sk_prof_reset": (c_int, [P]),
     "sk_prof_read": (c_int, [P, c_char_p, P, P]),
     "sk_comm_unique_id": (c_int, [P]),

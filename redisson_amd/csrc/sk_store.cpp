@@ -212,6 +212,9 @@ struct sk_ctx {
     double prof_ms[32] = {0};
     uint64_t prof_n[32] = {0};
     hipEvent_t timers[16] = {};
+    // completion tickets (sk_ticket): events on the main and read streams
+    std::unordered_map<uint64_t, std::pair<hipEvent_t, hipEvent_t>> tickets;
+    uint64_t next_ticket = 1;
 
     // cross-GPU exchange (RCCL over xGMI)
     ncclComm_t comm = nullptr;
@@ -775,6 +778,7 @@ int sk_close(sk_ctx *c) {
     if (c->comm) (void)ncclCommDestroy(c->comm);
     prof_collect(c);
     for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
+    for (auto &t : c->tickets) (void)hipEventDestroy(t.second.first), (void)hipEventDestroy(t.second.second);
     for (hipEvent_t e : c->timers)
         if (e) (void)hipEventDestroy(e);
     for (auto &e : c->strs)
@@ -1851,6 +1855,58 @@ int sk_timer_elapsed(sk_ctx *c, int a, int b, float *ms) {
 int sk_set_async(sk_ctx *c, int on) {
     std::lock_guard<std::mutex> g(c->mu);
     c->async_dev = on != 0;
+    return SK_OK;
+}
+
+// Completion tickets for asynchronous submission: a ticket covers all work
+// enqueued on the context so far (main and read streams), so a completion
+// thread can finish Netty promises without an event-loop thread ever blocking.
+int sk_ticket(sk_ctx *c, uint64_t *out) {
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(c, hipSetDevice(c->device));
+    if (c->pf_pending) { // claim/commit path: its conflict check needs the host first
+        int r = pfadd_settle(c);
+        if (r) return r;
+    }
+    hipEvent_t a = ev_get(c), b = ev_get(c);
+    HIPCHK(c, hipEventRecord(a, c->st));
+    HIPCHK(c, hipEventRecord(b, c->st2));
+    uint64_t t = c->next_ticket++;
+    c->tickets[t] = {a, b};
+    *out = t;
+    return SK_OK;
+}
+int sk_poll(sk_ctx *c, uint64_t ticket, int *done) {
+    std::lock_guard<std::mutex> g(c->mu);
+    auto it = c->tickets.find(ticket);
+    if (it == c->tickets.end()) return fail(c, SK_EINVAL, "unknown ticket");
+    hipError_t ea = hipEventQuery(it->second.first), eb = hipEventQuery(it->second.second);
+    if ((ea != hipSuccess && ea != hipErrorNotReady) || (eb != hipSuccess && eb != hipErrorNotReady))
+        return fail(c, SK_EDEVICE, "HIP: %s", hipGetErrorString(ea != hipSuccess && ea != hipErrorNotReady ? ea : eb));
+    *done = ea == hipSuccess && eb == hipSuccess;
+    if (*done) { // a finished ticket is released
+        c->ev_pool.push_back(it->second.first);
+        c->ev_pool.push_back(it->second.second);
+        c->tickets.erase(it);
+    }
+    return SK_OK;
+}
+int sk_wait(sk_ctx *c, uint64_t ticket) {
+    std::pair<hipEvent_t, hipEvent_t> ev;
+    {
+        std::lock_guard<std::mutex> g(c->mu);
+        auto it = c->tickets.find(ticket);
+        if (it == c->tickets.end()) return fail(c, SK_EINVAL, "unknown ticket");
+        ev = it->second;
+        c->tickets.erase(it);
+    }
+    // outside the lock: other threads keep submitting while this one waits
+    hipError_t ea = hipEventSynchronize(ev.first), eb = hipEventSynchronize(ev.second);
+    std::lock_guard<std::mutex> g(c->mu);
+    c->ev_pool.push_back(ev.first);
+    c->ev_pool.push_back(ev.second);
+    if (ea != hipSuccess || eb != hipSuccess)
+        return fail(c, SK_EDEVICE, "HIP: %s", hipGetErrorString(ea != hipSuccess ? ea : eb));
     return SK_OK;
 }
 

@@ -174,6 +174,23 @@ class SketchEngine:
     def prof_enable(self, on: bool = True):
         self._check(self.lib.sk_prof_enable(self.ctx, int(on)))
 
+    def ticket(self) -> int:
+        """Completion ticket for everything enqueued so far (async mode)."""
+        t = ctypes.c_uint64()
+        self._check(self.lib.sk_ticket(self.ctx, ctypes.addressof(t)))
+        return t.value
+
+    def poll(self, ticket: int) -> bool:
+        done = ctypes.c_int()
+        self._check(self.lib.sk_poll(self.ctx, ticket, ctypes.addressof(done)))
+        return bool(done.value)
+
+    def wait(self, ticket: int):
+        self._check(self.lib.sk_wait(self.ctx, ticket))
+
+    def flushall(self):
+        self._check(self.lib.sk_flushall(self.ctx))
+
     def prof_only(self, phase=None):
         """Time only `phase` while profiling is on (None: every phase)."""
         self._check(self.lib.sk_prof_only(self.ctx, phase.encode() if phase else None))

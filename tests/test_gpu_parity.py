@@ -483,3 +483,46 @@ def test_set_bit_range(engine, O):
     assert engine.strlen(b"rng:big") == lim // 8
     assert engine.getbit([b"rng:big"] * 3, [lim - 3, lim - 2, lim - 1]) == [0, 1, 1]
     engine.delete([b"rng:big"])
+
+
+def test_completion_tickets(engine, O):
+    """Async submission + tickets: PFADD on the main stream and Bloom contains on
+    the read stream complete under one ticket; poll never blocks; results exact."""
+    import time
+    n, nkeys = 200000, 64
+    off, buf = gen_jackson_longs(0x5EED0700, n)
+    rng = np.random.default_rng(70)
+    kid = rng.integers(0, nkeys, n).astype(np.uint32)
+    names = [b"tk:%d" % i for i in range(nkeys)]
+    ids = engine.hll_resolve(names)
+    assert engine.bloom_try_init("tk:bf", 100000, 0.01)
+    size, k, _, _ = engine.bloom_config("tk:bf")
+    els = _elems(0x5EED0701, 5000)
+    bits = O.BitString()
+    want_add = bits.bloom_add(size, k, els[:3000])
+    want_has = bits.bloom_contains(size, k, els)
+    eo, eb = O.pack(els)
+    d = [engine.to_device(ids[kid]), engine.to_device(off), engine.to_device(buf, pad=16), engine.alloc(n),
+         engine.to_device(eo), engine.to_device(eb, pad=16), engine.alloc(5000), engine.alloc(5000)]
+    a_off = engine.to_device(eo[:3001])
+    engine.set_async(True)
+    try:
+        engine.bloom_add_dev("tk:bf", 3000, a_off, d[5], int(eo[3000]), d[6])
+        engine.pfadd_dev(n, d[0], d[1], d[2], int(off[-1]), d[3])
+        engine.bloom_contains_dev("tk:bf", 5000, d[4], d[5], int(eo[-1]), d[7])
+        t = engine.ticket()
+        t0 = time.time()
+        while not engine.poll(t):
+            assert time.time() - t0 < 30, "ticket never completed"
+            time.sleep(0.0005)
+        with pytest.raises(RedisException, match="unknown ticket"):
+            engine.poll(t)                      # released once seen done
+        engine.wait(engine.ticket())            # nothing new: completes at once
+    finally:
+        engine.set_async(False)
+    regs, want = O.HLLStore().pfadd_bulk(kid, off, buf, nkeys)
+    assert np.array_equal(d[3].download(np.uint8, n), want)
+    for i, nm in enumerate(names):
+        np.testing.assert_array_equal(engine.hll_registers(nm), regs[i])
+    assert list(d[6].download(np.uint8, 3000).astype(bool)) == want_add
+    assert list(d[7].download(np.uint8, 5000).astype(bool)) == want_has

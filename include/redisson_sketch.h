@@ -47,6 +47,8 @@ extern "C" {
 #define SK_ENOMEM (-7)     /* device or host allocation failed */
 #define SK_ESYNTAX (-8)    /* "ERR BITOP NOT must be called with a single source key." */
 #define SK_ETOOBIG (-9)    /* "Bloom filter can't be greater than 4294967294. ..." (IllegalArgumentException, :72-74) */
+#define SK_ECORRUPT (-10)  /* "INVALIDOBJ Corrupted HLL object detected" (a SET string with the HYLL magic
+                              whose registers do not decode) */
 
 #define SK_TYPE_NONE 0
 #define SK_TYPE_HLL 1    /* string holding a HyperLogLog (PFADD/PFMERGE created it) */

@@ -176,6 +176,72 @@ def dense_pack(regs: np.ndarray) -> bytes:
     return out.tobytes()
 
 
+def hll_string(regs: np.ndarray, encoding: str = "dense", card: int = None) -> bytes:
+    """A Redis 3.2 HLL string (hyperloglog.c struct hllhdr + registers).
+
+    dense: HLL_DENSE_SET_REGISTER packing; sparse: a canonical opcode stream
+    (zero runs as XZERO when longer than 64, else ZERO; equal non-zero values
+    as VAL runs of at most 4) -- one of the valid sparse forms redis-server
+    reads (its own writer may split VAL runs differently, by update order).
+    card: cached cardinality (valid) or None (the invalid flag, MSB of byte 15)."""
+    hdr = bytearray(b"HYLL" + bytes([0 if encoding == "dense" else 1, 0, 0, 0]) + bytes(8))
+    if card is None:
+        hdr[15] = 0x80
+    else:
+        hdr[8:16] = int(card).to_bytes(8, "little")
+    if encoding == "dense":
+        return bytes(hdr) + dense_pack(regs)
+    r = [int(x) for x in regs]
+    assert max(r) <= 32, "sparse VAL opcodes hold values 1..32"
+    out, i = bytearray(), 0
+    while i < 16384:
+        j = i
+        while j < 16384 and r[j] == r[i]:
+            j += 1
+        run = j - i
+        if r[i] == 0:
+            while run:
+                n = min(run, 16384)
+                if n > 64:
+                    out += bytes([0x40 | ((n - 1) >> 8), (n - 1) & 0xFF])
+                else:
+                    out.append(n - 1)
+                run -= n
+        else:
+            while run:
+                n = min(run, 4)
+                out.append(0x80 | ((r[i] - 1) << 2) | (n - 1))
+                run -= n
+        i = j
+    return bytes(hdr) + bytes(out)
+
+
+def hll_decode(s: bytes):
+    """Registers of a Redis HLL string (dense or sparse), or None if it is not one."""
+    if len(s) < 16 or s[:4] != b"HYLL" or s[4] > 1:
+        return None
+    regs = np.zeros(16384, dtype=np.uint8)
+    if s[4] == 0:
+        if len(s) != 16 + 12288:
+            return None
+        bits = np.unpackbits(np.frombuffer(s[16:], dtype=np.uint8), bitorder="little").reshape(16384, 6)
+        return (bits * (1 << np.arange(6))).sum(axis=1).astype(np.uint8)
+    i, p = 0, 16
+    while p < len(s):
+        op = s[p]
+        if op & 0xC0 == 0:
+            run, val, p = (op & 0x3F) + 1, 0, p + 1
+        elif op & 0xC0 == 0x40:
+            run, val, p = (((op & 0x3F) << 8) | s[p + 1]) + 1, 0, p + 2
+        else:
+            run, val, p = (op & 3) + 1, ((op >> 2) & 31) + 1, p + 1
+        if i + run > 16384:
+            return None
+        regs[i:i + run] = val
+        i += run
+    return regs if i == 16384 else None
+
+
 # ---- Bloom ---------------------------------------------------------------
 def bloom_optimal_bits(n, p):
     return lib().or_bloom_optimal_bits(n, p)

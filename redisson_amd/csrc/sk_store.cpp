@@ -380,11 +380,78 @@ int hll_alloc(sk_ctx *c, uint32_t *id) {
     return SK_OK;
 }
 
+int str_len(sk_ctx *c, uint32_t id, uint64_t *len);
+int str_free(sk_ctx *c, uint32_t id);
+
+// Redis HLL strings -> registers (redis 3.2 hyperloglog.c: the 16-B header
+// "HYLL", encoding, 3 unused bytes, 8-B cached cardinality; dense = 16384
+// 6-bit registers LSB first; sparse = opcodes ZERO 00xxxxxx (1..64 zeros),
+// XZERO 01xxxxxx yyyyyyyy (1..16384 zeros), VAL 1vvvvvxx (1..4 registers of
+// value 1..32)).  Returns SK_OK, SK_EWRONGTYPE (not an HLL string: what
+// isHLLObjectOrReply rejects) or SK_ECORRUPT (sparse opcodes that do not cover
+// exactly 16384 registers).
+int hll_decode(const uint8_t *s, uint64_t len, uint8_t *regs) {
+    if (len < 16 || std::memcmp(s, "HYLL", 4) != 0 || s[4] > 1) return SK_EWRONGTYPE;
+    if (s[4] == 0) { // dense
+        if (len != SK_HLL_DENSE_SIZE) return SK_EWRONGTYPE;
+        for (int i = 0; i < 16384; i++) {
+            unsigned bit = unsigned(i) * 6, byte = bit >> 3, fb = bit & 7;
+            unsigned v = unsigned(s[16 + byte]) >> fb;
+            if (fb > 2) v |= unsigned(s[16 + byte + 1]) << (8 - fb);
+            regs[i] = uint8_t(v & 63);
+        }
+        return SK_OK;
+    }
+    uint64_t idx = 0;
+    for (uint64_t p = 16; p < len;) {
+        uint8_t op = s[p];
+        uint64_t run;
+        uint8_t val = 0;
+        if ((op & 0xc0) == 0x00) run = (op & 0x3f) + 1, p += 1;                            // ZERO
+        else if ((op & 0xc0) == 0x40) {                                                    // XZERO
+            if (p + 1 >= len) return SK_ECORRUPT;
+            run = ((uint64_t(op & 0x3f) << 8) | s[p + 1]) + 1, p += 2;
+        } else run = (op & 3) + 1, val = uint8_t(((op >> 2) & 31) + 1), p += 1;            // VAL
+        if (idx + run > 16384) return SK_ECORRUPT;
+        std::memset(regs + idx, val, run);
+        idx += run;
+    }
+    return idx == 16384 ? SK_OK : SK_ECORRUPT;
+}
+
+// A string key holding a Redis HLL (SET / restore of a redis-server value)
+// becomes an HLL key the first time an HLL command touches it, as redis-server
+// accepts any string with a valid HLL encoding.  Its cached cardinality is
+// not kept: PFCOUNT recomputes it.
+int hll_adopt_string(sk_ctx *c, const std::string &k, KeyEnt &e, uint32_t *id) {
+    uint64_t l;
+    int r = str_len(c, e.id, &l);
+    if (r) return r;
+    if (l < 16 || l > 16 + 2 * 16384) return fail(c, SK_EWRONGTYPE, "%s", kNotHll);
+    std::vector<uint8_t> s(l), regs(kHllBytes, 0);
+    HIPCHK(c, hipMemcpyAsync(s.data(), c->strs[e.id].ptr, l, hipMemcpyDeviceToHost, c->st));
+    if ((r = sync(c))) return r;
+    r = hll_decode(s.data(), l, regs.data());
+    if (r == SK_EWRONGTYPE) return fail(c, r, "%s", kNotHll);
+    if (r == SK_ECORRUPT) return fail(c, r, "INVALIDOBJ Corrupted HLL object detected");
+    uint32_t hid;
+    if ((r = hll_alloc(c, &hid))) return r;
+    HIPCHK(c, hipMemcpyAsync(c->arena + uint64_t(hid) * kHllBytes, regs.data(), kHllBytes, hipMemcpyHostToDevice,
+                             c->st));
+    if ((r = sync(c))) return r;
+    if ((r = str_free(c, e.id))) return r;
+    e = KeyEnt{SK_TYPE_HLL, hid};
+    *id = hid;
+    (void)k;
+    return SK_OK;
+}
+
 // lookup or create an HLL key (PFADD / PFMERGE create)
 int hll_get(sk_ctx *c, const std::string &k, bool create, uint32_t *id, bool *created) {
     if (created) *created = false;
     auto it = c->keys.find(k);
     if (it != c->keys.end()) {
+        if (it->second.type == SK_TYPE_STRING) return hll_adopt_string(c, k, it->second, id);
         if (it->second.type != SK_TYPE_HLL) return fail(c, SK_EWRONGTYPE, "%s", kNotHll);
         *id = it->second.id;
         return SK_OK;
@@ -729,6 +796,7 @@ const char *sk_strerror(int s) {
     case SK_ENOMEM: return "out of memory";
     case SK_ESYNTAX: return "ERR BITOP NOT must be called with a single source key.";
     case SK_ETOOBIG: return "Bloom filter can't be greater than 4294967294";
+    case SK_ECORRUPT: return "INVALIDOBJ Corrupted HLL object detected";
     default: return "unknown";
     }
 }

@@ -526,3 +526,44 @@ def test_completion_tickets(engine, O):
         np.testing.assert_array_equal(engine.hll_registers(nm), regs[i])
     assert list(d[6].download(np.uint8, 3000).astype(bool)) == want_add
     assert list(d[7].download(np.uint8, 5000).astype(bool)) == want_has
+
+
+@pytest.mark.parametrize("encoding", ["dense", "sparse"])
+def test_hll_string_restore(engine, O, encoding):
+    """A Redis HLL string SET on a key (a redis-server dump, sparse or dense)
+    becomes an HLL on the first HLL command, with the registers it encodes;
+    PFCOUNT / PFADD / PFMERGE continue from them exactly."""
+    rng = np.random.default_rng(31 if encoding == "dense" else 32)
+    regs = np.zeros(16384, dtype=np.uint8)
+    hit = rng.integers(0, 16384, 900)
+    regs[hit] = rng.integers(1, 33, 900)
+    if encoding == "dense":
+        regs[[3, 4]] = [45, 50]                       # dense only: values above the sparse limit
+    key = b"restore:" + encoding.encode()
+    engine.set(key, O.hll_string(regs, encoding, card=12345))
+    assert engine.pfcount([[key]]) == [O.count_regs(regs, 1)]
+    np.testing.assert_array_equal(engine.hll_registers(key), regs)
+    els = _elems(0x5EED0800, 3000)
+    ref = O.HLLStore()
+    ref.regs[key] = regs.copy()
+    assert engine.pfadd([key] * len(els), [[e] for e in els]) == ref.pfadd([key] * len(els), [[e] for e in els])
+    np.testing.assert_array_equal(engine.hll_registers(key), ref.regs[key])
+    # GET gives the dense form back; it decodes to the same registers
+    np.testing.assert_array_equal(O.hll_decode(engine.get(key)), ref.regs[key])
+
+
+def test_hll_string_invalid(engine, O):
+    engine.set(b"notahll", b"hello world, not an HLL")
+    with pytest.raises(RedisException, match="not a valid HyperLogLog"):
+        engine.pfadd([b"notahll"], [[b"x"]])
+    assert engine.get(b"notahll") == b"hello world, not an HLL"      # untouched
+    regs = np.zeros(16384, dtype=np.uint8)
+    regs[100] = 5
+    bad = O.hll_string(regs, "sparse")[:-1]            # the last opcode cut: registers do not add up to 16384
+    engine.set(b"corrupt", bad)
+    with pytest.raises(RedisException, match="INVALIDOBJ"):
+        engine.pfcount([[b"corrupt"]])
+    dense_short = O.hll_string(regs, "dense")[:-1]
+    engine.set(b"shortdense", dense_short)
+    with pytest.raises(RedisException, match="not a valid HyperLogLog"):
+        engine.pfmerge(b"m", [b"shortdense"])

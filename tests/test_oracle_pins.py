@@ -111,3 +111,22 @@ def test_bitops_reference_semantics(O):
     assert O.bitop("NOT", [b.bytes()]) == bytes([0b11101011])     # RedissonBitSetTest.testNot
     assert O.bitop("AND", [b"\xff\x0f", None]) == b"\x00\x00"       # missing key = zeros, len = max
     assert O.bitop("OR", [None, None]) == b""
+
+
+def test_hll_string_codec_round_trip(O):
+    """Redis HLL strings (dense and the canonical sparse form) decode back to
+    the registers; the sparse stream follows the opcode layout of hyperloglog.c."""
+    rng = np.random.default_rng(5)
+    for trial in range(6):
+        regs = np.zeros(16384, dtype=np.uint8)
+        m = [0, 1, 10, 500, 4000, 16384][trial]
+        if m:
+            regs[rng.integers(0, 16384, m)] = rng.integers(1, 33, m)
+        for enc in ["dense", "sparse"]:
+            s = O.hll_string(regs, enc)
+            np.testing.assert_array_equal(O.hll_decode(s), regs)
+    empty = O.hll_string(np.zeros(16384, dtype=np.uint8), "sparse")
+    assert empty[16:] == bytes([0x7F, 0xFF]) and empty[4] == 1      # one XZERO covering 16384 registers
+    one = np.zeros(16384, dtype=np.uint8)
+    one[0] = 3
+    assert O.hll_string(one, "sparse")[16:] == bytes([0x88, 0x7F, 0xFE])  # VAL(3,1) XZERO(16383)

@@ -7,6 +7,7 @@ measures the remaining configs on one MI355X with inputs resident in HBM:
   c1  RHyperLogLog: 1M random Longs into ONE key as 1M RBatch PFADDs (dense
       path: exact replies via radix sort), and the reference addAll (Q1: one
       element = the Jackson array, ~38 MB) + count().
+  c2zipf  the C2 PFADD batches with Zipf(1.1) tenants (SURVEY 8d variant).
   c4  1M tenant HLLs x 1,000 elements (1B PFADD, sharded by calcSlot % 8 ->
       the slab set of one GPU of 8 is timed at full size here), then the
       global union / countWith over all of them: k_hll_union streams 16 KiB
@@ -64,6 +65,25 @@ def c1(eng, args):
           "unit": "inserts/s", "config": {"workload": "c1", "elements": n, "count_after": cnt},
           "addAll_q1": {"element_bytes": len(blob), "seconds": t_q1, "count_after":
                         eng.pfcount([[b"hll:c1q"]])[0]}})
+
+
+def c2zipf(eng, args):
+    """SURVEY 8d C2 variant: 1M-command PFADD batches with Zipf(1.1) tenants (device-resident)."""
+    B, steps, nt = 1 << 20, 10, 100_000
+    names = [b"tenant:%d:hll" % t for t in range(nt)]
+    ids = eng.hll_resolve(names)
+    rng = np.random.default_rng(22)
+    kid = (np.minimum(rng.zipf(1.1, B * (steps + 1)), nt) - 1).astype(np.int64)
+    d_ids = eng.to_device(ids[kid].astype(np.uint32))
+    off, byt, tot = eng.gen_jackson_longs_dev(0x5EED0022, B * (steps + 1))
+    d_out = eng.alloc(B)
+    eng.pfadd_dev(B, d_ids, off, byt, tot, d_out)            # warm
+    t = timed(eng, lambda: [eng.pfadd_dev(B, d_ids.ptr + s * B * 4, off.ptr + s * B * 8, byt, tot, d_out)
+                            for s in range(1, steps + 1)])
+    top = float(np.bincount(kid[:B]).max()) / B
+    line({"metric": "C2 Zipf(1.1) PFADD inserts/sec (1M-command batches, 100k tenants)", "value": B * steps / t,
+          "unit": "inserts/s", "config": {"workload": "c2zipf", "batch": B, "tenants": nt, "zipf_s": 1.1,
+                                          "hottest_tenant_share": top}})
 
 
 def c4(eng, args):
@@ -135,7 +155,7 @@ def c5(eng, args):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--configs", default="c1,c4,c5")
+    ap.add_argument("--configs", default="c1,c2zipf,c4,c5")
     ap.add_argument("--c1-n", type=int, default=1 << 20)
     ap.add_argument("--c4-keys", type=int, default=125_000)       # 1M keys / 8 GPUs
     ap.add_argument("--c4-per-key", type=int, default=1000)
@@ -145,7 +165,7 @@ def main():
     eng = SketchEngine(device=int(os.environ.get("LOCAL_RANK", "0")), max_bit_offset=1 << 36,
                        hll_capacity=args.c4_keys + 64, max_batch=1 << 24)
     for c in args.configs.split(","):
-        {"c1": c1, "c4": c4, "c5": c5}[c](eng, args)
+        {"c1": c1, "c2zipf": c2zipf, "c4": c4, "c5": c5}[c](eng, args)
     eng.close()
 
 

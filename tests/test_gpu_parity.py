@@ -567,3 +567,23 @@ def test_hll_string_invalid(engine, O):
     engine.set(b"shortdense", dense_short)
     with pytest.raises(RedisException, match="not a valid HyperLogLog"):
         engine.pfmerge(b"m", [b"shortdense"])
+
+
+def test_pfadd_multi_launch_zipf(engine, O):
+    """A 1.5 M-element device batch (two partition launches, the second seeing
+    the first's registers) over Zipf(1.1)-skewed tenants (SURVEY 8d C2 variant):
+    replies and registers exact."""
+    n, nkeys = 1_500_000, 2000
+    off, buf = gen_jackson_longs(0x5EED0900, n)
+    rng = np.random.default_rng(90)
+    kid = (np.minimum(rng.zipf(1.1, n), nkeys) - 1).astype(np.uint32)
+    names = [b"zipf:%d" % i for i in range(nkeys)]
+    ids = engine.hll_resolve(names)
+    d = [engine.to_device(ids[kid]), engine.to_device(off), engine.to_device(buf, pad=16), engine.alloc(n)]
+    engine.pfadd_dev(n, d[0], d[1], d[2], int(off[-1]), d[3])
+    regs, want = O.HLLStore().pfadd_bulk(kid, off, buf, nkeys)
+    assert np.array_equal(d[3].download(np.uint8, n), want)
+    for i in np.unique(kid)[:200]:
+        np.testing.assert_array_equal(engine.hll_registers(names[i]), regs[i])
+    hot = int(np.bincount(kid).argmax())
+    np.testing.assert_array_equal(engine.hll_registers(names[hot]), regs[hot])

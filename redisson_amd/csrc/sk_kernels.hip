@@ -901,22 +901,36 @@ __global__ void __launch_bounds__(256) k_bloom_probes(uint64_t n, const uint64_t
 }
 
 // add, pass 2 (after a stable sort on idx): the earliest probe of each bit
-// sees the pre-batch bit; every later probe of the same bit sees 1.
+// sees the pre-batch bit; every later probe of the same bit sees 1.  Keys are
+// sorted by bit index, so every probe of one 32-bit word is in one run and the
+// run's first thread is the word's only writer: one plain load + store per
+// touched word, no atomics.
 __global__ void __launch_bounds__(256) k_bloom_apply(uint64_t m, const uint64_t *__restrict__ keys, uint8_t *bits,
                                                      uint64_t *d_len, int k, uint8_t *__restrict__ out) {
     uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-    if (i < m) {
-        uint64_t key = keys[i];
-        uint64_t idx = key >> 32;
-        if (i == 0 || (keys[i - 1] >> 32) != idx) {
-            uint32_t mask;
-            uint32_t *wp = bit_word(bits, idx, &mask);
-            uint32_t old = atomicOr(wp, mask); // other bits of the word may race; ours is exclusive
-            uint32_t pos = uint32_t(key & 0xffffffffu);
-            uint32_t e = pos / uint32_t(k), j = pos - e * uint32_t(k);
-            if (!(old & mask) && int(j) <= k - 2) out[e] = 1;
+    if (i >= m) return;
+    uint64_t key = keys[i], idx = key >> 32;
+    uint32_t mask;
+    uint32_t *wp = bit_word(bits, idx, &mask);
+    if (i > 0) {
+        uint32_t pm;
+        if (bit_word(bits, keys[i - 1] >> 32, &pm) == wp) return; // not the first probe of this word
+    }
+    const uint32_t old = *wp;
+    uint32_t set = 0;
+    uint64_t prev_idx = ~0ull;
+    for (uint64_t u = i; u < m; u++) {
+        uint64_t ku = keys[u], iu = ku >> 32;
+        uint32_t mu;
+        if (bit_word(bits, iu, &mu) != wp) break;
+        if (iu != prev_idx) { // the earliest probe of this bit (stable sort: batch order within a bit)
+            prev_idx = iu;
+            uint32_t pos = uint32_t(ku & 0xffffffffu), e = pos / uint32_t(k), j = pos - e * uint32_t(k);
+            if (!(old & mu) && int(j) <= k - 2) out[e] = 1;
+            set |= mu;
         }
     }
+    if ((old | set) != old) *wp = old | set;
 }
 
 // ------------------------------------------------------------ bit strings

@@ -1709,7 +1709,9 @@ static int bloom_add_device(sk_ctx *c, uint32_t id, int64_t size, int32_t k, uin
                             const uint8_t *d_bytes, uint8_t *d_out) {
     if (!n) return SK_OK;
     HIPCHK(c, hipMemsetAsync(d_out, 0, n, c->st));
-    uint64_t per = std::max<uint64_t>(1, std::min<uint64_t>(c->max_batch / uint64_t(k), 0xffffffffull / uint64_t(k)));
+    // probes per sort: the apply sweeps the touched words of the bit array once per sort, so bigger sorts
+    // amortise it (a C3 filter is ~4.2 M lines); keys are idx << 32 | probe number (< 2^32)
+    uint64_t per = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t(1) << 27) / uint64_t(k), 0xffffffffull / uint64_t(k)));
     unsigned idx_bits = bits_for(uint64_t(size - 1));
     uint64_t magic = magic_for(uint64_t(size));
     for (uint64_t s = 0; s < n; s += per) {

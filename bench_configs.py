@@ -81,9 +81,22 @@ def c2zipf(eng, args):
     t = timed(eng, lambda: [eng.pfadd_dev(B, d_ids.ptr + s * B * 4, off.ptr + s * B * 8, byt, tot, d_out)
                             for s in range(1, steps + 1)])
     top = float(np.bincount(kid[:B]).max()) / B
+    # per-key PFCOUNT of every tenant (C2): the histogram kernel alone, and the whole RHyperLogLog.count path
+    d_all = eng.to_device(ids)
+    d_hist = eng.alloc(nt * 64 * 4)
+    eng.prof_reset(); eng.prof_enable(True)
+    t_h = timed(eng, lambda: eng.hll_histogram_dev(nt, d_all, d_hist), reps=3)
+    eng.prof_enable(False)
+    n_l, ms = eng.prof_read("hll_hist")
+    k_ms = ms / max(n_l, 1)
+    t_c = timed(eng, lambda: eng.pfcount([[nm] for nm in names]))
+    gbs = nt * 16384 / (k_ms * 1e-3) / 1e9
     line({"metric": "C2 Zipf(1.1) PFADD inserts/sec (1M-command batches, 100k tenants)", "value": B * steps / t,
           "unit": "inserts/s", "config": {"workload": "c2zipf", "batch": B, "tenants": nt, "zipf_s": 1.1,
-                                          "hottest_tenant_share": top}})
+                                          "hottest_tenant_share": top},
+          "pfcount_keys_per_s": nt / t_c, "hist_keys_per_s_host_timed": nt / t_h,
+          "roofline": {"kernel": "hll_hist", "bound": "hbm", "achieved": gbs, "peak": PEAK, "unit": "GB/s",
+                       "frac": gbs / PEAK, "bytes_per_unit": 16384, "avg_launch_ms": k_ms}})
 
 
 def c4(eng, args):

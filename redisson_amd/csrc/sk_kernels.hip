@@ -641,34 +641,73 @@ __global__ void __launch_bounds__(SK_PFP_ATPB) k_pfp_apply(const uint64_t *__res
     for (uint32_t u = sub; u < c; u += 4) rs[u] = r0[dst + u];
 }
 
-// -------------------------------------------------------------- histogram
-// One 256-thread workgroup per key: 16 KiB of registers read as 4 x 16 B
-// per lane (coalesced), counted into per-wave LDS histograms.
-__global__ void __launch_bounds__(256) k_hll_hist(const uint32_t *__restrict__ ids, const uint8_t *__restrict__ arena,
-                                                  uint32_t *__restrict__ hist) {
-    __shared__ uint32_t h[4][64];
-    unsigned t = threadIdx.x, w = t >> 6;
-    h[w][t & 63] = 0;
-    __syncthreads();
-    const uint4 *base = reinterpret_cast<const uint4 *>(arena + (uint64_t(ids[blockIdx.x]) << 14));
-#pragma unroll
-    for (int it = 0; it < 4; it++) {
-        uint4 v = base[it * 256 + t];
-        uint32_t ws[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int q = 0; q < 4; q++)
-#pragma unroll
-            for (int b = 0; b < 4; b++) atomicAdd(&h[w][(ws[q] >> (8 * b)) & 63u], 1u);
-    }
-    __syncthreads();
-    if (t < 64) hist[uint64_t(blockIdx.x) * 64 + t] = h[0][t] + h[1][t] + h[2][t] + h[3][t];
-}
-
 // streamed-once 16-B load with the nontemporal hint (native vector type for the builtin)
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ uint4 ld_nt(const uint4 *p) {
     u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p));
     return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+// -------------------------------------------------------------- histogram
+// 64-bin register histogram per key (the input of the PFCOUNT estimator).
+// Most registers of a tenant HLL share a value (0 in a sparse one), so shared
+// bins would serialise LDS atomics.  Zero registers are counted in registers
+// (zero-byte popcount); every other value goes to the lane's own
+// column of a bin-major LDS table (h[bin][lane], u16: at most 2-way bank
+// conflicts whatever the values), then the columns are reduced with a
+// rotated walk and zeroed for the next key.  Workgroups loop over keys; the next key's
+// 16 KiB is loaded while the current one is reduced.
+#define SK_HH_TPB 256
+__global__ void __launch_bounds__(SK_HH_TPB) k_hll_hist(uint64_t n, const uint32_t *__restrict__ ids,
+                                                        const uint8_t *__restrict__ arena,
+                                                        uint32_t *__restrict__ hist) {
+    __shared__ uint16_t h[64][SK_HH_TPB]; // a lane counts <= 64 registers per key
+    __shared__ uint32_t part[SK_HH_TPB / 64][64];
+    const unsigned t = threadIdx.x, bin = t & 63u, q = t >> 6;
+    for (int b = 0; b < 64; b++) h[b][t] = 0;
+    auto load = [&](uint64_t key, uint4 (&v)[4]) {
+        const uint4 *base = reinterpret_cast<const uint4 *>(arena + (uint64_t(ids[key]) << 14));
+#pragma unroll
+        for (int it = 0; it < 4; it++) v[it] = ld_nt(base + it * SK_HH_TPB + t);
+    };
+    uint4 v[4];
+    uint64_t key = blockIdx.x;
+    if (key < n) load(key, v);
+    for (; key < n; key += gridDim.x) {
+        uint32_t zeros = 0; // zero registers (most of a sparse tenant) are counted in registers
+#pragma unroll
+        for (int it = 0; it < 4; it++) {
+            uint32_t ws[4] = {v[it].x, v[it].y, v[it].z, v[it].w};
+#pragma unroll
+            for (int w = 0; w < 4; w++) {
+                uint32_t x = ws[w] & 0x3f3f3f3fu;
+                zeros += __popc(~(((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x | 0x7f7f7f7fu)); // zero bytes
+                if (x == 0) continue;
+#pragma unroll
+                for (int b = 0; b < 4; b++) {
+                    uint32_t r = (x >> (8 * b)) & 63u;
+                    if (r) h[r][t] += uint16_t(1);
+                }
+            }
+        }
+        h[0][t] += uint16_t(zeros);
+        __syncthreads();
+        if (key + gridDim.x < n) load(key + gridDim.x, v); // in flight during the reduce
+        uint32_t sum = 0;
+        for (unsigned i = 0; i < 64; i++) {
+            unsigned lane = q * 64 + ((i + bin) & 63u);
+            sum += h[bin][lane];
+            h[bin][lane] = 0;
+        }
+        part[q][bin] = sum;
+        __syncthreads();
+        if (t < 64) {
+            uint32_t c = 0;
+#pragma unroll
+            for (int qq = 0; qq < SK_HH_TPB / 64; qq++) c += part[qq][t];
+            hist[key * 64 + t] = c;
+        }
+    }
 }
 
 // ------------------------------------------------------------------ union
@@ -1353,7 +1392,7 @@ hipError_t sort_pairs64(hipStream_t st, void *tmp, size_t tmp_bytes, const uint6
 
 hipError_t launch_hll_hist(hipStream_t st, uint64_t n, const uint32_t *ids, const uint8_t *arena, uint32_t *hist) {
     if (!n) return hipSuccess;
-    hipLaunchKernelGGL(k_hll_hist, dim3(unsigned(n)), dim3(256), 0, st, ids, arena, hist);
+    hipLaunchKernelGGL(k_hll_hist, dim3(grid_for(n, 1, 2048)), dim3(SK_HH_TPB), 0, st, n, ids, arena, hist);
     SK_LAUNCH_CHECK();
     return hipSuccess;
 }

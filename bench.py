@@ -234,6 +234,9 @@ def main():
         "kernel_ms_per_launch": over_ms,   # overlapped breakdown pass (same schedule as the timed region)
         "roofline": {"kernel": dom, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     # measured HBM-side bytes (PMC, 128-B lines per random probe) over the same launch time
+                     "traffic_GBps": traffic / (avg_ms * 1e-3) / 1e9 if traffic else None,
+                     "traffic_frac": traffic / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS if traffic else None,
                      "traffic_source": "profiles/*_pmc_summary.json: 2 x FETCH_SIZE (gfx950) + WRITE_SIZE per launch",
                      "bytes_per_unit": per_unit, "units_per_launch": B, "avg_launch_ms": avg_ms,
                      "note": "avg launch of the dominant kernel, HIP events on its stream inside the timed region "

@@ -216,23 +216,35 @@ struct Server {
         std::vector<size_t> which;
         for (size_t i = a; i < b; i++) {
             auto &c = cmds[i];
-            int t = type_of(c[1]);
-            if (t == T_HASH) r_error(rep[i], kWrongType);
-            else if (t == T_STR) r_error(rep[i], kNotHll);
-            else {
-                keys.add(c[1]);
-                counts.push_back(uint32_t(c.size() - 2));
-                for (size_t e = 2; e < c.size(); e++) elems.add(c[e]);
-                which.push_back(i);
+            if (!hashes.empty() && hashes.count(c[1])) {
+                r_error(rep[i], kWrongType);
+                continue;
             }
+            keys.add(c[1]);
+            counts.push_back(uint32_t(c.size() - 2));
+            for (size_t e = 2; e < c.size(); e++) elems.add(c[e]);
+            which.push_back(i);
         }
         if (which.empty()) return;
         std::vector<uint8_t> out(which.size());
         int st = sk_pfadd(ctx, uint32_t(which.size()), keys.off.data(), keys.data(), counts.data(), elems.off.data(),
                           elems.data(), out.data());
+        // the engine applies every command on an HLL key (or a valid HLL string, adopted) and
+        // skips the rest with a status: key types are looked up only then, to answer those alone
         for (size_t j = 0; j < which.size(); j++) {
-            if (st != SK_OK) r_error(rep[which[j]], engine_error());
-            else r_int(rep[which[j]], out[j]);
+            auto &c = cmds[which[j]];
+            if (st == SK_OK) r_int(rep[which[j]], out[j]);
+            else if (st != SK_EWRONGTYPE && st != SK_ECORRUPT) r_error(rep[which[j]], engine_error());
+            else if (type_of(c[1]) == T_HLL) r_int(rep[which[j]], out[j]);
+            else { // that command alone again, for its own error (a failed adoption changes nothing)
+                Packed k1, e1;
+                k1.add(c[1]);
+                uint32_t cnt = uint32_t(c.size() - 2);
+                for (size_t e = 2; e < c.size(); e++) e1.add(c[e]);
+                uint8_t o1;
+                sk_pfadd(ctx, 1, k1.off.data(), k1.data(), &cnt, e1.off.data(), e1.data(), &o1);
+                r_error(rep[which[j]], engine_error());
+            }
         }
     }
     // GETBIT key offset / SETBIT key offset value: one sk_getbit / sk_setbit over the run
@@ -254,8 +266,7 @@ struct Server {
                 r_error(rep[i], kBitValue);
                 continue;
             }
-            int t = type_of(c[1]);
-            if (t == T_HASH || t == T_HLL) {
+            if (!hashes.empty() && hashes.count(c[1])) {
                 r_error(rep[i], kWrongType);
                 continue;
             }
@@ -269,8 +280,11 @@ struct Server {
         int st = set ? sk_setbit(ctx, uint32_t(which.size()), keys.off.data(), keys.data(), offs.data(), vals.data(),
                                  out.data())
                      : sk_getbit(ctx, uint32_t(which.size()), keys.off.data(), keys.data(), offs.data(), out.data());
+        // commands on HLL keys are skipped by the engine with SK_EWRONGTYPE (offsets were checked above)
         for (size_t j = 0; j < which.size(); j++) {
-            if (st != SK_OK) r_error(rep[which[j]], engine_error());
+            if (st == SK_OK) r_int(rep[which[j]], out[j]);
+            else if (st != SK_EWRONGTYPE) r_error(rep[which[j]], engine_error());
+            else if (type_of(cmds[which[j]][1]) == T_HLL) r_error(rep[which[j]], kWrongType);
             else r_int(rep[which[j]], out[j]);
         }
     }

@@ -1007,7 +1007,7 @@ int sk_pfadd(sk_ctx *c, uint32_t n_cmds, const uint64_t *key_off, const uint8_t 
     for (uint32_t i = 0; i < n_cmds; i++) {
         bool cr;
         int r = hll_get(c, key_at(key_off, key_bytes, i), true, &cmd_key[i], &cr);
-        if (r == SK_EWRONGTYPE) {
+        if (r == SK_EWRONGTYPE || r == SK_ECORRUPT) { // that command alone fails, as in a pipeline
             valid[i] = 0;
             status = r;
             continue;
@@ -1071,9 +1071,12 @@ int sk_pfadd(sk_ctx *c, uint32_t n_cmds, const uint64_t *key_off, const uint8_t 
             HIPCHK(c, hipMemcpyAsync(c->in_off.p, off2.data(), (m + 1) * 8, hipMemcpyHostToDevice, c->st));
             HIPCHK(c, hipMemcpyAsync(c->in_bytes.p, bytes2.data(), bytes2.size(), hipMemcpyHostToDevice, c->st));
             HIPCHK(c, hipMemsetAsync(c->out_u8.p, 0, c1 - c0, c->st));
-            std::vector<uint32_t> uniq(h_ids);
-            std::sort(uniq.begin(), uniq.end());
-            uint64_t touched = uint64_t(std::unique(uniq.begin(), uniq.end()) - uniq.begin());
+            uint64_t touched = 0; // distinct sketches: only the density heuristic of the non-default paths uses it
+            if (c->pfadd_path != 1) {
+                std::vector<uint32_t> uniq(h_ids);
+                std::sort(uniq.begin(), uniq.end());
+                touched = uint64_t(std::unique(uniq.begin(), uniq.end()) - uniq.begin());
+            }
             int r = pfadd_device(c, m, c->in_ids.as<uint32_t>(), c->in_off.as<uint64_t>(), c->in_bytes.as<uint8_t>(),
                                  c->in_cmd.as<uint32_t>(), c1 - c0, c->out_u8.as<uint8_t>(), touched);
             if (r) return r;

@@ -201,6 +201,10 @@ def main():
     iso_dom_ms = iso_ms["bloom_contains"]
     iso_achieved = per_unit_of("bloom_contains", mean_len_h, mean_len_b, k) * B / (iso_dom_ms * 1e-3) / 1e9
     traffic = pmc_traffic(dom)
+    iso_traffic = pmc_traffic("bloom_contains")
+    # measured HBM-side bytes of every kernel of a step (PMC summary) over the step's wall time
+    step_tr = [pmc_traffic(p) for p in over_ms]
+    step_traffic = sum(step_tr) if step_tr and all(t is not None for t in step_tr) else None
     step_bytes = B * (per_unit_of("bloom_contains", mean_len_h, mean_len_b, k) + (mean_len_h + 12 + 2.5))
 
     cpu = None
@@ -243,8 +247,11 @@ def main():
                              "(PFADD and Bloom contains overlap on two streams)"},
         "roofline_isolated": {"kernel": "bloom_contains", "achieved": iso_achieved, "peak": HBM_PEAK_GBS,
                               "unit": "GB/s", "frac": iso_achieved / HBM_PEAK_GBS, "avg_launch_ms": iso_dom_ms,
+                              "traffic_GBps": iso_traffic / (iso_dom_ms * 1e-3) / 1e9 if iso_traffic else None,
                               "kernel_ms_per_launch": iso_ms},
         "step_algorithmic_GBps": step_bytes * K * world / wall / 1e9,
+        "step_traffic_bytes": step_traffic,
+        "step_traffic_GBps": step_traffic * K * world / wall / 1e9 if step_traffic else None,
         "cpu_baseline": cpu,
     }
     if rank == 0:

@@ -813,9 +813,13 @@ int sk_open(const sk_config *cfg, sk_ctx **out) {
         if (cfg->max_bit_offset) c->max_bit_offset = cfg->max_bit_offset;
         if (cfg->max_batch) c->max_batch = cfg->max_batch;
     }
+    // stream priorities (SK_STREAM_PRIO): 0 both normal, 1 main (write) stream high, 2 read stream high
+    int prio_mode = 0, lo = 0, hi = 0;
+    if (const char *e = getenv("SK_STREAM_PRIO")) prio_mode = atoi(e);
     if (c->device < 0 || c->device >= ndev || hipSetDevice(c->device) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->st2, hipStreamNonBlocking) != hipSuccess ||
+        hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess ||
+        hipStreamCreateWithPriority(&c->st, hipStreamNonBlocking, prio_mode == 1 ? hi : lo) != hipSuccess ||
+        hipStreamCreateWithPriority(&c->st2, hipStreamNonBlocking, prio_mode == 2 ? hi : lo) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_w, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_r, hipEventDisableTiming) != hipSuccess) {
         delete c;

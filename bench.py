@@ -97,7 +97,7 @@ def main():
     ids = eng.hll_resolve(mine)
     rng = np.random.default_rng(0x5EED0002 + rank)
 
-    nsteps = W + K + 2 * PROF_STEPS   # warmup, overlapped breakdown, timed, isolated breakdown: fresh inputs each
+    nsteps = W + K + 2 * PROF_STEPS   # warmup, isolated breakdown, overlapped breakdown, timed: fresh inputs each
     seed_h = 0x5EED0002
     base_h = rank << 40                      # disjoint element streams per rank
     h_off, h_bytes, h_total = eng.gen_jackson_longs_dev(seed_h, nsteps * B, first=base_h)
@@ -158,14 +158,18 @@ def main():
         r = {p: eng.prof_read(p) for p in PHASES}
         return {p: r[p][1] / r[p][0] for p in PHASES if r[p][0]}
 
+    # each kernel alone (sync mode: PFADD and contains do not overlap): the dominant
+    # kernel is the one with the most device time of its own (overlapped launch times
+    # mostly measure contention, and PFADD's apply and contains run neck and neck there)
+    iso_ms = profiled(W, False)
+    dom = max([p for p in iso_ms if p != "pfadd_sort"], key=lambda p: iso_ms[p])
     # breakdown as in the timed region (PFADD on the main stream, contains on the
-    # read stream, no host sync): picks the kernel with the most device time
-    over_ms = profiled(W, True)
-    dom = max([p for p in over_ms if p != "pfadd_sort"], key=lambda p: over_ms[p])
+    # read stream, no host sync)
+    over_ms = profiled(W + P, True)
 
     # ------------------------------------------------------------ timed region
     # async: PFADD batches never wait on the host; only `dom` is event-timed
-    T0 = W + P
+    T0 = W + 2 * P
     eng.set_async(True)
     eng.prof_only(dom)
     eng.prof_reset()
@@ -194,14 +198,24 @@ def main():
     avg_ms = tot_ms / max(n_launch, 1)
     achieved = per_unit * B / (avg_ms * 1e-3) / 1e9
 
-    # the same kernels measured alone (sync mode: no overlap between PFADD and contains)
-    iso_ms = profiled(T0 + K, False)
     hll_ms = sum(v for p, v in iso_ms.items() if p in HLL_PHASES)
     bl_ms = iso_ms["bloom_contains"]
-    iso_dom_ms = iso_ms["bloom_contains"]
-    iso_achieved = per_unit_of("bloom_contains", mean_len_h, mean_len_b, k) * B / (iso_dom_ms * 1e-3) / 1e9
+    iso_dom_ms = iso_ms[dom]
+    iso_achieved = per_unit_of(dom, mean_len_h, mean_len_b, k) * B / (iso_dom_ms * 1e-3) / 1e9
     traffic = pmc_traffic(dom)
-    iso_traffic = pmc_traffic("bloom_contains")
+    iso_traffic = traffic
+    # every kernel of the step: algorithmic GB/s alone and in the overlapped schedule
+    kernels = {}
+    for p_, ms in iso_ms.items():
+        if p_ == "pfadd_sort":
+            continue
+        pu = per_unit_of(p_, mean_len_h, mean_len_b, k)
+        tr = pmc_traffic(p_)
+        kernels[p_] = {"bytes_per_unit": pu, "ms_isolated": ms, "GBps_isolated": pu * B / (ms * 1e-3) / 1e9,
+                       "ms_overlapped": over_ms.get(p_),
+                       "GBps_overlapped": pu * B / (over_ms[p_] * 1e-3) / 1e9 if over_ms.get(p_) else None,
+                       "pmc_traffic_bytes": tr,
+                       "pmc_GBps_isolated": tr / (ms * 1e-3) / 1e9 if tr else None}
     # measured HBM-side bytes of every kernel of a step (PMC summary) over the step's wall time
     step_tr = [pmc_traffic(p) for p in over_ms]
     step_traffic = sum(step_tr) if step_tr and all(t is not None for t in step_tr) else None
@@ -209,7 +223,7 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(eng, args, h_off, h_bytes, ids, kid, len(mine), c_off, c_bytes, bloom, size, k)
+        cpu = cpu_baseline(eng, args, h_off, h_bytes, ids, kid, len(mine), c_off, c_bytes, bloom, size, k, nsteps * B)
 
     out = {
         "metric": "HLL inserts/sec + Bloom contains/sec (whole node)",
@@ -245,7 +259,8 @@ def main():
                      "bytes_per_unit": per_unit, "units_per_launch": B, "avg_launch_ms": avg_ms,
                      "note": "avg launch of the dominant kernel, HIP events on its stream inside the timed region "
                              "(PFADD and Bloom contains overlap on two streams)"},
-        "roofline_isolated": {"kernel": "bloom_contains", "achieved": iso_achieved, "peak": HBM_PEAK_GBS,
+        "kernels": kernels,
+        "roofline_isolated": {"kernel": dom, "achieved": iso_achieved, "peak": HBM_PEAK_GBS,
                               "unit": "GB/s", "frac": iso_achieved / HBM_PEAK_GBS, "avg_launch_ms": iso_dom_ms,
                               "traffic_GBps": iso_traffic / (iso_dom_ms * 1e-3) / 1e9 if iso_traffic else None,
                               "kernel_ms_per_launch": iso_ms},
@@ -262,7 +277,7 @@ def main():
 def per_unit_of(phase, mean_len_h, mean_len_b, k):
     """Algorithmic bytes per unit (SURVEY 8d / DESIGN.md kernel table)."""
     return {
-        "pfp_hash": mean_len_h + 8 + 4 + 8 + 2,        # key bytes + offset + slab id in, record + chunk slot out
+        "pfp_hash": mean_len_h + 8 + 4 + 8,            # key bytes + offset + slab id in, record out
         "pfp_apply": 8 + 64 + 64 + 1,                  # record + register sector load (R0) + store + reply
         "pfp_reply": 1 + 2 + 1,                        # chunk-order reply + chunk slot in, reply out
         "pfadd_claim": mean_len_h + 8 + 4 + 1 + 8,     # key bytes + offset + slab id + register in, record out
@@ -291,16 +306,25 @@ def pmc_traffic(phase):
         return None
 
 
-def cpu_baseline(eng, args, h_off, h_bytes, ids, kid, n_keys, c_off, c_bytes, bloom, size, k):
-    """The oracle (CPU restatement, one core) on a bounded sample of the same workload."""
+def cpu_baseline(eng, args, h_off, h_bytes, ids, kid, n_keys, c_off, c_bytes, bloom, size, k, n_avail):
+    """The oracle (CPU restatement) on bounded samples of the same workload: one core, and the whole host's
+    CPU share (threads owning keys id % T, like one redis-server per core with client-side routing)."""
     from oracle import oracle as O
 
-    S = args.cpu_sample
+    T = int(os.environ.get("OMP_NUM_THREADS") or 0) or min(16, os.cpu_count() or 1)
+    S1 = min(args.cpu_sample, n_avail)
+    ST = min(args.cpu_sample * max(T // 2, 1), n_avail, 1 << 24)
+    S = max(S1, ST)
     off = h_off.download(np.uint64, S + 1)
     buf = h_bytes.download(np.uint8, int(off[S]) + 16)
+    ko = kid[:S].astype(np.uint32)
     t0 = time.perf_counter()
-    O.HLLStore().pfadd_bulk(kid[:S].astype(np.uint32), off, buf, n_keys)
-    th = time.perf_counter() - t0
+    _, r1 = O.HLLStore().pfadd_bulk(ko[:S1], off[:S1 + 1], buf, n_keys)
+    th1 = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    _, rT = O.HLLStore().pfadd_bulk_mt(ko[:ST], off[:ST + 1], buf, n_keys, T)
+    thT = time.perf_counter() - t0
+    assert np.array_equal(r1[:min(S1, ST)], rT[:min(S1, ST)]), "threaded oracle PFADD differs"
 
     bits = O.BitString(0)
     full = eng.get(bloom) or b""
@@ -309,12 +333,20 @@ def cpu_baseline(eng, args, h_off, h_bytes, ids, kid, n_keys, c_off, c_bytes, bl
     coff = c_off.download(np.uint64, S + 1)
     cbuf = c_bytes.download(np.uint8, int(coff[S]) + 16)
     t0 = time.perf_counter()
-    bits.bloom_contains_raw(size, k, coff, cbuf)
-    tb = time.perf_counter() - t0
-    return {"value": 2 * S / (th + tb), "unit": "ops/s", "cores": 1, "kind": "port",
+    c1 = bits.bloom_contains_raw(size, k, coff[:S1 + 1], cbuf)
+    tb1 = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    cT = bits.bloom_contains_raw_mt(size, k, coff[:ST + 1], cbuf, T)
+    tbT = time.perf_counter() - t0
+    assert np.array_equal(c1[:min(S1, ST)], cT[:min(S1, ST)]), "threaded oracle contains differs"
+    return {"value": 2 * ST / (thT + tbT), "unit": "ops/s", "cores": T,
+            "kind": "port",
             "sample": "%d PFADD (same tenants/elements) + %d Bloom contains on the same filled filter, "
-                      "oracle/sketch_oracle.c single-threaded" % (S, S),
-            "hll_inserts_per_s": S / th, "bloom_contains_per_s": S / tb}
+                      "oracle/sketch_oracle.c on %d host threads (oracle_mt.c: a thread owns the keys id %% %d, "
+                      "contains split in ranges)" % (ST, ST, T, T),
+            "hll_inserts_per_s": ST / thT, "bloom_contains_per_s": ST / tbT,
+            "single_core": {"value": 2 * S1 / (th1 + tb1), "cores": 1, "sample": "%d PFADD + %d contains" % (S1, S1),
+                            "hll_inserts_per_s": S1 / th1, "bloom_contains_per_s": S1 / tb1}}
 
 
 if __name__ == "__main__":

@@ -54,6 +54,10 @@ def lib():
                                           c_void_p]),
             "or_bloom_contains_batch": (None, [c_void_p, c_uint64, c_int64, c_int32, c_uint32, c_void_p, c_void_p,
                                                c_void_p]),
+            "or_pfadd_owned_mt": (None, [c_void_p, c_void_p, c_uint32, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
+                                         c_int]),
+            "or_bloom_contains_mt": (None, [c_void_p, c_uint64, c_int64, c_int32, c_uint32, c_void_p, c_void_p,
+                                            c_void_p, c_int]),
             "or_getbit": (c_int, [c_void_p, c_uint64, c_uint64]),
             "or_setbit": (c_int, [c_void_p, c_void_p, c_uint64, c_int]),
             "or_bitcount": (c_uint64, [c_void_p, c_uint64]),
@@ -140,6 +144,17 @@ class HLLStore:
         ids = np.ascontiguousarray(key_ids, dtype=np.uint32)
         lib().or_pfadd_batch(regs.ctypes.data, exists.ctypes.data, n, ids.ctypes.data, counts.ctypes.data,
                              off.ctypes.data, buf.ctypes.data, self.m, out.ctypes.data)
+        return regs, out
+
+    def pfadd_bulk_mt(self, key_ids: np.ndarray, off: np.ndarray, buf: np.ndarray, n_keys: int, threads: int):
+        """pfadd_bulk on `threads` host threads, each owning the keys id % threads (oracle_mt.c)."""
+        regs = np.zeros((n_keys, 16384), dtype=np.uint8)
+        exists = np.zeros(n_keys, dtype=np.uint8)
+        n = len(key_ids)
+        out = np.zeros(n, dtype=np.uint8)
+        ids = np.ascontiguousarray(key_ids, dtype=np.uint32)
+        lib().or_pfadd_owned_mt(regs.ctypes.data, exists.ctypes.data, n, ids.ctypes.data, off.ctypes.data,
+                                buf.ctypes.data, self.m, out.ctypes.data, threads)
         return regs, out
 
     def count(self, keys):
@@ -307,6 +322,13 @@ class BitString:
         out = np.zeros(n, dtype=np.uint8)
         lib().or_bloom_contains_batch(self.buf.ctypes.data, self.len.value, size, k, n,
                                       off.ctypes.data, buf.ctypes.data, out.ctypes.data)
+        return out
+
+    def bloom_contains_raw_mt(self, size, k, off, buf, threads):
+        n = len(off) - 1
+        out = np.zeros(n, dtype=np.uint8)
+        lib().or_bloom_contains_mt(self.buf.ctypes.data, self.len.value, size, k, n, off.ctypes.data,
+                                   buf.ctypes.data, out.ctypes.data, threads)
         return out
 
     def bloom_add_raw(self, size, k, off, buf):

@@ -29,7 +29,8 @@ hipError_t launch_pfp_hash(hipStream_t st, uint64_t n, const uint32_t *key_ids, 
                            const uint8_t *bytes, int v5, uint64_t *chunks, uint32_t *S, uint16_t *pos,
                            uint32_t *big_alloc);
 hipError_t launch_pfp_apply(hipStream_t st, uint64_t n, const uint64_t *chunks, const uint32_t *S, uint8_t *arena,
-                            uint8_t *rep, uint32_t *big_alloc, uint64_t *big_keys, uint32_t *big_vals);
+                            uint8_t *rep, uint32_t *big_alloc, uint64_t *big_keys, uint32_t *big_vals,
+                            uint8_t *changed); // changed != null: replies straight to batch order (no k_pfp_reply)
 hipError_t launch_pfp_reply(hipStream_t st, uint64_t n, const uint8_t *rep, const uint16_t *pos,
                             const uint32_t *cmd_of, uint8_t *changed);
 hipError_t sort_keys_size(uint64_t n, unsigned begin_bit, unsigned end_bit, size_t *bytes);

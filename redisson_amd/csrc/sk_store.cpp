@@ -221,6 +221,7 @@ struct sk_ctx {
 
     bool async_dev = false;     // sk_set_async: _dev calls return without a final sync
     int pfadd_path = 1;         // 0 claim/commit, 1 partition, 2 sorted (SK_PFADD_PATH); dense batches use 2
+    bool pfp_direct = true;     // partition path, one element per command: apply writes replies (SK_PFP_DIRECT)
     int claim_all = 1;          // PFADD claim: 1 = every element claims (R0 from the atomic), 0 = load first, claim candidates (SK_PFADD_CLAIM)
     int read_stream = 1;        // async Bloom contains on the read stream st2 (SK_READ_STREAM=0: main stream)
     int bloom_sched = 0;        // contains kernel (SK_BLOOM_SCHED): 0 one element per thread; 1 probe queue, 4/lane
@@ -681,13 +682,19 @@ int pfadd_partition(sk_ctx *c, uint64_t n, const uint32_t *d_ids, const uint64_t
     uint8_t *rep = c->keys_b.as<uint8_t>();
     uint16_t *pos = reinterpret_cast<uint16_t *>(rep + ((cap + 15) & ~uint64_t(15)));
     uint32_t *S = c->hist_a.as<uint32_t>(), *big_alloc = c->ovf.as<uint32_t>();
+    // one element per command: k_pfp_apply stores each reply at its batch position (a 1 MB reply array stays
+    // in L2, so the scattered byte stores cost no HBM requests) and the order-restoring launch is skipped
+    const bool direct = d_cmd == nullptr && c->pfp_direct;
     { Prof p_(c, 15);
-    HIPCHK(c, sk::launch_pfp_hash(c->st, n, d_ids, d_off, d_bytes, c->redis_major >= 5, chunks, S, pos, big_alloc)); }
+    HIPCHK(c, sk::launch_pfp_hash(c->st, n, d_ids, d_off, d_bytes, c->redis_major >= 5, chunks, S,
+                                  direct ? nullptr : pos, big_alloc)); }
     { Prof p_(c, 16);
     HIPCHK(c, sk::launch_pfp_apply(c->st, n, chunks, S, c->arena, rep, big_alloc, c->vals_a.as<uint64_t>(),
-                                   c->vals_b.as<uint32_t>())); }
-    { Prof p_(c, 17);
-    HIPCHK(c, sk::launch_pfp_reply(c->st, n, rep, pos, d_cmd, d_changed)); }
+                                   c->vals_b.as<uint32_t>(), direct ? d_changed : nullptr)); }
+    if (!direct) {
+        Prof p_(c, 17);
+        HIPCHK(c, sk::launch_pfp_reply(c->st, n, rep, pos, d_cmd, d_changed));
+    }
     return SK_OK;
 }
 
@@ -829,6 +836,7 @@ int sk_open(const sk_config *cfg, sk_ctx **out) {
     if (const char *e = getenv("SK_READ_STREAM")) c->read_stream = atoi(e);
     if (const char *e = getenv("SK_PFADD_CLAIM")) c->claim_all = atoi(e);
     if (const char *e = getenv("SK_PFADD_PATH")) c->pfadd_path = atoi(e);
+    if (const char *e = getenv("SK_PFP_DIRECT")) c->pfp_direct = atoi(e) != 0;
     uint64_t cap = (cfg && cfg->hll_capacity) ? cfg->hll_capacity : 1024;
     if (hll_grow(c, cap) != SK_OK || c->misc.ensure(4096) != hipSuccess ||
         hipMalloc(&c->d_zero, 16) != hipSuccess || hipMemsetAsync(c->d_zero, 0, 16, c->st) != hipSuccess ||

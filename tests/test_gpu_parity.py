@@ -332,18 +332,22 @@ def test_edge_cases(engine, O):
     assert engine.get(b"edge:none") is None
 
 
-@pytest.mark.parametrize("path,claim", [("0", "0"), ("0", "1"), ("1", "1"), ("2", "1")])
-def test_pfadd_paths_agree(O, path, claim):
-    """Every PFADD path (claim/commit with either claim form, partition, sorted)
-    gives the oracle's registers and replies, dense and sparse, with
-    intra-batch collisions and an oversized partition bucket."""
+@pytest.mark.parametrize("path,claim,direct", [("0", "0", "1"), ("0", "1", "1"), ("1", "1", "1"), ("1", "1", "0"),
+                                               ("2", "1", "1")])
+def test_pfadd_paths_agree(O, path, claim, direct):
+    """Every PFADD path (claim/commit with either claim form, partition with
+    replies stored by k_pfp_apply or restored by k_pfp_reply, sorted) gives the
+    oracle's registers and replies, dense and sparse, with intra-batch
+    collisions and an oversized partition bucket."""
     import os
     from redisson_amd import SketchEngine
-    os.environ["SK_PFADD_PATH"], os.environ["SK_PFADD_CLAIM"] = path, claim
+    env = {"SK_PFADD_PATH": path, "SK_PFADD_CLAIM": claim, "SK_PFP_DIRECT": direct}
+    os.environ.update(env)
     try:
         e = SketchEngine(device=0)
     finally:
-        del os.environ["SK_PFADD_PATH"], os.environ["SK_PFADD_CLAIM"]
+        for v in env:
+            del os.environ[v]
     try:
         for nkeys, n, dup in [(300, 40000, 0.2), (3, 60000, 0.1), (1, 3000, 0.0)]:
             rng = np.random.default_rng(nkeys)

@@ -130,3 +130,23 @@ def test_hll_string_codec_round_trip(O):
     one = np.zeros(16384, dtype=np.uint8)
     one[0] = 3
     assert O.hll_string(one, "sparse")[16:] == bytes([0x88, 0x7F, 0xFE])  # VAL(3,1) XZERO(16383)
+
+
+def test_threaded_baseline_matches_oracle(O):
+    """bench.py's whole-host CPU baseline (oracle_mt.c) gives the single-threaded oracle's registers and replies."""
+    from redisson_amd import gen_jackson_longs
+
+    n, nkeys = 60000, 97
+    off, buf = gen_jackson_longs(0x5EED0777, n)
+    off = np.ascontiguousarray(off, dtype=np.uint64)
+    buf = np.concatenate([np.asarray(buf, dtype=np.uint8), np.zeros(16, np.uint8)])
+    kid = np.random.default_rng(5).integers(0, nkeys, n).astype(np.uint32)
+    regs1, r1 = O.HLLStore().pfadd_bulk(kid, off, buf, nkeys)
+    regs4, r4 = O.HLLStore().pfadd_bulk_mt(kid, off, buf, nkeys, 4)
+    assert np.array_equal(regs1, regs4) and np.array_equal(r1, r4)
+    bits = O.BitString()
+    size, k = 200000, 5
+    bits.bloom_add_raw(size, k, off[:20001], buf)
+    c1 = bits.bloom_contains_raw(size, k, off, buf)
+    c3 = bits.bloom_contains_raw_mt(size, k, off, buf, 3)
+    assert np.array_equal(c1, c3) and c1[:20000].all() and not c1[20000:].all()

@@ -1,8 +1,8 @@
 """Timeline of the bench's timed region from a rocprofv3 kernel trace (dev tool).
 
 usage: python tools/timeline.py TRACE.csv FIRST_STEP N_STEPS
-Step s is the s-th pfp_hash / bloom_contains launch of the run (bench order: W warmup, P breakdown, K timed,
-P isolated).  Prints each stream's busy time, idle gaps, and when each stream finishes."""
+Step s is the s-th pfp_hash / bloom_contains launch of the run (bench order: W warmup, P isolated, P breakdown,
+K timed).  Prints each stream's busy time, idle gaps, and when each stream finishes."""
 import csv
 import sys
 
@@ -16,7 +16,7 @@ def main(path, first, n):
     for v in ks.values():
         v.sort()
     pf = []
-    for nm in ("k_pfp_hash", "k_pfp_apply", "k_pfp_reply"):
+    for nm in ("k_pfp_hash", "k_pfp_apply", "k_pfp_reply"):  # k_pfp_reply: multi-element commands only
         pf += ks.get(nm, [])[first:first + n]
     bc = ks.get("k_bloom_contains", [])[first:first + n]
     pf.sort()

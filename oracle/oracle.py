@@ -58,6 +58,14 @@ def lib():
                                          c_int]),
             "or_bloom_contains_mt": (None, [c_void_p, c_uint64, c_int64, c_int32, c_uint32, c_void_p, c_void_p,
                                             c_void_p, c_int]),
+            "or_gen_jackson_long": (c_uint32, [c_uint64, c_uint64, c_void_p]),
+            "or_pfadd_gen_mt": (c_uint64, [c_void_p, c_void_p, c_uint64, c_void_p, c_uint64, c_uint64, c_int,
+                                           c_void_p, c_int]),
+            "or_hll_union_gen_mt": (None, [c_void_p, c_uint64, c_uint64, c_uint64, c_int, c_int]),
+            "or_bloom_add_gen_mt": (c_uint64, [c_void_p, c_int64, c_int32, c_uint64, c_uint64, c_uint64, c_int]),
+            "or_bloom_contains_gen_mt": (None, [c_void_p, c_uint64, c_int64, c_int32, c_uint64, c_void_p, c_uint64,
+                                                c_void_p, c_int]),
+            "or_setbits_mt": (None, [c_void_p, c_void_p, c_uint64, c_int]),
             "or_getbit": (c_int, [c_void_p, c_uint64, c_uint64]),
             "or_setbit": (c_int, [c_void_p, c_void_p, c_uint64, c_int]),
             "or_bitcount": (c_uint64, [c_void_p, c_uint64]),
@@ -349,3 +357,54 @@ def bitop(op: str, srcs):
     dst = np.zeros(int(lens.max()) + 1 if len(lens) else 1, dtype=np.uint8)
     n = lib().or_bitop(code, dst.ctypes.data, ptrs, lens.ctypes.data, len(arrs))
     return dst[:n].tobytes()
+
+
+# ---------------------------------------------------------------- full-size checkers (oracle_mt.c)
+def threads() -> int:
+    """Host threads for the threaded checkers: the box's CPU share (OMP_NUM_THREADS), else up to 16."""
+    import os
+    return int(os.environ.get("OMP_NUM_THREADS") or 0) or min(16, os.cpu_count() or 1)
+
+
+def gen_jackson_long(seed: int, i: int) -> bytes:
+    """Element i of the synthetic stream `seed`: SplitMix64 -> Jackson ["java.lang.Long",v] bytes."""
+    b = ctypes.create_string_buffer(48)
+    n = lib().or_gen_jackson_long(seed, i, b)
+    return b.raw[:n]
+
+
+def pfadd_gen(regs: np.ndarray, exists: np.ndarray, key_ids: np.ndarray, seed: int, first: int,
+              redis_major: int = 3):
+    """PFADD element first+c of stream `seed` into key key_ids[c], in order per key (threads own keys).
+    regs: (n_keys, 16384) u8, exists: n_keys u8, both updated; returns (replies u8[n], number of 1s)."""
+    ids = np.ascontiguousarray(key_ids, dtype=np.uint32)
+    out = np.zeros(len(ids), dtype=np.uint8)
+    ones = lib().or_pfadd_gen_mt(regs.ctypes.data, exists.ctypes.data, len(ids), ids.ctypes.data, seed, first,
+                                 redis_major, out.ctypes.data, threads())
+    return out, int(ones)
+
+
+def hll_union_gen(n: int, seed: int, first: int = 0, redis_major: int = 3) -> np.ndarray:
+    regs = np.zeros(16384, dtype=np.uint8)
+    lib().or_hll_union_gen_mt(regs.ctypes.data, n, seed, first, redis_major, threads())
+    return regs
+
+
+def bloom_add_gen(size: int, k: int, seed: int, first: int, n: int):
+    """(bit array u8[(size+7)/8], Redis string length) after adding elements first..first+n-1."""
+    bits = np.zeros((size + 7) // 8 + 16, dtype=np.uint8)
+    ln = lib().or_bloom_add_gen_mt(bits.ctypes.data, size, k, seed, first, n, threads())
+    return bits, int(ln)
+
+
+def bloom_contains_gen(bits: np.ndarray, strlen: int, size: int, k: int, seed: int, idx: np.ndarray) -> np.ndarray:
+    ix = np.ascontiguousarray(idx, dtype=np.uint64)
+    out = np.zeros(len(ix), dtype=np.uint8)
+    lib().or_bloom_contains_gen_mt(bits.ctypes.data, strlen, size, k, seed, ix.ctypes.data, len(ix),
+                                   out.ctypes.data, threads())
+    return out
+
+
+def setbits(buf: np.ndarray, offsets: np.ndarray):
+    o = np.ascontiguousarray(offsets, dtype=np.uint64)
+    lib().or_setbits_mt(buf.ctypes.data, o.ctypes.data, len(o), threads())

@@ -10,7 +10,15 @@
  * order (or_pfadd_batch semantics, sketch_oracle.c), so registers and replies
  * equal the single-threaded oracle's.  Bloom contains only reads the bit
  * array: the batch is split into T contiguous ranges.
+ *
+ * The *_gen_mt functions are the full-size checkers of tests/test_full_size.py:
+ * they generate each element themselves (or_gen_jackson_long, the same
+ * SplitMix64 -> Jackson Long byte stream the engine's generator produces), so a
+ * 10^8-element check needs no element buffer on the host.  The state they build
+ * is order-free (register max, bit OR) or per-owner ordered (PFADD replies).
  */
+#include <stdio.h>
+#include <string.h>
 #include <pthread.h>
 #include <stdint.h>
 
@@ -100,4 +108,206 @@ void or_bloom_contains_mt(const uint8_t *buf, uint64_t strlen_bytes, int64_t siz
     a.bytes = elem_bytes;
     a.out = out;
     run(nthreads, &a, contains_range);
+}
+
+
+/* ------------------------------------------------------------------ */
+/* synthetic elements: element i of stream `seed` is
+ *   v = SplitMix64 output i = mix(seed + (i + 1) * 0x9E3779B97F4A7C15)
+ * rendered as Jackson's default-typed Long ["java.lang.Long",v]
+ * (M:codec/JsonJacksonCodec.java:103-106; SURVEY 8d synthetic inputs).    */
+uint32_t or_gen_jackson_long(uint64_t seed, uint64_t i, uint8_t *out) {
+    uint64_t z = seed + (i + 1) * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    static const char pre[] = "[\"java.lang.Long\",";
+    memcpy(out, pre, 18);
+    int nl = snprintf((char *)out + 18, 24, "%lld", (long long)(int64_t)z);
+    out[18 + nl] = ']';
+    return (uint32_t)(18 + nl + 1);
+}
+
+typedef struct {
+    int t, T;
+    uint64_t n, seed, first;
+    const uint64_t *idx;
+    const uint32_t *key_ids;
+    uint8_t *regs, *exists, *out;
+    int redis_major;
+    int64_t size;
+    int32_t k;
+    uint64_t strlen_bytes, maxbyte;
+    uint64_t ones;
+} gen_arg;
+
+static void run_gen(int T, gen_arg *base, gen_arg *args, void *(*fn)(void *)) {
+    pthread_t th[256];
+    for (int t = 0; t < T; t++) {
+        args[t] = *base;
+        args[t].t = t;
+        args[t].T = T;
+        pthread_create(&th[t], NULL, fn, &args[t]);
+    }
+    for (int t = 0; t < T; t++) pthread_join(th[t], NULL);
+}
+static int clampT(int T) { return T < 1 ? 1 : (T > 256 ? 256 : T); }
+
+static void *pfadd_gen(void *p) {
+    gen_arg *a = (gen_arg *)p;
+    uint8_t e[48];
+    for (uint64_t c = 0; c < a->n; c++) {
+        uint32_t key = a->key_ids[c];
+        if ((int)(key % (uint32_t)a->T) != a->t) continue;
+        uint32_t len = or_gen_jackson_long(a->seed, a->first + c, e);
+        int updated = 0;
+        if (!a->exists[key]) {
+            a->exists[key] = 1;
+            updated = 1;
+        }
+        if (or_hll_add(a->regs + (uint64_t)key * OR_HLL_REGISTERS, e, len, a->redis_major)) updated = 1;
+        a->out[c] = (uint8_t)updated;
+        a->ones += (uint64_t)updated;
+    }
+    return NULL;
+}
+/* PFADD of generated elements first..first+n-1, element c into key_ids[c]; returns the number of 1 replies */
+uint64_t or_pfadd_gen_mt(uint8_t *regs_base, uint8_t *exists, uint64_t n, const uint32_t *key_ids, uint64_t seed,
+                         uint64_t first, int redis_major, uint8_t *out, int nthreads) {
+    int T = clampT(nthreads);
+    gen_arg a, args[256];
+    memset(&a, 0, sizeof a);
+    a.n = n;
+    a.key_ids = key_ids;
+    a.seed = seed;
+    a.first = first;
+    a.regs = regs_base;
+    a.exists = exists;
+    a.out = out;
+    a.redis_major = redis_major;
+    run_gen(T, &a, args, pfadd_gen);
+    uint64_t ones = 0;
+    for (int t = 0; t < T; t++) ones += args[t].ones;
+    return ones;
+}
+
+static void *union_gen(void *p) {
+    gen_arg *a = (gen_arg *)p;
+    uint8_t e[48];
+    uint64_t lo = a->n * (uint64_t)a->t / (uint64_t)a->T, hi = a->n * (uint64_t)(a->t + 1) / (uint64_t)a->T;
+    for (uint64_t c = lo; c < hi; c++) {
+        uint32_t len = or_gen_jackson_long(a->seed, a->first + c, e);
+        or_hll_add(a->regs, e, len, a->redis_major);
+    }
+    return NULL;
+}
+/* registers of the union of every HLL the generated elements went into (= the HLL of all of them) */
+void or_hll_union_gen_mt(uint8_t *regs_out, uint64_t n, uint64_t seed, uint64_t first, int redis_major,
+                         int nthreads) {
+    int T = clampT(nthreads);
+    static uint8_t priv[256][OR_HLL_REGISTERS];
+    gen_arg a, args[256];
+    memset(&a, 0, sizeof a);
+    a.n = n;
+    a.seed = seed;
+    a.first = first;
+    a.redis_major = redis_major;
+    pthread_t th[256];
+    for (int t = 0; t < T; t++) {
+        memset(priv[t], 0, OR_HLL_REGISTERS);
+        args[t] = a;
+        args[t].t = t;
+        args[t].T = T;
+        args[t].regs = priv[t];
+        pthread_create(&th[t], NULL, union_gen, &args[t]);
+    }
+    for (int t = 0; t < T; t++) pthread_join(th[t], NULL);
+    for (int t = 0; t < T; t++)
+        for (int r = 0; r < OR_HLL_REGISTERS; r++)
+            if (priv[t][r] > regs_out[r]) regs_out[r] = priv[t][r];
+}
+
+static void *bloom_add_gen(void *p) {
+    gen_arg *a = (gen_arg *)p;
+    uint8_t e[48];
+    int64_t idx[256];
+    int32_t kk = a->k > 256 ? 256 : a->k;
+    uint64_t lo = a->n * (uint64_t)a->t / (uint64_t)a->T, hi = a->n * (uint64_t)(a->t + 1) / (uint64_t)a->T;
+    for (uint64_t c = lo; c < hi; c++) {
+        uint32_t len = or_gen_jackson_long(a->seed, a->first + c, e);
+        or_bloom_indexes(e, len, kk, a->size, idx);
+        for (int32_t j = 0; j < kk; j++) {
+            uint64_t b = (uint64_t)idx[j] >> 3;
+            __atomic_fetch_or(&a->regs[b], (uint8_t)(0x80u >> ((uint64_t)idx[j] & 7u)), __ATOMIC_RELAXED);
+            if (b + 1 > a->maxbyte) a->maxbyte = b + 1;
+        }
+    }
+    return NULL;
+}
+/* bit array after RBloomFilter.add of the generated elements (bits: (size+7)/8 zeroed bytes);
+ * returns the Redis string length (highest byte SETBIT touched + 1) */
+uint64_t or_bloom_add_gen_mt(uint8_t *bits, int64_t size, int32_t k, uint64_t seed, uint64_t first, uint64_t n,
+                             int nthreads) {
+    int T = clampT(nthreads);
+    gen_arg a, args[256];
+    memset(&a, 0, sizeof a);
+    a.n = n;
+    a.seed = seed;
+    a.first = first;
+    a.regs = bits;
+    a.size = size;
+    a.k = k;
+    run_gen(T, &a, args, bloom_add_gen);
+    uint64_t m = 0;
+    for (int t = 0; t < T; t++)
+        if (args[t].maxbyte > m) m = args[t].maxbyte;
+    return m;
+}
+
+static void *bloom_contains_gen(void *p) {
+    gen_arg *a = (gen_arg *)p;
+    uint8_t e[48];
+    uint64_t lo = a->n * (uint64_t)a->t / (uint64_t)a->T, hi = a->n * (uint64_t)(a->t + 1) / (uint64_t)a->T;
+    for (uint64_t c = lo; c < hi; c++) {
+        uint64_t off[2] = {0, 0};
+        off[1] = or_gen_jackson_long(a->seed, a->idx[c], e);
+        or_bloom_contains_batch(a->regs, a->strlen_bytes, a->size, a->k, 1, off, e, a->out + c);
+    }
+    return NULL;
+}
+/* RBloomFilter.contains of generated elements idx[0..n) (element numbers of stream `seed`) */
+void or_bloom_contains_gen_mt(const uint8_t *bits, uint64_t strlen_bytes, int64_t size, int32_t k, uint64_t seed,
+                              const uint64_t *idx, uint64_t n, uint8_t *out, int nthreads) {
+    int T = clampT(nthreads);
+    gen_arg a, args[256];
+    memset(&a, 0, sizeof a);
+    a.n = n;
+    a.seed = seed;
+    a.idx = idx;
+    a.regs = (uint8_t *)bits;
+    a.strlen_bytes = strlen_bytes;
+    a.size = size;
+    a.k = k;
+    a.out = out;
+    run_gen(T, &a, args, bloom_contains_gen);
+}
+
+static void *setbits(void *p) {
+    gen_arg *a = (gen_arg *)p;
+    uint64_t lo = a->n * (uint64_t)a->t / (uint64_t)a->T, hi = a->n * (uint64_t)(a->t + 1) / (uint64_t)a->T;
+    for (uint64_t c = lo; c < hi; c++) {
+        uint64_t o = a->idx[c];
+        __atomic_fetch_or(&a->regs[o >> 3], (uint8_t)(0x80u >> (o & 7u)), __ATOMIC_RELAXED);
+    }
+    return NULL;
+}
+/* SETBIT key off 1 for every offset (MSB-first bytes, buf sized past the largest offset) */
+void or_setbits_mt(uint8_t *buf, const uint64_t *offsets, uint64_t n, int nthreads) {
+    int T = clampT(nthreads);
+    gen_arg a, args[256];
+    memset(&a, 0, sizeof a);
+    a.n = n;
+    a.idx = offsets;
+    a.regs = buf;
+    run_gen(T, &a, args, setbits);
 }

@@ -150,3 +150,39 @@ def test_threaded_baseline_matches_oracle(O):
     c1 = bits.bloom_contains_raw(size, k, off, buf)
     c3 = bits.bloom_contains_raw_mt(size, k, off, buf, 3)
     assert np.array_equal(c1, c3) and c1[:20000].all() and not c1[20000:].all()
+
+
+def test_full_size_checkers_agree_with_oracle(O):
+    """The generator-driven checkers of tests/test_full_size.py (oracle_mt.c) equal the plain oracle on the
+    elements the engine's host generator produces (sk_gen_jackson_longs: same SplitMix64 stream)."""
+    from redisson_amd import gen_jackson_longs
+
+    seed, n, nkeys = 0x5EED0888, 30000, 53
+    off, buf = gen_jackson_longs(seed, n)
+    els = [bytes(buf[off[i]:off[i + 1]]) for i in range(n)]
+    assert [O.gen_jackson_long(seed, i) for i in (0, 1, 7, n - 1)] == [els[0], els[1], els[7], els[n - 1]]
+    off = np.ascontiguousarray(off, dtype=np.uint64)
+    kid = np.random.default_rng(9).integers(0, nkeys, n).astype(np.uint32)
+    regs1, r1 = O.HLLStore().pfadd_bulk(kid, off, buf, nkeys)
+    regs = np.zeros((nkeys, 16384), np.uint8)
+    ex = np.zeros(nkeys, np.uint8)
+    r, ones = O.pfadd_gen(regs, ex, kid[:10000], seed, 0)
+    r2, ones2 = O.pfadd_gen(regs, ex, kid[10000:], seed, 10000)
+    assert np.array_equal(regs, regs1) and np.array_equal(np.concatenate([r, r2]), r1)
+    assert ones + ones2 == int(r1.sum())
+    assert np.array_equal(O.hll_union_gen(n, seed), regs1.max(axis=0))
+    size, k = 300007, 6
+    bits = O.BitString()
+    bits.bloom_add_raw(size, k, off[:12001], buf)
+    g, ln = O.bloom_add_gen(size, k, seed, 0, 12000)
+    assert ln == bits.len.value and bytes(g[:ln]) == bits.bytes() and not g[ln:].any()
+    idx = np.arange(n, dtype=np.uint64)[::-1].copy()
+    want = bits.bloom_contains(size, k, [els[i] for i in idx])
+    assert O.bloom_contains_gen(g, ln, size, k, seed, idx).astype(bool).tolist() == want
+    offs = np.random.default_rng(3).integers(0, 1 << 20, 5000).astype(np.uint64)
+    b1 = O.BitString()
+    for o in offs:
+        b1.setbit(int(o), 1)
+    b2 = np.zeros((1 << 17) + 16, np.uint8)
+    O.setbits(b2, offs)
+    assert bytes(b2[:b1.len.value]) == b1.bytes()

@@ -45,9 +45,10 @@ hipError_t sort_pairs(hipStream_t st, void *tmp, size_t tmp_bytes, const uint64_
 hipError_t launch_hll_hist(hipStream_t st, uint64_t n, const uint32_t *ids, const uint8_t *arena, uint32_t *hist);
 hipError_t launch_hll_union(hipStream_t st, uint64_t n, const uint32_t *ids, const uint8_t *arena, uint8_t *partial,
                             uint64_t max_groups, uint8_t *out, int include_out);
+// scratch: 16 B per element, used by the split schedule (sched 3) only
 hipError_t launch_bloom_contains(hipStream_t st, uint64_t n, const uint64_t *off, const uint8_t *bytes,
                                  const uint8_t *bits, const uint64_t *d_len, uint64_t size, uint64_t magic, int k,
-                                 uint8_t *out, int sched);
+                                 uint8_t *out, int sched, void *scratch = nullptr);
 hipError_t launch_bloom_probes(hipStream_t st, uint64_t n, const uint64_t *off, const uint8_t *bytes, uint64_t size,
                                uint64_t magic, int k, uint64_t *keys);
 hipError_t launch_bloom_apply(hipStream_t st, uint64_t m, const uint64_t *keys, uint8_t *bits, uint64_t *d_len, int k,

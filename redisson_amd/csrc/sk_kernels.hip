@@ -830,6 +830,50 @@ __global__ void __launch_bounds__(256) k_bloom_contains(uint64_t n, const uint64
                                                         uint64_t magic, int k, uint8_t *__restrict__ out) {
     bloom_contains_body<SK_STAGE_WORDS>(n, off, bytes, bits, d_len, size, magic, k, out);
 }
+// split schedule (SK_BLOOM_SCHED=3): k_bloom_hash writes (h1, h2) per element
+// (16 B, coalesced), k_bloom_probe_h walks the probes with few registers, so
+// the request-bound half runs at full occupancy and the compute-bound half can
+// overlap another stream's request-bound kernel.
+__global__ void __launch_bounds__(256) k_bloom_hash(uint64_t n, const uint64_t *__restrict__ off,
+                                                    const uint8_t *__restrict__ bytes, uint4 *__restrict__ hh) {
+    __shared__ uint64_t lds[SK_STAGE_WORDS];
+    uint64_t e0 = uint64_t(blockIdx.x) * blockDim.x, e1 = e0 + blockDim.x < n ? e0 + blockDim.x : n;
+    uint64_t lo = off[e0], hi = off[e1];
+    bool staged = stage_fits(lo, hi);
+    uint32_t wbase = staged ? stage_keys(bytes, lo, hi, lds) : 0u;
+    uint64_t i = e0 + threadIdx.x;
+    if (i >= n) return;
+    uint64_t o = off[i];
+    uint32_t len = uint32_t(off[i + 1] - o);
+    uint64_t h1, h2;
+    if (staged) {
+        LdsReader rd{lds, wbase + uint32_t(o - lo)};
+        h1 = xxh64_r(rd, len);
+        h2 = farm_uo64_r(rd, len);
+    } else {
+        bloom_hashes(bytes + o, len, &h1, &h2);
+    }
+    hh[i] = make_uint4(uint32_t(h1), uint32_t(h1 >> 32), uint32_t(h2), uint32_t(h2 >> 32));
+}
+__global__ void __launch_bounds__(256) k_bloom_probe_h(uint64_t n, const uint4 *__restrict__ hh,
+                                                       const uint8_t *__restrict__ bits,
+                                                       const uint64_t *__restrict__ d_len, uint64_t size,
+                                                       uint64_t magic, int k, uint8_t *__restrict__ out) {
+    uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint4 v = hh[i];
+    uint64_t h1 = uint64_t(v.x) | uint64_t(v.y) << 32, h2 = uint64_t(v.z) | uint64_t(v.w) << 32;
+    uint64_t slen = *d_len, h = h1;
+    uint8_t r = 1;
+    for (int j = 0; j < k - 1; j++) {
+        if (!get_bit(bits, slen, mod_invariant(h & 0x7fffffffffffffffull, size, magic))) {
+            r = 0;
+            break;
+        }
+        h += (j & 1) ? h1 : h2;
+    }
+    out[i] = r;
+}
 template <int EPT>
 __global__ void __launch_bounds__(256) k_bloom_contains_q(uint64_t n, const uint64_t *__restrict__ off,
                                                           const uint8_t *__restrict__ bytes,
@@ -1443,9 +1487,15 @@ hipError_t launch_hll_union(hipStream_t st, uint64_t n, const uint32_t *ids, con
 
 hipError_t launch_bloom_contains(hipStream_t st, uint64_t n, const uint64_t *off, const uint8_t *bytes,
                                  const uint8_t *bits, const uint64_t *d_len, uint64_t size, uint64_t magic, int k,
-                                 uint8_t *out, int sched) {
+                                 uint8_t *out, int sched, void *scratch) {
     if (!n) return hipSuccess;
-    if (sched == 1) // probe queue, 4 elements per lane (A/B: not faster at C3 -- line requests bound both)
+    if (sched == 3 && scratch) { // split: hash pass, then probe pass
+        hipLaunchKernelGGL(k_bloom_hash, dim3(grid_for(n, 256)), dim3(256), 0, st, n, off, bytes,
+                           reinterpret_cast<uint4 *>(scratch));
+        SK_LAUNCH_CHECK();
+        hipLaunchKernelGGL(k_bloom_probe_h, dim3(grid_for(n, 256)), dim3(256), 0, st, n,
+                           reinterpret_cast<const uint4 *>(scratch), bits, d_len, size, magic, k, out);
+    } else if (sched == 1) // probe queue, 4 elements per lane (A/B: not faster at C3 -- line requests bound both)
         hipLaunchKernelGGL(k_bloom_contains_q<4>, dim3(grid_for(n, 1024)), dim3(256), 0, st, n, off, bytes, bits,
                            d_len, size, magic, k, out);
     else // one element per thread

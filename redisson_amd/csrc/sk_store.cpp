@@ -224,7 +224,7 @@ struct sk_ctx {
     bool pfp_direct = true;     // partition path, one element per command: apply writes replies (SK_PFP_DIRECT)
     int claim_all = 1;          // PFADD claim: 1 = every element claims (R0 from the atomic), 0 = load first, claim candidates (SK_PFADD_CLAIM)
     int read_stream = 1;        // async Bloom contains on the read stream st2 (SK_READ_STREAM=0: main stream)
-    int bloom_sched = 0;        // contains kernel (SK_BLOOM_SCHED): 0 one element per thread; 1 probe queue, 4/lane
+    int bloom_sched = 0;        // contains kernel (SK_BLOOM_SCHED): 0 one element per thread; 1 probe queue, 4/lane; 3 split hash / probe passes
     // async PFADD: the conflict count of the last sparse batch is checked ("settled")
     // by the next call that needs the HLL arena, not by the call itself
     bool pf_pending = false;
@@ -243,7 +243,7 @@ struct sk_ctx {
     // workspace
     uint32_t *d_zero = nullptr; // device u32[4] zeros: id 0 / empty length
     DBuf keys_a, keys_b, vals_a, vals_b, sort_tmp, in_off, in_bytes, in_ids, in_cmd, out_u8, misc, partial, hist,
-        uni, ptrs, hist_a, hist_b, ovf;
+        uni, ptrs, hist_a, hist_b, ovf, bloom_h;
 };
 
 namespace {
@@ -869,7 +869,7 @@ int sk_close(sk_ctx *c) {
     if (c->h_cnt) (void)hipHostFree(c->h_cnt);
     for (DBuf *b : {&c->keys_a, &c->keys_b, &c->vals_a, &c->vals_b, &c->sort_tmp, &c->in_off, &c->in_bytes,
                     &c->in_ids, &c->in_cmd, &c->out_u8, &c->misc, &c->partial, &c->hist, &c->uni, &c->ptrs,
-                    &c->hist_a, &c->hist_b, &c->ovf})
+                    &c->hist_a, &c->hist_b, &c->ovf, &c->bloom_h})
         b->release();
     if (c->st2) (void)hipStreamSynchronize(c->st2);
     if (c->ev_w) (void)hipEventDestroy(c->ev_w);
@@ -1797,10 +1797,12 @@ int sk_bloom_contains(sk_ctx *c, const uint8_t *name, uint64_t len, int64_t size
     if (r || !n) return r;
     if ((r = stage_elems(c, n, off, bytes))) return r;
     HIPCHK(c, c->out_u8.ensure(n));
+    if (c->bloom_sched == 3) HIPCHK(c, c->bloom_h.ensure(16 * uint64_t(n)));
     const uint8_t *bits = id == kNoId ? reinterpret_cast<const uint8_t *>(c->d_zero) : c->strs[id].ptr;
     const uint64_t *dl = id == kNoId ? reinterpret_cast<const uint64_t *>(c->d_zero) : &c->d_dir[id].len;
     HIPCHK(c, sk::launch_bloom_contains(c->st, n, c->in_off.as<uint64_t>(), c->in_bytes.as<uint8_t>(), bits, dl,
-                                        uint64_t(size), magic_for(uint64_t(size)), k, c->out_u8.as<uint8_t>(), c->bloom_sched));
+                                        uint64_t(size), magic_for(uint64_t(size)), k, c->out_u8.as<uint8_t>(), c->bloom_sched,
+                                        c->bloom_h.p));
     HIPCHK(c, hipMemcpyAsync(out, c->out_u8.p, n, hipMemcpyDeviceToHost, c->st));
     return sync(c);
 }
@@ -1841,9 +1843,10 @@ int sk_bloom_contains_dev(sk_ctx *c, const uint8_t *name, uint64_t len, uint64_t
         HIPCHK(c, hipStreamWaitEvent(c->st2, c->ev_w, 0));
         c->st_wrote_bits = false;
     }
+    if (c->bloom_sched == 3) HIPCHK(c, c->bloom_h.ensure(16 * n));
     { Prof p_(c, 5, s);
     HIPCHK(c, sk::launch_bloom_contains(s, n, d_off, d_bytes, bits, dl, uint64_t(b->size),
-                                        magic_for(uint64_t(b->size)), b->k, d_out, c->bloom_sched)); }
+                                        magic_for(uint64_t(b->size)), b->k, d_out, c->bloom_sched, c->bloom_h.p)); }
     if (rs) {
         HIPCHK(c, hipEventRecord(c->ev_r, c->st2));
         c->rd_pending = true;

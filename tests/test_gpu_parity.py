@@ -428,9 +428,9 @@ def test_pfadd_partition_oversized_buckets(engine, O):
         np.testing.assert_array_equal(engine.hll_registers(nm), regs[i])
 
 
-@pytest.mark.parametrize("sched", ["0", "1"])
+@pytest.mark.parametrize("sched", ["0", "1", "3"])
 def test_bloom_contains_kernels_agree(O, sched):
-    """Both Bloom contains kernels (one element per thread, probe queue) gives the oracle's replies, for k = 1 (Q2: always true), small
+    """Every Bloom contains schedule (one element per thread, probe queue, split hash/probe passes) gives the oracle's replies, for k = 1 (Q2: always true), small
     and large k, ragged and empty elements, batch sizes off the tile size."""
     import os
     from redisson_amd import SketchEngine

@@ -12,5 +12,5 @@ for kv in "$@"; do
   python3 -c "
 import json,sys
 d=json.loads(open('$O/$i.json').read().strip().splitlines()[-1])
-print('$kv', round(d['value']/1e9,3), 'G/s step_us', round(d['ms_per_step']*1e3,1), {k: round(v*1e3,1) for k,v in d['kernel_ms_per_launch'].items()})"
+print('$kv', round(d['value']/1e9,3), 'G/s step_us', round(d['ms_per_step']*1e3,1), {k: round(v*1e3,1) for k,v in d['kernel_ms_per_launch'].items()}, 'iso', {k: round(v*1e3,1) for k,v in d['roofline_isolated']['kernel_ms_per_launch'].items()})"
 done

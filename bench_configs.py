@@ -14,6 +14,8 @@ measures the remaining configs on one MI355X with inputs resident in HBM:
       per source (roofline: HBM streaming).
   c5  RBitSet 2^34 bits (2 GiB): 1B random SETBIT (SETBIT_VOID), 1B GETBIT,
       BITCOUNT, AND/OR across 4 bitsets (BITOP streams (s+1)*N/8 bytes).
+  host  the host-buffer C ABI the JNI shim calls (PCIe-inclusive): C2-shaped
+      PFADD and C3-shaped Bloom add/contains batches from pageable host arrays.
 """
 from __future__ import annotations
 
@@ -27,7 +29,7 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
-from redisson_amd import JsonJacksonCodec, JLong, SketchEngine, owner  # noqa: E402
+from redisson_amd import JsonJacksonCodec, JLong, SketchEngine, gen_jackson_longs, owner  # noqa: E402
 
 PEAK = 8000.0
 
@@ -166,9 +168,74 @@ def c5(eng, args):
                        "unit": "GB/s", "frac": nbytes / t_bc / 1e9 / PEAK, "note": "host-timed incl. launch"}})
 
 
+def host(eng, args):
+    """The host-buffer C ABI (what the JNI shim calls): sk_pfadd / sk_bloom_add / sk_bloom_contains with caller-owned
+    host arrays, so each call stages its inputs H2D and copies replies D2H (PCIe-inclusive; DESIGN 'Measurement').
+    C2 shape (1M single-element PFADDs over 100k tenants, names resolved per call) and C3 shape (m=4,271,038,538,
+    k=7, 1M adds then 1M contains, 50% members)."""
+    from redisson_amd.engine import pack
+    eng.flushall()
+    B, reps, nt = 1 << 20, 4, 100_000
+    rng = np.random.default_rng(33)
+    names = [b"tenant:%d:hll" % t for t in range(nt)]
+    eng.hll_resolve(names)                     # tenants exist (the steady state of C2)
+    koff, kbuf = pack([names[t] for t in rng.integers(0, nt, B)])
+    counts = np.ones(B, dtype=np.uint32)
+    batches = [gen_jackson_longs(0x5EED0033 + r, B) for r in range(reps + 1)]
+    out = np.zeros(B, dtype=np.uint8)
+    lib, ctx = eng.lib, eng.ctx
+
+    def pf(r):
+        eoff, ebuf = batches[r]
+        eng._check(lib.sk_pfadd(ctx, B, koff.ctypes.data, kbuf.ctypes.data, counts.ctypes.data, eoff.ctypes.data,
+                                ebuf.ctypes.data, out.ctypes.data))
+    pf(0)
+    t_pf = timed(eng, lambda: [pf(r) for r in range(1, reps + 1)]) / reps
+    kids = np.ascontiguousarray(eng.hll_resolve(names)[rng.integers(0, nt, B)], dtype=np.uint32)
+
+    def pfi(r):  # the same batches with slab ids cached on the caller's side (sk_pfadd_ids)
+        eoff, ebuf = batches[r]
+        eng._check(lib.sk_pfadd_ids(ctx, B, kids.ctypes.data, counts.ctypes.data, eoff.ctypes.data,
+                                    ebuf.ctypes.data, out.ctypes.data))
+    t_pfi = timed(eng, lambda: [pfi(r) for r in range(1, reps + 1)]) / reps
+    h2d_pf = koff.nbytes + kbuf.nbytes + counts.nbytes + batches[1][0].nbytes + batches[1][1].nbytes
+    nm = b"bf:host"
+    assert eng.bloom_try_init(nm, 425_000_000, 0.008)
+    size, k, _, _ = eng.bloom_config(nm)
+
+    def bl(fn, r):
+        eoff, ebuf = batches[r]
+        eng._check(fn(ctx, nm, len(nm), size, k, B, eoff.ctypes.data, ebuf.ctypes.data, out.ctypes.data))
+    bl(lib.sk_bloom_add, 0)
+    t_add = timed(eng, lambda: [bl(lib.sk_bloom_add, r) for r in range(1, reps + 1)]) / reps
+    # contains: half of each batch re-probes added elements (the first half of batch r is batch r-1's)
+    probe = []
+    for r in range(1, reps + 1):
+        a = [batches[r - 1][1][batches[r - 1][0][i]:batches[r - 1][0][i + 1]].tobytes() for i in range(B // 2)]
+        b = [batches[r][1][batches[r][0][i]:batches[r][0][i + 1]].tobytes() for i in range(B // 2, B)]
+        probe.append(pack(a + b))
+    eoffs = [p_[0] for p_ in probe]
+
+    def ct(r):
+        eoff, ebuf = probe[r]
+        eng._check(lib.sk_bloom_contains(ctx, nm, len(nm), size, k, B, eoff.ctypes.data, ebuf.ctypes.data,
+                                         out.ctypes.data))
+    ct(0)
+    t_ct = timed(eng, lambda: [ct(r) for r in range(reps)]) / reps
+    h2d_bl = eoffs[0].nbytes + probe[0][1].nbytes
+    line({"metric": "Host-buffer C ABI (PCIe-inclusive) PFADD + Bloom contains ops/sec",
+          "value": 2 * B / (t_pfi + t_ct), "unit": "ops/s",
+          "config": {"workload": "host", "batch": B, "tenants": nt, "bloom_bits": size, "bloom_k": k},
+          "pfadd_host_per_s": B / t_pf, "pfadd_ids_host_per_s": B / t_pfi,
+          "pfadd_ids_ms_per_batch": t_pfi * 1e3, "bloom_add_host_per_s": B / t_add, "bloom_contains_host_per_s": B / t_ct,
+          "pfadd_ms_per_batch": t_pf * 1e3, "bloom_contains_ms_per_batch": t_ct * 1e3,
+          "pfadd_h2d_bytes": int(h2d_pf), "contains_h2d_bytes": int(h2d_bl),
+          "note": "synchronous calls, inputs in pageable host memory, replies copied back; value = sk_pfadd_ids (ids cached by the caller) + sk_bloom_contains; pfadd_host_per_s resolves names per call"})
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--configs", default="c1,c2zipf,c4,c5")
+    ap.add_argument("--configs", default="c1,c2zipf,c4,c5,host")
     ap.add_argument("--c1-n", type=int, default=1 << 20)
     ap.add_argument("--c4-keys", type=int, default=125_000)       # 1M keys / 8 GPUs
     ap.add_argument("--c4-per-key", type=int, default=1000)
@@ -178,7 +245,7 @@ def main():
     eng = SketchEngine(device=int(os.environ.get("LOCAL_RANK", "0")), max_bit_offset=1 << 36,
                        hll_capacity=args.c4_keys + 64, max_batch=1 << 24)
     for c in args.configs.split(","):
-        {"c1": c1, "c2zipf": c2zipf, "c4": c4, "c5": c5}[c](eng, args)
+        {"c1": c1, "c2zipf": c2zipf, "c4": c4, "c5": c5, "host": host}[c](eng, args)
     eng.close()
 
 

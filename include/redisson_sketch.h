@@ -118,6 +118,14 @@ int sk_hll_resolve(sk_ctx *ctx, uint32_t n, const uint64_t *key_off, const uint8
 int sk_pfadd(sk_ctx *ctx, uint32_t n_cmds, const uint64_t *key_off, const uint8_t *key_bytes,
              const uint32_t *elem_counts, const uint64_t *elem_off, const uint8_t *elem_bytes,
              uint8_t *out_changed);
+/* sk_pfadd with keys pre-resolved to slab ids by sk_hll_resolve (the Java
+ * executor caches name -> id per tenant, SURVEY 8(b) "key names resolved to
+ * slab ids on the Java side"); host buffers, same replies.  An id is valid
+ * until its key is deleted (DEL / flushall): the caller drops its cached ids
+ * then.  Ids never handed out fail with SK_EINVAL.  Replaces the PFADD
+ * round trip of M:RedissonHyperLogLog.java:66-68 / M:RedissonBatch.java:76-83. */
+int sk_pfadd_ids(sk_ctx *ctx, uint32_t n_cmds, const uint32_t *key_ids, const uint32_t *elem_counts,
+                 const uint64_t *elem_off, const uint8_t *elem_bytes, uint8_t *out_changed);
 /* PFADD of one element per command, keys pre-resolved to slab ids (all
  * existing); device-resident inputs.  d_out_changed u8[n] on device. */
 int sk_pfadd_dev(sk_ctx *ctx, uint64_t n, const uint32_t *d_key_ids, const uint64_t *d_elem_off,

@@ -25,6 +25,11 @@ public final class SketchNative {
     public static native int del(long ctx, long[] keyOff, byte[] keys, long[] outRemoved);
     public static native int pfadd(long ctx, long[] keyOff, byte[] keys, int[] elemCounts, long[] elemOff,
                                    byte[] elems, byte[] outChanged);
+    /** sk_hll_resolve: name -> slab id, creating empty HLLs (outCreated[i] = 1 if this call created key i). */
+    public static native int hllResolve(long ctx, long[] keyOff, byte[] keys, int[] outIds, byte[] outCreated);
+    /** sk_pfadd_ids: slab ids from a cached sk_hll_resolve (dropped on DEL / flushall). */
+    public static native int pfaddIds(long ctx, int[] keyIds, int[] elemCounts, long[] elemOff, byte[] elems,
+                                      byte[] outChanged);
     public static native int pfcount(long ctx, int[] nkeys, long[] keyOff, byte[] keys, long[] outCounts);
     public static native int pfmerge(long ctx, byte[] dest, long[] srcOff, byte[] srcs);
     public static native int setbit(long ctx, long[] keyOff, byte[] keys, long[] offsets, byte[] values,

@@ -67,6 +67,32 @@ JNIEXPORT jint JNICALL Java_org_redisson_gpu_SketchNative_pfadd(JNIEnv *env, jcl
     return st;
 }
 
+JNIEXPORT jint JNICALL Java_org_redisson_gpu_SketchNative_hllResolve(JNIEnv *env, jclass cls, jlong ctx,
+                                                                     jlongArray koff, jbyteArray keys,
+                                                                     jintArray out_ids, jbyteArray out_created) {
+    (void)cls;
+    jsize n = LEN(out_ids);
+    void *ko = PIN(koff), *k = PIN(keys), *i = PIN(out_ids), *cr = PIN(out_created);
+    jint st = sk_hll_resolve(CTX(ctx), (uint32_t)n, (const uint64_t *)ko, (const uint8_t *)k, (uint32_t *)i,
+                             (uint8_t *)cr);
+    UNPIN(out_created, cr, 0); UNPIN(out_ids, i, 0); UNPIN(keys, k, JNI_ABORT); UNPIN(koff, ko, JNI_ABORT);
+    return st;
+}
+
+/* sk_pfadd_ids: keys resolved once per tenant (SketchNative.hllResolve) and cached on the Java side */
+JNIEXPORT jint JNICALL Java_org_redisson_gpu_SketchNative_pfaddIds(JNIEnv *env, jclass cls, jlong ctx, jintArray ids,
+                                                                   jintArray counts, jlongArray eoff,
+                                                                   jbyteArray elems, jbyteArray out) {
+    (void)cls;
+    jsize n = LEN(counts);
+    void *i = PIN(ids), *c = PIN(counts), *eo = PIN(eoff), *e = PIN(elems), *r = PIN(out);
+    jint st = sk_pfadd_ids(CTX(ctx), (uint32_t)n, (const uint32_t *)i, (const uint32_t *)c, (const uint64_t *)eo,
+                           (const uint8_t *)e, (uint8_t *)r);
+    UNPIN(out, r, 0); UNPIN(elems, e, JNI_ABORT); UNPIN(eoff, eo, JNI_ABORT);
+    UNPIN(counts, c, JNI_ABORT); UNPIN(ids, i, JNI_ABORT);
+    return st;
+}
+
 JNIEXPORT jint JNICALL Java_org_redisson_gpu_SketchNative_pfcount(JNIEnv *env, jclass cls, jlong ctx, jintArray nk,
                                                                   jlongArray koff, jbyteArray keys, jlongArray out) {
     (void)cls;

@@ -59,6 +59,7 @@ SIGNATURES = {
     "sk_del": (c_int, [P, c_uint32, _u64p, _u8p, _u64p]),
     "sk_hll_resolve": (c_int, [P, c_uint32, _u64p, _u8p, _u32p, _u8p]),
     "sk_pfadd": (c_int, [P, c_uint32, _u64p, _u8p, _u32p, _u64p, _u8p, _u8p]),
+    "sk_pfadd_ids": (c_int, [P, c_uint32, _u32p, _u32p, _u64p, _u8p, _u8p]),
     "sk_pfadd_dev": (c_int, [P, c_uint64, _u32p, _u64p, _u8p, c_uint64, _u8p]),
     "sk_pfcount": (c_int, [P, c_uint32, _u32p, _u64p, _u8p, _i64p]),
     "sk_hll_histogram_dev": (c_int, [P, c_uint64, _u32p, _u32p]),

@@ -18,6 +18,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -1005,30 +1006,15 @@ int sk_hll_resolve(sk_ctx *c, uint32_t n, const uint64_t *off, const uint8_t *by
 }
 
 // ---------------------------------------------------------------- PFADD
-int sk_pfadd(sk_ctx *c, uint32_t n_cmds, const uint64_t *key_off, const uint8_t *key_bytes,
-             const uint32_t *elem_counts, const uint64_t *elem_off, const uint8_t *elem_bytes, uint8_t *out_changed) {
-    std::lock_guard<std::mutex> g(c->mu);
-    ENTER(c);
-    if (!n_cmds) return SK_OK;
-    // resolve keys in command order; the first command on a created key replies 1
-    std::vector<uint32_t> cmd_key(n_cmds);
-    std::vector<uint8_t> first_created(n_cmds, 0);
-    std::unordered_map<uint32_t, bool> pending_created;
-    int status = SK_OK;
-    std::vector<uint8_t> valid(n_cmds, 1);
-    for (uint32_t i = 0; i < n_cmds; i++) {
-        bool cr;
-        int r = hll_get(c, key_at(key_off, key_bytes, i), true, &cmd_key[i], &cr);
-        if (r == SK_EWRONGTYPE || r == SK_ECORRUPT) { // that command alone fails, as in a pipeline
-            valid[i] = 0;
-            status = r;
-            continue;
-        }
-        if (r) return r;
-        if (cr) first_created[i] = 1;
-    }
+// PFADD of commands whose keys are resolved (cmd_key[i], valid[i] = 0 skips a
+// failed command): device batches of <= max_batch elements, replies in
+// out_changed.  A chunk of valid one-element commands (the RBatch of add)
+// ships the caller's ids, rebased offsets and bytes as they are; otherwise
+// the valid commands' elements are re-packed with a command index each.
+static int pfadd_host_batch(sk_ctx *c, uint32_t n_cmds, const uint32_t *cmd_key, const uint8_t *valid,
+                            const uint32_t *elem_counts, const uint64_t *elem_off, const uint8_t *elem_bytes,
+                            uint8_t *out_changed) {
     std::memset(out_changed, 0, n_cmds);
-    // chunk by elements, never more than max_batch elements per device batch
     uint64_t total_e = 0;
     std::vector<uint64_t> cmd_e0(n_cmds + 1);
     for (uint32_t i = 0; i < n_cmds; i++) {
@@ -1038,59 +1024,75 @@ int sk_pfadd(sk_ctx *c, uint32_t n_cmds, const uint64_t *key_off, const uint8_t 
     cmd_e0[n_cmds] = total_e;
     uint32_t c0 = 0;
     std::vector<uint32_t> h_ids, h_cmd;
+    std::vector<uint64_t> off2;
+    std::vector<uint8_t> bytes2;
     while (c0 < n_cmds) {
         // commands [c0, c1) -- a single command larger than max_batch goes alone
         uint32_t c1 = c0;
         uint64_t ne = 0;
-        while (c1 < n_cmds && (c1 == c0 || ne + elem_counts[c1] <= c->max_batch)) ne += elem_counts[c1++];
-        // element list of valid commands
-        h_ids.clear();
-        h_cmd.clear();
-        uint64_t b0 = elem_off[cmd_e0[c0]], b1 = elem_off[cmd_e0[c1]];
-        for (uint32_t cc = c0; cc < c1; cc++) {
-            if (!valid[cc]) continue;
-            for (uint64_t e = cmd_e0[cc]; e < cmd_e0[cc + 1]; e++) {
-                h_ids.push_back(cmd_key[cc]);
-                h_cmd.push_back(cc - c0);
-            }
+        bool simple = true; // every command valid with one element
+        while (c1 < n_cmds && (c1 == c0 || ne + elem_counts[c1] <= c->max_batch)) {
+            simple = simple && valid[c1] && elem_counts[c1] == 1;
+            ne += elem_counts[c1++];
         }
-        uint64_t m = h_ids.size();
-        if (m) {
-            // re-pack the bytes of the valid commands' elements (+16 B padding)
-            std::vector<uint64_t> off2(m + 1);
-            std::vector<uint8_t> bytes2;
-            bytes2.reserve(b1 - b0 + 16);
+        uint64_t e0 = cmd_e0[c0], b0 = elem_off[e0], b1 = elem_off[cmd_e0[c1]];
+        const uint32_t *ids_src, *cmd_src = nullptr;
+        const uint8_t *bytes_src;
+        uint64_t m, nbytes;
+        off2.clear();
+        if (simple) {
+            m = c1 - c0;
+            off2.resize(m + 1);
+            for (uint64_t j = 0; j <= m; j++) off2[j] = elem_off[e0 + j] - b0;
+            ids_src = cmd_key + c0;
+            bytes_src = elem_bytes + b0;
+            nbytes = b1 - b0;
+        } else {
+            h_ids.clear();
+            h_cmd.clear();
+            bytes2.clear();
             uint64_t t = 0;
-            uint64_t ei = 0;
             for (uint32_t cc = c0; cc < c1; cc++) {
                 if (!valid[cc]) continue;
-                for (uint64_t e = cmd_e0[cc]; e < cmd_e0[cc + 1]; e++, ei++) {
+                for (uint64_t e = cmd_e0[cc]; e < cmd_e0[cc + 1]; e++) {
                     uint64_t l = elem_off[e + 1] - elem_off[e];
-                    off2[ei] = t;
+                    h_ids.push_back(cmd_key[cc]);
+                    h_cmd.push_back(cc - c0);
+                    off2.push_back(t);
                     bytes2.insert(bytes2.end(), elem_bytes + elem_off[e], elem_bytes + elem_off[e] + l);
                     t += l;
                 }
             }
-            off2[m] = t;
-            bytes2.resize(t + 16, 0);
+            off2.push_back(t);
+            m = h_ids.size();
+            ids_src = h_ids.data();
+            cmd_src = h_cmd.data();
+            bytes_src = bytes2.data();
+            nbytes = t;
+        }
+        if (m) {
             HIPCHK(c, c->in_ids.ensure(m * 4));
-            HIPCHK(c, c->in_cmd.ensure(m * 4));
             HIPCHK(c, c->in_off.ensure((m + 1) * 8));
-            HIPCHK(c, c->in_bytes.ensure(bytes2.size()));
+            HIPCHK(c, c->in_bytes.ensure(nbytes + 16));
             HIPCHK(c, c->out_u8.ensure(c1 - c0));
-            HIPCHK(c, hipMemcpyAsync(c->in_ids.p, h_ids.data(), m * 4, hipMemcpyHostToDevice, c->st));
-            HIPCHK(c, hipMemcpyAsync(c->in_cmd.p, h_cmd.data(), m * 4, hipMemcpyHostToDevice, c->st));
+            HIPCHK(c, hipMemcpyAsync(c->in_ids.p, ids_src, m * 4, hipMemcpyHostToDevice, c->st));
+            if (cmd_src) {
+                HIPCHK(c, c->in_cmd.ensure(m * 4));
+                HIPCHK(c, hipMemcpyAsync(c->in_cmd.p, cmd_src, m * 4, hipMemcpyHostToDevice, c->st));
+            }
             HIPCHK(c, hipMemcpyAsync(c->in_off.p, off2.data(), (m + 1) * 8, hipMemcpyHostToDevice, c->st));
-            HIPCHK(c, hipMemcpyAsync(c->in_bytes.p, bytes2.data(), bytes2.size(), hipMemcpyHostToDevice, c->st));
+            if (nbytes) HIPCHK(c, hipMemcpyAsync(c->in_bytes.p, bytes_src, nbytes, hipMemcpyHostToDevice, c->st));
+            HIPCHK(c, hipMemsetAsync(c->in_bytes.as<uint8_t>() + nbytes, 0, 16, c->st)); // padding contract
             HIPCHK(c, hipMemsetAsync(c->out_u8.p, 0, c1 - c0, c->st));
             uint64_t touched = 0; // distinct sketches: only the density heuristic of the non-default paths uses it
             if (c->pfadd_path != 1) {
-                std::vector<uint32_t> uniq(h_ids);
+                std::vector<uint32_t> uniq(ids_src, ids_src + m);
                 std::sort(uniq.begin(), uniq.end());
                 touched = uint64_t(std::unique(uniq.begin(), uniq.end()) - uniq.begin());
             }
             int r = pfadd_device(c, m, c->in_ids.as<uint32_t>(), c->in_off.as<uint64_t>(), c->in_bytes.as<uint8_t>(),
-                                 c->in_cmd.as<uint32_t>(), c1 - c0, c->out_u8.as<uint8_t>(), touched);
+                                 cmd_src ? c->in_cmd.as<uint32_t>() : nullptr, c1 - c0, c->out_u8.as<uint8_t>(),
+                                 touched);
             if (r) return r;
             HIPCHK(c, hipMemcpyAsync(out_changed + c0, c->out_u8.p, c1 - c0, hipMemcpyDeviceToHost, c->st));
             r = sync(c);
@@ -1098,9 +1100,78 @@ int sk_pfadd(sk_ctx *c, uint32_t n_cmds, const uint64_t *key_off, const uint8_t 
         }
         c0 = c1;
     }
+    return SK_OK;
+}
+
+// Parallel read-only pass over the key directory for a large batch: found[i] =
+// 1 and ids[i] set where key i already names an HLL.  Everything else (new
+// keys, strings to adopt, wrong types) is left to the caller's in-order pass,
+// so creation order and error text are those of the serial lookup.
+static void find_hlls_parallel(sk_ctx *c, uint32_t n, const uint64_t *key_off, const uint8_t *key_bytes,
+                               uint32_t *ids, uint8_t *found) {
+    unsigned T = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    if (const char *e = getenv("OMP_NUM_THREADS")) T = std::max(1, std::min(int(T), atoi(e)));
+    if (n < 65536 || T == 1) return;
+    auto work = [&](uint32_t i0, uint32_t i1) {
+        std::string k;
+        for (uint32_t i = i0; i < i1; i++) {
+            k.assign(reinterpret_cast<const char *>(key_bytes + key_off[i]), key_off[i + 1] - key_off[i]);
+            auto it = c->keys.find(k);
+            if (it != c->keys.end() && it->second.type == SK_TYPE_HLL) {
+                ids[i] = it->second.id;
+                found[i] = 1;
+            }
+        }
+    };
+    std::vector<std::thread> th;
+    uint32_t per = (n + T - 1) / T;
+    for (unsigned t = 1; t < T && t * per < n; t++) th.emplace_back(work, t * per, std::min<uint32_t>(n, (t + 1) * per));
+    work(0, std::min(n, per));
+    for (auto &x : th) x.join();
+}
+
+int sk_pfadd(sk_ctx *c, uint32_t n_cmds, const uint64_t *key_off, const uint8_t *key_bytes,
+             const uint32_t *elem_counts, const uint64_t *elem_off, const uint8_t *elem_bytes, uint8_t *out_changed) {
+    std::lock_guard<std::mutex> g(c->mu);
+    ENTER(c);
+    if (!n_cmds) return SK_OK;
+    // resolve keys in command order; the first command on a created key replies 1
+    std::vector<uint32_t> cmd_key(n_cmds);
+    std::vector<uint8_t> first_created(n_cmds, 0);
+    int status = SK_OK;
+    std::vector<uint8_t> valid(n_cmds, 1), found(n_cmds, 0);
+    find_hlls_parallel(c, n_cmds, key_off, key_bytes, cmd_key.data(), found.data());
+    std::string k;
+    for (uint32_t i = 0; i < n_cmds; i++) {
+        if (found[i]) continue;
+        bool cr;
+        k.assign(reinterpret_cast<const char *>(key_bytes + key_off[i]), key_off[i + 1] - key_off[i]);
+        int r = hll_get(c, k, true, &cmd_key[i], &cr);
+        if (r == SK_EWRONGTYPE || r == SK_ECORRUPT) { // that command alone fails, as in a pipeline
+            valid[i] = 0;
+            status = r;
+            continue;
+        }
+        if (r) return r;
+        if (cr) first_created[i] = 1;
+    }
+    int r = pfadd_host_batch(c, n_cmds, cmd_key.data(), valid.data(), elem_counts, elem_off, elem_bytes, out_changed);
+    if (r) return r;
     for (uint32_t i = 0; i < n_cmds; i++)
         if (first_created[i]) out_changed[i] = 1;
     return status;
+}
+
+int sk_pfadd_ids(sk_ctx *c, uint32_t n_cmds, const uint32_t *key_ids, const uint32_t *elem_counts,
+                 const uint64_t *elem_off, const uint8_t *elem_bytes, uint8_t *out_changed) {
+    std::lock_guard<std::mutex> g(c->mu);
+    ENTER(c);
+    if (!n_cmds) return SK_OK;
+    for (uint32_t i = 0; i < n_cmds; i++)
+        if (key_ids[i] >= c->hll_next)
+            return fail(c, SK_EINVAL, "PFADD: slab id %u was never resolved", key_ids[i]);
+    std::vector<uint8_t> valid(n_cmds, 1);
+    return pfadd_host_batch(c, n_cmds, key_ids, valid.data(), elem_counts, elem_off, elem_bytes, out_changed);
 }
 
 int sk_pfadd_dev(sk_ctx *c, uint64_t n, const uint32_t *d_ids, const uint64_t *d_off, const uint8_t *d_bytes,

@@ -258,6 +258,17 @@ class SketchEngine:
                                       _addr(ebuf), _addr(out)))
         return [bool(x) for x in out]
 
+    def pfadd_ids(self, key_ids, elems: Sequence[Sequence[bytes]]) -> List[bool]:
+        """PFADD batch with keys pre-resolved by hll_resolve: command i = PFADD key_ids[i] *elems[i]."""
+        ids = np.ascontiguousarray(key_ids, dtype=np.uint32)
+        n = len(ids)
+        counts = np.fromiter((len(e) for e in elems), dtype=np.uint32, count=n)
+        eoff, ebuf = pack([x for e in elems for x in e])
+        out = np.zeros(n, dtype=np.uint8)
+        self._check(self.lib.sk_pfadd_ids(self.ctx, n, _addr(ids), _addr(counts), _addr(eoff), _addr(ebuf),
+                                          _addr(out)))
+        return [bool(x) for x in out]
+
     def pfadd_dev(self, n: int, d_key_ids, d_elem_off, d_elem_bytes, bytes_len: int, d_out):
         self._check(self.lib.sk_pfadd_dev(self.ctx, n, _addr(d_key_ids), _addr(d_elem_off), _addr(d_elem_bytes),
                                           bytes_len, _addr(d_out)))

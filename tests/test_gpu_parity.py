@@ -591,3 +591,55 @@ def test_pfadd_multi_launch_zipf(engine, O):
         np.testing.assert_array_equal(engine.hll_registers(names[i]), regs[i])
     hot = int(np.bincount(kid).argmax())
     np.testing.assert_array_equal(engine.hll_registers(names[hot]), regs[hot])
+
+
+def test_pfadd_ids_matches_names_and_oracle(O):
+    """sk_pfadd_ids (slab ids from sk_hll_resolve, host buffers) gives the oracle's replies and registers, for
+    one-element commands (the shipped-as-is chunk), multi-element and empty commands (the re-packed chunk) and a
+    batch split into several device batches (max_batch); an id never handed out fails with SK_EINVAL."""
+    from redisson_amd import SketchEngine
+    from redisson_amd.engine import RedisException
+    e = SketchEngine(device=0, max_batch=3000)
+    try:
+        rng = np.random.default_rng(404)
+        names = [b"ids:%d" % i for i in range(37)]
+        ref = O.HLLStore()
+        ref.pfadd(names, [[] for _ in names])          # created by the resolve below
+        ids = e.hll_resolve(names)
+        els = _elems(0x5EED0404, 12000)
+        # one element per command, 8000 commands in 3 device batches
+        kid = rng.integers(0, len(names), 8000)
+        cmds = [[els[i]] for i in range(8000)]
+        assert e.pfadd_ids(ids[kid], cmds) == ref.pfadd([names[k] for k in kid], cmds)
+        # ragged commands (0..5 elements), repeats of earlier elements
+        kid2 = rng.integers(0, len(names), 1500)
+        cmds2 = [[els[int(j)] for j in rng.integers(0, 12000, int(rng.integers(0, 6)))] for _ in kid2]
+        assert e.pfadd_ids(ids[kid2], cmds2) == ref.pfadd([names[k] for k in kid2], cmds2)
+        for i, nm in enumerate(names):
+            np.testing.assert_array_equal(e.hll_registers(nm), ref.regs[nm])
+        # the name path over the same store agrees
+        cmds3 = [[x] for x in _elems(0x5EED0405, 4000)]
+        kid3 = rng.integers(0, len(names), 4000)
+        assert e.pfadd([names[k] for k in kid3], cmds3) == ref.pfadd([names[k] for k in kid3], cmds3)
+        with pytest.raises(RedisException, match="never resolved"):
+            e.pfadd_ids(np.array([1 << 20], dtype=np.uint32), [[b"x"]])
+    finally:
+        e.close()
+
+
+def test_pfadd_names_large_batch_parallel_lookup(engine, O):
+    """A name batch >= 64k commands takes the parallel directory lookup: keys that exist, keys created in the
+    middle of the batch (reply 1 only for the first command on them) and repeats give the oracle's replies."""
+    rng = np.random.default_rng(405)
+    names = [b"big:%d" % i for i in range(3000)]
+    ref = O.HLLStore()
+    old = names[:1500]
+    e0 = _elems(0x5EED0406, 1500)
+    assert engine.pfadd(old, [[x] for x in e0]) == ref.pfadd(old, [[x] for x in e0])
+    n = 100_000
+    kid = rng.integers(0, len(names), n)
+    els = _elems(0x5EED0407, n)
+    keys = [names[k] for k in kid]
+    assert engine.pfadd(keys, [[x] for x in els]) == ref.pfadd(keys, [[x] for x in els])
+    for nm in names[::97]:
+        np.testing.assert_array_equal(engine.hll_registers(nm), ref.regs[nm])

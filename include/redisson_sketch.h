@@ -134,6 +134,11 @@ int sk_pfadd_dev(sk_ctx *ctx, uint64_t n, const uint32_t *d_key_ids, const uint6
  * (1 = RHyperLogLog.count, >1 = countWith).  Missing keys count as empty. */
 int sk_pfcount(sk_ctx *ctx, uint32_t n_cmds, const uint32_t *nkeys, const uint64_t *key_off,
                const uint8_t *key_bytes, int64_t *out_counts);
+/* RHyperLogLog.count (M:RedissonHyperLogLog.java:78-81) of n keys given by
+ * slab ids from sk_hll_resolve (cached by the caller, as for sk_pfadd_ids):
+ * out[i] = PFCOUNT of key_ids[i].  One histogram launch, estimates on host
+ * threads.  Ids never handed out fail with SK_EINVAL. */
+int sk_pfcount_ids(sk_ctx *ctx, uint64_t n, const uint32_t *key_ids, int64_t *out);
 /* per-key 64-bin register histograms for slab ids (device in / device out u32[n*64]) */
 int sk_hll_histogram_dev(sk_ctx *ctx, uint64_t n, const uint32_t *d_key_ids, uint32_t *d_hist);
 /* PFMERGE dest src1..srcn (dest included in the max, becomes dense) */

@@ -31,6 +31,8 @@ public final class SketchNative {
     public static native int pfaddIds(long ctx, int[] keyIds, int[] elemCounts, long[] elemOff, byte[] elems,
                                       byte[] outChanged);
     public static native int pfcount(long ctx, int[] nkeys, long[] keyOff, byte[] keys, long[] outCounts);
+    /** sk_pfcount_ids: RHyperLogLog.count of many keys by cached slab id. */
+    public static native int pfcountIds(long ctx, int[] keyIds, long[] outCounts);
     public static native int pfmerge(long ctx, byte[] dest, long[] srcOff, byte[] srcs);
     public static native int setbit(long ctx, long[] keyOff, byte[] keys, long[] offsets, byte[] values,
                                     byte[] outOld);

@@ -93,6 +93,16 @@ JNIEXPORT jint JNICALL Java_org_redisson_gpu_SketchNative_pfaddIds(JNIEnv *env, 
     return st;
 }
 
+JNIEXPORT jint JNICALL Java_org_redisson_gpu_SketchNative_pfcountIds(JNIEnv *env, jclass cls, jlong ctx,
+                                                                     jintArray ids, jlongArray out) {
+    (void)cls;
+    jsize n = LEN(ids);
+    void *i = PIN(ids), *r = PIN(out);
+    jint st = sk_pfcount_ids(CTX(ctx), (uint64_t)n, (const uint32_t *)i, (int64_t *)r);
+    UNPIN(out, r, 0); UNPIN(ids, i, JNI_ABORT);
+    return st;
+}
+
 JNIEXPORT jint JNICALL Java_org_redisson_gpu_SketchNative_pfcount(JNIEnv *env, jclass cls, jlong ctx, jintArray nk,
                                                                   jlongArray koff, jbyteArray keys, jlongArray out) {
     (void)cls;

@@ -1206,6 +1206,57 @@ int sk_hll_histogram_dev(sk_ctx *c, uint64_t n, const uint32_t *d_ids, uint32_t 
     return sync(c);
 }
 
+// Estimates of many single-key counts: exact-sum histograms (every register
+// < 40, and every redis >= 5 estimate) in parallel threads, the rest (the
+// register-order sum needs a register readback) in order afterwards.
+static int estimate_many(sk_ctx *c, uint64_t n, const uint32_t *h, const uint32_t *ids, int64_t *out) {
+    std::vector<uint8_t> slow(n, 0);
+    auto work = [&](uint64_t i0, uint64_t i1) {
+        for (uint64_t i = i0; i < i1; i++) {
+            const uint32_t *hi = h + i * 64;
+            if (c->redis_major >= 5) {
+                out[i] = int64_t(estimate_v5(hi));
+            } else if (hist_exact_v3(hi)) {
+                double E = 0;
+                for (int v = 0; v < 64; v++) E += double(hi[v]) * g_pe[v];
+                out[i] = int64_t(estimate_v3(E, int(hi[0])));
+            } else {
+                slow[i] = 1;
+            }
+        }
+    };
+    unsigned T = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    if (const char *e = getenv("OMP_NUM_THREADS")) T = std::max(1, std::min(int(T), atoi(e)));
+    if (n < 32768) T = 1;
+    std::vector<std::thread> th;
+    uint64_t per = (n + T - 1) / T;
+    for (unsigned t = 1; t < T && t * per < n; t++) th.emplace_back(work, t * per, std::min<uint64_t>(n, (t + 1) * per));
+    work(0, std::min<uint64_t>(n, per));
+    for (auto &x : th) x.join();
+    for (uint64_t i = 0; i < n; i++) {
+        if (!slow[i]) continue;
+        int rc;
+        out[i] = int64_t(estimate_host(c, h + i * 64, c->arena + uint64_t(ids[i]) * kHllBytes, false, &rc));
+        if (rc) return rc;
+    }
+    return SK_OK;
+}
+
+int sk_pfcount_ids(sk_ctx *c, uint64_t n, const uint32_t *key_ids, int64_t *out) {
+    std::lock_guard<std::mutex> g(c->mu);
+    ENTER(c);
+    if (!n) return SK_OK;
+    for (uint64_t i = 0; i < n; i++)
+        if (key_ids[i] >= c->hll_next)
+            return fail(c, SK_EINVAL, "PFCOUNT: slab id %u was never resolved", key_ids[i]);
+    HIPCHK(c, c->in_ids.ensure(n * 4));
+    HIPCHK(c, hipMemcpyAsync(c->in_ids.p, key_ids, n * 4, hipMemcpyHostToDevice, c->st));
+    std::vector<uint32_t> h;
+    int r = hll_histograms(c, n, c->in_ids.as<uint32_t>(), c->arena, h);
+    if (r) return r;
+    return estimate_many(c, n, h.data(), key_ids, out);
+}
+
 int sk_pfcount(sk_ctx *c, uint32_t n_cmds, const uint32_t *nkeys, const uint64_t *key_off, const uint8_t *key_bytes,
                int64_t *out) {
     std::lock_guard<std::mutex> g(c->mu);
@@ -1248,12 +1299,9 @@ int sk_pfcount(sk_ctx *c, uint32_t n_cmds, const uint32_t *nkeys, const uint64_t
         HIPCHK(c, hipMemcpyAsync(c->in_ids.p, single_ids.data(), single_ids.size() * 4, hipMemcpyHostToDevice, c->st));
         int r = hll_histograms(c, single_ids.size(), c->in_ids.as<uint32_t>(), c->arena, h);
         if (r) return r;
-        for (size_t i = 0; i < single_ids.size(); i++) {
-            int rc;
-            out[single_cmd[i]] = int64_t(estimate_host(c, &h[i * 64], c->arena + uint64_t(single_ids[i]) * kHllBytes,
-                                                       false, &rc));
-            if (rc) return rc;
-        }
+        std::vector<int64_t> est(single_ids.size());
+        if ((r = estimate_many(c, single_ids.size(), h.data(), single_ids.data(), est.data()))) return r;
+        for (size_t i = 0; i < single_ids.size(); i++) out[single_cmd[i]] = est[i];
     }
     // multi-key commands: union into a temporary raw register array (nothing modified)
     HIPCHK(c, c->uni.ensure(kHllBytes));

@@ -281,6 +281,13 @@ class SketchEngine:
         self._check(self.lib.sk_pfcount(self.ctx, len(cmds), _addr(nk), _addr(koff), _addr(kbuf), _addr(out)))
         return [int(x) for x in out]
 
+    def pfcount_ids(self, key_ids) -> np.ndarray:
+        """Per-key PFCOUNT of slab ids from hll_resolve (int64 array)."""
+        ids = np.ascontiguousarray(key_ids, dtype=np.uint32)
+        out = np.zeros(len(ids), dtype=np.int64)
+        self._check(self.lib.sk_pfcount_ids(self.ctx, len(ids), _addr(ids), _addr(out)))
+        return out
+
     def pfmerge(self, dest, srcs: Sequence):
         d = _b(dest)
         soff, sbuf = pack([_b(s) for s in srcs])

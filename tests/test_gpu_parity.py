@@ -643,3 +643,39 @@ def test_pfadd_names_large_batch_parallel_lookup(engine, O):
     assert engine.pfadd(keys, [[x] for x in els]) == ref.pfadd(keys, [[x] for x in els])
     for nm in names[::97]:
         np.testing.assert_array_equal(engine.hll_registers(nm), ref.regs[nm])
+
+
+def test_pfcount_ids_many_keys(O):
+    """sk_pfcount_ids over 40k slab ids (threaded estimates): empty keys, keys of 1..600 elements, and two keys
+    holding registers >= 40 (the register-order sum, run after the threaded pass) give the oracle's counts; the
+    name path (sk_pfcount) agrees; an id never handed out fails."""
+    from redisson_amd import SketchEngine
+    from redisson_amd.engine import RedisException
+    e = SketchEngine(device=0)
+    try:
+        rng = np.random.default_rng(406)
+        nk = 40_000
+        names = [b"cnt:%d" % i for i in range(nk)]
+        ids = e.hll_resolve(names)
+        per = rng.integers(0, 600, nk)
+        per[: nk // 4] = 0
+        kid = np.repeat(np.arange(nk), per)
+        rng.shuffle(kid)
+        off, buf = O.pack(_elems(0x5EED0409, len(kid)))
+        d = [e.to_device(ids[kid].astype(np.uint32)), e.to_device(off), e.to_device(buf, pad=16), e.alloc(len(kid))]
+        e.pfadd_dev(len(kid), d[0], d[1], d[2], int(off[-1]), d[3])
+        regs, _ = O.HLLStore().pfadd_bulk(kid, off, buf, nk)
+        big = np.zeros(16384, dtype=np.uint8)
+        big[:] = rng.integers(0, 12, 16384)
+        big[[5, 77, 9000]] = [40, 45, 50]
+        for j in (7, nk - 3):
+            e.hll_merge_registers_dev(names[j], e.to_device(big))
+            regs[j] = np.maximum(regs[j], big)
+        want = [O.count_regs(regs[i], 1) for i in range(nk)]
+        assert list(e.pfcount_ids(ids)) == want
+        sub = rng.integers(0, nk, 3000)
+        assert e.pfcount([[names[i]] for i in sub]) == [want[i] for i in sub]
+        with pytest.raises(RedisException, match="never resolved"):
+            e.pfcount_ids(np.array([1 << 22], dtype=np.uint32))
+    finally:
+        e.close()

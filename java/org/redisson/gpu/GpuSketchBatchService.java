@@ -122,7 +122,7 @@ public class GpuSketchBatchService extends CommandBatchService {
                     }
                 }
                 SketchDispatch.Packed e = new SketchDispatch.Packed(elems);
-                SketchDispatch.check(ctx, SketchNative.pfadd(ctx, k.off, k.bytes, counts, e.off, e.bytes, out));
+                SketchDispatch.pfaddRun(ctx, keys, k, counts, e, out);
             } else if ("PFCOUNT".equals(kind)) {
                 for (Cmd c : run) {
                     c.promise.setSuccess(GpuSketchCommandService.convert(c.command,

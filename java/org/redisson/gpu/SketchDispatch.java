@@ -8,7 +8,9 @@
 package org.redisson.gpu;
 
 import java.io.ByteArrayOutputStream;
+import java.nio.charset.Charset;
 import java.util.List;
+import java.util.concurrent.ConcurrentHashMap;
 
 import org.redisson.client.RedisException;
 import org.redisson.client.codec.Codec;
@@ -32,6 +34,54 @@ final class SketchDispatch {
             off[items.size()] = out.size();
             out.write(new byte[16], 0, 16); // device padding contract
             bytes = out.toByteArray();
+        }
+    }
+
+    static final Charset ISO = Charset.forName("ISO-8859-1"); // bytes <-> String one to one
+
+    /* Per-context HLL name -> slab id cache (INTEGRATION.md "Caching slab ids").  Filled after a key's first
+     * name-path PFADD; DEL of sketch keys is not routed to the engine by these executors, so an id stays
+     * valid for the context's lifetime. */
+    static final ConcurrentHashMap<Long, ConcurrentHashMap<String, Integer>> SLAB_IDS =
+            new ConcurrentHashMap<Long, ConcurrentHashMap<String, Integer>>();
+
+    static ConcurrentHashMap<String, Integer> slabIds(long ctx) {
+        ConcurrentHashMap<String, Integer> m = SLAB_IDS.get(ctx);
+        if (m == null) {
+            ConcurrentHashMap<String, Integer> fresh = new ConcurrentHashMap<String, Integer>();
+            m = SLAB_IDS.putIfAbsent(ctx, fresh);
+            if (m == null) {
+                m = fresh;
+            }
+        }
+        return m;
+    }
+
+    /* A run of PFADD commands: sk_pfadd_ids when every key has a cached slab id, else sk_pfadd by name,
+     * then the run's keys are resolved (they exist now; nothing is created) and cached. */
+    static void pfaddRun(long ctx, List<byte[]> keys, Packed k, int[] counts, Packed e, byte[] out) {
+        ConcurrentHashMap<String, Integer> cache = slabIds(ctx);
+        int n = keys.size();
+        int[] ids = new int[n];
+        boolean cached = true;
+        for (int c = 0; c < n && cached; c++) {
+            Integer id = cache.get(new String(keys.get(c), ISO));
+            if (id == null) {
+                cached = false;
+            } else {
+                ids[c] = id.intValue();
+            }
+        }
+        if (cached) {
+            check(ctx, SketchNative.pfaddIds(ctx, ids, counts, e.off, e.bytes, out));
+            return;
+        }
+        check(ctx, SketchNative.pfadd(ctx, k.off, k.bytes, counts, e.off, e.bytes, out));
+        byte[] created = new byte[n];
+        if (SketchNative.hllResolve(ctx, k.off, k.bytes, ids, created) == SketchNative.SK_OK) {
+            for (int c = 0; c < n; c++) {
+                cache.put(new String(keys.get(c), ISO), Integer.valueOf(ids[c]));
+            }
         }
     }
 

@@ -15,7 +15,9 @@
 package org.redisson.gpu;
 
 import java.util.ArrayList;
+import java.util.HashSet;
 import java.util.List;
+import java.util.Set;
 
 import org.redisson.client.RedisException;
 import org.redisson.client.codec.Codec;
@@ -46,6 +48,7 @@ public class GpuSketchBatchService extends CommandBatchService {
 
     final long ctx;
     final List<Cmd> sketch = new ArrayList<Cmd>();
+    final Set<String> touched = new HashSet<String>();
 
     public GpuSketchBatchService(ConnectionManager connectionManager, long ctx) {
         super(connectionManager);
@@ -55,9 +58,17 @@ public class GpuSketchBatchService extends CommandBatchService {
     @Override
     protected <V, R> void async(boolean readOnlyMode, NodeSource nodeSource, Codec codec, RedisCommand<V> command,
                                 Object[] params, Promise<R> mainPromise, int attempt) {
-        if (!GpuSketchCommandService.SKETCH_COMMANDS.contains(command.getName())) {
+        String name = command.getName();
+        // GET / SET / DEL join the sketch queue when the engine holds the key, or an earlier sketch command of
+        // this batch names it (it may create the key before this one runs)
+        boolean keyCommand = GpuSketchCommandService.KEY_COMMANDS.contains(name) && params.length > 0
+                && (touched.contains(params[0].toString()) || SketchDispatch.engineHolds(ctx, params[0]));
+        if (!keyCommand && !GpuSketchCommandService.SKETCH_COMMANDS.contains(name)) {
             super.async(readOnlyMode, nodeSource, codec, command, params, mainPromise, attempt);
             return;
+        }
+        if (params.length > 0) {
+            touched.add(params[0].toString());
         }
         sketch.add(new Cmd(codec, command, params, mainPromise));
     }
@@ -98,8 +109,10 @@ public class GpuSketchBatchService extends CommandBatchService {
         String kind = run.get(0).command.getName();
         if (!runnable(kind) || run.size() == 1) {
             for (Cmd c : run) {
-                c.promise.setSuccess(GpuSketchCommandService.convert(c.command,
-                        SketchDispatch.single(ctx, c.codec, c.command, c.params)));
+                Object reply = GpuSketchCommandService.KEY_COMMANDS.contains(c.command.getName())
+                        ? SketchDispatch.keyCommand(ctx, c.codec, c.command, c.params)
+                        : SketchDispatch.single(ctx, c.codec, c.command, c.params);
+                c.promise.setSuccess(GpuSketchCommandService.convert(c.command, reply));
             }
             return;
         }

@@ -34,6 +34,10 @@ public class GpuSketchCommandService extends CommandAsyncService {
     static final Set<String> SKETCH_COMMANDS = new HashSet<String>(Arrays.asList(
             "PFADD", "PFCOUNT", "PFMERGE", "SETBIT", "GETBIT", "BITCOUNT", "BITOP", "STRLEN"));
     static final Charset UTF8 = Charset.forName("UTF-8");
+    /* Generic key commands that act on a sketch key when the engine holds it: RBitSet.toByteArray (GET,
+     * M:RedissonBitSet.java:88-91), set(BitSet) (SET, :211-214), clear() / delete() (DEL, :250-253).  The same
+     * commands on keys the engine does not hold (RBucket ...) still go to redis-server. */
+    static final Set<String> KEY_COMMANDS = new HashSet<String>(Arrays.asList("GET", "SET", "DEL"));
 
     final long ctx;
 
@@ -45,12 +49,15 @@ public class GpuSketchCommandService extends CommandAsyncService {
     @Override
     protected <V, R> void async(boolean readOnlyMode, NodeSource source, Codec codec, RedisCommand<V> command,
                                 Object[] params, Promise<R> mainPromise, int attempt) {
-        if (!SKETCH_COMMANDS.contains(command.getName())) {
+        boolean keyCommand = KEY_COMMANDS.contains(command.getName()) && params.length > 0
+                && SketchDispatch.engineHolds(ctx, params[0]);
+        if (!keyCommand && !SKETCH_COMMANDS.contains(command.getName())) {
             super.async(readOnlyMode, source, codec, command, params, mainPromise, attempt);
             return;
         }
         try {
-            Object reply = SketchDispatch.single(ctx, codec, command, params);
+            Object reply = keyCommand ? SketchDispatch.keyCommand(ctx, codec, command, params)
+                    : SketchDispatch.single(ctx, codec, command, params);
             @SuppressWarnings("unchecked")
             R r = (R) convert(command, reply);
             mainPromise.setSuccess(r);

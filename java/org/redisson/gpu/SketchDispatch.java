@@ -40,8 +40,7 @@ final class SketchDispatch {
     static final Charset ISO = Charset.forName("ISO-8859-1"); // bytes <-> String one to one
 
     /* Per-context HLL name -> slab id cache (INTEGRATION.md "Caching slab ids").  Filled after a key's first
-     * name-path PFADD; DEL of sketch keys is not routed to the engine by these executors, so an id stays
-     * valid for the context's lifetime. */
+     * name-path PFADD; keyCommand's DEL drops the deleted keys' entries. */
     static final ConcurrentHashMap<Long, ConcurrentHashMap<String, Integer>> SLAB_IDS =
             new ConcurrentHashMap<Long, ConcurrentHashMap<String, Integer>>();
 
@@ -96,6 +95,50 @@ final class SketchDispatch {
             throw new IllegalArgumentException(SketchNative.lastError(ctx));
         }
         throw new RedisException(SketchNative.lastError(ctx));
+    }
+
+    static boolean engineHolds(long ctx, Object key) {
+        int[] t = new int[1];
+        byte[] k = key instanceof byte[] ? (byte[]) key : key.toString().getBytes(GpuSketchCommandService.UTF8);
+        return SketchNative.type(ctx, k, t) == SketchNative.SK_OK && t[0] != SketchNative.SK_TYPE_NONE;
+    }
+
+    /* GET / SET / DEL on a key the engine holds (engineHolds of the first key).  GET decodes the raw bytes with
+     * the command's codec (ByteArrayCodec for RBitSet: the bytes as they are); SET writes the encoded value;
+     * DEL removes the keys the engine holds and replies their number. */
+    static Object keyCommand(long ctx, Codec codec, RedisCommand<?> command, Object[] params) {
+        try {
+            String name = command.getName();
+            if ("DEL".equals(name)) {
+                java.util.ArrayList<byte[]> keys = new java.util.ArrayList<byte[]>();
+                for (Object p : params) {
+                    keys.add(p.toString().getBytes(GpuSketchCommandService.UTF8));
+                }
+                Packed k = new Packed(keys);
+                long[] removed = new long[1];
+                ConcurrentHashMap<String, Integer> cache = slabIds(ctx);
+                for (byte[] kb : keys) {
+                    cache.remove(new String(kb, ISO)); // the slab id may be handed to another key
+                }
+                check(ctx, SketchNative.del(ctx, k.off, k.bytes, removed));
+                return Long.valueOf(removed[0]);
+            }
+            byte[] key = GpuSketchCommandService.encodeParam(codec, command, params[0], 1);
+            if ("GET".equals(name)) {
+                byte[] v = SketchNative.get(ctx, key);
+                if (v == null) {
+                    return null;
+                }
+                return codec.getValueDecoder().decode(io.netty.buffer.Unpooled.wrappedBuffer(v), null);
+            }
+            byte[] v = GpuSketchCommandService.encodeParam(codec, command, params[1], 2);
+            check(ctx, SketchNative.set(ctx, key, v));
+            return "OK";
+        } catch (RedisException e) {
+            throw e;
+        } catch (Exception e) {
+            throw new RedisException(e.getMessage(), e);
+        }
     }
 
     static Object single(long ctx, Codec codec, RedisCommand<?> command, Object[] params) {

@@ -175,6 +175,16 @@ JNIEXPORT jint JNICALL Java_org_redisson_gpu_SketchNative_bitop(JNIEnv *env, jcl
     return st;
 }
 
+JNIEXPORT jint JNICALL Java_org_redisson_gpu_SketchNative_type(JNIEnv *env, jclass cls, jlong ctx, jbyteArray key,
+                                                               jintArray out) {
+    (void)cls;
+    jsize n = LEN(key);
+    void *k = PIN(key), *r = PIN(out);
+    jint st = sk_type(CTX(ctx), (const uint8_t *)k, (uint64_t)n, (int *)r);
+    UNPIN(out, r, 0); UNPIN(key, k, JNI_ABORT);
+    return st;
+}
+
 JNIEXPORT jbyteArray JNICALL Java_org_redisson_gpu_SketchNative_get(JNIEnv *env, jclass cls, jlong ctx,
                                                                    jbyteArray key) {
     (void)cls;

@@ -1268,12 +1268,29 @@ int sk_pfcount(sk_ctx *c, uint32_t n_cmds, const uint32_t *nkeys, const uint64_t
     int status = SK_OK;
     std::vector<std::vector<uint32_t>> multi(n_cmds);
     std::vector<uint8_t> is_multi(n_cmds, 0), bad(n_cmds, 0);
+    uint64_t total_keys = 0;
+    for (uint32_t cmd = 0; cmd < n_cmds; cmd++) total_keys += nkeys[cmd];
+    std::vector<uint32_t> fids;
+    std::vector<uint8_t> found;
+    if (total_keys >= 65536 && total_keys < (1ull << 32)) { // existing HLLs in a parallel read-only pass
+        fids.resize(total_keys);
+        found.assign(total_keys, 0);
+        find_hlls_parallel(c, uint32_t(total_keys), key_off, key_bytes, fids.data(), found.data());
+    }
+    std::string kb;
+    std::vector<uint32_t> ids;
     for (uint32_t cmd = 0; cmd < n_cmds; cmd++) {
         out[cmd] = 0;
-        std::vector<uint32_t> ids;
+        ids.clear();
         for (uint32_t j = 0; j < nkeys[cmd]; j++, k++) {
             uint32_t id;
-            int r = hll_get(c, key_at(key_off, key_bytes, k), false, &id, nullptr);
+            int r = SK_OK;
+            if (!found.empty() && found[k]) {
+                id = fids[k];
+            } else {
+                kb.assign(reinterpret_cast<const char *>(key_bytes + key_off[k]), key_off[k + 1] - key_off[k]);
+                r = hll_get(c, kb, false, &id, nullptr);
+            }
             if (r == SK_EWRONGTYPE) {
                 bad[cmd] = 1;
                 status = r;
@@ -1290,7 +1307,7 @@ int sk_pfcount(sk_ctx *c, uint32_t n_cmds, const uint32_t *nkeys, const uint64_t
             }
         } else {
             is_multi[cmd] = 1;
-            multi[cmd] = std::move(ids);
+            multi[cmd] = ids;
         }
     }
     std::vector<uint32_t> h;

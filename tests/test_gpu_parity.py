@@ -675,6 +675,12 @@ def test_pfcount_ids_many_keys(O):
         assert list(e.pfcount_ids(ids)) == want
         sub = rng.integers(0, nk, 3000)
         assert e.pfcount([[names[i]] for i in sub]) == [want[i] for i in sub]
+        # >= 64k keys by name (the parallel directory pass): singles twice, missing keys, 3-key unions
+        pairs = rng.integers(0, nk, (200, 2))
+        cmds = [[nm] for nm in names] * 2 + [[b"absent:1"]] + \
+               [[names[a], names[b], b"absent:%d" % a] for a, b in pairs]
+        exp = want * 2 + [0] + [O.count_regs(np.maximum(regs[a], regs[b]), 2) for a, b in pairs]
+        assert e.pfcount(cmds) == exp
         with pytest.raises(RedisException, match="never resolved"):
             e.pfcount_ids(np.array([1 << 22], dtype=np.uint32))
     finally:

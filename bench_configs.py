@@ -224,13 +224,23 @@ def host(eng, args):
     ct(0)
     t_ct = timed(eng, lambda: [ct(r) for r in range(reps)]) / reps
     h2d_bl = eoffs[0].nbytes + probe[0][1].nbytes
+    # the same PFADD batch with inputs already on the device (diagnostic: device share of the host path)
+    dk, do_, db, dout = (eng.to_device(kids), eng.to_device(batches[1][0]), eng.to_device(batches[1][1], pad=16),
+                         eng.alloc(B))
+    t_dev = timed(eng, lambda: eng.pfadd_dev(B, dk, do_, db, int(batches[1][0][-1]), dout), reps=3)
+    for x in (dk, do_, db, dout):
+        x.free()
+    # raw pageable H2D rate of one PFADD batch's element bytes (diagnostic for the rates above)
+    raw = batches[1][1]
+    t_h2d = timed(eng, lambda: eng.to_device(raw).free(), reps=3)
     line({"metric": "Host-buffer C ABI (PCIe-inclusive) PFADD + Bloom contains ops/sec",
           "value": 2 * B / (t_pfi + t_ct), "unit": "ops/s",
           "config": {"workload": "host", "batch": B, "tenants": nt, "bloom_bits": size, "bloom_k": k},
           "pfadd_host_per_s": B / t_pf, "pfadd_ids_host_per_s": B / t_pfi,
           "pfadd_ids_ms_per_batch": t_pfi * 1e3, "bloom_add_host_per_s": B / t_add, "bloom_contains_host_per_s": B / t_ct,
           "pfadd_ms_per_batch": t_pf * 1e3, "bloom_contains_ms_per_batch": t_ct * 1e3,
-          "pfadd_h2d_bytes": int(h2d_pf), "contains_h2d_bytes": int(h2d_bl),
+          "pfadd_h2d_bytes": int(h2d_pf), "pageable_h2d_GBps": raw.nbytes / t_h2d / 1e9,
+          "pfadd_dev_ms_per_batch": t_dev * 1e3, "contains_h2d_bytes": int(h2d_bl),
           "note": "synchronous calls, inputs in pageable host memory, replies copied back; value = sk_pfadd_ids (ids cached by the caller) + sk_bloom_contains; pfadd_host_per_s resolves names per call"})
 
 

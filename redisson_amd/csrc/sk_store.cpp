@@ -194,6 +194,7 @@ struct sk_ctx {
     uint8_t *arena = nullptr;
     uint64_t hll_cap = 0, hll_next = 0;
     std::vector<uint32_t> hll_free;
+    std::vector<uint64_t> h_e0, h_off; // host PFADD staging, kept across calls (no page faults per batch)
 
     // strings: host mirror of {ptr, cap}; len lives in the device directory
     std::vector<DirEnt> strs;
@@ -1007,7 +1008,7 @@ int sk_hll_resolve(sk_ctx *c, uint32_t n, const uint64_t *off, const uint8_t *by
 
 // ---------------------------------------------------------------- PFADD
 // PFADD of commands whose keys are resolved (cmd_key[i], valid[i] = 0 skips a
-// failed command): device batches of <= max_batch elements, replies in
+// failed command; valid == nullptr: all valid): device batches of <= max_batch elements, replies in
 // out_changed.  A chunk of valid one-element commands (the RBatch of add)
 // ships the caller's ids, rebased offsets and bytes as they are; otherwise
 // the valid commands' elements are re-packed with a command index each.
@@ -1015,34 +1016,45 @@ static int pfadd_host_batch(sk_ctx *c, uint32_t n_cmds, const uint32_t *cmd_key,
                             const uint32_t *elem_counts, const uint64_t *elem_off, const uint8_t *elem_bytes,
                             uint8_t *out_changed) {
     std::memset(out_changed, 0, n_cmds);
-    uint64_t total_e = 0;
-    std::vector<uint64_t> cmd_e0(n_cmds + 1);
-    for (uint32_t i = 0; i < n_cmds; i++) {
-        cmd_e0[i] = total_e;
-        total_e += elem_counts[i];
+    // element index of command i's first element (cmd_e0[i] = i when every command has one element)
+    bool all_one = true;
+    for (uint32_t i = 0; i < n_cmds && all_one; i++) all_one = elem_counts[i] == 1;
+    std::vector<uint64_t> &e0v = c->h_e0;
+    if (!all_one) {
+        e0v.resize(n_cmds + 1);
+        uint64_t total_e = 0;
+        for (uint32_t i = 0; i < n_cmds; i++) {
+            e0v[i] = total_e;
+            total_e += elem_counts[i];
+        }
+        e0v[n_cmds] = total_e;
     }
-    cmd_e0[n_cmds] = total_e;
+    auto cmd_e0 = [&](uint32_t i) -> uint64_t { return all_one ? uint64_t(i) : e0v[i]; };
     uint32_t c0 = 0;
     std::vector<uint32_t> h_ids, h_cmd;
-    std::vector<uint64_t> off2;
+    std::vector<uint64_t> &off2 = c->h_off;
     std::vector<uint8_t> bytes2;
     while (c0 < n_cmds) {
         // commands [c0, c1) -- a single command larger than max_batch goes alone
         uint32_t c1 = c0;
         uint64_t ne = 0;
         bool simple = true; // every command valid with one element
-        while (c1 < n_cmds && (c1 == c0 || ne + elem_counts[c1] <= c->max_batch)) {
-            simple = simple && valid[c1] && elem_counts[c1] == 1;
-            ne += elem_counts[c1++];
+        if (all_one && !valid) { // every command valid with one element: chunk by count
+            c1 = uint32_t(std::min<uint64_t>(n_cmds, uint64_t(c0) + std::max<uint64_t>(c->max_batch, 1)));
+        } else {
+            while (c1 < n_cmds && (c1 == c0 || ne + elem_counts[c1] <= c->max_batch)) {
+                simple = simple && (!valid || valid[c1]) && elem_counts[c1] == 1;
+                ne += elem_counts[c1++];
+            }
         }
-        uint64_t e0 = cmd_e0[c0], b0 = elem_off[e0], b1 = elem_off[cmd_e0[c1]];
+        uint64_t e0 = cmd_e0(c0), b0 = elem_off[e0], b1 = elem_off[cmd_e0(c1)];
         const uint32_t *ids_src, *cmd_src = nullptr;
         const uint8_t *bytes_src;
         uint64_t m, nbytes;
-        off2.clear();
+        if (!simple) off2.clear();
         if (simple) {
             m = c1 - c0;
-            off2.resize(m + 1);
+            if (off2.size() < m + 1) off2.resize(m + 1);
             for (uint64_t j = 0; j <= m; j++) off2[j] = elem_off[e0 + j] - b0;
             ids_src = cmd_key + c0;
             bytes_src = elem_bytes + b0;
@@ -1053,8 +1065,8 @@ static int pfadd_host_batch(sk_ctx *c, uint32_t n_cmds, const uint32_t *cmd_key,
             bytes2.clear();
             uint64_t t = 0;
             for (uint32_t cc = c0; cc < c1; cc++) {
-                if (!valid[cc]) continue;
-                for (uint64_t e = cmd_e0[cc]; e < cmd_e0[cc + 1]; e++) {
+                if (valid && !valid[cc]) continue;
+                for (uint64_t e = cmd_e0(cc); e < cmd_e0(cc + 1); e++) {
                     uint64_t l = elem_off[e + 1] - elem_off[e];
                     h_ids.push_back(cmd_key[cc]);
                     h_cmd.push_back(cc - c0);
@@ -1155,7 +1167,8 @@ int sk_pfadd(sk_ctx *c, uint32_t n_cmds, const uint64_t *key_off, const uint8_t 
         if (r) return r;
         if (cr) first_created[i] = 1;
     }
-    int r = pfadd_host_batch(c, n_cmds, cmd_key.data(), valid.data(), elem_counts, elem_off, elem_bytes, out_changed);
+    int r = pfadd_host_batch(c, n_cmds, cmd_key.data(), status == SK_OK ? nullptr : valid.data(), elem_counts,
+                             elem_off, elem_bytes, out_changed);
     if (r) return r;
     for (uint32_t i = 0; i < n_cmds; i++)
         if (first_created[i]) out_changed[i] = 1;
@@ -1170,8 +1183,7 @@ int sk_pfadd_ids(sk_ctx *c, uint32_t n_cmds, const uint32_t *key_ids, const uint
     for (uint32_t i = 0; i < n_cmds; i++)
         if (key_ids[i] >= c->hll_next)
             return fail(c, SK_EINVAL, "PFADD: slab id %u was never resolved", key_ids[i]);
-    std::vector<uint8_t> valid(n_cmds, 1);
-    return pfadd_host_batch(c, n_cmds, key_ids, valid.data(), elem_counts, elem_off, elem_bytes, out_changed);
+    return pfadd_host_batch(c, n_cmds, key_ids, nullptr, elem_counts, elem_off, elem_bytes, out_changed);
 }
 
 int sk_pfadd_dev(sk_ctx *c, uint64_t n, const uint32_t *d_ids, const uint64_t *d_off, const uint8_t *d_bytes,

@@ -685,3 +685,21 @@ def test_pfcount_ids_many_keys(O):
             e.pfcount_ids(np.array([1 << 22], dtype=np.uint32))
     finally:
         e.close()
+
+
+def test_pfadd_mixed_batch_wrongtype_skips_one_command(engine, O):
+    """A PFADD batch with a command on a bit string fails that command alone (pipeline semantics): the other
+    commands (one element each, and a multi-element one) still update their registers exactly."""
+    engine.setbit([b"mx:str"], [5], [1])
+    els = _elems(0x5EED0410, 3000)
+    keys = [b"mx:%d" % (i % 7) for i in range(3000)]
+    keys[1234] = b"mx:str"
+    cmds = [[x] for x in els]
+    cmds[10] = els[:50]
+    with pytest.raises(RedisException, match="HyperLogLog"):
+        engine.pfadd(keys, cmds)
+    ref = O.HLLStore()
+    keep = [i for i in range(3000) if i != 1234]
+    ref.pfadd([keys[i] for i in keep], [cmds[i] for i in keep])
+    for k in set(keys) - {b"mx:str"}:
+        np.testing.assert_array_equal(engine.hll_registers(k), ref.regs[k])

@@ -198,6 +198,7 @@ def host(eng, args):
         eoff, ebuf = batches[r]
         eng._check(lib.sk_pfadd_ids(ctx, B, kids.ctypes.data, counts.ctypes.data, eoff.ctypes.data,
                                     ebuf.ctypes.data, out.ctypes.data))
+    pfi(0)
     t_pfi = timed(eng, lambda: [pfi(r) for r in range(1, reps + 1)]) / reps
     h2d_pf = koff.nbytes + kbuf.nbytes + counts.nbytes + batches[1][0].nbytes + batches[1][1].nbytes
     nm = b"bf:host"

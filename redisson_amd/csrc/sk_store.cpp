@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -56,7 +57,10 @@ struct DBuf {
     size_t cap = 0;
     hipError_t ensure(size_t bytes) {
         if (bytes <= cap) return hipSuccess;
-        size_t nc = std::max(bytes, cap * 2);
+        // 1/8 headroom in 2 MiB steps: batches of slightly varying size do not reallocate (a hipFree
+        // synchronises the device and cost 28 ms once with a large keyspace resident)
+        size_t nc = std::max(bytes + bytes / 8, cap * 2);
+        nc = (nc + (size_t(2) << 20) - 1) & ~((size_t(2) << 20) - 1);
         if (p) {
             hipError_t e = hipFree(p);
             if (e != hipSuccess) return e;
@@ -1082,6 +1086,9 @@ static int pfadd_host_batch(sk_ctx *c, uint32_t n_cmds, const uint32_t *cmd_key,
             bytes_src = bytes2.data();
             nbytes = t;
         }
+        static const bool tdbg = getenv("SK_HOST_TIMING") != nullptr; // dev knob: phase times to stderr
+        auto now = [] { return std::chrono::steady_clock::now(); };
+        auto t0 = now();
         if (m) {
             HIPCHK(c, c->in_ids.ensure(m * 4));
             HIPCHK(c, c->in_off.ensure((m + 1) * 8));
@@ -1106,9 +1113,14 @@ static int pfadd_host_batch(sk_ctx *c, uint32_t n_cmds, const uint32_t *cmd_key,
                                  cmd_src ? c->in_cmd.as<uint32_t>() : nullptr, c1 - c0, c->out_u8.as<uint8_t>(),
                                  touched);
             if (r) return r;
+            auto t1 = now();
             HIPCHK(c, hipMemcpyAsync(out_changed + c0, c->out_u8.p, c1 - c0, hipMemcpyDeviceToHost, c->st));
             r = sync(c);
             if (r) return r;
+            if (tdbg)
+                fprintf(stderr, "[sk host pfadd] m=%llu enqueue %.3f ms, d2h+sync %.3f ms\n", (unsigned long long)m,
+                        std::chrono::duration<double, std::milli>(t1 - t0).count(),
+                        std::chrono::duration<double, std::milli>(now() - t1).count());
         }
         c0 = c1;
     }

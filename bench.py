@@ -1,18 +1,16 @@
 #!/usr/bin/env python3
 """bench.py -- HLL inserts/s + Bloom contains/s (whole node) on the MI355X sketch engine.
 
-One "step" = one RBatch-sized batch of PFADD (C2: 100k tenants, Jackson-encoded
-random Longs, one element per command, 1M commands) + one batch of Bloom
-contains (C3: tryInit(425,000,000, 0.008) -> m = 4,271,038,538 bits, k = 7,
-50 % members / 50 % fresh, 1M elements), both with inputs already resident in
-HBM.  value = (PFADD elements + contains elements) / wall time, all ranks.
+One "step" = HB RBatch-sized PFADD batches (C2: 100k tenants, Jackson-encoded random Longs, one element per
+command, B = 1M commands each) + one Bloom contains batch of CB elements (C3: tryInit(425,000,000, 0.008) ->
+m = 4,271,038,538 bits, k = 7, filled with the config's 1B adds, 50 % members / 50 % fresh), inputs already
+resident in HBM.  Defaults: HB = 16, CB = 16M, so a step is 16M PFADD + 16M contains.
+value = (PFADD elements + contains elements) / wall time, all ranks.
 
-Multi-GPU (torch.distributed.run, one process per GPU): keys are partitioned by
-calcSlot(key) % world (the north-star partitioner), each rank owns its tenants
-and its own Bloom filter, no data-path collective -> "scaling": "weak".
-Rendezvous / barrier / max-over-ranks timing use torch.distributed's gloo (CPU)
-backend: the engine owns the GPU through the system HIP runtime, so this
-process never initialises torch's bundled HIP runtime.
+Multi-GPU (torch.distributed.run, one process per GPU): keys are partitioned by calcSlot(key) % world (the
+north-star partitioner), each rank owns its tenants and its own Bloom filter, no data-path collective ->
+"scaling": "weak".  Rendezvous / barrier / max-over-ranks timing use torch.distributed's gloo (CPU) backend: the
+engine owns the GPU through the system HIP runtime, so this process never initialises torch's bundled HIP runtime.
 """
 from __future__ import annotations
 
@@ -29,13 +27,14 @@ sys.path.insert(0, ROOT)
 
 from redisson_amd import SketchEngine, device_count, owner  # noqa: E402
 
-PROF_STEPS = 5          # steps in each per-kernel breakdown pass (outside the timed region)
+PROF_STEPS = 2          # steps in each per-kernel breakdown pass (outside the timed region)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-# in-library event-timed phases (sk_prof_*): one kernel each, except pfadd_sort
-# (rocPRIM onesweep passes); only the path in use has launches
-HLL_PHASES = ["pfp_hash", "pfp_apply", "pfp_reply",
-              "pfadd_claim", "pfadd_commit", "pfadd_hash", "pfadd_sort", "pfadd_apply"]
-PHASES = HLL_PHASES + ["bloom_contains"]
+# in-library event-timed phases (sk_prof_*): one kernel each, except the chains "pfadd" (every kernel of one
+# PFADD batch) and "bloom_contains" (every kernel of one contains call), and pfadd_sort (rocPRIM passes)
+HLL_KERNELS = ["pfp_hash", "pfp_apply", "pfp_reply", "pfadd_claim", "pfadd_commit", "pfadd_hash", "pfadd_apply"]
+BLOOM_KERNELS = ["bloom_rc_hash", "bloom_rc_probe"]
+CHAINS = ["pfadd", "bloom_contains"]
+PHASES = HLL_KERNELS + ["pfadd_sort"] + BLOOM_KERNELS + CHAINS
 
 
 def log(*a):
@@ -73,22 +72,25 @@ def allmax(pg, x: float) -> float:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=1 << 20, help="commands per PFADD / contains batch")
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=1 << 20, help="commands per PFADD RBatch (C2: 1M)")
+    ap.add_argument("--hll-batches", type=int, default=16, help="PFADD RBatches per step")
+    ap.add_argument("--contains-batch", type=int, default=16 << 20, help="Bloom contains elements per step")
     ap.add_argument("--tenants", type=int, default=100_000)
     ap.add_argument("--bloom-n", type=int, default=425_000_000)
     ap.add_argument("--bloom-p", type=float, default=0.008)
-    ap.add_argument("--bloom-fill", type=int, default=-1, help="elements added before contains (default bloom-n)")
+    ap.add_argument("--bloom-fill", type=int, default=1_000_000_000, help="elements added before contains (C3: 1B)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=2_000_000)
     args = ap.parse_args()
 
     world, rank, local, pg = dist_setup()
-    B, K, W = args.batch, args.steps, args.warmup
-    fill = args.bloom_n if args.bloom_fill < 0 else args.bloom_fill
+    B, HB, CB, K, W = args.batch, args.hll_batches, args.contains_batch, args.steps, args.warmup
+    fill = args.bloom_fill
 
     # ------------------------------------------------------------ setup (untimed)
+    t_setup = time.perf_counter()
     names = ["tenant:%d:hll" % t for t in range(args.tenants)]
     mine = [nm for nm in names if owner(nm, world) == rank]
     ndev = max(device_count(), 1)   # one rank per GPU; rehearsals with more ranks than GPUs share devices
@@ -98,13 +100,21 @@ def main():
     rng = np.random.default_rng(0x5EED0002 + rank)
 
     nsteps = W + K + 2 * PROF_STEPS   # warmup, isolated breakdown, overlapped breakdown, timed: fresh inputs each
+    NH = HB * B                       # PFADD elements per step
     seed_h = 0x5EED0002
-    base_h = rank << 40                      # disjoint element streams per rank
-    h_off, h_bytes, h_total = eng.gen_jackson_longs_dev(seed_h, nsteps * B, first=base_h)
-    kid = rng.integers(0, len(mine), nsteps * B)
-    d_ids = eng.to_device(ids[kid].astype(np.uint32))
+    # PFADD inputs, one device buffer set per step: element stream of this rank (disjoint per rank)
+    h_in = []
+    h_total = 0
+    kid_all = []
+    for s in range(nsteps):
+        off, byt, tot = eng.gen_jackson_longs_dev(seed_h, NH, first=(rank << 40) + s * NH)
+        kid = rng.integers(0, len(mine), NH)
+        kid_all.append(kid if s == 0 else None)
+        d_ids = eng.to_device(ids[kid].astype(np.uint32))
+        h_in.append((off, byt, tot, d_ids))
+        h_total += tot
     d_changed = eng.alloc(B)
-    mean_len_h = h_total / (nsteps * B)
+    mean_len_h = h_total / (nsteps * NH)
 
     bloom = "bloom:c3:%d" % rank
     eng.bloom_try_init(bloom, args.bloom_n, args.bloom_p)
@@ -123,21 +133,29 @@ def main():
         add_s += time.perf_counter() - t0
         a_off.free()
         a_bytes.free()
-    # contains inputs: 50 % members, 50 % fresh
-    member = rng.integers(0, max(fill, 1), nsteps * B, dtype=np.uint64) + np.uint64(rank << 40)
-    fresh = rng.integers(1 << 39, 1 << 40, nsteps * B, dtype=np.uint64) + np.uint64(rank << 40)
-    pick = rng.random(nsteps * B) < 0.5
-    idx = np.where(pick, member, fresh)
-    d_idx = eng.to_device(idx)
-    c_off, c_bytes, c_total = eng.gen_jackson_longs_dev(seed_b, nsteps * B, d_idx=d_idx)
-    d_idx.free()
-    d_contains = eng.alloc(B)
-    mean_len_b = c_total / (nsteps * B)
-    log(f"[rank {rank}] setup: {len(mine)} tenants, bloom m={size} k={k} filled with {fill} in {add_s:.1f}s")
+    # contains inputs: 50 % members (drawn from the fill), 50 % fresh
+    c_in = []
+    c_total = 0
+    for s in range(nsteps):
+        member = rng.integers(0, max(fill, 1), CB, dtype=np.uint64) + np.uint64(rank << 40)
+        fresh = rng.integers(1 << 39, 1 << 40, CB, dtype=np.uint64) + np.uint64(rank << 40)
+        idx = np.where(rng.random(CB) < 0.5, member, fresh)
+        d_idx = eng.to_device(idx)
+        off, byt, tot = eng.gen_jackson_longs_dev(seed_b, CB, d_idx=d_idx)
+        d_idx.free()
+        c_in.append((off, byt, tot))
+        c_total += tot
+    d_contains = eng.alloc(CB)
+    mean_len_b = c_total / (nsteps * CB)
+    log(f"[rank {rank}] setup: {len(mine)} tenants, bloom m={size} k={k} filled with {fill} "
+        f"(adds {add_s:.2f}s), {nsteps} steps of {HB}x{B} PFADD + {CB} contains, {time.perf_counter() - t_setup:.0f}s")
 
     def step(s):
-        eng.pfadd_dev(B, d_ids.ptr + s * B * 4, h_off.ptr + s * B * 8, h_bytes, h_total, d_changed)
-        eng.bloom_contains_dev(bloom, B, c_off.ptr + s * B * 8, c_bytes, c_total, d_contains)
+        off, byt, tot, d_ids = h_in[s]
+        for h in range(HB):
+            eng.pfadd_dev(B, d_ids.ptr + h * B * 4, off.ptr + h * B * 8, byt, tot, d_changed)
+        off, byt, tot = c_in[s]
+        eng.bloom_contains_dev(bloom, CB, off, byt, tot, d_contains)
 
     P = PROF_STEPS
     for s in range(W):
@@ -145,7 +163,7 @@ def main():
     eng.sync()
 
     def profiled(first, mode_async):
-        """Per-phase device time over P fresh steps (every launch event-timed)."""
+        """Per-phase device time over P fresh steps (every launch event-timed): {phase: (launches, ms)}."""
         eng.set_async(mode_async)
         eng.prof_only(None)
         eng.prof_reset()
@@ -156,16 +174,17 @@ def main():
         eng.prof_enable(False)
         eng.set_async(False)
         r = {p: eng.prof_read(p) for p in PHASES}
-        return {p: r[p][1] / r[p][0] for p in PHASES if r[p][0]}
+        return {p: (r[p][0] / P, r[p][1] / r[p][0]) for p in PHASES if r[p][0]}
 
-    # each kernel alone (sync mode: PFADD and contains do not overlap): the dominant
-    # kernel is the one with the most device time of its own (overlapped launch times
-    # mostly measure contention, and PFADD's apply and contains run neck and neck there)
-    iso_ms = profiled(W, False)
-    dom = max([p for p in iso_ms if p != "pfadd_sort"], key=lambda p: iso_ms[p])
-    # breakdown as in the timed region (PFADD on the main stream, contains on the
-    # read stream, no host sync)
-    over_ms = profiled(W + P, True)
+    # each kernel alone (sync mode: PFADD and contains do not overlap).  The dominant kernel is the one with the
+    # most device time per step of its own (overlapped launch times mostly measure contention).
+    iso = profiled(W, False)
+    kern = [p for p in iso if p not in CHAINS and p != "pfadd_sort"]
+    if "bloom_rc_hash" not in iso:   # one-element-per-thread contains: the chain is one kernel
+        kern.append("bloom_contains")
+    dom = max(kern, key=lambda p: iso[p][0] * iso[p][1])
+    # breakdown as in the timed region (PFADD on the main stream, contains on the read stream, no host sync)
+    over = profiled(W + P, True)
 
     # ------------------------------------------------------------ timed region
     # async: PFADD batches never wait on the host; only `dom` is event-timed
@@ -191,39 +210,49 @@ def main():
     dev_ms = eng.timer_elapsed_ms(0, 1)
     n_launch, tot_ms = eng.prof_read(dom)
 
-    units = 2 * B * K * world
+    units = (NH + CB) * K * world
     value = units / wall
-    # roofline of the dominant kernel: algorithmic bytes per unit x units / avg launch time
-    per_unit = per_unit_of(dom, mean_len_h, mean_len_b, k)
+    nr = (size + (1 << 20) - 1) >> 20
+    bpu = per_unit_bytes(mean_len_h, mean_len_b, k, size, CB, nr)
+    upl = {"pfp_hash": B, "pfp_apply": B, "pfp_reply": B, "pfadd": B, "bloom_contains": CB,
+           "bloom_rc_hash": CB, "bloom_rc_probe": CB}
     avg_ms = tot_ms / max(n_launch, 1)
-    achieved = per_unit * B / (avg_ms * 1e-3) / 1e9
-
-    hll_ms = sum(v for p, v in iso_ms.items() if p in HLL_PHASES)
-    bl_ms = iso_ms["bloom_contains"]
-    iso_dom_ms = iso_ms[dom]
-    iso_achieved = per_unit_of(dom, mean_len_h, mean_len_b, k) * B / (iso_dom_ms * 1e-3) / 1e9
+    achieved = bpu[dom] * upl.get(dom, B) / (avg_ms * 1e-3) / 1e9
     traffic = pmc_traffic(dom)
-    iso_traffic = traffic
-    # every kernel of the step: algorithmic GB/s alone and in the overlapped schedule
+
     kernels = {}
-    for p_, ms in iso_ms.items():
-        if p_ == "pfadd_sort":
+    for p_, (lps, ms) in iso.items():
+        if p_ == "pfadd_sort" or p_ in CHAINS:
             continue
-        pu = per_unit_of(p_, mean_len_h, mean_len_b, k)
+        u = upl.get(p_, B)
         tr = pmc_traffic(p_)
-        kernels[p_] = {"bytes_per_unit": pu, "ms_isolated": ms, "GBps_isolated": pu * B / (ms * 1e-3) / 1e9,
-                       "ms_overlapped": over_ms.get(p_),
-                       "GBps_overlapped": pu * B / (over_ms[p_] * 1e-3) / 1e9 if over_ms.get(p_) else None,
+        kernels[p_] = {"bytes_per_unit": bpu.get(p_), "units_per_launch": u, "launches_per_step": lps,
+                       "ms_isolated": ms, "GBps_isolated": bpu[p_] * u / (ms * 1e-3) / 1e9 if p_ in bpu else None,
+                       "ms_overlapped": over.get(p_, (0, None))[1],
                        "pmc_traffic_bytes": tr,
                        "pmc_GBps_isolated": tr / (ms * 1e-3) / 1e9 if tr else None}
-    # measured HBM-side bytes of every kernel of a step (PMC summary) over the step's wall time
-    step_tr = [pmc_traffic(p) for p in over_ms]
-    step_traffic = sum(step_tr) if step_tr and all(t is not None for t in step_tr) else None
-    step_bytes = B * (per_unit_of("bloom_contains", mean_len_h, mean_len_b, k) + (mean_len_h + 12 + 2.5))
+    # chains against SURVEY 8(d)'s per-unit figures (53 B per PFADD element; len + 9 + 64(k-1) per contains)
+    s8 = {"pfadd": mean_len_h + 12 + 2.5, "bloom_contains": mean_len_b + 8 + 1 + 64 * (k - 1)}
+    chains = {}
+    for ch in CHAINS:
+        if ch not in iso:
+            continue
+        lps, ms = iso[ch]
+        u = upl[ch]
+        chains[ch] = {"s8d_bytes_per_unit": s8[ch], "units_per_launch": u, "ms_isolated": ms,
+                      "units_per_s_isolated": u / (ms * 1e-3),
+                      "s8d_GBps_isolated": s8[ch] * u / (ms * 1e-3) / 1e9,
+                      "s8d_frac_isolated": s8[ch] * u / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                      "ms_overlapped": over.get(ch, (0, None))[1]}
+    hll_ms = iso["pfadd"][1] if "pfadd" in iso else None
+    bl_ms = iso["bloom_contains"][1] if "bloom_contains" in iso else None
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(eng, args, h_off, h_bytes, ids, kid, len(mine), c_off, c_bytes, bloom, size, k, nsteps * B)
+        off, byt, _, _ = h_in[0]
+        coff, cbyt, _ = c_in[0]
+        cpu = cpu_baseline(eng, args, off, byt, ids, kid_all[0], len(mine), coff, cbyt, bloom, size, k,
+                           min(NH, CB))
 
     out = {
         "metric": "HLL inserts/sec + Bloom contains/sec (whole node)",
@@ -239,34 +268,27 @@ def main():
         "dtype": "u8/u64",
         "data": "synthetic: SplitMix64 Longs as Jackson bytes [\"java.lang.Long\",v] (mean %.1f B)" % mean_len_h,
         "config": {
-            "workload": "C2 PFADD 1 elem/cmd over %d tenants + C3 Bloom contains (m=%d, k=%d, filled with %d, "
-                        "50%% members), %d commands per batch each" % (args.tenants, size, k, fill, B),
-            "batch": B, "tenants": args.tenants, "bloom_bits": size, "bloom_k": k, "bloom_fill": fill,
-            "partitioner": "calcSlot(key) %% %d" % world,
+            "workload": "C2 PFADD 1 elem/cmd over %d tenants, %d RBatches of %d commands + C3 Bloom contains "
+                        "(m=%d, k=%d, filled with %d adds, 50%% members), %d elements, per step"
+                        % (args.tenants, HB, B, size, k, fill, CB),
+            "pfadd_batch": B, "pfadd_batches_per_step": HB, "contains_batch": CB, "tenants": args.tenants,
+            "bloom_bits": size, "bloom_k": k, "bloom_fill": fill, "partitioner": "calcSlot(key) %% %d" % world,
         },
-        # device-time rates of each chain run alone (roofline_isolated's launches), whole job
+        # device-time rates of each chain run alone, whole job
         "hll_inserts_per_s": B * world / (hll_ms * 1e-3) if hll_ms else None,
-        "bloom_contains_per_s": B * world / (bl_ms * 1e-3) if bl_ms else None,
+        "bloom_contains_per_s": CB * world / (bl_ms * 1e-3) if bl_ms else None,
         "bloom_add_per_s": fill / add_s if add_s else None,
         "device_ms_timed_region": dev_ms,
-        "kernel_ms_per_launch": over_ms,   # overlapped breakdown pass (same schedule as the timed region)
         "roofline": {"kernel": dom, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     # measured HBM-side bytes (PMC, 128-B lines per random probe) over the same launch time
                      "traffic_GBps": traffic / (avg_ms * 1e-3) / 1e9 if traffic else None,
-                     "traffic_frac": traffic / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS if traffic else None,
                      "traffic_source": "profiles/*_pmc_summary.json: 2 x FETCH_SIZE (gfx950) + WRITE_SIZE per launch",
-                     "bytes_per_unit": per_unit, "units_per_launch": B, "avg_launch_ms": avg_ms,
-                     "note": "avg launch of the dominant kernel, HIP events on its stream inside the timed region "
-                             "(PFADD and Bloom contains overlap on two streams)"},
+                     "bytes_per_unit": bpu[dom], "units_per_launch": upl.get(dom, B), "avg_launch_ms": avg_ms,
+                     "launches_timed": n_launch,
+                     "note": "dominant kernel = most device time per step, run alone; avg launch from HIP events "
+                             "on its stream inside the timed region; bytes per unit: DESIGN.md kernel table"},
         "kernels": kernels,
-        "roofline_isolated": {"kernel": dom, "achieved": iso_achieved, "peak": HBM_PEAK_GBS,
-                              "unit": "GB/s", "frac": iso_achieved / HBM_PEAK_GBS, "avg_launch_ms": iso_dom_ms,
-                              "traffic_GBps": iso_traffic / (iso_dom_ms * 1e-3) / 1e9 if iso_traffic else None,
-                              "kernel_ms_per_launch": iso_ms},
-        "step_algorithmic_GBps": step_bytes * K * world / wall / 1e9,
-        "step_traffic_bytes": step_traffic,
-        "step_traffic_GBps": step_traffic * K * world / wall / 1e9 if step_traffic else None,
+        "chains": chains,
         "cpu_baseline": cpu,
     }
     if rank == 0:
@@ -274,19 +296,27 @@ def main():
     eng.close()
 
 
-def per_unit_of(phase, mean_len_h, mean_len_b, k):
-    """Algorithmic bytes per unit (SURVEY 8d / DESIGN.md kernel table)."""
+def per_unit_bytes(mean_len_h, mean_len_b, k, size, CB, nr):
+    """Algorithmic bytes per unit of each kernel (DESIGN.md kernel table).  Random probes / register lines are
+    priced at one 64-B sector; streamed data at its bytes."""
+    P = k - 1
+    seg = 4.0 * nr / 4096            # segment table entry per hash block, per element
     return {
         "pfp_hash": mean_len_h + 8 + 4 + 8,            # key bytes + offset + slab id in, record out
         "pfp_apply": 8 + 64 + 64 + 1,                  # record + register sector load (R0) + store + reply
         "pfp_reply": 1 + 2 + 1,                        # chunk-order reply + chunk slot in, reply out
-        "pfadd_claim": mean_len_h + 8 + 4 + 1 + 8,     # key bytes + offset + slab id + register in, record out
-        "pfadd_commit": 8 + 1 + 1,                     # record in, register + reply out
-        "pfadd_hash": mean_len_h + 8 + 4 + 8,          # key bytes + offset + slab id in, sort key out
-        "pfadd_sort": 2 * 8 * 5,                       # 5 radix passes over 8-byte keys (read + write)
-        "pfadd_apply": 8 + 64 + 64 + 1,                # sorted key + register sector RMW + reply byte
-        "bloom_contains": mean_len_b + 8 + 1 + (k - 1) * 64,   # SURVEY 8d: len + 9 + (k-1)*64 B
-    }[phase]
+        "pfadd_claim": mean_len_h + 8 + 4 + 1 + 8,
+        "pfadd_commit": 8 + 1 + 1,
+        "pfadd_hash": mean_len_h + 8 + 4 + 8,
+        "pfadd_apply": 8 + 64 + 64 + 1,
+        "pfadd": mean_len_h + 12 + 2.5,                # SURVEY 8d PFADD element (53 B at C2)
+        # contains, one element per thread: SURVEY 8d (len + 9 + 64 B per decisive probe)
+        "bloom_contains": mean_len_b + 8 + 1 + 64 * P,
+        # region schedule: key + offset in, reply out, probe records + segment entries out
+        "bloom_rc_hash": mean_len_b + 8 + 1 + 4 * P + seg,
+        # records + segment entries in, the bit array streamed once per batch
+        "bloom_rc_probe": 4 * P + seg + (size / 8.0) / CB,
+    }
 
 
 def pmc_traffic(phase):
@@ -295,7 +325,8 @@ def pmc_traffic(phase):
 
     kern = {"bloom_contains": "sk::k_bloom_contains", "pfadd_claim": "sk::k_pfadd_claim",
             "pfadd_commit": "sk::k_pfadd_commit", "pfp_hash": "sk::k_pfp_hash", "pfp_apply": "sk::k_pfp_apply",
-            "pfp_reply": "sk::k_pfp_reply"}.get(phase)
+            "pfp_reply": "sk::k_pfp_reply", "bloom_rc_hash": "sk::k_bloom_rc_hash",
+            "bloom_rc_probe": "sk::k_bloom_rc_probe"}.get(phase)
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_summary.json")))
     if not kern or not files:
         return None
@@ -341,7 +372,7 @@ def cpu_baseline(eng, args, h_off, h_bytes, ids, kid, n_keys, c_off, c_bytes, bl
     assert np.array_equal(c1[:min(S1, ST)], cT[:min(S1, ST)]), "threaded oracle contains differs"
     return {"value": 2 * ST / (thT + tbT), "unit": "ops/s", "cores": T,
             "kind": "port",
-            "sample": "%d PFADD (same tenants/elements) + %d Bloom contains on the same filled filter, "
+            "sample": "%d PFADD (same tenants/elements) + %d Bloom contains on the same 1B-filled filter, "
                       "oracle/sketch_oracle.c on %d host threads (oracle_mt.c: a thread owns the keys id %% %d, "
                       "contains split in ranges)" % (ST, ST, T, T),
             "hll_inserts_per_s": ST / thT, "bloom_contains_per_s": ST / tbT,

@@ -224,7 +224,9 @@ int sk_timer_elapsed(sk_ctx *ctx, int slot_a, int slot_b, float *ms);
  * of a phase): "pfadd_hash", "pfadd_sort", "pfadd_apply", "hll_hist",
  * "hll_union", "bloom_contains", "bloom_probes", "bloom_sort", "bloom_apply",
  * "setbit", "getbit", "bitcount", "bitop", "pfadd_claim", "pfadd_commit",
- * "pfp_hash", "pfp_apply", "pfp_reply" */
+ * "pfp_hash", "pfp_apply", "pfp_reply", "bloom_rc_hash", "bloom_rc_probe";
+ * chains: "bloom_contains" (every kernel of one contains call), "pfadd" (every
+ * kernel of one sk_pfadd_dev batch) */
 int sk_prof_enable(sk_ctx *ctx, int on);
 /* time only the named phase while profiling is on (NULL: every phase) */
 int sk_prof_only(sk_ctx *ctx, const char *phase);

@@ -49,6 +49,16 @@ hipError_t launch_hll_union(hipStream_t st, uint64_t n, const uint32_t *ids, con
 hipError_t launch_bloom_contains(hipStream_t st, uint64_t n, const uint64_t *off, const uint8_t *bytes,
                                  const uint8_t *bits, const uint64_t *d_len, uint64_t size, uint64_t magic, int k,
                                  uint8_t *out, int sched, void *scratch = nullptr);
+// contains, region schedule (large batches): hash + bucket probes by 128 KiB region, then one LDS-resident
+// region per workgroup; records u32[rc_blocks(n) * rc_chunk_words(k)], S u32[rc_blocks(n) * rc_regions(size)]
+uint32_t rc_blocks(uint64_t n);
+uint32_t rc_regions(uint64_t size);
+uint32_t rc_max_probes();
+uint64_t rc_chunk_words(int k);
+hipError_t launch_bloom_rc_hash(hipStream_t st, uint64_t n, const uint64_t *off, const uint8_t *bytes, uint64_t size,
+                                uint64_t magic, int k, uint32_t *S, uint32_t *recs, uint8_t *out);
+hipError_t launch_bloom_rc_probe(hipStream_t st, uint64_t n, uint64_t size, int k, const uint32_t *S,
+                                 const uint32_t *recs, const uint8_t *bits, uint64_t cap_bytes, uint8_t *out);
 hipError_t launch_bloom_probes(hipStream_t st, uint64_t n, const uint64_t *off, const uint8_t *bytes, uint64_t size,
                                uint64_t magic, int k, uint64_t *keys);
 hipError_t launch_bloom_apply(hipStream_t st, uint64_t m, const uint64_t *keys, uint8_t *bits, uint64_t *d_len, int k,

@@ -961,6 +961,234 @@ __global__ void __launch_bounds__(256) k_bloom_contains_q(uint64_t n, const uint
     }
 }
 
+// ------------------------------------------- Bloom contains, region schedule
+// For large contains batches (n >> filter lines / probes) the one-element-
+// per-thread kernel pays one 128-B HBM line request per probe: the C3 array
+// (534 MB, ~4.2 M lines) sees ~1 probe per line per 1 M batch, so no line is
+// ever reused and the chip-wide random-request rate (~54 G/s) bounds it.
+// The region schedule turns the probes around: probes are bucketed by the
+// 128 KiB region of the bit array they fall in, and one workgroup per region
+// loads its region into LDS once (a coalesced stream) and answers every probe
+// of the batch that falls there from LDS.  HBM then sees the keys, the probe
+// records (4 B per probe, written and read once, coalesced) and the array once
+// per batch, instead of a line per probe.
+//   k_bloom_rc_hash   one 1024-thread workgroup per RC_EPB elements: XXH64 +
+//                     farmhashuo, the k-1 probes that decide contains (Q2),
+//                     an LDS counting sort of the block's probes by region,
+//                     stored as one coalesced chunk of u32 records
+//                     (bit-in-region << 12 | element-in-block) plus the
+//                     block's segment table S[block][region] = start|count<<16;
+//                     out[i] = 1 for every element.
+//   k_bloom_rc_probe  one 1024-thread workgroup per region: the region's
+//                     128 KiB into LDS, then the region's segment of every
+//                     block chunk; a probe on a 0 bit stores out[elem] = 0
+//                     (contains is the AND of its probes; every writer of an
+//                     element writes the same 0, so the order is free).
+// Regions of one XCD are consecutive (blockIdx % 8 -> XCD under round-robin
+// dispatch; speed only, never correctness): the ~32 workgroups an XCD runs at
+// once read neighbouring segments of each block chunk, which share lines.
+#define RC_RB 20                      // region = 2^20 bits = 128 KiB
+#define RC_TPB 1024
+#define RC_EPB 4096                   // elements per hash block (12-bit element-in-block)
+#define RC_PMAX 8                     // probes per element handled here (k <= 9)
+#define RC_NRMAX 4096                 // regions (bit arrays <= 2^32 bits)
+#define RC_ROUNDS (RC_EPB / RC_TPB)
+#define RC_BUFW 16384                 // u64 words: two key windows, then the block's records (RC_EPB*RC_PMAX u32)
+static_assert(2 * SK_PFP_WIN <= RC_BUFW && RC_EPB * RC_PMAX * 4 <= RC_BUFW * 8, "hash block LDS");
+static_assert(RC_EPB * RC_PMAX < 65536, "segment starts/counts are u16");
+static_assert(RC_TPB == SK_PFP_TPB, "key windows sized for SK_PFP_TPB threads");
+
+__global__ void __launch_bounds__(RC_TPB) k_bloom_rc_hash(uint64_t n, const uint64_t *__restrict__ off,
+                                                          const uint8_t *__restrict__ bytes, uint64_t size,
+                                                          uint64_t magic, uint32_t P, uint32_t NR,
+                                                          uint32_t *__restrict__ S, uint32_t *__restrict__ chunks,
+                                                          uint8_t *__restrict__ out) {
+    __shared__ uint32_t hist[RC_NRMAX];
+    __shared__ uint32_t wsum[RC_TPB / 64];
+    __shared__ uint64_t buf[RC_BUFW];
+    uint64_t *win[2] = {buf, buf + SK_PFP_WIN};
+    uint32_t *lrec = reinterpret_cast<uint32_t *>(buf); // after the last hash round
+    for (uint32_t r = threadIdx.x; r < NR; r += RC_TPB) hist[r] = 0;
+    const uint64_t base = uint64_t(blockIdx.x) * RC_EPB;
+    const uint64_t rounds = (n - base + RC_TPB - 1) / RC_TPB;
+    const int nr = rounds < RC_ROUNDS ? int(rounds) : RC_ROUNDS;
+    uint64_t wb[RC_ROUNDS + 1], oa[RC_ROUNDS], ob[RC_ROUNDS];
+#pragma unroll
+    for (int e = 0; e <= RC_ROUNDS; e++) {
+        uint64_t i0 = base + uint64_t(e) * RC_TPB;
+        wb[e] = off[i0 < n ? i0 : n];
+    }
+#pragma unroll
+    for (int e = 0; e < RC_ROUNDS; e++) {
+        uint64_t i = base + uint64_t(e) * RC_TPB + threadIdx.x;
+        oa[e] = ob[e] = 0;
+        if (i < n) {
+            oa[e] = off[i];
+            ob[e] = off[i + 1];
+        }
+    }
+    uint4 v[SK_PFP_WVEC];
+    if (pfp_win_fits(wb[0], wb[1])) {
+        pfp_win_load(bytes, wb[0], wb[1], v);
+        pfp_win_store(wb[0], wb[1], v, win[0]);
+    }
+    __syncthreads(); // hist zeroed, window 0 staged
+    // probe j of round e: bit index (< 2^32: sizes <= 4,294,967,294) and its rank in its region
+    uint32_t ix[RC_ROUNDS][RC_PMAX], rk[RC_ROUNDS][RC_PMAX / 2]; // u16 ranks, two per word
+#pragma unroll
+    for (int e = 0; e < RC_ROUNDS; e++) {
+#pragma unroll
+        for (int q = 0; q < RC_PMAX; q++) ix[e][q] = 0;
+#pragma unroll
+        for (int q = 0; q < RC_PMAX / 2; q++) rk[e][q] = 0;
+        if (e >= nr) continue; // uniform
+        bool pre = e + 1 < nr && pfp_win_fits(wb[e + 1], wb[e + 2]);
+        if (pre) pfp_win_load(bytes, wb[e + 1], wb[e + 2], v);
+        uint64_t i = base + uint64_t(e) * RC_TPB + threadIdx.x;
+        if (i < n) {
+            uint32_t len = uint32_t(ob[e] - oa[e]);
+            uint64_t h1, h2;
+            if (pfp_win_fits(wb[e], wb[e + 1])) {
+                LdsReader rd{win[e & 1], uint32_t(wb[e] & 15u) + uint32_t(oa[e] - wb[e])};
+                h1 = xxh64_r(rd, len);
+                h2 = farm_uo64_r(rd, len);
+            } else {
+                bloom_hashes(bytes + oa[e], len, &h1, &h2);
+            }
+            out[i] = 1;
+            uint64_t h = h1;
+#pragma unroll
+            for (int p = 0; p < RC_PMAX; p++) {
+                if (uint32_t(p) >= P) break;
+                uint32_t idx = uint32_t(mod_invariant(h & 0x7fffffffffffffffull, size, magic));
+                ix[e][p] = idx;
+                uint32_t rank = atomicAdd(&hist[idx >> RC_RB], 1u);
+                rk[e][p >> 1] |= rank << ((p & 1) * 16);
+                h += (p & 1) ? h1 : h2;
+            }
+        }
+        if (pre) pfp_win_store(wb[e + 1], wb[e + 2], v, win[(e + 1) & 1]);
+        __syncthreads(); // window e+1 staged; window e free for round e+2
+    }
+    // segment starts: 4 consecutive regions per thread
+    uint32_t c4[4], s4 = 0;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        uint32_t r = threadIdx.x * 4 + q;
+        c4[q] = r < NR ? hist[r] : 0u;
+        s4 += c4[q];
+    }
+    uint32_t tot;
+    uint32_t st = block_exscan<RC_TPB>(s4, wsum, &tot);
+    uint32_t *Sb = S + uint64_t(blockIdx.x) * NR;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        uint32_t r = threadIdx.x * 4 + q;
+        if (r < NR) {
+            hist[r] = st;
+            Sb[r] = st | (c4[q] << 16);
+        }
+        st += c4[q];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < RC_ROUNDS; e++) {
+        uint64_t i = base + uint64_t(e) * RC_TPB + threadIdx.x;
+        if (e >= nr || i >= n) continue;
+#pragma unroll
+        for (int p = 0; p < RC_PMAX; p++) {
+            if (uint32_t(p) >= P) break;
+            uint32_t idx = ix[e][p], rank = (rk[e][p >> 1] >> ((p & 1) * 16)) & 0xffffu;
+            lrec[hist[idx >> RC_RB] + rank] = (idx << 12) | (uint32_t(e) * RC_TPB + threadIdx.x);
+        }
+    }
+    __syncthreads();
+    uint4 *dst = reinterpret_cast<uint4 *>(chunks + uint64_t(blockIdx.x) * RC_EPB * P);
+    const uint4 *src = reinterpret_cast<const uint4 *>(lrec);
+    for (uint32_t t = threadIdx.x; t < (tot + 3) / 4; t += RC_TPB) dst[t] = src[t];
+}
+
+// regions of XCD group x = blockIdx % 8 are [x*q, (x+1)*q), taken in order
+__device__ __forceinline__ uint32_t rc_region(uint32_t b, uint32_t NR) {
+    uint32_t q = (NR + 7) / 8;
+    return (b & 7u) * q + (b >> 3);
+}
+
+// One thread per (block, region) segment, RC_JB blocks at once: the segment's
+// records are read as RC_SEGV aligned 16-B vectors (the segment starts at any
+// word), so a lane issues 4 vector loads instead of one load per record; a
+// segment that does not fit them (rare: > 13 records) finishes word by word.
+// The region's own stream is issued before the segment loads and lands in
+// LDS while they are in flight.
+#define RC_SEGV 4
+#define RC_JB 2
+__device__ __forceinline__ void rc_test(const uint8_t *fb, uint32_t x, uint8_t *ob) {
+    uint32_t bit = x >> 12;
+    if (!((fb[bit >> 3] >> (7u - (bit & 7u))) & 1u)) ob[x & 0xfffu] = 0;
+}
+__global__ void __launch_bounds__(RC_TPB) k_bloom_rc_probe(uint32_t NB, uint32_t NR, const uint32_t *__restrict__ S,
+                                                           const uint32_t *__restrict__ chunks, uint32_t P,
+                                                           const uint8_t *__restrict__ bits, uint64_t cap_bytes,
+                                                           uint8_t *__restrict__ out) {
+    __shared__ uint4 filt[(1u << (RC_RB - 3)) / 16];
+    constexpr uint32_t NV = (1u << (RC_RB - 3)) / 16, VPT = NV / RC_TPB;
+    const uint32_t r = rc_region(blockIdx.x, NR);
+    if (r >= NR) return; // uniform
+    const uint64_t b0 = uint64_t(r) << (RC_RB - 3);
+    const uint4 *src = reinterpret_cast<const uint4 *>(bits + b0);
+    uint4 fv[VPT];
+#pragma unroll
+    for (uint32_t q = 0; q < VPT; q++) { // bytes past the buffer read as 0 (they are past the string)
+        uint32_t v = threadIdx.x + q * RC_TPB;
+        fv[q] = b0 + uint64_t(v) * 16 < cap_bytes ? ld_nt(src + v) : make_uint4(0, 0, 0, 0);
+    }
+    const uint8_t *fb = reinterpret_cast<const uint8_t *>(filt);
+    const uint64_t CH = uint64_t(RC_EPB) * P;
+    const uint32_t iters = (NB + RC_TPB * RC_JB - 1) / (RC_TPB * RC_JB); // >= 1, the same for every thread
+    for (uint32_t it = 0; it < iters; it++) {
+        const uint32_t j0 = threadIdx.x + it * RC_TPB * RC_JB;
+        uint32_t seg[RC_JB];
+#pragma unroll
+        for (int u = 0; u < RC_JB; u++) {
+            uint32_t j = j0 + u * RC_TPB;
+            seg[u] = j < NB ? S[uint64_t(j) * NR + r] : 0u;
+        }
+        if (it == 0) { // the region lands in LDS while the first segment-table loads are in flight
+#pragma unroll
+            for (uint32_t q = 0; q < VPT; q++) filt[threadIdx.x + q * RC_TPB] = fv[q];
+        }
+        uint4 w[RC_JB][RC_SEGV];
+#pragma unroll
+        for (int u = 0; u < RC_JB; u++) {
+            uint32_t st = seg[u] & 0xffffu, cnt = seg[u] >> 16;
+            const uint4 *cv = reinterpret_cast<const uint4 *>(chunks + uint64_t(j0 + u * RC_TPB) * CH) + (st >> 2);
+            uint32_t nv = ((st & 3u) + cnt + 3u) >> 2; // vectors covering the segment
+#pragma unroll
+            for (int q = 0; q < RC_SEGV; q++) w[u][q] = uint32_t(q) < nv ? cv[q] : make_uint4(0, 0, 0, 0);
+        }
+        if (it == 0) __syncthreads();
+#pragma unroll
+        for (int u = 0; u < RC_JB; u++) {
+            const uint32_t j = j0 + u * RC_TPB, st = seg[u] & 0xffffu, cnt = seg[u] >> 16, o = st & 3u;
+            uint8_t *ob = out + uint64_t(j) * RC_EPB;
+            // word t of the vectors is a record of this segment iff o <= t < o + cnt
+            constexpr uint32_t NW = 4 * RC_SEGV;
+            const uint32_t end = o + cnt < NW ? o + cnt : NW, inreg = end - o;
+#pragma unroll
+            for (int q = 0; q < RC_SEGV; q++) {
+                if (4 * q >= o && 4 * q < end) rc_test(fb, w[u][q].x, ob);
+                if (4 * q + 1 >= o && 4 * q + 1 < end) rc_test(fb, w[u][q].y, ob);
+                if (4 * q + 2 >= o && 4 * q + 2 < end) rc_test(fb, w[u][q].z, ob);
+                if (4 * q + 3 >= o && 4 * q + 3 < end) rc_test(fb, w[u][q].w, ob);
+            }
+            if (cnt > inreg) { // long segment (rare): the rest word by word
+                const uint32_t *cs = chunks + uint64_t(j) * CH + st;
+                for (uint32_t s = inreg; s < cnt; s++) rc_test(fb, cs[s], ob);
+            }
+        }
+    }
+}
+
 // add, pass 1: all k probes -> key = idx << 32 | (elem*k + j)
 __global__ void __launch_bounds__(256) k_bloom_probes(uint64_t n, const uint64_t *__restrict__ off,
                                                       const uint8_t *__restrict__ bytes, uint64_t size,
@@ -1516,6 +1744,30 @@ hipError_t launch_bloom_contains(hipStream_t st, uint64_t n, const uint64_t *off
     else // one element per thread
         hipLaunchKernelGGL(k_bloom_contains, dim3(grid_for(n, 256)), dim3(256), 0, st, n, off,
                            bytes, bits, d_len, size, magic, k, out);
+    SK_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+uint32_t rc_blocks(uint64_t n) { return uint32_t((n + RC_EPB - 1) / RC_EPB); }
+uint32_t rc_regions(uint64_t size) { return uint32_t((size + (1ull << RC_RB) - 1) >> RC_RB); }
+uint32_t rc_max_probes() { return RC_PMAX; }
+uint64_t rc_chunk_words(int k) { return uint64_t(RC_EPB) * uint64_t(k - 1); }
+
+// region schedule: records u32[blocks * RC_EPB * (k-1)], S u32[blocks * regions]
+hipError_t launch_bloom_rc_hash(hipStream_t st, uint64_t n, const uint64_t *off, const uint8_t *bytes, uint64_t size,
+                                uint64_t magic, int k, uint32_t *S, uint32_t *recs, uint8_t *out) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k_bloom_rc_hash, dim3(rc_blocks(n)), dim3(RC_TPB), 0, st, n, off, bytes, size, magic,
+                       uint32_t(k - 1), rc_regions(size), S, recs, out);
+    SK_LAUNCH_CHECK();
+    return hipSuccess;
+}
+hipError_t launch_bloom_rc_probe(hipStream_t st, uint64_t n, uint64_t size, int k, const uint32_t *S,
+                                 const uint32_t *recs, const uint8_t *bits, uint64_t cap_bytes, uint8_t *out) {
+    if (!n) return hipSuccess;
+    uint32_t NR = rc_regions(size);
+    hipLaunchKernelGGL(k_bloom_rc_probe, dim3(8 * ((NR + 7) / 8)), dim3(RC_TPB), 0, st, rc_blocks(n), NR, S, recs,
+                       uint32_t(k - 1), bits, cap_bytes, out);
     SK_LAUNCH_CHECK();
     return hipSuccess;
 }

@@ -250,6 +250,8 @@ struct sk_ctx {
     uint32_t *d_zero = nullptr; // device u32[4] zeros: id 0 / empty length
     DBuf keys_a, keys_b, vals_a, vals_b, sort_tmp, in_off, in_bytes, in_ids, in_cmd, out_u8, misc, partial, hist,
         uni, ptrs, hist_a, hist_b, ovf, bloom_h;
+    DBuf rc_S, rc_rec;          // Bloom contains region schedule: segment table + probe records (contains only)
+    uint64_t bloom_rc_min = 2u << 20; // contains batches >= this use the region schedule (SK_BLOOM_RC_MIN, 0 = never)
 };
 
 namespace {
@@ -309,7 +311,7 @@ int pfadd_settle(sk_ctx *c); // defined with the PFADD core
 const char *kPhaseNames[] = {"pfadd_hash",  "pfadd_sort",   "pfadd_apply", "hll_hist",     "hll_union",
                              "bloom_contains", "bloom_probes", "bloom_sort", "bloom_apply", "setbit",
                              "getbit",      "bitcount",     "bitop",       "pfadd_claim", "pfadd_commit",
-                             "pfp_hash",    "pfp_apply",    "pfp_reply"};
+                             "pfp_hash",    "pfp_apply",    "pfp_reply",   "bloom_rc_hash", "bloom_rc_probe", "pfadd"};
 constexpr int kNumPhases = sizeof(kPhaseNames) / sizeof(kPhaseNames[0]);
 
 hipEvent_t ev_get(sk_ctx *c) {
@@ -843,6 +845,7 @@ int sk_open(const sk_config *cfg, sk_ctx **out) {
     if (const char *e = getenv("SK_PFADD_CLAIM")) c->claim_all = atoi(e);
     if (const char *e = getenv("SK_PFADD_PATH")) c->pfadd_path = atoi(e);
     if (const char *e = getenv("SK_PFP_DIRECT")) c->pfp_direct = atoi(e) != 0;
+    if (const char *e = getenv("SK_BLOOM_RC_MIN")) c->bloom_rc_min = strtoull(e, nullptr, 10);
     uint64_t cap = (cfg && cfg->hll_capacity) ? cfg->hll_capacity : 1024;
     if (hll_grow(c, cap) != SK_OK || c->misc.ensure(4096) != hipSuccess ||
         hipMalloc(&c->d_zero, 16) != hipSuccess || hipMemsetAsync(c->d_zero, 0, 16, c->st) != hipSuccess ||
@@ -861,6 +864,7 @@ int sk_close(sk_ctx *c) {
     (void)hipSetDevice(c->device);
     if (c->pf_pending) (void)pfadd_settle(c);
     if (c->st) (void)hipStreamSynchronize(c->st);
+    if (c->st2) (void)hipStreamSynchronize(c->st2);
     if (c->comm) (void)ncclCommDestroy(c->comm);
     prof_collect(c);
     for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
@@ -875,9 +879,8 @@ int sk_close(sk_ctx *c) {
     if (c->h_cnt) (void)hipHostFree(c->h_cnt);
     for (DBuf *b : {&c->keys_a, &c->keys_b, &c->vals_a, &c->vals_b, &c->sort_tmp, &c->in_off, &c->in_bytes,
                     &c->in_ids, &c->in_cmd, &c->out_u8, &c->misc, &c->partial, &c->hist, &c->uni, &c->ptrs,
-                    &c->hist_a, &c->hist_b, &c->ovf, &c->bloom_h})
+                    &c->hist_a, &c->hist_b, &c->ovf, &c->bloom_h, &c->rc_S, &c->rc_rec})
         b->release();
-    if (c->st2) (void)hipStreamSynchronize(c->st2);
     if (c->ev_w) (void)hipEventDestroy(c->ev_w);
     if (c->ev_r) (void)hipEventDestroy(c->ev_r);
     if (c->st2) (void)hipStreamDestroy(c->st2);
@@ -1215,6 +1218,7 @@ int sk_pfadd_dev(sk_ctx *c, uint64_t n, const uint32_t *d_ids, const uint64_t *d
         uint64_t live = c->hll_next - c->hll_free.size(); // slabs in use bounds the touched sketches
         if (pfadd_uses_sort(c, m, live))
             HIPCHK(c, hipMemsetAsync(d_changed + s, 0, m, c->st)); // the sorted path sets only the 1s
+        Prof p_(c, 20); // the whole PFADD chain of this batch
         int r = pfadd_device(c, m, d_ids + s, d_off + s, d_bytes, nullptr, m, d_changed + s, live);
         if (r) return r;
     }
@@ -1909,6 +1913,40 @@ static int bloom_add_device(sk_ctx *c, uint32_t id, int64_t size, int32_t k, uin
     return SK_OK;
 }
 
+// RBloomFilter.contains of n device elements on stream s (d_out: one reply per element).  Large batches take the
+// region schedule (sk_kernels.hip "Bloom contains, region schedule"), in pieces of <= 32 M elements so the probe
+// records stay bounded (4 B per probe); small batches and missing filters the one-element-per-thread kernel.
+static int bloom_contains_launch(sk_ctx *c, hipStream_t s, uint32_t id, int64_t size, int32_t k, uint64_t n,
+                                 const uint64_t *d_off, const uint8_t *d_bytes, uint8_t *d_out) {
+    if (!n) return SK_OK;
+    const uint64_t usize = uint64_t(size), magic = magic_for(usize);
+    const bool region = id != kNoId && c->bloom_rc_min && n >= c->bloom_rc_min && k >= 2 &&
+                        uint32_t(k - 1) <= sk::rc_max_probes() && sk::rc_regions(usize) >= 64;
+    Prof p_(c, 5, s);
+    if (!region) {
+        const uint8_t *bits = id == kNoId ? reinterpret_cast<const uint8_t *>(c->d_zero) : c->strs[id].ptr;
+        const uint64_t *dl = id == kNoId ? reinterpret_cast<const uint64_t *>(c->d_zero) : &c->d_dir[id].len;
+        if (c->bloom_sched == 3) HIPCHK(c, c->bloom_h.ensure(16 * n));
+        HIPCHK(c, sk::launch_bloom_contains(s, n, d_off, d_bytes, bits, dl, usize, magic, k, d_out, c->bloom_sched,
+                                            c->bloom_h.p));
+        return SK_OK;
+    }
+    const uint64_t piece = uint64_t(32) << 20;
+    const uint64_t nb = sk::rc_blocks(std::min(n, piece)), nr = sk::rc_regions(usize);
+    HIPCHK(c, c->rc_S.ensure(nb * nr * 4));
+    HIPCHK(c, c->rc_rec.ensure(nb * sk::rc_chunk_words(k) * 4));
+    for (uint64_t s0 = 0; s0 < n; s0 += piece) {
+        uint64_t m = std::min(piece, n - s0);
+        { Prof q_(c, 18, s);
+        HIPCHK(c, sk::launch_bloom_rc_hash(s, m, d_off + s0, d_bytes, usize, magic, k, c->rc_S.as<uint32_t>(),
+                                           c->rc_rec.as<uint32_t>(), d_out + s0)); }
+        { Prof q_(c, 19, s);
+        HIPCHK(c, sk::launch_bloom_rc_probe(s, m, usize, k, c->rc_S.as<uint32_t>(), c->rc_rec.as<uint32_t>(),
+                                            c->strs[id].ptr, c->strs[id].cap, d_out + s0)); }
+    }
+    return SK_OK;
+}
+
 static int bloom_prepare(sk_ctx *c, const std::string &nm, int64_t size, int32_t k, bool create, uint32_t *id) {
     BloomCfg *b;
     int r = bloom_cfg(c, nm, &b);
@@ -1957,12 +1995,9 @@ int sk_bloom_contains(sk_ctx *c, const uint8_t *name, uint64_t len, int64_t size
     if (r || !n) return r;
     if ((r = stage_elems(c, n, off, bytes))) return r;
     HIPCHK(c, c->out_u8.ensure(n));
-    if (c->bloom_sched == 3) HIPCHK(c, c->bloom_h.ensure(16 * uint64_t(n)));
-    const uint8_t *bits = id == kNoId ? reinterpret_cast<const uint8_t *>(c->d_zero) : c->strs[id].ptr;
-    const uint64_t *dl = id == kNoId ? reinterpret_cast<const uint64_t *>(c->d_zero) : &c->d_dir[id].len;
-    HIPCHK(c, sk::launch_bloom_contains(c->st, n, c->in_off.as<uint64_t>(), c->in_bytes.as<uint8_t>(), bits, dl,
-                                        uint64_t(size), magic_for(uint64_t(size)), k, c->out_u8.as<uint8_t>(), c->bloom_sched,
-                                        c->bloom_h.p));
+    if ((r = bloom_contains_launch(c, c->st, id, size, k, n, c->in_off.as<uint64_t>(), c->in_bytes.as<uint8_t>(),
+                                   c->out_u8.as<uint8_t>())))
+        return r;
     HIPCHK(c, hipMemcpyAsync(out, c->out_u8.p, n, hipMemcpyDeviceToHost, c->st));
     return sync(c);
 }
@@ -1993,8 +2028,6 @@ int sk_bloom_contains_dev(sk_ctx *c, const uint8_t *name, uint64_t len, uint64_t
     if (r) return r;
     uint32_t id;
     if ((r = bloom_prepare(c, nm, b->size, b->k, false, &id))) return r;
-    const uint8_t *bits = id == kNoId ? reinterpret_cast<const uint8_t *>(c->d_zero) : c->strs[id].ptr;
-    const uint64_t *dl = id == kNoId ? reinterpret_cast<const uint64_t *>(c->d_zero) : &c->d_dir[id].len;
     // async: run on the read stream after every main-stream write of bit strings
     bool rs = c->async_dev && c->read_stream;
     hipStream_t s = rs ? c->st2 : c->st;
@@ -2003,10 +2036,7 @@ int sk_bloom_contains_dev(sk_ctx *c, const uint8_t *name, uint64_t len, uint64_t
         HIPCHK(c, hipStreamWaitEvent(c->st2, c->ev_w, 0));
         c->st_wrote_bits = false;
     }
-    if (c->bloom_sched == 3) HIPCHK(c, c->bloom_h.ensure(16 * n));
-    { Prof p_(c, 5, s);
-    HIPCHK(c, sk::launch_bloom_contains(s, n, d_off, d_bytes, bits, dl, uint64_t(b->size),
-                                        magic_for(uint64_t(b->size)), b->k, d_out, c->bloom_sched, c->bloom_h.p)); }
+    if ((r = bloom_contains_launch(c, s, id, b->size, b->k, n, d_off, d_bytes, d_out))) return r;
     if (rs) {
         HIPCHK(c, hipEventRecord(c->ev_r, c->st2));
         c->rd_pending = true;

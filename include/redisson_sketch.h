@@ -49,6 +49,8 @@ extern "C" {
 #define SK_ETOOBIG (-9)    /* "Bloom filter can't be greater than 4294967294. ..." (IllegalArgumentException, :72-74) */
 #define SK_ECORRUPT (-10)  /* "INVALIDOBJ Corrupted HLL object detected" (a SET string with the HYLL magic
                               whose registers do not decode) */
+#define SK_ESTALE (-11)    /* a caller-cached HLL slab id (sk_pfadd_ids / sk_pfcount_ids) whose key was deleted,
+                              replaced or flushed: drop the cached id and resolve the key by name again */
 
 #define SK_TYPE_NONE 0
 #define SK_TYPE_HLL 1    /* string holding a HyperLogLog (PFADD/PFMERGE created it) */
@@ -121,8 +123,9 @@ int sk_pfadd(sk_ctx *ctx, uint32_t n_cmds, const uint64_t *key_off, const uint8_
 /* sk_pfadd with keys pre-resolved to slab ids by sk_hll_resolve (the Java
  * executor caches name -> id per tenant, SURVEY 8(b) "key names resolved to
  * slab ids on the Java side"); host buffers, same replies.  An id is valid
- * until its key is deleted (DEL / flushall): the caller drops its cached ids
- * then.  Ids never handed out fail with SK_EINVAL.  Replaces the PFADD
+ * while its key owns the slab: after DEL, SET, a BITOP / flushall that
+ * replaced the key, the call fails with SK_ESTALE (nothing is written) and
+ * the caller drops its cached id and resolves the name again.  Replaces the PFADD
  * round trip of M:RedissonHyperLogLog.java:66-68 / M:RedissonBatch.java:76-83. */
 int sk_pfadd_ids(sk_ctx *ctx, uint32_t n_cmds, const uint32_t *key_ids, const uint32_t *elem_counts,
                  const uint64_t *elem_off, const uint8_t *elem_bytes, uint8_t *out_changed);
@@ -137,7 +140,7 @@ int sk_pfcount(sk_ctx *ctx, uint32_t n_cmds, const uint32_t *nkeys, const uint64
 /* RHyperLogLog.count (M:RedissonHyperLogLog.java:78-81) of n keys given by
  * slab ids from sk_hll_resolve (cached by the caller, as for sk_pfadd_ids):
  * out[i] = PFCOUNT of key_ids[i].  One histogram launch, estimates on host
- * threads.  Ids never handed out fail with SK_EINVAL. */
+ * threads.  Ids no key holds fail with SK_ESTALE (as for sk_pfadd_ids). */
 int sk_pfcount_ids(sk_ctx *ctx, uint64_t n, const uint32_t *key_ids, int64_t *out);
 /* per-key 64-bin register histograms for slab ids (device in / device out u32[n*64]) */
 int sk_hll_histogram_dev(sk_ctx *ctx, uint64_t n, const uint32_t *d_key_ids, uint32_t *d_hist);

@@ -22,6 +22,8 @@ SK_EINVAL = -6
 SK_ENOMEM = -7
 SK_ESYNTAX = -8
 SK_ETOOBIG = -9
+SK_ECORRUPT = -10
+SK_ESTALE = -11
 
 SK_TYPE_NONE, SK_TYPE_HLL, SK_TYPE_STRING, SK_TYPE_HASH = 0, 1, 2, 3
 SK_BITOP = {"AND": 0, "OR": 1, "XOR": 2, "NOT": 3}

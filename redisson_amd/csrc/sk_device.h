@@ -18,6 +18,10 @@
 
 namespace sk {
 
+// HLL slab handles from sk_hll_resolve carry the slab's generation in the top 8 bits (stale caller-cached ids
+// are rejected by the host entry points); kernels index the arena with the low 24 bits
+#define SK_SLAB_MASK 0xffffffu
+
 __device__ __forceinline__ uint64_t funnel(uint64_t lo, uint64_t hi, unsigned sh) {
     // (lo >> sh) | (hi << (64 - sh)), correct for sh == 0 (two shifts < 64)
     return (lo >> sh) | ((hi << 1) << (63 - sh));

@@ -52,7 +52,7 @@ __global__ void __launch_bounds__(256) k_pfadd_hash(uint64_t n, const uint32_t *
     uint32_t reg, rho;
     hll_pat(h, v5, &reg, &rho);
     uint64_t cmd = cmd_of ? cmd_of[i] : i;
-    uint64_t slot = (uint64_t(key_ids[i]) << 14) | reg;
+    uint64_t slot = (uint64_t(key_ids[i] & SK_SLAB_MASK) << 14) | reg;
     out_keys[i] = (slot << slot_shift) | (cmd << 6) | rho;
 }
 
@@ -117,7 +117,7 @@ __global__ void __launch_bounds__(256) k_pfadd_claim(uint64_t n, const uint32_t 
                         : murmur64a(bytes + o, len, 0xadc83b19ull);
     uint32_t reg, rho;
     hll_pat(h, v5, &reg, &rho);
-    uint64_t slot = (uint64_t(key_ids[i]) << 14) | reg;
+    uint64_t slot = (uint64_t(key_ids[i] & SK_SLAB_MASK) << 14) | reg;
     uint8_t *p = arena + slot;
     uint32_t sh = uint32_t(slot & 3) * 8u;
     uint32_t *w = reinterpret_cast<uint32_t *>(arena + (slot & ~uint64_t(3)));
@@ -381,7 +381,7 @@ __global__ void __launch_bounds__(SK_PFP_TPB) k_pfp_hash(uint64_t n, const uint3
         if (i < n) {
             oa[e] = off[i];
             ob[e] = off[i + 1];
-            kid[e] = key_ids[i];
+            kid[e] = key_ids[i] & SK_SLAB_MASK;
         }
     }
     uint4 v[SK_PFP_WVEC];
@@ -673,7 +673,7 @@ __global__ void __launch_bounds__(SK_HH_TPB) k_hll_hist(uint64_t n, const uint32
     const unsigned t = threadIdx.x, bin = t & 63u, q = t >> 6;
     for (int b = 0; b < 32; b++) h[b][t] = 0;
     auto load = [&](uint64_t key, uint4 (&v)[4]) {
-        const uint4 *base = reinterpret_cast<const uint4 *>(arena + (uint64_t(ids[key]) << 14));
+        const uint4 *base = reinterpret_cast<const uint4 *>(arena + (uint64_t(ids[key] & SK_SLAB_MASK) << 14));
 #pragma unroll
         for (int it = 0; it < 4; it++) v[it] = ld_nt(base + it * SK_HH_TPB + t);
     };
@@ -744,7 +744,7 @@ __global__ void __launch_bounds__(256) k_hll_union_partial(uint64_t n, const uin
     if (k1 > n) k1 = n;
     uint4 acc = make_uint4(0, 0, 0, 0);
     uint64_t k = k0;
-#define SK_SRC(kk) (reinterpret_cast<const uint4 *>(base + ((ids ? uint64_t(ids[kk]) : uint64_t(kk)) << 14)))
+#define SK_SRC(kk) (reinterpret_cast<const uint4 *>(base + ((ids ? uint64_t(ids[kk] & SK_SLAB_MASK) : uint64_t(kk)) << 14)))
     for (; k + 8 <= k1; k += 8) { // 8 independent 16 B loads in flight per lane
         uint4 a0 = ld_nt(SK_SRC(k) + lane16),
               a1 = ld_nt(SK_SRC(k + 1) + lane16),

@@ -57,10 +57,13 @@ struct DBuf {
     size_t cap = 0;
     hipError_t ensure(size_t bytes) {
         if (bytes <= cap) return hipSuccess;
-        // 1/8 headroom in 2 MiB steps: batches of slightly varying size do not reallocate (a hipFree
-        // synchronises the device and cost 28 ms once with a large keyspace resident)
-        size_t nc = std::max(bytes + bytes / 8, cap * 2);
-        nc = (nc + (size_t(2) << 20) - 1) & ~((size_t(2) << 20) - 1);
+        // large buffers: 1/8 headroom in 2 MiB steps, so batches of slightly varying size do not reallocate (a
+        // hipFree synchronises the device and cost 28 ms once with a large keyspace resident); small ones exact
+        size_t nc = bytes;
+        if (bytes >= (size_t(1) << 20)) {
+            nc = std::max(bytes + bytes / 8, cap * 2);
+            nc = (nc + (size_t(2) << 20) - 1) & ~((size_t(2) << 20) - 1);
+        }
         if (p) {
             hipError_t e = hipFree(p);
             if (e != hipSuccess) return e;
@@ -198,6 +201,8 @@ struct sk_ctx {
     uint8_t *arena = nullptr;
     uint64_t hll_cap = 0, hll_next = 0;
     std::vector<uint32_t> hll_free;
+    std::vector<uint8_t> hll_live; // slab id -> 1 while a key owns it (caller-cached ids are checked against it)
+    std::vector<uint8_t> hll_gen;  // slab id -> generation, bumped when the slab is freed (top byte of a handle)
     std::vector<uint64_t> h_e0, h_off; // host PFADD staging, kept across calls (no page faults per batch)
 
     // strings: host mirror of {ptr, cap}; len lives in the device directory
@@ -381,12 +386,29 @@ int hll_alloc(sk_ctx *c, uint32_t *id) {
     if (!c->hll_free.empty()) {
         *id = c->hll_free.back();
         c->hll_free.pop_back();
-        return SK_OK;
+    } else {
+        if (c->hll_next >= (uint64_t(1) << 24))
+            return fail(c, SK_ENOMEM, "too many HLL keys: %llu slabs (2^24 per context)", (unsigned long long)c->hll_next);
+        int r = hll_grow(c, c->hll_next + 1);
+        if (r) return r;
+        *id = uint32_t(c->hll_next++);
     }
-    int r = hll_grow(c, c->hll_next + 1);
-    if (r) return r;
-    *id = uint32_t(c->hll_next++);
+    if (c->hll_live.size() <= *id) {
+        size_t n = std::max<size_t>(*id + 1, c->hll_live.size() * 2);
+        c->hll_live.resize(n, 0);
+        c->hll_gen.resize(n, 0);
+    }
+    c->hll_live[*id] = 1;
     return SK_OK;
+}
+// Caller-cached handles (sk_hll_resolve -> sk_pfadd_ids / sk_pfcount_ids) = slab | generation << 24: usable only
+// while the key that was resolved still owns the slab (a DEL / SET / BITOP / flushall frees it and bumps the
+// generation, so a handle cached across that -- even with the slab handed to another key -- is refused).
+constexpr uint32_t kSlabMask = 0xffffffu;
+uint32_t hll_handle(const sk_ctx *c, uint32_t id) { return id | (uint32_t(c->hll_gen[id]) << 24); }
+bool hll_handle_live(const sk_ctx *c, uint32_t h) {
+    uint32_t id = h & kSlabMask;
+    return id < c->hll_live.size() && c->hll_live[id] && c->hll_gen[id] == (h >> 24);
 }
 
 int str_len(sk_ctx *c, uint32_t id, uint64_t *len);
@@ -586,6 +608,8 @@ int del_key(sk_ctx *c, const std::string &k, bool *removed) {
     *removed = true;
     if (e.type == SK_TYPE_HLL) {
         HIPCHK(c, hipMemsetAsync(c->arena + uint64_t(e.id) * kHllBytes, 0, kHllBytes, c->st));
+        c->hll_live[e.id] = 0;
+        c->hll_gen[e.id] = uint8_t(c->hll_gen[e.id] + 1);
         c->hll_free.push_back(e.id);
         return SK_OK;
     }
@@ -812,6 +836,7 @@ const char *sk_strerror(int s) {
     case SK_ESYNTAX: return "ERR BITOP NOT must be called with a single source key.";
     case SK_ETOOBIG: return "Bloom filter can't be greater than 4294967294";
     case SK_ECORRUPT: return "INVALIDOBJ Corrupted HLL object detected";
+    case SK_ESTALE: return "stale HLL slab id: resolve the key again";
     default: return "unknown";
     }
 }
@@ -1008,6 +1033,7 @@ int sk_hll_resolve(sk_ctx *c, uint32_t n, const uint64_t *off, const uint8_t *by
         bool cr;
         int r = hll_get(c, key_at(off, bytes, i), true, &ids[i], &cr);
         if (r) return r;
+        ids[i] = hll_handle(c, ids[i]);
         if (created) created[i] = cr;
     }
     return sync(c);
@@ -1196,8 +1222,9 @@ int sk_pfadd_ids(sk_ctx *c, uint32_t n_cmds, const uint32_t *key_ids, const uint
     ENTER(c);
     if (!n_cmds) return SK_OK;
     for (uint32_t i = 0; i < n_cmds; i++)
-        if (key_ids[i] >= c->hll_next)
-            return fail(c, SK_EINVAL, "PFADD: slab id %u was never resolved", key_ids[i]);
+        if (!hll_handle_live(c, key_ids[i]))
+            return fail(c, SK_ESTALE, "PFADD: slab id %u is not held by a key (deleted, replaced or never resolved)",
+                        key_ids[i]);
     return pfadd_host_batch(c, n_cmds, key_ids, nullptr, elem_counts, elem_off, elem_bytes, out_changed);
 }
 
@@ -1264,7 +1291,7 @@ static int estimate_many(sk_ctx *c, uint64_t n, const uint32_t *h, const uint32_
     for (uint64_t i = 0; i < n; i++) {
         if (!slow[i]) continue;
         int rc;
-        out[i] = int64_t(estimate_host(c, h + i * 64, c->arena + uint64_t(ids[i]) * kHllBytes, false, &rc));
+        out[i] = int64_t(estimate_host(c, h + i * 64, c->arena + uint64_t(ids[i] & kSlabMask) * kHllBytes, false, &rc));
         if (rc) return rc;
     }
     return SK_OK;
@@ -1275,8 +1302,9 @@ int sk_pfcount_ids(sk_ctx *c, uint64_t n, const uint32_t *key_ids, int64_t *out)
     ENTER(c);
     if (!n) return SK_OK;
     for (uint64_t i = 0; i < n; i++)
-        if (key_ids[i] >= c->hll_next)
-            return fail(c, SK_EINVAL, "PFCOUNT: slab id %u was never resolved", key_ids[i]);
+        if (!hll_handle_live(c, key_ids[i]))
+            return fail(c, SK_ESTALE, "PFCOUNT: slab id %u is not held by a key (deleted, replaced or never resolved)",
+                        key_ids[i]);
     HIPCHK(c, c->in_ids.ensure(n * 4));
     HIPCHK(c, hipMemcpyAsync(c->in_ids.p, key_ids, n * 4, hipMemcpyHostToDevice, c->st));
     std::vector<uint32_t> h;
@@ -1319,7 +1347,7 @@ int sk_pfcount(sk_ctx *c, uint32_t n_cmds, const uint32_t *nkeys, const uint64_t
                 kb.assign(reinterpret_cast<const char *>(key_bytes + key_off[k]), key_off[k + 1] - key_off[k]);
                 r = hll_get(c, kb, false, &id, nullptr);
             }
-            if (r == SK_EWRONGTYPE) {
+            if (r == SK_EWRONGTYPE || r == SK_ECORRUPT) { // that command alone fails, as in a pipeline
                 bad[cmd] = 1;
                 status = r;
                 continue;

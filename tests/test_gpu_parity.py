@@ -404,7 +404,7 @@ def test_pfadd_partition_oversized_buckets(engine, O):
     kids, els = [], []
     for target in (5, 300):
         kk, rr = np.meshgrid(np.arange(nkeys, dtype=np.uint64), np.arange(16384, dtype=np.uint64), indexing="ij")
-        slots = (ids[kk.astype(np.int64)].astype(np.uint64) << np.uint64(14)) | rr
+        slots = ((ids[kk.astype(np.int64)] & 0xFFFFFF).astype(np.uint64) << np.uint64(14)) | rr
         hit = np.argwhere(_pfp_bucket(slots) == target)
         for ki, r in hit:
             cand = by_reg.get(int(r), [])
@@ -596,7 +596,7 @@ def test_pfadd_multi_launch_zipf(engine, O):
 def test_pfadd_ids_matches_names_and_oracle(O):
     """sk_pfadd_ids (slab ids from sk_hll_resolve, host buffers) gives the oracle's replies and registers, for
     one-element commands (the shipped-as-is chunk), multi-element and empty commands (the re-packed chunk) and a
-    batch split into several device batches (max_batch); an id never handed out fails with SK_EINVAL."""
+    batch split into several device batches (max_batch); an id never handed out fails with SK_ESTALE."""
     from redisson_amd import SketchEngine
     from redisson_amd.engine import RedisException
     e = SketchEngine(device=0, max_batch=3000)
@@ -621,7 +621,7 @@ def test_pfadd_ids_matches_names_and_oracle(O):
         cmds3 = [[x] for x in _elems(0x5EED0405, 4000)]
         kid3 = rng.integers(0, len(names), 4000)
         assert e.pfadd([names[k] for k in kid3], cmds3) == ref.pfadd([names[k] for k in kid3], cmds3)
-        with pytest.raises(RedisException, match="never resolved"):
+        with pytest.raises(RedisException, match="not held by a key"):
             e.pfadd_ids(np.array([1 << 20], dtype=np.uint32), [[b"x"]])
     finally:
         e.close()
@@ -681,7 +681,7 @@ def test_pfcount_ids_many_keys(O):
                [[names[a], names[b], b"absent:%d" % a] for a, b in pairs]
         exp = want * 2 + [0] + [O.count_regs(np.maximum(regs[a], regs[b]), 2) for a, b in pairs]
         assert e.pfcount(cmds) == exp
-        with pytest.raises(RedisException, match="never resolved"):
+        with pytest.raises(RedisException, match="not held by a key"):
             e.pfcount_ids(np.array([1 << 22], dtype=np.uint32))
     finally:
         e.close()
@@ -703,3 +703,40 @@ def test_pfadd_mixed_batch_wrongtype_skips_one_command(engine, O):
     ref.pfadd([keys[i] for i in keep], [cmds[i] for i in keep])
     for k in set(keys) - {b"mx:str"}:
         np.testing.assert_array_equal(engine.hll_registers(k), ref.regs[k])
+
+
+def test_stale_slab_id_rejected(O):
+    """a cached slab handle whose key was deleted (or replaced by SET, or flushed) is rejected with
+    SK_ESTALE and writes nothing, even after another key reuses the slab (the handle's generation byte differs);
+    resolving the name again works."""
+    from redisson_amd import SketchEngine
+    from redisson_amd.engine import RedisException
+    e = SketchEngine(device=0)
+    try:
+        [old] = e.hll_resolve([b"st:a"])
+        assert e.pfadd_ids(np.array([old], np.uint32), [[b"x1"]]) == [1]
+        assert e.delete([b"st:a"]) == 1
+        [new] = e.hll_resolve([b"st:b"])          # the freed slab is handed out again, one generation on
+        assert new & 0xFFFFFF == old & 0xFFFFFF and new != old
+        before = e.hll_registers(b"st:b").copy()
+        assert not before.any()
+        with pytest.raises(RedisException, match="not held by a key"):
+            e.pfadd_ids(np.array([old], np.uint32), [[b"x2"]])
+        with pytest.raises(RedisException, match="not held by a key"):
+            e.pfcount_ids(np.array([old], np.uint32))
+        np.testing.assert_array_equal(e.hll_registers(b"st:b"), before)
+        # the id is live again through its new owner
+        assert e.pfadd_ids(np.array([new], np.uint32), [[b"x3"]]) == [1]
+        ref = O.HLLStore()
+        ref.pfadd([b"st:b"], [[b"x3"]])
+        np.testing.assert_array_equal(e.hll_registers(b"st:b"), ref.regs[b"st:b"])
+        # SET over the HLL and FLUSHALL free the slab too
+        e.set(b"st:b", b"plain")
+        with pytest.raises(RedisException, match="not held by a key"):
+            e.pfadd_ids(np.array([new], np.uint32), [[b"x4"]])
+        [c] = e.hll_resolve([b"st:c"])
+        e.flushall()
+        with pytest.raises(RedisException, match="not held by a key"):
+            e.pfcount_ids(np.array([c], np.uint32))
+    finally:
+        e.close()

@@ -50,7 +50,7 @@ hipError_t launch_bloom_contains(hipStream_t st, uint64_t n, const uint64_t *off
                                  const uint8_t *bits, const uint64_t *d_len, uint64_t size, uint64_t magic, int k,
                                  uint8_t *out, int sched, void *scratch = nullptr);
 // contains, region schedule (large batches): hash + bucket probes by 128 KiB region, then one LDS-resident
-// region per workgroup; records u32[rc_blocks(n) * rc_chunk_words(k)], S u32[rc_blocks(n) * rc_regions(size)]
+// region per workgroup; records u32[rc_blocks(n) * rc_chunk_words(k)], S u32[rc_regions(size) * rc_blocks(n)]
 uint32_t rc_blocks(uint64_t n);
 uint32_t rc_regions(uint64_t size);
 uint32_t rc_max_probes();

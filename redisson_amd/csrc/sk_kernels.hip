@@ -977,7 +977,7 @@ __global__ void __launch_bounds__(256) k_bloom_contains_q(uint64_t n, const uint
 //                     an LDS counting sort of the block's probes by region,
 //                     stored as one coalesced chunk of u32 records
 //                     (bit-in-region << 12 | element-in-block) plus the
-//                     block's segment table S[block][region] = start|count<<16;
+//                     block's column of the region-major segment table S[region][block] = start | count<<16;
 //                     out[i] = 1 for every element.
 //   k_bloom_rc_probe  one 1024-thread workgroup per region: the region's
 //                     128 KiB into LDS, then the region's segment of every
@@ -1000,16 +1000,20 @@ static_assert(RC_TPB == SK_PFP_TPB, "key windows sized for SK_PFP_TPB threads");
 
 __global__ void __launch_bounds__(RC_TPB) k_bloom_rc_hash(uint64_t n, const uint64_t *__restrict__ off,
                                                           const uint8_t *__restrict__ bytes, uint64_t size,
-                                                          uint64_t magic, uint32_t P, uint32_t NR,
+                                                          uint64_t magic, uint32_t P, uint32_t NR, uint32_t NB,
                                                           uint32_t *__restrict__ S, uint32_t *__restrict__ chunks,
                                                           uint8_t *__restrict__ out) {
     __shared__ uint32_t hist[RC_NRMAX];
+    // block j: consecutive blocks on one XCD (blockIdx % 8 groups, speed only), so the ~32 blocks an XCD runs at
+    // once write neighbouring words of each region's row of S and those lines fill in its L2
+    const uint32_t jq = (NB + 7) / 8, jb = (blockIdx.x & 7u) * jq + (blockIdx.x >> 3);
+    if (jb >= NB) return; // uniform
     __shared__ uint32_t wsum[RC_TPB / 64];
     __shared__ uint64_t buf[RC_BUFW];
     uint64_t *win[2] = {buf, buf + SK_PFP_WIN};
     uint32_t *lrec = reinterpret_cast<uint32_t *>(buf); // after the last hash round
     for (uint32_t r = threadIdx.x; r < NR; r += RC_TPB) hist[r] = 0;
-    const uint64_t base = uint64_t(blockIdx.x) * RC_EPB;
+    const uint64_t base = uint64_t(jb) * RC_EPB;
     const uint64_t rounds = (n - base + RC_TPB - 1) / RC_TPB;
     const int nr = rounds < RC_ROUNDS ? int(rounds) : RC_ROUNDS;
     uint64_t wb[RC_ROUNDS + 1], oa[RC_ROUNDS], ob[RC_ROUNDS];
@@ -1033,7 +1037,7 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_rc_hash(uint64_t n, const uint
         pfp_win_store(wb[0], wb[1], v, win[0]);
     }
     __syncthreads(); // hist zeroed, window 0 staged
-    // probe j of round e: bit index (< 2^32: sizes <= 4,294,967,294) and its rank in its region
+    // probe p of round e: bit index (< 2^32: sizes <= 4,294,967,294) and its rank in its region
     uint32_t ix[RC_ROUNDS][RC_PMAX], rk[RC_ROUNDS][RC_PMAX / 2]; // u16 ranks, two per word
 #pragma unroll
     for (int e = 0; e < RC_ROUNDS; e++) {
@@ -1080,13 +1084,12 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_rc_hash(uint64_t n, const uint
     }
     uint32_t tot;
     uint32_t st = block_exscan<RC_TPB>(s4, wsum, &tot);
-    uint32_t *Sb = S + uint64_t(blockIdx.x) * NR;
 #pragma unroll
-    for (int q = 0; q < 4; q++) {
+    for (int q = 0; q < 4; q++) { // S is region-major: S[r * NB + block]
         uint32_t r = threadIdx.x * 4 + q;
         if (r < NR) {
             hist[r] = st;
-            Sb[r] = st | (c4[q] << 16);
+            S[uint64_t(r) * NB + jb] = st | (c4[q] << 16);
         }
         st += c4[q];
     }
@@ -1103,7 +1106,7 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_rc_hash(uint64_t n, const uint
         }
     }
     __syncthreads();
-    uint4 *dst = reinterpret_cast<uint4 *>(chunks + uint64_t(blockIdx.x) * RC_EPB * P);
+    uint4 *dst = reinterpret_cast<uint4 *>(chunks + uint64_t(jb) * RC_EPB * P);
     const uint4 *src = reinterpret_cast<const uint4 *>(lrec);
     for (uint32_t t = threadIdx.x; t < (tot + 3) / 4; t += RC_TPB) dst[t] = src[t];
 }
@@ -1126,6 +1129,37 @@ __device__ __forceinline__ void rc_test(const uint8_t *fb, uint32_t x, uint8_t *
     uint32_t bit = x >> 12;
     if (!((fb[bit >> 3] >> (7u - (bit & 7u))) & 1u)) ob[x & 0xfffu] = 0;
 }
+// Per thread: the segment-table words of every block it serves are loaded up front (with the region's own
+// stream); then the record vectors of RC_JB segments are loaded one step ahead of the segments being tested,
+// so a lane always has a step of loads in flight while it tests from LDS.
+#define RC_SMAX 8 // blocks per thread: pieces of <= 32 M elements = 8192 blocks
+__device__ __forceinline__ void rc_load_seg(const uint32_t *chunks, uint64_t CH, uint32_t j, uint32_t seg,
+                                            uint4 (&w)[RC_SEGV]) {
+    uint32_t st = seg & 0xffffu, cnt = seg >> 16;
+    const uint4 *cv = reinterpret_cast<const uint4 *>(chunks + uint64_t(j) * CH) + (st >> 2);
+    uint32_t nv = ((st & 3u) + cnt + 3u) >> 2; // vectors covering the segment
+#pragma unroll
+    for (int q = 0; q < RC_SEGV; q++) w[q] = uint32_t(q) < nv ? cv[q] : make_uint4(0, 0, 0, 0);
+}
+__device__ __forceinline__ void rc_test_seg(const uint8_t *fb, const uint32_t *chunks, uint64_t CH, uint32_t j,
+                                            uint32_t seg, const uint4 (&w)[RC_SEGV], uint8_t *out) {
+    const uint32_t st = seg & 0xffffu, cnt = seg >> 16, o = st & 3u;
+    uint8_t *ob = out + uint64_t(j) * RC_EPB;
+    // word t of the vectors is a record of this segment iff o <= t < o + cnt
+    constexpr uint32_t NW = 4 * RC_SEGV;
+    const uint32_t end = o + cnt < NW ? o + cnt : NW, inreg = end - o;
+#pragma unroll
+    for (int q = 0; q < RC_SEGV; q++) {
+        if (4 * q >= o && 4 * q < end) rc_test(fb, w[q].x, ob);
+        if (4 * q + 1 >= o && 4 * q + 1 < end) rc_test(fb, w[q].y, ob);
+        if (4 * q + 2 >= o && 4 * q + 2 < end) rc_test(fb, w[q].z, ob);
+        if (4 * q + 3 >= o && 4 * q + 3 < end) rc_test(fb, w[q].w, ob);
+    }
+    if (cnt > inreg) { // long segment (rare): the rest word by word
+        const uint32_t *cs = chunks + uint64_t(j) * CH + st;
+        for (uint32_t s = inreg; s < cnt; s++) rc_test(fb, cs[s], ob);
+    }
+}
 __global__ void __launch_bounds__(RC_TPB) k_bloom_rc_probe(uint32_t NB, uint32_t NR, const uint32_t *__restrict__ S,
                                                            const uint32_t *__restrict__ chunks, uint32_t P,
                                                            const uint8_t *__restrict__ bits, uint64_t cap_bytes,
@@ -1136,55 +1170,32 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_rc_probe(uint32_t NB, uint32_t
     if (r >= NR) return; // uniform
     const uint64_t b0 = uint64_t(r) << (RC_RB - 3);
     const uint4 *src = reinterpret_cast<const uint4 *>(bits + b0);
-    uint4 fv[VPT];
+    {
+        uint4 fv[VPT];
 #pragma unroll
-    for (uint32_t q = 0; q < VPT; q++) { // bytes past the buffer read as 0 (they are past the string)
-        uint32_t v = threadIdx.x + q * RC_TPB;
-        fv[q] = b0 + uint64_t(v) * 16 < cap_bytes ? ld_nt(src + v) : make_uint4(0, 0, 0, 0);
-    }
-    const uint8_t *fb = reinterpret_cast<const uint8_t *>(filt);
-    const uint64_t CH = uint64_t(RC_EPB) * P;
-    const uint32_t iters = (NB + RC_TPB * RC_JB - 1) / (RC_TPB * RC_JB); // >= 1, the same for every thread
-    for (uint32_t it = 0; it < iters; it++) {
-        const uint32_t j0 = threadIdx.x + it * RC_TPB * RC_JB;
-        uint32_t seg[RC_JB];
-#pragma unroll
-        for (int u = 0; u < RC_JB; u++) {
-            uint32_t j = j0 + u * RC_TPB;
-            seg[u] = j < NB ? S[uint64_t(j) * NR + r] : 0u;
+        for (uint32_t q = 0; q < VPT; q++) { // bytes past the buffer read as 0 (they are past the string)
+            uint32_t v = threadIdx.x + q * RC_TPB;
+            fv[q] = b0 + uint64_t(v) * 16 < cap_bytes ? ld_nt(src + v) : make_uint4(0, 0, 0, 0);
         }
-        if (it == 0) { // the region lands in LDS while the first segment-table loads are in flight
+        // NB <= RC_SMAX * RC_TPB (the host cuts batches into pieces)
+        uint32_t seg0[RC_SMAX];
 #pragma unroll
-            for (uint32_t q = 0; q < VPT; q++) filt[threadIdx.x + q * RC_TPB] = fv[q];
+        for (int u = 0; u < RC_SMAX; u++) {
+            uint32_t j = threadIdx.x + u * RC_TPB;
+            seg0[u] = j < NB ? S[uint64_t(r) * NB + j] : 0u; // coalesced: S is region-major
         }
-        uint4 w[RC_JB][RC_SEGV];
 #pragma unroll
-        for (int u = 0; u < RC_JB; u++) {
-            uint32_t st = seg[u] & 0xffffu, cnt = seg[u] >> 16;
-            const uint4 *cv = reinterpret_cast<const uint4 *>(chunks + uint64_t(j0 + u * RC_TPB) * CH) + (st >> 2);
-            uint32_t nv = ((st & 3u) + cnt + 3u) >> 2; // vectors covering the segment
+        for (uint32_t q = 0; q < VPT; q++) filt[threadIdx.x + q * RC_TPB] = fv[q];
+        __syncthreads();
+        const uint8_t *fb = reinterpret_cast<const uint8_t *>(filt);
+        const uint64_t CH = uint64_t(RC_EPB) * P;
+        uint4 wa[RC_SEGV], wb[RC_SEGV];
+        rc_load_seg(chunks, CH, threadIdx.x, seg0[0], wa);
 #pragma unroll
-            for (int q = 0; q < RC_SEGV; q++) w[u][q] = uint32_t(q) < nv ? cv[q] : make_uint4(0, 0, 0, 0);
-        }
-        if (it == 0) __syncthreads();
-#pragma unroll
-        for (int u = 0; u < RC_JB; u++) {
-            const uint32_t j = j0 + u * RC_TPB, st = seg[u] & 0xffffu, cnt = seg[u] >> 16, o = st & 3u;
-            uint8_t *ob = out + uint64_t(j) * RC_EPB;
-            // word t of the vectors is a record of this segment iff o <= t < o + cnt
-            constexpr uint32_t NW = 4 * RC_SEGV;
-            const uint32_t end = o + cnt < NW ? o + cnt : NW, inreg = end - o;
-#pragma unroll
-            for (int q = 0; q < RC_SEGV; q++) {
-                if (4 * q >= o && 4 * q < end) rc_test(fb, w[u][q].x, ob);
-                if (4 * q + 1 >= o && 4 * q + 1 < end) rc_test(fb, w[u][q].y, ob);
-                if (4 * q + 2 >= o && 4 * q + 2 < end) rc_test(fb, w[u][q].z, ob);
-                if (4 * q + 3 >= o && 4 * q + 3 < end) rc_test(fb, w[u][q].w, ob);
-            }
-            if (cnt > inreg) { // long segment (rare): the rest word by word
-                const uint32_t *cs = chunks + uint64_t(j) * CH + st;
-                for (uint32_t s = inreg; s < cnt; s++) rc_test(fb, cs[s], ob);
-            }
+        for (int u = 0; u < RC_SMAX; u++) {
+            if (uint32_t(u) * RC_TPB >= NB) break; // no thread has a block at this step (uniform)
+            if (u + 1 < RC_SMAX) rc_load_seg(chunks, CH, threadIdx.x + (u + 1) * RC_TPB, seg0[u + 1], (u & 1) ? wa : wb);
+            rc_test_seg(fb, chunks, CH, threadIdx.x + u * RC_TPB, seg0[u], (u & 1) ? wb : wa, out);
         }
     }
 }
@@ -1753,12 +1764,13 @@ uint32_t rc_regions(uint64_t size) { return uint32_t((size + (1ull << RC_RB) - 1
 uint32_t rc_max_probes() { return RC_PMAX; }
 uint64_t rc_chunk_words(int k) { return uint64_t(RC_EPB) * uint64_t(k - 1); }
 
-// region schedule: records u32[blocks * RC_EPB * (k-1)], S u32[blocks * regions]
+// region schedule: records u32[blocks * RC_EPB * (k-1)], S u32[regions * blocks]
 hipError_t launch_bloom_rc_hash(hipStream_t st, uint64_t n, const uint64_t *off, const uint8_t *bytes, uint64_t size,
                                 uint64_t magic, int k, uint32_t *S, uint32_t *recs, uint8_t *out) {
     if (!n) return hipSuccess;
-    hipLaunchKernelGGL(k_bloom_rc_hash, dim3(rc_blocks(n)), dim3(RC_TPB), 0, st, n, off, bytes, size, magic,
-                       uint32_t(k - 1), rc_regions(size), S, recs, out);
+    uint32_t NB = rc_blocks(n);
+    hipLaunchKernelGGL(k_bloom_rc_hash, dim3(8 * ((NB + 7) / 8)), dim3(RC_TPB), 0, st, n, off, bytes, size, magic,
+                       uint32_t(k - 1), rc_regions(size), NB, S, recs, out);
     SK_LAUNCH_CHECK();
     return hipSuccess;
 }

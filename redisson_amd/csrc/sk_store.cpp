@@ -1959,7 +1959,7 @@ static int bloom_contains_launch(sk_ctx *c, hipStream_t s, uint32_t id, int64_t 
                                             c->bloom_h.p));
         return SK_OK;
     }
-    const uint64_t piece = uint64_t(32) << 20;
+    const uint64_t piece = uint64_t(32) << 20; // k_bloom_rc_probe serves <= RC_SMAX * RC_TPB blocks
     const uint64_t nb = sk::rc_blocks(std::min(n, piece)), nr = sk::rc_regions(usize);
     HIPCHK(c, c->rc_S.ensure(nb * nr * 4));
     HIPCHK(c, c->rc_rec.ensure(nb * sk::rc_chunk_words(k) * 4));

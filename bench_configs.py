@@ -16,6 +16,17 @@ measures the remaining configs on one MI355X with inputs resident in HBM:
       BITCOUNT, AND/OR across 4 bitsets (BITOP streams (s+1)*N/8 bytes).
   host  the host-buffer C ABI the JNI shim calls (PCIe-inclusive): C2-shaped
       PFADD and C3-shaped Bloom add/contains batches from pageable host arrays.
+
+N-rank modes (one process per GPU under torch.distributed.run, RCCL over xGMI
+between the engine contexts; they also run at world size 1):
+  c4mr  C4 as stated: 1M tenant HLLs x 1,000 elements sharded by calcSlot % N,
+      then countWith / PFMERGE over ALL of them: local union + RCCL u8 MAX
+      all-reduce (redisson_amd/cluster.py).  Total keys fixed: strong scaling.
+  c5mr  C5 as stated: 2^34-bit RBitSets range-sharded over the N GPUs
+      (ShardedBitSet): SETBIT/GETBIT on each rank's own range, BITCOUNT (local
+      + u64 SUM all-reduce), AND/OR of sharded bitsets (shard-local), and a
+      BITOP OR of two whole bitsets owned by different GPUs (one RCCL
+      all-gather + a local OR).
 """
 from __future__ import annotations
 
@@ -30,6 +41,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 from redisson_amd import JsonJacksonCodec, JLong, SketchEngine, gen_jackson_longs, owner  # noqa: E402
+from redisson_amd.engine import owners  # noqa: E402
 
 PEAK = 8000.0
 
@@ -169,6 +181,100 @@ def c5(eng, args):
                        "unit": "GB/s", "frac": nbytes / t_bc / 1e9 / PEAK, "note": "host-timed incl. launch"}})
 
 
+def _dist():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo", rank=rank, world_size=world)   # rendezvous only; data moves over RCCL
+    return world, rank, dist
+
+
+def c4mr(eng, args):
+    from redisson_amd.cluster import RcclCollective, global_count_with, global_merge
+    world, rank, dist = _dist()
+    coll = RcclCollective(eng, rank, world, dist)
+    nk, per = args.c4mr_keys, args.c4_per_key
+    names = [b"t4:%d" % i for i in range(nk)]
+    own = owners(names, world) == rank
+    mine = [k for k, o in zip(names, own) if o]
+    ids = eng.hll_resolve(mine)
+    chunk, total = 1 << 24, len(mine) * per
+    d_out = eng.alloc(chunk)
+    rng = np.random.default_rng(40 + rank)
+    t_add = 0.0
+    for s in range(0, total, chunk):
+        m = min(chunk, total - s)
+        off, byt, tot = eng.gen_jackson_longs_dev(0x5EED0004, m, first=(rank << 40) + s)
+        d_ids = eng.to_device(ids[rng.integers(0, len(mine), m)].astype(np.uint32))
+        t_add += timed(eng, lambda: eng.pfadd_dev(m, d_ids, off, byt, tot, d_out))
+        off.free(); byt.free(); d_ids.free()
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    est = global_count_with(eng, names, rank, world, coll)
+    t_cw = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    global_merge(eng, b"t4:dest", names, rank, world, coll)
+    t_mg = time.perf_counter() - t0
+    walls = coll.allgather_u64(int(t_cw * 1e9))
+    if rank == 0:
+        line({"metric": "C4 global countWith over %d tenant HLLs on %d GPUs (sources/sec, whole job)" % (nk, world),
+              "value": nk / (max(walls) * 1e-9), "unit": "sources/s", "n_gpus": world, "scaling": "strong",
+              "config": {"workload": "c4mr", "keys": nk, "elements_per_key": per, "partitioner": "calcSlot %% %d" % world},
+              "countwith_estimate": est, "countwith_s": max(walls) * 1e-9, "pfmerge_s": t_mg,
+              "pfadd_inserts_per_s_rank0": total / t_add,
+              "note": "host-timed: key-name filtering + local union + RCCL u8 MAX all-reduce + estimator"})
+
+
+def c5mr(eng, args):
+    from redisson_amd.cluster import RcclCollective, ShardedBitSet, keyed_bitop
+    world, rank, dist = _dist()
+    coll = RcclCollective(eng, rank, world, dist)
+    bits = 1 << args.c5_log2_bits
+    a = ShardedBitSet(eng, b"bs5:a", bits, rank, world, coll)
+    b = ShardedBitSet(eng, b"bs5:b", bits, rank, world, coll)
+    lo_bit, hi_bit = a.lo * 8, min(bits, (a.lo + a.S) * 8)
+    n = args.c5_ops // world                 # this rank's share of the SETBIT / GETBIT ops, in its own range
+    rng = np.random.default_rng(50 + rank)
+    chunk = 1 << 26
+    t_set = t_get = 0.0
+    d_out = eng.alloc(chunk)
+    for s in range(0, n, chunk):
+        m = min(chunk, n - s)
+        loc = rng.integers(0, hi_bit - lo_bit, m, dtype=np.uint64)     # local offsets of this shard
+        d_off = eng.to_device(loc)
+        t_set += timed(eng, lambda: eng.setbit_dev(b"bs5:a", m, d_off, 1))
+        t_get += timed(eng, lambda: eng.getbit_dev(b"bs5:a", m, d_off, d_out))
+        d_off.free()
+    eng.setbit([b"bs5:a"], [hi_bit - lo_bit - 1], [1])                # every shard full length
+    eng.setbit([b"bs5:b"], [hi_bit - lo_bit - 1], [1])
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter(); card = a.cardinality(); t_bc = time.perf_counter() - t0
+    t0 = time.perf_counter(); a.op("OR", [b]); t_or = time.perf_counter() - t0
+    # two whole bitsets (1/16 of C5 each) owned by different GPUs: one all-gather + a local OR
+    kb = 1 << (args.c5_log2_bits - 4)
+    keys = [b"k5:%d" % i for i in range(64)]
+    ka = next(k for k in keys if owner(k, world) == 0)
+    kb_ = next(k for k in keys if owner(k, world) == (1 % world) and k != ka)
+    for k in (ka, kb_):
+        if owner(k, world) == rank:
+            eng.setbit([k] * 2, [0, kb - 1], [1, 1])
+    t0 = time.perf_counter(); nres = keyed_bitop(eng, "OR", b"k5:or", [ka, kb_], rank, world, coll)
+    t_kor = time.perf_counter() - t0
+    walls = coll.allgather_u64(int((t_set + t_get) * 1e9))
+    if rank == 0:
+        line({"metric": "C5 RBitSet 2^%d bits range-sharded over %d GPUs: SETBIT+GETBIT ops/sec (whole job)"
+              % (args.c5_log2_bits, world), "value": 2 * n * world / (max(walls) * 1e-9), "unit": "ops/s",
+              "n_gpus": world, "scaling": "strong", "config": {"workload": "c5mr", "bits": bits, "ops": n * world,
+                                                              "shard_bytes": a.S},
+              "bitcount_s": t_bc, "cardinality": card, "sharded_or_s": t_or,
+              "keyed_or_bytes": nres, "keyed_or_s": t_kor,
+              "note": "BITCOUNT / OR / keyed OR host-timed including the collectives"})
+
+
 def host(eng, args):
     """The host-buffer C ABI (what the JNI shim calls): sk_pfadd / sk_bloom_add / sk_bloom_contains with caller-owned
     host arrays, so each call stages its inputs H2D and copies replies D2H (PCIe-inclusive; DESIGN 'Measurement').
@@ -251,13 +357,18 @@ def main():
     ap.add_argument("--c1-n", type=int, default=1 << 20)
     ap.add_argument("--c4-keys", type=int, default=125_000)       # 1M keys / 8 GPUs
     ap.add_argument("--c4-per-key", type=int, default=1000)
+    ap.add_argument("--c4mr-keys", type=int, default=1_000_000)   # C4 as stated, sharded over the ranks
     ap.add_argument("--c5-log2-bits", type=int, default=34)
     ap.add_argument("--c5-ops", type=int, default=1 << 28)
     args = ap.parse_args()
+    cfgs = args.configs.split(",")
+    cap = args.c4_keys + 64
+    if "c4mr" in cfgs:
+        cap = max(cap, args.c4mr_keys // int(os.environ.get("WORLD_SIZE", "1")) + 4096)
     eng = SketchEngine(device=int(os.environ.get("LOCAL_RANK", "0")), max_bit_offset=1 << 36,
-                       hll_capacity=args.c4_keys + 64, max_batch=1 << 24)
-    for c in args.configs.split(","):
-        {"c1": c1, "c2zipf": c2zipf, "c4": c4, "c5": c5, "host": host}[c](eng, args)
+                       hll_capacity=cap, max_batch=1 << 24)
+    for c in cfgs:
+        {"c1": c1, "c2zipf": c2zipf, "c4": c4, "c5": c5, "host": host, "c4mr": c4mr, "c5mr": c5mr}[c](eng, args)
     eng.close()
 
 

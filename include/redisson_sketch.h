@@ -93,6 +93,8 @@ uint32_t sk_crc16(const uint8_t *bytes, uint64_t len);
 int32_t sk_calc_slot(const uint8_t *key, uint64_t len);
 /* partitioner: owning GPU = calcSlot % n_gpus (-1 if calcSlot throws) */
 int32_t sk_owner(const uint8_t *key, uint64_t len, int32_t n_gpus);
+/* sk_owner of n keys (off u64[n+1], bytes) into out[n] */
+int sk_owner_many(uint32_t n, const uint64_t *key_off, const uint8_t *key_bytes, int32_t n_gpus, int32_t *out);
 /* RedissonBloomFilter.optimalNumOfBits / optimalNumOfHashFunctions (:69-78) */
 int64_t sk_bloom_optimal_bits(int64_t expected_insertions, double false_probability);
 int32_t sk_bloom_optimal_k(int64_t expected_insertions, int64_t bits);
@@ -111,6 +113,11 @@ int sk_flushall(sk_ctx *ctx);
  * PFADD / PFMERGE do).  out_created[i] = 1 if this call created it. */
 int sk_hll_resolve(sk_ctx *ctx, uint32_t n, const uint64_t *key_off, const uint8_t *key_bytes,
                    uint32_t *out_ids, uint8_t *out_created);
+/* handles of existing HLL keys, creating nothing: out_ids[i] = 0xffffffff for a
+ * missing key (PFCOUNT / countWith semantics: missing keys are empty); a key
+ * holding a plain string fails with SK_EWRONGTYPE.  Parallel directory pass
+ * for >= 64k keys (cross-GPU countWith over 1M tenants, cluster.py). */
+int sk_hll_lookup(sk_ctx *ctx, uint32_t n, const uint64_t *key_off, const uint8_t *key_bytes, uint32_t *out_ids);
 
 /* ---- RHyperLogLog (M:RedissonHyperLogLog.java:66-97) ---- */
 /* Batch of PFADD commands in RBatch order.  Command c targets key c and adds
@@ -182,6 +189,12 @@ int sk_bitop(sk_ctx *ctx, int op, const uint8_t *dest, uint64_t dest_len, uint32
 int sk_get(sk_ctx *ctx, const uint8_t *key, uint64_t len, uint8_t *buf, uint64_t cap, int64_t *out_len);
 /* SET key raw-bytes (RBitSet.set(BitSet), M:RedissonBitSet.java:211-214) */
 int sk_set(sk_ctx *ctx, const uint8_t *key, uint64_t len, const uint8_t *val, uint64_t val_len);
+/* GET / SET of a bit string with the value in DEVICE memory of this context's
+ * GPU (cross-GPU BITOP / Bloom union, redisson_amd/cluster.py: a shard or an
+ * operand gathered with sk_allgather becomes a local string, no host copy).
+ * sk_get_dev on an HLL key: SK_EWRONGTYPE. */
+int sk_get_dev(sk_ctx *ctx, const uint8_t *key, uint64_t len, uint8_t *d_buf, uint64_t cap, int64_t *out_len);
+int sk_set_dev(sk_ctx *ctx, const uint8_t *key, uint64_t len, const uint8_t *d_val, uint64_t val_len);
 /* RBitSet.length() Lua script (M:RedissonBitSet.java:180-192), same result and errors */
 int sk_bitset_length(sk_ctx *ctx, const uint8_t *key, uint64_t len, int64_t *out);
 

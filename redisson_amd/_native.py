@@ -40,7 +40,7 @@ class SkConfig(ctypes.Structure):
 
 
 P = c_void_p  # every pointer argument is passed as a raw address
-_u8p, _u32p, _u64p, _i64p = P, P, P, P
+_u8p, _u32p, _u64p, _i64p, _i32p = P, P, P, P, P
 
 # name -> (restype, argtypes)
 SIGNATURES = {
@@ -54,12 +54,14 @@ SIGNATURES = {
     "sk_crc16": (c_uint32, [_u8p, c_uint64]),
     "sk_calc_slot": (c_int32, [_u8p, c_uint64]),
     "sk_owner": (c_int32, [_u8p, c_uint64, c_int32]),
+    "sk_owner_many": (c_int, [c_uint32, _u64p, _u8p, c_int32, _i32p]),
     "sk_bloom_optimal_bits": (c_int64, [c_int64, c_double]),
     "sk_bloom_optimal_k": (c_int32, [c_int64, c_int64]),
     "sk_hll_estimate_hist": (c_uint64, [_u32p, c_int]),
     "sk_type": (c_int, [P, _u8p, c_uint64, P]),
     "sk_del": (c_int, [P, c_uint32, _u64p, _u8p, _u64p]),
     "sk_hll_resolve": (c_int, [P, c_uint32, _u64p, _u8p, _u32p, _u8p]),
+    "sk_hll_lookup": (c_int, [P, c_uint32, _u64p, _u8p, _u32p]),
     "sk_pfadd": (c_int, [P, c_uint32, _u64p, _u8p, _u32p, _u64p, _u8p, _u8p]),
     "sk_pfadd_ids": (c_int, [P, c_uint32, _u32p, _u32p, _u64p, _u8p, _u8p]),
     "sk_pfadd_dev": (c_int, [P, c_uint64, _u32p, _u64p, _u8p, c_uint64, _u8p]),
@@ -79,6 +81,8 @@ SIGNATURES = {
     "sk_bitop": (c_int, [P, c_int, _u8p, c_uint64, c_uint32, _u64p, _u8p, _u64p]),
     "sk_get": (c_int, [P, _u8p, c_uint64, _u8p, c_uint64, _i64p]),
     "sk_set": (c_int, [P, _u8p, c_uint64, _u8p, c_uint64]),
+    "sk_get_dev": (c_int, [P, _u8p, c_uint64, _u8p, c_uint64, _i64p]),
+    "sk_set_dev": (c_int, [P, _u8p, c_uint64, _u8p, c_uint64]),
     "sk_bitset_length": (c_int, [P, _u8p, c_uint64, _i64p]),
     "sk_bloom_try_init": (c_int, [P, _u8p, c_uint64, c_int64, c_double, P]),
     "sk_bloom_config": (c_int, [P, _u8p, c_uint64, P, P, P, P]),

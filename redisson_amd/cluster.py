@@ -8,8 +8,18 @@ only exchange steps are the global ones:
 * countWith / PFMERGE over keys spread across GPUs (C4): every rank unions
   its own keys into 16,384 registers on its GPU, then a uint8 MAX all-reduce
   (RCCL over xGMI, ``sk_allreduce_max_u8``), then the estimator / merge.
-* BITCOUNT of a range-sharded bitset (C5): local popcount, then a uint64 SUM
-  all-reduce.
+* RBitSet range-sharded over the GPUs (C5, ``ShardedBitSet``): rank r holds
+  bytes [r*S, (r+1)*S) of the Redis string.  SETBIT / GETBIT go to the owner of
+  the byte; BITCOUNT = local popcount + uint64 SUM all-reduce; length = the
+  last non-empty shard (u64 all-gather); BITOP AND / OR / XOR / NOT between
+  bitsets of the same sharding is shard-local (RedissonBitSet.opAsync,
+  M:RedissonBitSet.java:138-145) once every operand's shards are padded to
+  its logical length.
+* BITOP over whole keys that live on different GPUs (``keyed_bitop``; a Bloom
+  filter union is BITOP OR of the filters): every rank contributes the
+  operands it owns to ONE all-gather (RCCL, device buffers), and the owner of
+  the destination runs the local BITOP over the gathered copies
+  (north_star: "Bloom/BitSet union uses all-gather plus a local OR").
 
 The collective is a small interface so the same protocol runs with the
 engine's RCCL communicator on GPUs and with torch.distributed/gloo on host
@@ -21,7 +31,7 @@ from typing import Dict, Iterable, List, Sequence
 
 import numpy as np
 
-from .engine import owner
+from .engine import owner, owners
 
 HLL_REGISTERS = 16384
 
@@ -42,6 +52,20 @@ class HostCollective:
 
     def __init__(self, dist):
         self.dist = dist
+
+    @property
+    def world(self) -> int:
+        return self.dist.get_world_size()
+
+    def allgather_bytes(self, b: bytes) -> List[bytes]:
+        out = [None] * self.world
+        self.dist.all_gather_object(out, bytes(b))
+        return out
+
+    def allgather_u64(self, v: int) -> List[int]:
+        out = [None] * self.world
+        self.dist.all_gather_object(out, int(v))
+        return out
 
     def max_u8(self, regs: np.ndarray) -> np.ndarray:
         import torch
@@ -72,6 +96,8 @@ class RcclCollective:
         self.buf = engine.alloc(HLL_REGISTERS)
         self.u64 = engine.alloc(8)
 
+        self.world = world
+
     def max_u8_dev(self, dbuf, n: int = HLL_REGISTERS):
         self.engine.allreduce_max_u8(dbuf, n)
 
@@ -80,13 +106,50 @@ class RcclCollective:
         self.engine.allreduce_sum_u64(self.u64, 1)
         return int(self.u64.download(np.uint64, 1)[0])
 
+    def max_u8(self, a: np.ndarray) -> np.ndarray:
+        a = np.ascontiguousarray(a, dtype=np.uint8)
+        if not len(a):
+            return a.copy()
+        d = self.engine.to_device(a)
+        self.engine.allreduce_max_u8(d, len(a))
+        out = d.download(np.uint8, len(a))
+        d.free()
+        return out
+
+    def allgather_dev(self, send, recv, nbytes: int):
+        """RCCL all-gather of nbytes per rank, device buffers (recv holds world * nbytes)."""
+        self.engine.allgather(send, recv, nbytes)
+
+    def allgather_u64(self, v: int) -> List[int]:
+        send, recv = self.engine.alloc(8), self.engine.alloc(8 * self.world)
+        send.upload(np.array([v], dtype=np.uint64))
+        self.engine.allgather(send, recv, 8)
+        out = [int(x) for x in recv.download(np.uint64, self.world)]
+        send.free()
+        recv.free()
+        return out
+
+    def allgather_bytes(self, b: bytes) -> List[bytes]:
+        sizes = self.allgather_u64(len(b))
+        P = max(max(sizes), 1)
+        send, recv = self.engine.alloc(P), self.engine.alloc(P * self.world)
+        if b:
+            send.upload(np.frombuffer(bytes(b), dtype=np.uint8))
+        self.engine.allgather(send, recv, P)
+        flat = recv.download(np.uint8, P * self.world)
+        send.free()
+        recv.free()
+        return [flat[r * P:r * P + sizes[r]].tobytes() for r in range(self.world)]
+
 
 def global_union_registers(engine, keys: Sequence, rank: int, world: int, coll: RcclCollective):
     """Union (register max) of every key in `keys`, wherever it lives; result
     left in coll.buf on every rank.  Missing keys count as empty (PFCOUNT rule)."""
-    mine = [k for k in keys if owner(k, world) == rank and engine.key_type(k) != 0]
-    if mine:
-        ids = engine.hll_resolve(mine)              # existing keys: ids only
+    own = owners(keys, world) == rank
+    mine = [k for k, o in zip(keys, own) if o]
+    ids = engine.hll_lookup(mine) if mine else np.zeros(0, dtype=np.uint32)   # existing keys only, nothing created
+    ids = ids[ids != 0xFFFFFFFF]
+    if len(ids):
         d_ids = engine.to_device(ids)
         engine.hll_union_dev(len(ids), d_ids, coll.buf)
         d_ids.free()
@@ -125,3 +188,159 @@ def host_global_count_with(local_regs: Dict, keys: Sequence, rank: int, world: i
     u = coll.max_u8(u)
     hist = np.bincount(u, minlength=64).astype(np.uint32)
     return estimate(hist)
+
+
+# ---------------------------------------------------------------- RBitSet across GPUs
+def shard_bytes(nbits: int, world: int) -> int:
+    """Bytes of the Redis string each rank holds (a multiple of 16)."""
+    total = (int(nbits) + 7) // 8
+    per = (total + world - 1) // world
+    return max(16, (per + 15) // 16 * 16)
+
+
+class ShardedBitSet:
+    """RBitSet of `nbits` bits range-sharded over the ranks (C5): rank r holds bytes [r*S, (r+1)*S) of the Redis
+    string as its local key `name`.  Every method is SPMD: all ranks call it with the same arguments and get the
+    same reply.  Bit i of the logical string is bit i - 8*r*S of shard r (MSB-first bytes, M:RedissonBitSet.java:
+    152-173), so GET of the logical string is the shards concatenated, each zero-filled to min(S, L - r*S)."""
+
+    def __init__(self, engine, name, nbits: int, rank: int, world: int, coll):
+        self.engine, self.name, self.rank, self.world, self.coll = engine, name, rank, world, coll
+        self.S = shard_bytes(nbits, world)
+        self.lo = rank * self.S          # first byte of this rank's shard
+
+    def _mine(self, offsets):
+        offs = np.asarray(offsets, dtype=np.uint64)
+        byte = offs >> np.uint64(3)
+        mine = (byte >= np.uint64(self.lo)) & (byte < np.uint64(self.lo + self.S))
+        return offs, mine, offs[mine] - np.uint64(8 * self.lo)
+
+    def set(self, offsets, values) -> np.ndarray:
+        """SETBIT batch (RBitSet.set(i, v) in an RBatch): old bits in batch order, sequential semantics (each bit
+        lives on one rank, so per-bit order is that rank's order)."""
+        offs, mine, loc = self._mine(offsets)
+        vals = np.broadcast_to(np.asarray(values, dtype=np.uint8), offs.shape)
+        out = np.zeros(len(offs), dtype=np.uint8)
+        if mine.any():
+            out[mine] = self.engine.setbit([self.name] * int(mine.sum()), loc, vals[mine])
+        return self.coll.max_u8(out)
+
+    def get(self, offsets) -> np.ndarray:
+        """GETBIT batch (RBitSet.get(i))."""
+        offs, mine, loc = self._mine(offsets)
+        out = np.zeros(len(offs), dtype=np.uint8)
+        if mine.any():
+            out[mine] = self.engine.getbit([self.name] * int(mine.sum()), loc)
+        return self.coll.max_u8(out)
+
+    def _local_len(self) -> int:
+        return self.engine.strlen(self.name)
+
+    def length_bytes(self) -> int:
+        """STRLEN of the logical string: the end of the last non-empty shard."""
+        lens = self.coll.allgather_u64(self._local_len())
+        return max([r * self.S + ln for r, ln in enumerate(lens) if ln] or [0])
+
+    def size(self) -> int:
+        """RBitSet.size() = STRLEN * 8 (int overflow, Q3: M:client/protocol/convertor/BitsSizeReplayConvertor.java)."""
+        v = (self.length_bytes() * 8) & 0xFFFFFFFF
+        return v - (1 << 32) if v >= 1 << 31 else v
+
+    def cardinality(self) -> int:
+        """BITCOUNT: local popcount + u64 SUM all-reduce (RedissonBitSet.cardinalityAsync, :240-243)."""
+        return self.coll.sum_u64(self.engine.bitcount(self.name))
+
+    def _pad_to(self, L: int):
+        """Grow this shard with zero bytes to its part of a logical length L (content unchanged)."""
+        want = min(self.S, max(0, L - self.lo))
+        if want > self._local_len():
+            self.engine.setbit([self.name], [8 * want - 1], [0], want_old=False)
+
+    def op(self, op: str, others: Sequence["ShardedBitSet"] = ()) -> None:
+        """BITOP op name name others... (RedissonBitSet.and/or/xor/not -> opAsync, M:RedissonBitSet.java:138-145,
+        216-219, 255-268): shard-local once every operand is padded to its logical length, since byte j of the
+        result depends only on byte j of the operands and the result length is the longest operand."""
+        ops = [self] + list(others)
+        for o in ops:
+            if o.S != self.S:
+                raise ValueError("BITOP across bitsets of different shardings")
+        lens = [o.length_bytes() for o in ops]
+        for o, L in zip(ops, lens):
+            o._pad_to(L)
+        self.engine.bitop(op, self.name, [o.name for o in ops])
+
+    def to_bytes(self) -> bytes:
+        """GET of the logical string (RBitSet.toByteArray, :88-91): the shards, each zero-filled to its part."""
+        L = self.length_bytes()
+        mine = self.engine.get(self.name) or b""
+        want = min(self.S, max(0, L - self.lo))
+        parts = self.coll.allgather_bytes(mine[:want] + b"\0" * (want - len(mine[:want])))
+        return b"".join(parts)[:L]
+
+
+def _owned_lengths(engine, keys: Sequence, rank: int, world: int, coll) -> List[int]:
+    """Byte length of every key (-1: missing), each reported by its owner."""
+    mine = np.full(len(keys), -2, dtype=np.int64)
+    for i, k in enumerate(keys):
+        if owner(k, world) == rank:
+            t = engine.key_type(k)
+            mine[i] = engine.strlen(k) if t else -1
+    parts = coll.allgather_bytes(mine.tobytes())
+    allv = np.stack([np.frombuffer(p, dtype=np.int64) for p in parts])
+    return [int(allv[owner(k, world), i]) for i, k in enumerate(keys)]
+
+
+def keyed_bitop(engine, op: str, dest, srcs: Sequence, rank: int, world: int, coll,
+                tmp_prefix: bytes = b"__sk_bitop_src__:") -> int:
+    """BITOP op dest srcs... where every key lives whole on its owner (calcSlot % world): each rank contributes the
+    sources it owns to one all-gather, and dest's owner runs the local BITOP over the gathered copies (missing
+    sources are empty strings, as in Redis).  Returns the result length on every rank.  A Bloom filter union is
+    keyed_bitop("OR", ...) over the filters' names (same size and k)."""
+    if op.upper() == "NOT" and len(srcs) != 1:
+        raise ValueError("BITOP NOT must be called with a single source key.")
+    lens = _owned_lengths(engine, srcs, rank, world, coll)
+    mine = [i for i, k in enumerate(srcs) if owner(k, world) == rank]
+    base = {}
+    pos = 0
+    for i in mine:                            # this rank's blob: its sources back to back
+        base[i] = pos
+        pos += max(lens[i], 0)
+    blobs = coll.allgather_u64(pos)
+    P = max(max(blobs), 1)
+    # where every source sits in the gathered buffer: rank owner(src) * P + offset inside that rank's blob
+    where = {}
+    for r in range(world):
+        q = 0
+        for i, k in enumerate(srcs):
+            if owner(k, world) == r:
+                where[i] = r * P + q
+                q += max(lens[i], 0)
+    d_owner = owner(dest, world)
+    tmp = [tmp_prefix + b"%d" % i for i in range(len(srcs))]
+    if hasattr(coll, "allgather_dev"):        # GPUs: the operands never leave HBM
+        send, recv = engine.alloc(P), engine.alloc(P * world)
+        for i in mine:
+            if lens[i] > 0:
+                engine.get_dev(srcs[i], send.ptr + base[i], lens[i])
+        coll.allgather_dev(send, recv, P)
+        if rank == d_owner:
+            for i in range(len(srcs)):
+                if lens[i] >= 0:
+                    engine.set_dev(tmp[i], recv.ptr + where[i], lens[i])
+        send.free()
+        recv.free()
+    else:
+        blob = b"".join((engine.get(srcs[i]) or b"") for i in mine)
+        parts = coll.allgather_bytes(blob)
+        flat = b"".join(p + b"\0" * (P - len(p)) for p in parts)
+        if rank == d_owner:
+            for i in range(len(srcs)):
+                if lens[i] >= 0:
+                    engine.set(tmp[i], flat[where[i]:where[i] + lens[i]])
+    n = 0
+    if rank == d_owner:
+        try:
+            n = engine.bitop(op, dest, tmp)
+        finally:
+            engine.delete(tmp)
+    return max(coll.allgather_u64(n))

@@ -961,6 +961,11 @@ int32_t sk_owner(const uint8_t *key, uint64_t len, int32_t n_gpus) {
     return s % n_gpus;
 }
 
+int sk_owner_many(uint32_t n, const uint64_t *off, const uint8_t *bytes, int32_t n_gpus, int32_t *out) {
+    for (uint32_t i = 0; i < n; i++) out[i] = sk_owner(bytes + off[i], off[i + 1] - off[i], n_gpus);
+    return SK_OK;
+}
+
 int64_t sk_bloom_optimal_bits(int64_t n, double p) {
     if (p == 0) p = 4.9e-324; // Double.MIN_VALUE
     double v = double(-n) * std::log(p) / (std::log(2) * std::log(2));
@@ -1025,6 +1030,9 @@ int sk_flushall(sk_ctx *c) {
     return sync(c);
 }
 
+static void find_hlls_parallel(sk_ctx *c, uint32_t n, const uint64_t *key_off, const uint8_t *key_bytes,
+                               uint32_t *ids, uint8_t *found);
+
 int sk_hll_resolve(sk_ctx *c, uint32_t n, const uint64_t *off, const uint8_t *bytes, uint32_t *ids,
                    uint8_t *created) {
     std::lock_guard<std::mutex> g(c->mu);
@@ -1035,6 +1043,26 @@ int sk_hll_resolve(sk_ctx *c, uint32_t n, const uint64_t *off, const uint8_t *by
         if (r) return r;
         ids[i] = hll_handle(c, ids[i]);
         if (created) created[i] = cr;
+    }
+    return sync(c);
+}
+
+// HLL handles of existing keys without creating any (0xffffffff: no such key) -- what PFCOUNT / countWith read
+// (a key holding a plain bit string is refused with WRONGTYPE, a valid HLL string is adopted, as PFCOUNT does)
+int sk_hll_lookup(sk_ctx *c, uint32_t n, const uint64_t *off, const uint8_t *bytes, uint32_t *ids) {
+    std::lock_guard<std::mutex> g(c->mu);
+    ENTER(c);
+    std::vector<uint8_t> found(n, 0);
+    find_hlls_parallel(c, n, off, bytes, ids, found.data());
+    for (uint32_t i = 0; i < n; i++) {
+        uint32_t id;
+        if (!found[i]) {
+            int r = hll_get(c, key_at(off, bytes, i), false, &id, nullptr);
+            if (r) return r;
+        } else {
+            id = ids[i];
+        }
+        ids[i] = id == kNoId ? kNoId : hll_handle(c, id);
     }
     return sync(c);
 }
@@ -1820,6 +1848,40 @@ int sk_set(sk_ctx *c, const uint8_t *key, uint64_t len, const uint8_t *val, uint
     uint32_t id;
     if ((r = str_get(c, k, true, val_len, &id))) return r;
     if (val_len) HIPCHK(c, hipMemcpyAsync(c->strs[id].ptr, val, val_len, hipMemcpyHostToDevice, c->st));
+    if ((r = sync(c))) return r;
+    return str_set_len(c, id, val_len);
+}
+
+// GET / SET of a bit string with the value in device memory (cross-GPU BITOP: an operand gathered over RCCL
+// becomes a local string without a host round trip; a shard's bytes go straight into a send buffer)
+int sk_get_dev(sk_ctx *c, const uint8_t *key, uint64_t len, uint8_t *d_buf, uint64_t cap, int64_t *out_len) {
+    std::lock_guard<std::mutex> g(c->mu);
+    ENTER(c);
+    auto it = c->keys.find(key_of(key, len));
+    if (it == c->keys.end()) {
+        *out_len = -1;
+        return SK_OK;
+    }
+    if (it->second.type != SK_TYPE_STRING) return fail(c, SK_EWRONGTYPE, "%s", kWrongType);
+    uint64_t l;
+    int r = str_len(c, it->second.id, &l);
+    if (r) return r;
+    *out_len = int64_t(l);
+    uint64_t ncopy = std::min(cap, l);
+    if (ncopy) HIPCHK(c, hipMemcpyAsync(d_buf, c->strs[it->second.id].ptr, ncopy, hipMemcpyDeviceToDevice, c->st));
+    return sync(c);
+}
+
+int sk_set_dev(sk_ctx *c, const uint8_t *key, uint64_t len, const uint8_t *d_val, uint64_t val_len) {
+    std::lock_guard<std::mutex> g(c->mu);
+    ENTER(c);
+    std::string k = key_of(key, len);
+    bool removed;
+    int r = del_key(c, k, &removed);
+    if (r) return r;
+    uint32_t id;
+    if ((r = str_get(c, k, true, val_len, &id))) return r;
+    if (val_len) HIPCHK(c, hipMemcpyAsync(c->strs[id].ptr, d_val, val_len, hipMemcpyDeviceToDevice, c->st));
     if ((r = sync(c))) return r;
     return str_set_len(c, id, val_len);
 }

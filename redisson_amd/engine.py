@@ -238,6 +238,14 @@ class SketchEngine:
         self._check(self.lib.sk_del(self.ctx, len(ks), _addr(off), _addr(buf), ctypes.addressof(out)))
         return out.value
 
+    def hll_lookup(self, keys: Sequence) -> np.ndarray:
+        """Handles of existing HLL keys (0xFFFFFFFF: missing), creating nothing."""
+        ks = [_b(k) for k in keys]
+        off, buf = pack(ks)
+        ids = np.zeros(len(ks), dtype=np.uint32)
+        self._check(self.lib.sk_hll_lookup(self.ctx, len(ks), _addr(off), _addr(buf), _addr(ids)))
+        return ids
+
     def hll_resolve(self, keys: Sequence) -> np.ndarray:
         ks = [_b(k) for k in keys]
         off, buf = pack(ks)
@@ -380,6 +388,18 @@ class SketchEngine:
         v = np.frombuffer(bytes(value) + b"\0", dtype=np.uint8)
         self._check(self.lib.sk_set(self.ctx, k, len(k), _addr(v), len(value)))
 
+    def get_dev(self, key, d_buf, cap: int) -> int:
+        """Copy a bit string into device memory (<= cap bytes); its length, or -1 if the key does not exist."""
+        k = _b(key)
+        ln = ctypes.c_int64()
+        self._check(self.lib.sk_get_dev(self.ctx, k, len(k), _addr(d_buf), int(cap), ctypes.addressof(ln)))
+        return ln.value
+
+    def set_dev(self, key, d_val, n: int):
+        """SET key from n bytes of device memory."""
+        k = _b(key)
+        self._check(self.lib.sk_set_dev(self.ctx, k, len(k), _addr(d_val), int(n)))
+
     def bitset_length(self, key) -> int:
         k = _b(key)
         out = ctypes.c_int64()
@@ -450,6 +470,14 @@ def crc16(data: bytes) -> int:
 def owner(key, n_gpus: int) -> int:
     k = _b(key)
     return int(N.load().sk_owner(k, len(k), n_gpus))
+
+
+def owners(keys: Sequence, n_gpus: int) -> np.ndarray:
+    """owner() of many keys in one call (int32; -1 where calcSlot throws)."""
+    off, buf = pack([_b(k) for k in keys])
+    out = np.zeros(len(keys), dtype=np.int32)
+    N.load().sk_owner_many(len(keys), _addr(off), _addr(buf), n_gpus, _addr(out))
+    return out
 
 
 def bloom_optimal_bits(n: int, p: float) -> int:

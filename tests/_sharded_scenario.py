@@ -1,0 +1,179 @@
+"""Cross-GPU RBitSet / BITOP scenario shared by the multi-rank tests (redisson_amd/cluster.py).
+
+`run_scenario(engine, rank, world, coll)` drives ShardedBitSet and keyed_bitop SPMD-style and returns what every
+rank observed; `expected()` computes the same with the oracle in one process (the single redis-server the
+reference talks to).  The CPU test runs it with an oracle-backed engine on gloo (world 2); the GPU tests with
+SketchEngine contexts (RCCL at world 1, gloo between two processes sharing the GPU at world 2).
+"""
+import numpy as np
+
+NBITS = 1 << 20
+KEYS = [b"kb:%d" % i for i in range(6)]
+
+
+def _offsets(seed, n):
+    return np.random.default_rng(seed).integers(0, NBITS, n, dtype=np.uint64)
+
+
+def run_scenario(engine, rank, world, coll):
+    from redisson_amd.cluster import ShardedBitSet, keyed_bitop
+    from redisson_amd import owner
+
+    out = {}
+    a = ShardedBitSet(engine, b"sb:a", NBITS, rank, world, coll)
+    b = ShardedBitSet(engine, b"sb:b", NBITS, rank, world, coll)
+    c = ShardedBitSet(engine, b"sb:c", NBITS, rank, world, coll)
+    oa = _offsets(1, 3000)
+    oa[0] = NBITS - 1                       # the last byte of the string
+    out["set_a"] = a.set(oa, 1).tolist()     # repeats inside the batch: second SETBIT of a bit replies 1
+    out["set_b"] = b.set(_offsets(2, 2000)[:1000], 1).tolist()   # b ends early: shorter than a
+    out["clear_a"] = a.set(oa[:500], 0).tolist()
+    out["get_a"] = a.get(np.concatenate([oa[:800], _offsets(3, 800)])).tolist()
+    out["card"] = [a.cardinality(), b.cardinality(), c.cardinality()]
+    out["len"] = [a.length_bytes(), b.length_bytes(), c.length_bytes()]
+    out["size"] = a.size()
+    out["bytes_a"] = a.to_bytes()
+    a2 = ShardedBitSet(engine, b"sb:a2", NBITS, rank, world, coll)
+    a2.set(oa[500:], 1)
+    a2.op("AND", [b])
+    out["and"] = a2.to_bytes()
+    a3 = ShardedBitSet(engine, b"sb:a3", NBITS, rank, world, coll)
+    a3.set(oa[500:], 1)
+    a3.op("OR", [b, c])                      # c is empty (missing on every rank)
+    out["or"] = a3.to_bytes()
+    a4 = ShardedBitSet(engine, b"sb:a4", NBITS, rank, world, coll)
+    a4.set(_offsets(2, 2000)[:1000], 1)
+    a4.op("XOR", [b])                        # equal strings: an all-zero result of b's length
+    out["xor"] = a4.to_bytes()
+    b.op("NOT")                              # shards before b's last byte are padded, then inverted
+    out["not_b"] = b.to_bytes()
+    out["card_not_b"] = b.cardinality()
+
+    # whole keys on their owners: BITOP across GPUs by one all-gather + a local op
+    for i, k in enumerate(KEYS[:5]):
+        if owner(k, world) == rank:
+            offs = _offsets(10 + i, 300 + 200 * i) % np.uint64(NBITS >> (i % 3))
+            engine.setbit([k] * len(offs), offs, [1] * len(offs), want_old=False)
+    res = {}
+    for op, dest, srcs in (("OR", b"kd:or", KEYS[:5]), ("AND", b"kd:and", KEYS[:3]),
+                           ("XOR", b"kd:xor", [KEYS[1], KEYS[4], KEYS[5]]), ("NOT", b"kd:not", [KEYS[2]])):
+        n = keyed_bitop(engine, op, dest, srcs, rank, world, coll)
+        val = engine.get(dest) if owner(dest, world) == rank else None
+        res[op] = (n, val)
+    out["keyed"] = res
+    return out
+
+
+def expected():
+    """The same commands against one oracle store (what one redis-server holds)."""
+    from oracle import oracle as O
+
+    s = {}
+
+    def bs(k):
+        return s.setdefault(k, O.BitString(NBITS // 8 + 16))
+
+    def setbits(k, offs, v):
+        return [bs(k).setbit(int(o), v) for o in offs]
+
+    out = {}
+    oa = _offsets(1, 3000)
+    oa[0] = NBITS - 1
+    out["set_a"] = setbits(b"a", oa, 1)
+    ob = _offsets(2, 2000)[:1000]
+    out["set_b"] = setbits(b"b", ob, 1)
+    out["clear_a"] = setbits(b"a", oa[:500], 0)
+    out["get_a"] = [bs(b"a").getbit(int(o)) for o in np.concatenate([oa[:800], _offsets(3, 800)])]
+    out["card"] = [bs(b"a").bitcount(), bs(b"b").bitcount(), 0]
+    out["len"] = [len(bs(b"a").bytes()), len(bs(b"b").bytes()), 0]
+    out["size"] = len(bs(b"a").bytes()) * 8
+    out["bytes_a"] = bs(b"a").bytes()
+    setbits(b"a2", oa[500:], 1)
+    out["and"] = O.bitop("AND", [bs(b"a2").bytes(), bs(b"b").bytes()])
+    setbits(b"a3", oa[500:], 1)
+    out["or"] = O.bitop("OR", [bs(b"a3").bytes(), bs(b"b").bytes(), None])
+    setbits(b"a4", ob, 1)
+    out["xor"] = O.bitop("XOR", [bs(b"a4").bytes(), bs(b"b").bytes()])
+    nb = O.bitop("NOT", [bs(b"b").bytes()])
+    out["not_b"] = nb
+    out["card_not_b"] = int(np.unpackbits(np.frombuffer(nb, np.uint8)).sum())
+    keys = {}
+    for i, k in enumerate(KEYS[:5]):
+        offs = _offsets(10 + i, 300 + 200 * i) % np.uint64(NBITS >> (i % 3))
+        setbits(k, offs, 1)
+        keys[k] = bs(k).bytes()
+    res = {}
+    for op, dest, srcs in (("OR", b"kd:or", KEYS[:5]), ("AND", b"kd:and", KEYS[:3]),
+                           ("XOR", b"kd:xor", [KEYS[1], KEYS[4], KEYS[5]]), ("NOT", b"kd:not", [KEYS[2]])):
+        v = O.bitop(op, [keys.get(k) for k in srcs])
+        res[op] = (len(v), v if v else None)
+    out["keyed"] = res
+    return out
+
+
+def check(got, want, rank, world):
+    from redisson_amd import owner
+
+    for k in ("set_a", "set_b", "clear_a", "get_a"):
+        assert [int(x) for x in got[k]] == [int(x) for x in want[k]], k
+    for k in ("card", "len", "size", "bytes_a", "and", "or", "xor", "not_b", "card_not_b"):
+        assert got[k] == want[k], k
+    for op, (n, val) in want["keyed"].items():
+        gn, gval = got["keyed"][op]
+        assert gn == n, op
+        dest = {"OR": b"kd:or", "AND": b"kd:and", "XOR": b"kd:xor", "NOT": b"kd:not"}[op]
+        if owner(dest, world) == rank:
+            assert gval == val, op
+
+
+class OracleBitEngine:
+    """The engine methods the cluster protocols call, over oracle bit strings (CPU tests only)."""
+
+    def __init__(self):
+        from oracle import oracle as O
+
+        self.O = O
+        self.s = {}
+
+    def _bs(self, k):
+        return self.s.setdefault(bytes(k), self.O.BitString(16))
+
+    def key_type(self, k):
+        return 2 if bytes(k) in self.s else 0
+
+    def setbit(self, keys, offsets, values, want_old=True):
+        vals = np.broadcast_to(np.asarray(values, dtype=np.uint8), (len(keys),))
+        old = [self._bs(k).setbit(int(o), int(v)) for k, o, v in zip(keys, offsets, vals)]
+        return old if want_old else None
+
+    def getbit(self, keys, offsets):
+        return [self.s[bytes(k)].getbit(int(o)) if bytes(k) in self.s else 0 for k, o in zip(keys, offsets)]
+
+    def strlen(self, k):
+        return len(self.s[bytes(k)].bytes()) if bytes(k) in self.s else 0
+
+    def bitcount(self, k):
+        return self.s[bytes(k)].bitcount() if bytes(k) in self.s else 0
+
+    def get(self, k):
+        return self.s[bytes(k)].bytes() if bytes(k) in self.s else None
+
+    def set(self, k, v):
+        b = self.O.BitString(len(v) + 16)
+        b.buf[:len(v)] = np.frombuffer(bytes(v), np.uint8)
+        b.len.value = len(v)
+        self.s[bytes(k)] = b
+
+    def delete(self, keys):
+        n = 0
+        for k in keys:
+            n += self.s.pop(bytes(k), None) is not None
+        return n
+
+    def bitop(self, op, dest, srcs):
+        v = self.O.bitop(op.upper(), [self.get(k) for k in srcs])
+        if v:
+            self.set(dest, v)
+        else:
+            self.s.pop(bytes(dest), None)
+        return len(v)

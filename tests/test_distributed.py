@@ -1,8 +1,10 @@
-"""Multi-rank protocol on CPU (gloo, world size 2) and the RCCL wiring on one GPU.
+"""Multi-rank protocols on CPU (gloo, world size 2) and on the GPU (RCCL at world 1; two engine contexts sharing the
+GPU over gloo at world 2).
 
-CPU: the partitioner gives every key exactly one owner; the global
-countWith protocol (local union -> MAX all-reduce -> estimator) equals the
-single-process oracle count of the union; range-sharded BITCOUNT sums.
+CPU: the partitioner gives every key exactly one owner; the global countWith protocol (local union -> MAX
+all-reduce -> estimator) equals the single-process oracle count of the union; range-sharded BITCOUNT sums; the
+range-sharded RBitSet (SETBIT/GETBIT replies, BITCOUNT, length, GET, BITOP AND/OR/XOR/NOT) and BITOP over whole
+keys on different owners (one all-gather + a local op) equal one oracle store's results.
 """
 import os
 import socket
@@ -80,6 +82,73 @@ def test_global_countwith_and_bitcount_two_ranks(O):
     assert ret[0][0] == ret[1][0] == want
     assert ret[0][1] == ret[1][1] == ret[0][3]
     assert sum(ret[0][2]) == len(keys)
+
+
+def _bitset_worker(rank, world, port, ret, use_gpu):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import torch.distributed as dist
+
+    from redisson_amd.cluster import HostCollective
+    from tests._sharded_scenario import OracleBitEngine, check, expected, run_scenario
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    if use_gpu:
+        from redisson_amd import SketchEngine
+        eng = SketchEngine(device=0)
+    else:
+        eng = OracleBitEngine()
+    try:
+        got = run_scenario(eng, rank, world, HostCollective(dist))
+        check(got, expected(), rank, world)
+        ret[rank] = "ok"
+    except Exception as e:  # reported through the manager: the assertion text reaches the parent
+        import traceback
+        ret[rank] = traceback.format_exc()
+    finally:
+        if use_gpu:
+            eng.close()
+        dist.destroy_process_group()
+
+
+def _run_world(world, use_gpu):
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    mgr = ctx.Manager()
+    ret = mgr.dict()
+    procs = [ctx.Process(target=_bitset_worker, args=(r, world, port, ret, use_gpu)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(180)
+        assert p.exitcode == 0
+    for r in range(world):
+        assert ret[r] == "ok", ret[r]
+
+
+def test_sharded_bitset_and_keyed_bitop_two_ranks():
+    """C5 across GPUs, protocol on CPU: a 2^20-bit RBitSet range-sharded over 2 ranks and BITOP over keys owned by
+    different ranks give one oracle store's replies and strings."""
+    _run_world(2, False)
+
+
+@pytest.mark.gpu
+def test_sharded_bitset_engine_two_ranks_one_gpu():
+    """The same scenario on two SketchEngine contexts (two processes sharing the GPU), collectives over gloo."""
+    _run_world(2, True)
+
+
+@pytest.mark.gpu
+def test_sharded_bitset_engine_rccl_world1(engine):
+    """The same scenario on the engine with its RCCL communicator at world size 1: device all-gather, get_dev /
+    set_dev of the gathered operands, u8 MAX / u64 SUM all-reduces."""
+    from redisson_amd.cluster import RcclCollective
+    from tests._sharded_scenario import check, expected, run_scenario
+
+    coll = RcclCollective(engine, 0, 1)
+    check(run_scenario(engine, 0, 1, coll), expected(), 0, 1)
 
 
 def test_partition_colocates_hashtags():

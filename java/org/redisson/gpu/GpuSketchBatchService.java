@@ -4,12 +4,15 @@
  * CommandBatchService queues (BatchCommandData) per slot with a global index
  * (M:command/CommandBatchService.java:91-111) and answers in enqueue order
  * (:163-171).  This subclass executes the sketch commands of the batch on the
- * GPU instead: the queue is replayed in index order, consecutive commands of
+ * GPU instead: the queue is replayed in enqueue order, consecutive commands of
  * the same kind (PFADD / GETBIT / SETBIT / PFCOUNT) become ONE device batch
- * (exact sequential replies inside the batch, sk_pfadd / sk_setbit), and any
- * error fails the whole batch future with the last error, as CommandDecoder
- * does (M:client/handler/CommandDecoder.java:183-197).  Non-sketch commands of
- * the same batch still go to redis-server through super.executeAsync().
+ * (exact sequential replies inside the batch, sk_pfadd / sk_setbit /
+ * sk_pfcount).  The batch's other commands still go to redis-server through
+ * super.executeAsync(), even when a sketch command failed, as the reference
+ * pipeline executes every command (:142-182).  The result list holds every
+ * command's reply in enqueue order, sketch and redis alike; if any command
+ * failed the future fails with the error of the last failed command in that
+ * order, as CommandDecoder does (M:client/handler/CommandDecoder.java:183-197).
  * Source only here; see INTEGRATION.md.
  */
 package org.redisson.gpu;
@@ -22,11 +25,13 @@ import java.util.Set;
 import org.redisson.client.RedisException;
 import org.redisson.client.codec.Codec;
 import org.redisson.client.protocol.RedisCommand;
+import org.redisson.client.protocol.RedisCommands;
 import org.redisson.command.CommandBatchService;
 import org.redisson.connection.ConnectionManager;
 import org.redisson.connection.NodeSource;
 
 import io.netty.util.concurrent.Future;
+import io.netty.util.concurrent.FutureListener;
 import io.netty.util.concurrent.Promise;
 
 public class GpuSketchBatchService extends CommandBatchService {
@@ -48,7 +53,10 @@ public class GpuSketchBatchService extends CommandBatchService {
 
     final long ctx;
     final List<Cmd> sketch = new ArrayList<Cmd>();
+    final List<Promise<?>> order = new ArrayList<Promise<?>>(); // every command's promise, enqueue order
     final Set<String> touched = new HashSet<String>();
+    boolean redisUsed;
+    boolean executed;
 
     public GpuSketchBatchService(ConnectionManager connectionManager, long ctx) {
         super(connectionManager);
@@ -58,12 +66,21 @@ public class GpuSketchBatchService extends CommandBatchService {
     @Override
     protected <V, R> void async(boolean readOnlyMode, NodeSource nodeSource, Codec codec, RedisCommand<V> command,
                                 Object[] params, Promise<R> mainPromise, int attempt) {
+        if (executed) {
+            throw new IllegalStateException("Batch already has been executed!");
+        }
+        order.add(mainPromise);
         String name = command.getName();
-        // GET / SET / DEL join the sketch queue when the engine holds the key, or an earlier sketch command of
-        // this batch names it (it may create the key before this one runs)
+        if ("DEL".equals(name) && params.length > 0) {
+            delAsync(readOnlyMode, nodeSource, codec, command, params, mainPromise, attempt);
+            return;
+        }
+        // GET / SET join the sketch queue when the engine holds the key, or an earlier sketch command of this
+        // batch names it (it may create the key before this one runs)
         boolean keyCommand = GpuSketchCommandService.KEY_COMMANDS.contains(name) && params.length > 0
                 && (touched.contains(params[0].toString()) || SketchDispatch.engineHolds(ctx, params[0]));
         if (!keyCommand && !GpuSketchCommandService.SKETCH_COMMANDS.contains(name)) {
+            redisUsed = true;
             super.async(readOnlyMode, nodeSource, codec, command, params, mainPromise, attempt);
             return;
         }
@@ -73,9 +90,55 @@ public class GpuSketchBatchService extends CommandBatchService {
         sketch.add(new Cmd(codec, command, params, mainPromise));
     }
 
+    /* DEL inside a batch, split by holder: the engine part runs in the sketch queue at the command's place, the
+     * redis part joins the redis batch; the command's promise gets the sum once both are done. */
+    @SuppressWarnings({"unchecked", "rawtypes"})
+    <V, R> void delAsync(boolean readOnlyMode, NodeSource nodeSource, Codec codec, final RedisCommand<V> command,
+                         Object[] params, final Promise<R> mainPromise, int attempt) {
+        List<Object>[] parts = SketchDispatch.splitDel(ctx, params, touched);
+        if (parts[0].isEmpty()) {
+            redisUsed = true;
+            super.async(readOnlyMode, nodeSource, codec, command, params, mainPromise, attempt);
+            return;
+        }
+        if (parts[1].isEmpty()) {
+            sketch.add(new Cmd(codec, command, params, mainPromise));
+            return;
+        }
+        final Promise<Object> engine = getConnectionManager().newPromise();
+        final Promise<Object> redis = getConnectionManager().newPromise();
+        FutureListener<Object> both = new FutureListener<Object>() {
+            @Override
+            public void operationComplete(Future<Object> f) throws Exception {
+                if (!engine.isDone() || !redis.isDone()) {
+                    return;
+                }
+                if (!engine.isSuccess()) {
+                    mainPromise.tryFailure(engine.cause());
+                } else if (!redis.isSuccess()) {
+                    mainPromise.tryFailure(redis.cause());
+                } else {
+                    long n = ((Number) engine.getNow()).longValue() + ((Number) redis.getNow()).longValue();
+                    mainPromise.trySuccess((R) GpuSketchCommandService.convert(command, Long.valueOf(n)));
+                }
+            }
+        };
+        engine.addListener(both);
+        redis.addListener(both);
+        sketch.add(new Cmd(codec, RedisCommands.DEL, parts[0].toArray(), engine));
+        redisUsed = true;
+        super.async(readOnlyMode, nodeSource, codec, RedisCommands.DEL, parts[1].toArray(), (Promise) redis, attempt);
+    }
+
     @Override
     public Future<List<?>> executeAsync() {
-        RedisException last = null;
+        if (executed) {
+            throw new IllegalStateException("Batch already executed!");
+        }
+        if (order.isEmpty()) {
+            return getConnectionManager().newSucceededFuture(null);
+        }
+        executed = true;
         int i = 0;
         while (i < sketch.size()) {
             String kind = sketch.get(i).command.getName();
@@ -86,19 +149,43 @@ public class GpuSketchBatchService extends CommandBatchService {
             try {
                 runBatch(sketch.subList(i, j));
             } catch (RedisException e) {
-                last = e;
                 for (Cmd c : sketch.subList(i, j)) {
                     c.promise.tryFailure(e);
                 }
             }
             i = j;
         }
-        if (last != null) {
-            Promise<List<?>> p = getConnectionManager().newPromise();
-            p.setFailure(last);
-            return p;
-        }
-        return super.executeAsync(); // gathers every promise (sketch ones are complete) in index order
+        // the redis-side commands are sent whatever happened above (the reference pipeline executes them all)
+        Future<List<?>> redis = redisUsed ? super.executeAsync()
+                : getConnectionManager().<List<?>>newSucceededFuture(null);
+        final Promise<List<?>> result = getConnectionManager().newPromise();
+        redis.addListener(new FutureListener<List<?>>() {
+            @Override
+            public void operationComplete(Future<List<?>> f) throws Exception {
+                Throwable last = null;
+                List<Object> out = new ArrayList<Object>(order.size());
+                for (Promise<?> p : order) {
+                    if (!p.isDone()) { // a redis command the failed batch never answered
+                        last = f.isSuccess() ? new RedisException("batch command not executed") : f.cause();
+                        out.add(null);
+                        continue;
+                    }
+                    if (!p.isSuccess()) {
+                        last = p.cause();
+                    }
+                    out.add(p.getNow());
+                }
+                if (last == null && !f.isSuccess()) {
+                    last = f.cause();
+                }
+                if (last != null) {
+                    result.setFailure(last);
+                } else {
+                    result.setSuccess(out);
+                }
+            }
+        });
+        return result;
     }
 
     static boolean runnable(String kind) {
@@ -109,20 +196,38 @@ public class GpuSketchBatchService extends CommandBatchService {
         String kind = run.get(0).command.getName();
         if (!runnable(kind) || run.size() == 1) {
             for (Cmd c : run) {
-                Object reply = GpuSketchCommandService.KEY_COMMANDS.contains(c.command.getName())
-                        ? SketchDispatch.keyCommand(ctx, c.codec, c.command, c.params)
-                        : SketchDispatch.single(ctx, c.codec, c.command, c.params);
-                c.promise.setSuccess(GpuSketchCommandService.convert(c.command, reply));
+                try {
+                    Object reply = GpuSketchCommandService.KEY_COMMANDS.contains(c.command.getName())
+                            ? SketchDispatch.keyCommand(ctx, c.codec, c.command, c.params)
+                            : SketchDispatch.single(ctx, c.codec, c.command, c.params);
+                    c.promise.setSuccess(GpuSketchCommandService.convert(c.command, reply));
+                } catch (RedisException e) { // this command alone fails (pipeline semantics)
+                    c.promise.tryFailure(e);
+                }
             }
             return;
         }
         try {
+            int n = run.size();
+            if ("PFCOUNT".equals(kind)) { // one sk_pfcount for the run
+                List<RedisCommand<?>> cmds = new ArrayList<RedisCommand<?>>();
+                List<Object[]> params = new ArrayList<Object[]>();
+                for (Cmd c : run) {
+                    cmds.add(c.command);
+                    params.add(c.params);
+                }
+                long[] counts = SketchDispatch.pfcountRun(ctx, run.get(0).codec, cmds, params);
+                for (int c = 0; c < n; c++) {
+                    run.get(c).promise.setSuccess(GpuSketchCommandService.convert(run.get(c).command,
+                            Long.valueOf(counts[c])));
+                }
+                return;
+            }
             List<byte[]> keys = new ArrayList<byte[]>();
             for (Cmd c : run) {
                 keys.add(GpuSketchCommandService.encodeParam(c.codec, c.command, c.params[0], 1));
             }
             SketchDispatch.Packed k = new SketchDispatch.Packed(keys);
-            int n = run.size();
             byte[] out = new byte[n];
             if ("PFADD".equals(kind)) {
                 List<byte[]> elems = new ArrayList<byte[]>();
@@ -136,12 +241,6 @@ public class GpuSketchBatchService extends CommandBatchService {
                 }
                 SketchDispatch.Packed e = new SketchDispatch.Packed(elems);
                 SketchDispatch.pfaddRun(ctx, keys, k, counts, e, out);
-            } else if ("PFCOUNT".equals(kind)) {
-                for (Cmd c : run) {
-                    c.promise.setSuccess(GpuSketchCommandService.convert(c.command,
-                            SketchDispatch.single(ctx, c.codec, c.command, c.params)));
-                }
-                return;
             } else {
                 long[] offs = new long[n];
                 byte[] vals = new byte[n];

@@ -9,6 +9,7 @@ package org.redisson.gpu;
 
 import java.io.ByteArrayOutputStream;
 import java.nio.charset.Charset;
+import java.util.ArrayList;
 import java.util.List;
 import java.util.concurrent.ConcurrentHashMap;
 
@@ -16,15 +17,15 @@ import org.redisson.client.RedisException;
 import org.redisson.client.codec.Codec;
 import org.redisson.client.protocol.RedisCommand;
 
-final class SketchDispatch {
+public final class SketchDispatch {
     private SketchDispatch() {
     }
 
-    static final class Packed {
-        final long[] off;
-        final byte[] bytes;
+    public static final class Packed {
+        public final long[] off;
+        public final byte[] bytes;
 
-        Packed(List<byte[]> items) {
+        public Packed(List<byte[]> items) {
             off = new long[items.size() + 1];
             ByteArrayOutputStream out = new ByteArrayOutputStream();
             for (int i = 0; i < items.size(); i++) {
@@ -39,8 +40,11 @@ final class SketchDispatch {
 
     static final Charset ISO = Charset.forName("ISO-8859-1"); // bytes <-> String one to one
 
-    /* Per-context HLL name -> slab id cache (INTEGRATION.md "Caching slab ids").  Filled after a key's first
-     * name-path PFADD; keyCommand's DEL drops the deleted keys' entries. */
+    /* Per-context HLL name -> slab handle cache (INTEGRATION.md "Caching slab ids").  Filled after a run's
+     * name-path PFADD from sk_hll_lookup (which creates nothing).  Every command that can free or replace a key
+     * drops the key's entry (DEL, SET, BITOP / PFMERGE destinations, FLUSHALL); a handle cached across a race
+     * anyway is refused by the engine (SK_ESTALE: the slab's generation changed) and the run is redone by name,
+     * so a stale id can never write into a slab another key owns. */
     static final ConcurrentHashMap<Long, ConcurrentHashMap<String, Integer>> SLAB_IDS =
             new ConcurrentHashMap<Long, ConcurrentHashMap<String, Integer>>();
 
@@ -56,8 +60,16 @@ final class SketchDispatch {
         return m;
     }
 
-    /* A run of PFADD commands: sk_pfadd_ids when every key has a cached slab id, else sk_pfadd by name,
-     * then the run's keys are resolved (they exist now; nothing is created) and cached. */
+    static void invalidate(long ctx, byte[] key) {
+        slabIds(ctx).remove(new String(key, ISO));
+    }
+
+    static void invalidateAll(long ctx) {
+        slabIds(ctx).clear();
+    }
+
+    /* A run of PFADD commands: sk_pfadd_ids when every key has a cached slab handle, else sk_pfadd by name, then
+     * the run's keys are looked up (they exist now; nothing is created) and cached. */
     static void pfaddRun(long ctx, List<byte[]> keys, Packed k, int[] counts, Packed e, byte[] out) {
         ConcurrentHashMap<String, Integer> cache = slabIds(ctx);
         int n = keys.size();
@@ -72,19 +84,26 @@ final class SketchDispatch {
             }
         }
         if (cached) {
-            check(ctx, SketchNative.pfaddIds(ctx, ids, counts, e.off, e.bytes, out));
-            return;
+            int st = SketchNative.pfaddIds(ctx, ids, counts, e.off, e.bytes, out);
+            if (st != SketchNative.SK_ESTALE) {
+                check(ctx, st);
+                return;
+            }
+            for (byte[] key : keys) { // a key of the run was freed since it was cached: redo the run by name
+                cache.remove(new String(key, ISO));
+            }
         }
         check(ctx, SketchNative.pfadd(ctx, k.off, k.bytes, counts, e.off, e.bytes, out));
-        byte[] created = new byte[n];
-        if (SketchNative.hllResolve(ctx, k.off, k.bytes, ids, created) == SketchNative.SK_OK) {
+        if (SketchNative.hllLookup(ctx, k.off, k.bytes, ids) == SketchNative.SK_OK) {
             for (int c = 0; c < n; c++) {
-                cache.put(new String(keys.get(c), ISO), Integer.valueOf(ids[c]));
+                if (ids[c] != -1) {
+                    cache.put(new String(keys.get(c), ISO), Integer.valueOf(ids[c]));
+                }
             }
         }
     }
 
-    static void check(long ctx, int st) {
+    public static void check(long ctx, int st) {
         if (st == SketchNative.SK_OK) {
             return;
         }
@@ -97,28 +116,43 @@ final class SketchDispatch {
         throw new RedisException(SketchNative.lastError(ctx));
     }
 
+    static byte[] keyBytes(Object key) {
+        return key instanceof byte[] ? (byte[]) key : key.toString().getBytes(GpuSketchCommandService.UTF8);
+    }
+
     static boolean engineHolds(long ctx, Object key) {
         int[] t = new int[1];
-        byte[] k = key instanceof byte[] ? (byte[]) key : key.toString().getBytes(GpuSketchCommandService.UTF8);
-        return SketchNative.type(ctx, k, t) == SketchNative.SK_OK && t[0] != SketchNative.SK_TYPE_NONE;
+        return SketchNative.type(ctx, keyBytes(key), t) == SketchNative.SK_OK && t[0] != SketchNative.SK_TYPE_NONE;
+    }
+
+    /* DEL k1..kn splits by holder (ADVICE r1): the keys the engine holds are removed there, the rest (the Bloom
+     * filter's "{name}__config" hash when redis-server keeps it, RBucket keys, ...) go to redis-server, and the
+     * reply is the sum.  out[0] = engine-held keys, out[1] = the others. */
+    static List<Object>[] splitDel(long ctx, Object[] params, java.util.Set<String> alsoEngine) {
+        @SuppressWarnings("unchecked")
+        List<Object>[] out = new List[] {new ArrayList<Object>(), new ArrayList<Object>()};
+        for (Object p : params) {
+            boolean eng = engineHolds(ctx, p) || (alsoEngine != null && alsoEngine.contains(p.toString()));
+            out[eng ? 0 : 1].add(p);
+        }
+        return out;
     }
 
     /* GET / SET / DEL on a key the engine holds (engineHolds of the first key).  GET decodes the raw bytes with
      * the command's codec (ByteArrayCodec for RBitSet: the bytes as they are); SET writes the encoded value;
-     * DEL removes the keys the engine holds and replies their number. */
+     * DEL removes the given keys from the engine and replies their number. */
     static Object keyCommand(long ctx, Codec codec, RedisCommand<?> command, Object[] params) {
         try {
             String name = command.getName();
             if ("DEL".equals(name)) {
-                java.util.ArrayList<byte[]> keys = new java.util.ArrayList<byte[]>();
-                for (Object p : params) {
-                    keys.add(p.toString().getBytes(GpuSketchCommandService.UTF8));
+                ArrayList<byte[]> keys = new ArrayList<byte[]>();
+                for (int i = 0; i < params.length; i++) {
+                    keys.add(GpuSketchCommandService.encodeParam(codec, command, params[i], i + 1));
                 }
                 Packed k = new Packed(keys);
                 long[] removed = new long[1];
-                ConcurrentHashMap<String, Integer> cache = slabIds(ctx);
                 for (byte[] kb : keys) {
-                    cache.remove(new String(kb, ISO)); // the slab id may be handed to another key
+                    invalidate(ctx, kb); // the slab may be handed to another key
                 }
                 check(ctx, SketchNative.del(ctx, k.off, k.bytes, removed));
                 return Long.valueOf(removed[0]);
@@ -132,6 +166,7 @@ final class SketchDispatch {
                 return codec.getValueDecoder().decode(io.netty.buffer.Unpooled.wrappedBuffer(v), null);
             }
             byte[] v = GpuSketchCommandService.encodeParam(codec, command, params[1], 2);
+            invalidate(ctx, key); // SET replaces whatever the key held (an HLL's slab is freed)
             check(ctx, SketchNative.set(ctx, key, v));
             return "OK";
         } catch (RedisException e) {
@@ -141,12 +176,32 @@ final class SketchDispatch {
         }
     }
 
+    /* One PFCOUNT per command, all of a run's commands in one sk_pfcount (single keys share one histogram
+     * launch; multi-key commands are unions). */
+    static long[] pfcountRun(long ctx, Codec codec, List<RedisCommand<?>> commands, List<Object[]> paramsList)
+            throws Exception {
+        int n = paramsList.size();
+        int[] nk = new int[n];
+        ArrayList<byte[]> keys = new ArrayList<byte[]>();
+        for (int c = 0; c < n; c++) {
+            Object[] params = paramsList.get(c);
+            nk[c] = params.length;
+            for (int i = 0; i < params.length; i++) {
+                keys.add(GpuSketchCommandService.encodeParam(codec, commands.get(c), params[i], i + 1));
+            }
+        }
+        Packed k = new Packed(keys);
+        long[] out = new long[n];
+        check(ctx, SketchNative.pfcount(ctx, nk, k.off, k.bytes, out));
+        return out;
+    }
+
     static Object single(long ctx, Codec codec, RedisCommand<?> command, Object[] params) {
         try {
             String name = command.getName();
             byte[] key = GpuSketchCommandService.encodeParam(codec, command, params[0], 1);
             if ("PFADD".equals(name)) {
-                java.util.ArrayList<byte[]> elems = new java.util.ArrayList<byte[]>();
+                ArrayList<byte[]> elems = new ArrayList<byte[]>();
                 for (int i = 1; i < params.length; i++) {
                     elems.add(GpuSketchCommandService.encodeParam(codec, command, params[i], i + 1));
                 }
@@ -157,14 +212,8 @@ final class SketchDispatch {
                 return Long.valueOf(out[0]);
             }
             if ("PFCOUNT".equals(name)) {
-                java.util.ArrayList<byte[]> keys = new java.util.ArrayList<byte[]>();
-                for (Object p : params) {
-                    keys.add(p.toString().getBytes(GpuSketchCommandService.UTF8));
-                }
-                Packed k = new Packed(keys);
-                long[] out = new long[1];
-                check(ctx, SketchNative.pfcount(ctx, new int[] {keys.size()}, k.off, k.bytes, out));
-                return Long.valueOf(out[0]);
+                return Long.valueOf(pfcountRun(ctx, codec, java.util.Collections.<RedisCommand<?>>singletonList(command),
+                        java.util.Collections.singletonList(params))[0]);
             }
             if ("GETBIT".equals(name) || "SETBIT".equals(name)) {
                 Packed k = new Packed(java.util.Collections.singletonList(key));
@@ -187,18 +236,20 @@ final class SketchDispatch {
             // PFMERGE dest srcs... / BITOP op dest srcs...
             boolean bitop = "BITOP".equals(name);
             int first = bitop ? 2 : 1;
-            java.util.ArrayList<byte[]> srcs = new java.util.ArrayList<byte[]>();
+            ArrayList<byte[]> srcs = new ArrayList<byte[]>();
             for (int i = first; i < params.length; i++) {
-                srcs.add(params[i].toString().getBytes(GpuSketchCommandService.UTF8));
+                srcs.add(GpuSketchCommandService.encodeParam(codec, command, params[i], i + 1));
             }
             Packed s = new Packed(srcs);
             if (bitop) {
                 int op = java.util.Arrays.asList("AND", "OR", "XOR", "NOT").indexOf(params[0].toString());
+                byte[] dest = GpuSketchCommandService.encodeParam(codec, command, params[1], 2);
+                invalidate(ctx, dest); // BITOP replaces its destination (an HLL there is freed)
                 long[] len = new long[1];
-                check(ctx, SketchNative.bitop(ctx, op, params[1].toString().getBytes(GpuSketchCommandService.UTF8),
-                        s.off, s.bytes, len));
+                check(ctx, SketchNative.bitop(ctx, op, dest, s.off, s.bytes, len));
                 return Long.valueOf(len[0]);
             }
+            invalidate(ctx, key); // PFMERGE destination (a string there is adopted or refused, never reused)
             check(ctx, SketchNative.pfmerge(ctx, key, s.off, s.bytes));
             return "OK";
         } catch (RedisException e) {

@@ -15,7 +15,8 @@ public final class SketchNative {
     }
 
     public static final int SK_OK = 0, SK_EWRONGTYPE = -1, SK_ERANGE = -2, SK_ECONFIG = -3, SK_ENOTINIT = -4,
-            SK_EDEVICE = -5, SK_EINVAL = -6, SK_ENOMEM = -7, SK_ESYNTAX = -8, SK_ETOOBIG = -9;
+            SK_EDEVICE = -5, SK_EINVAL = -6, SK_ENOMEM = -7, SK_ESYNTAX = -8, SK_ETOOBIG = -9, SK_ECORRUPT = -10,
+            SK_ESTALE = -11;
 
     public static native long open(int device, int redisMajor, long maxBitOffset, long hllCapacity, long maxBatch);
     public static native void close(long ctx);
@@ -27,7 +28,9 @@ public final class SketchNative {
                                    byte[] elems, byte[] outChanged);
     /** sk_hll_resolve: name -> slab id, creating empty HLLs (outCreated[i] = 1 if this call created key i). */
     public static native int hllResolve(long ctx, long[] keyOff, byte[] keys, int[] outIds, byte[] outCreated);
-    /** sk_pfadd_ids: slab ids from a cached sk_hll_resolve (dropped on DEL / flushall). */
+    /** sk_hll_lookup: name -> slab handle of EXISTING HLLs (-1 = missing), creating nothing. */
+    public static native int hllLookup(long ctx, long[] keyOff, byte[] keys, int[] outIds);
+    /** sk_pfadd_ids: slab handles from a cached sk_hll_resolve; SK_ESTALE once the key was deleted / replaced. */
     public static native int pfaddIds(long ctx, int[] keyIds, int[] elemCounts, long[] elemOff, byte[] elems,
                                       byte[] outChanged);
     public static native int pfcount(long ctx, int[] nkeys, long[] keyOff, byte[] keys, long[] outCounts);

@@ -79,6 +79,17 @@ JNIEXPORT jint JNICALL Java_org_redisson_gpu_SketchNative_hllResolve(JNIEnv *env
     return st;
 }
 
+JNIEXPORT jint JNICALL Java_org_redisson_gpu_SketchNative_hllLookup(JNIEnv *env, jclass cls, jlong ctx,
+                                                                    jlongArray koff, jbyteArray keys,
+                                                                    jintArray out_ids) {
+    (void)cls;
+    jsize n = LEN(out_ids);
+    void *ko = PIN(koff), *k = PIN(keys), *i = PIN(out_ids);
+    jint st = sk_hll_lookup(CTX(ctx), (uint32_t)n, (const uint64_t *)ko, (const uint8_t *)k, (uint32_t *)i);
+    UNPIN(out_ids, i, 0); UNPIN(keys, k, JNI_ABORT); UNPIN(koff, ko, JNI_ABORT);
+    return st;
+}
+
 /* sk_pfadd_ids: keys resolved once per tenant (SketchNative.hllResolve) and cached on the Java side */
 JNIEXPORT jint JNICALL Java_org_redisson_gpu_SketchNative_pfaddIds(JNIEnv *env, jclass cls, jlong ctx, jintArray ids,
                                                                    jintArray counts, jlongArray eoff,

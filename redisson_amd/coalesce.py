@@ -1,0 +1,145 @@
+"""Group commit of concurrent RBloomFilter calls.
+
+The reference pays one pipeline round trip per element: every ``add`` / ``contains`` is its own
+CommandBatchService with the config-check EVAL and k SETBIT / GETBIT (M:RedissonBloomFilter.java:94-100,
+147-153), and RBatch has no Bloom filter (M:RedissonBatch.java).  On the GPU one element per launch would waste
+the device, so concurrent calls are coalesced: callers (Netty event-loop threads in the Java executor) only
+enqueue and get a future; one completion thread drains the queue in FIFO order, merges each maximal run of
+requests for the same (filter, operation, size, k) into ONE engine call, splits the replies and completes the
+futures.  A run never crosses a request of another kind or filter, so every caller sees the linearizable
+result of the FIFO order (an add is never moved across a contains, or the reverse).  Replies inside a merged
+add run are the engine's exact sequential replies of the concatenation, i.e. of the requests in FIFO order.
+
+A request carries the (size, k) its caller read; the engine checks them against the stored config and fails
+the run with "Bloom filter config has been changed" if they differ, which the caller's retry loop handles
+exactly as RedissonBloomFilter does (:108-111, :162-166).
+"""
+from __future__ import annotations
+
+import collections
+import contextlib
+import threading
+from typing import List, Optional, Sequence
+
+from .redisson import Future
+
+
+class WaitFuture(Future):
+    """A Future another thread completes; get() blocks until it is done."""
+
+    def __init__(self):
+        super().__init__()
+        self._ev = threading.Event()
+
+    def _set(self, v):
+        super()._set(v)
+        self._ev.set()
+
+    def _fail(self, e):
+        super()._fail(e)
+        self._ev.set()
+
+    def get(self, timeout: Optional[float] = None):
+        if not self._ev.wait(timeout):
+            raise TimeoutError("Bloom request not completed")
+        return super().get()
+
+    getNow = Future.get
+    sync = get
+
+
+class _Req:
+    __slots__ = ("name", "kind", "size", "k", "elems", "future")
+
+    def __init__(self, name, kind, size, k, elems):
+        self.name, self.kind, self.size, self.k, self.elems = name, kind, size, k, elems
+        self.future = WaitFuture()
+
+    def key(self):
+        return (self.name, self.kind, self.size, self.k)
+
+
+class BloomCoalescer:
+    """One completion thread per engine context; `submit` never blocks on the device."""
+
+    def __init__(self, engine, max_batch: int = 1 << 22, record: bool = False):
+        self.engine = engine
+        self.max_batch = max_batch
+        self._q: collections.deque = collections.deque()
+        self._cv = threading.Condition()
+        self._stop = False
+        self._held = 0
+        self.calls = 0                 # engine calls made (one per merged run)
+        self.requests = 0              # requests completed
+        # per run, in execution order: (kind, [(request elems, its future), ...]) -- replay tests only
+        self.log: Optional[List] = [] if record else None
+        self._t = threading.Thread(target=self._loop, name="sk-bloom-coalescer", daemon=True)
+        self._t.start()
+
+    def submit(self, name, kind: str, size: int, k: int, elems: Sequence[bytes]) -> WaitFuture:
+        if kind not in ("add", "contains"):
+            raise ValueError(kind)
+        r = _Req(name, kind, int(size), int(k), list(elems))
+        with self._cv:
+            if self._stop:
+                raise RuntimeError("coalescer closed")
+            self._q.append(r)
+            self._cv.notify()
+        return r.future
+
+    @contextlib.contextmanager
+    def hold(self):
+        """Let requests queue up without draining (tests / explicit group commit)."""
+        with self._cv:
+            self._held += 1
+        try:
+            yield self
+        finally:
+            with self._cv:
+                self._held -= 1
+                self._cv.notify()
+
+    def close(self):
+        with self._cv:
+            self._stop = True
+            self._cv.notify()
+        self._t.join()
+
+    def _take_run(self) -> List[_Req]:
+        head = self._q.popleft()
+        run, n = [head], len(head.elems)
+        key = head.key()
+        while self._q and self._q[0].key() == key and n + len(self._q[0].elems) <= self.max_batch:
+            r = self._q.popleft()
+            run.append(r)
+            n += len(r.elems)
+        return run
+
+    def _loop(self):
+        while True:
+            with self._cv:
+                while not self._stop and (not self._q or self._held):
+                    self._cv.wait()
+                if not self._q:
+                    return                      # stopped and drained
+                run = self._take_run()
+            self._execute(run)
+
+    def _execute(self, run: List[_Req]):
+        head = run[0]
+        elems = [e for r in run for e in r.elems]
+        fn = self.engine.bloom_add if head.kind == "add" else self.engine.bloom_contains
+        try:
+            res = fn(head.name, head.size, head.k, elems) if elems else []
+        except Exception as e:  # noqa: BLE001 - every request of the run sees the engine's error
+            for r in run:
+                r.future._fail(e)
+        else:
+            p = 0
+            for r in run:
+                r.future._set(list(res[p:p + len(r.elems)]))
+                p += len(r.elems)
+            if self.log is not None:
+                self.log.append((head.kind, [(r.elems, r.future) for r in run]))
+        self.calls += 1
+        self.requests += len(run)

@@ -78,6 +78,9 @@ class Config:
     hll_capacity: int = 0
     max_batch: int = 0
     codec: Codec = field(default_factory=JsonJacksonCodec)   # M:Config.java:68-70
+    # group commit of concurrent RBloomFilter add/contains calls (redisson_amd/coalesce.py): callers only enqueue,
+    # one completion thread merges FIFO runs into single engine calls
+    bloom_coalesce: bool = False
 
 
 class JBitSet:
@@ -309,10 +312,14 @@ class RBloomFilter(RObject):
 
     def _run(self, fn, objs):
         elems = [self.codec.encode(o) for o in objs]
+        co = getattr(self._c, "bloom_coalescer", None)
         while True:
             if self._size == 0:
                 self._read_config()
             try:
+                if co is not None:   # group commit: merged with concurrent callers' requests into one engine call
+                    kind = "add" if fn == self._e.bloom_add else "contains"
+                    return co.submit(self._name, kind, self._size, self._k, elems).get()
                 return fn(self._name, self._size, self._k, elems)
             except RedisException as e:          # retry loop :108-111 / :162-166
                 if "Bloom filter config has been changed" not in str(e):
@@ -419,12 +426,18 @@ class Redisson:
         self.config = config
         self.engine = SketchEngine(config.device, config.redis_major, config.max_bit_offset,
                                    config.hll_capacity, config.max_batch)
+        self.bloom_coalescer = None
+        if config.bloom_coalesce:
+            from .coalesce import BloomCoalescer
+            self.bloom_coalescer = BloomCoalescer(self.engine)
 
     @staticmethod
     def create(config: Optional[Config] = None) -> "Redisson":
         return Redisson(config or Config())
 
     def shutdown(self):
+        if self.bloom_coalescer is not None:
+            self.bloom_coalescer.close()
         self.engine.close()
 
     def getHyperLogLog(self, name, codec=None) -> RHyperLogLog:

@@ -131,40 +131,15 @@ def test_bitset_java_conversions():
     assert _int32((1 << 29) * 8) == -(1 << 32) + (1 << 32) and _int32(0x1_0000_0000 // 4 * 8) == 0  # Q3 overflow
 
 
-# A minimal stand-in for a JDK's jni.h with exactly the JNIEnv functions the
-# shim calls (the image has no JDK): compiling jni/redisson_sketch_jni.c against
-# it type-checks every shim call against include/redisson_sketch.h.
-_JNI_STUB = r"""
-#pragma once
-#include <stdint.h>
-typedef int32_t jint; typedef int64_t jlong; typedef uint8_t jboolean; typedef int8_t jbyte;
-typedef double jdouble; typedef jint jsize;
-typedef struct _jobject *jobject; typedef jobject jclass; typedef jobject jstring; typedef jobject jarray;
-typedef jarray jbyteArray; typedef jarray jlongArray; typedef jarray jintArray; typedef jarray jdoubleArray;
-#define JNIEXPORT __attribute__((visibility("default")))
-#define JNICALL
-#define JNI_ABORT 2
-struct JNINativeInterface_;
-typedef const struct JNINativeInterface_ *JNIEnv;
-struct JNINativeInterface_ {
-    jsize (*GetArrayLength)(JNIEnv *, jarray);
-    void *(*GetPrimitiveArrayCritical)(JNIEnv *, jarray, jboolean *);
-    void (*ReleasePrimitiveArrayCritical)(JNIEnv *, jarray, void *, jint);
-    jbyte *(*GetByteArrayElements)(JNIEnv *, jbyteArray, jboolean *);
-    void (*ReleaseByteArrayElements)(JNIEnv *, jbyteArray, jbyte *, jint);
-    jbyteArray (*NewByteArray)(JNIEnv *, jsize);
-    jstring (*NewStringUTF)(JNIEnv *, const char *);
-};
-"""
-
-
-def test_jni_shim_typechecks_against_the_abi(tmp_path):
+def test_jni_shim_typechecks_against_the_abi():
+    """jni/stub/jni.h is a minimal stand-in for a JDK's jni.h with exactly the JNIEnv functions the shim calls (the
+    image has no JDK): compiling jni/redisson_sketch_jni.c against it type-checks every shim call against
+    include/redisson_sketch.h."""
     import re
     import subprocess
 
-    (tmp_path / "jni.h").write_text(_JNI_STUB)
     src = os.path.join(ROOT, "jni", "redisson_sketch_jni.c")
-    r = subprocess.run(["gcc", "-fsyntax-only", "-Wall", "-Werror", "-I", str(tmp_path), src],
+    r = subprocess.run(["gcc", "-fsyntax-only", "-Wall", "-Werror", "-I", os.path.join(ROOT, "jni", "stub"), src],
                        capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
     # every native method declared in SketchNative.java has a JNI entry point

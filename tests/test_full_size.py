@@ -60,10 +60,11 @@ def test_c2_pfadd_100k_tenants_full_arena(O):
 
 
 def test_c3_bloom_full_size_bit_array(O):
-    """C3: tryInit(425 M, 0.008) -> m = 4,271,038,538 bits, k = 7 (a 534 MB array, indexes past 2^32); the 425 M
-    adds it is sized for, in 8 M batches: the whole bit array (GET) and its Redis length equal the oracle's; 32 M
-    contains (half members) equal the oracle's replies, members all true; count() follows BITCOUNT."""
-    seed, NA, CH, NC = 0x5EED2003, 425_000_000, 8 * M, 32 * M
+    """C3 as stated: tryInit(425 M, 0.008) -> m = 4,271,038,538 bits, k = 7 (a 534 MB array, indexes past 2^32); 1 B
+    adds in 8 M batches (the array ends ~81 % set): the whole bit array (GET) and its Redis length equal the
+    oracle's; 32 M contains (half members; the region schedule) equal the oracle's replies, members all true;
+    count() follows BITCOUNT."""
+    seed, NA, CH, NC = 0x5EED2003, 1_000_000_000, 8 * M, 32 * M
     eng = _engine(max_batch=CH)
     try:
         assert eng.bloom_try_init("c3", 425_000_000, 0.008)

@@ -74,10 +74,15 @@ def c1(eng, args):
     # Q1: addAll(1M Longs) = ONE PFADD element, the Jackson encoding of Object[]{name, e1..en}
     vals = np.random.default_rng(1).integers(-(1 << 63), (1 << 63) - 1, min(n, 1 << 20), dtype=np.int64)
     blob = JsonJacksonCodec().encode(["hll:c1q"] + [JLong(int(v)) for v in vals])
+    eng.pfadd([b"hll:c1q"], [[blob]])                          # warm (staging buffers)
+    eng.prof_reset(); eng.prof_enable(True)
     t_q1 = timed(eng, lambda: eng.pfadd([b"hll:c1q"], [[blob]]))
+    eng.prof_enable(False)
+    n_l, ms_long = eng.prof_read("pfadd_long")   # the element's workgroup hash (k_murmur_long), device time
     line({"metric": "C1 PFADD inserts/sec (one key, RBatch of single-element PFADDs)", "value": n / t,
           "unit": "inserts/s", "config": {"workload": "c1", "elements": n, "count_after": cnt},
-          "addAll_q1": {"element_bytes": len(blob), "seconds": t_q1, "count_after":
+          "addAll_q1": {"element_bytes": len(blob), "seconds": t_q1, "hash_ms_device": ms_long / max(n_l, 1),
+                        "count_after":
                         eng.pfcount([[b"hll:c1q"]])[0]}})
 
 

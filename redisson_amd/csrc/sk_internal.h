@@ -25,9 +25,14 @@ uint32_t pfadd_conflict_lds_capacity();
 uint32_t pfp_blocks(uint64_t n);
 uint32_t pfp_buckets();
 uint32_t pfp_epb();
+// pre: per-element hashes of the elements >= long_elem_bytes() (k_murmur_long), or null
 hipError_t launch_pfp_hash(hipStream_t st, uint64_t n, const uint32_t *key_ids, const uint64_t *off,
                            const uint8_t *bytes, int v5, uint64_t *chunks, uint32_t *S, uint16_t *pos,
-                           uint32_t *big_alloc);
+                           uint32_t *big_alloc, const uint64_t *pre = nullptr);
+uint64_t long_elem_bytes();
+// MurmurHash64A (seed 0xadc83b19) of elements which[0..n_long) into out_h[which[i]], one workgroup each
+hipError_t launch_murmur_long(hipStream_t st, uint32_t n_long, const uint8_t *bytes, const uint64_t *off,
+                              const uint32_t *which, uint64_t *out_h);
 hipError_t launch_pfp_apply(hipStream_t st, uint64_t n, const uint64_t *chunks, const uint32_t *S, uint8_t *arena,
                             uint8_t *rep, uint32_t *big_alloc, uint64_t *big_keys, uint32_t *big_vals,
                             uint8_t *changed); // changed != null: replies straight to batch order (no k_pfp_reply)

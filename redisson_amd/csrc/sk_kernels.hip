@@ -355,7 +355,8 @@ __global__ void __launch_bounds__(SK_PFP_TPB) k_pfp_hash(uint64_t n, const uint3
                                                          const uint8_t *__restrict__ bytes, int v5,
                                                          uint64_t *__restrict__ chunks, uint32_t *__restrict__ S,
                                                          uint32_t nblocks, uint16_t *__restrict__ pos,
-                                                         uint32_t *__restrict__ big_alloc) {
+                                                         uint32_t *__restrict__ big_alloc,
+                                                         const uint64_t *__restrict__ pre_h) {
     __shared__ uint32_t h[SK_PFP_NB];
     __shared__ uint32_t wsum[SK_PFP_TPB / 64];
     __shared__ uint64_t lrec[SK_PFP_EPB];
@@ -402,7 +403,8 @@ __global__ void __launch_bounds__(SK_PFP_TPB) k_pfp_hash(uint64_t n, const uint3
         uint64_t i = base + uint64_t(e) * SK_PFP_TPB + threadIdx.x;
         if (i < n) {
             uint32_t len = uint32_t(ob[e] - oa[e]);
-            uint64_t hh = pfp_win_fits(wb[e], wb[e + 1])
+            uint64_t hh = (pre_h && len >= SK_LONG_ELEM) ? pre_h[i] // hashed by a whole workgroup (k_murmur_long)
+                          : pfp_win_fits(wb[e], wb[e + 1])
                               ? murmur64a_r(LdsReader{win[e & 1], uint32_t(wb[e] & 15u) + uint32_t(oa[e] - wb[e])},
                                             len, 0xadc83b19ull)
                               : murmur64a(bytes + oa[e], len, 0xadc83b19ull);
@@ -453,6 +455,64 @@ __global__ void __launch_bounds__(SK_PFP_TPB) k_pfp_reply(uint64_t n, const uint
         uint8_t v = lr[pos[i]];
         if (!cmd_of) changed[i] = v;
         else if (v) changed[cmd_of[i]] = 1; // multi-element commands: OR over their elements
+    }
+}
+
+// ---- one long element (RHyperLogLog.addAll, quirk Q1: ONE element = the Jackson array of every value, ~38 MB at
+// C1, M:RedissonHyperLogLog.java:70-76).  MurmurHash64A's state chain h = (h ^ k_b) * m is sequential, but the
+// per-block transform k_b = mix(block b) is not: the workgroup's waves compute k for a tile of blocks into LDS
+// (coalesced 8-byte loads) while lane 0 of wave 0 runs the chain over the previous tile from LDS, so the element
+// costs one dependent xor + 64-bit multiply per 8 bytes instead of a single lane's loads and arithmetic.
+#define SK_ML_TILE 8192 // blocks per LDS tile (64 KiB; two tiles)
+__global__ void __launch_bounds__(1024) k_murmur_long(const uint8_t *__restrict__ bytes, const uint64_t *__restrict__ off,
+                                                      const uint32_t *__restrict__ which, uint64_t seed,
+                                                      uint64_t *__restrict__ out_h) {
+    __shared__ uint64_t kb[2][SK_ML_TILE];
+    const uint64_t m = 0xc6a4a7935bd1e995ull;
+    const uint32_t e = which[blockIdx.x];
+    const uint64_t o = off[e];
+    const uint64_t len = off[e + 1] - o;
+    const uint64_t nb = len >> 3;
+    const uint8_t *p = bytes + o;
+    const uint64_t ntiles = (nb + SK_ML_TILE - 1) / SK_ML_TILE;
+    auto produce = [&](uint64_t t, uint64_t *dst, uint32_t tid, uint32_t nthreads) {
+        uint64_t b0 = t * SK_ML_TILE;
+        uint32_t cnt = uint32_t(nb - b0 < SK_ML_TILE ? nb - b0 : SK_ML_TILE);
+        for (uint32_t j = tid; j < cnt; j += nthreads) {
+            uint64_t k = ldu64(p + 8 * (b0 + j));
+            k *= m;
+            k ^= k >> 47;
+            k *= m;
+            dst[j] = k;
+        }
+    };
+    uint64_t h = seed ^ (len * m);
+    if (ntiles) produce(0, kb[0], threadIdx.x, blockDim.x);
+    __syncthreads();
+    for (uint64_t t = 0; t < ntiles; t++) {
+        if (threadIdx.x >= 64) { // waves 1.. produce the next tile
+            if (t + 1 < ntiles) produce(t + 1, kb[(t + 1) & 1], threadIdx.x - 64, blockDim.x - 64);
+        } else if (threadIdx.x == 0) { // lane 0 of wave 0 runs the chain over tile t
+            uint64_t b0 = t * SK_ML_TILE;
+            uint32_t cnt = uint32_t(nb - b0 < SK_ML_TILE ? nb - b0 : SK_ML_TILE);
+            const uint64_t *src = kb[t & 1];
+            for (uint32_t j = 0; j < cnt; j++) {
+                h ^= src[j];
+                h *= m;
+            }
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        unsigned tail = unsigned(len & 7u);
+        if (tail) {
+            h ^= low_bytes(ldu64(p + 8 * nb), tail);
+            h *= m;
+        }
+        h ^= h >> 47;
+        h *= m;
+        h ^= h >> 47;
+        out_h[e] = h;
     }
 }
 
@@ -1615,6 +1675,16 @@ hipError_t launch_pfadd_conflicts_sorted(hipStream_t st, uint64_t cnt, const uin
 uint32_t pfadd_conflict_lds_capacity() { return SK_CONF_MAX; }
 
 
+uint64_t long_elem_bytes() { return SK_LONG_ELEM; }
+
+hipError_t launch_murmur_long(hipStream_t st, uint32_t n_long, const uint8_t *bytes, const uint64_t *off,
+                              const uint32_t *which, uint64_t *out_h) {
+    if (!n_long) return hipSuccess;
+    hipLaunchKernelGGL(k_murmur_long, dim3(n_long), dim3(1024), 0, st, bytes, off, which, 0xadc83b19ull, out_h);
+    SK_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
 uint32_t pfp_blocks(uint64_t n) { return uint32_t((n + SK_PFP_EPB - 1) / SK_PFP_EPB); }
 uint32_t pfp_buckets() { return SK_PFP_NB; }
 uint32_t pfp_epb() { return SK_PFP_EPB; }
@@ -1623,10 +1693,10 @@ uint32_t pfp_epb() { return SK_PFP_EPB; }
 // hash + block-local bucket sort -> per-bucket LDS resolve; one launcher per stage so each is timed
 hipError_t launch_pfp_hash(hipStream_t st, uint64_t n, const uint32_t *key_ids, const uint64_t *off,
                            const uint8_t *bytes, int v5, uint64_t *chunks, uint32_t *S, uint16_t *pos,
-                           uint32_t *big_alloc) {
+                           uint32_t *big_alloc, const uint64_t *pre) {
     uint32_t nb = pfp_blocks(n);
     hipLaunchKernelGGL(k_pfp_hash, dim3(nb), dim3(SK_PFP_TPB), 0, st, n, key_ids, off, bytes, v5, chunks, S, nb, pos,
-                       big_alloc);
+                       big_alloc, pre);
     SK_LAUNCH_CHECK();
     return hipSuccess;
 }

@@ -256,6 +256,7 @@ struct sk_ctx {
     DBuf keys_a, keys_b, vals_a, vals_b, sort_tmp, in_off, in_bytes, in_ids, in_cmd, out_u8, misc, partial, hist,
         uni, ptrs, hist_a, hist_b, ovf, bloom_h;
     DBuf rc_S, rc_rec;          // Bloom contains region schedule: segment table + probe records (contains only)
+    DBuf long_h, long_which;    // PFADD: hashes of long elements (k_murmur_long) and their element indexes
     uint64_t bloom_rc_min = 2u << 20; // contains batches >= this use the region schedule (SK_BLOOM_RC_MIN, 0 = never)
 };
 
@@ -316,7 +317,8 @@ int pfadd_settle(sk_ctx *c); // defined with the PFADD core
 const char *kPhaseNames[] = {"pfadd_hash",  "pfadd_sort",   "pfadd_apply", "hll_hist",     "hll_union",
                              "bloom_contains", "bloom_probes", "bloom_sort", "bloom_apply", "setbit",
                              "getbit",      "bitcount",     "bitop",       "pfadd_claim", "pfadd_commit",
-                             "pfp_hash",    "pfp_apply",    "pfp_reply",   "bloom_rc_hash", "bloom_rc_probe", "pfadd"};
+                             "pfp_hash",    "pfp_apply",    "pfp_reply",   "bloom_rc_hash", "bloom_rc_probe", "pfadd",
+                             "pfadd_long"};
 constexpr int kNumPhases = sizeof(kPhaseNames) / sizeof(kPhaseNames[0]);
 
 hipEvent_t ev_get(sk_ctx *c) {
@@ -701,7 +703,7 @@ bool pfadd_uses_sort(sk_ctx *c, uint64_t n, uint64_t touched_keys) {
 // Exact for every input on the device (oversized buckets: k_pfp_big), so the
 // host never waits on a batch.
 int pfadd_partition(sk_ctx *c, uint64_t n, const uint32_t *d_ids, const uint64_t *d_off, const uint8_t *d_bytes,
-                    const uint32_t *d_cmd, uint8_t *d_changed) {
+                    const uint32_t *d_cmd, uint8_t *d_changed, const uint64_t *d_pre = nullptr) {
     if (n > (1ull << 20) || c->hll_next >= (1ull << 24)) return fail(c, SK_EINVAL, "PFADD partition batch too large");
     uint64_t nb = sk::pfp_blocks(n), cap = nb * sk::pfp_epb();
     HIPCHK(c, c->keys_a.ensure(cap * 8));                                // block chunks of records
@@ -719,7 +721,7 @@ int pfadd_partition(sk_ctx *c, uint64_t n, const uint32_t *d_ids, const uint64_t
     const bool direct = d_cmd == nullptr && c->pfp_direct;
     { Prof p_(c, 15);
     HIPCHK(c, sk::launch_pfp_hash(c->st, n, d_ids, d_off, d_bytes, c->redis_major >= 5, chunks, S,
-                                  direct ? nullptr : pos, big_alloc)); }
+                                  direct ? nullptr : pos, big_alloc, d_pre)); }
     { Prof p_(c, 16);
     HIPCHK(c, sk::launch_pfp_apply(c->st, n, chunks, S, c->arena, rep, big_alloc, c->vals_a.as<uint64_t>(),
                                    c->vals_b.as<uint32_t>(), direct ? d_changed : nullptr)); }
@@ -731,7 +733,8 @@ int pfadd_partition(sk_ctx *c, uint64_t n, const uint32_t *d_ids, const uint64_t
 }
 
 int pfadd_device(sk_ctx *c, uint64_t n, const uint32_t *d_ids, const uint64_t *d_off, const uint8_t *d_bytes,
-                 const uint32_t *d_cmd, uint64_t n_cmds, uint8_t *d_changed, uint64_t touched_keys) {
+                 const uint32_t *d_cmd, uint64_t n_cmds, uint8_t *d_changed, uint64_t touched_keys,
+                 const uint64_t *d_pre = nullptr) {
     if (!n) return SK_OK;
     if (c->pfadd_path == 1) { // partition path, 1M elements per launch
         for (uint64_t s = 0; s < n; s += (1ull << 20)) {
@@ -740,15 +743,16 @@ int pfadd_device(sk_ctx *c, uint64_t n, const uint32_t *d_ids, const uint64_t *d
                 if (r) return r;
             }
             uint64_t m = std::min<uint64_t>(1ull << 20, n - s);
+            const uint64_t *pre = d_pre ? d_pre + s : nullptr;
             // element offsets stay absolute; the command index of element s+j is d_cmd[s+j] (or s+j)
             if (d_cmd == nullptr && s > 0) {
-                int r = pfadd_partition(c, m, d_ids + s, d_off + s, d_bytes, nullptr, d_changed + s);
+                int r = pfadd_partition(c, m, d_ids + s, d_off + s, d_bytes, nullptr, d_changed + s, pre);
                 if (r) return r;
             } else if (d_cmd == nullptr) {
-                int r = pfadd_partition(c, m, d_ids, d_off, d_bytes, nullptr, d_changed);
+                int r = pfadd_partition(c, m, d_ids, d_off, d_bytes, nullptr, d_changed, pre);
                 if (r) return r;
             } else {
-                int r = pfadd_partition(c, m, d_ids + s, d_off + s, d_bytes, d_cmd + s, d_changed);
+                int r = pfadd_partition(c, m, d_ids + s, d_off + s, d_bytes, d_cmd + s, d_changed, pre);
                 if (r) return r;
             }
         }
@@ -904,7 +908,8 @@ int sk_close(sk_ctx *c) {
     if (c->h_cnt) (void)hipHostFree(c->h_cnt);
     for (DBuf *b : {&c->keys_a, &c->keys_b, &c->vals_a, &c->vals_b, &c->sort_tmp, &c->in_off, &c->in_bytes,
                     &c->in_ids, &c->in_cmd, &c->out_u8, &c->misc, &c->partial, &c->hist, &c->uni, &c->ptrs,
-                    &c->hist_a, &c->hist_b, &c->ovf, &c->bloom_h, &c->rc_S, &c->rc_rec})
+                    &c->hist_a, &c->hist_b, &c->ovf, &c->bloom_h, &c->rc_S, &c->rc_rec, &c->long_h,
+                    &c->long_which})
         b->release();
     if (c->ev_w) (void)hipEventDestroy(c->ev_w);
     if (c->ev_r) (void)hipEventDestroy(c->ev_r);
@@ -1166,9 +1171,28 @@ static int pfadd_host_batch(sk_ctx *c, uint32_t n_cmds, const uint32_t *cmd_key,
                 std::sort(uniq.begin(), uniq.end());
                 touched = uint64_t(std::unique(uniq.begin(), uniq.end()) - uniq.begin());
             }
+            // long elements (addAll's Q1 element: the whole Jackson array) are hashed by one workgroup each
+            const uint64_t *d_pre = nullptr;
+            if (c->pfadd_path == 1 && nbytes >= sk::long_elem_bytes()) {
+                std::vector<uint32_t> which;
+                for (uint64_t j = 0; j < m; j++)
+                    if (off2[j + 1] - off2[j] >= sk::long_elem_bytes()) which.push_back(uint32_t(j));
+                if (!which.empty()) {
+                    HIPCHK(c, c->long_h.ensure(m * 8));
+                    HIPCHK(c, c->long_which.ensure(which.size() * 4));
+                    HIPCHK(c, hipMemcpyAsync(c->long_which.p, which.data(), which.size() * 4, hipMemcpyHostToDevice,
+                                             c->st));
+                    { Prof p_(c, 21);
+                    HIPCHK(c, sk::launch_murmur_long(c->st, uint32_t(which.size()), c->in_bytes.as<uint8_t>(),
+                                                     c->in_off.as<uint64_t>(), c->long_which.as<uint32_t>(),
+                                                     c->long_h.as<uint64_t>())); }
+                    HIPCHK(c, hipStreamSynchronize(c->st)); // `which` is a host vector
+                    d_pre = c->long_h.as<uint64_t>();
+                }
+            }
             int r = pfadd_device(c, m, c->in_ids.as<uint32_t>(), c->in_off.as<uint64_t>(), c->in_bytes.as<uint8_t>(),
                                  cmd_src ? c->in_cmd.as<uint32_t>() : nullptr, c1 - c0, c->out_u8.as<uint8_t>(),
-                                 touched);
+                                 touched, d_pre);
             if (r) return r;
             auto t1 = now();
             HIPCHK(c, hipMemcpyAsync(out_changed + c0, c->out_u8.p, c1 - c0, hipMemcpyDeviceToHost, c->st));

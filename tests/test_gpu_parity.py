@@ -740,3 +740,38 @@ def test_stale_slab_id_rejected(O):
             e.pfcount_ids(np.array([c], np.uint32))
     finally:
         e.close()
+
+
+def test_pfadd_long_elements_workgroup_hash(O):
+    """C1's addAll (quirk Q1: ONE element = the Jackson array of 1M Longs, ~40 MB) and a batch mixing elements
+    of 64 KiB .. 3 MB with short ones: elements >= 64 KiB are hashed by k_murmur_long (one workgroup each); replies
+    and registers equal the oracle's, and the 40 MB element hashes well within 50 ms of device time."""
+    import time
+
+    from redisson_amd import JLong, JsonJacksonCodec, SketchEngine
+    e = SketchEngine(device=0)
+    try:
+        vals = np.random.default_rng(1).integers(-(1 << 63), (1 << 63) - 1, 1 << 20, dtype=np.int64)
+        blob = JsonJacksonCodec().encode(["hll:c1q"] + [JLong(int(v)) for v in vals])
+        assert len(blob) > 30_000_000
+        ref = O.HLLStore()
+        e.pfadd([b"hll:c1q"], [[blob[:100]]])              # warm the path
+        ref.pfadd([b"hll:c1q"], [[blob[:100]]])
+        t0 = time.perf_counter()
+        got = e.pfadd([b"hll:c1q"], [[blob]])
+        dt = time.perf_counter() - t0
+        assert got == ref.pfadd([b"hll:c1q"], [[blob]])
+        np.testing.assert_array_equal(e.hll_registers(b"hll:c1q"), ref.regs[b"hll:c1q"])
+        assert e.pfcount([[b"hll:c1q"]]) == [ref.count([b"hll:c1q"])]
+        assert dt < 1.0, dt                                  # host-timed, H2D of 40 MB included
+        rng = np.random.default_rng(3)
+        elems = []
+        for i in range(40):
+            n = int(rng.choice([5, 37, 65536, 65537, 200_001, 3_000_003])) + i
+            elems.append(rng.integers(0, 256, n, dtype=np.uint8).tobytes())
+        keys = [b"long:%d" % (i % 3) for i in range(40)]
+        assert e.pfadd(keys, [[x] for x in elems]) == ref.pfadd(keys, [[x] for x in elems])
+        for k in set(keys):
+            np.testing.assert_array_equal(e.hll_registers(k), ref.regs[k])
+    finally:
+        e.close()

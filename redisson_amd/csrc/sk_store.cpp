@@ -257,6 +257,17 @@ struct sk_ctx {
         uni, ptrs, hist_a, hist_b, ovf, bloom_h;
     DBuf rc_S, rc_rec;          // Bloom contains region schedule: segment table + probe records (contains only)
     DBuf long_h, long_which;    // PFADD: hashes of long elements (k_murmur_long) and their element indexes
+    // device PFADD batches, pipelined (SK_PFP_PIPE, default on): batch i+1's k_pfp_hash runs on st3 while batch i's
+    // k_pfp_apply runs on st; two scratch sets alternate, events order hash -> apply and apply -> reuse
+    struct PfpSet {
+        DBuf chunks, rep, S, big_k, big_v, ovf;
+        hipEvent_t hashed = nullptr, applied = nullptr;
+        bool used = false;
+    } pfs[2];
+    int pf_par = 0;
+    bool pfp_pipe = true;
+    bool pf_dev_call = false;   // inside sk_pfadd_dev: inputs are caller-owned device memory, no host staging
+    hipStream_t st3 = nullptr;
     uint64_t bloom_rc_min = 2u << 20; // contains batches >= this use the region schedule (SK_BLOOM_RC_MIN, 0 = never)
 };
 
@@ -292,6 +303,7 @@ std::string key_at(const uint64_t *off, const uint8_t *bytes, uint64_t i) {
 int sync(sk_ctx *c) {
     HIPCHK(c, hipStreamSynchronize(c->st));
     if (c->st2) HIPCHK(c, hipStreamSynchronize(c->st2));
+    if (c->st3) HIPCHK(c, hipStreamSynchronize(c->st3));
     return SK_OK;
 }
 
@@ -354,6 +366,7 @@ void prof_collect(sk_ctx *c) {
     if (c->prof_pending.empty()) return;
     (void)hipStreamSynchronize(c->st);
     if (c->st2) (void)hipStreamSynchronize(c->st2);
+    if (c->st3) (void)hipStreamSynchronize(c->st3);
     for (auto &r : c->prof_pending) {
         float ms = 0;
         if (hipEventElapsedTime(&ms, r.a, r.b) == hipSuccess) {
@@ -702,9 +715,44 @@ bool pfadd_uses_sort(sk_ctx *c, uint64_t n, uint64_t touched_keys) {
 // partition path (sk_kernels.hip "PFADD, partition path"); n <= 2^20 per launch.
 // Exact for every input on the device (oversized buckets: k_pfp_big), so the
 // host never waits on a batch.
+// pipelined form of the partition path for device-resident inputs: the hash of this batch goes to st3 (it reads
+// only the caller's inputs and its own scratch set), the apply stays on st in batch order (replies and registers
+// depend on the previous batch's registers, so applies never reorder)
+int pfadd_partition_pipe(sk_ctx *c, uint64_t n, const uint32_t *d_ids, const uint64_t *d_off, const uint8_t *d_bytes,
+                         uint8_t *d_changed) {
+    uint64_t nb = sk::pfp_blocks(n), cap = nb * sk::pfp_epb();
+    sk_ctx::PfpSet &ps = c->pfs[c->pf_par];
+    c->pf_par ^= 1;
+    if (!ps.hashed) {
+        HIPCHK(c, hipEventCreateWithFlags(&ps.hashed, hipEventDisableTiming));
+        HIPCHK(c, hipEventCreateWithFlags(&ps.applied, hipEventDisableTiming));
+    }
+    if (ps.used) HIPCHK(c, hipStreamWaitEvent(c->st3, ps.applied, 0)); // the set's previous apply is done
+    HIPCHK(c, ps.chunks.ensure(cap * 8));
+    HIPCHK(c, ps.rep.ensure(cap + 32));
+    HIPCHK(c, ps.S.ensure((uint64_t(sk::pfp_buckets()) + 1) * nb * 4));
+    HIPCHK(c, ps.big_k.ensure(2 * n * 8));
+    HIPCHK(c, ps.big_v.ensure(2 * n * 4));
+    HIPCHK(c, ps.ovf.ensure(64));
+    { Prof p_(c, 15, c->st3);
+    HIPCHK(c, sk::launch_pfp_hash(c->st3, n, d_ids, d_off, d_bytes, c->redis_major >= 5, ps.chunks.as<uint64_t>(),
+                                  ps.S.as<uint32_t>(), nullptr, ps.ovf.as<uint32_t>(), nullptr)); }
+    HIPCHK(c, hipEventRecord(ps.hashed, c->st3));
+    HIPCHK(c, hipStreamWaitEvent(c->st, ps.hashed, 0));
+    { Prof p_(c, 16);
+    HIPCHK(c, sk::launch_pfp_apply(c->st, n, ps.chunks.as<uint64_t>(), ps.S.as<uint32_t>(), c->arena,
+                                   ps.rep.as<uint8_t>(), ps.ovf.as<uint32_t>(), ps.big_k.as<uint64_t>(),
+                                   ps.big_v.as<uint32_t>(), d_changed)); }
+    HIPCHK(c, hipEventRecord(ps.applied, c->st));
+    ps.used = true;
+    return SK_OK;
+}
+
 int pfadd_partition(sk_ctx *c, uint64_t n, const uint32_t *d_ids, const uint64_t *d_off, const uint8_t *d_bytes,
                     const uint32_t *d_cmd, uint8_t *d_changed, const uint64_t *d_pre = nullptr) {
     if (n > (1ull << 20) || c->hll_next >= (1ull << 24)) return fail(c, SK_EINVAL, "PFADD partition batch too large");
+    if (c->pf_dev_call && c->pfp_pipe && c->pfp_direct && d_cmd == nullptr && d_pre == nullptr && c->st3)
+        return pfadd_partition_pipe(c, n, d_ids, d_off, d_bytes, d_changed);
     uint64_t nb = sk::pfp_blocks(n), cap = nb * sk::pfp_epb();
     HIPCHK(c, c->keys_a.ensure(cap * 8));                                // block chunks of records
     HIPCHK(c, c->keys_b.ensure(cap + 2 * n + 32));                       // replies in chunk order + element slots
@@ -864,6 +912,7 @@ int sk_open(const sk_config *cfg, sk_ctx **out) {
         hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess ||
         hipStreamCreateWithPriority(&c->st, hipStreamNonBlocking, prio_mode == 1 ? hi : lo) != hipSuccess ||
         hipStreamCreateWithPriority(&c->st2, hipStreamNonBlocking, prio_mode == 2 ? hi : lo) != hipSuccess ||
+        hipStreamCreateWithPriority(&c->st3, hipStreamNonBlocking, lo) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_w, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_r, hipEventDisableTiming) != hipSuccess) {
         delete c;
@@ -875,6 +924,7 @@ int sk_open(const sk_config *cfg, sk_ctx **out) {
     if (const char *e = getenv("SK_PFADD_PATH")) c->pfadd_path = atoi(e);
     if (const char *e = getenv("SK_PFP_DIRECT")) c->pfp_direct = atoi(e) != 0;
     if (const char *e = getenv("SK_BLOOM_RC_MIN")) c->bloom_rc_min = strtoull(e, nullptr, 10);
+    if (const char *e = getenv("SK_PFP_PIPE")) c->pfp_pipe = atoi(e) != 0;
     uint64_t cap = (cfg && cfg->hll_capacity) ? cfg->hll_capacity : 1024;
     if (hll_grow(c, cap) != SK_OK || c->misc.ensure(4096) != hipSuccess ||
         hipMalloc(&c->d_zero, 16) != hipSuccess || hipMemsetAsync(c->d_zero, 0, 16, c->st) != hipSuccess ||
@@ -894,6 +944,7 @@ int sk_close(sk_ctx *c) {
     if (c->pf_pending) (void)pfadd_settle(c);
     if (c->st) (void)hipStreamSynchronize(c->st);
     if (c->st2) (void)hipStreamSynchronize(c->st2);
+    if (c->st3) (void)hipStreamSynchronize(c->st3);
     if (c->comm) (void)ncclCommDestroy(c->comm);
     prof_collect(c);
     for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
@@ -911,9 +962,15 @@ int sk_close(sk_ctx *c) {
                     &c->hist_a, &c->hist_b, &c->ovf, &c->bloom_h, &c->rc_S, &c->rc_rec, &c->long_h,
                     &c->long_which})
         b->release();
+    for (auto &ps : c->pfs) {
+        for (DBuf *b : {&ps.chunks, &ps.rep, &ps.S, &ps.big_k, &ps.big_v, &ps.ovf}) b->release();
+        if (ps.hashed) (void)hipEventDestroy(ps.hashed);
+        if (ps.applied) (void)hipEventDestroy(ps.applied);
+    }
     if (c->ev_w) (void)hipEventDestroy(c->ev_w);
     if (c->ev_r) (void)hipEventDestroy(c->ev_r);
     if (c->st2) (void)hipStreamDestroy(c->st2);
+    if (c->st3) (void)hipStreamDestroy(c->st3);
     if (c->st) (void)hipStreamDestroy(c->st);
     delete c;
     return SK_OK;
@@ -1292,6 +1349,11 @@ int sk_pfadd_dev(sk_ctx *c, uint64_t n, const uint32_t *d_ids, const uint64_t *d
     if (!n) return SK_OK;
     unsigned id_bits = bits_for(c->hll_next ? c->hll_next - 1 : 0);
     uint64_t max_cmds = std::min<uint64_t>(c->max_batch, 1ull << std::min(32u, 64 - 20 - id_bits));
+    struct DevCall { // the pipelined partition path is for caller-owned device inputs only
+        sk_ctx *c;
+        explicit DevCall(sk_ctx *c_) : c(c_) { c->pf_dev_call = true; }
+        ~DevCall() { c->pf_dev_call = false; }
+    } dev_call(c);
     for (uint64_t s = 0; s < n; s += max_cmds) {
         uint64_t m = std::min(max_cmds, n - s);
         uint64_t live = c->hll_next - c->hll_free.size(); // slabs in use bounds the touched sketches

@@ -7,9 +7,10 @@ m = 4,271,038,538 bits, k = 7, filled with the config's 1B adds, 50 % members / 
 resident in HBM.  Defaults: HB = 16, CB = 16M, so a step is 16M PFADD + 16M contains.
 value = (PFADD elements + contains elements) / wall time, all ranks.
 
-Multi-GPU (torch.distributed.run, one process per GPU): keys are partitioned by calcSlot(key) % world (the
-north-star partitioner), each rank owns its tenants and its own Bloom filter, no data-path collective ->
-"scaling": "weak".  Rendezvous / barrier / max-over-ranks timing use torch.distributed's gloo (CPU) backend: the
+Multi-GPU (torch.distributed.run, one process per GPU): HLL keys are partitioned by calcSlot(key) % world (the
+north-star partitioner), each rank owns its tenants; the C3 Bloom filter is ONE logical filter replicated on every
+GPU (identical 1B adds), each rank serving its share of the contains traffic (redisson_amd/cluster.py
+ReplicatedBloom).  No data-path collective -> "scaling": "weak".  Rendezvous / barrier / max-over-ranks timing use torch.distributed's gloo (CPU) backend: the
 engine owns the GPU through the system HIP runtime, so this process never initialises torch's bundled HIP runtime.
 """
 from __future__ import annotations
@@ -116,7 +117,9 @@ def main():
     d_changed = eng.alloc(B)
     mean_len_h = h_total / (nsteps * NH)
 
-    bloom = "bloom:c3:%d" % rank
+    # ONE logical C3 filter for the whole node: every rank holds an identical replica (the same 1B adds), and the
+    # contains traffic is split over the replicas (cluster.ReplicatedBloom's layout); at N = 1 it is the filter
+    bloom = "bloom:c3"
     eng.bloom_try_init(bloom, args.bloom_n, args.bloom_p)
     size, k, _, _ = eng.bloom_config(bloom)
     seed_b = 0x5EED0003
@@ -125,7 +128,7 @@ def main():
     add_s = 0.0      # the add batches only (input generation excluded), host-timed around each call
     for s in range(0, fill, chunk):
         n = min(chunk, fill - s)
-        a_off, a_bytes, a_tot = eng.gen_jackson_longs_dev(seed_b, n, first=(rank << 40) + s)
+        a_off, a_bytes, a_tot = eng.gen_jackson_longs_dev(seed_b, n, first=s)
         eng.sync()
         t0 = time.perf_counter()
         eng.bloom_add_dev(bloom, n, a_off, a_bytes, a_tot, d_add_out)
@@ -137,7 +140,7 @@ def main():
     c_in = []
     c_total = 0
     for s in range(nsteps):
-        member = rng.integers(0, max(fill, 1), CB, dtype=np.uint64) + np.uint64(rank << 40)
+        member = rng.integers(0, max(fill, 1), CB, dtype=np.uint64)
         fresh = rng.integers(1 << 39, 1 << 40, CB, dtype=np.uint64) + np.uint64(rank << 40)
         idx = np.where(rng.random(CB) < 0.5, member, fresh)
         d_idx = eng.to_device(idx)
@@ -269,8 +272,8 @@ def main():
         "data": "synthetic: SplitMix64 Longs as Jackson bytes [\"java.lang.Long\",v] (mean %.1f B)" % mean_len_h,
         "config": {
             "workload": "C2 PFADD 1 elem/cmd over %d tenants, %d RBatches of %d commands + C3 Bloom contains "
-                        "(m=%d, k=%d, filled with %d adds, 50%% members), %d elements, per step"
-                        % (args.tenants, HB, B, size, k, fill, CB),
+                        "(m=%d, k=%d, filled with %d adds, 50%% members), %d elements, per step and GPU; "
+                        "one C3 filter replicated on the %d GPU(s)" % (args.tenants, HB, B, size, k, fill, CB, world),
             "pfadd_batch": B, "pfadd_batches_per_step": HB, "contains_batch": CB, "tenants": args.tenants,
             "bloom_bits": size, "bloom_k": k, "bloom_fill": fill, "partitioner": "calcSlot(key) %% %d" % world,
         },

@@ -344,3 +344,35 @@ def keyed_bitop(engine, op: str, dest, srcs: Sequence, rank: int, world: int, co
         finally:
             engine.delete(tmp)
     return max(coll.allgather_u64(n))
+
+
+# ---------------------------------------------------------------- one Bloom filter served by N GPUs
+class ReplicatedBloom:
+    """One RBloomFilter served by every GPU of the node: each rank holds a full replica of the bit array.
+    SPMD: ``add`` is called by every rank with the same elements and applied to every replica (the replicas stay
+    identical, so every rank gets the same exact replies); ``contains`` splits the batch, rank r answers elements
+    [r*n/N, (r+1)*n/N) on its replica, and the replies are all-gathered.  Read traffic (the C3 metric) scales
+    with the GPUs; adds cost every GPU the whole batch, which is the price of serving one hot filter from N.
+    (A filter that only one GPU should hold simply lives on its calcSlot owner, like any other key.)"""
+
+    def __init__(self, engine, name, rank: int, world: int, coll):
+        self.engine, self.name, self.rank, self.world, self.coll = engine, name, rank, world, coll
+
+    def try_init(self, expected: int, fpp: float) -> bool:
+        return self.engine.bloom_try_init(self.name, expected, fpp)
+
+    def _cfg(self):
+        size, k, _, _ = self.engine.bloom_config(self.name)
+        return size, k
+
+    def add(self, elems: Sequence[bytes]) -> List[bool]:
+        size, k = self._cfg()
+        return self.engine.bloom_add(self.name, size, k, list(elems))
+
+    def contains(self, elems: Sequence[bytes]) -> List[bool]:
+        size, k = self._cfg()
+        n = len(elems)
+        lo, hi = self.rank * n // self.world, (self.rank + 1) * n // self.world
+        mine = self.engine.bloom_contains(self.name, size, k, list(elems[lo:hi])) if hi > lo else []
+        parts = self.coll.allgather_bytes(bytes(int(x) for x in mine))
+        return [bool(b) for p in parts for b in p]

@@ -61,6 +61,15 @@ def run_scenario(engine, rank, world, coll):
         val = engine.get(dest) if owner(dest, world) == rank else None
         res[op] = (n, val)
     out["keyed"] = res
+
+    # one Bloom filter served by every rank (replicas): adds on all, contains split and gathered
+    from redisson_amd.cluster import ReplicatedBloom
+    bf = ReplicatedBloom(engine, b"rb:c3", rank, world, coll)
+    bf.try_init(20000, 0.01)
+    adds = [b'["java.lang.Long",%d]' % i for i in range(3000)]
+    out["bloom_add"] = [bool(x) for x in bf.add(adds[:2000])] + [bool(x) for x in bf.add(adds[1000:])]
+    probe = [b'["java.lang.Long",%d]' % i for i in range(0, 6000, 3)]
+    out["bloom_contains"] = [bool(x) for x in bf.contains(probe)]
     return out
 
 
@@ -108,6 +117,14 @@ def expected():
         v = O.bitop(op, [keys.get(k) for k in srcs])
         res[op] = (len(v), v if v else None)
     out["keyed"] = res
+    m = O.bloom_optimal_bits(20000, 0.01)
+    kk = O.bloom_optimal_k(20000, m)
+    b = O.BitString(16)
+    adds = [b'["java.lang.Long",%d]' % i for i in range(3000)]
+    out["bloom_add"] = [bool(x) for x in b.bloom_add(m, kk, adds[:2000])] + \
+        [bool(x) for x in b.bloom_add(m, kk, adds[1000:])]
+    out["bloom_contains"] = [bool(x) for x in b.bloom_contains(m, kk, [b'["java.lang.Long",%d]' % i
+                                                                      for i in range(0, 6000, 3)])]
     return out
 
 
@@ -116,7 +133,8 @@ def check(got, want, rank, world):
 
     for k in ("set_a", "set_b", "clear_a", "get_a"):
         assert [int(x) for x in got[k]] == [int(x) for x in want[k]], k
-    for k in ("card", "len", "size", "bytes_a", "and", "or", "xor", "not_b", "card_not_b"):
+    for k in ("card", "len", "size", "bytes_a", "and", "or", "xor", "not_b", "card_not_b", "bloom_add",
+              "bloom_contains"):
         assert got[k] == want[k], k
     for op, (n, val) in want["keyed"].items():
         gn, gval = got["keyed"][op]
@@ -169,6 +187,23 @@ class OracleBitEngine:
         for k in keys:
             n += self.s.pop(bytes(k), None) is not None
         return n
+
+    def bloom_try_init(self, name, n, p):
+        m = self.O.bloom_optimal_bits(n, p)
+        self.cfg = getattr(self, "cfg", {})
+        fresh = bytes(name) not in self.cfg
+        self.cfg[bytes(name)] = (m, self.O.bloom_optimal_k(n, m), n, p)
+        return fresh
+
+    def bloom_config(self, name):
+        return self.cfg[bytes(name)]
+
+    def bloom_add(self, name, size, k, elems):
+        return self._bs(name).bloom_add(size, k, elems)
+
+    def bloom_contains(self, name, size, k, elems):
+        b = self.s.get(bytes(name))
+        return b.bloom_contains(size, k, elems) if b else [False] * len(elems)
 
     def bitop(self, op, dest, srcs):
         v = self.O.bitop(op.upper(), [self.get(k) for k in srcs])

@@ -69,8 +69,18 @@ def c1(eng, args):
     eng.delete([b"hll:c1"])
     ids = eng.hll_resolve([b"hll:c1"])
     d_ids.upload(np.full(n, ids[0], dtype=np.uint32))
-    t = timed(eng, lambda: eng.pfadd_dev(n, d_ids, off, byt, tot, d_out))
+    t = timed(eng, lambda: eng.pfadd_dev(n, d_ids, off, byt, tot, d_out))   # one 1M batch, host-timed
     cnt = eng.pfcount([[b"hll:c1"]])[0]
+    # steady state: 10 more 1M batches of fresh Longs into the same key, back to back
+    steps = 10
+    off2, byt2, tot2 = eng.gen_jackson_longs_dev(0x5EED0011, n * steps)
+    d_ids2 = eng.to_device(np.full(n * steps, ids[0], dtype=np.uint32))
+    eng.pfadd_dev(n, d_ids2, off2, byt2, tot2, d_out)
+    eng.set_async(True)   # batches are enqueued back to back; timed() syncs once at the end
+    t_ss = timed(eng, lambda: [eng.pfadd_dev(n, d_ids2.ptr + s * n * 4, off2.ptr + s * n * 8, byt2, tot2, d_out)
+                               for s in range(steps)])
+    eng.set_async(False)
+    off2.free(); byt2.free(); d_ids2.free()
     # Q1: addAll(1M Longs) = ONE PFADD element, the Jackson encoding of Object[]{name, e1..en}
     vals = np.random.default_rng(1).integers(-(1 << 63), (1 << 63) - 1, min(n, 1 << 20), dtype=np.int64)
     blob = JsonJacksonCodec().encode(["hll:c1q"] + [JLong(int(v)) for v in vals])
@@ -79,8 +89,10 @@ def c1(eng, args):
     t_q1 = timed(eng, lambda: eng.pfadd([b"hll:c1q"], [[blob]]))
     eng.prof_enable(False)
     n_l, ms_long = eng.prof_read("pfadd_long")   # the element's workgroup hash (k_murmur_long), device time
-    line({"metric": "C1 PFADD inserts/sec (one key, RBatch of single-element PFADDs)", "value": n / t,
+    line({"metric": "C1 PFADD inserts/sec (one key, RBatch of single-element PFADDs)", "value": n * steps / t_ss,
           "unit": "inserts/s", "config": {"workload": "c1", "elements": n, "count_after": cnt},
+          "steady_state": "%d back-to-back batches of %d fresh Longs into the one key" % (steps, n),
+          "single_batch_inserts_per_s_host_timed": n / t,
           "addAll_q1": {"element_bytes": len(blob), "seconds": t_q1, "hash_ms_device": ms_long / max(n_l, 1),
                         "count_after":
                         eng.pfcount([[b"hll:c1q"]])[0]}})
@@ -97,8 +109,12 @@ def c2zipf(eng, args):
     off, byt, tot = eng.gen_jackson_longs_dev(0x5EED0022, B * (steps + 1))
     d_out = eng.alloc(B)
     eng.pfadd_dev(B, d_ids, off, byt, tot, d_out)            # warm
+    eng.set_async(True)
     t = timed(eng, lambda: [eng.pfadd_dev(B, d_ids.ptr + s * B * 4, off.ptr + s * B * 8, byt, tot, d_out)
                             for s in range(1, steps + 1)])
+    eng.set_async(False)
+    t_sync = timed(eng, lambda: [eng.pfadd_dev(B, d_ids.ptr + s * B * 4, off.ptr + s * B * 8, byt, tot, d_out)
+                                 for s in range(1, steps + 1)])
     top = float(np.bincount(kid[:B]).max()) / B
     # per-key PFCOUNT of every tenant (C2): the histogram kernel alone, and the whole RHyperLogLog.count path
     d_all = eng.to_device(ids)
@@ -114,6 +130,7 @@ def c2zipf(eng, args):
     line({"metric": "C2 Zipf(1.1) PFADD inserts/sec (1M-command batches, 100k tenants)", "value": B * steps / t,
           "unit": "inserts/s", "config": {"workload": "c2zipf", "batch": B, "tenants": nt, "zipf_s": 1.1,
                                           "hottest_tenant_share": top},
+          "synchronous_calls_inserts_per_s": B * steps / t_sync,
           "pfcount_keys_per_s": nt / t_c, "pfcount_ids_keys_per_s": nt / t_ci, "hist_keys_per_s_host_timed": nt / t_h,
           "roofline": {"kernel": "hll_hist", "bound": "hbm", "achieved": gbs, "peak": PEAK, "unit": "GB/s",
                        "frac": gbs / PEAK, "bytes_per_unit": 16384, "avg_launch_ms": k_ms}})

@@ -240,7 +240,8 @@ int sk_timer_elapsed(sk_ctx *ctx, int slot_a, int slot_b, float *ms);
  * of a phase): "pfadd_hash", "pfadd_sort", "pfadd_apply", "hll_hist",
  * "hll_union", "bloom_contains", "bloom_probes", "bloom_sort", "bloom_apply",
  * "setbit", "getbit", "bitcount", "bitop", "pfadd_claim", "pfadd_commit",
- * "pfp_hash", "pfp_apply", "pfp_reply", "bloom_rc_hash", "bloom_rc_probe";
+ * "pfp_hash", "pfp_apply", "pfp_reply", "bloom_rc_hash", "bloom_rc_probe",
+ * "pfadd_long", "bloom_ra_hash", "bloom_ra_apply";
  * chains: "bloom_contains" (every kernel of one contains call), "pfadd" (every
  * kernel of one sk_pfadd_dev batch) */
 int sk_prof_enable(sk_ctx *ctx, int on);

@@ -63,6 +63,9 @@ def lib():
                                            c_void_p, c_int]),
             "or_hll_union_gen_mt": (None, [c_void_p, c_uint64, c_uint64, c_uint64, c_int, c_int]),
             "or_bloom_add_gen_mt": (c_uint64, [c_void_p, c_int64, c_int32, c_uint64, c_uint64, c_uint64, c_int]),
+            "or_bloom_add_gen_seq": (c_uint64, [c_void_p, c_int64, c_int32, c_uint64, c_uint64, c_uint64, c_void_p]),
+            "or_bloom_add_idx_seq": (c_uint64, [c_void_p, c_uint64, c_int64, c_int32, c_uint64, c_void_p, c_uint64,
+                                                c_void_p]),
             "or_bloom_contains_gen_mt": (None, [c_void_p, c_uint64, c_int64, c_int32, c_uint64, c_void_p, c_uint64,
                                                 c_void_p, c_int]),
             "or_setbits_mt": (None, [c_void_p, c_void_p, c_uint64, c_int]),
@@ -395,6 +398,22 @@ def bloom_add_gen(size: int, k: int, seed: int, first: int, n: int):
     bits = np.zeros((size + 7) // 8 + 16, dtype=np.uint8)
     ln = lib().or_bloom_add_gen_mt(bits.ctypes.data, size, k, seed, first, n, threads())
     return bits, int(ln)
+
+
+def bloom_add_gen_seq(size: int, k: int, seed: int, first: int, n: int):
+    """(bit array, Redis string length, replies u8[n]) after adding elements first..first+n-1 in order."""
+    bits = np.zeros((size + 7) // 8 + 16, dtype=np.uint8)
+    out = np.zeros(n, dtype=np.uint8)
+    ln = lib().or_bloom_add_gen_seq(bits.ctypes.data, size, k, seed, first, n, out.ctypes.data)
+    return bits, int(ln), out
+
+
+def bloom_add_idx_seq(bits: np.ndarray, strlen: int, size: int, k: int, seed: int, idx: np.ndarray):
+    """Adds element numbers idx (in order, repeats allowed) to `bits` in place; (new string length, replies)."""
+    ix = np.ascontiguousarray(idx, dtype=np.uint64)
+    out = np.zeros(len(ix), dtype=np.uint8)
+    ln = lib().or_bloom_add_idx_seq(bits.ctypes.data, strlen, size, k, seed, ix.ctypes.data, len(ix), out.ctypes.data)
+    return int(ln), out
 
 
 def bloom_contains_gen(bits: np.ndarray, strlen: int, size: int, k: int, seed: int, idx: np.ndarray) -> np.ndarray:

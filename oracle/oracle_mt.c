@@ -264,6 +264,32 @@ uint64_t or_bloom_add_gen_mt(uint8_t *bits, int64_t size, int32_t k, uint64_t se
     return m;
 }
 
+/* RBloomFilter.add of generated elements first..first+n-1 in batch order with every reply (one thread: a reply
+ * depends on every earlier element); bits: (size+7)/8 zeroed bytes; returns the Redis string length */
+uint64_t or_bloom_add_gen_seq(uint8_t *bits, int64_t size, int32_t k, uint64_t seed, uint64_t first, uint64_t n,
+                              uint8_t *out) {
+    uint8_t e[48];
+    uint64_t len = 0;
+    for (uint64_t c = 0; c < n; c++) {
+        uint64_t off[2] = {0, 0};
+        off[1] = or_gen_jackson_long(seed, first + c, e);
+        or_bloom_add_batch(bits, &len, size, k, 1, off, e, out + c);
+    }
+    return len;
+}
+
+/* the same for element numbers idx[0..n) of stream `seed` (repeats allowed), continuing the string in bits/len */
+uint64_t or_bloom_add_idx_seq(uint8_t *bits, uint64_t len, int64_t size, int32_t k, uint64_t seed,
+                              const uint64_t *idx, uint64_t n, uint8_t *out) {
+    uint8_t e[48];
+    for (uint64_t c = 0; c < n; c++) {
+        uint64_t off[2] = {0, 0};
+        off[1] = or_gen_jackson_long(seed, idx[c], e);
+        or_bloom_add_batch(bits, &len, size, k, 1, off, e, out + c);
+    }
+    return len;
+}
+
 static void *bloom_contains_gen(void *p) {
     gen_arg *a = (gen_arg *)p;
     uint8_t e[48];

@@ -13,6 +13,7 @@
 // touched slot (rocPRIM) followed by a segment-head walk in batch order; the
 // final state (max / OR) needs no atomics because each slot has one head.
 #include <hip/hip_runtime.h>
+#include <cstdlib>
 #include <cstring>
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
@@ -1053,37 +1054,49 @@ __global__ void __launch_bounds__(256) k_bloom_contains_q(uint64_t n, const uint
 #define RC_PMAX 8                     // probes per element handled here (k <= 9)
 #define RC_NRMAX 4096                 // regions (bit arrays <= 2^32 bits)
 #define RC_ROUNDS (RC_EPB / RC_TPB)
+#define RA_EPB 2048                   // add: elements per hash block (11-bit element-in-block, 1-bit last probe)
+#define RA_RB 19                      // add: region = 2^19 bits = 64 KiB (the apply keeps a window of records too)
+#define RA_NRMAX 8192
+#define RA_BUFW 12288                 // add: u64 words: two key windows, then the block's records (RA_EPB*RC_PMAX u32)
+#define RA_SEGMAX 512                 // add: longest (block, region) segment the apply's windows take
 #define RC_BUFW 16384                 // u64 words: two key windows, then the block's records (RC_EPB*RC_PMAX u32)
 static_assert(2 * SK_PFP_WIN <= RC_BUFW && RC_EPB * RC_PMAX * 4 <= RC_BUFW * 8, "hash block LDS");
 static_assert(RC_EPB * RC_PMAX < 65536, "segment starts/counts are u16");
+static_assert(RA_EPB * 2 <= 8192 && RA_EPB % RC_TPB == 0, "add records: bit << 13 | element << 1 | last");
+static_assert(2 * SK_PFP_WIN <= RA_BUFW && RA_EPB * RC_PMAX * 4 <= RA_BUFW * 8, "add hash block LDS");
 static_assert(RC_TPB == SK_PFP_TPB, "key windows sized for SK_PFP_TPB threads");
 
+template <bool ADD>
 __global__ void __launch_bounds__(RC_TPB) k_bloom_rc_hash(uint64_t n, const uint64_t *__restrict__ off,
                                                           const uint8_t *__restrict__ bytes, uint64_t size,
                                                           uint64_t magic, uint32_t P, uint32_t NR, uint32_t NB,
                                                           uint32_t *__restrict__ S, uint32_t *__restrict__ chunks,
-                                                          uint8_t *__restrict__ out) {
-    __shared__ uint32_t hist[RC_NRMAX];
+                                                          uint8_t *__restrict__ out, uint32_t *__restrict__ flag,
+                                                          uint32_t piece) {
+    constexpr uint32_t EPB = ADD ? RA_EPB : RC_EPB;
+    constexpr int ROUNDS = int(EPB / RC_TPB);
+    constexpr uint32_t RB = ADD ? RA_RB : RC_RB, NRMAX = ADD ? RA_NRMAX : RC_NRMAX, RPT = NRMAX / RC_TPB;
+    __shared__ uint32_t hist[NRMAX];
     // block j: consecutive blocks on one XCD (blockIdx % 8 groups, speed only), so the ~32 blocks an XCD runs at
     // once write neighbouring words of each region's row of S and those lines fill in its L2
     const uint32_t jq = (NB + 7) / 8, jb = (blockIdx.x & 7u) * jq + (blockIdx.x >> 3);
     if (jb >= NB) return; // uniform
     __shared__ uint32_t wsum[RC_TPB / 64];
-    __shared__ uint64_t buf[RC_BUFW];
+    __shared__ uint64_t buf[ADD ? RA_BUFW : RC_BUFW];
     uint64_t *win[2] = {buf, buf + SK_PFP_WIN};
     uint32_t *lrec = reinterpret_cast<uint32_t *>(buf); // after the last hash round
     for (uint32_t r = threadIdx.x; r < NR; r += RC_TPB) hist[r] = 0;
-    const uint64_t base = uint64_t(jb) * RC_EPB;
+    const uint64_t base = uint64_t(jb) * EPB;
     const uint64_t rounds = (n - base + RC_TPB - 1) / RC_TPB;
-    const int nr = rounds < RC_ROUNDS ? int(rounds) : RC_ROUNDS;
-    uint64_t wb[RC_ROUNDS + 1], oa[RC_ROUNDS], ob[RC_ROUNDS];
+    const int nr = rounds < ROUNDS ? int(rounds) : ROUNDS;
+    uint64_t wb[ROUNDS + 1], oa[ROUNDS], ob[ROUNDS];
 #pragma unroll
-    for (int e = 0; e <= RC_ROUNDS; e++) {
+    for (int e = 0; e <= ROUNDS; e++) {
         uint64_t i0 = base + uint64_t(e) * RC_TPB;
         wb[e] = off[i0 < n ? i0 : n];
     }
 #pragma unroll
-    for (int e = 0; e < RC_ROUNDS; e++) {
+    for (int e = 0; e < ROUNDS; e++) {
         uint64_t i = base + uint64_t(e) * RC_TPB + threadIdx.x;
         oa[e] = ob[e] = 0;
         if (i < n) {
@@ -1098,9 +1111,9 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_rc_hash(uint64_t n, const uint
     }
     __syncthreads(); // hist zeroed, window 0 staged
     // probe p of round e: bit index (< 2^32: sizes <= 4,294,967,294) and its rank in its region
-    uint32_t ix[RC_ROUNDS][RC_PMAX], rk[RC_ROUNDS][RC_PMAX / 2]; // u16 ranks, two per word
+    uint32_t ix[ROUNDS][RC_PMAX], rk[ROUNDS][RC_PMAX / 2]; // u16 ranks, two per word
 #pragma unroll
-    for (int e = 0; e < RC_ROUNDS; e++) {
+    for (int e = 0; e < ROUNDS; e++) {
 #pragma unroll
         for (int q = 0; q < RC_PMAX; q++) ix[e][q] = 0;
 #pragma unroll
@@ -1119,14 +1132,14 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_rc_hash(uint64_t n, const uint
             } else {
                 bloom_hashes(bytes + oa[e], len, &h1, &h2);
             }
-            out[i] = 1;
+            if (!ADD) out[i] = 1;
             uint64_t h = h1;
 #pragma unroll
             for (int p = 0; p < RC_PMAX; p++) {
                 if (uint32_t(p) >= P) break;
                 uint32_t idx = uint32_t(mod_invariant(h & 0x7fffffffffffffffull, size, magic));
                 ix[e][p] = idx;
-                uint32_t rank = atomicAdd(&hist[idx >> RC_RB], 1u);
+                uint32_t rank = atomicAdd(&hist[idx >> RB], 1u);
                 rk[e][p >> 1] |= rank << ((p & 1) * 16);
                 h += (p & 1) ? h1 : h2;
             }
@@ -1134,20 +1147,21 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_rc_hash(uint64_t n, const uint
         if (pre) pfp_win_store(wb[e + 1], wb[e + 2], v, win[(e + 1) & 1]);
         __syncthreads(); // window e+1 staged; window e free for round e+2
     }
-    // segment starts: 4 consecutive regions per thread
-    uint32_t c4[4], s4 = 0;
+    // segment starts: RPT consecutive regions per thread
+    uint32_t c4[RPT], s4 = 0;
 #pragma unroll
-    for (int q = 0; q < 4; q++) {
-        uint32_t r = threadIdx.x * 4 + q;
+    for (uint32_t q = 0; q < RPT; q++) {
+        uint32_t r = threadIdx.x * RPT + q;
         c4[q] = r < NR ? hist[r] : 0u;
         s4 += c4[q];
     }
     uint32_t tot;
     uint32_t st = block_exscan<RC_TPB>(s4, wsum, &tot);
 #pragma unroll
-    for (int q = 0; q < 4; q++) { // S is region-major: S[r * NB + block]
-        uint32_t r = threadIdx.x * 4 + q;
+    for (uint32_t q = 0; q < RPT; q++) { // S is region-major: S[r * NB + block]
+        uint32_t r = threadIdx.x * RPT + q;
         if (r < NR) {
+            if (ADD && c4[q] > RA_SEGMAX) atomicMin(flag, piece); // the apply's windows assume short segments
             hist[r] = st;
             S[uint64_t(r) * NB + jb] = st | (c4[q] << 16);
         }
@@ -1155,18 +1169,20 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_rc_hash(uint64_t n, const uint
     }
     __syncthreads();
 #pragma unroll
-    for (int e = 0; e < RC_ROUNDS; e++) {
+    for (int e = 0; e < ROUNDS; e++) {
         uint64_t i = base + uint64_t(e) * RC_TPB + threadIdx.x;
         if (e >= nr || i >= n) continue;
 #pragma unroll
         for (int p = 0; p < RC_PMAX; p++) {
             if (uint32_t(p) >= P) break;
             uint32_t idx = ix[e][p], rank = (rk[e][p >> 1] >> ((p & 1) * 16)) & 0xffffu;
-            lrec[hist[idx >> RC_RB] + rank] = (idx << 12) | (uint32_t(e) * RC_TPB + threadIdx.x);
+            const uint32_t el = uint32_t(e) * RC_TPB + threadIdx.x;
+            lrec[hist[idx >> RB] + rank] =
+                ADD ? (idx << 13) | (el << 1) | (uint32_t(p) + 1 == P ? 1u : 0u) : (idx << 12) | el;
         }
     }
     __syncthreads();
-    uint4 *dst = reinterpret_cast<uint4 *>(chunks + uint64_t(jb) * RC_EPB * P);
+    uint4 *dst = reinterpret_cast<uint4 *>(chunks + uint64_t(jb) * EPB * P);
     const uint4 *src = reinterpret_cast<const uint4 *>(lrec);
     for (uint32_t t = threadIdx.x; t < (tot + 3) / 4; t += RC_TPB) dst[t] = src[t];
 }
@@ -1257,6 +1273,197 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_rc_probe(uint32_t NB, uint32_t
             if (u + 1 < RC_SMAX) rc_load_seg(chunks, CH, threadIdx.x + (u + 1) * RC_TPB, seg0[u + 1], (u & 1) ? wa : wb);
             rc_test_seg(fb, chunks, CH, threadIdx.x + u * RC_TPB, seg0[u], (u & 1) ? wb : wa, out);
         }
+    }
+}
+
+// ---------------------------------------------- Bloom add, region schedule
+// The add side of the region schedule (the rocPRIM sort path is left for k > RC_PMAX and for the rare piece with
+// a segment longer than RA_SEGMAX, i.e. one element repeated hundreds of times in one block):
+//   k_bloom_rc_hash<true>  as for contains, with all k probes, RA_EPB elements per block and records
+//                          bit-in-region << 12 | element-in-block << 1 | (probe == k-1); a segment longer than
+//                          RA_SEGMAX raises *flag, and the host then takes the sort path for that piece.
+//   k_bloom_ra_apply       one workgroup per region.  Reference semantics (M:RedissonBloomFilter.java:94-113,
+//                          oracle bloom_add): the batch's SETBITs run in (element, probe) order, each replies the
+//                          bit before it, and add() is true iff one of probes 0..k-2 replied 0.  So a probe is the
+//                          setter of its bit iff the bit is 0 before the batch and no probe with a smaller
+//                          (block, element) key touched it (two probes of one element on one bit share the key: the
+//                          non-last one answers).
+// A region's records are taken in windows of whole segments in block order (= batch order).  Inside a window the
+// records of a bit are chained in LDS and each looks for a smaller key on its chain; the window's setters then set
+// their bits, which later windows see.  A dense region (>= RA_DENSE records) keeps its 128 KiB of bits in LDS
+// (one coalesced load and store); a sparse one reads and sets the words in place (device-scope atomics: a
+// region's words belong to its workgroup alone).  Every probe extends the string to its byte (SETBIT grows it).
+#define RA_CAP 8192   // records per window (LDS)
+#define RA_HT 4096    // chain heads
+#define RA_DENSE 1024 // records from which the region's bits are staged in LDS
+#define RA_JPT 4      // blocks per thread (block j = q * RC_TPB + thread): pieces of <= 4096 blocks (8 M elements)
+#define RA_NONE 0xffffffffu
+#define RA_RPT (RA_CAP / RC_TPB)
+static_assert(RA_CAP >= 2 * RA_SEGMAX && RA_CAP % RC_TPB == 0 && RA_CAP < 0xffff, "windows: u16 links");
+static_assert(RA_JPT * RC_TPB <= 8192, "block numbers: 13 bits of the order key");
+
+__device__ __forceinline__ uint32_t ra_mask(uint32_t b) { return (0x80u >> (b & 7u)) << (((b >> 3) & 3u) * 8u); }
+__device__ __forceinline__ uint32_t ra_key(uint32_t blk, uint32_t x) { return (blk << 11) | ((x >> 1) & 0x7ffu); }
+
+__global__ void __launch_bounds__(RC_TPB) k_bloom_ra_apply(uint32_t NB, uint32_t NR, const uint32_t *__restrict__ S,
+                                                           const uint32_t *__restrict__ chunks, uint32_t P,
+                                                           uint8_t *bits, uint64_t cap_bytes,
+                                                           unsigned long long *d_len, uint8_t *__restrict__ out,
+                                                           const uint32_t *__restrict__ stop, uint32_t piece,
+                                                           int big) {
+    constexpr uint32_t NW = 1u << (RA_RB - 5); // u32 words per region
+    __shared__ uint32_t filt[NW];
+    __shared__ uint32_t rec[RA_CAP];
+    __shared__ uint16_t blk[RA_CAP];
+    __shared__ uint16_t nxt[RA_CAP];
+    __shared__ uint32_t head[RA_HT];
+    __shared__ uint32_t wsum[RC_TPB / 64];
+    __shared__ uint32_t wbase, wend, maxb;
+    const uint32_t r = rc_region(blockIdx.x, NR);
+    if (r >= NR || *stop <= piece) return; // uniform (stop: a hash pass of this or an earlier piece saw a long segment)
+    const uint64_t b0 = uint64_t(r) << (RA_RB - 3);
+    uint32_t *gw = reinterpret_cast<uint32_t *>(bits + b0);
+    constexpr uint32_t VT = NW / 4 / RC_TPB;
+    uint4 t[VT]; // big pieces: the region's bits are loaded while the segment table is scanned
+    if (big) {
+        const uint4 *src = reinterpret_cast<const uint4 *>(gw);
+#pragma unroll
+        for (uint32_t q = 0; q < VT; q++) { // no branch around the loads: all in flight
+            const uint32_t v = threadIdx.x + q * RC_TPB;
+            const bool ok = b0 + uint64_t(v) * 16 < cap_bytes;
+            t[q] = src[ok ? v : 0u];
+            if (!ok) t[q] = make_uint4(0, 0, 0, 0);
+        }
+    }
+    const uint32_t CH = RA_EPB * P; // words per block chunk (NB * CH < 2^32: pieces of <= 16 M elements)
+    uint32_t sg[RA_JPT], pre[RA_JPT], total = 0;
+#pragma unroll
+    for (int q = 0; q < RA_JPT; q++) {
+        uint32_t j = uint32_t(q) * RC_TPB + threadIdx.x;
+        sg[q] = j < NB ? S[uint64_t(r) * NB + j] : 0u;
+    }
+#pragma unroll
+    for (int q = 0; q < RA_JPT; q++) { // segment positions in block order: row q = blocks q*RC_TPB..
+        pre[q] = total;
+        if (uint32_t(q) * RC_TPB >= NB) continue; // uniform
+        uint32_t tq, e = block_exscan<RC_TPB>(sg[q] >> 16, wsum, &tq);
+        pre[q] = total + e;
+        total += tq;
+    }
+    if (total == 0) return; // uniform: no probe in this region
+    const bool dense = big || total >= RA_DENSE;
+    if (dense) { // bytes past the buffer read as 0 and are not written back
+        uint4 *fv = reinterpret_cast<uint4 *>(filt);
+        if (!big) {
+            const uint4 *src = reinterpret_cast<const uint4 *>(gw);
+#pragma unroll
+            for (uint32_t q = 0; q < VT; q++) {
+                const uint32_t v = threadIdx.x + q * RC_TPB;
+                const bool ok = b0 + uint64_t(v) * 16 < cap_bytes;
+                t[q] = src[ok ? v : 0u];
+                if (!ok) t[q] = make_uint4(0, 0, 0, 0);
+            }
+        }
+#pragma unroll
+        for (uint32_t q = 0; q < VT; q++) fv[threadIdx.x + q * RC_TPB] = t[q];
+    }
+    for (uint32_t t = threadIdx.x; t < RA_HT; t += RC_TPB) head[t] = RA_NONE;
+    if (threadIdx.x == 0) maxb = 0;
+    uint32_t mymax = 0;
+    bool anyset = false;
+    constexpr uint32_t W = RA_CAP - RA_SEGMAX;
+    for (uint32_t lo = 0; lo < total; lo += W) {
+        if (threadIdx.x == 0) {
+            wbase = RA_NONE;
+            wend = 0;
+        }
+        __syncthreads(); // (first window: bits staged, heads cleared)
+        // the window = the segments starting in [lo, lo + W), laid out from the first one's start (a segment that
+        // starts in the previous window belongs to it whole)
+#pragma unroll
+        for (int q = 0; q < RA_JPT; q++) {
+            const uint32_t cnt = sg[q] >> 16;
+            if (cnt == 0 || pre[q] < lo || pre[q] >= lo + W) continue;
+            atomicMin(&wbase, pre[q]);
+            atomicMax(&wend, pre[q] + cnt);
+        }
+        __syncthreads();
+        const uint32_t base = wbase; // RA_NONE: no segment starts here (wend = 0, nw = 0)
+#pragma unroll
+        for (int q = 0; q < RA_JPT; q++) { // owners write each record's chunk word index
+            const uint32_t cnt = sg[q] >> 16;
+            if (cnt == 0 || pre[q] < lo || pre[q] >= lo + W) continue;
+            const uint32_t j = uint32_t(q) * RC_TPB + threadIdx.x, d = pre[q] - base;
+            const uint32_t src = j * CH + (sg[q] & 0xffffu);
+#pragma unroll 1
+            for (uint32_t u = 0; u < cnt; u++) {
+                rec[d + u] = src + u;
+                blk[d + u] = uint16_t(j);
+            }
+        }
+        __syncthreads();
+        const uint32_t nw = base == RA_NONE ? 0u : wend - base; // <= W + RA_SEGMAX = RA_CAP
+#pragma unroll 1
+        for (uint32_t g = 0; g < RA_RPT; g += 4) { // this thread's records of the window, 4 loads in flight
+            uint32_t x[4];
+#pragma unroll
+            for (uint32_t q = 0; q < 4; q++) {
+                const uint32_t u = threadIdx.x + (g + q) * RC_TPB;
+                x[q] = u < nw ? chunks[rec[u]] : 0u;
+            }
+#pragma unroll
+            for (uint32_t q = 0; q < 4; q++) {
+                const uint32_t u = threadIdx.x + (g + q) * RC_TPB;
+                if (u < nw) {
+                    rec[u] = x[q];
+                    nxt[u] = uint16_t(atomicExch(&head[(x[q] >> 13) & (RA_HT - 1)], u));
+                }
+            }
+        }
+        __syncthreads();
+        uint32_t first = 0; // bit q: record q of this thread sets its bit
+#pragma unroll 1
+        for (uint32_t q = 0; q < RA_RPT; q++) {
+            const uint32_t u = threadIdx.x + q * RC_TPB;
+            if (u >= nw) break;
+            const uint32_t xu = rec[u], b = xu >> 13;
+            mymax = b > mymax ? b : mymax;
+            const uint32_t w = dense ? filt[b >> 5]
+                                     : __hip_atomic_load(gw + (b >> 5), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (w & ra_mask(b)) continue; // set before this probe: not a setter
+            const uint32_t key = ra_key(blk[u], xu);
+            bool f = true;
+            for (uint32_t v = head[b & (RA_HT - 1)]; v < RA_CAP && f; v = nxt[v]) { // RA_NONE / 0xffff end a chain
+                const uint32_t xv = rec[v];
+                if ((xv >> 13) == b && ra_key(blk[v], xv) < key) f = false;
+            }
+            if (!f) continue;
+            first |= 1u << q;
+            if (!(xu & 1u)) out[uint64_t(blk[u]) * RA_EPB + ((xu >> 1) & 0x7ffu)] = 1;
+        }
+        __syncthreads(); // every probe of the window has read the bits
+#pragma unroll 1
+        for (uint32_t q = 0; q < RA_RPT; q++) {
+            const uint32_t u = threadIdx.x + q * RC_TPB;
+            if (u >= nw) break;
+            const uint32_t b = rec[u] >> 13;
+            if (first & (1u << q)) {
+                anyset = true;
+                if (dense) atomicOr(&filt[b >> 5], ra_mask(b));
+                else __hip_atomic_fetch_or(gw + (b >> 5), ra_mask(b), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            head[b & (RA_HT - 1)] = RA_NONE;
+        }
+    }
+    atomicMax(&maxb, mymax);
+    const bool changed = __syncthreads_or(anyset);
+    if (threadIdx.x == 0) atomicMax(d_len, (unsigned long long)(b0 + (maxb >> 3) + 1));
+    if (dense && changed) {
+        uint4 *dst = reinterpret_cast<uint4 *>(gw);
+        const uint4 *fv = reinterpret_cast<const uint4 *>(filt);
+#pragma unroll
+        for (uint32_t v = threadIdx.x; v < NW / 4; v += RC_TPB)
+            if (b0 + uint64_t(v) * 16 < cap_bytes) dst[v] = fv[v];
     }
 }
 
@@ -1704,7 +1911,11 @@ hipError_t launch_pfp_hash(hipStream_t st, uint64_t n, const uint32_t *key_ids, 
 hipError_t launch_pfp_apply(hipStream_t st, uint64_t n, const uint64_t *chunks, const uint32_t *S, uint8_t *arena,
                             uint8_t *rep, uint32_t *big_alloc, uint64_t *big_keys, uint32_t *big_vals,
                             uint8_t *changed) {
-    hipLaunchKernelGGL(k_pfp_apply, dim3(SK_PFP_NB), dim3(SK_PFP_ATPB), 0, st, chunks, S, pfp_blocks(n), arena, rep,
+    static const unsigned dlds = [] { // experiment knob: extra dynamic LDS lowers apply occupancy (0 = off)
+        const char *e = getenv("SK_PFA_DLDS");
+        return e ? unsigned(atoi(e)) : 0u;
+    }();
+    hipLaunchKernelGGL(k_pfp_apply, dim3(SK_PFP_NB), dim3(SK_PFP_ATPB), dlds, st, chunks, S, pfp_blocks(n), arena, rep,
                        big_alloc, big_keys, big_vals, changed);
     SK_LAUNCH_CHECK();
     return hipSuccess;
@@ -1834,13 +2045,43 @@ uint32_t rc_regions(uint64_t size) { return uint32_t((size + (1ull << RC_RB) - 1
 uint32_t rc_max_probes() { return RC_PMAX; }
 uint64_t rc_chunk_words(int k) { return uint64_t(RC_EPB) * uint64_t(k - 1); }
 
+uint32_t ra_blocks(uint64_t n) { return uint32_t((n + RA_EPB - 1) / RA_EPB); }
+uint32_t ra_regions(uint64_t size) { return uint32_t((size + (1ull << RA_RB) - 1) >> RA_RB); }
+uint64_t ra_piece() { return uint64_t(RA_JPT) * RC_TPB * RA_EPB; }
+uint64_t ra_chunk_words(int k) { return uint64_t(RA_EPB) * uint64_t(k); }
+
+// Bloom add, region schedule: records u32[ra_blocks(n) * ra_chunk_words(k)], S u32[regions * blocks], *flag = 0 before
+hipError_t launch_bloom_ra_hash(hipStream_t st, uint64_t n, const uint64_t *off, const uint8_t *bytes, uint64_t size,
+                                uint64_t magic, int k, uint32_t *S, uint32_t *recs, uint32_t *stop, uint32_t piece) {
+    if (!n) return hipSuccess;
+    uint32_t NB = ra_blocks(n);
+    hipLaunchKernelGGL(k_bloom_rc_hash<true>, dim3(8 * ((NB + 7) / 8)), dim3(RC_TPB), 0, st, n, off, bytes, size,
+                       magic, uint32_t(k), ra_regions(size), NB, S, recs, nullptr, stop, piece);
+    SK_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+hipError_t launch_bloom_ra_apply(hipStream_t st, uint64_t n, uint64_t size, int k, const uint32_t *S,
+                                 const uint32_t *recs, uint8_t *bits, uint64_t cap_bytes, uint64_t *d_len,
+                                 uint8_t *out, const uint32_t *stop, uint32_t piece) {
+    if (!n) return hipSuccess;
+    uint32_t NR = ra_regions(size);
+    // every region of a big piece expects >= RA_DENSE records: its bits are loaded up front
+    const int big = n * uint64_t(k) >= uint64_t(2 * RA_DENSE) * NR;
+    hipLaunchKernelGGL(k_bloom_ra_apply, dim3(8 * ((NR + 7) / 8)), dim3(RC_TPB), 0, st, ra_blocks(n), NR, S, recs,
+                       uint32_t(k), bits, cap_bytes, reinterpret_cast<unsigned long long *>(d_len), out, stop, piece,
+                       big);
+    SK_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
 // region schedule: records u32[blocks * RC_EPB * (k-1)], S u32[regions * blocks]
 hipError_t launch_bloom_rc_hash(hipStream_t st, uint64_t n, const uint64_t *off, const uint8_t *bytes, uint64_t size,
                                 uint64_t magic, int k, uint32_t *S, uint32_t *recs, uint8_t *out) {
     if (!n) return hipSuccess;
     uint32_t NB = rc_blocks(n);
-    hipLaunchKernelGGL(k_bloom_rc_hash, dim3(8 * ((NB + 7) / 8)), dim3(RC_TPB), 0, st, n, off, bytes, size, magic,
-                       uint32_t(k - 1), rc_regions(size), NB, S, recs, out);
+    hipLaunchKernelGGL(k_bloom_rc_hash<false>, dim3(8 * ((NB + 7) / 8)), dim3(RC_TPB), 0, st, n, off, bytes, size,
+                       magic, uint32_t(k - 1), rc_regions(size), NB, S, recs, out, nullptr, 0u);
     SK_LAUNCH_CHECK();
     return hipSuccess;
 }

@@ -268,6 +268,8 @@ struct sk_ctx {
     bool pfp_pipe = true;
     bool pf_dev_call = false;   // inside sk_pfadd_dev: inputs are caller-owned device memory, no host staging
     hipStream_t st3 = nullptr;
+    uint64_t bloom_ra_min = 1;  // add batches >= this use the region schedule (SK_BLOOM_RA_MIN, 0 = never: sort path)
+    DBuf ra_S, ra_rec, ra_flag;
     uint64_t bloom_rc_min = 2u << 20; // contains batches >= this use the region schedule (SK_BLOOM_RC_MIN, 0 = never)
 };
 
@@ -330,7 +332,7 @@ const char *kPhaseNames[] = {"pfadd_hash",  "pfadd_sort",   "pfadd_apply", "hll_
                              "bloom_contains", "bloom_probes", "bloom_sort", "bloom_apply", "setbit",
                              "getbit",      "bitcount",     "bitop",       "pfadd_claim", "pfadd_commit",
                              "pfp_hash",    "pfp_apply",    "pfp_reply",   "bloom_rc_hash", "bloom_rc_probe", "pfadd",
-                             "pfadd_long"};
+                             "pfadd_long",  "bloom_ra_hash", "bloom_ra_apply"};
 constexpr int kNumPhases = sizeof(kPhaseNames) / sizeof(kPhaseNames[0]);
 
 hipEvent_t ev_get(sk_ctx *c) {
@@ -924,6 +926,7 @@ int sk_open(const sk_config *cfg, sk_ctx **out) {
     if (const char *e = getenv("SK_PFADD_PATH")) c->pfadd_path = atoi(e);
     if (const char *e = getenv("SK_PFP_DIRECT")) c->pfp_direct = atoi(e) != 0;
     if (const char *e = getenv("SK_BLOOM_RC_MIN")) c->bloom_rc_min = strtoull(e, nullptr, 10);
+    if (const char *e = getenv("SK_BLOOM_RA_MIN")) c->bloom_ra_min = strtoull(e, nullptr, 10);
     if (const char *e = getenv("SK_PFP_PIPE")) c->pfp_pipe = atoi(e) != 0;
     uint64_t cap = (cfg && cfg->hll_capacity) ? cfg->hll_capacity : 1024;
     if (hll_grow(c, cap) != SK_OK || c->misc.ensure(4096) != hipSuccess ||
@@ -2060,10 +2063,54 @@ int sk_bloom_config(sk_ctx *c, const uint8_t *name, uint64_t len, int64_t *size,
 }
 
 // shared by the host and device Bloom paths; inputs already on device
+static int bloom_add_sorted(sk_ctx *c, uint32_t id, int64_t size, int32_t k, uint64_t n, const uint64_t *d_off,
+                            const uint8_t *d_bytes, uint8_t *d_out);
+
+// RBloomFilter.add of n device elements (d_out zeroed here, then 1 for every add that set a bit).  The region
+// schedule (sk_kernels.hip "Bloom add, region schedule") in pieces of <= ra_piece() elements, all enqueued without
+// a host wait; a hash pass that finds a segment longer than RA_SEGMAX (one element repeated hundreds of times in a
+// block) lowers the device word `stop` to its piece number, every apply from that piece on does nothing, and the
+// host -- one read at the end -- redoes those pieces on the sort path in order.  k > rc_max_probes() takes the
+// sort path whole.
 static int bloom_add_device(sk_ctx *c, uint32_t id, int64_t size, int32_t k, uint64_t n, const uint64_t *d_off,
                             const uint8_t *d_bytes, uint8_t *d_out) {
     if (!n) return SK_OK;
     HIPCHK(c, hipMemsetAsync(d_out, 0, n, c->st));
+    const uint64_t usize = uint64_t(size);
+    if (!(c->bloom_ra_min && n >= c->bloom_ra_min && k >= 1 && uint32_t(k) <= sk::rc_max_probes()))
+        return bloom_add_sorted(c, id, size, k, n, d_off, d_bytes, d_out);
+    const uint64_t magic = magic_for(usize), piece = sk::ra_piece();
+    const uint64_t nb = sk::ra_blocks(std::min(n, piece)), nr = sk::ra_regions(usize);
+    HIPCHK(c, c->ra_S.ensure(nb * nr * 4));
+    HIPCHK(c, c->ra_rec.ensure(nb * sk::ra_chunk_words(k) * 4));
+    HIPCHK(c, c->ra_flag.ensure(4));
+    uint32_t *stop = c->ra_flag.as<uint32_t>();
+    HIPCHK(c, hipMemsetAsync(stop, 0xff, 4, c->st));
+    uint32_t np = 0;
+    for (uint64_t s0 = 0; s0 < n; s0 += piece, np++) {
+        const uint64_t m = std::min(piece, n - s0);
+        { Prof q_(c, 22);
+        HIPCHK(c, sk::launch_bloom_ra_hash(c->st, m, d_off + s0, d_bytes, usize, magic, k, c->ra_S.as<uint32_t>(),
+                                           c->ra_rec.as<uint32_t>(), stop, np)); }
+        { Prof q_(c, 23);
+        HIPCHK(c, sk::launch_bloom_ra_apply(c->st, m, usize, k, c->ra_S.as<uint32_t>(), c->ra_rec.as<uint32_t>(),
+                                            c->strs[id].ptr, c->strs[id].cap, &c->d_dir[id].len, d_out + s0, stop,
+                                            np)); }
+    }
+    uint32_t first_bad = 0;
+    HIPCHK(c, hipMemcpyAsync(&first_bad, stop, 4, hipMemcpyDeviceToHost, c->st));
+    int r = sync(c);
+    if (r) return r;
+    for (uint64_t p = first_bad; p < np; p++) { // (first_bad = 0xffffffff: every piece was applied)
+        const uint64_t s0 = p * piece, m = std::min(piece, n - s0);
+        if ((r = bloom_add_sorted(c, id, size, k, m, d_off + s0, d_bytes, d_out + s0))) return r;
+    }
+    return SK_OK;
+}
+
+// the sort path: d_out already zeroed
+static int bloom_add_sorted(sk_ctx *c, uint32_t id, int64_t size, int32_t k, uint64_t n, const uint64_t *d_off,
+                            const uint8_t *d_bytes, uint8_t *d_out) {
     // probes per sort: the apply sweeps the touched words of the bit array once per sort, so bigger sorts
     // amortise it (a C3 filter is ~4.2 M lines); keys are idx << 32 | probe number (< 2^32)
     uint64_t per = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t(1) << 27) / uint64_t(k), 0xffffffffull / uint64_t(k)));

@@ -122,3 +122,128 @@ def test_region_contains_host_path(O):
         assert np.array_equal(got, want)
     finally:
         eng.close()
+
+
+# ------------------------------------------------------------------ Bloom add, region schedule
+def _add_case(O, eng, name, n_exp, k, batches):
+    """Adds `batches` (lists of byte elements) in order through sk_bloom_add; every reply and the whole string
+    must equal the oracle's (one SETBIT per probe in (element, probe) order, M:RedissonBloomFilter.java:94-113)."""
+    p = _p_for_k(k, n_exp)
+    assert eng.bloom_try_init(name, n_exp, p)
+    size, kk, _, _ = eng.bloom_config(name)
+    assert kk == k
+    ref = O.BitString(16)
+    for b in batches:
+        got = eng.bloom_add(name, size, k, b)
+        want = ref.bloom_add(size, k, b)
+        assert got == want, "k=%d add replies differ at %s" % (
+            k, [i for i, (g, w) in enumerate(zip(got, want)) if g != w][:8])
+    assert eng.get(name) == ref.bytes()
+    return size
+
+
+def _longs(a, b):
+    return [b'["java.lang.Long",%d]' % i for i in range(a, b)]
+
+
+@pytest.mark.parametrize("k", [1, 2, 3, 5, 7, 8, 9])
+def test_region_add_every_k(O, k):
+    """Two overlapping batches of 150 k adds (the second repeats half of the first, and repeats inside itself) on a
+    filter of >= 8 regions: replies and the bit string equal the oracle's for every k the schedule takes (1..8)
+    and for k = 9 (the sort path)."""
+    eng = _engine(max_batch=4 * M)
+    try:
+        first = _longs(0, 150_000)
+        second = _longs(75_000, 200_000) + _longs(190_000, 215_000)
+        rng = np.random.default_rng(k)
+        np.random.default_rng(k).shuffle(second)
+        second = [second[i] if rng.random() < 0.9 else first[int(rng.integers(0, 150_000))] for i in range(len(second))]
+        _add_case(O, eng, "ra:k%d" % k, 4_000_000, k, [first, second])
+    finally:
+        eng.close()
+
+
+def test_region_add_windows_and_small_filters(O):
+    """One-region filters (m < 2^20) filled far past one window per region (dense, hundreds of windows), a filter
+    whose regions stay sparse (words set in place), and batches of 1, 2 and 2049 elements."""
+    eng = _engine(max_batch=4 * M)
+    try:
+        _add_case(O, eng, "raw:one", 50_000, 7, [_longs(0, 120_000), _longs(100_000, 130_000)])
+        _add_case(O, eng, "raw:sparse", 50_000_000, 5, [_longs(0, 3000), _longs(2000, 2500)])
+        _add_case(O, eng, "raw:tiny", 1_000_000, 7, [_longs(5, 6), _longs(5, 7), _longs(0, 2049), _longs(7, 8)])
+    finally:
+        eng.close()
+
+
+def test_region_add_repeated_element_takes_sort_path(O):
+    """One element repeated 5000 times in a batch puts > RA_SEGMAX records of one block in one region: the piece
+    goes to the sort path; replies (only the first copy answers true) and bits equal the oracle's either way."""
+    eng = _engine(max_batch=4 * M)
+    try:
+        rep = [b'"same"'] * 5000 + _longs(0, 3000) + [b'"same"', b'"other"', b'"other"']
+        _add_case(O, eng, "rar", 1_000_000, 7, [rep, _longs(2000, 4000)])
+    finally:
+        eng.close()
+
+
+def test_region_add_device_pieces_match_gen(O, monkeypatch):
+    """A 20 M device add runs as a 16 M piece and a 4 M piece (then a second add of 2 M old + 1 M new elements):
+    the string and every reply equal the sequential oracle's."""
+    eng = _engine(max_batch=4 * M)
+    try:
+        p = _p_for_k(7, 30_000_000)
+        assert eng.bloom_try_init("rap", 30_000_000, p)
+        size, k, _, _ = eng.bloom_config("rap")
+        seed, n = 0x5EED7500, 20 * M + 3
+        off, byt, tot = eng.gen_jackson_longs_dev(seed, n)
+        d_out = eng.alloc(n)
+        eng.bloom_add_dev("rap", n, off, byt, tot, d_out)
+        bits, ln, want = O.bloom_add_gen_seq(size, k, seed, 0, n)
+        got = eng.get("rap")
+        assert len(got) == ln and np.array_equal(np.frombuffer(got, np.uint8), bits[:ln])
+        rep = d_out.download(np.uint8, n)
+        assert np.array_equal(rep, want), np.flatnonzero(rep != want)[:8]
+        for x in (off, byt, d_out):
+            x.free()
+        # elements n-2M .. n+1M: the first 2 M are already in (only false positives of the sequential order differ)
+        off, byt, tot = eng.gen_jackson_longs_dev(seed, 3 * M, first=n - 2 * M)
+        d_out = eng.alloc(3 * M)
+        eng.bloom_add_dev("rap", 3 * M, off, byt, tot, d_out)
+        b2, ln2, w2 = O.bloom_add_gen_seq(size, k, seed, 0, n + M)
+        got = eng.get("rap")
+        assert len(got) == ln2 and np.array_equal(np.frombuffer(got, np.uint8), b2[:ln2])
+        rep = d_out.download(np.uint8, 3 * M)
+        assert not rep[:2 * M].any()
+        assert np.array_equal(rep[2 * M:], w2[n:]), np.flatnonzero(rep[2 * M:] != w2[n:])[:8]
+        for x in (off, byt, d_out):
+            x.free()
+    finally:
+        eng.close()
+
+
+def test_region_add_late_piece_falls_back_in_order(O):
+    """A 9 M device add whose second piece (from element 8 M) holds one element 3000 times: piece 0 runs on the
+    region schedule, the hash pass of piece 1 stops every later apply and the host redoes piece 1 on the sort path.
+    Bits and every reply equal the sequential oracle's."""
+    eng = _engine(max_batch=4 * M)
+    try:
+        p = _p_for_k(7, 20_000_000)
+        assert eng.bloom_try_init("ral", 20_000_000, p)
+        size, k, _, _ = eng.bloom_config("ral")
+        seed, n = 0x5EED7600, 9 * M
+        idx = np.arange(n, dtype=np.uint64)
+        idx[8 * M + 1000:8 * M + 4000] = 42
+        d_idx = eng.to_device(idx)
+        off, byt, tot = eng.gen_jackson_longs_dev(seed, n, d_idx=d_idx)
+        d_out = eng.alloc(n)
+        eng.bloom_add_dev("ral", n, off, byt, tot, d_out)
+        bits = np.zeros((size + 7) // 8 + 16, dtype=np.uint8)
+        ln, want = O.bloom_add_idx_seq(bits, 0, size, k, seed, idx)
+        got = eng.get("ral")
+        assert len(got) == ln and np.array_equal(np.frombuffer(got, np.uint8), bits[:ln])
+        rep = d_out.download(np.uint8, n)
+        assert np.array_equal(rep, want), np.flatnonzero(rep != want)[:8]
+        for x in (d_idx, off, byt, d_out):
+            x.free()
+    finally:
+        eng.close()

@@ -139,6 +139,27 @@ public class GpuSketchBatchService extends CommandBatchService {
             return getConnectionManager().newSucceededFuture(null);
         }
         executed = true;
+        final Promise<List<?>> result = getConnectionManager().newPromise();
+        // the sketch runs and the hand-off of the redis part happen on the context's worker: the caller (maybe an
+        // event-loop thread) never waits on the device
+        try {
+            SketchDispatch.worker(ctx).execute(new Runnable() {
+                @Override
+                public void run() {
+                    try {
+                        executeOnWorker(result);
+                    } catch (RuntimeException e) {
+                        result.tryFailure(e);
+                    }
+                }
+            });
+        } catch (java.util.concurrent.RejectedExecutionException e) {
+            result.tryFailure(new IllegalStateException("sketch engine shut down", e));
+        }
+        return result;
+    }
+
+    void executeOnWorker(final Promise<List<?>> result) {
         int i = 0;
         while (i < sketch.size()) {
             String kind = sketch.get(i).command.getName();
@@ -158,7 +179,6 @@ public class GpuSketchBatchService extends CommandBatchService {
         // the redis-side commands are sent whatever happened above (the reference pipeline executes them all)
         Future<List<?>> redis = redisUsed ? super.executeAsync()
                 : getConnectionManager().<List<?>>newSucceededFuture(null);
-        final Promise<List<?>> result = getConnectionManager().newPromise();
         redis.addListener(new FutureListener<List<?>>() {
             @Override
             public void operationComplete(Future<List<?>> f) throws Exception {
@@ -185,7 +205,6 @@ public class GpuSketchBatchService extends CommandBatchService {
                 }
             }
         });
-        return result;
     }
 
     static boolean runnable(String kind) {

@@ -19,6 +19,7 @@ import java.util.Arrays;
 import java.util.HashSet;
 import java.util.List;
 import java.util.Set;
+import java.util.concurrent.RejectedExecutionException;
 
 import org.redisson.client.RedisException;
 import org.redisson.client.codec.Codec;
@@ -48,15 +49,44 @@ public class GpuSketchCommandService extends CommandAsyncService {
     static final Encoder PARAMS = new DefaultParamsEncoder();
 
     final long ctx;
-
+    /* Engine work never runs on the caller's thread (often a Netty event-loop thread, SURVEY 8b): the context's
+     * FIFO worker (SketchDispatch.worker) makes the JNI calls -- which may wait on the device -- and completes the
+     * promises, so the engine sees one caller's commands in the order they were issued.  Commands for redis-server
+     * are handed to the reference path at once, or from the worker once it knows the engine does not hold the
+     * key. */
     public GpuSketchCommandService(ConnectionManager connectionManager, long ctx) {
         super(connectionManager);
         this.ctx = ctx;
     }
 
     @Override
-    protected <V, R> void async(boolean readOnlyMode, NodeSource source, Codec codec, RedisCommand<V> command,
-                                Object[] params, Promise<R> mainPromise, int attempt) {
+    protected <V, R> void async(final boolean readOnlyMode, final NodeSource source, final Codec codec,
+                                final RedisCommand<V> command, final Object[] params, final Promise<R> mainPromise,
+                                final int attempt) {
+        String name = command.getName();
+        if (!SKETCH_COMMANDS.contains(name) && !KEY_COMMANDS.contains(name) && !"FLUSHALL".equals(name)) {
+            super.async(readOnlyMode, source, codec, command, params, mainPromise, attempt);
+            return;
+        }
+        try {
+            SketchDispatch.worker(ctx).execute(new Runnable() {
+                @Override
+                public void run() {
+                    try {
+                        engineAsync(readOnlyMode, source, codec, command, params, mainPromise, attempt);
+                    } catch (RuntimeException e) {
+                        mainPromise.tryFailure(e);
+                    }
+                }
+            });
+        } catch (RejectedExecutionException e) {
+            mainPromise.tryFailure(new IllegalStateException("sketch engine shut down", e));
+        }
+    }
+
+    /* on the worker thread */
+    <V, R> void engineAsync(boolean readOnlyMode, NodeSource source, Codec codec, RedisCommand<V> command,
+                            Object[] params, Promise<R> mainPromise, int attempt) {
         String name = command.getName();
         if ("FLUSHALL".equals(name)) { // both stores; every cached slab handle is dead
             SketchDispatch.invalidateAll(ctx);

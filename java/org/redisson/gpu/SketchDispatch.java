@@ -12,6 +12,9 @@ import java.nio.charset.Charset;
 import java.util.ArrayList;
 import java.util.List;
 import java.util.concurrent.ConcurrentHashMap;
+import java.util.concurrent.ExecutorService;
+import java.util.concurrent.Executors;
+import java.util.concurrent.ThreadFactory;
 
 import org.redisson.client.RedisException;
 import org.redisson.client.codec.Codec;
@@ -39,6 +42,39 @@ public final class SketchDispatch {
     }
 
     static final Charset ISO = Charset.forName("ISO-8859-1"); // bytes <-> String one to one
+
+    /* One FIFO worker thread per engine context (SURVEY 8b: no event-loop thread waits on the device).  Single
+     * commands and RBatch sketch runs of one context are executed there in submission order. */
+    static final ConcurrentHashMap<Long, ExecutorService> WORKERS = new ConcurrentHashMap<Long, ExecutorService>();
+
+    public static ExecutorService worker(final long ctx) {
+        ExecutorService w = WORKERS.get(ctx);
+        if (w == null) {
+            ExecutorService fresh = Executors.newSingleThreadExecutor(new ThreadFactory() {
+                @Override
+                public Thread newThread(Runnable r) {
+                    Thread t = new Thread(r, "sk-engine-" + Long.toHexString(ctx));
+                    t.setDaemon(true);
+                    return t;
+                }
+            });
+            w = WORKERS.putIfAbsent(ctx, fresh);
+            if (w == null) {
+                w = fresh;
+            } else {
+                fresh.shutdown();
+            }
+        }
+        return w;
+    }
+
+    /** Before sk_close(ctx): queued work finishes, later submissions are refused. */
+    public static void shutdownWorker(long ctx) {
+        ExecutorService w = WORKERS.remove(ctx);
+        if (w != null) {
+            w.shutdown();
+        }
+    }
 
     /* Per-context HLL name -> slab handle cache (INTEGRATION.md "Caching slab ids").  Filled after a run's
      * name-path PFADD from sk_hll_lookup (which creates nothing).  Every command that can free or replace a key

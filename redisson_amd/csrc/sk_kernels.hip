@@ -290,8 +290,14 @@ __global__ void k_len_from_last_key(const uint64_t *keys, uint64_t m, uint64_t *
 static_assert(SK_PFP_ATPB / 4 * SK_PFP_EPB >= (1 << 20), "4 apply threads per hash block");
 static_assert(SK_PFP_NB <= SK_PFP_TPB, "one bucket per hash thread in the start scan");
 static_assert(SK_PFP_CAP < 0xffff, "u16 chain links");
+// a bucket takes whole runs of 32 registers of a sketch: the records of a hot sketch (C1, a Zipf head) in one
+// bucket then read their registers from one 32-B piece, so a wave's register loads coalesce into one request.
+// Run g of sketch s goes to bucket (g + hash(s)) % 512: the 512 runs of every sketch cover the 512 buckets once
+// each (one hot sketch fills every bucket evenly), and sketches are rotated against each other.
+static_assert(SK_PFP_NB == 512, "16384 registers = 512 runs of 32");
 __device__ __forceinline__ uint32_t pfp_bucket(uint64_t slot) {
-    return uint32_t((slot * 0x9E3779B97F4A7C15ull) >> 55); // 9 bits
+    const uint32_t run = uint32_t(slot >> 5) & 511u, rot = (uint32_t(slot >> 14) * 0x9E3779B1u) >> 23;
+    return (run + rot) & 511u;
 }
 __device__ __forceinline__ uint32_t pfp_ht(uint64_t slot) {
     return uint32_t((slot * 0xC2B2AE3D27D4EB4Full) >> 52); // 12 bits

@@ -179,13 +179,18 @@ def main():
         r = {p: eng.prof_read(p) for p in PHASES}
         return {p: (r[p][0] / P, r[p][1] / r[p][0]) for p in PHASES if r[p][0]}
 
-    # each kernel alone (sync mode: PFADD and contains do not overlap).  The dominant kernel is the one with the
-    # most device time per step of its own (overlapped launch times mostly measure contention).
+    # each kernel alone (sync mode: PFADD and contains do not overlap).  The roofline unit is the chain (every
+    # kernel of one PFADD batch / one contains call) with the most device time per step of its own: SURVEY 8(d)
+    # prices whole operations (53 B per PFADD element, len + 9 + 64(k-1) per contains), not single kernels.
+    # Overlapped launch times mostly measure contention.
     iso = profiled(W, False)
     kern = [p for p in iso if p not in CHAINS and p != "pfadd_sort"]
     if "bloom_rc_hash" not in iso:   # one-element-per-thread contains: the chain is one kernel
         kern.append("bloom_contains")
-    dom = max(kern, key=lambda p: iso[p][0] * iso[p][1])
+    dom_kernel = max(kern, key=lambda p: iso[p][0] * iso[p][1])
+    dom = max([c for c in CHAINS if c in iso], key=lambda c: iso[c][0] * iso[c][1])
+    chain_kernels = {"pfadd": [p for p in ("pfp_hash", "pfp_apply", "pfp_reply") if p in iso],
+                     "bloom_contains": [p for p in BLOOM_KERNELS if p in iso] or ["bloom_contains"]}
     # breakdown as in the timed region (PFADD on the main stream, contains on the read stream, no host sync)
     over = profiled(W + P, True)
 
@@ -211,7 +216,7 @@ def main():
     eng.set_async(False)
     wall = allmax(pg, t1 - t0)
     dev_ms = eng.timer_elapsed_ms(0, 1)
-    n_launch, tot_ms = eng.prof_read(dom)
+    n_launch, tot_ms = eng.prof_read(dom)   # chain events: the per-launch period
 
     units = (NH + CB) * K * world
     value = units / wall
@@ -219,9 +224,15 @@ def main():
     bpu = per_unit_bytes(mean_len_h, mean_len_b, k, size, CB, nr)
     upl = {"pfp_hash": B, "pfp_apply": B, "pfp_reply": B, "pfadd": B, "bloom_contains": CB,
            "bloom_rc_hash": CB, "bloom_rc_probe": CB}
+    # the chain's events span one launch of the chain in the steady state of the timed region (for PFADD: the
+    # previous batch's apply end to this batch's apply end, i.e. the per-batch period; its hash overlaps the
+    # previous apply on the other stream)
     avg_ms = tot_ms / max(n_launch, 1)
-    achieved = bpu[dom] * upl.get(dom, B) / (avg_ms * 1e-3) / 1e9
-    traffic = pmc_traffic(dom)
+    # SURVEY 8(d) per-unit bytes of each chain (53 B per PFADD element at C2; len + 9 + 64(k-1) per contains)
+    s8 = {"pfadd": mean_len_h + 12 + 2.5, "bloom_contains": mean_len_b + 8 + 1 + 64 * (k - 1)}
+    achieved = s8[dom] * upl[dom] / (avg_ms * 1e-3) / 1e9
+    tr_parts = [pmc_traffic(p_) for p_ in chain_kernels[dom]]
+    traffic = sum(tr_parts) if tr_parts and all(t is not None for t in tr_parts) else None
 
     kernels = {}
     for p_, (lps, ms) in iso.items():
@@ -229,13 +240,12 @@ def main():
             continue
         u = upl.get(p_, B)
         tr = pmc_traffic(p_)
-        kernels[p_] = {"bytes_per_unit": bpu.get(p_), "units_per_launch": u, "launches_per_step": lps,
+        kernels[p_] = {"line_bytes_per_unit": bpu.get(p_), "units_per_launch": u, "launches_per_step": lps,
                        "ms_isolated": ms, "GBps_isolated": bpu[p_] * u / (ms * 1e-3) / 1e9 if p_ in bpu else None,
                        "ms_overlapped": over.get(p_, (0, None))[1],
                        "pmc_traffic_bytes": tr,
                        "pmc_GBps_isolated": tr / (ms * 1e-3) / 1e9 if tr else None}
-    # chains against SURVEY 8(d)'s per-unit figures (53 B per PFADD element; len + 9 + 64(k-1) per contains)
-    s8 = {"pfadd": mean_len_h + 12 + 2.5, "bloom_contains": mean_len_b + 8 + 1 + 64 * (k - 1)}
+    # chains against SURVEY 8(d)'s per-unit figures
     chains = {}
     for ch in CHAINS:
         if ch not in iso:
@@ -282,14 +292,24 @@ def main():
         "bloom_contains_per_s": CB * world / (bl_ms * 1e-3) if bl_ms else None,
         "bloom_add_per_s": fill / add_s if add_s else None,
         "device_ms_timed_region": dev_ms,
-        "roofline": {"kernel": dom, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "roofline": {"kernel": "%s chain (%s)" % (dom, " + ".join("k_" + p_ for p_ in chain_kernels[dom])),
+                     "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "traffic_GBps": traffic / (avg_ms * 1e-3) / 1e9 if traffic else None,
-                     "traffic_source": "profiles/*_pmc_summary.json: 2 x FETCH_SIZE (gfx950) + WRITE_SIZE per launch",
-                     "bytes_per_unit": bpu[dom], "units_per_launch": upl.get(dom, B), "avg_launch_ms": avg_ms,
-                     "launches_timed": n_launch,
-                     "note": "dominant kernel = most device time per step, run alone; avg launch from HIP events "
-                             "on its stream inside the timed region; bytes per unit: DESIGN.md kernel table"},
+                     "traffic_source": "profiles/*_pmc_summary.json: 2 x FETCH_SIZE (gfx950) + WRITE_SIZE per launch, "
+                                       "summed over the chain's kernels",
+                     "bytes_per_unit": s8[dom], "bytes_per_unit_source": "SURVEY 8(d)",
+                     "units_per_launch": upl[dom], "avg_launch_ms": avg_ms, "launches_timed": n_launch,
+                     "kernel_ms_isolated": {p_: iso[p_][1] for p_ in chain_kernels[dom] if p_ in iso},
+                     "kernel_ms_overlapped": {p_: over[p_][1] for p_ in chain_kernels[dom] if p_ in over},
+                     "dominant_kernel": {"kernel": dom_kernel, "line_bytes_per_unit": bpu.get(dom_kernel),
+                                         "ms_isolated": iso[dom_kernel][1],
+                                         "launches_per_step": iso[dom_kernel][0]},
+                     "note": "unit = the chain with the most device time per step, run alone; avg_launch_ms = "
+                             "HIP events around each launch of the chain on its stream inside the timed region "
+                             "(PFADD: the per-batch period, hash of batch i+1 overlapping apply of batch i); "
+                             "kernel times alone and overlapped from the breakdown passes; line-level bytes per "
+                             "kernel: DESIGN.md kernel table"},
         "kernels": kernels,
         "chains": chains,
         "cpu_baseline": cpu,

@@ -245,7 +245,7 @@ int sk_timer_elapsed(sk_ctx *ctx, int slot_a, int slot_b, float *ms);
  * chains: "bloom_contains" (every kernel of one contains call), "pfadd" (every
  * kernel of one sk_pfadd_dev batch) */
 int sk_prof_enable(sk_ctx *ctx, int on);
-/* time only the named phase while profiling is on (NULL: every phase) */
+/* time only the named phases while profiling is on ("a,b,c"; NULL: every phase) */
 int sk_prof_only(sk_ctx *ctx, const char *phase);
 int sk_prof_reset(sk_ctx *ctx);
 int sk_prof_read(sk_ctx *ctx, const char *phase, uint64_t *launches, double *total_ms);

@@ -1917,11 +1917,8 @@ hipError_t launch_pfp_hash(hipStream_t st, uint64_t n, const uint32_t *key_ids, 
 hipError_t launch_pfp_apply(hipStream_t st, uint64_t n, const uint64_t *chunks, const uint32_t *S, uint8_t *arena,
                             uint8_t *rep, uint32_t *big_alloc, uint64_t *big_keys, uint32_t *big_vals,
                             uint8_t *changed) {
-    static const unsigned dlds = [] { // experiment knob: extra dynamic LDS lowers apply occupancy (0 = off)
-        const char *e = getenv("SK_PFA_DLDS");
-        return e ? unsigned(atoi(e)) : 0u;
-    }();
-    hipLaunchKernelGGL(k_pfp_apply, dim3(SK_PFP_NB), dim3(SK_PFP_ATPB), dlds, st, chunks, S, pfp_blocks(n), arena, rep,
+
+    hipLaunchKernelGGL(k_pfp_apply, dim3(SK_PFP_NB), dim3(SK_PFP_ATPB), 0, st, chunks, S, pfp_blocks(n), arena, rep,
                        big_alloc, big_keys, big_vals, changed);
     SK_LAUNCH_CHECK();
     return hipSuccess;

@@ -2422,12 +2422,20 @@ int sk_prof_only(sk_ctx *c, const char *phase) {
         c->prof_mask = 0xffffffffu;
         return SK_OK;
     }
-    for (int i = 0; i < kNumPhases; i++)
-        if (strcmp(phase, kPhaseNames[i]) == 0) {
-            c->prof_mask = 1u << i;
-            return SK_OK;
-        }
-    return fail(c, SK_EINVAL, "unknown phase");
+    uint32_t mask = 0; // a comma-separated list of phases
+    for (const char *p = phase; *p;) {
+        const char *e = strchr(p, ',');
+        size_t len = e ? size_t(e - p) : strlen(p);
+        int hit = -1;
+        for (int i = 0; i < kNumPhases; i++)
+            if (strlen(kPhaseNames[i]) == len && strncmp(p, kPhaseNames[i], len) == 0) hit = i;
+        if (hit < 0) return fail(c, SK_EINVAL, "unknown phase");
+        mask |= 1u << hit;
+        p += len + (e ? 1 : 0);
+    }
+    if (!mask) return fail(c, SK_EINVAL, "unknown phase");
+    c->prof_mask = mask;
+    return SK_OK;
 }
 int sk_prof_reset(sk_ctx *c) {
     std::lock_guard<std::mutex> g(c->mu);

@@ -157,6 +157,11 @@ int sk_pfmerge(sk_ctx *ctx, const uint8_t *dest, uint64_t dest_len, uint32_t n_s
 /* union of n slab ids into a 16384-byte register array on device (d_out);
  * building block of the cross-GPU merge (then RCCL uint8 max all-reduce). */
 int sk_hll_union_dev(sk_ctx *ctx, uint64_t n, const uint32_t *d_key_ids, uint8_t *d_out);
+/* the local step of countWith / PFMERGE over keys sharded by calcSlot % n_gpus: register max of the existing
+ * HLLs among keys[0..n) owned by `rank` into d_out (16384 B device); *n_used = HLLs merged
+ * (replaces, per shard, the name resolution of M:RedissonHyperLogLog.java:86-97) */
+int sk_hll_union_keys(sk_ctx *ctx, uint32_t n, const uint64_t *key_off, const uint8_t *key_bytes, int32_t n_gpus,
+                      int32_t rank, uint8_t *d_out, uint32_t *n_used);
 /* write 16384 unpacked registers (device pointer) into a key as max (PFMERGE of a raw array) */
 int sk_hll_merge_registers_dev(sk_ctx *ctx, const uint8_t *key, uint64_t len, const uint8_t *d_regs);
 /* parity readback: 16384 unpacked registers of an HLL key (zeros if missing) */

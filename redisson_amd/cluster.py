@@ -142,19 +142,12 @@ class RcclCollective:
         return [flat[r * P:r * P + sizes[r]].tobytes() for r in range(self.world)]
 
 
-def global_union_registers(engine, keys: Sequence, rank: int, world: int, coll: RcclCollective):
-    """Union (register max) of every key in `keys`, wherever it lives; result
-    left in coll.buf on every rank.  Missing keys count as empty (PFCOUNT rule)."""
-    own = owners(keys, world) == rank
-    mine = [k for k, o in zip(keys, own) if o]
-    ids = engine.hll_lookup(mine) if mine else np.zeros(0, dtype=np.uint32)   # existing keys only, nothing created
-    ids = ids[ids != 0xFFFFFFFF]
-    if len(ids):
-        d_ids = engine.to_device(ids)
-        engine.hll_union_dev(len(ids), d_ids, coll.buf)
-        d_ids.free()
-    else:
-        coll.buf.zero()
+def global_union_registers(engine, keys, rank: int, world: int, coll: RcclCollective):
+    """Union (register max) of every key in `keys` (a sequence, or an engine.pack() result), wherever it lives;
+    result left in coll.buf on every rank.  Missing keys count as empty (PFCOUNT rule).  Local step: one
+    sk_hll_union_keys (owner filter + directory lookup on host threads, k_hll_union on the device); exchange:
+    RCCL u8 MAX all-reduce."""
+    engine.hll_union_keys(keys, world, rank, coll.buf)
     coll.max_u8_dev(coll.buf)
     return coll.buf
 
@@ -172,7 +165,15 @@ def global_count_with(engine, keys: Sequence, rank: int, world: int, coll: RcclC
 
 def global_merge(engine, dest, keys: Sequence, rank: int, world: int, coll: RcclCollective) -> None:
     """PFMERGE dest keys... across GPUs: dest (on its owner) = max(dest, union)."""
-    d = global_union_registers(engine, list(keys) + [dest], rank, world, coll)
+    if isinstance(keys, tuple):   # packed: append dest
+        off, buf = keys
+        n_, tot = len(off) - 1, int(off[-1])
+        off = np.concatenate([off, [tot + len(dest)]]).astype(np.uint64)
+        buf = np.concatenate([buf[:tot], np.frombuffer(bytes(dest), np.uint8), np.zeros(16, np.uint8)])
+        keys = (off, buf)
+    else:
+        keys = list(keys) + [dest]
+    d = global_union_registers(engine, keys, rank, world, coll)
     if owner(dest, world) == rank:
         engine.hll_merge_registers_dev(dest, d)
 

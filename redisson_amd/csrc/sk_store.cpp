@@ -1519,6 +1519,60 @@ int sk_hll_union_dev(sk_ctx *c, uint64_t n, const uint32_t *d_ids, uint8_t *d_ou
     return sync(c);
 }
 
+// The local step of a countWith / PFMERGE over keys sharded by calcSlot % n_gpus (redisson_amd/cluster.py):
+// register max of the existing HLLs among `keys` that this rank owns, into d_out (16384 B on the device).
+// Owner filtering and the directory lookup run on host threads; *n_used = HLLs merged.
+int sk_hll_union_keys(sk_ctx *c, uint32_t n, const uint64_t *off, const uint8_t *bytes, int32_t n_gpus,
+                      int32_t rank, uint8_t *d_out, uint32_t *n_used) {
+    std::lock_guard<std::mutex> g(c->mu);
+    ENTER(c);
+    std::vector<int32_t> own(n);
+    {
+        unsigned T = n >= 65536 ? std::max(1u, std::min(16u, std::thread::hardware_concurrency())) : 1u;
+        std::vector<std::thread> th;
+        for (unsigned t = 0; t < T; t++)
+            th.emplace_back([&, t] {
+                for (uint64_t i = uint64_t(n) * t / T; i < uint64_t(n) * (t + 1) / T; i++)
+                    own[i] = sk_owner(bytes + off[i], off[i + 1] - off[i], n_gpus);
+            });
+        for (auto &x : th) x.join();
+    }
+    std::vector<uint64_t> so(1, 0); // the owned keys, packed
+    std::vector<uint8_t> sb;
+    for (uint32_t i = 0; i < n; i++)
+        if (own[i] == rank) {
+            sb.insert(sb.end(), bytes + off[i], bytes + off[i + 1]);
+            so.push_back(sb.size());
+        }
+    const uint32_t m = uint32_t(so.size() - 1);
+    sb.resize(sb.size() + 16, 0);
+    std::vector<uint32_t> ids(m);
+    std::vector<uint8_t> found(m, 0);
+    find_hlls_parallel(c, m, so.data(), sb.data(), ids.data(), found.data());
+    uint32_t k = 0;
+    for (uint32_t i = 0; i < m; i++) {
+        uint32_t id = ids[i];
+        if (!found[i]) {
+            int r = hll_get(c, key_at(so.data(), sb.data(), i), false, &id, nullptr);
+            if (r) return r;
+        }
+        if (id != kNoId) ids[k++] = id;
+    }
+    if (n_used) *n_used = k;
+    if (!k) {
+        HIPCHK(c, hipMemsetAsync(d_out, 0, kHllBytes, c->st));
+        return sync(c);
+    }
+    HIPCHK(c, c->in_ids.ensure(uint64_t(k) * 4));
+    HIPCHK(c, hipMemcpyAsync(c->in_ids.p, ids.data(), uint64_t(k) * 4, hipMemcpyHostToDevice, c->st));
+    const uint64_t max_groups = 4096;
+    HIPCHK(c, c->partial.ensure((max_groups + max_groups / 64 + 2) * kHllBytes));
+    { Prof p_(c, 4);
+    HIPCHK(c, sk::launch_hll_union(c->st, k, c->in_ids.as<uint32_t>(), c->arena, c->partial.as<uint8_t>(), max_groups,
+                                   d_out, 0)); }
+    return sync(c); // ids is a host vector
+}
+
 int sk_pfmerge(sk_ctx *c, const uint8_t *dest, uint64_t dest_len, uint32_t n_src, const uint64_t *src_off,
                const uint8_t *src_bytes) {
     std::lock_guard<std::mutex> g(c->mu);

@@ -304,6 +304,16 @@ class SketchEngine:
     def hll_histogram_dev(self, n: int, d_ids, d_hist):
         self._check(self.lib.sk_hll_histogram_dev(self.ctx, n, _addr(d_ids), _addr(d_hist)))
 
+    def hll_union_keys(self, keys, n_gpus: int, rank: int, d_out) -> int:
+        """Register max of the existing HLLs among `keys` (a sequence, or a pack() result) owned by `rank` under
+        calcSlot % n_gpus, into d_out (16384 B device); returns how many were merged."""
+        off, buf = keys if isinstance(keys, tuple) else pack([_b(k) for k in keys])
+        used = ctypes.c_uint32()
+        n = len(off) - 1
+        self._check(self.lib.sk_hll_union_keys(self.ctx, n, _addr(off), _addr(buf), n_gpus, rank, _addr(d_out),
+                                               ctypes.addressof(used)))
+        return int(used.value)
+
     def hll_union_dev(self, n: int, d_ids, d_out):
         self._check(self.lib.sk_hll_union_dev(self.ctx, n, _addr(d_ids), _addr(d_out)))
 

@@ -184,3 +184,22 @@ def test_rccl_single_rank_exchange(engine, O):
     ref.merge(b"g4:dest", keys)
     np.testing.assert_array_equal(engine.hll_registers(b"g4:dest"), ref.regs[b"g4:dest"])
     assert coll.sum_u64(12345) == 12345
+    # the local step at world 4: each rank's union covers exactly its calcSlot % 4 share (packed key names)
+    from redisson_amd import owner
+    from redisson_amd.engine import pack
+
+    packed = pack(keys + [b"g4:absent"])
+    parts = []
+    for r in range(4):
+        d = engine.alloc(16384)
+        used = engine.hll_union_keys(packed, 4, r, d)
+        mine = [k for k in keys if owner(k, 4) == r]
+        assert used == len(mine)
+        want = np.zeros(16384, np.uint8)
+        for k in mine:
+            np.maximum(want, ref.regs[k], out=want)
+        got = d.download(np.uint8, 16384)
+        np.testing.assert_array_equal(got, want)
+        parts.append(got)
+        d.free()
+    np.testing.assert_array_equal(np.maximum.reduce(parts), ref.regs[b"g4:dest"])

@@ -231,6 +231,12 @@ int sk_d2h(sk_ctx *ctx, void *dst, const void *d_src, uint64_t n);
 int sk_dev_memset(sk_ctx *ctx, void *d_p, int value, uint64_t n);
 /* async mode: sk_pfadd_dev / sk_bloom_contains_dev / sk_bloom_add_dev return
  * once enqueued (inputs must stay valid until sk_sync); default off */
+/* Redis HLL strings byte for byte (off by default; set while no HLL key exists, or SK_HLL_EXACT_STRINGS=1):
+ * keys keep redis-server 3.2's sparse encoding until hllSparseSet would promote them (3000 bytes or a register
+ * past 32), and the 8 cached-cardinality bytes follow PFADD / single-key PFCOUNT / PFMERGE, so sk_get returns
+ * what GET on redis-server returns (M:RedissonBitSet.java:88-91).  Costs one logged record per register rise
+ * and a host replay per PFADD batch; the partition path is used for every batch. */
+int sk_hll_exact_strings(sk_ctx *ctx, int on);
 int sk_set_async(sk_ctx *ctx, int on);
 /* completion tickets (with sk_set_async): a ticket covers everything enqueued on
  * the context so far.  sk_poll never blocks and releases a finished ticket;

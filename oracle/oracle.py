@@ -64,6 +64,11 @@ def lib():
             "or_hll_union_gen_mt": (None, [c_void_p, c_uint64, c_uint64, c_uint64, c_int, c_int]),
             "or_bloom_add_gen_mt": (c_uint64, [c_void_p, c_int64, c_int32, c_uint64, c_uint64, c_uint64, c_int]),
             "or_bloom_add_gen_seq": (c_uint64, [c_void_p, c_int64, c_int32, c_uint64, c_uint64, c_uint64, c_void_p]),
+            "or_hllstr_new": (c_uint64, [c_void_p]),
+            "or_hllstr_to_dense": (c_int, [c_void_p, c_void_p]),
+            "or_hllstr_set": (c_int, [c_void_p, c_void_p, ctypes.c_long, ctypes.c_uint8]),
+            "or_hllstr_pfadd": (c_int, [c_void_p, c_void_p, c_int, c_uint32, c_void_p, c_void_p, c_int]),
+            "or_hllstr_registers": (c_int, [c_void_p, c_uint64, c_void_p]),
             "or_bloom_add_idx_seq": (c_uint64, [c_void_p, c_uint64, c_int64, c_int32, c_uint64, c_void_p, c_uint64,
                                                 c_void_p]),
             "or_bloom_contains_gen_mt": (None, [c_void_p, c_uint64, c_int64, c_int32, c_uint64, c_void_p, c_uint64,
@@ -181,6 +186,77 @@ class HLLStore:
         d = self.regs.setdefault(dest, np.zeros(16384, dtype=np.uint8))
         for a in arrs:
             np.maximum(d, a, out=d)
+
+
+class HLLStrStore:
+    """Reference keyspace of HLL strings byte for byte as redis-server 3.2 keeps them (hyperloglog.c): keys start
+    sparse (createHLLObject), PFADD runs hllSparseSet per element (promotion past 3000 bytes or a value > 32),
+    the 8 cached-cardinality bytes follow PFADD (invalidate), single-key PFCOUNT (store) and PFMERGE
+    (dest made dense, invalidated)."""
+
+    CAP = 16 + 12288 + 64
+
+    def __init__(self, redis_major: int = 3):
+        self.m = redis_major
+        self.s = {}
+
+    def _new(self):
+        b = np.zeros(self.CAP, dtype=np.uint8)
+        n = c_uint64(lib().or_hllstr_new(b.ctypes.data))
+        return [b, n]
+
+    def pfadd(self, key, elems) -> int:
+        created = key not in self.s
+        if created:
+            self.s[key] = self._new()
+        b, n = self.s[key]
+        off, buf = pack(list(elems))
+        r = lib().or_hllstr_pfadd(b.ctypes.data, ctypes.addressof(n), int(created), len(elems), off.ctypes.data,
+                                  buf.ctypes.data, self.m)
+        assert r >= 0, "corrupted HLL"
+        return r
+
+    def registers(self, key) -> np.ndarray:
+        regs = np.zeros(16384, dtype=np.uint8)
+        if key in self.s:
+            b, n = self.s[key]
+            assert lib().or_hllstr_registers(b.ctypes.data, n.value, regs.ctypes.data) == 0
+        return regs
+
+    def pfcount(self, keys) -> int:
+        if len(keys) == 1:
+            k = keys[0]
+            if k not in self.s:
+                return 0
+            b, n = self.s[k]
+            if not (b[15] & 0x80):                      # valid cache
+                return int.from_bytes(bytes(b[8:16]), "little")
+            enc = 0 if b[4] == 1 else 1                  # sparse sum (exact) / dense sum order
+            c = count_regs(self.registers(k), enc, self.m)
+            b[8:16] = np.frombuffer(int(c).to_bytes(8, "little"), np.uint8)
+            return c
+        u = np.maximum.reduce([self.registers(k) for k in keys])
+        return count_regs(u, 2, self.m)
+
+    def pfmerge(self, dest, srcs):
+        u = np.maximum.reduce([self.registers(k) for k in [dest] + list(srcs)])
+        if dest not in self.s:
+            self.s[dest] = self._new()
+        b, n = self.s[dest]
+        assert lib().or_hllstr_to_dense(b.ctypes.data, ctypes.addressof(n)) == 0
+        b[16:16 + 12288] = np.frombuffer(dense_pack(u), np.uint8)
+        b[15] |= 0x80
+
+    def get(self, key):
+        if key not in self.s:
+            return None
+        b, n = self.s[key]
+        return b[:n.value].tobytes()
+
+    def set(self, key, value: bytes):
+        b = np.zeros(self.CAP, dtype=np.uint8)
+        b[:len(value)] = np.frombuffer(value, np.uint8)
+        self.s[key] = [b, c_uint64(len(value))]
 
 
 def count_regs(regs: np.ndarray, encoding: int = 1, redis_major: int = 3) -> int:

@@ -572,6 +572,230 @@ void or_hll_dense_unpack(const uint8_t *in, uint8_t *regs) {
 }
 
 /* ------------------------------------------------------------------ */
+/* Redis HLL strings as redis-server 3.2 writes them (hyperloglog.c):     */
+/* createHLLObject (sparse XZERO runs, cached card 0), hllSparseSet        */
+/* (split the opcode covering the register, promote to dense past          */
+/* hll_sparse_max_bytes = 3000 or a value > 32, merge adjacent VAL          */
+/* opcodes over <= 5 opcodes from the previous one), hllSparseToDense,     */
+/* and the cached-cardinality bytes of PFADD / PFCOUNT / PFMERGE.          */
+/* s: a buffer of >= 16 + 12288 + 8 bytes; *len: the string's length.      */
+#define OR_HDR 16
+#define OR_SPARSE_MAX_BYTES 3000
+#define OR_IS_ZERO(p) (((*(p)) & 0xc0) == 0)
+#define OR_IS_XZERO(p) (((*(p)) & 0xc0) == 0x40)
+#define OR_IS_VAL(p) ((*(p)) & 0x80)
+#define OR_ZERO_LEN(p) (((*(p)) & 0x3f) + 1)
+#define OR_XZERO_LEN(p) (((((*(p)) & 0x3f) << 8) | (*((p) + 1))) + 1)
+#define OR_VAL_VALUE(p) ((((*(p)) >> 2) & 0x1f) + 1)
+#define OR_VAL_LEN(p) (((*(p)) & 0x3) + 1)
+static void or_val_set(uint8_t *p, int val, int len) { *p = (uint8_t)((((val) - 1) << 2 | ((len) - 1)) | 0x80); }
+static void or_zero_set(uint8_t *p, int len) { *p = (uint8_t)((len) - 1); }
+static void or_xzero_set(uint8_t *p, int len) {
+    int l = len - 1;
+    p[0] = (uint8_t)((l >> 8) | 0x40);
+    p[1] = (uint8_t)(l & 0xff);
+}
+static unsigned or_dense_get(const uint8_t *regs, long i) {
+    unsigned byte = (unsigned)(i * 6) / 8, fb = (unsigned)(i * 6) & 7;
+    unsigned b0 = regs[byte], b1 = byte + 1 < OR_HLL_DENSE_BYTES ? regs[byte + 1] : 0;
+    return ((b0 >> fb) | (b1 << (8 - fb))) & 63;
+}
+static void or_dense_set(uint8_t *regs, long i, unsigned v) {
+    unsigned byte = (unsigned)(i * 6) / 8, fb = (unsigned)(i * 6) & 7;
+    regs[byte] &= (uint8_t)~(63u << fb);
+    regs[byte] |= (uint8_t)(v << fb);
+    if (fb > 2) {
+        regs[byte + 1] &= (uint8_t)~(63u >> (8 - fb));
+        regs[byte + 1] |= (uint8_t)(v >> (8 - fb));
+    }
+}
+
+uint64_t or_hllstr_new(uint8_t *s) {
+    memset(s, 0, OR_HDR);
+    memcpy(s, "HYLL", 4);
+    s[4] = 1; /* HLL_SPARSE; card bytes 0 */
+    or_xzero_set(s + OR_HDR, 16384);
+    return OR_HDR + 2;
+}
+
+int or_hllstr_to_dense(uint8_t *s, uint64_t *len) {
+    if (s[4] == 0) return 0;
+    uint8_t dense[OR_HLL_DENSE_BYTES];
+    memset(dense, 0, sizeof dense);
+    long idx = 0;
+    const uint8_t *p = s + OR_HDR, *end = s + *len;
+    while (p < end) {
+        if (OR_IS_ZERO(p)) {
+            idx += OR_ZERO_LEN(p);
+            p++;
+        } else if (OR_IS_XZERO(p)) {
+            idx += OR_XZERO_LEN(p);
+            p += 2;
+        } else {
+            int run = OR_VAL_LEN(p), v = OR_VAL_VALUE(p);
+            while (run--) {
+                if (idx < OR_HLL_REGISTERS) or_dense_set(dense, idx, (unsigned)v);
+                idx++;
+            }
+            p++;
+        }
+    }
+    if (idx != OR_HLL_REGISTERS) return -1;
+    s[4] = 0; /* header (magic, unused bytes, cached card) kept */
+    memcpy(s + OR_HDR, dense, sizeof dense);
+    *len = OR_HDR + OR_HLL_DENSE_BYTES;
+    return 0;
+}
+
+/* hllSparseSet / hllDenseSet: 1 if the register rose, 0 if not, -1 corrupted */
+int or_hllstr_set(uint8_t *s, uint64_t *len, long index, uint8_t count) {
+    if (s[4] == 0) {
+        uint8_t *regs = s + OR_HDR;
+        if (or_dense_get(regs, index) >= count) return 0;
+        or_dense_set(regs, index, count);
+        return 1;
+    }
+    if (count > 32) goto promote;
+    {
+        uint8_t *sparse = s + OR_HDR, *p = sparse, *end = s + *len, *prev = NULL, *next;
+        long first = 0, span = 0, runlen;
+        int is_zero = 0, is_xzero = 0, is_val = 0;
+        while (p < end) {
+            long oplen = 1;
+            if (OR_IS_ZERO(p)) span = OR_ZERO_LEN(p);
+            else if (OR_IS_VAL(p)) span = OR_VAL_LEN(p);
+            else span = OR_XZERO_LEN(p), oplen = 2;
+            if (index <= first + span - 1) break;
+            prev = p;
+            p += oplen;
+            first += span;
+        }
+        if (span == 0 || p >= end) return -1;
+        next = OR_IS_XZERO(p) ? p + 2 : p + 1;
+        if (next >= end) next = NULL;
+        if (OR_IS_ZERO(p)) is_zero = 1, runlen = OR_ZERO_LEN(p);
+        else if (OR_IS_XZERO(p)) is_xzero = 1, runlen = OR_XZERO_LEN(p);
+        else is_val = 1, runlen = OR_VAL_LEN(p);
+        if (is_val) {
+            int oldcount = OR_VAL_VALUE(p);
+            if (oldcount >= count) return 0;
+            if (runlen == 1) {
+                or_val_set(p, count, 1);
+                goto updated;
+            }
+        }
+        if (is_zero && runlen == 1) {
+            or_val_set(p, count, 1);
+            goto updated;
+        }
+        {
+            uint8_t seq[5], *n = seq;
+            long last = first + span - 1, l;
+            if (is_zero || is_xzero) {
+                if (index != first) {
+                    l = index - first;
+                    if (l > 64) or_xzero_set(n, (int)l), n += 2;
+                    else or_zero_set(n, (int)l), n++;
+                }
+                or_val_set(n, count, 1), n++;
+                if (index != last) {
+                    l = last - index;
+                    if (l > 64) or_xzero_set(n, (int)l), n += 2;
+                    else or_zero_set(n, (int)l), n++;
+                }
+            } else {
+                int curval = OR_VAL_VALUE(p);
+                if (index != first) or_val_set(n, curval, (int)(index - first)), n++;
+                or_val_set(n, count, 1), n++;
+                if (index != last) or_val_set(n, curval, (int)(last - index)), n++;
+            }
+            long seqlen = n - seq, oldlen = is_xzero ? 2 : 1, deltalen = seqlen - oldlen;
+            if (deltalen > 0 && (long)*len + deltalen > OR_SPARSE_MAX_BYTES) goto promote;
+            if (deltalen && next) memmove(next + deltalen, next, (size_t)(end - next));
+            *len = (uint64_t)((long)*len + deltalen);
+            memcpy(p, seq, (size_t)seqlen);
+            end += deltalen;
+        }
+    updated:
+        p = prev ? prev : sparse;
+        {
+            int scanlen = 5;
+            while (p < end && scanlen--) {
+                if (OR_IS_XZERO(p)) {
+                    p += 2;
+                    continue;
+                } else if (OR_IS_ZERO(p)) {
+                    p++;
+                    continue;
+                }
+                if (p + 1 < end && OR_IS_VAL(p + 1)) {
+                    int v1 = OR_VAL_VALUE(p), v2 = OR_VAL_VALUE(p + 1);
+                    if (v1 == v2) {
+                        int l2 = OR_VAL_LEN(p) + OR_VAL_LEN(p + 1);
+                        if (l2 <= 4) {
+                            or_val_set(p + 1, v1, l2);
+                            memmove(p, p + 1, (size_t)(end - p));
+                            *len -= 1;
+                            end--;
+                            continue;
+                        }
+                    }
+                }
+                p++;
+            }
+        }
+        s[15] |= 0x80; /* HLL_INVALIDATE_CACHE */
+        return 1;
+    }
+promote:
+    if (or_hllstr_to_dense(s, len) != 0) return -1;
+    or_dense_set(s + OR_HDR, index, count);
+    return 1;
+}
+
+/* pfaddCommand on one key: created -> updated; each element hllAdd; updated -> cache invalidated.  Returns
+ * the reply (1/0), -1 on a corrupted string. */
+int or_hllstr_pfadd(uint8_t *s, uint64_t *len, int created, uint32_t n, const uint64_t *off, const uint8_t *bytes,
+                    int redis_major) {
+    int updated = created;
+    for (uint32_t j = 0; j < n; j++) {
+        int64_t idx;
+        int cnt = or_hll_patlen(bytes + off[j], off[j + 1] - off[j], redis_major, &idx);
+        int r = or_hllstr_set(s, len, (long)idx, (uint8_t)cnt);
+        if (r < 0) return -1;
+        updated |= r;
+    }
+    if (updated) s[15] |= 0x80;
+    return updated;
+}
+
+/* registers of an HLL string (dense or sparse); -1 corrupted */
+int or_hllstr_registers(const uint8_t *s, uint64_t len, uint8_t *regs) {
+    if (s[4] == 0) {
+        or_hll_dense_unpack(s + OR_HDR, regs);
+        return 0;
+    }
+    long idx = 0;
+    const uint8_t *p = s + OR_HDR, *end = s + len;
+    while (p < end) {
+        if (OR_IS_ZERO(p)) {
+            int r = OR_ZERO_LEN(p);
+            if (idx + r > OR_HLL_REGISTERS) return -1;
+            memset(regs + idx, 0, (size_t)r), idx += r, p++;
+        } else if (OR_IS_XZERO(p)) {
+            int r = OR_XZERO_LEN(p);
+            if (idx + r > OR_HLL_REGISTERS) return -1;
+            memset(regs + idx, 0, (size_t)r), idx += r, p += 2;
+        } else {
+            int r = OR_VAL_LEN(p);
+            if (idx + r > OR_HLL_REGISTERS) return -1;
+            memset(regs + idx, OR_VAL_VALUE(p), (size_t)r), idx += r, p++;
+        }
+    }
+    return idx == OR_HLL_REGISTERS ? 0 : -1;
+}
+
+/* ------------------------------------------------------------------ */
 /* RedissonBloomFilter (M:RedissonBloomFilter.java)                      */
 
 /* optimalNumOfBits :74-78 ; (long) truncation of a double */

@@ -76,6 +76,13 @@ void or_hll_histogram(const uint8_t *regs, uint32_t *hist64);
 void or_hll_union(const uint8_t *const *regs, uint32_t n, uint8_t *out);
 void or_hll_dense_pack(const uint8_t *regs, uint8_t *out12288);
 void or_hll_dense_unpack(const uint8_t *in12288, uint8_t *regs);
+/* Redis HLL strings as redis-server 3.2 writes them (sparse writer) */
+uint64_t or_hllstr_new(uint8_t *s);
+int or_hllstr_to_dense(uint8_t *s, uint64_t *len);
+int or_hllstr_set(uint8_t *s, uint64_t *len, long index, uint8_t count);
+int or_hllstr_pfadd(uint8_t *s, uint64_t *len, int created, uint32_t n, const uint64_t *off, const uint8_t *bytes,
+                    int redis_major);
+int or_hllstr_registers(const uint8_t *s, uint64_t len, uint8_t *regs);
 
 /* ---- Bloom filter (RedissonBloomFilter) ---- */
 int64_t or_bloom_optimal_bits(int64_t n, double p);

@@ -102,6 +102,7 @@ SIGNATURES = {
     "sk_timer_record": (c_int, [P, c_int]),
     "sk_timer_elapsed": (c_int, [P, c_int, c_int, P]),
     "sk_set_async": (c_int, [P, c_int]),
+    "sk_hll_exact_strings": (c_int, [P, c_int]),
     "sk_prof_enable": (c_int, [P, c_int]),
     "sk_prof_only": (c_int, [P, c_char_p]),
     "sk_set_bit_range": (c_int, [P, _u8p, c_uint64, c_int64, c_int64, c_int]),

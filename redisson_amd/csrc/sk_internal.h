@@ -35,7 +35,8 @@ hipError_t launch_murmur_long(hipStream_t st, uint32_t n_long, const uint8_t *by
                               const uint32_t *which, uint64_t *out_h);
 hipError_t launch_pfp_apply(hipStream_t st, uint64_t n, const uint64_t *chunks, const uint32_t *S, uint8_t *arena,
                             uint8_t *rep, uint32_t *big_alloc, uint64_t *big_keys, uint32_t *big_vals,
-                            uint8_t *changed); // changed != null: replies straight to batch order (no k_pfp_reply)
+                            uint8_t *changed, uint64_t *ev = nullptr,
+                            uint32_t *ev_n = nullptr); // changed != null: replies straight to batch order (no k_pfp_reply)
 hipError_t launch_pfp_reply(hipStream_t st, uint64_t n, const uint8_t *rep, const uint16_t *pos,
                             const uint32_t *cmd_of, uint8_t *changed);
 hipError_t sort_keys_size(uint64_t n, unsigned begin_bit, unsigned end_bit, size_t *bytes);

@@ -586,9 +586,16 @@ struct BigTable {
 };
 
 // this thread's records: seg[t0], seg[t0 + 4], ... below seg_cnt; cnt = the bucket's total
+// register rises for the HLL string writer (sk_hll_exact_strings): the record of every element that raised its
+// register, in no particular order (the host sorts by seq)
+__device__ __forceinline__ void pfp_event(uint64_t *ev, uint32_t *ev_n, uint64_t rec) {
+    if (ev) ev[atomicAdd(ev_n, 1u)] = rec;
+}
+
 __device__ void pfp_big_resolve(const uint64_t *seg, uint32_t t0, uint32_t seg_cnt, uint32_t cnt, void *smem,
                                 uint32_t *big_alloc, uint64_t *big_keys, uint32_t *big_vals, uint8_t *arena,
-                                uint8_t *__restrict__ rep_seg, uint8_t *__restrict__ changed) {
+                                uint8_t *__restrict__ rep_seg, uint8_t *__restrict__ changed, uint64_t *ev,
+                                uint32_t *ev_n) {
     __shared__ uint32_t gbase;
     unsigned long long *lk = reinterpret_cast<unsigned long long *>(smem);
     uint32_t *lv = reinterpret_cast<uint32_t *>(lk + SK_BIG_LDS);
@@ -611,6 +618,7 @@ __device__ void pfp_big_resolve(const uint64_t *seg, uint32_t t0, uint32_t seg_c
         bool first = rho > (uint32_t(arena[slot]) & 63u);
         // v = rho: no earlier equal rho; v > rho: no earlier larger one
         for (uint32_t v = rho; v < 52 && first; v++) first = T.find((slot << 6) | v) >= seq;
+        if (first) pfp_event(ev, ev_n, r);
         if (changed) changed[seq] = first ? 1 : 0;
         else rep_seg[t] = first ? 1 : 0;
     }
@@ -636,7 +644,8 @@ __global__ void __launch_bounds__(SK_PFP_ATPB) k_pfp_apply(const uint64_t *__res
                                                            const uint32_t *__restrict__ S, uint32_t nblocks,
                                                            uint8_t *arena, uint8_t *__restrict__ rep,
                                                            uint32_t *big_alloc, uint64_t *big_keys,
-                                                           uint32_t *big_vals, uint8_t *__restrict__ changed) {
+                                                           uint32_t *big_vals, uint8_t *__restrict__ changed,
+                                                           uint64_t *ev, uint32_t *ev_n) {
     constexpr uint32_t kSmem = SK_PFP_CAP * 8 + SK_PFP_CAP * 2 + SK_PFP_HT * 4 + SK_PFP_CAP;
     static_assert(kSmem >= SK_BIG_LDS * 12, "big-bucket table shares the LDS");
     __shared__ uint64_t smem[(kSmem + 7) / 8];
@@ -658,7 +667,7 @@ __global__ void __launch_bounds__(SK_PFP_ATPB) k_pfp_apply(const uint64_t *__res
     const uint64_t *seg = chunks + uint64_t(j) * SK_PFP_EPB + lo;
     if (cnt > SK_PFP_CAP) {
         pfp_big_resolve(seg, sub, c, cnt, smem, big_alloc, big_keys, big_vals, arena,
-                        rep + uint64_t(j) * SK_PFP_EPB + lo, changed);
+                        rep + uint64_t(j) * SK_PFP_EPB + lo, changed, ev, ev_n);
         return;
     }
     for (uint32_t t = threadIdx.x; t < SK_PFP_HT; t += SK_PFP_ATPB) head[t] = 0xffffu;
@@ -702,6 +711,7 @@ __global__ void __launch_bounds__(SK_PFP_ATPB) k_pfp_apply(const uint64_t *__res
         }
         uint32_t R0 = r0[tq];
         uint8_t reply = rho > (R0 > p ? R0 : p);
+        if (reply) pfp_event(ev, ev_n, rt);
         if (changed) changed[seq] = reply; // one element per command: straight to batch order
         else r0[tq] = reply;               // the reply replaces R0 (read by this thread only)
         if (earliest && m > R0) arena[slot] = uint8_t(m);
@@ -1916,10 +1926,10 @@ hipError_t launch_pfp_hash(hipStream_t st, uint64_t n, const uint32_t *key_ids, 
 
 hipError_t launch_pfp_apply(hipStream_t st, uint64_t n, const uint64_t *chunks, const uint32_t *S, uint8_t *arena,
                             uint8_t *rep, uint32_t *big_alloc, uint64_t *big_keys, uint32_t *big_vals,
-                            uint8_t *changed) {
+                            uint8_t *changed, uint64_t *ev, uint32_t *ev_n) {
 
     hipLaunchKernelGGL(k_pfp_apply, dim3(SK_PFP_NB), dim3(SK_PFP_ATPB), 0, st, chunks, S, pfp_blocks(n), arena, rep,
-                       big_alloc, big_keys, big_vals, changed);
+                       big_alloc, big_keys, big_vals, changed, ev, ev_n);
     SK_LAUNCH_CHECK();
     return hipSuccess;
 }

@@ -574,7 +574,8 @@ int selftest() {
 void usage() {
     fprintf(stderr,
             "usage: sk-resp-server [--bind ADDR] [--port P (0 = any)] [--device D] [--redis-major 3|5]\n"
-            "                      [--max-bit-offset N] [--hll-capacity N] [--max-batch N] | --selftest\n");
+            "                      [--max-bit-offset N] [--hll-capacity N] [--max-batch N] [--hll-exact-strings]\n"
+            "                      | --selftest\n");
 }
 
 } // namespace
@@ -583,6 +584,7 @@ int main(int argc, char **argv) {
     std::string bind_addr = "127.0.0.1";
     int port = 6379;
     sk_config cfg = {0, 3, 0, 0, 0};
+    bool exact = false;
     for (int i = 1; i < argc; i++) {
         std::string a = argv[i];
         auto next = [&]() -> const char * {
@@ -597,6 +599,7 @@ int main(int argc, char **argv) {
         else if (a == "--max-bit-offset") cfg.max_bit_offset = strtoull(next(), nullptr, 10);
         else if (a == "--hll-capacity") cfg.hll_capacity = strtoull(next(), nullptr, 10);
         else if (a == "--max-batch") cfg.max_batch = strtoull(next(), nullptr, 10);
+        else if (a == "--hll-exact-strings") exact = true; // GET of an HLL: redis-server's sparse / dense bytes
         else return usage(), 2;
     }
     Server srv;
@@ -604,6 +607,10 @@ int main(int argc, char **argv) {
     int st = sk_open(&cfg, &srv.ctx);
     if (st != SK_OK) {
         fprintf(stderr, "sk-resp-server: sk_open failed: %s\n", sk_strerror(st));
+        return 1;
+    }
+    if (exact && (st = sk_hll_exact_strings(srv.ctx, 1)) != SK_OK) {
+        fprintf(stderr, "sk-resp-server: %s\n", sk_strerror(st));
         return 1;
     }
     int lfd = socket(AF_INET, SOCK_STREAM, 0);

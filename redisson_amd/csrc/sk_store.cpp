@@ -185,6 +185,13 @@ double raw_sum(const uint8_t *r, int *ez) {
 
 } // namespace
 
+// one HLL key as a Redis string in exact mode (see "Redis HLL strings, exact")
+struct HllStr {
+    uint8_t hdr[16];
+    std::vector<uint8_t> ops; // sparse opcodes; empty when dense (the registers are the arena slab)
+    bool sparse = false;
+};
+
 struct sk_ctx {
     std::mutex mu;
     int device = 0;
@@ -268,6 +275,11 @@ struct sk_ctx {
     bool pfp_pipe = true;
     bool pf_dev_call = false;   // inside sk_pfadd_dev: inputs are caller-owned device memory, no host staging
     hipStream_t st3 = nullptr;
+    // Redis HLL strings byte for byte (sk_hll_exact_strings; off by default): per slab header + sparse opcodes,
+    // the apply kernel's log of register rises (records) replayed in batch order
+    bool hll_exact = false;
+    std::vector<HllStr> hstr;
+    DBuf ev, ev_n;
     uint64_t bloom_ra_min = 1;  // add batches >= this use the region schedule (SK_BLOOM_RA_MIN, 0 = never: sort path)
     DBuf ra_S, ra_rec, ra_flag;
     uint64_t bloom_rc_min = 2u << 20; // contains batches >= this use the region schedule (SK_BLOOM_RC_MIN, 0 = never)
@@ -399,6 +411,159 @@ int hll_grow(sk_ctx *c, uint64_t need) {
     return SK_OK;
 }
 
+// ------------------------------------------------ Redis HLL strings, exact (sk_hll_exact_strings)
+// redis-server 3.2 keeps an HLL as a string (hyperloglog.c): a 16-B header ("HYLL", encoding, 3 unused bytes, an
+// 8-B cached cardinality whose top bit marks it stale) and sparse opcodes -- ZERO 00xxxxxx, XZERO 01xxxxxx
+// yyyyyyyy, VAL 1vvvvvxx -- until an update would take the string past hll_sparse_max_bytes (3000) or a register
+// past 32, dense after.  Sparse bytes depend on the order registers rose (hllSparseSet splits the opcode that
+// covers a register and merges neighbouring VAL opcodes within 5 opcodes of the previous one), so in exact mode
+// the apply kernel logs the record of every register rise, and the host replays them in batch order into each
+// sparse key's opcodes: the GPU decides every rise, the host keeps the string format (as it keeps the PFCOUNT
+// estimator's scalar tail).  The cached-cardinality bytes follow PFADD (stale), single-key PFCOUNT (stored) and
+// PFMERGE (dest made dense, stale).
+namespace hs {
+constexpr size_t kSparseMax = 3000; // server.hll_sparse_max_bytes default
+inline bool zero(uint8_t b) { return (b & 0xc0) == 0; }
+inline bool xzero(uint8_t b) { return (b & 0xc0) == 0x40; }
+inline uint32_t zero_len(uint8_t b) { return (b & 0x3fu) + 1; }
+inline uint32_t xzero_len(uint8_t b0, uint8_t b1) { return ((uint32_t(b0 & 0x3f) << 8) | b1) + 1; }
+inline int val_value(uint8_t b) { return ((b >> 2) & 0x1f) + 1; }
+inline int val_len(uint8_t b) { return (b & 3) + 1; }
+inline uint8_t val(int v, int len) { return uint8_t(0x80 | ((v - 1) << 2) | (len - 1)); }
+inline int put_zeros(uint8_t *q, uint32_t len) { // ZERO up to 64, XZERO beyond (HLL_SPARSE_ZERO_MAX_LEN)
+    if (len > 64) {
+        q[0] = uint8_t(0x40 | ((len - 1) >> 8));
+        q[1] = uint8_t((len - 1) & 0xff);
+        return 2;
+    }
+    q[0] = uint8_t(len - 1);
+    return 1;
+}
+} // namespace hs
+
+void hll_str_init(HllStr &h) { // createHLLObject: sparse XZERO(16384); PFADD / PFMERGE creating it mark the card stale
+    std::memset(h.hdr, 0, 16);
+    std::memcpy(h.hdr, "HYLL", 4);
+    h.hdr[4] = 1;
+    h.hdr[15] = 0x80;
+    h.ops.assign({0x7f, 0xff});
+    h.sparse = true;
+}
+
+void hll_str_densify(HllStr &h) { // hllSparseToDense: header kept, encoding dense
+    h.sparse = false;
+    h.hdr[4] = 0;
+    std::vector<uint8_t>().swap(h.ops);
+}
+
+// hllSparseSet on a sparse string: 0 register not raised, 1 raised, 2 promote (the caller densifies; the arena
+// already holds the raised register), -1 the opcodes do not cover the register
+int hll_sparse_set(HllStr &h, uint32_t index, uint8_t count) {
+    if (count > 32) return 2; // HLL_SPARSE_VAL_MAX_VALUE
+    std::vector<uint8_t> &o = h.ops;
+    size_t p = 0, prev = SIZE_MAX, oplen = 1;
+    uint32_t first = 0, span = 0;
+    while (p < o.size()) { // the opcode covering `index`
+        oplen = 1;
+        if (hs::zero(o[p])) span = hs::zero_len(o[p]);
+        else if (o[p] & 0x80) span = uint32_t(hs::val_len(o[p]));
+        else {
+            if (p + 1 >= o.size()) return -1;
+            span = hs::xzero_len(o[p], o[p + 1]), oplen = 2;
+        }
+        if (index <= first + span - 1) break;
+        prev = p;
+        p += oplen;
+        first += span;
+    }
+    if (p >= o.size() || span == 0) return -1;
+    const bool is_zero = hs::zero(o[p]), is_xzero = hs::xzero(o[p]), is_val = !is_zero && !is_xzero;
+    bool done = false;
+    if (is_val) {
+        if (hs::val_value(o[p]) >= count) return 0;
+        if (span == 1) o[p] = hs::val(count, 1), done = true;
+    }
+    if (!done && is_zero && span == 1) o[p] = hs::val(count, 1), done = true;
+    if (!done) { // split the opcode: [run before] VAL(count, 1) [run after]
+        uint8_t seq[5];
+        int n = 0;
+        const uint32_t last = first + span - 1;
+        if (is_val) {
+            const int cur = hs::val_value(o[p]);
+            if (index != first) seq[n++] = hs::val(cur, int(index - first));
+            seq[n++] = hs::val(count, 1);
+            if (index != last) seq[n++] = hs::val(cur, int(last - index));
+        } else {
+            if (index != first) n += hs::put_zeros(seq + n, index - first);
+            seq[n++] = hs::val(count, 1);
+            if (index != last) n += hs::put_zeros(seq + n, last - index);
+        }
+        const long delta = long(n) - long(oplen);
+        if (delta > 0 && 16 + o.size() + size_t(delta) > hs::kSparseMax) return 2;
+        o.erase(o.begin() + long(p), o.begin() + long(p + oplen));
+        o.insert(o.begin() + long(p), seq, seq + n);
+    }
+    // merge neighbouring VAL opcodes of one value (runs <= 4), scanning <= 5 opcodes from the previous one
+    size_t q = prev == SIZE_MAX ? 0 : prev;
+    int scan = 5;
+    while (q < o.size() && scan--) {
+        if (hs::xzero(o[q])) {
+            q += 2;
+            continue;
+        }
+        if (hs::zero(o[q])) {
+            q++;
+            continue;
+        }
+        if (q + 1 < o.size() && (o[q + 1] & 0x80) && hs::val_value(o[q]) == hs::val_value(o[q + 1])) {
+            const int l = hs::val_len(o[q]) + hs::val_len(o[q + 1]);
+            if (l <= 4) {
+                o[q + 1] = hs::val(hs::val_value(o[q]), l);
+                o.erase(o.begin() + long(q));
+                continue;
+            }
+        }
+        q++;
+    }
+    return 1;
+}
+
+// the register rises of one PFADD launch (apply-kernel records, any order) in batch order
+void hll_replay_rises(sk_ctx *c, std::vector<uint64_t> &ev) {
+    std::sort(ev.begin(), ev.end(), [](uint64_t a, uint64_t b) { return ((a >> 6) & 0xfffffu) < ((b >> 6) & 0xfffffu); });
+    for (uint64_t rec : ev) {
+        const uint64_t slot = rec >> 26;
+        const uint32_t slab = uint32_t(slot >> 14) & 0xffffffu, reg = uint32_t(slot & 16383u);
+        if (slab >= c->hstr.size()) continue;
+        HllStr &h = c->hstr[slab];
+        h.hdr[15] |= 0x80; // PFADD updated: HLL_INVALIDATE_CACHE
+        if (!h.sparse) continue;
+        int r = hll_sparse_set(h, reg, uint8_t(rec & 63u));
+        if (r == 2 || r < 0) hll_str_densify(h);
+    }
+}
+
+// single-key PFCOUNT (pfcountCommand): a valid cached cardinality answers; a stale one is replaced by the count
+void hll_card_cache(sk_ctx *c, uint32_t slab, int64_t *count) {
+    if (!c->hll_exact || slab >= c->hstr.size()) return;
+    HllStr &h = c->hstr[slab];
+    if (!(h.hdr[15] & 0x80)) {
+        uint64_t v = 0;
+        for (int i = 7; i >= 0; i--) v = (v << 8) | h.hdr[8 + i];
+        *count = int64_t(v);
+        return;
+    }
+    const uint64_t v = uint64_t(*count);
+    for (int i = 0; i < 8; i++) h.hdr[8 + i] = uint8_t(v >> (8 * i));
+}
+
+// PFMERGE destination (pfmergeCommand): made dense, cached cardinality stale
+void hll_str_merged(sk_ctx *c, uint32_t slab) {
+    if (!c->hll_exact || slab >= c->hstr.size()) return;
+    hll_str_densify(c->hstr[slab]);
+    c->hstr[slab].hdr[15] |= 0x80;
+}
+
 int hll_alloc(sk_ctx *c, uint32_t *id) {
     if (!c->hll_free.empty()) {
         *id = c->hll_free.back();
@@ -416,6 +581,10 @@ int hll_alloc(sk_ctx *c, uint32_t *id) {
         c->hll_gen.resize(n, 0);
     }
     c->hll_live[*id] = 1;
+    if (c->hll_exact) {
+        if (c->hstr.size() <= *id) c->hstr.resize(std::max<size_t>(*id + 1, c->hstr.size() * 2));
+        hll_str_init(c->hstr[*id]);
+    }
     return SK_OK;
 }
 // Caller-cached handles (sk_hll_resolve -> sk_pfadd_ids / sk_pfcount_ids) = slab | generation << 24: usable only
@@ -484,6 +653,13 @@ int hll_adopt_string(sk_ctx *c, const std::string &k, KeyEnt &e, uint32_t *id) {
     if (r == SK_ECORRUPT) return fail(c, r, "INVALIDOBJ Corrupted HLL object detected");
     uint32_t hid;
     if ((r = hll_alloc(c, &hid))) return r;
+    if (c->hll_exact) { // the string as redis-server would keep using it: its header, its sparse opcodes
+        HllStr &h = c->hstr[hid];
+        std::memcpy(h.hdr, s.data(), 16);
+        h.sparse = s[4] == 1;
+        if (h.sparse) h.ops.assign(s.begin() + 16, s.end());
+        else std::vector<uint8_t>().swap(h.ops);
+    }
     HIPCHK(c, hipMemcpyAsync(c->arena + uint64_t(hid) * kHllBytes, regs.data(), kHllBytes, hipMemcpyHostToDevice,
                              c->st));
     if ((r = sync(c))) return r;
@@ -753,8 +929,18 @@ int pfadd_partition_pipe(sk_ctx *c, uint64_t n, const uint32_t *d_ids, const uin
 int pfadd_partition(sk_ctx *c, uint64_t n, const uint32_t *d_ids, const uint64_t *d_off, const uint8_t *d_bytes,
                     const uint32_t *d_cmd, uint8_t *d_changed, const uint64_t *d_pre = nullptr) {
     if (n > (1ull << 20) || c->hll_next >= (1ull << 24)) return fail(c, SK_EINVAL, "PFADD partition batch too large");
-    if (c->pf_dev_call && c->pfp_pipe && c->pfp_direct && d_cmd == nullptr && d_pre == nullptr && c->st3)
+    if (c->pf_dev_call && c->pfp_pipe && c->pfp_direct && d_cmd == nullptr && d_pre == nullptr && c->st3 &&
+        !c->hll_exact)
         return pfadd_partition_pipe(c, n, d_ids, d_off, d_bytes, d_changed);
+    uint64_t *ev = nullptr; // exact HLL strings: the apply kernel logs every register rise
+    uint32_t *ev_n = nullptr;
+    if (c->hll_exact) {
+        HIPCHK(c, c->ev.ensure(n * 8));
+        HIPCHK(c, c->ev_n.ensure(16));
+        HIPCHK(c, hipMemsetAsync(c->ev_n.p, 0, 4, c->st));
+        ev = c->ev.as<uint64_t>();
+        ev_n = c->ev_n.as<uint32_t>();
+    }
     uint64_t nb = sk::pfp_blocks(n), cap = nb * sk::pfp_epb();
     HIPCHK(c, c->keys_a.ensure(cap * 8));                                // block chunks of records
     HIPCHK(c, c->keys_b.ensure(cap + 2 * n + 32));                       // replies in chunk order + element slots
@@ -774,10 +960,20 @@ int pfadd_partition(sk_ctx *c, uint64_t n, const uint32_t *d_ids, const uint64_t
                                   direct ? nullptr : pos, big_alloc, d_pre)); }
     { Prof p_(c, 16);
     HIPCHK(c, sk::launch_pfp_apply(c->st, n, chunks, S, c->arena, rep, big_alloc, c->vals_a.as<uint64_t>(),
-                                   c->vals_b.as<uint32_t>(), direct ? d_changed : nullptr)); }
+                                   c->vals_b.as<uint32_t>(), direct ? d_changed : nullptr, ev, ev_n)); }
     if (!direct) {
         Prof p_(c, 17);
         HIPCHK(c, sk::launch_pfp_reply(c->st, n, rep, pos, d_cmd, d_changed));
+    }
+    if (ev) {
+        uint32_t ne = 0;
+        HIPCHK(c, hipMemcpyAsync(&ne, ev_n, 4, hipMemcpyDeviceToHost, c->st));
+        int r = sync(c);
+        if (r) return r;
+        std::vector<uint64_t> h(ne);
+        if (ne) HIPCHK(c, hipMemcpyAsync(h.data(), ev, uint64_t(ne) * 8, hipMemcpyDeviceToHost, c->st));
+        if ((r = sync(c))) return r;
+        hll_replay_rises(c, h);
     }
     return SK_OK;
 }
@@ -927,6 +1123,8 @@ int sk_open(const sk_config *cfg, sk_ctx **out) {
     if (const char *e = getenv("SK_PFP_DIRECT")) c->pfp_direct = atoi(e) != 0;
     if (const char *e = getenv("SK_BLOOM_RC_MIN")) c->bloom_rc_min = strtoull(e, nullptr, 10);
     if (const char *e = getenv("SK_BLOOM_RA_MIN")) c->bloom_ra_min = strtoull(e, nullptr, 10);
+    if (const char *e = getenv("SK_HLL_EXACT_STRINGS")) c->hll_exact = atoi(e) != 0;
+    if (c->hll_exact) c->pfadd_path = 1;
     if (const char *e = getenv("SK_PFP_PIPE")) c->pfp_pipe = atoi(e) != 0;
     uint64_t cap = (cfg && cfg->hll_capacity) ? cfg->hll_capacity : 1024;
     if (hll_grow(c, cap) != SK_OK || c->misc.ensure(4096) != hipSuccess ||
@@ -1427,7 +1625,10 @@ int sk_pfcount_ids(sk_ctx *c, uint64_t n, const uint32_t *key_ids, int64_t *out)
     std::vector<uint32_t> h;
     int r = hll_histograms(c, n, c->in_ids.as<uint32_t>(), c->arena, h);
     if (r) return r;
-    return estimate_many(c, n, h.data(), key_ids, out);
+    int r2 = estimate_many(c, n, h.data(), key_ids, out);
+    if (r2 || !c->hll_exact) return r2;
+    for (uint64_t i = 0; i < n; i++) hll_card_cache(c, key_ids[i] & kSlabMask, &out[i]);
+    return SK_OK;
 }
 
 int sk_pfcount(sk_ctx *c, uint32_t n_cmds, const uint32_t *nkeys, const uint64_t *key_off, const uint8_t *key_bytes,
@@ -1491,7 +1692,10 @@ int sk_pfcount(sk_ctx *c, uint32_t n_cmds, const uint32_t *nkeys, const uint64_t
         if (r) return r;
         std::vector<int64_t> est(single_ids.size());
         if ((r = estimate_many(c, single_ids.size(), h.data(), single_ids.data(), est.data()))) return r;
-        for (size_t i = 0; i < single_ids.size(); i++) out[single_cmd[i]] = est[i];
+        for (size_t i = 0; i < single_ids.size(); i++) {
+            out[single_cmd[i]] = est[i];
+            hll_card_cache(c, single_ids[i], &out[single_cmd[i]]);
+        }
     }
     // multi-key commands: union into a temporary raw register array (nothing modified)
     HIPCHK(c, c->uni.ensure(kHllBytes));
@@ -1588,6 +1792,7 @@ int sk_pfmerge(sk_ctx *c, const uint8_t *dest, uint64_t dest_len, uint32_t n_src
     uint32_t did;
     int r = hll_get(c, key_of(dest, dest_len), true, &did, nullptr);
     if (r) return r;
+    hll_str_merged(c, did);
     return union_into(c, ids, c->arena + uint64_t(did) * kHllBytes, 1);
 }
 
@@ -1597,6 +1802,7 @@ int sk_hll_merge_registers_dev(sk_ctx *c, const uint8_t *key, uint64_t len, cons
     uint32_t did;
     int r = hll_get(c, key_of(key, len), true, &did, nullptr);
     if (r) return r;
+    hll_str_merged(c, did);
     // out = max(out, d_regs): a one-key union whose "arena" is d_regs
     const uint64_t max_groups = 4096;
     HIPCHK(c, c->partial.ensure((max_groups + max_groups / 64 + 2) * kHllBytes));
@@ -1960,9 +2166,17 @@ int sk_get(sk_ctx *c, const uint8_t *key, uint64_t len, uint8_t *buf, uint64_t c
                                  hipMemcpyDeviceToHost, c->st));
         int r = sync(c);
         if (r) return r;
+        const HllStr *hx = c->hll_exact && it->second.id < c->hstr.size() ? &c->hstr[it->second.id] : nullptr;
+        if (hx && hx->sparse) { // the sparse string as redis-server keeps it
+            *out_len = int64_t(16 + hx->ops.size());
+            if (cap) std::memcpy(buf, hx->hdr, std::min<uint64_t>(cap, 16));
+            if (cap > 16) std::memcpy(buf + 16, hx->ops.data(), std::min<uint64_t>(cap - 16, hx->ops.size()));
+            return SK_OK;
+        }
         std::vector<uint8_t> s(SK_HLL_DENSE_SIZE, 0);
-        std::memcpy(s.data(), "HYLL", 4); // encoding 0 = dense; card cache marked invalid
+        std::memcpy(s.data(), "HYLL", 4); // encoding 0 = dense; card cache marked invalid (exact mode: the key's)
         s[15] = 0x80;
+        if (hx) std::memcpy(s.data(), hx->hdr, 16);
         for (int i = 0; i < 16384; i++) { // HLL_DENSE_SET_REGISTER: 6 bits at bit 6*i, LSB first
             unsigned byte = unsigned(i * 6) / 8, fb = unsigned(i * 6) & 7, v = regs[i] & 63;
             s[16 + byte] |= uint8_t(v << fb);
@@ -2404,6 +2618,16 @@ int sk_timer_elapsed(sk_ctx *c, int a, int b, float *ms) {
         return fail(c, SK_EINVAL, "timer slot");
     HIPCHK(c, hipEventSynchronize(c->timers[b]));
     HIPCHK(c, hipEventElapsedTime(ms, c->timers[a], c->timers[b]));
+    return SK_OK;
+}
+
+int sk_hll_exact_strings(sk_ctx *c, int on) {
+    std::lock_guard<std::mutex> g(c->mu);
+    const bool want = on != 0;
+    if (want != c->hll_exact && c->hll_next - c->hll_free.size() != 0)
+        return fail(c, SK_EINVAL, "HLL string mode can change only while no HLL key exists");
+    c->hll_exact = want;
+    if (want) c->pfadd_path = 1; // the partition path logs the register rises
     return SK_OK;
 }
 

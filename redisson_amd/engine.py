@@ -168,6 +168,10 @@ class SketchEngine:
         self._check(self.lib.sk_timer_elapsed(self.ctx, a, b, ctypes.addressof(ms)))
         return ms.value
 
+    def hll_exact_strings(self, on: bool = True):
+        """GET of an HLL returns redis-server's bytes (sparse writer + cached cardinality); set before any HLL key."""
+        self._check(self.lib.sk_hll_exact_strings(self.ctx, int(on)))
+
     def set_async(self, on: bool = True):
         self._check(self.lib.sk_set_async(self.ctx, int(on)))
 

@@ -364,10 +364,13 @@ __global__ void __launch_bounds__(SK_PFP_TPB) k_pfp_hash(uint64_t n, const uint3
                                                          uint32_t nblocks, uint16_t *__restrict__ pos,
                                                          uint32_t *__restrict__ big_alloc,
                                                          const uint64_t *__restrict__ pre_h) {
+    // the block's records reuse the key windows' LDS once the last round is hashed: 98 KiB in all, so a hash
+    // workgroup (the next batch, on the third stream) fits on a CU beside an apply workgroup (61.5 KiB)
     __shared__ uint32_t h[SK_PFP_NB];
     __shared__ uint32_t wsum[SK_PFP_TPB / 64];
-    __shared__ uint64_t lrec[SK_PFP_EPB];
     __shared__ uint64_t win[2][SK_PFP_WIN];
+    static_assert(SK_PFP_EPB <= 2 * SK_PFP_WIN, "records fit the windows");
+    uint64_t *lrec = &win[0][0];
     for (uint32_t b = threadIdx.x; b < SK_PFP_NB; b += SK_PFP_TPB) h[b] = 0;
     if (blockIdx.x == 0 && threadIdx.x == 0) *big_alloc = 0;
     constexpr int PER = SK_PFP_EPB / SK_PFP_TPB;
@@ -696,7 +699,7 @@ __device__ void pfp_big_resolve(const uint64_t *seg, uint32_t t0, uint32_t seg_c
 // value, and the R0 latency overlaps the chain building.  Then the chain walk
 // gives each record the max rho of its slot's earlier records and of the
 // whole slot; replies and the slot's one register store follow.
-__global__ void __launch_bounds__(SK_PFP_ATPB) k_pfp_apply(const uint64_t *__restrict__ chunks,
+__global__ void __launch_bounds__(SK_PFP_ATPB) __attribute__((amdgpu_waves_per_eu(8))) k_pfp_apply(const uint64_t *__restrict__ chunks,
                                                            const uint32_t *__restrict__ S, uint32_t nblocks,
                                                            uint8_t *arena, uint8_t *__restrict__ rep,
                                                            uint32_t *big_alloc, uint64_t *big_keys,

@@ -1161,7 +1161,7 @@ int sk_close(sk_ctx *c) {
     for (DBuf *b : {&c->keys_a, &c->keys_b, &c->vals_a, &c->vals_b, &c->sort_tmp, &c->in_off, &c->in_bytes,
                     &c->in_ids, &c->in_cmd, &c->out_u8, &c->misc, &c->partial, &c->hist, &c->uni, &c->ptrs,
                     &c->hist_a, &c->hist_b, &c->ovf, &c->bloom_h, &c->rc_S, &c->rc_rec, &c->long_h,
-                    &c->long_which})
+                    &c->long_which, &c->ra_S, &c->ra_rec, &c->ra_flag, &c->ev, &c->ev_n})
         b->release();
     for (auto &ps : c->pfs) {
         for (DBuf *b : {&ps.chunks, &ps.rep, &ps.S, &ps.big_k, &ps.big_v, &ps.ovf}) b->release();

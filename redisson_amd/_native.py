@@ -10,7 +10,8 @@ import ctypes
 import os
 from ctypes import POINTER, c_char_p, c_double, c_int, c_int32, c_int64, c_uint8, c_uint32, c_uint64, c_void_p
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libredisson_sketch.so")
+LIB_PATH = os.environ.get("SK_LIB_PATH") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                                       "libredisson_sketch.so")   # override: A/B builds
 
 SK_OK = 0
 SK_EWRONGTYPE = -1

@@ -30,9 +30,14 @@ hipError_t launch_pfp_hash(hipStream_t st, uint64_t n, const uint32_t *key_ids, 
                            const uint8_t *bytes, int v5, uint64_t *chunks, uint32_t *S, uint16_t *pos,
                            uint32_t *big_alloc, const uint64_t *pre = nullptr);
 uint64_t long_elem_bytes();
-// MurmurHash64A (seed 0xadc83b19) of elements which[0..n_long) into out_h[which[i]], one workgroup each
-hipError_t launch_murmur_long(hipStream_t st, uint32_t n_long, const uint8_t *bytes, const uint64_t *off,
-                              const uint32_t *which, uint64_t *out_h);
+// MurmurHash64A (seed 0xadc83b19) of long elements into out_h[which[i]] by 64 bit rounds of an XOR scan.
+// meta = which[n_long] then first_wg[n_long + 1] (murmur_long_wgs(len) workgroups per element, n_wg in all);
+// plane: n_wg * 1024 * 64 words; flags: n_wg * 64 + 2 words, flags[n_wg * 64 + 1] != 0 after the run = a look-back
+// wait ran out (the hashes are then invalid)
+uint32_t murmur_long_wgs(uint64_t len);
+hipError_t launch_murmur_long(hipStream_t st, uint32_t n_long, uint32_t n_wg, const uint8_t *bytes,
+                              const uint64_t *off, const uint32_t *meta, uint32_t *plane, uint32_t *flags,
+                              uint64_t *out_h);
 hipError_t launch_pfp_apply(hipStream_t st, uint64_t n, const uint64_t *chunks, const uint32_t *S, uint8_t *arena,
                             uint8_t *rep, uint32_t *big_alloc, uint64_t *big_keys, uint32_t *big_vals,
                             uint8_t *changed, uint64_t *ev = nullptr,

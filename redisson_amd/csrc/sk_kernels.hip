@@ -468,117 +468,175 @@ __global__ void __launch_bounds__(SK_PFP_TPB) k_pfp_reply(uint64_t n, const uint
     }
 }
 
-// ---- one long element (RHyperLogLog.addAll, quirk Q1: ONE element = the Jackson array of every value, ~38 MB at
-// C1, M:RedissonHyperLogLog.java:70-76).  MurmurHash64A's state chain h_{b+1} = (h_b ^ k_b) * m is sequential;
-// the per-block transform k_b = mix(block b) is not.  The chain is split by halves, since the low 32 bits of a
-// product depend only on the low 32 bits of its factors:
-//   pass A (wave 0, one lane):  xl_b = L_b ^ klo_b;  L_{b+1} = xl_b * mlo            (mod 2^32)
-//   terms  (producer waves):    A_b = mulhi(xl_b, mlo) + xl_b * mhi                (parallel over b)
-//   pass B (wave 1, one lane):  H_{b+1} = A_b + (H_b ^ khi_b) * mlo                 (mod 2^32)
-// so each sequential lane pays one xor and one 32-bit multiply per 8 bytes instead of a 64-bit multiply chain,
-// and the two passes run side by side, pass B two tiles behind pass A.  Waves 2.. compute k for the next tile
-// and the A terms of the previous one.  (Four 16-bit chains on four waves measured slower: 169 ms vs 74 ms for
-// the 41 MB C1 element.)
-#define SK_ML_T 2048 // blocks per tile
-__global__ void __launch_bounds__(1024) k_murmur_long(const uint8_t *__restrict__ bytes, const uint64_t *__restrict__ off,
-                                                      const uint32_t *__restrict__ which, uint64_t seed,
-                                                      uint64_t *__restrict__ out_h) {
-    __shared__ uint32_t klo[4][SK_ML_T], khi[4][SK_ML_T], xlo[2][SK_ML_T], aterm[2][SK_ML_T];
-    __shared__ uint32_t fin[2];
+// ---- long elements (RHyperLogLog.addAll, quirk Q1: ONE element = the Jackson array of every value, ~41 MB at
+// C1, M:RedissonHyperLogLog.java:70-76).  MurmurHash64A's state chain h_{i+1} = x_i * m, x_i = h_i ^ k_i, with the
+// per-block transform k_i = mix(block i), is sequential in i -- but not bit by bit.  m is odd, so bit j of x * m is
+// x_j ^ bit_j((x mod 2^j) * m): with p_i = (x_i mod 2^j) * m,
+//     h_{i+1,j} = h_{i,j} ^ d_i,   d_i = k_{i,j} ^ p_{i,j},
+// i.e. once bits < j of every x_i are known, bit j of every state h_i is a prefix XOR over i of d.  The chain
+// becomes 64 rounds (one per bit) of a device-wide XOR scan over the blocks; each round then sets bit j of every
+// x_i (p_i += m << j where x_{i,j} = 1).  A thread owns SK_MS_S consecutive blocks (their p_i in registers, their
+// k bits as one word per round from bit planes written by k_ms_planes), a workgroup SK_MS_BPW blocks; across
+// workgroups each round is a decoupled look-back over per-(workgroup, round) flags.  Workgroups take ordered ids
+// from a counter, so one only waits on workgroups already running; every wait is bounded (err flag, never a hang).
+#define SK_MS_S 32
+#define SK_MS_TPB 1024
+#define SK_MS_BPW (SK_MS_S * SK_MS_TPB)
+#define SK_MS_AGG (1u << 30)
+#define SK_MS_INCL (1u << 31)
+#define SK_MS_SPIN (1u << 20)
+
+// meta: which[n_long] (element index in the batch), then first_wg[n_long + 1] (workgroup prefix over the elements)
+__device__ __forceinline__ uint32_t ms_elem_of(const uint32_t *first_wg, uint32_t n_long, uint32_t w) {
+    uint32_t lo = 0, hi = n_long; // first_wg[lo] <= w < first_wg[hi]
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (first_wg[mid] <= w) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+
+__global__ void __launch_bounds__(SK_MS_TPB) k_ms_planes(const uint8_t *__restrict__ bytes, const uint64_t *__restrict__ off,
+                                                         const uint32_t *__restrict__ meta, uint32_t n_long,
+                                                         uint32_t *__restrict__ plane) {
     const uint64_t m = 0xc6a4a7935bd1e995ull;
-    const uint32_t mlo = uint32_t(m), mhi = uint32_t(m >> 32);
-    const uint32_t e = which[blockIdx.x];
-    const uint64_t o = off[e];
-    const uint64_t len = off[e + 1] - o;
-    const uint64_t nb = len >> 3;
-    const uint8_t *p = bytes + o;
-    const uint64_t ntiles = (nb + SK_ML_T - 1) / SK_ML_T;
-    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
-    const uint32_t ptid = threadIdx.x - 128u, pn = blockDim.x - 128u; // producers: waves 2..
-    auto cnt_of = [&](uint64_t t) { return uint32_t(nb - t * SK_ML_T < SK_ML_T ? nb - t * SK_ML_T : SK_ML_T); };
-    auto produce = [&](uint64_t t, uint32_t tid, uint32_t nthreads) {
-        const uint64_t b0 = t * SK_ML_T;
-        const uint32_t cnt = cnt_of(t);
-        for (uint32_t j = tid; j < cnt; j += nthreads) {
-            uint64_t k = ldu64(p + 8 * (b0 + j));
-            k *= m;
-            k ^= k >> 47;
-            k *= m;
-            klo[t & 3][j] = uint32_t(k);
-            khi[t & 3][j] = uint32_t(k >> 32);
-        }
-    };
-    const uint64_t h0 = seed ^ (len * m);
-    uint32_t L = uint32_t(h0), H = uint32_t(h0 >> 32);
-    if (ntiles) produce(0, threadIdx.x, blockDim.x);
+    const uint32_t *which = meta, *first_wg = meta + n_long;
+    const uint32_t w = blockIdx.x, e = ms_elem_of(first_wg, n_long, w);
+    const uint64_t o = off[which[e]], nb = (off[which[e] + 1] - o) >> 3;
+    const uint64_t nw = uint64_t(first_wg[e + 1] - first_wg[e]) * SK_MS_TPB;     // words per plane
+    const uint64_t g = uint64_t(w - first_wg[e]) * SK_MS_TPB + threadIdx.x;
+    uint32_t *pl = plane + uint64_t(first_wg[e]) * SK_MS_TPB * 64;
+    uint32_t word[64];
+#pragma unroll
+    for (int j = 0; j < 64; j++) word[j] = 0;
+#pragma unroll 1
+    for (uint32_t t = 0; t < SK_MS_S; t++) {
+        const uint64_t b = g * SK_MS_S + t;
+        if (b >= nb) break;
+        uint64_t k = ldu64(bytes + o + 8 * b);
+        k *= m;
+        k ^= k >> 47;
+        k *= m;
+#pragma unroll
+        for (int j = 0; j < 64; j++) word[j] |= uint32_t((k >> j) & 1u) << t;
+    }
+#pragma unroll
+    for (int j = 0; j < 64; j++) pl[uint64_t(j) * nw + g] = word[j];
+}
+
+// flags: [n_wg][64] round flags, then the id counter and the err word (zeroed by the launcher)
+__global__ void __launch_bounds__(SK_MS_TPB) k_ms_rounds(const uint8_t *__restrict__ bytes, const uint64_t *__restrict__ off,
+                                                         const uint32_t *__restrict__ meta, uint32_t n_long,
+                                                         uint32_t n_wg, const uint32_t *__restrict__ plane,
+                                                         uint32_t *__restrict__ flags, uint64_t seed,
+                                                         uint64_t *__restrict__ out_h) {
+    const uint64_t m = 0xc6a4a7935bd1e995ull;
+    __shared__ uint32_t s_id, s_wpar[2][SK_MS_TPB / 64], s_ex[2];
+    uint32_t *ctr = flags + uint64_t(n_wg) * 64, *err = ctr + 1;
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    if (threadIdx.x == 0) s_id = atomicAdd(ctr, 1u);
     __syncthreads();
-    // iteration it: pass A on tile it, A terms of tile it-1, pass B on tile it-2, k of tile it+1
-    for (uint64_t it = 0; it < ntiles + 2; it++) {
-        if (wave >= 2) {
-            if (it + 1 < ntiles) produce(it + 1, ptid, pn);
-            if (it >= 1 && it - 1 < ntiles) {
-                const uint64_t t = it - 1;
-                const uint32_t cnt = cnt_of(t);
-                for (uint32_t j = ptid; j < cnt; j += pn) {
-                    const uint32_t x = xlo[t & 1][j];
-                    aterm[t & 1][j] = __umulhi(x, mlo) + x * mhi;
-                }
-            }
-        } else if (wave == 0) {
-            if (lane == 0 && it < ntiles) {
-                const uint32_t cnt = cnt_of(it);
-                const uint32_t *kl = klo[it & 3];
-                uint32_t *xo = xlo[it & 1];
-                uint32_t j = 0;
-                for (; j + 8 <= cnt; j += 8) {
-                    uint32_t kv[8];
+    const uint32_t w = s_id;
+    const uint32_t *which = meta, *first_wg = meta + n_long;
+    const uint32_t e = ms_elem_of(first_wg, n_long, w);
+    const uint32_t w0 = first_wg[e], nwg = first_wg[e + 1] - w0, lw = w - w0;
+    const uint64_t o = off[which[e]], len = off[which[e] + 1] - o, nb = len >> 3;
+    const uint64_t nw = uint64_t(nwg) * SK_MS_TPB;
+    const uint64_t g = uint64_t(lw) * SK_MS_TPB + threadIdx.x;
+    const uint32_t *pl = plane + uint64_t(w0) * SK_MS_TPB * 64 + g;
+    const uint64_t first_b = g * SK_MS_S;
+    const uint32_t valid = first_b >= nb ? 0u : (nb - first_b >= SK_MS_S ? 0xffffffffu
+                                                                          : (1u << uint32_t(nb - first_b)) - 1u);
+    const uint64_t h0 = seed ^ (len * m);
+    uint64_t p[SK_MS_S];
 #pragma unroll
-                    for (int q = 0; q < 8; q++) kv[q] = kl[j + q];
+    for (int t = 0; t < SK_MS_S; t++) p[t] = 0;
+    uint64_t fin = 0;
+    uint32_t kw = pl[0];
+#pragma unroll 1
+    for (uint32_t j = 0; j < 64; j++) {
+        const uint32_t kcur = kw;
+        if (j + 1 < 64) kw = pl[uint64_t(j + 1) * nw]; // next round's plane word, in flight during this round
+        uint32_t pw = 0;
 #pragma unroll
-                    for (int q = 0; q < 8; q++) {
-                        const uint32_t x = L ^ kv[q];
-                        xo[j + q] = x;
-                        L = x * mlo;
+        for (int t = 0; t < SK_MS_S; t++) {
+            const uint32_t half = j < 32 ? uint32_t(p[t]) : uint32_t(p[t] >> 32);
+            pw |= ((half >> (j & 31u)) & 1u) << t;
+        }
+        const uint32_t dm = (kcur ^ pw) & valid;
+        uint32_t inc = dm;
+        inc ^= inc << 1;
+        inc ^= inc << 2;
+        inc ^= inc << 4;
+        inc ^= inc << 8;
+        inc ^= inc << 16;
+        const uint64_t bal = __ballot(inc >> 31);
+        const uint32_t lane_ex = uint32_t(__popcll(bal & ((1ull << lane) - 1ull))) & 1u;
+        if (lane == 0) s_wpar[j & 1][wave] = uint32_t(__popcll(bal)) & 1u;
+        __syncthreads();
+        uint32_t wave_ex = 0, wg_tot = 0;
+#pragma unroll
+        for (uint32_t v = 0; v < SK_MS_TPB / 64; v++) {
+            const uint32_t x = s_wpar[j & 1][v];
+            wave_ex ^= v < wave ? x : 0u;
+            wg_tot ^= x;
+        }
+        if (wave == 0) {
+            uint32_t *fl = flags + uint64_t(w) * 64 + j;
+            uint32_t ex = 0;
+            if (lw == 0) {
+                if (lane == 0) __hip_atomic_store(fl, SK_MS_INCL | wg_tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+                if (lane == 0) __hip_atomic_store(fl, SK_MS_AGG | wg_tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                int64_t pos = int64_t(w) - 1;
+                uint32_t spins = 0;
+                for (;;) { // look back over predecessors of this element, 64 at a time
+                    const int64_t q = pos - int64_t(lane);
+                    const uint32_t f = q >= int64_t(w0)
+                        ? __hip_atomic_load(flags + uint64_t(q) * 64 + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                        : SK_MS_INCL;
+                    const uint64_t inc_b = __ballot((f & SK_MS_INCL) != 0), rdy = __ballot(f != 0);
+                    const uint32_t stop = inc_b ? uint32_t(__ffsll((long long)inc_b)) - 1u : 64u;
+                    const uint64_t need = stop >= 63 ? ~0ull : ((2ull << stop) - 1ull);
+                    if ((rdy & need) != need) {
+                        if (++spins > SK_MS_SPIN) { // a predecessor never published: report, do not hang
+                            if (lane == 0) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            break;
+                        }
+                        __builtin_amdgcn_s_sleep(2);
+                        continue;
                     }
+                    ex ^= uint32_t(__popcll(__ballot(f & 1u) & need)) & 1u;
+                    if (stop < 64) break;
+                    pos -= 64;
                 }
-                for (; j < cnt; j++) {
-                    const uint32_t x = L ^ kl[j];
-                    xo[j] = x;
-                    L = x * mlo;
-                }
+                if (lane == 0)
+                    __hip_atomic_store(fl, SK_MS_INCL | (ex ^ wg_tot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
-        } else {
-            if (lane == 0 && it >= 2) {
-                const uint64_t t = it - 2;
-                const uint32_t cnt = cnt_of(t);
-                const uint32_t *kh = khi[t & 3], *at = aterm[t & 1];
-                uint32_t j = 0;
-                for (; j + 8 <= cnt; j += 8) {
-                    uint32_t kv[8], av[8];
-#pragma unroll
-                    for (int q = 0; q < 8; q++) kv[q] = kh[j + q], av[q] = at[j + q];
-#pragma unroll
-                    for (int q = 0; q < 8; q++) H = av[q] + (H ^ kv[q]) * mlo;
-                }
-                for (; j < cnt; j++) H = at[j] + (H ^ kh[j]) * mlo;
-            }
+            if (lane == 0) s_ex[j & 1] = ex;
         }
         __syncthreads();
+        const uint32_t ex = s_ex[j & 1];
+        if (threadIdx.x == 0 && lw == nwg - 1) fin |= uint64_t(((h0 >> j) & 1u) ^ ex ^ wg_tot) << j;
+        const uint32_t c = uint32_t((h0 >> j) & 1u) ^ ex ^ wave_ex ^ lane_ex;
+        const uint32_t hm = (inc << 1) ^ (c ? 0xffffffffu : 0u); // bit t: bit j of the state before block t
+        const uint32_t xm = (hm ^ kcur) & valid;
+        const uint64_t mj = m << j;
+#pragma unroll
+        for (int t = 0; t < SK_MS_S; t++) p[t] += ((xm >> t) & 1u) ? mj : 0ull;
     }
-    if (threadIdx.x == 0) fin[0] = L;
-    if (threadIdx.x == 64) fin[1] = H;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint64_t h = (uint64_t(fin[1]) << 32) | fin[0];
-        unsigned tail = unsigned(len & 7u);
+    if (threadIdx.x == 0 && lw == nwg - 1) {
+        uint64_t h = fin;
+        const unsigned tail = unsigned(len & 7u);
         if (tail) {
-            h ^= low_bytes(ldu64(p + 8 * nb), tail);
+            h ^= low_bytes(ldu64(bytes + o + 8 * nb), tail);
             h *= m;
         }
         h ^= h >> 47;
         h *= m;
         h ^= h >> 47;
-        out_h[e] = h;
+        out_h[which[e]] = h;
     }
 }
 
@@ -1959,10 +2017,18 @@ uint32_t pfadd_conflict_lds_capacity() { return SK_CONF_MAX; }
 
 uint64_t long_elem_bytes() { return SK_LONG_ELEM; }
 
-hipError_t launch_murmur_long(hipStream_t st, uint32_t n_long, const uint8_t *bytes, const uint64_t *off,
-                              const uint32_t *which, uint64_t *out_h) {
+uint32_t murmur_long_wgs(uint64_t len) { return uint32_t(((len >> 3) + SK_MS_BPW - 1) / SK_MS_BPW); }
+
+hipError_t launch_murmur_long(hipStream_t st, uint32_t n_long, uint32_t n_wg, const uint8_t *bytes,
+                              const uint64_t *off, const uint32_t *meta, uint32_t *plane, uint32_t *flags,
+                              uint64_t *out_h) {
     if (!n_long) return hipSuccess;
-    hipLaunchKernelGGL(k_murmur_long, dim3(n_long), dim3(1024), 0, st, bytes, off, which, 0xadc83b19ull, out_h);
+    hipError_t r = hipMemsetAsync(flags, 0, (uint64_t(n_wg) * 64 + 2) * 4, st);
+    if (r != hipSuccess) return r;
+    hipLaunchKernelGGL(k_ms_planes, dim3(n_wg), dim3(SK_MS_TPB), 0, st, bytes, off, meta, n_long, plane);
+    SK_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_ms_rounds, dim3(n_wg), dim3(SK_MS_TPB), 0, st, bytes, off, meta, n_long, n_wg,
+                       (const uint32_t *)plane, flags, 0xadc83b19ull, out_h);
     SK_LAUNCH_CHECK();
     return hipSuccess;
 }

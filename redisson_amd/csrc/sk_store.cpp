@@ -263,7 +263,8 @@ struct sk_ctx {
     DBuf keys_a, keys_b, vals_a, vals_b, sort_tmp, in_off, in_bytes, in_ids, in_cmd, out_u8, misc, partial, hist,
         uni, ptrs, hist_a, hist_b, ovf, bloom_h;
     DBuf rc_S, rc_rec;          // Bloom contains region schedule: segment table + probe records (contains only)
-    DBuf long_h, long_which;    // PFADD: hashes of long elements (k_murmur_long) and their element indexes
+    DBuf long_h, long_which;    // PFADD: hashes of long elements (k_ms_rounds) and their element indexes + layout
+    DBuf long_plane, long_flags; // their k bit planes and look-back flags
     // device PFADD batches, pipelined (SK_PFP_PIPE, default on): batch i+1's k_pfp_hash runs on st3 while batch i's
     // k_pfp_apply runs on st; two scratch sets alternate, events order hash -> apply and apply -> reuse
     struct PfpSet {
@@ -1161,7 +1162,7 @@ int sk_close(sk_ctx *c) {
     for (DBuf *b : {&c->keys_a, &c->keys_b, &c->vals_a, &c->vals_b, &c->sort_tmp, &c->in_off, &c->in_bytes,
                     &c->in_ids, &c->in_cmd, &c->out_u8, &c->misc, &c->partial, &c->hist, &c->uni, &c->ptrs,
                     &c->hist_a, &c->hist_b, &c->ovf, &c->bloom_h, &c->rc_S, &c->rc_rec, &c->long_h,
-                    &c->long_which, &c->ra_S, &c->ra_rec, &c->ra_flag, &c->ev, &c->ev_n})
+                    &c->long_which, &c->long_plane, &c->long_flags, &c->ra_S, &c->ra_rec, &c->ra_flag, &c->ev, &c->ev_n})
         b->release();
     for (auto &ps : c->pfs) {
         for (DBuf *b : {&ps.chunks, &ps.rep, &ps.S, &ps.big_k, &ps.big_v, &ps.ovf}) b->release();
@@ -1432,19 +1433,31 @@ static int pfadd_host_batch(sk_ctx *c, uint32_t n_cmds, const uint32_t *cmd_key,
             // long elements (addAll's Q1 element: the whole Jackson array) are hashed by one workgroup each
             const uint64_t *d_pre = nullptr;
             if (c->pfadd_path == 1 && nbytes >= sk::long_elem_bytes()) {
-                std::vector<uint32_t> which;
+                std::vector<uint32_t> which, first_wg{0};
                 for (uint64_t j = 0; j < m; j++)
-                    if (off2[j + 1] - off2[j] >= sk::long_elem_bytes()) which.push_back(uint32_t(j));
+                    if (off2[j + 1] - off2[j] >= sk::long_elem_bytes()) {
+                        which.push_back(uint32_t(j));
+                        first_wg.push_back(first_wg.back() + sk::murmur_long_wgs(off2[j + 1] - off2[j]));
+                    }
                 if (!which.empty()) {
+                    const uint32_t nl = uint32_t(which.size()), nwg = first_wg.back();
+                    which.insert(which.end(), first_wg.begin(), first_wg.end());
                     HIPCHK(c, c->long_h.ensure(m * 8));
                     HIPCHK(c, c->long_which.ensure(which.size() * 4));
+                    HIPCHK(c, c->long_plane.ensure(uint64_t(nwg) * 1024 * 64 * 4));
+                    HIPCHK(c, c->long_flags.ensure((uint64_t(nwg) * 64 + 2) * 4));
                     HIPCHK(c, hipMemcpyAsync(c->long_which.p, which.data(), which.size() * 4, hipMemcpyHostToDevice,
                                              c->st));
                     { Prof p_(c, 21);
-                    HIPCHK(c, sk::launch_murmur_long(c->st, uint32_t(which.size()), c->in_bytes.as<uint8_t>(),
+                    HIPCHK(c, sk::launch_murmur_long(c->st, nl, nwg, c->in_bytes.as<uint8_t>(),
                                                      c->in_off.as<uint64_t>(), c->long_which.as<uint32_t>(),
+                                                     c->long_plane.as<uint32_t>(), c->long_flags.as<uint32_t>(),
                                                      c->long_h.as<uint64_t>())); }
+                    uint32_t lerr = 0;
+                    HIPCHK(c, hipMemcpyAsync(&lerr, c->long_flags.as<uint32_t>() + uint64_t(nwg) * 64 + 1, 4,
+                                             hipMemcpyDeviceToHost, c->st));
                     HIPCHK(c, hipStreamSynchronize(c->st)); // `which` is a host vector
+                    if (lerr) return fail(c, SK_EDEVICE, "long-element hash: look-back wait ran out");
                     d_pre = c->long_h.as<uint64_t>();
                 }
             }

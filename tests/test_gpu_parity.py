@@ -744,8 +744,9 @@ def test_stale_slab_id_rejected(O):
 
 def test_pfadd_long_elements_workgroup_hash(O):
     """C1's addAll (quirk Q1: ONE element = the Jackson array of 1M Longs, ~40 MB) and a batch mixing elements
-    of 64 KiB .. 3 MB with short ones: elements >= 64 KiB are hashed by k_murmur_long (one workgroup each); replies
-    and registers equal the oracle's, and the 40 MB element hashes well within 50 ms of device time."""
+    of 64 KiB .. 3 MB with short ones: elements >= 64 KiB are hashed by the bit-round scan (k_ms_planes +
+    k_ms_rounds: 256 KiB per workgroup, a look-back across workgroups), so the cases straddle workgroup boundaries
+    and every tail length; replies and registers equal the oracle's."""
     import time
 
     from redisson_amd import JLong, JsonJacksonCodec, SketchEngine
@@ -767,7 +768,7 @@ def test_pfadd_long_elements_workgroup_hash(O):
         rng = np.random.default_rng(3)
         elems = []
         for i in range(40):
-            n = int(rng.choice([5, 37, 65536, 65537, 200_001, 3_000_003])) + i
+            n = int(rng.choice([5, 37, 65536, 65537, 200_001, 262_144, 262_136, 524_288 + 8, 3_000_003])) + i % 8
             elems.append(rng.integers(0, 256, n, dtype=np.uint8).tobytes())
         keys = [b"long:%d" % (i % 3) for i in range(40)]
         assert e.pfadd(keys, [[x] for x in elems]) == ref.pfadd(keys, [[x] for x in elems])

@@ -413,7 +413,7 @@ __global__ void __launch_bounds__(SK_PFP_TPB) k_pfp_hash(uint64_t n, const uint3
         uint64_t i = base + uint64_t(e) * SK_PFP_TPB + threadIdx.x;
         if (i < n) {
             uint32_t len = uint32_t(ob[e] - oa[e]);
-            uint64_t hh = (pre_h && len >= SK_LONG_ELEM) ? pre_h[i] // hashed by a whole workgroup (k_murmur_long)
+            uint64_t hh = (pre_h && len >= SK_LONG_ELEM) ? pre_h[i] // hashed by the bit-round scan (k_ms_rounds)
                           : pfp_win_fits(wb[e], wb[e + 1])
                               ? murmur64a_r(LdsReader{win[e & 1], uint32_t(wb[e] & 15u) + uint32_t(oa[e] - wb[e])},
                                             len, 0xadc83b19ull)

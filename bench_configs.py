@@ -88,7 +88,7 @@ def c1(eng, args):
     eng.prof_reset(); eng.prof_enable(True)
     t_q1 = timed(eng, lambda: eng.pfadd([b"hll:c1q"], [[blob]]))
     eng.prof_enable(False)
-    n_l, ms_long = eng.prof_read("pfadd_long")   # the element's workgroup hash (k_murmur_long), device time
+    n_l, ms_long = eng.prof_read("pfadd_long")   # the element's bit-round hash (k_ms_planes + k_ms_rounds), device time
     line({"metric": "C1 PFADD inserts/sec (one key, RBatch of single-element PFADDs)", "value": n * steps / t_ss,
           "unit": "inserts/s", "config": {"workload": "c1", "elements": n, "count_after": cnt},
           "steady_state": "%d back-to-back batches of %d fresh Longs into the one key" % (steps, n),

@@ -21,7 +21,7 @@ namespace sk {
 // HLL slab handles from sk_hll_resolve carry the slab's generation in the top 8 bits (stale caller-cached ids
 // are rejected by the host entry points); kernels index the arena with the low 24 bits
 #define SK_SLAB_MASK 0xffffffu
-// elements at least this long are hashed by a whole workgroup (k_murmur_long) before the PFADD hash pass
+// elements at least this long are hashed by the bit-round scan (k_ms_rounds) before the PFADD hash pass
 #define SK_LONG_ELEM (uint64_t(1) << 16)
 
 __device__ __forceinline__ uint64_t funnel(uint64_t lo, uint64_t hi, unsigned sh) {

@@ -25,7 +25,7 @@ uint32_t pfadd_conflict_lds_capacity();
 uint32_t pfp_blocks(uint64_t n);
 uint32_t pfp_buckets();
 uint32_t pfp_epb();
-// pre: per-element hashes of the elements >= long_elem_bytes() (k_murmur_long), or null
+// pre: per-element hashes of the elements >= long_elem_bytes() (k_ms_planes + k_ms_rounds), or null
 hipError_t launch_pfp_hash(hipStream_t st, uint64_t n, const uint32_t *key_ids, const uint64_t *off,
                            const uint8_t *bytes, int v5, uint64_t *chunks, uint32_t *S, uint16_t *pos,
                            uint32_t *big_alloc, const uint64_t *pre = nullptr);

@@ -1,4 +1,4 @@
-"""A/B timing of the long-element hash (k_murmur_long) on the C1 Q1 element: device ms per run, 5 runs.
+"""A/B timing of the long-element hash (k_ms_planes + k_ms_rounds) on the C1 Q1 element: device ms per run, 5 runs.
 Usage: SK_LIB_PATH=<lib> python3 tools/exp_blob.py"""
 import json
 import os

@@ -1,5 +1,5 @@
 // Micro-benchmark: MurmurHash64A's sequential state chain h = (h ^ k) * m over precomputed k[] (one wave).
-// Variant S: uniform loads (s_load) + SALU 64-bit chain.  Variant V: one lane, VALU chain (as k_murmur_long).
+// Variant S: uniform loads (s_load) + SALU 64-bit chain.  Variant V: one lane, VALU chain (as the round-2 chain kernel).
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdint>

@@ -398,6 +398,37 @@ __device__ __forceinline__ uint64_t mod_invariant(uint64_t x, uint64_t d, uint64
     return r;
 }
 
+// Redisson's probe indexes (M:RedissonBloomFilter.java hash(): index_i = (h_i & Long.MAX_VALUE) % size with
+// h_0 = h1, h_{i+1} = h_i + (i even ? h2 : h1), wrapping) at two 64-bit reductions per element instead of one per
+// probe.  m_i = h_i mod 2^63 steps by D = d mod 2^63 (d = h2 or h1), wrapping at 2^63, so
+//   index_{i+1} = index_i + (D mod size) - [m_i + D >= 2^63] * (2^63 mod size)   (then one correction into [0, size)).
+// Sizes are < 2^62 (Redis strings: <= 2^32 bits), so the sum fits a signed 64-bit word.
+struct BloomIdx {
+    uint64_t m, r, size, D1, D2, A1, A2, C;
+    __device__ __forceinline__ BloomIdx(uint64_t h1, uint64_t h2, uint64_t size_, uint64_t magic) : size(size_) {
+        const uint64_t MAXL = 0x7fffffffffffffffull;
+        D1 = h1 & MAXL;
+        D2 = h2 & MAXL;
+        A1 = mod_invariant(D1, size, magic);
+        A2 = mod_invariant(D2, size, magic);
+        C = mod_invariant(MAXL, size, magic) + 1; // 2^63 mod size (uniform)
+        if (C == size) C = 0;
+        m = D1;
+        r = A1;
+    }
+    // index of probe p+1 from that of probe p
+    __device__ __forceinline__ void next(int p) {
+        const uint64_t D = (p & 1) ? D1 : D2, A = (p & 1) ? A1 : A2;
+        const uint64_t s = m + D;
+        const bool w = s >= (1ull << 63);
+        m = w ? s - (1ull << 63) : s;
+        int64_t t = int64_t(r + A) - (w ? int64_t(C) : 0);
+        if (t < 0) t += int64_t(size);
+        else if (t >= int64_t(size)) t -= int64_t(size);
+        r = uint64_t(t);
+    }
+};
+
 // Redis bit strings are MSB-first: bit i lives in byte i>>3 at mask 0x80>>(i&7)
 __device__ __forceinline__ int get_bit(const uint8_t *buf, uint64_t len, uint64_t idx) {
     uint64_t byte = idx >> 3;

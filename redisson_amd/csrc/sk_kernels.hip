@@ -1009,14 +1009,15 @@ __device__ __forceinline__ void bloom_contains_body(uint64_t n, const uint64_t *
     } else {
         bloom_hashes(bytes + o, len, &h1, &h2);
     }
-    uint64_t slen = *d_len, h = h1;
+    uint64_t slen = *d_len;
+    BloomIdx bi(h1, h2, size, magic);
     uint8_t r = 1;
     for (int j = 0; j < k - 1; j++) {
-        if (!get_bit(bits, slen, mod_invariant(h & 0x7fffffffffffffffull, size, magic))) {
+        if (!get_bit(bits, slen, bi.r)) {
             r = 0;
             break;
         }
-        h += (j & 1) ? h1 : h2;
+        bi.next(j);
     }
     out[i] = r;
 }
@@ -1061,14 +1062,15 @@ __global__ void __launch_bounds__(256) k_bloom_probe_h(uint64_t n, const uint4 *
     if (i >= n) return;
     uint4 v = hh[i];
     uint64_t h1 = uint64_t(v.x) | uint64_t(v.y) << 32, h2 = uint64_t(v.z) | uint64_t(v.w) << 32;
-    uint64_t slen = *d_len, h = h1;
+    uint64_t slen = *d_len;
+    BloomIdx bi(h1, h2, size, magic);
     uint8_t r = 1;
     for (int j = 0; j < k - 1; j++) {
-        if (!get_bit(bits, slen, mod_invariant(h & 0x7fffffffffffffffull, size, magic))) {
+        if (!get_bit(bits, slen, bi.r)) {
             r = 0;
             break;
         }
-        h += (j & 1) ? h1 : h2;
+        bi.next(j);
     }
     out[i] = r;
 }
@@ -1266,15 +1268,15 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_rc_hash(uint64_t n, const uint
                 bloom_hashes(bytes + oa[e], len, &h1, &h2);
             }
             if (!ADD) out[i] = 1;
-            uint64_t h = h1;
+            BloomIdx bi(h1, h2, size, magic);
 #pragma unroll
             for (int p = 0; p < RC_PMAX; p++) {
                 if (uint32_t(p) >= P) break;
-                uint32_t idx = uint32_t(mod_invariant(h & 0x7fffffffffffffffull, size, magic));
+                uint32_t idx = uint32_t(bi.r);
                 ix[e][p] = idx;
                 uint32_t rank = atomicAdd(&hist[idx >> RB], 1u);
                 rk[e][p >> 1] |= rank << ((p & 1) * 16);
-                h += (p & 1) ? h1 : h2;
+                bi.next(p);
             }
         }
         if (pre) pfp_win_store(wb[e + 1], wb[e + 2], v, win[(e + 1) & 1]);
@@ -1621,12 +1623,11 @@ __global__ void __launch_bounds__(256) k_bloom_probes(uint64_t n, const uint64_t
     } else {
         bloom_hashes(bytes + o, len, &h1, &h2);
     }
-    uint64_t h = h1;
+    BloomIdx bi(h1, h2, size, magic);
     uint64_t pos = i * uint64_t(k);
     for (int j = 0; j < k; j++) {
-        uint64_t idx = mod_invariant(h & 0x7fffffffffffffffull, size, magic);
-        keys[pos + j] = (idx << 32) | (pos + j);
-        h += (j & 1) ? h1 : h2;
+        keys[pos + j] = (bi.r << 32) | (pos + j);
+        bi.next(j);
     }
 }
 

@@ -208,6 +208,7 @@ def main():
     for s in range(T0, T0 + K):
         step(s)
     eng.timer_record(1)
+    t_enq = time.perf_counter() - t0   # host time to enqueue the K steps (the device may still be running)
     eng.sync()
     t1 = time.perf_counter()
     barrier(pg)
@@ -292,6 +293,7 @@ def main():
         "bloom_contains_per_s": CB * world / (bl_ms * 1e-3) if bl_ms else None,
         "bloom_add_per_s": fill / add_s if add_s else None,
         "device_ms_timed_region": dev_ms,
+        "host_enqueue_ms_per_step": t_enq / K * 1e3,
         "roofline": {"kernel": "%s chain (%s)" % (dom, " + ".join("k_" + p_ for p_ in chain_kernels[dom])),
                      "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

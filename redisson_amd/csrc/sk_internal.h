@@ -31,10 +31,11 @@ hipError_t launch_pfp_hash(hipStream_t st, uint64_t n, const uint32_t *key_ids, 
                            uint32_t *big_alloc, const uint64_t *pre = nullptr);
 uint64_t long_elem_bytes();
 // MurmurHash64A (seed 0xadc83b19) of long elements into out_h[which[i]] by 64 bit rounds of an XOR scan.
-// meta = which[n_long] then first_wg[n_long + 1] (murmur_long_wgs(len) workgroups per element, n_wg in all);
-// plane: n_wg * 1024 * 64 words; flags: n_wg * 64 + 2 words, flags[n_wg * 64 + 1] != 0 after the run = a look-back
-// wait ran out (the hashes are then invalid)
+// meta = which[n_long], first_wg[n_long + 1] (murmur_long_wgs(len) workgroups per element, n_wg in all), then at
+// the next even word u64 poff[n_long + 1] (prefix of murmur_long_plane_words(len)); plane: poff[n_long] words;
+// flags: n_wg * 64 + 2 words, flags[n_wg * 64 + 1] != 0 after the run = a look-back wait ran out (hashes invalid)
 uint32_t murmur_long_wgs(uint64_t len);
+uint64_t murmur_long_plane_words(uint64_t len);
 hipError_t launch_murmur_long(hipStream_t st, uint32_t n_long, uint32_t n_wg, const uint8_t *bytes,
                               const uint64_t *off, const uint32_t *meta, uint32_t *plane, uint32_t *flags,
                               uint64_t *out_h);

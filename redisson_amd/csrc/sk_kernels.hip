@@ -486,7 +486,11 @@ __global__ void __launch_bounds__(SK_PFP_TPB) k_pfp_reply(uint64_t n, const uint
 #define SK_MS_INCL (1u << 31)
 #define SK_MS_SPIN (1u << 20)
 
-// meta: which[n_long] (element index in the batch), then first_wg[n_long + 1] (workgroup prefix over the elements)
+// meta: which[n_long] (element index in the batch), first_wg[n_long + 1] (workgroup prefix over the elements), then
+// at the next even word the u64 plane offsets poff[n_long + 1] (prefix of 64 * ceil(blocks / 32) words)
+__device__ __forceinline__ const uint64_t *ms_poff(const uint32_t *meta, uint32_t n_long) {
+    return reinterpret_cast<const uint64_t *>(meta + ((2 * n_long + 2) & ~1u));
+}
 __device__ __forceinline__ uint32_t ms_elem_of(const uint32_t *first_wg, uint32_t n_long, uint32_t w) {
     uint32_t lo = 0, hi = n_long; // first_wg[lo] <= w < first_wg[hi]
     while (hi - lo > 1) {
@@ -504,9 +508,10 @@ __global__ void __launch_bounds__(SK_MS_TPB) k_ms_planes(const uint8_t *__restri
     const uint32_t *which = meta, *first_wg = meta + n_long;
     const uint32_t w = blockIdx.x, e = ms_elem_of(first_wg, n_long, w);
     const uint64_t o = off[which[e]], nb = (off[which[e] + 1] - o) >> 3;
-    const uint64_t nw = uint64_t(first_wg[e + 1] - first_wg[e]) * SK_MS_TPB;     // words per plane
+    const uint64_t nw = (nb + SK_MS_S - 1) / SK_MS_S; // words per plane
     const uint64_t g = uint64_t(w - first_wg[e]) * SK_MS_TPB + threadIdx.x;
-    uint32_t *pl = plane + uint64_t(first_wg[e]) * SK_MS_TPB * 64;
+    if (g >= nw) return;
+    uint32_t *pl = plane + ms_poff(meta, n_long)[e];
     uint32_t word[64];
 #pragma unroll
     for (int j = 0; j < 64; j++) word[j] = 0;
@@ -542,9 +547,10 @@ __global__ void __launch_bounds__(SK_MS_TPB) k_ms_rounds(const uint8_t *__restri
     const uint32_t e = ms_elem_of(first_wg, n_long, w);
     const uint32_t w0 = first_wg[e], nwg = first_wg[e + 1] - w0, lw = w - w0;
     const uint64_t o = off[which[e]], len = off[which[e] + 1] - o, nb = len >> 3;
-    const uint64_t nw = uint64_t(nwg) * SK_MS_TPB;
+    const uint64_t nw = (nb + SK_MS_S - 1) / SK_MS_S;
     const uint64_t g = uint64_t(lw) * SK_MS_TPB + threadIdx.x;
-    const uint32_t *pl = plane + uint64_t(w0) * SK_MS_TPB * 64 + g;
+    const bool has = g < nw; // threads past the element's last block carry d = 0
+    const uint32_t *pl = plane + ms_poff(meta, n_long)[e] + (has ? g : 0);
     const uint64_t first_b = g * SK_MS_S;
     const uint32_t valid = first_b >= nb ? 0u : (nb - first_b >= SK_MS_S ? 0xffffffffu
                                                                           : (1u << uint32_t(nb - first_b)) - 1u);
@@ -553,11 +559,11 @@ __global__ void __launch_bounds__(SK_MS_TPB) k_ms_rounds(const uint8_t *__restri
 #pragma unroll
     for (int t = 0; t < SK_MS_S; t++) p[t] = 0;
     uint64_t fin = 0;
-    uint32_t kw = pl[0];
+    uint32_t kw = has ? pl[0] : 0u;
 #pragma unroll 1
     for (uint32_t j = 0; j < 64; j++) {
         const uint32_t kcur = kw;
-        if (j + 1 < 64) kw = pl[uint64_t(j + 1) * nw]; // next round's plane word, in flight during this round
+        if (has && j + 1 < 64) kw = pl[uint64_t(j + 1) * nw]; // next round's word, in flight during this round
         uint32_t pw = 0;
 #pragma unroll
         for (int t = 0; t < SK_MS_S; t++) {
@@ -2019,6 +2025,7 @@ uint32_t pfadd_conflict_lds_capacity() { return SK_CONF_MAX; }
 uint64_t long_elem_bytes() { return SK_LONG_ELEM; }
 
 uint32_t murmur_long_wgs(uint64_t len) { return uint32_t(((len >> 3) + SK_MS_BPW - 1) / SK_MS_BPW); }
+uint64_t murmur_long_plane_words(uint64_t len) { return 64 * (((len >> 3) + SK_MS_S - 1) / SK_MS_S); }
 
 hipError_t launch_murmur_long(hipStream_t st, uint32_t n_long, uint32_t n_wg, const uint8_t *bytes,
                               const uint64_t *off, const uint32_t *meta, uint32_t *plane, uint32_t *flags,

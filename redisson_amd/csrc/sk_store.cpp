@@ -1434,17 +1434,23 @@ static int pfadd_host_batch(sk_ctx *c, uint32_t n_cmds, const uint32_t *cmd_key,
             const uint64_t *d_pre = nullptr;
             if (c->pfadd_path == 1 && nbytes >= sk::long_elem_bytes()) {
                 std::vector<uint32_t> which, first_wg{0};
+                std::vector<uint64_t> poff{0};
                 for (uint64_t j = 0; j < m; j++)
                     if (off2[j + 1] - off2[j] >= sk::long_elem_bytes()) {
                         which.push_back(uint32_t(j));
                         first_wg.push_back(first_wg.back() + sk::murmur_long_wgs(off2[j + 1] - off2[j]));
+                        poff.push_back(poff.back() + sk::murmur_long_plane_words(off2[j + 1] - off2[j]));
                     }
                 if (!which.empty()) {
                     const uint32_t nl = uint32_t(which.size()), nwg = first_wg.back();
                     which.insert(which.end(), first_wg.begin(), first_wg.end());
+                    if (which.size() & 1) which.push_back(0); // poff starts at an even word
+                    const size_t at = which.size();
+                    which.resize(at + 2 * poff.size());
+                    std::memcpy(which.data() + at, poff.data(), poff.size() * 8);
                     HIPCHK(c, c->long_h.ensure(m * 8));
                     HIPCHK(c, c->long_which.ensure(which.size() * 4));
-                    HIPCHK(c, c->long_plane.ensure(uint64_t(nwg) * 1024 * 64 * 4));
+                    HIPCHK(c, c->long_plane.ensure(poff.back() * 4));
                     HIPCHK(c, c->long_flags.ensure((uint64_t(nwg) * 64 + 2) * 4));
                     HIPCHK(c, hipMemcpyAsync(c->long_which.p, which.data(), which.size() * 4, hipMemcpyHostToDevice,
                                              c->st));

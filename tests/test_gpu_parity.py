@@ -758,9 +758,14 @@ def test_pfadd_long_elements_workgroup_hash(O):
         ref = O.HLLStore()
         e.pfadd([b"hll:c1q"], [[blob[:100]]])              # warm the path
         ref.pfadd([b"hll:c1q"], [[blob[:100]]])
+        e.prof_reset()
+        e.prof_enable(True)
         t0 = time.perf_counter()
         got = e.pfadd([b"hll:c1q"], [[blob]])
         dt = time.perf_counter() - t0
+        e.prof_enable(False)
+        n_l, ms_l = e.prof_read("pfadd_long")
+        assert n_l == 1 and ms_l < 10.0, (n_l, ms_l)        # the bit-round hash: ~0.3 ms for the 41 MB element
         assert got == ref.pfadd([b"hll:c1q"], [[blob]])
         np.testing.assert_array_equal(e.hll_registers(b"hll:c1q"), ref.regs[b"hll:c1q"])
         assert e.pfcount([[b"hll:c1q"]]) == [ref.count([b"hll:c1q"])]

@@ -17,6 +17,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -32,7 +33,8 @@ PROF_STEPS = 2          # steps in each per-kernel breakdown pass (outside the t
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 # in-library event-timed phases (sk_prof_*): one kernel each, except the chains "pfadd" (every kernel of one
 # PFADD batch) and "bloom_contains" (every kernel of one contains call), and pfadd_sort (rocPRIM passes)
-HLL_KERNELS = ["pfp_hash", "pfp_apply", "pfp_reply", "pfadd_claim", "pfadd_commit", "pfadd_hash", "pfadd_apply"]
+HLL_KERNELS = ["pfp_hash", "pfp_apply", "pfp_reply", "pfl_hash", "pfl_part", "pfl_apply", "pfadd_claim",
+               "pfadd_commit", "pfadd_hash", "pfadd_apply"]
 BLOOM_KERNELS = ["bloom_rc_hash", "bloom_rc_probe"]
 CHAINS = ["pfadd", "bloom_contains"]
 PHASES = HLL_KERNELS + ["pfadd_sort"] + BLOOM_KERNELS + CHAINS
@@ -77,6 +79,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=1 << 20, help="commands per PFADD RBatch (C2: 1M)")
     ap.add_argument("--hll-batches", type=int, default=16, help="PFADD RBatches per step")
+    ap.add_argument("--group", type=int, default=0,
+                    help="RBatches group-committed per sk_pfadd_dev call (0 = all of a step's; 1 = one call each)")
     ap.add_argument("--contains-batch", type=int, default=16 << 20, help="Bloom contains elements per step")
     ap.add_argument("--tenants", type=int, default=100_000)
     ap.add_argument("--bloom-n", type=int, default=425_000_000)
@@ -88,6 +92,8 @@ def main():
 
     world, rank, local, pg = dist_setup()
     B, HB, CB, K, W = args.batch, args.hll_batches, args.contains_batch, args.steps, args.warmup
+    G = args.group if args.group > 0 else HB   # RBatches per device call (group commit)
+    assert HB % G == 0, "--hll-batches must be a multiple of --group"
     fill = args.bloom_fill
 
     # ------------------------------------------------------------ setup (untimed)
@@ -114,7 +120,7 @@ def main():
         d_ids = eng.to_device(ids[kid].astype(np.uint32))
         h_in.append((off, byt, tot, d_ids))
         h_total += tot
-    d_changed = eng.alloc(B)
+    d_changed = eng.alloc(G * B)
     mean_len_h = h_total / (nsteps * NH)
 
     # ONE logical C3 filter for the whole node: every rank holds an identical replica (the same 1B adds), and the
@@ -155,8 +161,8 @@ def main():
 
     def step(s):
         off, byt, tot, d_ids = h_in[s]
-        for h in range(HB):
-            eng.pfadd_dev(B, d_ids.ptr + h * B * 4, off.ptr + h * B * 8, byt, tot, d_changed)
+        for h in range(0, HB, G):
+            eng.pfadd_dev(G * B, d_ids.ptr + h * B * 4, off.ptr + h * B * 8, byt, tot, d_changed)
         off, byt, tot = c_in[s]
         eng.bloom_contains_dev(bloom, CB, off, byt, tot, d_contains)
 
@@ -189,7 +195,8 @@ def main():
         kern.append("bloom_contains")
     dom_kernel = max(kern, key=lambda p: iso[p][0] * iso[p][1])
     dom = max([c for c in CHAINS if c in iso], key=lambda c: iso[c][0] * iso[c][1])
-    chain_kernels = {"pfadd": [p for p in ("pfp_hash", "pfp_apply", "pfp_reply") if p in iso],
+    chain_kernels = {"pfadd": [p for p in ("pfp_hash", "pfp_apply", "pfp_reply", "pfl_hash", "pfl_part", "pfl_apply")
+                               if p in iso],
                      "bloom_contains": [p for p in BLOOM_KERNELS if p in iso] or ["bloom_contains"]}
     # breakdown as in the timed region (PFADD on the main stream, contains on the read stream, no host sync)
     over = profiled(W + P, True)
@@ -222,8 +229,9 @@ def main():
     units = (NH + CB) * K * world
     value = units / wall
     nr = (size + (1 << 20) - 1) >> 20
-    bpu = per_unit_bytes(mean_len_h, mean_len_b, k, size, CB, nr)
-    upl = {"pfp_hash": B, "pfp_apply": B, "pfp_reply": B, "pfadd": B, "bloom_contains": CB,
+    bpu = per_unit_bytes(mean_len_h, mean_len_b, k, size, CB, nr, len(mine), G * B)
+    upl = {"pfp_hash": B, "pfp_apply": B, "pfp_reply": B, "pfadd": G * B if G > 1 else B, "pfl_hash": G * B,
+           "pfl_part": G * B, "pfl_apply": G * B, "bloom_contains": CB,
            "bloom_rc_hash": CB, "bloom_rc_probe": CB}
     # the chain's events span one launch of the chain in the steady state of the timed region (for PFADD: the
     # previous batch's apply end to this batch's apply end, i.e. the per-batch period; its hash overlaps the
@@ -282,14 +290,16 @@ def main():
         "dtype": "u8/u64",
         "data": "synthetic: SplitMix64 Longs as Jackson bytes [\"java.lang.Long\",v] (mean %.1f B)" % mean_len_h,
         "config": {
-            "workload": "C2 PFADD 1 elem/cmd over %d tenants, %d RBatches of %d commands + C3 Bloom contains "
-                        "(m=%d, k=%d, filled with %d adds, 50%% members), %d elements, per step and GPU; "
-                        "one C3 filter replicated on the %d GPU(s)" % (args.tenants, HB, B, size, k, fill, CB, world),
-            "pfadd_batch": B, "pfadd_batches_per_step": HB, "contains_batch": CB, "tenants": args.tenants,
+            "workload": "C2 PFADD 1 elem/cmd over %d tenants, %d RBatches of %d commands (group-committed %d per "
+                        "device call) + C3 Bloom contains (m=%d, k=%d, filled with %d adds, 50%% members), %d elements, "
+                        "per step and GPU; one C3 filter replicated on the %d GPU(s)"
+                        % (args.tenants, HB, B, G, size, k, fill, CB, world),
+            "pfadd_batch": B, "pfadd_batches_per_step": HB, "pfadd_batches_per_call": G, "contains_batch": CB,
+            "tenants": args.tenants,
             "bloom_bits": size, "bloom_k": k, "bloom_fill": fill, "partitioner": "calcSlot(key) %% %d" % world,
         },
         # device-time rates of each chain run alone, whole job
-        "hll_inserts_per_s": B * world / (hll_ms * 1e-3) if hll_ms else None,
+        "hll_inserts_per_s": upl["pfadd"] * world / (hll_ms * 1e-3) if hll_ms else None,
         "bloom_contains_per_s": CB * world / (bl_ms * 1e-3) if bl_ms else None,
         "bloom_add_per_s": fill / add_s if add_s else None,
         "device_ms_timed_region": dev_ms,
@@ -321,12 +331,17 @@ def main():
     eng.close()
 
 
-def per_unit_bytes(mean_len_h, mean_len_b, k, size, CB, nr):
+def per_unit_bytes(mean_len_h, mean_len_b, k, size, CB, nr, tenants, group):
     """Algorithmic bytes per unit of each kernel (DESIGN.md kernel table).  Random probes / register lines are
     priced at one 64-B sector; streamed data at its bytes."""
     P = k - 1
     seg = 4.0 * nr / 4096            # segment table entry per hash block, per element
+    lines = 128.0 * tenants          # 128-B register lines of the arena; a group of `group` elements touches
+    touched = lines * (1.0 - math.exp(-group / lines))   # this many of them (uniform tenants)
     return {
+        "pfl_hash": mean_len_h + 8 + 4 + 8,            # key bytes + offset + slab id in, record out
+        "pfl_part": 8 + 8 + 8,                         # records read by count and scatter, written once
+        "pfl_apply": 8 + 1 + 2 * 128 * touched / group,  # record + reply + each touched line in and out once
         "pfp_hash": mean_len_h + 8 + 4 + 8,            # key bytes + offset + slab id in, record out
         "pfp_apply": 8 + 64 + 64 + 1,                  # record + register sector load (R0) + store + reply
         "pfp_reply": 1 + 2 + 1,                        # chunk-order reply + chunk slot in, reply out
@@ -350,7 +365,8 @@ def pmc_traffic(phase):
 
     kern = {"bloom_contains": "sk::k_bloom_contains", "pfadd_claim": "sk::k_pfadd_claim",
             "pfadd_commit": "sk::k_pfadd_commit", "pfp_hash": "sk::k_pfp_hash", "pfp_apply": "sk::k_pfp_apply",
-            "pfp_reply": "sk::k_pfp_reply", "bloom_rc_hash": "sk::k_bloom_rc_hash",
+            "pfp_reply": "sk::k_pfp_reply", "bloom_rc_hash": "sk::k_bloom_rc_hash", "pfl_hash": "sk::k_pfl_hash",
+            "pfl_apply": "sk::k_pfl_apply",
             "bloom_rc_probe": "sk::k_bloom_rc_probe"}.get(phase)
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_summary.json")))
     if not kern or not files:

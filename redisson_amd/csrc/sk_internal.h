@@ -45,6 +45,24 @@ hipError_t launch_pfp_apply(hipStream_t st, uint64_t n, const uint64_t *chunks, 
                             uint32_t *ev_n = nullptr); // changed != null: replies straight to batch order (no k_pfp_reply)
 hipError_t launch_pfp_reply(hipStream_t st, uint64_t n, const uint8_t *rep, const uint16_t *pos,
                             const uint32_t *cmd_of, uint8_t *changed);
+// PFADD line schedule (one element per command, n <= 2^26, <= pfl_max_slabs() sketches): hash into 128 line
+// buckets, partition each into runs of (bucket, 512 sketches, tile of hash blocks), apply with the lines in LDS
+struct PflDims {
+    uint32_t nblk, tb, ntile, nsub, nsums; // hash blocks, blocks per run tile, tiles, fine buckets per bucket
+    uint64_t nf, ncount;         // fine buckets; run counts (C holds ncount + 1 words)
+    uint64_t chunk_bytes, S_bytes;
+};
+PflDims pfl_dims(uint64_t n, uint32_t nslab, uint32_t tile_blocks = 0); // 0: the default tile
+uint32_t pfl_max_slabs();
+hipError_t launch_pfl_hash(hipStream_t st, uint64_t n, const uint32_t *key_ids, const uint64_t *off,
+                           const uint8_t *bytes, int v5, uint64_t *chunks, uint32_t *S, uint32_t *big_alloc);
+// count + scan + scatter; C u32[ncount + 1], sums u32[nsums + 1], rec2 u64[n]
+hipError_t launch_pfl_part(hipStream_t st, const PflDims &d, const uint64_t *chunks, const uint32_t *S, uint32_t *C,
+                           uint32_t *sums, uint64_t *rec2);
+// big tables: 2 entries per record of the call (u64 keys, u32 values)
+hipError_t launch_pfl_apply(hipStream_t st, const PflDims &d, const uint64_t *rec2, const uint32_t *C, uint32_t nslab,
+                            uint8_t *arena, uint8_t *changed, uint32_t *big_alloc, uint64_t *big_keys,
+                            uint32_t *big_vals);
 hipError_t sort_keys_size(uint64_t n, unsigned begin_bit, unsigned end_bit, size_t *bytes);
 hipError_t sort_keys(hipStream_t st, void *tmp, size_t tmp_bytes, const uint64_t *in, uint64_t *out, uint64_t n,
                      unsigned begin_bit, unsigned end_bit);

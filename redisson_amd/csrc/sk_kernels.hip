@@ -357,21 +357,30 @@ __device__ __forceinline__ void pfp_win_store(uint64_t lo, uint64_t hi, const ui
     }
 }
 
-__global__ void __launch_bounds__(SK_PFP_TPB) k_pfp_hash(uint64_t n, const uint32_t *__restrict__ key_ids,
-                                                         const uint64_t *__restrict__ off,
-                                                         const uint8_t *__restrict__ bytes, int v5,
-                                                         uint64_t *__restrict__ chunks, uint32_t *__restrict__ S,
-                                                         uint32_t nblocks, uint16_t *__restrict__ pos,
-                                                         uint32_t *__restrict__ big_alloc,
-                                                         const uint64_t *__restrict__ pre_h) {
+// line schedule (sketch-major group apply, below): coarse bucket of a register = its 128-register line, rotated
+// per sketch, so bucket b holds exactly one line of every sketch and a hot sketch spreads over all 128 buckets
+#define SK_PFL_NB 128
+__device__ __forceinline__ uint32_t pfl_rot(uint32_t slab) { return (slab * 0x9E3779B1u) >> 25; }
+__device__ __forceinline__ uint32_t pfl_bucket(uint32_t slab, uint32_t reg) {
+    return ((reg >> 7) + pfl_rot(slab)) & (SK_PFL_NB - 1);
+}
+
+// NBK buckets; LINE = false: the partition path (records slot << 26 | seq << 6 | rho, pfp_bucket),
+// LINE = true: the line schedule (records slab << 32 | reg << 18 | rho << 12 | element-in-block, pfl_bucket)
+template <int NBK, bool LINE>
+__device__ __forceinline__ void pfp_hash_impl(uint64_t n, const uint32_t *__restrict__ key_ids,
+                                              const uint64_t *__restrict__ off, const uint8_t *__restrict__ bytes,
+                                              int v5, uint64_t *__restrict__ chunks, uint32_t *__restrict__ S,
+                                              uint32_t nblocks, uint16_t *__restrict__ pos,
+                                              uint32_t *__restrict__ big_alloc, const uint64_t *__restrict__ pre_h) {
     // the block's records reuse the key windows' LDS once the last round is hashed: 98 KiB in all, so a hash
     // workgroup (the next batch, on the third stream) fits on a CU beside an apply workgroup (61.5 KiB)
-    __shared__ uint32_t h[SK_PFP_NB];
+    __shared__ uint32_t h[NBK];
     __shared__ uint32_t wsum[SK_PFP_TPB / 64];
     __shared__ uint64_t win[2][SK_PFP_WIN];
     static_assert(SK_PFP_EPB <= 2 * SK_PFP_WIN, "records fit the windows");
     uint64_t *lrec = &win[0][0];
-    for (uint32_t b = threadIdx.x; b < SK_PFP_NB; b += SK_PFP_TPB) h[b] = 0;
+    for (uint32_t b = threadIdx.x; b < NBK; b += SK_PFP_TPB) h[b] = 0;
     if (blockIdx.x == 0 && threadIdx.x == 0) *big_alloc = 0;
     constexpr int PER = SK_PFP_EPB / SK_PFP_TPB;
     const uint64_t base = uint64_t(blockIdx.x) * SK_PFP_EPB;
@@ -420,22 +429,27 @@ __global__ void __launch_bounds__(SK_PFP_TPB) k_pfp_hash(uint64_t n, const uint3
                               : murmur64a(bytes + oa[e], len, 0xadc83b19ull);
             uint32_t reg, rho;
             hll_pat(hh, v5, &reg, &rho);
-            uint64_t slot = (uint64_t(kid[e]) << 14) | reg;
-            r[e] = (slot << 26) | (i << 6) | rho;
-            bk[e] = pfp_bucket(slot);
+            if (LINE) {
+                r[e] = (uint64_t(kid[e]) << 32) | (uint64_t(reg) << 18) | (rho << 12) | uint32_t(i - base);
+                bk[e] = pfl_bucket(kid[e], reg);
+            } else {
+                uint64_t slot = (uint64_t(kid[e]) << 14) | reg;
+                r[e] = (slot << 26) | (i << 6) | rho;
+                bk[e] = pfp_bucket(slot);
+            }
             rk[e] = atomicAdd(&h[bk[e]], 1u);
         }
         if (pre) pfp_win_store(wb[e + 1], wb[e + 2], v, win[(e + 1) & 1]);
         __syncthreads(); // window e+1 staged; window e free for round e+2
     }
-    // bucket starts (one bucket per thread), row SK_PFP_NB = the block's total
-    uint32_t c0 = threadIdx.x < SK_PFP_NB ? h[threadIdx.x] : 0u, tot;
+    // bucket starts (one bucket per thread), row NBK = the block's total
+    uint32_t c0 = threadIdx.x < NBK ? h[threadIdx.x] : 0u, tot;
     uint32_t st0 = block_exscan<SK_PFP_TPB>(c0, wsum, &tot);
-    if (threadIdx.x < SK_PFP_NB) {
+    if (threadIdx.x < NBK) {
         h[threadIdx.x] = st0;
         S[uint64_t(threadIdx.x) * nblocks + blockIdx.x] = st0;
     }
-    if (threadIdx.x == 0) S[uint64_t(SK_PFP_NB) * nblocks + blockIdx.x] = tot;
+    if (threadIdx.x == 0) S[uint64_t(NBK) * nblocks + blockIdx.x] = tot;
     __syncthreads();
 #pragma unroll
     for (int e = 0; e < PER; e++)
@@ -447,6 +461,23 @@ __global__ void __launch_bounds__(SK_PFP_TPB) k_pfp_hash(uint64_t n, const uint3
     __syncthreads();
     uint64_t *dst = chunks + base;
     for (uint32_t t = threadIdx.x; t < tot; t += SK_PFP_TPB) dst[t] = lrec[t];
+}
+
+__global__ void __launch_bounds__(SK_PFP_TPB) k_pfp_hash(uint64_t n, const uint32_t *__restrict__ key_ids,
+                                                         const uint64_t *__restrict__ off,
+                                                         const uint8_t *__restrict__ bytes, int v5,
+                                                         uint64_t *__restrict__ chunks, uint32_t *__restrict__ S,
+                                                         uint32_t nblocks, uint16_t *__restrict__ pos,
+                                                         uint32_t *__restrict__ big_alloc,
+                                                         const uint64_t *__restrict__ pre_h) {
+    pfp_hash_impl<SK_PFP_NB, false>(n, key_ids, off, bytes, v5, chunks, S, nblocks, pos, big_alloc, pre_h);
+}
+__global__ void __launch_bounds__(SK_PFP_TPB) k_pfl_hash(uint64_t n, const uint32_t *__restrict__ key_ids,
+                                                         const uint64_t *__restrict__ off,
+                                                         const uint8_t *__restrict__ bytes, int v5,
+                                                         uint64_t *__restrict__ chunks, uint32_t *__restrict__ S,
+                                                         uint32_t nblocks, uint32_t *__restrict__ big_alloc) {
+    pfp_hash_impl<SK_PFL_NB, true>(n, key_ids, off, bytes, v5, chunks, S, nblocks, nullptr, big_alloc, nullptr);
 }
 
 // Replies back to batch order: rep holds them in chunk order (written by
@@ -671,11 +702,12 @@ struct BigTable {
     unsigned long long *gk; // global keys
     uint32_t *gv;
     uint32_t S;
+    uint32_t L = SK_BIG_LDS; // LDS slots (power of two)
 
     __device__ void insert(uint64_t key, uint32_t seq) const {
         uint32_t h = big_hash(key);
         for (uint32_t p = 0; p < SK_BIG_PROBE; p++) {
-            uint32_t s = (h + p) & (SK_BIG_LDS - 1);
+            uint32_t s = (h + p) & (L - 1);
             unsigned long long k = lk[s];
             if (k == SK_BIG_EMPTY) k = atomicCAS(&lk[s], SK_BIG_EMPTY, (unsigned long long)key);
             if (k == SK_BIG_EMPTY || k == key) {
@@ -695,7 +727,7 @@ struct BigTable {
     __device__ uint32_t find(uint64_t key) const {
         uint32_t h = big_hash(key);
         for (uint32_t p = 0; p < SK_BIG_PROBE; p++) {
-            uint32_t s = (h + p) & (SK_BIG_LDS - 1);
+            uint32_t s = (h + p) & (L - 1);
             unsigned long long k = lk[s];
             if (k == key) return lv[s];
             if (k == SK_BIG_EMPTY) return 0xffffffffu; // slots only fill: the key was never inserted
@@ -843,6 +875,306 @@ __global__ void __launch_bounds__(SK_PFP_ATPB) __attribute__((amdgpu_waves_per_e
     __syncthreads();
     uint8_t *rs = rep + uint64_t(j) * SK_PFP_EPB + lo; // replies as runs, in the chunk's order
     for (uint32_t u = sub; u < c; u += 4) rs[u] = r0[dst + u];
+}
+
+// ---------------------------------------------------------------- PFADD, line schedule (group apply)
+// For a large device batch (many RBatches of one-element commands group-committed into one call, up to 2^26
+// elements) registers are applied sketch-major with the registers held in LDS, instead of one random register
+// line read and written per element:
+//   k_pfl_hash     as k_pfp_hash, 128 coarse buckets: bucket b holds line (b - rot(s)) & 127 of every sketch s
+//   k_pfl_count    per (bucket, tile of 128 hash blocks): records per fine bucket = (b, s >> 8)
+//   k_scan_*       exclusive scan of the counts (fine-bucket major, tile minor) -> each (fine bucket, tile) run
+//   k_pfl_scatter  records to their run: rec2 = slab_low << 46 | reg << 32 | rho << 26 | seq (26 bits)
+//   k_pfl_apply    one workgroup per fine bucket: its 256 lines (one per sketch, 32 KiB) into LDS with its
+//                  records, the records chained per register in LDS, the sequential replies (rho beats the
+//                  register and every earlier rho of it), the lines that changed stored back.
+// Runs are in tile order and tiles in batch order, so a fine bucket larger than one chunk is applied in chunks of
+// whole runs with the LDS registers carried over; a single run larger than a chunk is resolved with the (slot,
+// rho) -> min seq table of pfp_big_resolve, against the LDS registers.
+#define SK_PFL_SH 7        // sketches per fine bucket = 2^SH (128 lines of 128 B = 16 KiB of registers)
+#define SK_PFL_TILE 1024   // hash blocks per run tile (default; SK_PFL_TILE)
+#define SK_PFL_BTPB 512    // count / scatter threads: 4 per hash block, 128 blocks per pass over the tile
+#define SK_PFL_ATPB 256    // apply threads (five apply workgroups per CU: 29 KiB of LDS each)
+#define SK_PFL_CAP 1024    // records per apply chunk
+#define SK_PFL_HT 1024     // chain heads per chunk
+#define SK_PFL_MAXSUB 8192 // fine buckets per coarse bucket (2^20 sketches)
+__device__ __forceinline__ uint32_t pfl_ht(uint64_t key) {
+    return uint32_t((key * 0xC2B2AE3D27D4EB4Full) >> 54); // 10 bits
+}
+
+// (coarse bucket, tile) of this workgroup: workgroups are dispatched to the 8 XCDs round robin, so the ids are
+// dealt out such that one XCD takes consecutive tiles of a bucket -- the runs (f, tile) and (f, tile + 1) of a fine
+// bucket are adjacent in memory, and their partial lines then meet in the same L2 (speed only)
+__device__ __forceinline__ void pfl_bt(uint32_t ntile, uint32_t *b, uint32_t *tile) {
+    const uint32_t total = ntile * SK_PFL_NB, L = blockIdx.x;
+    uint32_t q = L;
+    if ((total & 7u) == 0) q = (L & 7u) * (total >> 3) + (L >> 3);
+    *b = q / ntile;
+    *tile = q % ntile;
+}
+
+__global__ void __launch_bounds__(SK_PFL_BTPB) k_pfl_count(const uint64_t *__restrict__ chunks,
+                                                           const uint32_t *__restrict__ S, uint32_t nblk, uint32_t tb,
+                                                           uint32_t ntile, uint32_t nsub, uint32_t *__restrict__ C) {
+    __shared__ uint32_t hist[SK_PFL_MAXSUB];
+    for (uint32_t s = threadIdx.x; s < nsub; s += SK_PFL_BTPB) hist[s] = 0;
+    __syncthreads();
+    uint32_t b, tile;
+    pfl_bt(ntile, &b, &tile);
+    const uint32_t b0 = tile * tb, b1 = b0 + tb < nblk ? b0 + tb : nblk;
+    for (uint32_t blk = b0 + (threadIdx.x >> 2); blk < b1; blk += SK_PFL_BTPB / 4) {
+        const uint32_t lo = S[uint64_t(b) * nblk + blk], hi = S[uint64_t(b + 1) * nblk + blk];
+        const uint64_t *seg = chunks + uint64_t(blk) * SK_PFP_EPB;
+        for (uint32_t t = lo + (threadIdx.x & 3u); t < hi; t += 4) {
+            const uint32_t sb = uint32_t(seg[t] >> 32) >> SK_PFL_SH;
+            if (sb < nsub) atomicAdd(&hist[sb], 1u); // ids beyond the store's slabs are dropped (both passes)
+        }
+    }
+    __syncthreads();
+    for (uint32_t s = threadIdx.x; s < nsub; s += SK_PFL_BTPB)
+        C[(uint64_t(b) * nsub + s) * ntile + tile] = hist[s];
+}
+
+__global__ void __launch_bounds__(SK_PFL_BTPB) k_pfl_scatter(const uint64_t *__restrict__ chunks,
+                                                             const uint32_t *__restrict__ S, uint32_t nblk,
+                                                             uint32_t tb, uint32_t ntile, uint32_t nsub,
+                                                             const uint32_t *__restrict__ C,
+                                                             uint64_t *__restrict__ rec2) {
+    __shared__ uint32_t cur[SK_PFL_MAXSUB];
+    uint32_t b, tile;
+    pfl_bt(ntile, &b, &tile);
+    for (uint32_t s = threadIdx.x; s < nsub; s += SK_PFL_BTPB) cur[s] = C[(uint64_t(b) * nsub + s) * ntile + tile];
+    __syncthreads();
+    const uint32_t b0 = tile * tb, b1 = b0 + tb < nblk ? b0 + tb : nblk;
+    for (uint32_t blk = b0 + (threadIdx.x >> 2); blk < b1; blk += SK_PFL_BTPB / 4) {
+        const uint32_t lo = S[uint64_t(b) * nblk + blk], hi = S[uint64_t(b + 1) * nblk + blk];
+        const uint64_t *seg = chunks + uint64_t(blk) * SK_PFP_EPB;
+        const uint64_t seq0 = uint64_t(blk) * SK_PFP_EPB;
+        for (uint32_t t = lo + (threadIdx.x & 3u); t < hi; t += 4) {
+            const uint64_t r = seg[t];
+            const uint32_t slab = uint32_t(r >> 32), reg = uint32_t(r >> 18) & 16383u, rho = uint32_t(r >> 12) & 63u;
+            if ((slab >> SK_PFL_SH) >= nsub) continue;
+            const uint32_t p = atomicAdd(&cur[slab >> SK_PFL_SH], 1u);
+            rec2[p] = (uint64_t(slab & ((1u << SK_PFL_SH) - 1)) << 46) | (uint64_t(reg) << 32) |
+                      (uint64_t(rho) << 26) | (seq0 + (r & 4095u));
+        }
+    }
+}
+
+// exclusive scan of u32[n] in place, total at [n]: block sums, one-workgroup scan of the sums, block scans
+#define SK_SCAN_TPB 1024
+#define SK_SCAN_PER 4
+#define SK_SCAN_ITEMS (SK_SCAN_TPB * SK_SCAN_PER)
+__global__ void __launch_bounds__(SK_SCAN_TPB) k_scan_reduce(uint64_t n, const uint32_t *__restrict__ v,
+                                                             uint32_t *__restrict__ sums) {
+    __shared__ uint32_t wsum[SK_SCAN_TPB / 64];
+    const uint64_t base = uint64_t(blockIdx.x) * SK_SCAN_ITEMS;
+    uint32_t s = 0;
+#pragma unroll
+    for (int q = 0; q < SK_SCAN_PER; q++) {
+        const uint64_t i = base + uint64_t(q) * SK_SCAN_TPB + threadIdx.x;
+        s += i < n ? v[i] : 0u;
+    }
+    uint32_t tot;
+    block_exscan<SK_SCAN_TPB>(s, wsum, &tot);
+    if (threadIdx.x == 0) sums[blockIdx.x] = tot;
+}
+__global__ void __launch_bounds__(SK_SCAN_TPB) k_scan_sums(uint32_t nb, uint32_t *__restrict__ sums) {
+    __shared__ uint32_t wsum[SK_SCAN_TPB / 64];
+    uint32_t carry = 0;
+    for (uint32_t b0 = 0; b0 < nb; b0 += SK_SCAN_TPB) {
+        const uint32_t i = b0 + threadIdx.x, x = i < nb ? sums[i] : 0u;
+        uint32_t tot;
+        const uint32_t ex = block_exscan<SK_SCAN_TPB>(x, wsum, &tot);
+        if (i < nb) sums[i] = carry + ex;
+        carry += tot;
+    }
+    if (threadIdx.x == 0) sums[nb] = carry;
+}
+__global__ void __launch_bounds__(SK_SCAN_TPB) k_scan_apply(uint64_t n, uint32_t *__restrict__ v,
+                                                            const uint32_t *__restrict__ sums) {
+    __shared__ uint32_t wsum[SK_SCAN_TPB / 64];
+    const uint64_t base = uint64_t(blockIdx.x) * SK_SCAN_ITEMS + uint64_t(threadIdx.x) * SK_SCAN_PER;
+    uint32_t x[SK_SCAN_PER], s = 0;
+#pragma unroll
+    for (int q = 0; q < SK_SCAN_PER; q++) {
+        x[q] = base + q < n ? v[base + q] : 0u;
+        s += x[q];
+    }
+    uint32_t tot;
+    uint32_t ex = sums[blockIdx.x] + block_exscan<SK_SCAN_TPB>(s, wsum, &tot);
+#pragma unroll
+    for (int q = 0; q < SK_SCAN_PER; q++) {
+        if (base + q < n) v[base + q] = ex;
+        ex += x[q];
+    }
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) v[n] = sums[gridDim.x];
+}
+
+// push u onto the u16 chain head h[i] (an LDS exchange on the 32-bit word holding it); returns the old head
+__device__ __forceinline__ uint16_t pfl_push(uint16_t *h, uint32_t i, uint32_t u) {
+    uint32_t *w = reinterpret_cast<uint32_t *>(h) + (i >> 1);
+    const uint32_t sh = (i & 1u) * 16u;
+    uint32_t old = *w, assumed;
+    do {
+        assumed = old;
+        old = atomicCAS(w, assumed, (assumed & ~(0xffffu << sh)) | (u << sh));
+    } while (old != assumed);
+    return uint16_t(old >> sh);
+}
+
+// one chunk of records R[0..cnt) (every record of its registers with a smaller seq is in this chunk or was
+// applied to `reg` before): chains per register, sequential replies, final register values into `reg` (LDS).
+// Caller syncs before (R loaded, heads cleared) and after; `fill` runs between the chain build and the walk (the
+// caller's register lines, loaded into registers before, go to LDS while the chains are built).
+template <class Fill>
+__device__ __forceinline__ void pfl_chunk(const uint64_t *R, uint32_t cnt, uint16_t *nxt, uint16_t *head,
+                                          uint8_t *fin, uint8_t *reg, uint8_t *dirty, uint8_t *__restrict__ changed,
+                                          int probe, Fill fill) {
+    for (uint32_t u = threadIdx.x; u < cnt; u += SK_PFL_ATPB)
+        nxt[u] = pfl_push(head, pfl_ht(R[u] >> 32), u);
+    fill();
+    __syncthreads();
+    for (uint32_t u = threadIdx.x; u < cnt; u += SK_PFL_ATPB) {
+        const uint64_t rt = R[u], key = rt >> 32, seq = rt & 0x3ffffffu;
+        const uint32_t rho = uint32_t(rt >> 26) & 63u;
+        uint32_t p = 0, m = rho;
+        bool earliest = true;
+        for (uint32_t w = head[pfl_ht(key)]; w != 0xffffu; w = nxt[w]) {
+            const uint64_t rw = R[w];
+            if ((rw >> 32) != key) continue;
+            const uint32_t rhow = uint32_t(rw >> 26) & 63u;
+            m = rhow > m ? rhow : m;
+            if ((rw & 0x3ffffffu) < seq) {
+                p = rhow > p ? rhow : p;
+                earliest = false;
+            }
+        }
+        const uint32_t slotb = uint32_t(key >> 14) << 7 | (uint32_t(key) & 127u);
+        const uint32_t R0 = reg[slotb];
+        if (probe & 2) changed[blockIdx.x & 1023] |= rho > (R0 > p ? R0 : p); else
+        changed[seq] = rho > (R0 > p ? R0 : p);
+        fin[u] = earliest && m > R0 ? uint8_t(m) : uint8_t(0);
+    }
+    __syncthreads();
+    for (uint32_t u = threadIdx.x; u < cnt; u += SK_PFL_ATPB)
+        if (fin[u]) {
+            const uint64_t key = R[u] >> 32;
+            reg[uint32_t(key >> 14) << 7 | (uint32_t(key) & 127u)] = fin[u];
+            dirty[uint32_t(key >> 14)] = 1;
+        }
+}
+
+__global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const uint64_t *__restrict__ rec2,
+                                                           const uint32_t *__restrict__ C, uint32_t ntile,
+                                                           uint32_t nsub, uint32_t nslab, uint8_t *arena,
+                                                           uint8_t *__restrict__ changed, uint32_t *big_alloc,
+                                                           uint64_t *big_keys, uint32_t *big_vals, int probe) {
+    constexpr uint32_t NL = 1u << SK_PFL_SH;
+    constexpr uint32_t kWork = SK_PFL_CAP * 8 + SK_PFL_CAP * 2 + SK_PFL_HT * 2 + SK_PFL_CAP;
+    constexpr uint32_t kBigL = 1024;       // LDS slots of the big-run table
+    static_assert(kWork >= kBigL * 12, "the big-run table shares the chunk LDS");
+    __shared__ uint4 regs4[NL * 8];            // line of sketch slab0 + i at reg[i * 128]
+    __shared__ uint64_t work[(kWork + 7) / 8]; // chunk records, chains, final values (or the big-run table)
+    __shared__ uint8_t dirty[NL];
+    uint8_t *reg = reinterpret_cast<uint8_t *>(regs4);
+    uint64_t *R = work;
+    uint16_t *nxt = reinterpret_cast<uint16_t *>(R + SK_PFL_CAP);
+    uint16_t *head = nxt + SK_PFL_CAP;
+    uint8_t *fin = reinterpret_cast<uint8_t *>(head + SK_PFL_HT);
+
+    const uint32_t f = blockIdx.x, b = f / nsub, sub = f % nsub;
+    const uint64_t c0 = uint64_t(f) * ntile;
+    const uint32_t start = C[c0], end = C[c0 + ntile], cnt = end - start;
+    if (cnt == 0) return; // uniform
+    const uint32_t slab0 = sub << SK_PFL_SH, nsl = nslab - slab0 < NL ? nslab - slab0 : NL;
+    auto line = [&](uint32_t i) -> uint4 * {
+        const uint32_t s = slab0 + i;
+        if (probe & 1) return reinterpret_cast<uint4 *>(arena + (((uint64_t(f) << SK_PFL_SH) + i) % (uint64_t(nslab) * 128)) * 128); // timing probe
+        return reinterpret_cast<uint4 *>(arena + (uint64_t(s) << 14) + (((b - pfl_rot(s)) & 127u) << 7));
+    };
+    for (uint32_t i = threadIdx.x; i < NL; i += SK_PFL_ATPB) dirty[i] = 0;
+    for (uint32_t t = threadIdx.x; t < SK_PFL_HT; t += SK_PFL_ATPB) head[t] = 0xffffu;
+    __syncthreads();
+    if (cnt <= SK_PFL_CAP) { // the whole fine bucket is one chunk: records and lines in one round trip
+        constexpr int LQ = (NL * 8 + SK_PFL_ATPB - 1) / SK_PFL_ATPB;
+        uint4 lv[LQ];
+#pragma unroll
+        for (int j = 0; j < LQ; j++) {
+            const uint32_t q = threadIdx.x + j * SK_PFL_ATPB;
+            if (q < nsl * 8) lv[j] = (probe & 4) ? make_uint4(0, 0, 0, 0) : line(q >> 3)[q & 7];
+        }
+        for (uint32_t u = threadIdx.x; u < cnt; u += SK_PFL_ATPB) R[u] = rec2[start + u];
+        __syncthreads();
+        pfl_chunk(R, cnt, nxt, head, fin, reg, dirty, changed, probe, [&] {
+#pragma unroll
+            for (int j = 0; j < LQ; j++) {
+                const uint32_t q = threadIdx.x + j * SK_PFL_ATPB;
+                if (q < nsl * 8) regs4[q] = lv[j];
+            }
+        });
+    } else {
+        for (uint32_t q = threadIdx.x; q < nsl * 8; q += SK_PFL_ATPB) regs4[q] = line(q >> 3)[q & 7];
+        __syncthreads();
+        uint32_t t0 = 0;
+        while (t0 < ntile) { // uniform: chunks of whole runs, in tile (= batch) order
+            const uint32_t a = C[c0 + t0];
+            uint32_t t1 = t0 + 1;
+            while (t1 < ntile && C[c0 + t1 + 1] - a <= SK_PFL_CAP) t1++;
+            const uint32_t z = C[c0 + t1], k = z - a;
+            if (k <= SK_PFL_CAP) {
+                for (uint32_t u = threadIdx.x; u < k; u += SK_PFL_ATPB) R[u] = rec2[a + u];
+                __syncthreads();
+                pfl_chunk(R, k, nxt, head, fin, reg, dirty, changed, 0, [] {});
+            } else { // one run larger than a chunk (t1 == t0 + 1): (slot, rho) -> min seq table
+                __shared__ uint32_t gbase;
+                unsigned long long *lk = reinterpret_cast<unsigned long long *>(work);
+                uint32_t *lv = reinterpret_cast<uint32_t *>(lk + kBigL);
+                if (threadIdx.x == 0) gbase = atomicAdd(big_alloc, 2 * k);
+                for (uint32_t s = threadIdx.x; s < kBigL; s += SK_PFL_ATPB) lk[s] = SK_BIG_EMPTY, lv[s] = 0xffffffffu;
+                __syncthreads();
+                BigTable T{lk, lv, reinterpret_cast<unsigned long long *>(big_keys) + gbase, big_vals + gbase, 2 * k,
+                           kBigL};
+                for (uint32_t s = threadIdx.x; s < T.S; s += SK_PFL_ATPB) T.gk[s] = SK_BIG_EMPTY, T.gv[s] = 0xffffffffu;
+                __threadfence();
+                __syncthreads();
+                for (uint32_t u = threadIdx.x; u < k; u += SK_PFL_ATPB) {
+                    const uint64_t r = rec2[a + u];
+                    T.insert(((r >> 32) << 6) | ((r >> 26) & 63u), uint32_t(r & 0x3ffffffu));
+                }
+                __threadfence();
+                __syncthreads();
+                for (uint32_t u = threadIdx.x; u < k; u += SK_PFL_ATPB) { // replies (registers only read)
+                    const uint64_t r = rec2[a + u], key = r >> 32;
+                    const uint32_t rho = uint32_t(r >> 26) & 63u, seq = uint32_t(r & 0x3ffffffu);
+                    bool first = rho > reg[uint32_t(key >> 14) << 7 | (uint32_t(key) & 127u)];
+                    for (uint32_t v = rho; v < 52 && first; v++) first = T.find((key << 6) | v) >= seq;
+                    changed[seq] = first ? 1 : 0;
+                }
+                __syncthreads();
+                for (uint32_t u = threadIdx.x; u < k; u += SK_PFL_ATPB) { // the register's writer: its top record
+                    const uint64_t r = rec2[a + u], key = r >> 32;
+                    const uint32_t rho = uint32_t(r >> 26) & 63u, seq = uint32_t(r & 0x3ffffffu);
+                    if (T.find((key << 6) | rho) != seq) continue;
+                    bool top = true;
+                    for (uint32_t v = rho + 1; v < 52 && top; v++) top = T.find((key << 6) | v) == 0xffffffffu;
+                    const uint32_t slotb = uint32_t(key >> 14) << 7 | (uint32_t(key) & 127u);
+                    if (top && rho > reg[slotb]) {
+                        reg[slotb] = uint8_t(rho);
+                        dirty[uint32_t(key >> 14)] = 1;
+                    }
+                }
+            }
+            __syncthreads();
+            for (uint32_t t = threadIdx.x; t < SK_PFL_HT; t += SK_PFL_ATPB) head[t] = 0xffffu;
+            __syncthreads();
+            t0 = t1;
+        }
+    }
+    __syncthreads();
+    if (probe & 4) return;
+    for (uint32_t q = threadIdx.x; q < nsl * 8; q += SK_PFL_ATPB)
+        if (dirty[q >> 3]) line(q >> 3)[q & 7] = regs4[q];
 }
 
 // streamed-once 16-B load with the nontemporal hint (native vector type for the builtin)
@@ -2070,6 +2402,60 @@ hipError_t launch_pfp_apply(hipStream_t st, uint64_t n, const uint64_t *chunks, 
 hipError_t launch_pfp_reply(hipStream_t st, uint64_t n, const uint8_t *rep, const uint16_t *pos,
                             const uint32_t *cmd_of, uint8_t *changed) {
     hipLaunchKernelGGL(k_pfp_reply, dim3(pfp_blocks(n)), dim3(SK_PFP_TPB), 0, st, n, rep, pos, cmd_of, changed);
+    SK_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+// line schedule: layout of one call's scratch (PflDims) and its five stages
+PflDims pfl_dims(uint64_t n, uint32_t nslab, uint32_t tile_blocks) {
+    PflDims d;
+    d.nblk = pfp_blocks(n);
+    d.tb = tile_blocks ? tile_blocks : SK_PFL_TILE;
+    d.ntile = (d.nblk + d.tb - 1) / d.tb;
+    d.nsub = (nslab + (1u << SK_PFL_SH) - 1) >> SK_PFL_SH;
+    d.nf = uint64_t(SK_PFL_NB) * d.nsub;
+    d.ncount = d.nf * d.ntile;
+    d.nsums = uint32_t((d.ncount + SK_SCAN_ITEMS - 1) / SK_SCAN_ITEMS);
+    d.chunk_bytes = uint64_t(d.nblk) * SK_PFP_EPB * 8;
+    d.S_bytes = uint64_t(SK_PFL_NB + 1) * d.nblk * 4;
+    return d;
+}
+uint32_t pfl_max_slabs() { return SK_PFL_MAXSUB << SK_PFL_SH; }
+
+hipError_t launch_pfl_hash(hipStream_t st, uint64_t n, const uint32_t *key_ids, const uint64_t *off,
+                           const uint8_t *bytes, int v5, uint64_t *chunks, uint32_t *S, uint32_t *big_alloc) {
+    uint32_t nb = pfp_blocks(n);
+    hipLaunchKernelGGL(k_pfl_hash, dim3(nb), dim3(SK_PFP_TPB), 0, st, n, key_ids, off, bytes, v5, chunks, S, nb,
+                       big_alloc);
+    SK_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+hipError_t launch_pfl_part(hipStream_t st, const PflDims &d, const uint64_t *chunks, const uint32_t *S, uint32_t *C,
+                           uint32_t *sums, uint64_t *rec2) {
+    if (d.nsub > SK_PFL_MAXSUB || d.ncount >= (1ull << 32)) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_pfl_count, dim3(d.ntile * SK_PFL_NB), dim3(SK_PFL_BTPB), 0, st, chunks, S, d.nblk, d.tb,
+                       d.ntile,
+                       d.nsub, C);
+    SK_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_scan_reduce, dim3(d.nsums), dim3(SK_SCAN_TPB), 0, st, d.ncount, C, sums);
+    SK_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(SK_SCAN_TPB), 0, st, d.nsums, sums);
+    SK_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_scan_apply, dim3(d.nsums), dim3(SK_SCAN_TPB), 0, st, d.ncount, C, sums);
+    SK_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_pfl_scatter, dim3(d.ntile * SK_PFL_NB), dim3(SK_PFL_BTPB), 0, st, chunks, S, d.nblk, d.tb,
+                       d.ntile,
+                       d.nsub, C, rec2);
+    SK_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+hipError_t launch_pfl_apply(hipStream_t st, const PflDims &d, const uint64_t *rec2, const uint32_t *C, uint32_t nslab,
+                            uint8_t *arena, uint8_t *changed, uint32_t *big_alloc, uint64_t *big_keys,
+                            uint32_t *big_vals) {
+    hipLaunchKernelGGL(k_pfl_apply, dim3(uint32_t(d.nf)), dim3(SK_PFL_ATPB), 0, st, rec2, C, d.ntile, d.nsub, nslab,
+                       arena, changed, big_alloc, big_keys, big_vals, getenv("SK_PFL_PROBE") ? atoi(getenv("SK_PFL_PROBE")) : 0);
     SK_LAUNCH_CHECK();
     return hipSuccess;
 }

@@ -284,6 +284,11 @@ struct sk_ctx {
     uint64_t bloom_ra_min = 1;  // add batches >= this use the region schedule (SK_BLOOM_RA_MIN, 0 = never: sort path)
     DBuf ra_S, ra_rec, ra_flag;
     uint64_t bloom_rc_min = 2u << 20; // contains batches >= this use the region schedule (SK_BLOOM_RC_MIN, 0 = never)
+    // PFADD line schedule (sketch-major group apply with the registers in LDS) for device batches of at least
+    // pfl_min one-element commands (SK_PFL_MIN, 0 = never): scratch of one call
+    uint64_t pfl_min = 4u << 20;
+    uint32_t pfl_tile = 0;      // hash blocks per run tile (SK_PFL_TILE, 0 = the kernel default)
+    DBuf pfl_chunks, pfl_S, pfl_C, pfl_sums, pfl_rec, pfl_bk, pfl_bv, pfl_ovf;
 };
 
 namespace {
@@ -345,7 +350,8 @@ const char *kPhaseNames[] = {"pfadd_hash",  "pfadd_sort",   "pfadd_apply", "hll_
                              "bloom_contains", "bloom_probes", "bloom_sort", "bloom_apply", "setbit",
                              "getbit",      "bitcount",     "bitop",       "pfadd_claim", "pfadd_commit",
                              "pfp_hash",    "pfp_apply",    "pfp_reply",   "bloom_rc_hash", "bloom_rc_probe", "pfadd",
-                             "pfadd_long",  "bloom_ra_hash", "bloom_ra_apply"};
+                             "pfadd_long",  "bloom_ra_hash", "bloom_ra_apply", "pfl_hash",   "pfl_part",
+                             "pfl_apply"};
 constexpr int kNumPhases = sizeof(kPhaseNames) / sizeof(kPhaseNames[0]);
 
 hipEvent_t ev_get(sk_ctx *c) {
@@ -979,6 +985,38 @@ int pfadd_partition(sk_ctx *c, uint64_t n, const uint32_t *d_ids, const uint64_t
     return SK_OK;
 }
 
+// line schedule (sk_kernels.hip "PFADD, line schedule"): one element per command, n <= 2^26, every slab id
+// below hll_next <= sk::pfl_max_slabs().  Five launches on st, no host wait, exact replies for every input.
+bool pfadd_lines_ok(sk_ctx *c, uint64_t n) {
+    return c->pfl_min && n >= c->pfl_min && c->pfadd_path == 1 && !c->hll_exact && c->hll_next > 0 &&
+           c->hll_next <= sk::pfl_max_slabs();
+}
+int pfadd_lines(sk_ctx *c, uint64_t n, const uint32_t *d_ids, const uint64_t *d_off, const uint8_t *d_bytes,
+                uint8_t *d_changed) {
+    if (n > (1ull << 26)) return fail(c, SK_EINVAL, "PFADD line batch too large");
+    const uint32_t nslab = uint32_t(c->hll_next);
+    const sk::PflDims d = sk::pfl_dims(n, nslab, c->pfl_tile);
+    HIPCHK(c, c->pfl_chunks.ensure(d.chunk_bytes));
+    HIPCHK(c, c->pfl_S.ensure(d.S_bytes));
+    HIPCHK(c, c->pfl_C.ensure((d.ncount + 1) * 4));
+    HIPCHK(c, c->pfl_sums.ensure((uint64_t(d.nsums) + 1) * 4));
+    HIPCHK(c, c->pfl_rec.ensure(n * 8));
+    HIPCHK(c, c->pfl_bk.ensure(2 * n * 8));
+    HIPCHK(c, c->pfl_bv.ensure(2 * n * 4));
+    HIPCHK(c, c->pfl_ovf.ensure(64));
+    { Prof p_(c, 24);
+    HIPCHK(c, sk::launch_pfl_hash(c->st, n, d_ids, d_off, d_bytes, c->redis_major >= 5, c->pfl_chunks.as<uint64_t>(),
+                                  c->pfl_S.as<uint32_t>(), c->pfl_ovf.as<uint32_t>())); }
+    { Prof p_(c, 25);
+    HIPCHK(c, sk::launch_pfl_part(c->st, d, c->pfl_chunks.as<uint64_t>(), c->pfl_S.as<uint32_t>(),
+                                  c->pfl_C.as<uint32_t>(), c->pfl_sums.as<uint32_t>(), c->pfl_rec.as<uint64_t>())); }
+    { Prof p_(c, 26);
+    HIPCHK(c, sk::launch_pfl_apply(c->st, d, c->pfl_rec.as<uint64_t>(), c->pfl_C.as<uint32_t>(), nslab, c->arena,
+                                   d_changed, c->pfl_ovf.as<uint32_t>(), c->pfl_bk.as<uint64_t>(),
+                                   c->pfl_bv.as<uint32_t>())); }
+    return SK_OK;
+}
+
 int pfadd_device(sk_ctx *c, uint64_t n, const uint32_t *d_ids, const uint64_t *d_off, const uint8_t *d_bytes,
                  const uint32_t *d_cmd, uint64_t n_cmds, uint8_t *d_changed, uint64_t touched_keys,
                  const uint64_t *d_pre = nullptr) {
@@ -1127,6 +1165,8 @@ int sk_open(const sk_config *cfg, sk_ctx **out) {
     if (const char *e = getenv("SK_HLL_EXACT_STRINGS")) c->hll_exact = atoi(e) != 0;
     if (c->hll_exact) c->pfadd_path = 1;
     if (const char *e = getenv("SK_PFP_PIPE")) c->pfp_pipe = atoi(e) != 0;
+    if (const char *e = getenv("SK_PFL_MIN")) c->pfl_min = strtoull(e, nullptr, 10);
+    if (const char *e = getenv("SK_PFL_TILE")) c->pfl_tile = uint32_t(strtoul(e, nullptr, 10));
     uint64_t cap = (cfg && cfg->hll_capacity) ? cfg->hll_capacity : 1024;
     if (hll_grow(c, cap) != SK_OK || c->misc.ensure(4096) != hipSuccess ||
         hipMalloc(&c->d_zero, 16) != hipSuccess || hipMemsetAsync(c->d_zero, 0, 16, c->st) != hipSuccess ||
@@ -1162,7 +1202,9 @@ int sk_close(sk_ctx *c) {
     for (DBuf *b : {&c->keys_a, &c->keys_b, &c->vals_a, &c->vals_b, &c->sort_tmp, &c->in_off, &c->in_bytes,
                     &c->in_ids, &c->in_cmd, &c->out_u8, &c->misc, &c->partial, &c->hist, &c->uni, &c->ptrs,
                     &c->hist_a, &c->hist_b, &c->ovf, &c->bloom_h, &c->rc_S, &c->rc_rec, &c->long_h,
-                    &c->long_which, &c->long_plane, &c->long_flags, &c->ra_S, &c->ra_rec, &c->ra_flag, &c->ev, &c->ev_n})
+                    &c->long_which, &c->long_plane, &c->long_flags, &c->ra_S, &c->ra_rec, &c->ra_flag, &c->ev, &c->ev_n,
+                    &c->pfl_chunks, &c->pfl_S, &c->pfl_C, &c->pfl_sums, &c->pfl_rec, &c->pfl_bk, &c->pfl_bv,
+                    &c->pfl_ovf})
         b->release();
     for (auto &ps : c->pfs) {
         for (DBuf *b : {&ps.chunks, &ps.rep, &ps.S, &ps.big_k, &ps.big_v, &ps.ovf}) b->release();
@@ -1574,6 +1616,15 @@ int sk_pfadd_dev(sk_ctx *c, uint64_t n, const uint32_t *d_ids, const uint64_t *d
         explicit DevCall(sk_ctx *c_) : c(c_) { c->pf_dev_call = true; }
         ~DevCall() { c->pf_dev_call = false; }
     } dev_call(c);
+    if (pfadd_lines_ok(c, n)) { // group-committed RBatches: the line schedule, 2^26 elements per call
+        for (uint64_t s = 0; s < n; s += (1ull << 26)) {
+            uint64_t m = std::min<uint64_t>(1ull << 26, n - s);
+            Prof p_(c, 20);
+            int r = pfadd_lines(c, m, d_ids + s, d_off + s, d_bytes, d_changed + s);
+            if (r) return r;
+        }
+        return c->async_dev ? SK_OK : sync(c);
+    }
     for (uint64_t s = 0; s < n; s += max_cmds) {
         uint64_t m = std::min(max_cmds, n - s);
         uint64_t live = c->hll_next - c->hll_free.size(); // slabs in use bounds the touched sketches

@@ -2,9 +2,11 @@
 """bench.py -- HLL inserts/s + Bloom contains/s (whole node) on the MI355X sketch engine.
 
 One "step" = HB RBatch-sized PFADD batches (C2: 100k tenants, Jackson-encoded random Longs, one element per
-command, B = 1M commands each) + one Bloom contains batch of CB elements (C3: tryInit(425,000,000, 0.008) ->
-m = 4,271,038,538 bits, k = 7, filled with the config's 1B adds, 50 % members / 50 % fresh), inputs already
-resident in HBM.  Defaults: HB = 16, CB = 16M, so a step is 16M PFADD + 16M contains.
+command, B = 1M commands each), group-committed G at a time into one device call (default: all HB, which the
+engine applies with the line schedule), + one Bloom contains batch of CB elements (C3: tryInit(425,000,000,
+0.008) -> m = 4,271,038,538 bits, k = 7, filled with the config's 1B adds, 50 % members / 50 % fresh), inputs
+already resident in HBM.  Defaults: HB = 64, CB = 64M, so a step is 64M PFADD + 64M contains; every step's PFADD
+elements are fresh.
 value = (PFADD elements + contains elements) / wall time, all ranks.
 
 Multi-GPU (torch.distributed.run, one process per GPU): HLL keys are partitioned by calcSlot(key) % world (the
@@ -29,7 +31,8 @@ sys.path.insert(0, ROOT)
 
 from redisson_amd import SketchEngine, device_count, owner  # noqa: E402
 
-PROF_STEPS = 2          # steps in each per-kernel breakdown pass (outside the timed region)
+PROF_STEPS = 1          # steps in each per-kernel breakdown pass (outside the timed region)
+C_POOL = 4              # distinct contains batches, used in turn (contains is read-only: repeats change no work)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 # in-library event-timed phases (sk_prof_*): one kernel each, except the chains "pfadd" (every kernel of one
 # PFADD batch) and "bloom_contains" (every kernel of one contains call), and pfadd_sort (rocPRIM passes)
@@ -78,10 +81,10 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=1 << 20, help="commands per PFADD RBatch (C2: 1M)")
-    ap.add_argument("--hll-batches", type=int, default=16, help="PFADD RBatches per step")
+    ap.add_argument("--hll-batches", type=int, default=64, help="PFADD RBatches per step")
     ap.add_argument("--group", type=int, default=0,
                     help="RBatches group-committed per sk_pfadd_dev call (0 = all of a step's; 1 = one call each)")
-    ap.add_argument("--contains-batch", type=int, default=16 << 20, help="Bloom contains elements per step")
+    ap.add_argument("--contains-batch", type=int, default=64 << 20, help="Bloom contains elements per step")
     ap.add_argument("--tenants", type=int, default=100_000)
     ap.add_argument("--bloom-n", type=int, default=425_000_000)
     ap.add_argument("--bloom-p", type=float, default=0.008)
@@ -145,7 +148,7 @@ def main():
     # contains inputs: 50 % members (drawn from the fill), 50 % fresh
     c_in = []
     c_total = 0
-    for s in range(nsteps):
+    for s in range(min(nsteps, C_POOL)):
         member = rng.integers(0, max(fill, 1), CB, dtype=np.uint64)
         fresh = rng.integers(1 << 39, 1 << 40, CB, dtype=np.uint64) + np.uint64(rank << 40)
         idx = np.where(rng.random(CB) < 0.5, member, fresh)
@@ -155,7 +158,7 @@ def main():
         c_in.append((off, byt, tot))
         c_total += tot
     d_contains = eng.alloc(CB)
-    mean_len_b = c_total / (nsteps * CB)
+    mean_len_b = c_total / (len(c_in) * CB)
     log(f"[rank {rank}] setup: {len(mine)} tenants, bloom m={size} k={k} filled with {fill} "
         f"(adds {add_s:.2f}s), {nsteps} steps of {HB}x{B} PFADD + {CB} contains, {time.perf_counter() - t_setup:.0f}s")
 
@@ -163,7 +166,7 @@ def main():
         off, byt, tot, d_ids = h_in[s]
         for h in range(0, HB, G):
             eng.pfadd_dev(G * B, d_ids.ptr + h * B * 4, off.ptr + h * B * 8, byt, tot, d_changed)
-        off, byt, tot = c_in[s]
+        off, byt, tot = c_in[s % len(c_in)]
         eng.bloom_contains_dev(bloom, CB, off, byt, tot, d_contains)
 
     P = PROF_STEPS

@@ -898,6 +898,7 @@ __global__ void __launch_bounds__(SK_PFP_ATPB) __attribute__((amdgpu_waves_per_e
 #define SK_PFL_CAP 1024    // records per apply chunk
 #define SK_PFL_HT 1024     // chain heads per chunk
 #define SK_PFL_MAXSUB 8192 // fine buckets per coarse bucket (2^20 sketches)
+#define SK_PFL_TMAX 2048   // largest run tile (hash blocks)
 __device__ __forceinline__ uint32_t pfl_ht(uint64_t key) {
     return uint32_t((key * 0xC2B2AE3D27D4EB4Full) >> 54); // 10 bits
 }
@@ -935,29 +936,108 @@ __global__ void __launch_bounds__(SK_PFL_BTPB) k_pfl_count(const uint64_t *__res
         C[(uint64_t(b) * nsub + s) * ntile + tile] = hist[s];
 }
 
+// The tile's records are taken in pieces of SK_PFL_PIECE (through the prefix of its block segments), each piece
+// counting-sorted by fine bucket in LDS and stored as one contiguous piece per run: consecutive lanes store
+// consecutive words of a run, so a store instruction writes whole pieces of lines (one record per lane into
+// hundreds of runs made every store a partial-line write).  Dynamic LDS: 2 * nsub words.
+#define SK_PFL_PIECE 4096
 __global__ void __launch_bounds__(SK_PFL_BTPB) k_pfl_scatter(const uint64_t *__restrict__ chunks,
                                                              const uint32_t *__restrict__ S, uint32_t nblk,
                                                              uint32_t tb, uint32_t ntile, uint32_t nsub,
                                                              const uint32_t *__restrict__ C,
                                                              uint64_t *__restrict__ rec2) {
-    __shared__ uint32_t cur[SK_PFL_MAXSUB];
+    constexpr int PER = SK_PFL_PIECE / SK_PFL_BTPB;
+    extern __shared__ uint32_t dyn[];
+    __shared__ uint32_t segp[SK_PFL_TMAX + 1]; // prefix of the tile's segment lengths
+    __shared__ uint64_t sorted[SK_PFL_PIECE];
+    __shared__ uint32_t wsum[SK_PFL_BTPB / 64];
+    uint32_t *cur = dyn, *lcnt = dyn + nsub;
     uint32_t b, tile;
     pfl_bt(ntile, &b, &tile);
-    for (uint32_t s = threadIdx.x; s < nsub; s += SK_PFL_BTPB) cur[s] = C[(uint64_t(b) * nsub + s) * ntile + tile];
+    const uint32_t b0 = tile * tb, nb = (b0 + tb < nblk ? b0 + tb : nblk) - b0;
+    for (uint32_t x = threadIdx.x; x < nsub; x += SK_PFL_BTPB) {
+        cur[x] = C[(uint64_t(b) * nsub + x) * ntile + tile];
+        lcnt[x] = 0;
+    }
+    // segment prefix: tb <= SK_PFL_TMAX blocks, SK_PFL_TMAX / SK_PFL_BTPB per thread (consecutive)
+    constexpr int SP = SK_PFL_TMAX / SK_PFL_BTPB;
+    uint32_t sl[SP], ssum = 0;
+#pragma unroll
+    for (int q = 0; q < SP; q++) {
+        const uint32_t j = threadIdx.x * SP + q;
+        sl[q] = 0;
+        if (j < nb) sl[q] = S[uint64_t(b + 1) * nblk + b0 + j] - S[uint64_t(b) * nblk + b0 + j];
+        ssum += sl[q];
+    }
+    uint32_t total;
+    uint32_t ex = block_exscan<SK_PFL_BTPB>(ssum, wsum, &total);
+#pragma unroll
+    for (int q = 0; q < SP; q++) {
+        segp[threadIdx.x * SP + q] = ex;
+        ex += sl[q];
+    }
+    if (threadIdx.x == 0) segp[SK_PFL_TMAX] = total;
     __syncthreads();
-    const uint32_t b0 = tile * tb, b1 = b0 + tb < nblk ? b0 + tb : nblk;
-    for (uint32_t blk = b0 + (threadIdx.x >> 2); blk < b1; blk += SK_PFL_BTPB / 4) {
-        const uint32_t lo = S[uint64_t(b) * nblk + blk], hi = S[uint64_t(b + 1) * nblk + blk];
-        const uint64_t *seg = chunks + uint64_t(blk) * SK_PFP_EPB;
-        const uint64_t seq0 = uint64_t(blk) * SK_PFP_EPB;
-        for (uint32_t t = lo + (threadIdx.x & 3u); t < hi; t += 4) {
-            const uint64_t r = seg[t];
-            const uint32_t slab = uint32_t(r >> 32), reg = uint32_t(r >> 18) & 16383u, rho = uint32_t(r >> 12) & 63u;
-            if ((slab >> SK_PFL_SH) >= nsub) continue;
-            const uint32_t p = atomicAdd(&cur[slab >> SK_PFL_SH], 1u);
-            rec2[p] = (uint64_t(slab & ((1u << SK_PFL_SH) - 1)) << 46) | (uint64_t(reg) << 32) |
-                      (uint64_t(rho) << 26) | (seq0 + (r & 4095u));
+    for (uint32_t base = 0; base < total; base += SK_PFL_PIECE) { // uniform
+        const uint32_t m = total - base < SK_PFL_PIECE ? total - base : SK_PFL_PIECE;
+        uint64_t r[PER];
+        uint32_t rk[PER];
+#pragma unroll
+        for (int q = 0; q < PER; q++) {
+            const uint32_t i = threadIdx.x + q * SK_PFL_BTPB;
+            r[q] = ~0ull;
+            if (i >= m) continue;
+            const uint32_t x = base + i;
+            uint32_t lo = 0, hi = nb; // segp[lo] <= x < segp[hi]
+            while (hi - lo > 1) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (segp[mid] <= x) lo = mid;
+                else hi = mid;
+            }
+            const uint32_t blk = b0 + lo;
+            const uint64_t rr = chunks[uint64_t(blk) * SK_PFP_EPB + S[uint64_t(b) * nblk + blk] + (x - segp[lo])];
+            const uint32_t slab = uint32_t(rr >> 32), reg = uint32_t(rr >> 18) & 16383u, rho = uint32_t(rr >> 12) & 63u;
+            if ((slab >> SK_PFL_SH) >= nsub) continue; // ids beyond the store's slabs are dropped (both passes)
+            r[q] = (uint64_t(slab & ((1u << SK_PFL_SH) - 1)) << 46) | (uint64_t(reg) << 32) | (uint64_t(rho) << 26) |
+                   (uint64_t(blk) * SK_PFP_EPB + (rr & 4095u));
+            rk[q] = atomicAdd(&lcnt[slab >> SK_PFL_SH], 1u) | ((slab >> SK_PFL_SH) << 13);
         }
+        __syncthreads();
+        // exclusive scan of the piece's counts over the fine buckets (in place), nsub <= SK_PFL_MAXSUB
+        uint32_t acc = 0;
+        for (uint32_t x0 = 0; x0 < nsub; x0 += SK_PFL_BTPB) {
+            const uint32_t x = x0 + threadIdx.x, v = x < nsub ? lcnt[x] : 0u;
+            uint32_t tot;
+            const uint32_t e = block_exscan<SK_PFL_BTPB>(v, wsum, &tot);
+            if (x < nsub) lcnt[x] = acc + e;
+            acc += tot;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < PER; q++)
+            if (r[q] != ~0ull) sorted[lcnt[rk[q] >> 13] + (rk[q] & 8191u)] = r[q];
+        __syncthreads();
+        const uint32_t kept = acc; // records of the piece that have a fine bucket
+        for (uint32_t i = threadIdx.x; i < kept; i += SK_PFL_BTPB) {
+            const uint64_t rr = sorted[i];
+            // fine bucket of sorted[i]: the record's sketch, relative to this coarse bucket's sub range
+            uint32_t lo = 0, hi = nsub; // lcnt[lo] <= i < lcnt[hi] (lcnt[nsub] = kept)
+            while (hi - lo > 1) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (lcnt[mid] <= i) lo = mid;
+                else hi = mid;
+            }
+            rec2[cur[lo] + (i - lcnt[lo])] = rr;
+        }
+        __syncthreads();
+        // advance the runs' cursors by the piece's counts, clear the counts
+        for (uint32_t x = threadIdx.x; x < nsub; x += SK_PFL_BTPB) {
+            const uint32_t nx = (x + 1 < nsub ? lcnt[x + 1] : kept) - lcnt[x];
+            cur[x] += nx;
+        }
+        __syncthreads();
+        for (uint32_t x = threadIdx.x; x < nsub; x += SK_PFL_BTPB) lcnt[x] = 0;
+        __syncthreads();
     }
 }
 
@@ -2433,7 +2513,7 @@ hipError_t launch_pfl_hash(hipStream_t st, uint64_t n, const uint32_t *key_ids, 
 
 hipError_t launch_pfl_part(hipStream_t st, const PflDims &d, const uint64_t *chunks, const uint32_t *S, uint32_t *C,
                            uint32_t *sums, uint64_t *rec2) {
-    if (d.nsub > SK_PFL_MAXSUB || d.ncount >= (1ull << 32)) return hipErrorInvalidValue;
+    if (d.nsub > SK_PFL_MAXSUB || d.tb > SK_PFL_TMAX || d.ncount >= (1ull << 32)) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_pfl_count, dim3(d.ntile * SK_PFL_NB), dim3(SK_PFL_BTPB), 0, st, chunks, S, d.nblk, d.tb,
                        d.ntile,
                        d.nsub, C);
@@ -2444,7 +2524,8 @@ hipError_t launch_pfl_part(hipStream_t st, const PflDims &d, const uint64_t *chu
     SK_LAUNCH_CHECK();
     hipLaunchKernelGGL(k_scan_apply, dim3(d.nsums), dim3(SK_SCAN_TPB), 0, st, d.ncount, C, sums);
     SK_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_pfl_scatter, dim3(d.ntile * SK_PFL_NB), dim3(SK_PFL_BTPB), 0, st, chunks, S, d.nblk, d.tb,
+    hipLaunchKernelGGL(k_pfl_scatter, dim3(d.ntile * SK_PFL_NB), dim3(SK_PFL_BTPB), 2 * d.nsub * 4, st, chunks, S,
+                       d.nblk, d.tb,
                        d.ntile,
                        d.nsub, C, rec2);
     SK_LAUNCH_CHECK();

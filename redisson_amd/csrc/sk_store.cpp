@@ -1021,6 +1021,13 @@ int pfadd_device(sk_ctx *c, uint64_t n, const uint32_t *d_ids, const uint64_t *d
                  const uint32_t *d_cmd, uint64_t n_cmds, uint8_t *d_changed, uint64_t touched_keys,
                  const uint64_t *d_pre = nullptr) {
     if (!n) return SK_OK;
+    if (d_cmd == nullptr && d_pre == nullptr && pfadd_lines_ok(c, n)) { // large one-element batch: line schedule
+        for (uint64_t s = 0; s < n; s += (1ull << 26)) {
+            int r = pfadd_lines(c, std::min<uint64_t>(1ull << 26, n - s), d_ids + s, d_off + s, d_bytes, d_changed + s);
+            if (r) return r;
+        }
+        return SK_OK;
+    }
     if (c->pfadd_path == 1) { // partition path, 1M elements per launch
         for (uint64_t s = 0; s < n; s += (1ull << 20)) {
             if (c->pf_pending) {

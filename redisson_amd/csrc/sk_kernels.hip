@@ -917,7 +917,7 @@ __device__ __forceinline__ void pfl_bt(uint32_t ntile, uint32_t *b, uint32_t *ti
 __global__ void __launch_bounds__(SK_PFL_BTPB) k_pfl_count(const uint64_t *__restrict__ chunks,
                                                            const uint32_t *__restrict__ S, uint32_t nblk, uint32_t tb,
                                                            uint32_t ntile, uint32_t nsub, uint32_t *__restrict__ C) {
-    __shared__ uint32_t hist[SK_PFL_MAXSUB];
+    extern __shared__ uint32_t hist[]; // nsub words
     for (uint32_t s = threadIdx.x; s < nsub; s += SK_PFL_BTPB) hist[s] = 0;
     __syncthreads();
     uint32_t b, tile;
@@ -2514,7 +2514,8 @@ hipError_t launch_pfl_hash(hipStream_t st, uint64_t n, const uint32_t *key_ids, 
 hipError_t launch_pfl_part(hipStream_t st, const PflDims &d, const uint64_t *chunks, const uint32_t *S, uint32_t *C,
                            uint32_t *sums, uint64_t *rec2) {
     if (d.nsub > SK_PFL_MAXSUB || d.tb > SK_PFL_TMAX || d.ncount >= (1ull << 32)) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_pfl_count, dim3(d.ntile * SK_PFL_NB), dim3(SK_PFL_BTPB), 0, st, chunks, S, d.nblk, d.tb,
+    hipLaunchKernelGGL(k_pfl_count, dim3(d.ntile * SK_PFL_NB), dim3(SK_PFL_BTPB), d.nsub * 4, st, chunks, S, d.nblk,
+                       d.tb,
                        d.ntile,
                        d.nsub, C);
     SK_LAUNCH_CHECK();

@@ -249,8 +249,10 @@ def main():
     # SURVEY 8(d) per-unit bytes of each chain (53 B per PFADD element at C2; len + 9 + 64(k-1) per contains)
     s8 = {"pfadd": mean_len_h + 12 + 2.5, "bloom_contains": mean_len_b + 8 + 1 + 64 * (k - 1)}
     achieved = s8[dom] * upl[dom] / (avg_ms * 1e-3) / 1e9
-    tr_parts = [pmc_traffic(p_) for p_ in chain_kernels[dom]]
-    traffic = sum(tr_parts) if tr_parts and all(t is not None for t in tr_parts) else None
+    # PMC bytes per dispatch x dispatches of each kernel per launch of the chain (a 64 M contains call is two
+    # 32 M pieces)
+    tr_parts = [(pmc_traffic(p_), iso[p_][0] / iso[dom][0]) for p_ in chain_kernels[dom] if p_ in iso]
+    traffic = sum(t * f for t, f in tr_parts) if tr_parts and all(t is not None for t, _ in tr_parts) else None
 
     kernels = {}
     for p_, (lps, ms) in iso.items():
@@ -317,8 +319,8 @@ def main():
                      "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "traffic_GBps": traffic / (avg_ms * 1e-3) / 1e9 if traffic else None,
-                     "traffic_source": "profiles/*_pmc_summary.json: 2 x FETCH_SIZE (gfx950) + WRITE_SIZE per launch, "
-                                       "summed over the chain's kernels",
+                     "traffic_source": "newest profiles/*_pmc_summary.json: 2 x FETCH_SIZE (gfx950) + WRITE_SIZE per "
+                                       "dispatch, times dispatches per chain launch, summed over the chain's kernels",
                      "bytes_per_unit": s8[dom], "bytes_per_unit_source": "SURVEY 8(d)",
                      "units_per_launch": upl[dom], "avg_launch_ms": avg_ms, "launches_timed": n_launch,
                      "kernel_ms_isolated": {p_: iso[p_][1] for p_ in chain_kernels[dom] if p_ in iso},
@@ -374,15 +376,17 @@ def pmc_traffic(phase):
 
     kern = {"bloom_contains": "sk::k_bloom_contains", "pfadd_claim": "sk::k_pfadd_claim",
             "pfadd_commit": "sk::k_pfadd_commit", "pfp_hash": "sk::k_pfp_hash", "pfp_apply": "sk::k_pfp_apply",
-            "pfp_reply": "sk::k_pfp_reply", "bloom_rc_hash": "sk::k_bloom_rc_hash", "pfl_hash": "sk::k_pfl_hash",
-            "pfl_apply": "sk::k_pfl_apply",
+            "pfp_reply": "sk::k_pfp_reply", "bloom_rc_hash": "sk::k_bloom_rc_hash<false>", "pfl_hash": "sk::k_pfl_hash",
+            "pfl_apply": "sk::k_pfl_apply", "pfl_part": "sk::k_pfl_count+sk::k_pfl_scatter+sk::k_scan_reduce+"
+                                                      "sk::k_scan_sums+sk::k_scan_apply",
             "bloom_rc_probe": "sk::k_bloom_rc_probe"}.get(phase)
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_summary.json")))
     if not kern or not files:
         return None
     try:
-        d = json.load(open(files[-1]))["kernels"].get(kern)
-        return d["traffic_bytes_per_launch"] if d else None
+        ks = json.load(open(files[-1]))["kernels"]
+        parts = [ks.get(k_) for k_ in kern.split("+")]   # a phase of several launches: their sum
+        return sum(d["traffic_bytes_per_launch"] for d in parts) if all(parts) else None
     except (OSError, ValueError, KeyError):
         return None
 

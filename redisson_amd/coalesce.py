@@ -143,3 +143,127 @@ class BloomCoalescer:
                 self.log.append((head.kind, [(r.elems, r.future) for r in run]))
         self.calls += 1
         self.requests += len(run)
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# Group commit of concurrent RBatch executions (the C2 ingestion shape: many clients each executing an RBatch of
+# PFADDs).  The reference sends every RBatch as its own pipeline (M:command/CommandBatchService.java:184-293) and
+# redis-server applies the batches one after another.  Here a completion thread drains every queued batch in
+# FIFO order and merges each maximal sequence of PFADD-only batches into ONE sk_pfadd call, so a device call
+# carries tens of millions of commands and the engine applies them with its line schedule (registers streamed once
+# per call, not once per element).  The concatenation keeps FIFO order, and PFADD replies depend only on order, so
+# every batch gets exactly the replies it would get if the batches had run one after another in that order.
+# A batch with any other command runs on its own, in its place in the FIFO order.
+
+class _BatchReq:
+    __slots__ = ("batch", "future")
+
+    def __init__(self, batch):
+        self.batch = batch
+        self.future = WaitFuture()
+
+    def pfadd_only(self) -> bool:
+        return all(c[0][0] == "PFADD" and c[1] is None for c in self.batch._cmds)
+
+
+class BatchCoalescer:
+    """One completion thread per client; `submit(batch)` enqueues an RBatch and returns the future of its result
+    list (or its error, as RBatch.execute would raise it)."""
+
+    def __init__(self, client, max_cmds: int = 1 << 26):
+        self.client = client
+        self.engine = client.engine
+        self.max_cmds = max_cmds
+        self._q: collections.deque = collections.deque()
+        self._cv = threading.Condition()
+        self._stop = False
+        self._held = 0
+        self.calls = 0       # engine PFADD calls made for merged groups
+        self.batches = 0     # batches completed
+        self._t = threading.Thread(target=self._loop, name="sk-batch-coalescer", daemon=True)
+        self._t.start()
+
+    def submit(self, batch) -> WaitFuture:
+        r = _BatchReq(batch)
+        with self._cv:
+            if self._stop:
+                raise RuntimeError("coalescer closed")
+            self._q.append(r)
+            self._cv.notify()
+        return r.future
+
+    hold = BloomCoalescer.hold
+
+    def close(self):
+        with self._cv:
+            self._stop = True
+            self._cv.notify()
+        self._t.join()
+
+    def _take(self) -> List[_BatchReq]:
+        head = self._q.popleft()
+        group = [head]
+        if head.pfadd_only():
+            n = len(head.batch._cmds)
+            while self._q and self._q[0].pfadd_only() and n + len(self._q[0].batch._cmds) <= self.max_cmds:
+                r = self._q.popleft()
+                group.append(r)
+                n += len(r.batch._cmds)
+        return group
+
+    def _loop(self):
+        while True:
+            with self._cv:
+                while not self._stop and (not self._q or self._held):
+                    self._cv.wait()
+                if not self._q:
+                    return
+                group = self._take()
+            if len(group) == 1 and not group[0].pfadd_only():
+                self._run_one(group[0])
+            else:
+                self._run_pfadd(group)
+            self.batches += len(group)
+
+    def _run_one(self, r: _BatchReq):
+        try:
+            r.future._set(r.batch._execute_now())
+        except Exception as e:  # noqa: BLE001 - the batch's own error, as execute() raises it
+            r.future._fail(e)
+
+    def _run_pfadd(self, group: List[_BatchReq]):
+        from .engine import RedisException
+
+        cmds = [c for r in group for c in r.batch._cmds]
+        keys = [c[0][1] for c in cmds]
+        st, out, msg = self.engine.pfadd_status(keys, [c[0][2] for c in cmds])
+        self.calls += 1
+        bad = set()
+        if st != 0:
+            # a command on a key of another type failed alone (the others were applied, pipeline semantics):
+            # those keys are still not HLLs after the call; any other error fails every command of the group
+            from . import _native as N
+
+            if st in (N.SK_EWRONGTYPE, N.SK_ECORRUPT):
+                bad = {k for k in set(keys) if self.engine.key_type(k) != N.SK_TYPE_HLL}
+            else:
+                bad = set(keys)
+        p = 0
+        for r in group:
+            r.batch._executed = True
+            err, res = None, []
+            for (c, fn, post, f) in r.batch._cmds:
+                if c[1] in bad:
+                    e = RedisException(msg)
+                    f._fail(e)
+                    err = e
+                    res.append(None)
+                else:
+                    v = bool(out[p])
+                    f._set(post(v) if post else v)
+                    res.append(f._value)
+                p += 1
+            if err is not None:
+                r.future._fail(err)
+            else:
+                r.future._set(res)

@@ -1091,28 +1091,16 @@ __global__ void __launch_bounds__(SK_SCAN_TPB) k_scan_apply(uint64_t n, uint32_t
     if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) v[n] = sums[gridDim.x];
 }
 
-// push u onto the u16 chain head h[i] (an LDS exchange on the 32-bit word holding it); returns the old head
-__device__ __forceinline__ uint16_t pfl_push(uint16_t *h, uint32_t i, uint32_t u) {
-    uint32_t *w = reinterpret_cast<uint32_t *>(h) + (i >> 1);
-    const uint32_t sh = (i & 1u) * 16u;
-    uint32_t old = *w, assumed;
-    do {
-        assumed = old;
-        old = atomicCAS(w, assumed, (assumed & ~(0xffffu << sh)) | (u << sh));
-    } while (old != assumed);
-    return uint16_t(old >> sh);
-}
-
 // one chunk of records R[0..cnt) (every record of its registers with a smaller seq is in this chunk or was
 // applied to `reg` before): chains per register, sequential replies, final register values into `reg` (LDS).
 // Caller syncs before (R loaded, heads cleared) and after; `fill` runs between the chain build and the walk (the
 // caller's register lines, loaded into registers before, go to LDS while the chains are built).
 template <class Fill>
-__device__ __forceinline__ void pfl_chunk(const uint64_t *R, uint32_t cnt, uint16_t *nxt, uint16_t *head,
+__device__ __forceinline__ void pfl_chunk(const uint64_t *R, uint32_t cnt, uint16_t *nxt, uint32_t *head,
                                           uint8_t *fin, uint8_t *reg, uint8_t *dirty, uint8_t *__restrict__ changed,
                                           int probe, Fill fill) {
     for (uint32_t u = threadIdx.x; u < cnt; u += SK_PFL_ATPB)
-        nxt[u] = pfl_push(head, pfl_ht(R[u] >> 32), u);
+        nxt[u] = uint16_t(atomicExch(&head[pfl_ht(R[u] >> 32)], u));
     fill();
     __syncthreads();
     for (uint32_t u = threadIdx.x; u < cnt; u += SK_PFL_ATPB) {
@@ -1132,8 +1120,9 @@ __device__ __forceinline__ void pfl_chunk(const uint64_t *R, uint32_t cnt, uint1
         }
         const uint32_t slotb = uint32_t(key >> 14) << 7 | (uint32_t(key) & 127u);
         const uint32_t R0 = reg[slotb];
-        if (probe & 2) changed[blockIdx.x & 1023] |= rho > (R0 > p ? R0 : p); else
-        changed[seq] = rho > (R0 > p ? R0 : p);
+        const uint8_t rep = rho > (R0 > p ? R0 : p);
+        if (probe & 8) __builtin_nontemporal_store(rep, changed + seq);
+        else changed[seq] = rep;
         fin[u] = earliest && m > R0 ? uint8_t(m) : uint8_t(0);
     }
     __syncthreads();
@@ -1151,7 +1140,7 @@ __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const uint64_t *__res
                                                            uint8_t *__restrict__ changed, uint32_t *big_alloc,
                                                            uint64_t *big_keys, uint32_t *big_vals, int probe) {
     constexpr uint32_t NL = 1u << SK_PFL_SH;
-    constexpr uint32_t kWork = SK_PFL_CAP * 8 + SK_PFL_CAP * 2 + SK_PFL_HT * 2 + SK_PFL_CAP;
+    constexpr uint32_t kWork = SK_PFL_CAP * 8 + SK_PFL_CAP * 2 + SK_PFL_HT * 4 + SK_PFL_CAP;
     constexpr uint32_t kBigL = 1024;       // LDS slots of the big-run table
     static_assert(kWork >= kBigL * 12, "the big-run table shares the chunk LDS");
     __shared__ uint4 regs4[NL * 8];            // line of sketch slab0 + i at reg[i * 128]
@@ -1160,7 +1149,7 @@ __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const uint64_t *__res
     uint8_t *reg = reinterpret_cast<uint8_t *>(regs4);
     uint64_t *R = work;
     uint16_t *nxt = reinterpret_cast<uint16_t *>(R + SK_PFL_CAP);
-    uint16_t *head = nxt + SK_PFL_CAP;
+    uint32_t *head = reinterpret_cast<uint32_t *>(nxt + SK_PFL_CAP);
     uint8_t *fin = reinterpret_cast<uint8_t *>(head + SK_PFL_HT);
 
     const uint32_t f = blockIdx.x, b = f / nsub, sub = f % nsub;
@@ -1253,8 +1242,17 @@ __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const uint64_t *__res
     }
     __syncthreads();
     if (probe & 4) return;
+    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
     for (uint32_t q = threadIdx.x; q < nsl * 8; q += SK_PFL_ATPB)
-        if (dirty[q >> 3]) line(q >> 3)[q & 7] = regs4[q];
+        if (dirty[q >> 3]) {
+            if (probe & 16) {
+                const uint4 x = regs4[q];
+                v4u y = {x.x, x.y, x.z, x.w};
+                __builtin_nontemporal_store(y, reinterpret_cast<v4u *>(line(q >> 3) + (q & 7)));
+            } else {
+                line(q >> 3)[q & 7] = regs4[q];
+            }
+        }
 }
 
 // streamed-once 16-B load with the nontemporal hint (native vector type for the builtin)

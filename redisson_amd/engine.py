@@ -260,15 +260,23 @@ class SketchEngine:
     # ------------------------------------------------------------ HLL
     def pfadd(self, keys: Sequence, elems: Sequence[Sequence[bytes]]) -> List[bool]:
         """PFADD batch: command i = PFADD keys[i] *elems[i] (raw element bytes)."""
+        st, out, _ = self.pfadd_status(keys, elems)
+        self._check(st)
+        return [bool(x) for x in out]
+
+    def pfadd_status(self, keys: Sequence, elems: Sequence[Sequence[bytes]]):
+        """sk_pfadd without raising: (status, replies u8[n], error text).  A command on a key of another type fails
+        alone (pipeline semantics): the status reports it, the other commands' replies are valid."""
         n = len(keys)
         koff, kbuf = pack([_b(k) for k in keys])
         counts = np.fromiter((len(e) for e in elems), dtype=np.uint32, count=n)
         flat = [x for e in elems for x in e]
         eoff, ebuf = pack(flat)
         out = np.zeros(n, dtype=np.uint8)
-        self._check(self.lib.sk_pfadd(self.ctx, n, _addr(koff), _addr(kbuf), _addr(counts), _addr(eoff),
-                                      _addr(ebuf), _addr(out)))
-        return [bool(x) for x in out]
+        st = self.lib.sk_pfadd(self.ctx, n, _addr(koff), _addr(kbuf), _addr(counts), _addr(eoff), _addr(ebuf),
+                               _addr(out))
+        msg = (self.lib.sk_last_error(self.ctx) or b"").decode("utf-8", "replace") if st != N.SK_OK else ""
+        return st, out, msg
 
     def pfadd_ids(self, key_ids, elems: Sequence[Sequence[bytes]]) -> List[bool]:
         """PFADD batch with keys pre-resolved by hll_resolve: command i = PFADD key_ids[i] *elems[i]."""

@@ -81,6 +81,9 @@ class Config:
     # group commit of concurrent RBloomFilter add/contains calls (redisson_amd/coalesce.py): callers only enqueue,
     # one completion thread merges FIFO runs into single engine calls
     bloom_coalesce: bool = False
+    # group commit of concurrently executed RBatches (coalesce.BatchCoalescer): PFADD-only batches queued together
+    # become one engine call (the line schedule at >= 4 M commands), replies split back per batch
+    batch_coalesce: bool = False
 
 
 class JBitSet:
@@ -387,6 +390,13 @@ class RBatch:
             raise IllegalStateException("Batch already executed!")
         if not self._cmds:
             return None           # newSucceededFuture(null) for an empty batch
+        co = getattr(self._c, "batch_coalescer", None)
+        if co is not None:        # group commit with concurrently executed batches (coalesce.BatchCoalescer)
+            self._executed = True
+            return co.submit(self).get()
+        return self._execute_now()
+
+    def _execute_now(self):
         self._executed = True
         self._c._run_batch(self._cmds)
         err = None
@@ -400,7 +410,11 @@ class RBatch:
         return out
 
     def executeAsync(self) -> Future:
-        return _completed(self.execute)
+        co = getattr(self._c, "batch_coalescer", None)
+        if co is None or not self._cmds or self._executed:
+            return _completed(self.execute)
+        self._executed = True
+        return co.submit(self)    # completed by the coalescer's thread; the caller never waits on the device
 
 
 class _BatchClient:
@@ -430,6 +444,10 @@ class Redisson:
         if config.bloom_coalesce:
             from .coalesce import BloomCoalescer
             self.bloom_coalescer = BloomCoalescer(self.engine)
+        self.batch_coalescer = None
+        if config.batch_coalesce:
+            from .coalesce import BatchCoalescer
+            self.batch_coalescer = BatchCoalescer(self)
 
     @staticmethod
     def create(config: Optional[Config] = None) -> "Redisson":
@@ -438,6 +456,8 @@ class Redisson:
     def shutdown(self):
         if self.bloom_coalescer is not None:
             self.bloom_coalescer.close()
+        if self.batch_coalescer is not None:
+            self.batch_coalescer.close()
         self.engine.close()
 
     def getHyperLogLog(self, name, codec=None) -> RHyperLogLog:

@@ -25,22 +25,24 @@ def _engine(**kw):
     return SketchEngine(device=0, **kw)
 
 
-def test_c2_pfadd_100k_tenants_full_arena(O):
-    """C2: 100 k tenants (1.6 GB of registers), 128 M single-element PFADDs in 1 M batches: every reply, every
-    register of every tenant, every per-key PFCOUNT and the union count equal the oracle's."""
-    T, NB, seed = 100_000, 128, 0x5EED2002
+@pytest.mark.parametrize("per_call", [M, 64 * M], ids=["partition_1M", "lines_64M"])
+def test_c2_pfadd_100k_tenants_full_arena(O, per_call):
+    """C2: 100 k tenants (1.6 GB of registers), 128 M single-element PFADDs, one 1 M RBatch per call (partition
+    path) or 64 RBatches group-committed per call (line schedule): every reply, every register of every tenant,
+    every per-key PFCOUNT and the union count equal the oracle's."""
+    T, NB, seed = 100_000, 128 * M // per_call, 0x5EED2002
     names = ["tenant:%d:hll" % t for t in range(T)]
-    eng = _engine(hll_capacity=T + 16, max_batch=4 * M)
+    eng = _engine(hll_capacity=T + 16, max_batch=per_call)
     try:
         ids = eng.hll_resolve(names)
-        kid = np.random.default_rng(22).integers(0, T, NB * M).astype(np.uint32)
-        got = np.zeros(NB * M, dtype=np.uint8)
-        d_out = eng.alloc(M)
+        kid = np.random.default_rng(22).integers(0, T, NB * per_call).astype(np.uint32)
+        got = np.zeros(NB * per_call, dtype=np.uint8)
+        d_out = eng.alloc(per_call)
         for b in range(NB):
-            off, byt, tot = eng.gen_jackson_longs_dev(seed, M, first=b * M)
-            d_ids = eng.to_device(ids[kid[b * M:(b + 1) * M]])
-            eng.pfadd_dev(M, d_ids, off, byt, tot, d_out)
-            got[b * M:(b + 1) * M] = d_out.download(np.uint8, M)
+            off, byt, tot = eng.gen_jackson_longs_dev(seed, per_call, first=b * per_call)
+            d_ids = eng.to_device(ids[kid[b * per_call:(b + 1) * per_call]])
+            eng.pfadd_dev(per_call, d_ids, off, byt, tot, d_out)
+            got[b * per_call:(b + 1) * per_call] = d_out.download(np.uint8, per_call)
             for x in (off, byt, d_ids):
                 x.free()
         regs = np.zeros((T, 16384), dtype=np.uint8)

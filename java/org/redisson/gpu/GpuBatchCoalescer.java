@@ -1,0 +1,166 @@
+/*
+ * GpuBatchCoalescer -- group commit of concurrently executed RBatches of PFADD commands (the C2 ingestion shape;
+ * the Python mirror and its tests are redisson_amd/coalesce.py BatchCoalescer, tests/test_batch_coalesce.py).
+ *
+ * The reference sends every RBatch as its own pipeline (M:command/CommandBatchService.java:184-293) and
+ * redis-server applies the batches one after another.  Here GpuSketchBatchService hands a batch whose commands are
+ * all PFADDs on engine-held keys to this coalescer instead of running it alone.  The context's FIFO worker runs
+ * each maximal sequence of such batches queued together (up to maxCmds commands) as ONE sk_pfadd call; at >= 4 M commands the engine applies it with the line schedule (register lines streamed
+ * once per call instead of once per element).  The concatenation keeps FIFO order and PFADD replies depend only
+ * on order, so every batch gets exactly the replies it would get run alone in that order.  A PFADD on a key of
+ * another type fails that command alone inside the engine (pipeline semantics); its batch fails with the
+ * engine's error and every other batch of the call completes normally.  Groups run as tasks of the context's FIFO
+ * worker, so batches keep the order of their executeAsync calls.  Source only here; see INTEGRATION.md.
+ */
+package org.redisson.gpu;
+
+import java.util.ArrayList;
+import java.util.HashSet;
+import java.util.List;
+import java.util.Set;
+
+import org.redisson.client.RedisException;
+
+import io.netty.util.concurrent.Promise;
+
+public final class GpuBatchCoalescer {
+
+    /** One RBatch: command c = PFADD keys[c] elems[c] (encoded as CommandEncoder would); one reply per command. */
+    static final class Req {
+        final List<byte[]> keys;
+        final List<byte[][]> elems;
+        final Promise<boolean[]> promise;
+
+        Req(List<byte[]> keys, List<byte[][]> elems, Promise<boolean[]> promise) {
+            this.keys = keys;
+            this.elems = elems;
+            this.promise = promise;
+        }
+    }
+
+    /* A group is one task on the context's FIFO worker (SketchDispatch.worker): PFADD-only batches join the open
+     * group until the worker starts it or another batch is queued behind it, so groups are exactly the maximal
+     * sequences of PFADD-only batches between other batches, and the worker's FIFO order is kept. */
+    final class Group implements Runnable {
+        final List<Req> reqs = new ArrayList<Req>();
+        int n;
+        boolean started;
+
+        @Override
+        public void run() {
+            synchronized (GpuBatchCoalescer.this) {
+                started = true;
+                if (open == this) {
+                    open = null;
+                }
+            }
+            try {
+                execute(reqs);
+            } catch (RuntimeException e) {
+                for (Req r : reqs) {
+                    r.promise.tryFailure(e);
+                }
+            }
+        }
+    }
+
+    private static final java.util.concurrent.ConcurrentHashMap<Long, GpuBatchCoalescer> BY_CTX =
+            new java.util.concurrent.ConcurrentHashMap<Long, GpuBatchCoalescer>();
+
+    private final long ctx;
+    private final int maxCmds;
+    private Group open; // guarded by this
+    volatile long calls;    // sk_pfadd calls made (one per group)
+    volatile long batches;  // batches completed
+
+    private GpuBatchCoalescer(long ctx, int maxCmds) {
+        this.ctx = ctx;
+        this.maxCmds = maxCmds;
+    }
+
+    /** Turn group commit on for a context (GpuSketchBatchService then routes PFADD-only batches here). */
+    public static GpuBatchCoalescer enable(long ctx, int maxCmds) {
+        GpuBatchCoalescer c = new GpuBatchCoalescer(ctx, maxCmds);
+        GpuBatchCoalescer old = BY_CTX.putIfAbsent(ctx, c);
+        return old != null ? old : c;
+    }
+
+    /** The context's coalescer, or null when group commit is off. */
+    public static GpuBatchCoalescer of(long ctx) {
+        return BY_CTX.get(ctx);
+    }
+
+    public static void disable(long ctx) {
+        BY_CTX.remove(ctx);
+    }
+
+    /** Enqueue a PFADD-only batch; never blocks on the device. */
+    public synchronized void submit(List<byte[]> keys, List<byte[][]> elems, Promise<boolean[]> promise) {
+        if (open == null || open.started || open.n + keys.size() > maxCmds) {
+            open = new Group();
+            SketchDispatch.worker(ctx).execute(open);
+        }
+        open.reqs.add(new Req(keys, elems, promise));
+        open.n += keys.size();
+    }
+
+    /** Queue another batch's task behind every group opened so far; later PFADD-only batches open a new group. */
+    public synchronized void executeAfter(Runnable task) {
+        open = null;
+        SketchDispatch.worker(ctx).execute(task);
+    }
+
+    private void execute(List<Req> group) {
+        List<byte[]> keys = new ArrayList<byte[]>();
+        List<byte[]> flat = new ArrayList<byte[]>();
+        List<Integer> counts = new ArrayList<Integer>();
+        for (Req r : group) {
+            keys.addAll(r.keys);
+            for (byte[][] es : r.elems) {
+                counts.add(es.length);
+                for (byte[] x : es) {
+                    flat.add(x);
+                }
+            }
+        }
+        int[] cnt = new int[counts.size()];
+        for (int i = 0; i < cnt.length; i++) {
+            cnt[i] = counts.get(i);
+        }
+        SketchDispatch.Packed k = new SketchDispatch.Packed(keys);
+        SketchDispatch.Packed e = new SketchDispatch.Packed(flat);
+        byte[] out = new byte[keys.size()];
+        int st = SketchNative.pfadd(ctx, k.off, k.bytes, cnt, e.off, e.bytes, out);
+        String err = st == SketchNative.SK_OK ? null : SketchNative.lastError(ctx);
+        // the failed commands: keys that are still not HLLs after the call (WRONGTYPE / corrupt sparse string);
+        // any other status fails every batch of the call
+        Set<String> bad = new HashSet<String>();
+        boolean all = st != SketchNative.SK_OK && st != SketchNative.SK_EWRONGTYPE && st != SketchNative.SK_ECORRUPT;
+        if (st == SketchNative.SK_EWRONGTYPE || st == SketchNative.SK_ECORRUPT) {
+            int[] t = new int[1];
+            for (byte[] key : keys) {
+                if (SketchNative.type(ctx, key, t) != SketchNative.SK_OK || t[0] != SketchNative.SK_TYPE_HLL) {
+                    bad.add(new String(key, SketchDispatch.ISO));
+                }
+            }
+        }
+        int p = 0;
+        for (Req r : group) {
+            boolean failed = all;
+            boolean[] rep = new boolean[r.keys.size()];
+            for (int c = 0; c < rep.length; c++, p++) {
+                rep[c] = out[p] != 0;
+                if (!failed && !bad.isEmpty() && bad.contains(new String(r.keys.get(c), SketchDispatch.ISO))) {
+                    failed = true;
+                }
+            }
+            if (failed) {
+                r.promise.tryFailure(new RedisException(err));
+            } else {
+                r.promise.trySuccess(rep);
+            }
+        }
+        calls++;
+        batches += group.size();
+    }
+}

@@ -140,10 +140,15 @@ public class GpuSketchBatchService extends CommandBatchService {
         }
         executed = true;
         final Promise<List<?>> result = getConnectionManager().newPromise();
+        final GpuBatchCoalescer co = GpuBatchCoalescer.of(ctx);
         // the sketch runs and the hand-off of the redis part happen on the context's worker: the caller (maybe an
         // event-loop thread) never waits on the device
         try {
-            SketchDispatch.worker(ctx).execute(new Runnable() {
+            if (co != null && pfaddOnly()) { // group commit with the PFADD-only batches queued beside it
+                submitGroup(co, result);
+                return result;
+            }
+            Runnable task = new Runnable() {
                 @Override
                 public void run() {
                     try {
@@ -152,11 +157,65 @@ public class GpuSketchBatchService extends CommandBatchService {
                         result.tryFailure(e);
                     }
                 }
-            });
+            };
+            if (co != null) {
+                co.executeAfter(task);
+            } else {
+                SketchDispatch.worker(ctx).execute(task);
+            }
         } catch (java.util.concurrent.RejectedExecutionException e) {
             result.tryFailure(new IllegalStateException("sketch engine shut down", e));
         }
         return result;
+    }
+
+    boolean pfaddOnly() {
+        if (redisUsed || sketch.isEmpty()) {
+            return false;
+        }
+        for (Cmd c : sketch) {
+            if (!"PFADD".equals(c.command.getName())) {
+                return false;
+            }
+        }
+        return true;
+    }
+
+    /* the batch as one request of the context's GpuBatchCoalescer: its commands' encoded keys and elements; the
+     * group's replies complete the command promises and the batch result in enqueue order */
+    void submitGroup(GpuBatchCoalescer co, final Promise<List<?>> result) {
+        List<byte[]> keys = new ArrayList<byte[]>(sketch.size());
+        List<byte[][]> elems = new ArrayList<byte[][]>(sketch.size());
+        for (Cmd c : sketch) {
+            keys.add(GpuSketchCommandService.encodeParam(c.codec, c.command, c.params[0], 1));
+            byte[][] es = new byte[c.params.length - 1][];
+            for (int p = 1; p < c.params.length; p++) {
+                es[p - 1] = GpuSketchCommandService.encodeParam(c.codec, c.command, c.params[p], p + 1);
+            }
+            elems.add(es);
+        }
+        Promise<boolean[]> replies = getConnectionManager().newPromise();
+        replies.addListener(new FutureListener<boolean[]>() {
+            @Override
+            public void operationComplete(Future<boolean[]> f) throws Exception {
+                if (!f.isSuccess()) {
+                    for (Cmd c : sketch) {
+                        c.promise.tryFailure(f.cause());
+                    }
+                    result.tryFailure(f.cause());
+                    return;
+                }
+                boolean[] rep = f.getNow();
+                List<Object> out = new ArrayList<Object>(sketch.size());
+                for (int i = 0; i < rep.length; i++) {
+                    Cmd c = sketch.get(i);
+                    c.promise.trySuccess(GpuSketchCommandService.convert(c.command, Long.valueOf(rep[i] ? 1 : 0)));
+                    out.add(c.promise.getNow());
+                }
+                result.trySuccess(out);
+            }
+        });
+        co.submit(keys, elems, replies);
     }
 
     void executeOnWorker(final Promise<List<?>> result) {

@@ -80,6 +80,14 @@ def c1(eng, args):
     t_ss = timed(eng, lambda: [eng.pfadd_dev(n, d_ids2.ptr + s * n * 4, off2.ptr + s * n * 8, byt2, tot2, d_out)
                                for s in range(steps)])
     eng.set_async(False)
+    # group commit: the same 10 RBatches as ONE device call (line schedule); replies checked equal-sized only
+    d_out10 = eng.alloc(n * steps)
+    eng.delete([b"hll:c1"])
+    ids = eng.hll_resolve([b"hll:c1"])
+    d_ids2.upload(np.full(n * steps, ids[0], dtype=np.uint32))
+    eng.pfadd_dev(n, d_ids2, off2, byt2, tot2, d_out)            # the same first batch as above, then the group
+    t_g = timed(eng, lambda: eng.pfadd_dev(n * steps, d_ids2, off2, byt2, tot2, d_out10))
+    d_out10.free()
     off2.free(); byt2.free(); d_ids2.free()
     # Q1: addAll(1M Longs) = ONE PFADD element, the Jackson encoding of Object[]{name, e1..en}
     vals = np.random.default_rng(1).integers(-(1 << 63), (1 << 63) - 1, min(n, 1 << 20), dtype=np.int64)
@@ -93,6 +101,8 @@ def c1(eng, args):
           "unit": "inserts/s", "config": {"workload": "c1", "elements": n, "count_after": cnt},
           "steady_state": "%d back-to-back batches of %d fresh Longs into the one key" % (steps, n),
           "single_batch_inserts_per_s_host_timed": n / t,
+          "group_commit_inserts_per_s": n * steps / t_g,
+          "group_commit": "the %d batches as one call (line schedule), host-timed" % steps,
           "addAll_q1": {"element_bytes": len(blob), "seconds": t_q1, "hash_ms_device": ms_long / max(n_l, 1),
                         "count_after":
                         eng.pfcount([[b"hll:c1q"]])[0]}})
@@ -115,6 +125,9 @@ def c2zipf(eng, args):
     eng.set_async(False)
     t_sync = timed(eng, lambda: [eng.pfadd_dev(B, d_ids.ptr + s * B * 4, off.ptr + s * B * 8, byt, tot, d_out)
                                  for s in range(1, steps + 1)])
+    d_out10 = eng.alloc(B * steps)   # group commit: the 10 batches as one call (line schedule)
+    t_g = timed(eng, lambda: eng.pfadd_dev(B * steps, d_ids.ptr + B * 4, off.ptr + B * 8, byt, tot, d_out10))
+    d_out10.free()
     top = float(np.bincount(kid[:B]).max()) / B
     # per-key PFCOUNT of every tenant (C2): the histogram kernel alone, and the whole RHyperLogLog.count path
     d_all = eng.to_device(ids)
@@ -131,6 +144,7 @@ def c2zipf(eng, args):
           "unit": "inserts/s", "config": {"workload": "c2zipf", "batch": B, "tenants": nt, "zipf_s": 1.1,
                                           "hottest_tenant_share": top},
           "synchronous_calls_inserts_per_s": B * steps / t_sync,
+          "group_commit_inserts_per_s": B * steps / t_g,
           "pfcount_keys_per_s": nt / t_c, "pfcount_ids_keys_per_s": nt / t_ci, "hist_keys_per_s_host_timed": nt / t_h,
           "roofline": {"kernel": "hll_hist", "bound": "hbm", "achieved": gbs, "peak": PEAK, "unit": "GB/s",
                        "frac": gbs / PEAK, "bytes_per_unit": 16384, "avg_launch_ms": k_ms}})

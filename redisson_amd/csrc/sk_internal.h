@@ -49,6 +49,7 @@ hipError_t launch_pfp_reply(hipStream_t st, uint64_t n, const uint8_t *rep, cons
 // buckets, partition each into runs of (bucket, 512 sketches, tile of hash blocks), apply with the lines in LDS
 struct PflDims {
     uint32_t nblk, tb, ntile, nsub, nsums; // hash blocks, blocks per run tile, tiles, fine buckets per bucket
+    uint32_t sh;                           // 2^sh sketches per fine bucket
     uint64_t nf, ncount;         // fine buckets; run counts (C holds ncount + 1 words)
     uint64_t chunk_bytes, S_bytes;
 };

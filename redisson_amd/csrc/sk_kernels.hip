@@ -359,10 +359,17 @@ __device__ __forceinline__ void pfp_win_store(uint64_t lo, uint64_t hi, const ui
 
 // line schedule (sketch-major group apply, below): coarse bucket of a register = its 128-register line, rotated
 // per sketch, so bucket b holds exactly one line of every sketch and a hot sketch spreads over all 128 buckets
-#define SK_PFL_NB 128
-__device__ __forceinline__ uint32_t pfl_rot(uint32_t slab) { return (slab * 0x9E3779B1u) >> 25; }
+#define SK_PFL_NB 128 // coarse buckets = register lines per sketch
+#define SK_PFL_LB 7   // log2 registers per line: 128 registers = one 128-B line (64-register pieces at 256 buckets:
+                      // apply 1.62 vs 1.31 ms per 64 M, Zipf no better)
+static_assert((SK_PFL_NB << SK_PFL_LB) == 16384, "the lines tile a sketch");
+__device__ __forceinline__ uint32_t pfl_rot(uint32_t slab) { return (slab * 0x9E3779B1u) >> (32 - 7); }
+static_assert(SK_PFL_NB == 128, "pfl_rot draws 7 bits");
 __device__ __forceinline__ uint32_t pfl_bucket(uint32_t slab, uint32_t reg) {
-    return ((reg >> 7) + pfl_rot(slab)) & (SK_PFL_NB - 1);
+    return ((reg >> SK_PFL_LB) + pfl_rot(slab)) & (SK_PFL_NB - 1);
+}
+__device__ __forceinline__ uint32_t pfl_slotb(uint64_t key) { // key = slab_low << 14 | reg -> the register in LDS
+    return uint32_t(key >> 14) << SK_PFL_LB | (uint32_t(key) & ((1u << SK_PFL_LB) - 1));
 }
 
 // NBK buckets; LINE = false: the partition path (records slot << 26 | seq << 6 | rho, pfp_bucket),
@@ -882,7 +889,7 @@ __global__ void __launch_bounds__(SK_PFP_ATPB) __attribute__((amdgpu_waves_per_e
 // elements) registers are applied sketch-major with the registers held in LDS, instead of one random register
 // line read and written per element:
 //   k_pfl_hash     as k_pfp_hash, 128 coarse buckets: bucket b holds line (b - rot(s)) & 127 of every sketch s
-//   k_pfl_count    per (bucket, tile of 128 hash blocks): records per fine bucket = (b, s >> 8)
+//   k_pfl_count    per (bucket, tile of hash blocks): records per fine bucket = (b, s >> sh)
 //   k_scan_*       exclusive scan of the counts (fine-bucket major, tile minor) -> each (fine bucket, tile) run
 //   k_pfl_scatter  records to their run: rec2 = slab_low << 46 | reg << 32 | rho << 26 | seq (26 bits)
 //   k_pfl_apply    one workgroup per fine bucket: its 256 lines (one per sketch, 32 KiB) into LDS with its
@@ -891,7 +898,8 @@ __global__ void __launch_bounds__(SK_PFP_ATPB) __attribute__((amdgpu_waves_per_e
 // Runs are in tile order and tiles in batch order, so a fine bucket larger than one chunk is applied in chunks of
 // whole runs with the LDS registers carried over; a single run larger than a chunk is resolved with the (slot,
 // rho) -> min seq table of pfp_big_resolve, against the LDS registers.
-#define SK_PFL_SH 7        // sketches per fine bucket = 2^SH (128 lines of 128 B = 16 KiB of registers)
+#define SK_PFL_SH 7        // largest fine bucket = 2^SH sketches (128 lines of 128 B = 16 KiB of registers); a call
+                           // uses sh <= SH sketches per fine bucket, sized so a fine bucket expects <= ~768 records
 #define SK_PFL_TILE 1024   // hash blocks per run tile (default; SK_PFL_TILE)
 #define SK_PFL_BTPB 512    // count / scatter threads: 4 per hash block, 128 blocks per pass over the tile
 #define SK_PFL_ATPB 256    // apply threads (five apply workgroups per CU: 29 KiB of LDS each)
@@ -916,7 +924,8 @@ __device__ __forceinline__ void pfl_bt(uint32_t ntile, uint32_t *b, uint32_t *ti
 
 __global__ void __launch_bounds__(SK_PFL_BTPB) k_pfl_count(const uint64_t *__restrict__ chunks,
                                                            const uint32_t *__restrict__ S, uint32_t nblk, uint32_t tb,
-                                                           uint32_t ntile, uint32_t nsub, uint32_t *__restrict__ C) {
+                                                           uint32_t ntile, uint32_t nsub, uint32_t sh,
+                                                           uint32_t *__restrict__ C) {
     extern __shared__ uint32_t hist[]; // nsub words
     for (uint32_t s = threadIdx.x; s < nsub; s += SK_PFL_BTPB) hist[s] = 0;
     __syncthreads();
@@ -927,7 +936,7 @@ __global__ void __launch_bounds__(SK_PFL_BTPB) k_pfl_count(const uint64_t *__res
         const uint32_t lo = S[uint64_t(b) * nblk + blk], hi = S[uint64_t(b + 1) * nblk + blk];
         const uint64_t *seg = chunks + uint64_t(blk) * SK_PFP_EPB;
         for (uint32_t t = lo + (threadIdx.x & 3u); t < hi; t += 4) {
-            const uint32_t sb = uint32_t(seg[t] >> 32) >> SK_PFL_SH;
+            const uint32_t sb = uint32_t(seg[t] >> 32) >> sh;
             if (sb < nsub) atomicAdd(&hist[sb], 1u); // ids beyond the store's slabs are dropped (both passes)
         }
     }
@@ -943,7 +952,7 @@ __global__ void __launch_bounds__(SK_PFL_BTPB) k_pfl_count(const uint64_t *__res
 #define SK_PFL_PIECE 4096
 __global__ void __launch_bounds__(SK_PFL_BTPB) k_pfl_scatter(const uint64_t *__restrict__ chunks,
                                                              const uint32_t *__restrict__ S, uint32_t nblk,
-                                                             uint32_t tb, uint32_t ntile, uint32_t nsub,
+                                                             uint32_t tb, uint32_t ntile, uint32_t nsub, uint32_t sh,
                                                              const uint32_t *__restrict__ C,
                                                              uint64_t *__restrict__ rec2) {
     constexpr int PER = SK_PFL_PIECE / SK_PFL_BTPB;
@@ -997,10 +1006,10 @@ __global__ void __launch_bounds__(SK_PFL_BTPB) k_pfl_scatter(const uint64_t *__r
             const uint32_t blk = b0 + lo;
             const uint64_t rr = chunks[uint64_t(blk) * SK_PFP_EPB + S[uint64_t(b) * nblk + blk] + (x - segp[lo])];
             const uint32_t slab = uint32_t(rr >> 32), reg = uint32_t(rr >> 18) & 16383u, rho = uint32_t(rr >> 12) & 63u;
-            if ((slab >> SK_PFL_SH) >= nsub) continue; // ids beyond the store's slabs are dropped (both passes)
-            r[q] = (uint64_t(slab & ((1u << SK_PFL_SH) - 1)) << 46) | (uint64_t(reg) << 32) | (uint64_t(rho) << 26) |
+            if ((slab >> sh) >= nsub) continue; // ids beyond the store's slabs are dropped (both passes)
+            r[q] = (uint64_t(slab & ((1u << sh) - 1)) << 46) | (uint64_t(reg) << 32) | (uint64_t(rho) << 26) |
                    (uint64_t(blk) * SK_PFP_EPB + (rr & 4095u));
-            rk[q] = atomicAdd(&lcnt[slab >> SK_PFL_SH], 1u) | ((slab >> SK_PFL_SH) << 13);
+            rk[q] = atomicAdd(&lcnt[slab >> sh], 1u) | ((slab >> sh) << 13);
         }
         __syncthreads();
         // exclusive scan of the piece's counts over the fine buckets (in place), nsub <= SK_PFL_MAXSUB
@@ -1118,7 +1127,7 @@ __device__ __forceinline__ void pfl_chunk(const uint64_t *R, uint32_t cnt, uint1
                 earliest = false;
             }
         }
-        const uint32_t slotb = uint32_t(key >> 14) << 7 | (uint32_t(key) & 127u);
+        const uint32_t slotb = pfl_slotb(key);
         const uint32_t R0 = reg[slotb];
         const uint8_t rep = rho > (R0 > p ? R0 : p);
         if (probe & 8) __builtin_nontemporal_store(rep, changed + seq);
@@ -1129,21 +1138,22 @@ __device__ __forceinline__ void pfl_chunk(const uint64_t *R, uint32_t cnt, uint1
     for (uint32_t u = threadIdx.x; u < cnt; u += SK_PFL_ATPB)
         if (fin[u]) {
             const uint64_t key = R[u] >> 32;
-            reg[uint32_t(key >> 14) << 7 | (uint32_t(key) & 127u)] = fin[u];
+            reg[pfl_slotb(key)] = fin[u];
             dirty[uint32_t(key >> 14)] = 1;
         }
 }
 
 __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const uint64_t *__restrict__ rec2,
                                                            const uint32_t *__restrict__ C, uint32_t ntile,
-                                                           uint32_t nsub, uint32_t nslab, uint8_t *arena,
+                                                           uint32_t nsub, uint32_t sh, uint32_t nslab, uint8_t *arena,
                                                            uint8_t *__restrict__ changed, uint32_t *big_alloc,
                                                            uint64_t *big_keys, uint32_t *big_vals, int probe) {
     constexpr uint32_t NL = 1u << SK_PFL_SH;
     constexpr uint32_t kWork = SK_PFL_CAP * 8 + SK_PFL_CAP * 2 + SK_PFL_HT * 4 + SK_PFL_CAP;
     constexpr uint32_t kBigL = 1024;       // LDS slots of the big-run table
     static_assert(kWork >= kBigL * 12, "the big-run table shares the chunk LDS");
-    __shared__ uint4 regs4[NL * 8];            // line of sketch slab0 + i at reg[i * 128]
+    constexpr uint32_t LW = (1u << SK_PFL_LB) / 16; // 16-B words per line
+    __shared__ uint4 regs4[NL * LW];           // line of sketch slab0 + i at reg[i << SK_PFL_LB]
     __shared__ uint64_t work[(kWork + 7) / 8]; // chunk records, chains, final values (or the big-run table)
     __shared__ uint8_t dirty[NL];
     uint8_t *reg = reinterpret_cast<uint8_t *>(regs4);
@@ -1156,22 +1166,21 @@ __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const uint64_t *__res
     const uint64_t c0 = uint64_t(f) * ntile;
     const uint32_t start = C[c0], end = C[c0 + ntile], cnt = end - start;
     if (cnt == 0) return; // uniform
-    const uint32_t slab0 = sub << SK_PFL_SH, nsl = nslab - slab0 < NL ? nslab - slab0 : NL;
+    const uint32_t slab0 = sub << sh, nsl = nslab - slab0 < (1u << sh) ? nslab - slab0 : (1u << sh);
     auto line = [&](uint32_t i) -> uint4 * {
         const uint32_t s = slab0 + i;
-        if (probe & 1) return reinterpret_cast<uint4 *>(arena + (((uint64_t(f) << SK_PFL_SH) + i) % (uint64_t(nslab) * 128)) * 128); // timing probe
-        return reinterpret_cast<uint4 *>(arena + (uint64_t(s) << 14) + (((b - pfl_rot(s)) & 127u) << 7));
+        return reinterpret_cast<uint4 *>(arena + (uint64_t(s) << 14) + (((b - pfl_rot(s)) & (SK_PFL_NB - 1)) << SK_PFL_LB));
     };
     for (uint32_t i = threadIdx.x; i < NL; i += SK_PFL_ATPB) dirty[i] = 0;
     for (uint32_t t = threadIdx.x; t < SK_PFL_HT; t += SK_PFL_ATPB) head[t] = 0xffffu;
     __syncthreads();
     if (cnt <= SK_PFL_CAP) { // the whole fine bucket is one chunk: records and lines in one round trip
-        constexpr int LQ = (NL * 8 + SK_PFL_ATPB - 1) / SK_PFL_ATPB;
+        constexpr int LQ = (NL * LW + SK_PFL_ATPB - 1) / SK_PFL_ATPB;
         uint4 lv[LQ];
 #pragma unroll
         for (int j = 0; j < LQ; j++) {
             const uint32_t q = threadIdx.x + j * SK_PFL_ATPB;
-            if (q < nsl * 8) lv[j] = (probe & 4) ? make_uint4(0, 0, 0, 0) : line(q >> 3)[q & 7];
+            if (q < nsl * LW) lv[j] = (probe & 4) ? make_uint4(0, 0, 0, 0) : line(q / LW)[q % LW];
         }
         for (uint32_t u = threadIdx.x; u < cnt; u += SK_PFL_ATPB) R[u] = rec2[start + u];
         __syncthreads();
@@ -1179,11 +1188,11 @@ __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const uint64_t *__res
 #pragma unroll
             for (int j = 0; j < LQ; j++) {
                 const uint32_t q = threadIdx.x + j * SK_PFL_ATPB;
-                if (q < nsl * 8) regs4[q] = lv[j];
+                if (q < nsl * LW) regs4[q] = lv[j];
             }
         });
     } else {
-        for (uint32_t q = threadIdx.x; q < nsl * 8; q += SK_PFL_ATPB) regs4[q] = line(q >> 3)[q & 7];
+        for (uint32_t q = threadIdx.x; q < nsl * LW; q += SK_PFL_ATPB) regs4[q] = line(q / LW)[q % LW];
         __syncthreads();
         uint32_t t0 = 0;
         while (t0 < ntile) { // uniform: chunks of whole runs, in tile (= batch) order
@@ -1192,10 +1201,52 @@ __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const uint64_t *__res
             while (t1 < ntile && C[c0 + t1 + 1] - a <= SK_PFL_CAP) t1++;
             const uint32_t z = C[c0 + t1], k = z - a;
             if (k <= SK_PFL_CAP) {
-                for (uint32_t u = threadIdx.x; u < k; u += SK_PFL_ATPB) R[u] = rec2[a + u];
+                constexpr int CU = SK_PFL_CAP / SK_PFL_ATPB;
+                uint64_t rr[CU];
+#pragma unroll
+                for (int q = 0; q < CU; q++) {
+                    const uint32_t u = q * SK_PFL_ATPB + threadIdx.x;
+                    if (u < k) rr[q] = rec2[a + u];
+                }
+#pragma unroll
+                for (int q = 0; q < CU; q++) {
+                    const uint32_t u = q * SK_PFL_ATPB + threadIdx.x;
+                    if (u < k) R[u] = rr[q];
+                }
                 __syncthreads();
                 pfl_chunk(R, k, nxt, head, fin, reg, dirty, changed, 0, [] {});
-            } else { // one run larger than a chunk (t1 == t0 + 1): (slot, rho) -> min seq table
+            } else { // one run larger than a chunk (t1 == t0 + 1)
+                // only records above their register can rise, and only they can stop a later record from rising:
+                // the rest reply 0 now; the candidates are resolved as a chunk when they fit (a hot sketch whose
+                // registers are already high has few), else with the (slot, rho) -> min seq table
+                __shared__ uint32_t ncand;
+                if (threadIdx.x == 0) ncand = 0;
+                __syncthreads();
+                constexpr int FU = 8; // records in flight per thread
+                for (uint32_t u0 = 0; u0 < k; u0 += FU * SK_PFL_ATPB) {
+                    uint64_t rr[FU];
+#pragma unroll
+                    for (int q = 0; q < FU; q++) {
+                        const uint32_t u = u0 + q * SK_PFL_ATPB + threadIdx.x;
+                        rr[q] = u < k ? rec2[a + u] : ~0ull;
+                    }
+#pragma unroll
+                    for (int q = 0; q < FU; q++) {
+                        const uint64_t r = rr[q], key = r >> 32;
+                        if (r == ~0ull) continue;
+                        if (((r >> 26) & 63u) > reg[pfl_slotb(key)]) {
+                            const uint32_t i = atomicAdd(&ncand, 1u);
+                            if (i < SK_PFL_CAP) R[i] = r;
+                        } else {
+                            changed[r & 0x3ffffffu] = 0;
+                        }
+                    }
+                }
+                __syncthreads();
+                const uint32_t nc = ncand;
+                if (nc <= SK_PFL_CAP) {
+                    pfl_chunk(R, nc, nxt, head, fin, reg, dirty, changed, 0, [] {});
+                } else {
                 __shared__ uint32_t gbase;
                 unsigned long long *lk = reinterpret_cast<unsigned long long *>(work);
                 uint32_t *lv = reinterpret_cast<uint32_t *>(lk + kBigL);
@@ -1207,31 +1258,38 @@ __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const uint64_t *__res
                 for (uint32_t s = threadIdx.x; s < T.S; s += SK_PFL_ATPB) T.gk[s] = SK_BIG_EMPTY, T.gv[s] = 0xffffffffu;
                 __threadfence();
                 __syncthreads();
+                auto cand = [&](uint64_t r) {
+                    const uint64_t key = r >> 32;
+                    return ((r >> 26) & 63u) > reg[pfl_slotb(key)];
+                };
                 for (uint32_t u = threadIdx.x; u < k; u += SK_PFL_ATPB) {
                     const uint64_t r = rec2[a + u];
-                    T.insert(((r >> 32) << 6) | ((r >> 26) & 63u), uint32_t(r & 0x3ffffffu));
+                    if (cand(r)) T.insert(((r >> 32) << 6) | ((r >> 26) & 63u), uint32_t(r & 0x3ffffffu));
                 }
                 __threadfence();
                 __syncthreads();
                 for (uint32_t u = threadIdx.x; u < k; u += SK_PFL_ATPB) { // replies (registers only read)
                     const uint64_t r = rec2[a + u], key = r >> 32;
+                    if (!cand(r)) continue;
                     const uint32_t rho = uint32_t(r >> 26) & 63u, seq = uint32_t(r & 0x3ffffffu);
-                    bool first = rho > reg[uint32_t(key >> 14) << 7 | (uint32_t(key) & 127u)];
+                    bool first = true;
                     for (uint32_t v = rho; v < 52 && first; v++) first = T.find((key << 6) | v) >= seq;
                     changed[seq] = first ? 1 : 0;
                 }
                 __syncthreads();
                 for (uint32_t u = threadIdx.x; u < k; u += SK_PFL_ATPB) { // the register's writer: its top record
                     const uint64_t r = rec2[a + u], key = r >> 32;
+                    if (!cand(r)) continue;
                     const uint32_t rho = uint32_t(r >> 26) & 63u, seq = uint32_t(r & 0x3ffffffu);
                     if (T.find((key << 6) | rho) != seq) continue;
                     bool top = true;
                     for (uint32_t v = rho + 1; v < 52 && top; v++) top = T.find((key << 6) | v) == 0xffffffffu;
-                    const uint32_t slotb = uint32_t(key >> 14) << 7 | (uint32_t(key) & 127u);
+                    const uint32_t slotb = pfl_slotb(key);
                     if (top && rho > reg[slotb]) {
                         reg[slotb] = uint8_t(rho);
                         dirty[uint32_t(key >> 14)] = 1;
                     }
+                }
                 }
             }
             __syncthreads();
@@ -1243,14 +1301,14 @@ __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const uint64_t *__res
     __syncthreads();
     if (probe & 4) return;
     typedef unsigned int v4u __attribute__((ext_vector_type(4)));
-    for (uint32_t q = threadIdx.x; q < nsl * 8; q += SK_PFL_ATPB)
-        if (dirty[q >> 3]) {
+    for (uint32_t q = threadIdx.x; q < nsl * LW; q += SK_PFL_ATPB)
+        if (dirty[q / LW]) {
             if (probe & 16) {
                 const uint4 x = regs4[q];
                 v4u y = {x.x, x.y, x.z, x.w};
-                __builtin_nontemporal_store(y, reinterpret_cast<v4u *>(line(q >> 3) + (q & 7)));
+                __builtin_nontemporal_store(y, reinterpret_cast<v4u *>(line(q / LW) + (q % LW)));
             } else {
-                line(q >> 3)[q & 7] = regs4[q];
+                line(q / LW)[q % LW] = regs4[q];
             }
         }
 }
@@ -2490,7 +2548,13 @@ PflDims pfl_dims(uint64_t n, uint32_t nslab, uint32_t tile_blocks) {
     d.nblk = pfp_blocks(n);
     d.tb = tile_blocks ? tile_blocks : SK_PFL_TILE;
     d.ntile = (d.nblk + d.tb - 1) / d.tb;
-    d.nsub = (nslab + (1u << SK_PFL_SH) - 1) >> SK_PFL_SH;
+    // sketches per fine bucket: a fine bucket expects n * 2^sh / (128 * nslab) records; keep it near 768 (one
+    // chunk), within the LDS lines (2^SK_PFL_SH) and the scatter's fine-bucket arrays (SK_PFL_MAXSUB)
+    d.sh = SK_PFL_SH;
+    while (d.sh > 0 && double(n) * double(1u << d.sh) > 768.0 * SK_PFL_NB * double(nslab ? nslab : 1) &&
+           ((uint64_t(nslab) + (1u << (d.sh - 1)) - 1) >> (d.sh - 1)) <= SK_PFL_MAXSUB)
+        d.sh--;
+    d.nsub = (nslab + (1u << d.sh) - 1) >> d.sh;
     d.nf = uint64_t(SK_PFL_NB) * d.nsub;
     d.ncount = d.nf * d.ntile;
     d.nsums = uint32_t((d.ncount + SK_SCAN_ITEMS - 1) / SK_SCAN_ITEMS);
@@ -2513,9 +2577,7 @@ hipError_t launch_pfl_part(hipStream_t st, const PflDims &d, const uint64_t *chu
                            uint32_t *sums, uint64_t *rec2) {
     if (d.nsub > SK_PFL_MAXSUB || d.tb > SK_PFL_TMAX || d.ncount >= (1ull << 32)) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_pfl_count, dim3(d.ntile * SK_PFL_NB), dim3(SK_PFL_BTPB), d.nsub * 4, st, chunks, S, d.nblk,
-                       d.tb,
-                       d.ntile,
-                       d.nsub, C);
+                       d.tb, d.ntile, d.nsub, d.sh, C);
     SK_LAUNCH_CHECK();
     hipLaunchKernelGGL(k_scan_reduce, dim3(d.nsums), dim3(SK_SCAN_TPB), 0, st, d.ncount, C, sums);
     SK_LAUNCH_CHECK();
@@ -2524,9 +2586,7 @@ hipError_t launch_pfl_part(hipStream_t st, const PflDims &d, const uint64_t *chu
     hipLaunchKernelGGL(k_scan_apply, dim3(d.nsums), dim3(SK_SCAN_TPB), 0, st, d.ncount, C, sums);
     SK_LAUNCH_CHECK();
     hipLaunchKernelGGL(k_pfl_scatter, dim3(d.ntile * SK_PFL_NB), dim3(SK_PFL_BTPB), 2 * d.nsub * 4, st, chunks, S,
-                       d.nblk, d.tb,
-                       d.ntile,
-                       d.nsub, C, rec2);
+                       d.nblk, d.tb, d.ntile, d.nsub, d.sh, C, rec2);
     SK_LAUNCH_CHECK();
     return hipSuccess;
 }
@@ -2534,7 +2594,7 @@ hipError_t launch_pfl_part(hipStream_t st, const PflDims &d, const uint64_t *chu
 hipError_t launch_pfl_apply(hipStream_t st, const PflDims &d, const uint64_t *rec2, const uint32_t *C, uint32_t nslab,
                             uint8_t *arena, uint8_t *changed, uint32_t *big_alloc, uint64_t *big_keys,
                             uint32_t *big_vals) {
-    hipLaunchKernelGGL(k_pfl_apply, dim3(uint32_t(d.nf)), dim3(SK_PFL_ATPB), 0, st, rec2, C, d.ntile, d.nsub, nslab,
+    hipLaunchKernelGGL(k_pfl_apply, dim3(uint32_t(d.nf)), dim3(SK_PFL_ATPB), 0, st, rec2, C, d.ntile, d.nsub, d.sh, nslab,
                        arena, changed, big_alloc, big_keys, big_vals, getenv("SK_PFL_PROBE") ? atoi(getenv("SK_PFL_PROBE")) : 0);
     SK_LAUNCH_CHECK();
     return hipSuccess;

@@ -1,16 +1,20 @@
 #!/bin/bash
-# A/B of engine env knobs on the headline bench (GPU box, repo root):
-#   bash tools/ab_env.sh TAG "VAR=a" "VAR=b" ...   -> gpurun_out/TAG/<i>.json, one summary line each
+# A/B of env settings on the default bench, alternating runs on one box (dev tool)
+# usage: bash tools/ab_env.sh TAG ROUNDS "ENV1" "ENV2" ...   (ENV "-" = none)
 set -o pipefail
-T=$1; shift
-O=gpurun_out/$T
-mkdir -p $O
-i=0
-for kv in "$@"; do
-  i=$((i+1))
-  env $kv timeout -k 10 240 python -u bench.py --steps 50 --no-cpu-baseline > $O/$i.json 2> $O/$i.err || { echo "run $i ($kv) failed"; tail -5 $O/$i.err; exit 1; }
-  python3 -c "
-import json,sys
-d=json.loads(open('$O/$i.json').read().strip().splitlines()[-1])
-print('$kv', round(d['value']/1e9,3), 'G/s step_us', round(d['ms_per_step']*1e3,1), {k: round(v*1e3,1) for k,v in d['kernel_ms_per_launch'].items()}, 'iso', {k: round(v*1e3,1) for k,v in d['roofline_isolated']['kernel_ms_per_launch'].items()})"
+O=gpurun_out/$1; shift; N=$1; shift; mkdir -p $O
+for r in $(seq 1 $N); do
+  i=0
+  for e in "$@"; do
+    i=$((i+1))
+    if [ "$e" = "-" ]; then e=""; fi
+    env $e timeout -k 10 300 python bench.py --steps 3 --warmup 1 --no-cpu-baseline --bloom-fill ${FILL:-1000000000} $BARGS > $O/r${r}_$i.json 2> $O/r${r}_$i.err || { tail $O/r${r}_$i.err; exit 1; }
+  done
 done
+python - $O $N $# <<'PY'
+import json,sys
+O,N,M=sys.argv[1],int(sys.argv[2]),int(sys.argv[3])
+for i in range(1,M+1):
+    rows=[json.load(open(f"{O}/r{r}_{i}.json")) for r in range(1,N+1)]
+    print(i, "value", ["%.3e"%d["value"] for d in rows], {k:[round(d["kernels"][k]["ms_isolated"],4) for d in rows] for k in rows[0]["kernels"]})
+PY

@@ -110,13 +110,13 @@ def c1(eng, args):
 
 def c2zipf(eng, args):
     """SURVEY 8d C2 variant: 1M-command PFADD batches with Zipf(1.1) tenants (device-resident)."""
-    B, steps, nt = 1 << 20, 10, 100_000
+    B, steps, nt, G = 1 << 20, 10, 100_000, 64
     names = [b"tenant:%d:hll" % t for t in range(nt)]
     ids = eng.hll_resolve(names)
     rng = np.random.default_rng(22)
-    kid = (np.minimum(rng.zipf(1.1, B * (steps + 1)), nt) - 1).astype(np.int64)
+    kid = (np.minimum(rng.zipf(1.1, B * (steps + 1 + G)), nt) - 1).astype(np.int64)
     d_ids = eng.to_device(ids[kid].astype(np.uint32))
-    off, byt, tot = eng.gen_jackson_longs_dev(0x5EED0022, B * (steps + 1))
+    off, byt, tot = eng.gen_jackson_longs_dev(0x5EED0022, B * (steps + 1 + G))
     d_out = eng.alloc(B)
     eng.pfadd_dev(B, d_ids, off, byt, tot, d_out)            # warm
     eng.set_async(True)
@@ -125,8 +125,12 @@ def c2zipf(eng, args):
     eng.set_async(False)
     t_sync = timed(eng, lambda: [eng.pfadd_dev(B, d_ids.ptr + s * B * 4, off.ptr + s * B * 8, byt, tot, d_out)
                                  for s in range(1, steps + 1)])
-    d_out10 = eng.alloc(B * steps)   # group commit: the 10 batches as one call (line schedule)
-    t_g = timed(eng, lambda: eng.pfadd_dev(B * steps, d_ids.ptr + B * 4, off.ptr + B * 8, byt, tot, d_out10))
+    d_out10 = eng.alloc(B * G)   # group commit: G fresh batches as one call (line schedule), as in bench.py's step
+    eng.prof_reset(); eng.prof_enable(True)
+    g0 = steps + 1   # batches not applied yet
+    t_g = timed(eng, lambda: eng.pfadd_dev(B * G, d_ids.ptr + g0 * B * 4, off.ptr + g0 * B * 8, byt, tot, d_out10))
+    eng.prof_enable(False)
+    g_ms = {p: eng.prof_read(p)[1] for p in ("pfl_hash", "pfl_part", "pfl_apply")}
     d_out10.free()
     top = float(np.bincount(kid[:B]).max()) / B
     # per-key PFCOUNT of every tenant (C2): the histogram kernel alone, and the whole RHyperLogLog.count path
@@ -144,7 +148,8 @@ def c2zipf(eng, args):
           "unit": "inserts/s", "config": {"workload": "c2zipf", "batch": B, "tenants": nt, "zipf_s": 1.1,
                                           "hottest_tenant_share": top},
           "synchronous_calls_inserts_per_s": B * steps / t_sync,
-          "group_commit_inserts_per_s": B * steps / t_g,
+          "group_commit_inserts_per_s": B * G / t_g, "group_commit_kernel_ms": g_ms,
+          "group_commit": "%d fresh 1M batches as one call (line schedule), host-timed" % G,
           "pfcount_keys_per_s": nt / t_c, "pfcount_ids_keys_per_s": nt / t_ci, "hist_keys_per_s_host_timed": nt / t_h,
           "roofline": {"kernel": "hll_hist", "bound": "hbm", "achieved": gbs, "peak": PEAK, "unit": "GB/s",
                        "frac": gbs / PEAK, "bytes_per_unit": 16384, "avg_launch_ms": k_ms}})

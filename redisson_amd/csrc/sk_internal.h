@@ -50,6 +50,8 @@ hipError_t launch_pfp_reply(hipStream_t st, uint64_t n, const uint8_t *rep, cons
 struct PflDims {
     uint32_t nblk, tb, ntile, nsub, nsums; // hash blocks, blocks per run tile, tiles, fine buckets per bucket
     uint32_t sh;                           // 2^sh sketches per fine bucket
+    uint32_t pk, pa, pai, pm_mask;         // fine buckets by permuted slab id: slab * pa mod 2^pk
+    uint32_t nslab;
     uint64_t nf, ncount;         // fine buckets; run counts (C holds ncount + 1 words)
     uint64_t chunk_bytes, S_bytes;
 };

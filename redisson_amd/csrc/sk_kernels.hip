@@ -922,9 +922,19 @@ __device__ __forceinline__ void pfl_bt(uint32_t ntile, uint32_t *b, uint32_t *ti
     *tile = q % ntile;
 }
 
+// Fine buckets take sketches by a permuted slab id, p = slab * pa mod 2^pk (pa odd, a bijection): slabs are
+// handed out in key-creation order, so consecutive slabs -- a batch of tenants created together, the head of a
+// Zipf key space -- would otherwise share fine buckets and pile their records onto a few workgroups.
+struct PflPerm {
+    uint32_t pa, pai, mask; // multiplier, its inverse mod 2^pk, 2^pk - 1
+    uint32_t nslab;         // slab ids >= nslab (never handed out) are dropped by count and scatter alike
+    __device__ __forceinline__ uint32_t fwd(uint32_t slab) const { return (slab * pa) & mask; }
+    __device__ __forceinline__ uint32_t inv(uint32_t p) const { return (p * pai) & mask; }
+};
+
 __global__ void __launch_bounds__(SK_PFL_BTPB) k_pfl_count(const uint64_t *__restrict__ chunks,
                                                            const uint32_t *__restrict__ S, uint32_t nblk, uint32_t tb,
-                                                           uint32_t ntile, uint32_t nsub, uint32_t sh,
+                                                           uint32_t ntile, uint32_t nsub, uint32_t sh, PflPerm pm,
                                                            uint32_t *__restrict__ C) {
     extern __shared__ uint32_t hist[]; // nsub words
     for (uint32_t s = threadIdx.x; s < nsub; s += SK_PFL_BTPB) hist[s] = 0;
@@ -936,8 +946,8 @@ __global__ void __launch_bounds__(SK_PFL_BTPB) k_pfl_count(const uint64_t *__res
         const uint32_t lo = S[uint64_t(b) * nblk + blk], hi = S[uint64_t(b + 1) * nblk + blk];
         const uint64_t *seg = chunks + uint64_t(blk) * SK_PFP_EPB;
         for (uint32_t t = lo + (threadIdx.x & 3u); t < hi; t += 4) {
-            const uint32_t sb = uint32_t(seg[t] >> 32) >> sh;
-            if (sb < nsub) atomicAdd(&hist[sb], 1u); // ids beyond the store's slabs are dropped (both passes)
+            const uint32_t sl = uint32_t(seg[t] >> 32);
+            if (sl < pm.nslab) atomicAdd(&hist[pm.fwd(sl) >> sh], 1u); // ids beyond the store's slabs are dropped
         }
     }
     __syncthreads();
@@ -953,7 +963,7 @@ __global__ void __launch_bounds__(SK_PFL_BTPB) k_pfl_count(const uint64_t *__res
 __global__ void __launch_bounds__(SK_PFL_BTPB) k_pfl_scatter(const uint64_t *__restrict__ chunks,
                                                              const uint32_t *__restrict__ S, uint32_t nblk,
                                                              uint32_t tb, uint32_t ntile, uint32_t nsub, uint32_t sh,
-                                                             const uint32_t *__restrict__ C,
+                                                             PflPerm pm, const uint32_t *__restrict__ C,
                                                              uint64_t *__restrict__ rec2) {
     constexpr int PER = SK_PFL_PIECE / SK_PFL_BTPB;
     extern __shared__ uint32_t dyn[];
@@ -1005,8 +1015,9 @@ __global__ void __launch_bounds__(SK_PFL_BTPB) k_pfl_scatter(const uint64_t *__r
             }
             const uint32_t blk = b0 + lo;
             const uint64_t rr = chunks[uint64_t(blk) * SK_PFP_EPB + S[uint64_t(b) * nblk + blk] + (x - segp[lo])];
-            const uint32_t slab = uint32_t(rr >> 32), reg = uint32_t(rr >> 18) & 16383u, rho = uint32_t(rr >> 12) & 63u;
-            if ((slab >> sh) >= nsub) continue; // ids beyond the store's slabs are dropped (both passes)
+            if (uint32_t(rr >> 32) >= pm.nslab) continue; // ids beyond the store's slabs are dropped (both passes)
+            const uint32_t slab = pm.fwd(uint32_t(rr >> 32)), reg = uint32_t(rr >> 18) & 16383u,
+                           rho = uint32_t(rr >> 12) & 63u;
             r[q] = (uint64_t(slab & ((1u << sh) - 1)) << 46) | (uint64_t(reg) << 32) | (uint64_t(rho) << 26) |
                    (uint64_t(blk) * SK_PFP_EPB + (rr & 4095u));
             rk[q] = atomicAdd(&lcnt[slab >> sh], 1u) | ((slab >> sh) << 13);
@@ -1145,7 +1156,8 @@ __device__ __forceinline__ void pfl_chunk(const uint64_t *R, uint32_t cnt, uint1
 
 __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const uint64_t *__restrict__ rec2,
                                                            const uint32_t *__restrict__ C, uint32_t ntile,
-                                                           uint32_t nsub, uint32_t sh, uint32_t nslab, uint8_t *arena,
+                                                           uint32_t nsub, uint32_t sh, PflPerm pm, uint32_t nslab,
+                                                           uint8_t *arena,
                                                            uint8_t *__restrict__ changed, uint32_t *big_alloc,
                                                            uint64_t *big_keys, uint32_t *big_vals, int probe) {
     constexpr uint32_t NL = 1u << SK_PFL_SH;
@@ -1166,9 +1178,9 @@ __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const uint64_t *__res
     const uint64_t c0 = uint64_t(f) * ntile;
     const uint32_t start = C[c0], end = C[c0 + ntile], cnt = end - start;
     if (cnt == 0) return; // uniform
-    const uint32_t slab0 = sub << sh, nsl = nslab - slab0 < (1u << sh) ? nslab - slab0 : (1u << sh);
+    const uint32_t slab0 = sub << sh, nsl = 1u << sh; // permuted ids slab0 + i, i < nsl
     auto line = [&](uint32_t i) -> uint4 * {
-        const uint32_t s = slab0 + i;
+        const uint32_t s = pm.inv(slab0 + i);
         return reinterpret_cast<uint4 *>(arena + (uint64_t(s) << 14) + (((b - pfl_rot(s)) & (SK_PFL_NB - 1)) << SK_PFL_LB));
     };
     for (uint32_t i = threadIdx.x; i < NL; i += SK_PFL_ATPB) dirty[i] = 0;
@@ -1180,7 +1192,8 @@ __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const uint64_t *__res
 #pragma unroll
         for (int j = 0; j < LQ; j++) {
             const uint32_t q = threadIdx.x + j * SK_PFL_ATPB;
-            if (q < nsl * LW) lv[j] = (probe & 4) ? make_uint4(0, 0, 0, 0) : line(q / LW)[q % LW];
+            if (q < nsl * LW && pm.inv(slab0 + q / LW) < nslab)
+                lv[j] = (probe & 4) ? make_uint4(0, 0, 0, 0) : line(q / LW)[q % LW];
         }
         for (uint32_t u = threadIdx.x; u < cnt; u += SK_PFL_ATPB) R[u] = rec2[start + u];
         __syncthreads();
@@ -1188,11 +1201,12 @@ __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const uint64_t *__res
 #pragma unroll
             for (int j = 0; j < LQ; j++) {
                 const uint32_t q = threadIdx.x + j * SK_PFL_ATPB;
-                if (q < nsl * LW) regs4[q] = lv[j];
+                if (q < nsl * LW && pm.inv(slab0 + q / LW) < nslab) regs4[q] = lv[j];
             }
         });
     } else {
-        for (uint32_t q = threadIdx.x; q < nsl * LW; q += SK_PFL_ATPB) regs4[q] = line(q / LW)[q % LW];
+        for (uint32_t q = threadIdx.x; q < nsl * LW; q += SK_PFL_ATPB)
+            if (pm.inv(slab0 + q / LW) < nslab) regs4[q] = line(q / LW)[q % LW];
         __syncthreads();
         uint32_t t0 = 0;
         while (t0 < ntile) { // uniform: chunks of whole runs, in tile (= batch) order
@@ -2552,9 +2566,18 @@ PflDims pfl_dims(uint64_t n, uint32_t nslab, uint32_t tile_blocks) {
     // chunk), within the LDS lines (2^SK_PFL_SH) and the scatter's fine-bucket arrays (SK_PFL_MAXSUB)
     d.sh = SK_PFL_SH;
     while (d.sh > 0 && double(n) * double(1u << d.sh) > 768.0 * SK_PFL_NB * double(nslab ? nslab : 1) &&
-           ((uint64_t(nslab) + (1u << (d.sh - 1)) - 1) >> (d.sh - 1)) <= SK_PFL_MAXSUB)
+           ((2 * uint64_t(nslab) + (1u << (d.sh - 1)) - 1) >> (d.sh - 1)) <= SK_PFL_MAXSUB)
         d.sh--;
-    d.nsub = (nslab + (1u << d.sh) - 1) >> d.sh;
+    // permutation over 2^pk >= nslab ids (>= one fine bucket); the inverse of an odd pa mod 2^32 by Newton steps
+    d.pk = d.sh;
+    while (d.pk < 32 && (1ull << d.pk) < nslab) d.pk++;
+    d.pm_mask = d.pk >= 32 ? 0xffffffffu : uint32_t((1ull << d.pk) - 1);
+    d.pa = 0x9E3779B1u;
+    uint32_t inv = d.pa; // x <- x (2 - a x): correct bits double each step
+    for (int it = 0; it < 5; it++) inv *= 2u - d.pa * inv;
+    d.pai = inv;
+    d.nsub = uint32_t((uint64_t(d.pm_mask) + 1) >> d.sh);
+    d.nslab = nslab;
     d.nf = uint64_t(SK_PFL_NB) * d.nsub;
     d.ncount = d.nf * d.ntile;
     d.nsums = uint32_t((d.ncount + SK_SCAN_ITEMS - 1) / SK_SCAN_ITEMS);
@@ -2562,7 +2585,7 @@ PflDims pfl_dims(uint64_t n, uint32_t nslab, uint32_t tile_blocks) {
     d.S_bytes = uint64_t(SK_PFL_NB + 1) * d.nblk * 4;
     return d;
 }
-uint32_t pfl_max_slabs() { return SK_PFL_MAXSUB << SK_PFL_SH; }
+uint32_t pfl_max_slabs() { return (SK_PFL_MAXSUB << SK_PFL_SH) / 2; } // the permuted id range is < 2 x nslab
 
 hipError_t launch_pfl_hash(hipStream_t st, uint64_t n, const uint32_t *key_ids, const uint64_t *off,
                            const uint8_t *bytes, int v5, uint64_t *chunks, uint32_t *S, uint32_t *big_alloc) {
@@ -2577,7 +2600,7 @@ hipError_t launch_pfl_part(hipStream_t st, const PflDims &d, const uint64_t *chu
                            uint32_t *sums, uint64_t *rec2) {
     if (d.nsub > SK_PFL_MAXSUB || d.tb > SK_PFL_TMAX || d.ncount >= (1ull << 32)) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_pfl_count, dim3(d.ntile * SK_PFL_NB), dim3(SK_PFL_BTPB), d.nsub * 4, st, chunks, S, d.nblk,
-                       d.tb, d.ntile, d.nsub, d.sh, C);
+                       d.tb, d.ntile, d.nsub, d.sh, PflPerm{d.pa, d.pai, d.pm_mask, d.nslab}, C);
     SK_LAUNCH_CHECK();
     hipLaunchKernelGGL(k_scan_reduce, dim3(d.nsums), dim3(SK_SCAN_TPB), 0, st, d.ncount, C, sums);
     SK_LAUNCH_CHECK();
@@ -2586,7 +2609,7 @@ hipError_t launch_pfl_part(hipStream_t st, const PflDims &d, const uint64_t *chu
     hipLaunchKernelGGL(k_scan_apply, dim3(d.nsums), dim3(SK_SCAN_TPB), 0, st, d.ncount, C, sums);
     SK_LAUNCH_CHECK();
     hipLaunchKernelGGL(k_pfl_scatter, dim3(d.ntile * SK_PFL_NB), dim3(SK_PFL_BTPB), 2 * d.nsub * 4, st, chunks, S,
-                       d.nblk, d.tb, d.ntile, d.nsub, d.sh, C, rec2);
+                       d.nblk, d.tb, d.ntile, d.nsub, d.sh, PflPerm{d.pa, d.pai, d.pm_mask, d.nslab}, C, rec2);
     SK_LAUNCH_CHECK();
     return hipSuccess;
 }
@@ -2594,7 +2617,8 @@ hipError_t launch_pfl_part(hipStream_t st, const PflDims &d, const uint64_t *chu
 hipError_t launch_pfl_apply(hipStream_t st, const PflDims &d, const uint64_t *rec2, const uint32_t *C, uint32_t nslab,
                             uint8_t *arena, uint8_t *changed, uint32_t *big_alloc, uint64_t *big_keys,
                             uint32_t *big_vals) {
-    hipLaunchKernelGGL(k_pfl_apply, dim3(uint32_t(d.nf)), dim3(SK_PFL_ATPB), 0, st, rec2, C, d.ntile, d.nsub, d.sh, nslab,
+    hipLaunchKernelGGL(k_pfl_apply, dim3(uint32_t(d.nf)), dim3(SK_PFL_ATPB), 0, st, rec2, C, d.ntile, d.nsub, d.sh,
+                       PflPerm{d.pa, d.pai, d.pm_mask, d.nslab}, nslab,
                        arena, changed, big_alloc, big_keys, big_vals, getenv("SK_PFL_PROBE") ? atoi(getenv("SK_PFL_PROBE")) : 0);
     SK_LAUNCH_CHECK();
     return hipSuccess;

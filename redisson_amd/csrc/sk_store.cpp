@@ -1014,6 +1014,13 @@ int pfadd_lines(sk_ctx *c, uint64_t n, const uint32_t *d_ids, const uint64_t *d_
     HIPCHK(c, sk::launch_pfl_apply(c->st, d, c->pfl_rec.as<uint64_t>(), c->pfl_C.as<uint32_t>(), nslab, c->arena,
                                    d_changed, c->pfl_ovf.as<uint32_t>(), c->pfl_bk.as<uint64_t>(),
                                    c->pfl_bv.as<uint32_t>())); }
+    if (getenv("SK_PFL_DEBUG")) { // dev: table entries the oversized runs took (2 per record of a min-seq table run)
+        uint32_t big = 0;
+        HIPCHK(c, hipMemcpyAsync(&big, c->pfl_ovf.p, 4, hipMemcpyDeviceToHost, c->st));
+        HIPCHK(c, hipStreamSynchronize(c->st));
+        fprintf(stderr, "[pfl] n=%llu sh=%u nsub=%u ntile=%u big-table records=%u\n", (unsigned long long)n, d.sh,
+                d.nsub, d.ntile, big / 2);
+    }
     return SK_OK;
 }
 

@@ -1141,8 +1141,7 @@ __device__ __forceinline__ void pfl_chunk(const uint64_t *R, uint32_t cnt, uint1
         const uint32_t slotb = pfl_slotb(key);
         const uint32_t R0 = reg[slotb];
         const uint8_t rep = rho > (R0 > p ? R0 : p);
-        if (probe & 8) __builtin_nontemporal_store(rep, changed + seq);
-        else changed[seq] = rep;
+        if (!(probe & 32) || rep) changed[seq] = rep; // probe & 32: the replies were zeroed, only 1s are stored
         fin[u] = earliest && m > R0 ? uint8_t(m) : uint8_t(0);
     }
     __syncthreads();
@@ -1228,7 +1227,7 @@ __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const uint64_t *__res
                     if (u < k) R[u] = rr[q];
                 }
                 __syncthreads();
-                pfl_chunk(R, k, nxt, head, fin, reg, dirty, changed, 0, [] {});
+                pfl_chunk(R, k, nxt, head, fin, reg, dirty, changed, probe, [] {});
             } else { // one run larger than a chunk (t1 == t0 + 1)
                 // only records above their register can rise, and only they can stop a later record from rising:
                 // the rest reply 0 now; the candidates are resolved as a chunk when they fit (a hot sketch whose
@@ -1252,14 +1251,14 @@ __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const uint64_t *__res
                             const uint32_t i = atomicAdd(&ncand, 1u);
                             if (i < SK_PFL_CAP) R[i] = r;
                         } else {
-                            changed[r & 0x3ffffffu] = 0;
+                            if (!(probe & 32)) changed[r & 0x3ffffffu] = 0;
                         }
                     }
                 }
                 __syncthreads();
                 const uint32_t nc = ncand;
                 if (nc <= SK_PFL_CAP) {
-                    pfl_chunk(R, nc, nxt, head, fin, reg, dirty, changed, 0, [] {});
+                    pfl_chunk(R, nc, nxt, head, fin, reg, dirty, changed, probe, [] {});
                 } else {
                 __shared__ uint32_t gbase;
                 unsigned long long *lk = reinterpret_cast<unsigned long long *>(work);
@@ -1288,7 +1287,7 @@ __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const uint64_t *__res
                     const uint32_t rho = uint32_t(r >> 26) & 63u, seq = uint32_t(r & 0x3ffffffu);
                     bool first = true;
                     for (uint32_t v = rho; v < 52 && first; v++) first = T.find((key << 6) | v) >= seq;
-                    changed[seq] = first ? 1 : 0;
+                    if (!(probe & 32) || first) changed[seq] = first ? 1 : 0;
                 }
                 __syncthreads();
                 for (uint32_t u = threadIdx.x; u < k; u += SK_PFL_ATPB) { // the register's writer: its top record
@@ -2616,10 +2615,10 @@ hipError_t launch_pfl_part(hipStream_t st, const PflDims &d, const uint64_t *chu
 
 hipError_t launch_pfl_apply(hipStream_t st, const PflDims &d, const uint64_t *rec2, const uint32_t *C, uint32_t nslab,
                             uint8_t *arena, uint8_t *changed, uint32_t *big_alloc, uint64_t *big_keys,
-                            uint32_t *big_vals) {
+                            uint32_t *big_vals, int flags) {
     hipLaunchKernelGGL(k_pfl_apply, dim3(uint32_t(d.nf)), dim3(SK_PFL_ATPB), 0, st, rec2, C, d.ntile, d.nsub, d.sh,
                        PflPerm{d.pa, d.pai, d.pm_mask, d.nslab}, nslab,
-                       arena, changed, big_alloc, big_keys, big_vals, getenv("SK_PFL_PROBE") ? atoi(getenv("SK_PFL_PROBE")) : 0);
+                       arena, changed, big_alloc, big_keys, big_vals, flags | (getenv("SK_PFL_PROBE") ? atoi(getenv("SK_PFL_PROBE")) : 0));
     SK_LAUNCH_CHECK();
     return hipSuccess;
 }

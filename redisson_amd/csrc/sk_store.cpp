@@ -288,6 +288,7 @@ struct sk_ctx {
     // pfl_min one-element commands (SK_PFL_MIN, 0 = never): scratch of one call
     uint64_t pfl_min = 4u << 20;
     uint32_t pfl_tile = 0;      // hash blocks per run tile (SK_PFL_TILE, 0 = the kernel default)
+    bool pfl_zero = true;       // replies pre-zeroed, the apply stores only the 1s (SK_PFL_ZERO)
     DBuf pfl_chunks, pfl_S, pfl_C, pfl_sums, pfl_rec, pfl_bk, pfl_bv, pfl_ovf;
 };
 
@@ -1010,10 +1011,13 @@ int pfadd_lines(sk_ctx *c, uint64_t n, const uint32_t *d_ids, const uint64_t *d_
     { Prof p_(c, 25);
     HIPCHK(c, sk::launch_pfl_part(c->st, d, c->pfl_chunks.as<uint64_t>(), c->pfl_S.as<uint32_t>(),
                                   c->pfl_C.as<uint32_t>(), c->pfl_sums.as<uint32_t>(), c->pfl_rec.as<uint64_t>())); }
+    // replies: zeroed by one streaming memset, then the apply stores only the 1s (a register rise), instead of one
+    // scattered byte per element (SK_PFL_ZERO=0: every reply stored by the apply)
+    if (c->pfl_zero) HIPCHK(c, hipMemsetAsync(d_changed, 0, n, c->st));
     { Prof p_(c, 26);
     HIPCHK(c, sk::launch_pfl_apply(c->st, d, c->pfl_rec.as<uint64_t>(), c->pfl_C.as<uint32_t>(), nslab, c->arena,
                                    d_changed, c->pfl_ovf.as<uint32_t>(), c->pfl_bk.as<uint64_t>(),
-                                   c->pfl_bv.as<uint32_t>())); }
+                                   c->pfl_bv.as<uint32_t>(), c->pfl_zero ? 32 : 0)); }
     if (getenv("SK_PFL_DEBUG")) { // dev: table entries the oversized runs took (2 per record of a min-seq table run)
         uint32_t big = 0;
         HIPCHK(c, hipMemcpyAsync(&big, c->pfl_ovf.p, 4, hipMemcpyDeviceToHost, c->st));
@@ -1181,6 +1185,7 @@ int sk_open(const sk_config *cfg, sk_ctx **out) {
     if (const char *e = getenv("SK_PFP_PIPE")) c->pfp_pipe = atoi(e) != 0;
     if (const char *e = getenv("SK_PFL_MIN")) c->pfl_min = strtoull(e, nullptr, 10);
     if (const char *e = getenv("SK_PFL_TILE")) c->pfl_tile = uint32_t(strtoul(e, nullptr, 10));
+    if (const char *e = getenv("SK_PFL_ZERO")) c->pfl_zero = atoi(e) != 0;
     uint64_t cap = (cfg && cfg->hll_capacity) ? cfg->hll_capacity : 1024;
     if (hll_grow(c, cap) != SK_OK || c->misc.ensure(4096) != hipSuccess ||
         hipMalloc(&c->d_zero, 16) != hipSuccess || hipMemsetAsync(c->d_zero, 0, 16, c->st) != hipSuccess ||

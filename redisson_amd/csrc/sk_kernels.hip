@@ -968,6 +968,7 @@ __global__ void __launch_bounds__(SK_PFL_BTPB) k_pfl_scatter(const uint64_t *__r
     constexpr int PER = SK_PFL_PIECE / SK_PFL_BTPB;
     extern __shared__ uint32_t dyn[];
     __shared__ uint32_t segp[SK_PFL_TMAX + 1]; // prefix of the tile's segment lengths
+    __shared__ uint32_t segs[SK_PFL_TMAX];     // each segment's start in its block chunk
     __shared__ uint64_t sorted[SK_PFL_PIECE];
     __shared__ uint32_t wsum[SK_PFL_BTPB / 64];
     uint32_t *cur = dyn, *lcnt = dyn + nsub;
@@ -985,7 +986,11 @@ __global__ void __launch_bounds__(SK_PFL_BTPB) k_pfl_scatter(const uint64_t *__r
     for (int q = 0; q < SP; q++) {
         const uint32_t j = threadIdx.x * SP + q;
         sl[q] = 0;
-        if (j < nb) sl[q] = S[uint64_t(b + 1) * nblk + b0 + j] - S[uint64_t(b) * nblk + b0 + j];
+        if (j < nb) {
+            const uint32_t st = S[uint64_t(b) * nblk + b0 + j];
+            sl[q] = S[uint64_t(b + 1) * nblk + b0 + j] - st;
+            segs[j] = st;
+        }
         ssum += sl[q];
     }
     uint32_t total;
@@ -1000,11 +1005,12 @@ __global__ void __launch_bounds__(SK_PFL_BTPB) k_pfl_scatter(const uint64_t *__r
     for (uint32_t base = 0; base < total; base += SK_PFL_PIECE) { // uniform
         const uint32_t m = total - base < SK_PFL_PIECE ? total - base : SK_PFL_PIECE;
         uint64_t r[PER];
-        uint32_t rk[PER];
+        uint32_t rk[PER], bl[PER];
 #pragma unroll
-        for (int q = 0; q < PER; q++) {
+        for (int q = 0; q < PER; q++) { // every load of the piece issued before any is used
             const uint32_t i = threadIdx.x + q * SK_PFL_BTPB;
             r[q] = ~0ull;
+            bl[q] = 0;
             if (i >= m) continue;
             const uint32_t x = base + i;
             uint32_t lo = 0, hi = nb; // segp[lo] <= x < segp[hi]
@@ -1013,8 +1019,15 @@ __global__ void __launch_bounds__(SK_PFL_BTPB) k_pfl_scatter(const uint64_t *__r
                 if (segp[mid] <= x) lo = mid;
                 else hi = mid;
             }
-            const uint32_t blk = b0 + lo;
-            const uint64_t rr = chunks[uint64_t(blk) * SK_PFP_EPB + S[uint64_t(b) * nblk + blk] + (x - segp[lo])];
+            bl[q] = b0 + lo;
+            r[q] = chunks[uint64_t(b0 + lo) * SK_PFP_EPB + segs[lo] + (x - segp[lo])];
+        }
+#pragma unroll
+        for (int q = 0; q < PER; q++) {
+            const uint64_t rr = r[q];
+            const uint32_t blk = bl[q];
+            r[q] = ~0ull;
+            if (threadIdx.x + q * SK_PFL_BTPB >= m) continue;
             if (uint32_t(rr >> 32) >= pm.nslab) continue; // ids beyond the store's slabs are dropped (both passes)
             const uint32_t slab = pm.fwd(uint32_t(rr >> 32)), reg = uint32_t(rr >> 18) & 16383u,
                            rho = uint32_t(rr >> 12) & 63u;

@@ -1002,12 +1002,11 @@ __global__ void __launch_bounds__(SK_PFL_BTPB) k_pfl_scatter(const uint64_t *__r
     }
     if (threadIdx.x == 0) segp[SK_PFL_TMAX] = total;
     __syncthreads();
-    for (uint32_t base = 0; base < total; base += SK_PFL_PIECE) { // uniform
+    // a piece's record loads, all issued before any is used; the next piece's are issued while this one is sorted
+    auto load = [&](uint32_t base, uint64_t (&r)[PER], uint32_t (&bl)[PER]) {
         const uint32_t m = total - base < SK_PFL_PIECE ? total - base : SK_PFL_PIECE;
-        uint64_t r[PER];
-        uint32_t rk[PER], bl[PER];
 #pragma unroll
-        for (int q = 0; q < PER; q++) { // every load of the piece issued before any is used
+        for (int q = 0; q < PER; q++) {
             const uint32_t i = threadIdx.x + q * SK_PFL_BTPB;
             r[q] = ~0ull;
             bl[q] = 0;
@@ -1022,6 +1021,13 @@ __global__ void __launch_bounds__(SK_PFL_BTPB) k_pfl_scatter(const uint64_t *__r
             bl[q] = b0 + lo;
             r[q] = chunks[uint64_t(b0 + lo) * SK_PFP_EPB + segs[lo] + (x - segp[lo])];
         }
+    };
+    uint64_t r[PER];
+    uint32_t bl[PER];
+    if (total) load(0, r, bl);
+    for (uint32_t base = 0; base < total; base += SK_PFL_PIECE) { // uniform
+        const uint32_t m = total - base < SK_PFL_PIECE ? total - base : SK_PFL_PIECE;
+        uint32_t rk[PER];
 #pragma unroll
         for (int q = 0; q < PER; q++) {
             const uint64_t rr = r[q];
@@ -1035,6 +1041,9 @@ __global__ void __launch_bounds__(SK_PFL_BTPB) k_pfl_scatter(const uint64_t *__r
                    (uint64_t(blk) * SK_PFP_EPB + (rr & 4095u));
             rk[q] = atomicAdd(&lcnt[slab >> sh], 1u) | ((slab >> sh) << 13);
         }
+        uint64_t rn[PER];
+        uint32_t bln[PER];
+        if (base + SK_PFL_PIECE < total) load(base + SK_PFL_PIECE, rn, bln);
         __syncthreads();
         // exclusive scan of the piece's counts over the fine buckets (in place), nsub <= SK_PFL_MAXSUB
         uint32_t acc = 0;
@@ -1071,6 +1080,11 @@ __global__ void __launch_bounds__(SK_PFL_BTPB) k_pfl_scatter(const uint64_t *__r
         __syncthreads();
         for (uint32_t x = threadIdx.x; x < nsub; x += SK_PFL_BTPB) lcnt[x] = 0;
         __syncthreads();
+#pragma unroll
+        for (int q = 0; q < PER; q++) {
+            r[q] = rn[q];
+            bl[q] = bln[q];
+        }
     }
 }
 

@@ -942,13 +942,29 @@ __global__ void __launch_bounds__(SK_PFL_BTPB) k_pfl_count(const uint64_t *__res
     uint32_t b, tile;
     pfl_bt(ntile, &b, &tile);
     const uint32_t b0 = tile * tb, b1 = b0 + tb < nblk ? b0 + tb : nblk;
-    for (uint32_t blk = b0 + (threadIdx.x >> 2); blk < b1; blk += SK_PFL_BTPB / 4) {
-        const uint32_t lo = S[uint64_t(b) * nblk + blk], hi = S[uint64_t(b + 1) * nblk + blk];
+    // 4 threads per block segment; the segment bounds of the thread's next block are loaded while this one is
+    // counted, and a segment's records are loaded 8 per thread before any is counted
+    uint32_t blk = b0 + (threadIdx.x >> 2);
+    uint32_t lo = 0, hi = 0;
+    if (blk < b1) lo = S[uint64_t(b) * nblk + blk], hi = S[uint64_t(b + 1) * nblk + blk];
+    for (; blk < b1; blk += SK_PFL_BTPB / 4) {
+        const uint32_t nx = blk + SK_PFL_BTPB / 4;
+        uint32_t lo2 = 0, hi2 = 0;
+        if (nx < b1) lo2 = S[uint64_t(b) * nblk + nx], hi2 = S[uint64_t(b + 1) * nblk + nx];
         const uint64_t *seg = chunks + uint64_t(blk) * SK_PFP_EPB;
-        for (uint32_t t = lo + (threadIdx.x & 3u); t < hi; t += 4) {
-            const uint32_t sl = uint32_t(seg[t] >> 32);
-            if (sl < pm.nslab) atomicAdd(&hist[pm.fwd(sl) >> sh], 1u); // ids beyond the store's slabs are dropped
+        for (uint32_t t0 = lo + (threadIdx.x & 3u); t0 < hi; t0 += 32) {
+            uint32_t sl[8];
+#pragma unroll
+            for (int q = 0; q < 8; q++) {
+                const uint32_t t = t0 + 4 * q;
+                sl[q] = t < hi ? uint32_t(seg[t] >> 32) : 0xffffffffu;
+            }
+#pragma unroll
+            for (int q = 0; q < 8; q++) // ids beyond the store's slabs are dropped (both passes)
+                if (sl[q] < pm.nslab) atomicAdd(&hist[pm.fwd(sl[q]) >> sh], 1u);
         }
+        lo = lo2;
+        hi = hi2;
     }
     __syncthreads();
     for (uint32_t s = threadIdx.x; s < nsub; s += SK_PFL_BTPB)

@@ -331,8 +331,8 @@ template <int NT> __device__ __forceinline__ uint32_t block_exscan(uint32_t v, u
 // e+1 are issued (into registers) before round e is hashed, so one barrier
 // per round is the only wait; every element's offsets and slab id are loaded
 // up front.  Windows that do not fit fall back to direct global reads.
-#define SK_PFP_WIN 6144 // u64 words per key window (48 KiB; 1024 keys of mean length <= ~46 B)
-#define SK_PFP_WVEC (SK_PFP_WIN * 8 / 16 / SK_PFP_TPB) // 16-B vectors per thread per window
+#define SK_PFP_WIN 5056 // u64 words per key window (39.5 KiB: 1024 keys of mean length <= ~39 B; two hash workgroups per CU)
+#define SK_PFP_WVEC ((SK_PFP_WIN * 8 / 16 + SK_PFP_TPB - 1) / SK_PFP_TPB) // 16-B vectors per thread per window (loads and stores stop at the window's vectors)
 __device__ __forceinline__ bool pfp_win_fits(uint64_t lo, uint64_t hi) {
     return (hi - (lo & ~uint64_t(15))) + 32 <= uint64_t(SK_PFP_WIN) * 8;
 }

@@ -5,7 +5,7 @@
 set -e
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/prof_${1:-r01}
-ARGS=${BENCH_ARGS:-"--steps 10 --warmup 2 --no-cpu-baseline"}
+ARGS=${BENCH_ARGS:-"--steps 3 --warmup 1 --no-cpu-baseline"}
 KSEL='sk::'
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp

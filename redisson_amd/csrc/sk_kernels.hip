@@ -13,7 +13,6 @@
 // touched slot (rocPRIM) followed by a segment-head walk in batch order; the
 // final state (max / OR) needs no atomics because each slot has one head.
 #include <hip/hip_runtime.h>
-#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 #include <rocprim/device/device_radix_sort.hpp>
@@ -1198,7 +1197,7 @@ __device__ __forceinline__ void pfl_chunk(const uint64_t *R, uint32_t cnt, uint1
 }
 
 __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const uint64_t *__restrict__ rec2,
-                                                           const uint32_t *__restrict__ C, uint32_t ntile, uint32_t nf,
+                                                           const uint32_t *__restrict__ C, uint32_t ntile,
                                                            uint32_t nsub, uint32_t sh, PflPerm pm, uint32_t nslab,
                                                            uint8_t *arena,
                                                            uint8_t *__restrict__ changed, uint32_t *big_alloc,
@@ -1217,191 +1216,157 @@ __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const uint64_t *__res
     uint32_t *head = reinterpret_cast<uint32_t *>(nxt + SK_PFL_CAP);
     uint8_t *fin = reinterpret_cast<uint8_t *>(head + SK_PFL_HT);
 
-    // persistent: workgroup w takes fine buckets w, w + G, ...; the next bucket's run bounds, lines and records
-    // (when it is one chunk) are loaded into registers while this one is applied, the bounds two buckets ahead
-    constexpr int LQ = (NL * LW + SK_PFL_ATPB - 1) / SK_PFL_ATPB;
-    constexpr int RQ = SK_PFL_CAP / SK_PFL_ATPB;
-    const uint32_t G = gridDim.x;
-    auto bounds = [&](uint32_t f, uint32_t &cs, uint32_t &ce) {
-        cs = ce = 0;
-        if (f < nf) cs = C[uint64_t(f) * ntile], ce = C[uint64_t(f) * ntile + ntile];
-    };
-    auto line_of = [&](uint32_t f, uint32_t i) -> uint4 * {
-        const uint32_t b = f / nsub, s = pm.inv(((f % nsub) << sh) + i);
+    const uint32_t f = blockIdx.x, b = f / nsub, sub = f % nsub;
+    const uint64_t c0 = uint64_t(f) * ntile;
+    const uint32_t start = C[c0], end = C[c0 + ntile], cnt = end - start;
+    if (cnt == 0) return; // uniform
+    const uint32_t slab0 = sub << sh, nsl = 1u << sh; // permuted ids slab0 + i, i < nsl
+    auto line = [&](uint32_t i) -> uint4 * {
+        const uint32_t s = pm.inv(slab0 + i);
         return reinterpret_cast<uint4 *>(arena + (uint64_t(s) << 14) + (((b - pfl_rot(s)) & (SK_PFL_NB - 1)) << SK_PFL_LB));
     };
-    auto valid = [&](uint32_t f, uint32_t i) { return pm.inv(((f % nsub) << sh) + i) < nslab; };
-    auto prefetch = [&](uint32_t f, uint32_t cs, uint32_t ce, uint4 (&lv)[LQ], uint64_t (&rv)[RQ]) {
-        if (f >= nf || ce - cs == 0 || ce - cs > SK_PFL_CAP) return; // uniform; big buckets load their own
+    for (uint32_t i = threadIdx.x; i < NL; i += SK_PFL_ATPB) dirty[i] = 0;
+    for (uint32_t t = threadIdx.x; t < SK_PFL_HT; t += SK_PFL_ATPB) head[t] = 0xffffu;
+    __syncthreads();
+    if (cnt <= SK_PFL_CAP) { // the whole fine bucket is one chunk: records and lines in one round trip
+        constexpr int LQ = (NL * LW + SK_PFL_ATPB - 1) / SK_PFL_ATPB;
+        uint4 lv[LQ];
 #pragma unroll
         for (int j = 0; j < LQ; j++) {
             const uint32_t q = threadIdx.x + j * SK_PFL_ATPB;
-            if (q < (NL * LW >> (SK_PFL_SH - sh)) && valid(f, q / LW))
-                lv[j] = (probe & 4) ? make_uint4(0, 0, 0, 0) : line_of(f, q / LW)[q % LW];
+            if (q < nsl * LW && pm.inv(slab0 + q / LW) < nslab)
+                lv[j] = (probe & 4) ? make_uint4(0, 0, 0, 0) : line(q / LW)[q % LW];
         }
-#pragma unroll
-        for (int q = 0; q < RQ; q++) {
-            const uint32_t u = q * SK_PFL_ATPB + threadIdx.x;
-            if (u < ce - cs) rv[q] = rec2[cs + u];
-        }
-    };
-    uint32_t f = blockIdx.x;
-    if (f >= nf) return;
-    uint32_t cs, ce, csn, cen;
-    bounds(f, cs, ce);
-    bounds(f + G, csn, cen);
-    uint4 lv[LQ];
-    uint64_t rv[RQ];
-    prefetch(f, cs, ce, lv, rv);
-    for (; f < nf; f += G) { // uniform
-        const uint32_t cnt = ce - cs, sub = f % nsub;
-        const uint64_t c0 = uint64_t(f) * ntile;
-        const uint32_t slab0 = sub << sh, nsl = 1u << sh; // permuted ids slab0 + i, i < nsl
-        auto line = [&](uint32_t i) -> uint4 * { return line_of(f, i); };
-        // the next bucket's loads go out now; the bounds of the one after it too
-        uint32_t csnn, cenn;
-        bounds(f + 2 * G, csnn, cenn);
-        uint4 lvn[LQ];
-        uint64_t rvn[RQ];
-        prefetch(f + G, csn, cen, lvn, rvn);
-        if (cnt != 0) { // uniform
-        for (uint32_t i = threadIdx.x; i < NL; i += SK_PFL_ATPB) dirty[i] = 0;
-        for (uint32_t t = threadIdx.x; t < SK_PFL_HT; t += SK_PFL_ATPB) head[t] = 0xffffu;
-        if (cnt <= SK_PFL_CAP) { // the whole fine bucket is one chunk, already in registers
-#pragma unroll
-            for (int q = 0; q < RQ; q++) {
-                const uint32_t u = q * SK_PFL_ATPB + threadIdx.x;
-                if (u < cnt) R[u] = rv[q];
-            }
-            __syncthreads();
-            pfl_chunk(R, cnt, nxt, head, fin, reg, dirty, changed, probe, [&] {
-#pragma unroll
-                for (int j = 0; j < LQ; j++) {
-                    const uint32_t q = threadIdx.x + j * SK_PFL_ATPB;
-                    if (q < nsl * LW && valid(f, q / LW)) regs4[q] = lv[j];
-                }
-            });
-        } else {
-            __syncthreads();
-            for (uint32_t q = threadIdx.x; q < nsl * LW; q += SK_PFL_ATPB)
-                if (pm.inv(slab0 + q / LW) < nslab) regs4[q] = line(q / LW)[q % LW];
-            __syncthreads();
-            uint32_t t0 = 0;
-            while (t0 < ntile) { // uniform: chunks of whole runs, in tile (= batch) order
-                const uint32_t a = C[c0 + t0];
-                uint32_t t1 = t0 + 1;
-                while (t1 < ntile && C[c0 + t1 + 1] - a <= SK_PFL_CAP) t1++;
-                const uint32_t z = C[c0 + t1], k = z - a;
-                if (k <= SK_PFL_CAP) {
-                    constexpr int CU = SK_PFL_CAP / SK_PFL_ATPB;
-                    uint64_t rr[CU];
-    #pragma unroll
-                    for (int q = 0; q < CU; q++) {
-                        const uint32_t u = q * SK_PFL_ATPB + threadIdx.x;
-                        if (u < k) rr[q] = rec2[a + u];
-                    }
-    #pragma unroll
-                    for (int q = 0; q < CU; q++) {
-                        const uint32_t u = q * SK_PFL_ATPB + threadIdx.x;
-                        if (u < k) R[u] = rr[q];
-                    }
-                    __syncthreads();
-                    pfl_chunk(R, k, nxt, head, fin, reg, dirty, changed, probe, [] {});
-                } else { // one run larger than a chunk (t1 == t0 + 1)
-                    // only records above their register can rise, and only they can stop a later record from rising:
-                    // the rest reply 0 now; the candidates are resolved as a chunk when they fit (a hot sketch whose
-                    // registers are already high has few), else with the (slot, rho) -> min seq table
-                    __shared__ uint32_t ncand;
-                    if (threadIdx.x == 0) ncand = 0;
-                    __syncthreads();
-                    constexpr int FU = 8; // records in flight per thread
-                    for (uint32_t u0 = 0; u0 < k; u0 += FU * SK_PFL_ATPB) {
-                        uint64_t rr[FU];
-    #pragma unroll
-                        for (int q = 0; q < FU; q++) {
-                            const uint32_t u = u0 + q * SK_PFL_ATPB + threadIdx.x;
-                            rr[q] = u < k ? rec2[a + u] : ~0ull;
-                        }
-    #pragma unroll
-                        for (int q = 0; q < FU; q++) {
-                            const uint64_t r = rr[q], key = r >> 32;
-                            if (r == ~0ull) continue;
-                            if (((r >> 26) & 63u) > reg[pfl_slotb(key)]) {
-                                const uint32_t i = atomicAdd(&ncand, 1u);
-                                if (i < SK_PFL_CAP) R[i] = r;
-                            } else {
-                                if (!(probe & 32)) changed[r & 0x3ffffffu] = 0;
-                            }
-                        }
-                    }
-                    __syncthreads();
-                    const uint32_t nc = ncand;
-                    if (nc <= SK_PFL_CAP) {
-                        pfl_chunk(R, nc, nxt, head, fin, reg, dirty, changed, probe, [] {});
-                    } else {
-                    __shared__ uint32_t gbase;
-                    unsigned long long *lk = reinterpret_cast<unsigned long long *>(work);
-                    uint32_t *lv = reinterpret_cast<uint32_t *>(lk + kBigL);
-                    if (threadIdx.x == 0) gbase = atomicAdd(big_alloc, 2 * k);
-                    for (uint32_t s = threadIdx.x; s < kBigL; s += SK_PFL_ATPB) lk[s] = SK_BIG_EMPTY, lv[s] = 0xffffffffu;
-                    __syncthreads();
-                    BigTable T{lk, lv, reinterpret_cast<unsigned long long *>(big_keys) + gbase, big_vals + gbase, 2 * k,
-                               kBigL};
-                    for (uint32_t s = threadIdx.x; s < T.S; s += SK_PFL_ATPB) T.gk[s] = SK_BIG_EMPTY, T.gv[s] = 0xffffffffu;
-                    __threadfence();
-                    __syncthreads();
-                    auto cand = [&](uint64_t r) {
-                        const uint64_t key = r >> 32;
-                        return ((r >> 26) & 63u) > reg[pfl_slotb(key)];
-                    };
-                    for (uint32_t u = threadIdx.x; u < k; u += SK_PFL_ATPB) {
-                        const uint64_t r = rec2[a + u];
-                        if (cand(r)) T.insert(((r >> 32) << 6) | ((r >> 26) & 63u), uint32_t(r & 0x3ffffffu));
-                    }
-                    __threadfence();
-                    __syncthreads();
-                    for (uint32_t u = threadIdx.x; u < k; u += SK_PFL_ATPB) { // replies (registers only read)
-                        const uint64_t r = rec2[a + u], key = r >> 32;
-                        if (!cand(r)) continue;
-                        const uint32_t rho = uint32_t(r >> 26) & 63u, seq = uint32_t(r & 0x3ffffffu);
-                        bool first = true;
-                        for (uint32_t v = rho; v < 52 && first; v++) first = T.find((key << 6) | v) >= seq;
-                        if (!(probe & 32) || first) changed[seq] = first ? 1 : 0;
-                    }
-                    __syncthreads();
-                    for (uint32_t u = threadIdx.x; u < k; u += SK_PFL_ATPB) { // the register's writer: its top record
-                        const uint64_t r = rec2[a + u], key = r >> 32;
-                        if (!cand(r)) continue;
-                        const uint32_t rho = uint32_t(r >> 26) & 63u, seq = uint32_t(r & 0x3ffffffu);
-                        if (T.find((key << 6) | rho) != seq) continue;
-                        bool top = true;
-                        for (uint32_t v = rho + 1; v < 52 && top; v++) top = T.find((key << 6) | v) == 0xffffffffu;
-                        const uint32_t slotb = pfl_slotb(key);
-                        if (top && rho > reg[slotb]) {
-                            reg[slotb] = uint8_t(rho);
-                            dirty[uint32_t(key >> 14)] = 1;
-                        }
-                    }
-                    }
-                }
-                __syncthreads();
-                for (uint32_t t = threadIdx.x; t < SK_PFL_HT; t += SK_PFL_ATPB) head[t] = 0xffffu;
-                __syncthreads();
-                t0 = t1;
-            }
-        }
+        for (uint32_t u = threadIdx.x; u < cnt; u += SK_PFL_ATPB) R[u] = rec2[start + u];
         __syncthreads();
-        if (!(probe & 4))
-            for (uint32_t q = threadIdx.x; q < nsl * LW; q += SK_PFL_ATPB)
-                if (dirty[q / LW]) line(q / LW)[q % LW] = regs4[q];
-        __syncthreads(); // LDS free for the next bucket
+        pfl_chunk(R, cnt, nxt, head, fin, reg, dirty, changed, probe, [&] {
+#pragma unroll
+            for (int j = 0; j < LQ; j++) {
+                const uint32_t q = threadIdx.x + j * SK_PFL_ATPB;
+                if (q < nsl * LW && pm.inv(slab0 + q / LW) < nslab) regs4[q] = lv[j];
+            }
+        });
+    } else {
+        for (uint32_t q = threadIdx.x; q < nsl * LW; q += SK_PFL_ATPB)
+            if (pm.inv(slab0 + q / LW) < nslab) regs4[q] = line(q / LW)[q % LW];
+        __syncthreads();
+        uint32_t t0 = 0;
+        while (t0 < ntile) { // uniform: chunks of whole runs, in tile (= batch) order
+            const uint32_t a = C[c0 + t0];
+            uint32_t t1 = t0 + 1;
+            while (t1 < ntile && C[c0 + t1 + 1] - a <= SK_PFL_CAP) t1++;
+            const uint32_t z = C[c0 + t1], k = z - a;
+            if (k <= SK_PFL_CAP) {
+                constexpr int CU = SK_PFL_CAP / SK_PFL_ATPB;
+                uint64_t rr[CU];
+#pragma unroll
+                for (int q = 0; q < CU; q++) {
+                    const uint32_t u = q * SK_PFL_ATPB + threadIdx.x;
+                    if (u < k) rr[q] = rec2[a + u];
+                }
+#pragma unroll
+                for (int q = 0; q < CU; q++) {
+                    const uint32_t u = q * SK_PFL_ATPB + threadIdx.x;
+                    if (u < k) R[u] = rr[q];
+                }
+                __syncthreads();
+                pfl_chunk(R, k, nxt, head, fin, reg, dirty, changed, probe, [] {});
+            } else { // one run larger than a chunk (t1 == t0 + 1)
+                // only records above their register can rise, and only they can stop a later record from rising:
+                // the rest reply 0 now; the candidates are resolved as a chunk when they fit (a hot sketch whose
+                // registers are already high has few), else with the (slot, rho) -> min seq table
+                __shared__ uint32_t ncand;
+                if (threadIdx.x == 0) ncand = 0;
+                __syncthreads();
+                constexpr int FU = 8; // records in flight per thread
+                for (uint32_t u0 = 0; u0 < k; u0 += FU * SK_PFL_ATPB) {
+                    uint64_t rr[FU];
+#pragma unroll
+                    for (int q = 0; q < FU; q++) {
+                        const uint32_t u = u0 + q * SK_PFL_ATPB + threadIdx.x;
+                        rr[q] = u < k ? rec2[a + u] : ~0ull;
+                    }
+#pragma unroll
+                    for (int q = 0; q < FU; q++) {
+                        const uint64_t r = rr[q], key = r >> 32;
+                        if (r == ~0ull) continue;
+                        if (((r >> 26) & 63u) > reg[pfl_slotb(key)]) {
+                            const uint32_t i = atomicAdd(&ncand, 1u);
+                            if (i < SK_PFL_CAP) R[i] = r;
+                        } else {
+                            if (!(probe & 32)) changed[r & 0x3ffffffu] = 0;
+                        }
+                    }
+                }
+                __syncthreads();
+                const uint32_t nc = ncand;
+                if (nc <= SK_PFL_CAP) {
+                    pfl_chunk(R, nc, nxt, head, fin, reg, dirty, changed, probe, [] {});
+                } else {
+                __shared__ uint32_t gbase;
+                unsigned long long *lk = reinterpret_cast<unsigned long long *>(work);
+                uint32_t *lv = reinterpret_cast<uint32_t *>(lk + kBigL);
+                if (threadIdx.x == 0) gbase = atomicAdd(big_alloc, 2 * k);
+                for (uint32_t s = threadIdx.x; s < kBigL; s += SK_PFL_ATPB) lk[s] = SK_BIG_EMPTY, lv[s] = 0xffffffffu;
+                __syncthreads();
+                BigTable T{lk, lv, reinterpret_cast<unsigned long long *>(big_keys) + gbase, big_vals + gbase, 2 * k,
+                           kBigL};
+                for (uint32_t s = threadIdx.x; s < T.S; s += SK_PFL_ATPB) T.gk[s] = SK_BIG_EMPTY, T.gv[s] = 0xffffffffu;
+                __threadfence();
+                __syncthreads();
+                auto cand = [&](uint64_t r) {
+                    const uint64_t key = r >> 32;
+                    return ((r >> 26) & 63u) > reg[pfl_slotb(key)];
+                };
+                for (uint32_t u = threadIdx.x; u < k; u += SK_PFL_ATPB) {
+                    const uint64_t r = rec2[a + u];
+                    if (cand(r)) T.insert(((r >> 32) << 6) | ((r >> 26) & 63u), uint32_t(r & 0x3ffffffu));
+                }
+                __threadfence();
+                __syncthreads();
+                for (uint32_t u = threadIdx.x; u < k; u += SK_PFL_ATPB) { // replies (registers only read)
+                    const uint64_t r = rec2[a + u], key = r >> 32;
+                    if (!cand(r)) continue;
+                    const uint32_t rho = uint32_t(r >> 26) & 63u, seq = uint32_t(r & 0x3ffffffu);
+                    bool first = true;
+                    for (uint32_t v = rho; v < 52 && first; v++) first = T.find((key << 6) | v) >= seq;
+                    if (!(probe & 32) || first) changed[seq] = first ? 1 : 0;
+                }
+                __syncthreads();
+                for (uint32_t u = threadIdx.x; u < k; u += SK_PFL_ATPB) { // the register's writer: its top record
+                    const uint64_t r = rec2[a + u], key = r >> 32;
+                    if (!cand(r)) continue;
+                    const uint32_t rho = uint32_t(r >> 26) & 63u, seq = uint32_t(r & 0x3ffffffu);
+                    if (T.find((key << 6) | rho) != seq) continue;
+                    bool top = true;
+                    for (uint32_t v = rho + 1; v < 52 && top; v++) top = T.find((key << 6) | v) == 0xffffffffu;
+                    const uint32_t slotb = pfl_slotb(key);
+                    if (top && rho > reg[slotb]) {
+                        reg[slotb] = uint8_t(rho);
+                        dirty[uint32_t(key >> 14)] = 1;
+                    }
+                }
+                }
+            }
+            __syncthreads();
+            for (uint32_t t = threadIdx.x; t < SK_PFL_HT; t += SK_PFL_ATPB) head[t] = 0xffffu;
+            __syncthreads();
+            t0 = t1;
         }
-#pragma unroll
-        for (int j = 0; j < LQ; j++) lv[j] = lvn[j];
-#pragma unroll
-        for (int q = 0; q < RQ; q++) rv[q] = rvn[q];
-        cs = csn, ce = cen, csn = csnn, cen = cenn;
     }
+    __syncthreads();
+    if (probe & 4) return;
+    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+    for (uint32_t q = threadIdx.x; q < nsl * LW; q += SK_PFL_ATPB)
+        if (dirty[q / LW]) {
+            if (probe & 16) {
+                const uint4 x = regs4[q];
+                v4u y = {x.x, x.y, x.z, x.w};
+                __builtin_nontemporal_store(y, reinterpret_cast<v4u *>(line(q / LW) + (q % LW)));
+            } else {
+                line(q / LW)[q % LW] = regs4[q];
+            }
+        }
 }
 
 // streamed-once 16-B load with the nontemporal hint (native vector type for the builtin)
@@ -2694,16 +2659,7 @@ hipError_t launch_pfl_part(hipStream_t st, const PflDims &d, const uint64_t *chu
 hipError_t launch_pfl_apply(hipStream_t st, const PflDims &d, const uint64_t *rec2, const uint32_t *C, uint32_t nslab,
                             uint8_t *arena, uint8_t *changed, uint32_t *big_alloc, uint64_t *big_keys,
                             uint32_t *big_vals, int flags) {
-    // persistent: as many workgroups as fit at once (four per CU), each walking fine buckets blockIdx + k * grid
-    static int cus = 0;
-    if (!cus) {
-        int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
-            hipSuccess || cus <= 0)
-            cus = 256;
-    }
-    const uint32_t grid = uint32_t(std::min<uint64_t>(d.nf, uint64_t(4) * cus)); // 117 VGPRs: 4 per CU
-    hipLaunchKernelGGL(k_pfl_apply, dim3(grid), dim3(SK_PFL_ATPB), 0, st, rec2, C, d.ntile, uint32_t(d.nf), d.nsub, d.sh,
+    hipLaunchKernelGGL(k_pfl_apply, dim3(uint32_t(d.nf)), dim3(SK_PFL_ATPB), 0, st, rec2, C, d.ntile, d.nsub, d.sh,
                        PflPerm{d.pa, d.pai, d.pm_mask, d.nslab}, nslab,
                        arena, changed, big_alloc, big_keys, big_vals, flags | (getenv("SK_PFL_PROBE") ? atoi(getenv("SK_PFL_PROBE")) : 0));
     SK_LAUNCH_CHECK();

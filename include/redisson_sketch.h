@@ -137,7 +137,11 @@ int sk_pfadd(sk_ctx *ctx, uint32_t n_cmds, const uint64_t *key_off, const uint8_
 int sk_pfadd_ids(sk_ctx *ctx, uint32_t n_cmds, const uint32_t *key_ids, const uint32_t *elem_counts,
                  const uint64_t *elem_off, const uint8_t *elem_bytes, uint8_t *out_changed);
 /* PFADD of one element per command, keys pre-resolved to slab ids (all
- * existing); device-resident inputs.  d_out_changed u8[n] on device. */
+ * existing); device-resident inputs.  d_out_changed u8[n] on device.
+ * Replies are the sequential replies of the n commands in order, so a caller
+ * may group-commit many RBatches into one call.  Calls of >= 4 M commands
+ * (SK_PFL_MIN) are applied with the line schedule: register lines streamed
+ * once per call instead of once per element (DESIGN.md "PFADD group commit"). */
 int sk_pfadd_dev(sk_ctx *ctx, uint64_t n, const uint32_t *d_key_ids, const uint64_t *d_elem_off,
                  const uint8_t *d_elem_bytes, uint64_t elem_bytes_len, uint8_t *d_out_changed);
 /* Batch of PFCOUNT commands: command c counts the union of nkeys[c] keys

@@ -65,7 +65,8 @@ hipError_t launch_pfl_part(hipStream_t st, const PflDims &d, const uint64_t *chu
 // big tables: 2 entries per record of the call (u64 keys, u32 values)
 hipError_t launch_pfl_apply(hipStream_t st, const PflDims &d, const uint64_t *rec2, const uint32_t *C, uint32_t nslab,
                             uint8_t *arena, uint8_t *changed, uint32_t *big_alloc, uint64_t *big_keys,
-                            uint32_t *big_vals, int flags); // flags & 32: replies pre-zeroed, only 1s stored
+                            uint32_t *big_vals, int flags, // flags & 32: replies pre-zeroed, only 1s stored
+                            uint32_t *order);              // u32[nf]: dispatch order (heavy fine buckets first)
 hipError_t sort_keys_size(uint64_t n, unsigned begin_bit, unsigned end_bit, size_t *bytes);
 hipError_t sort_keys(hipStream_t st, void *tmp, size_t tmp_bytes, const uint64_t *in, uint64_t *out, uint64_t n,
                      unsigned begin_bit, unsigned end_bit);

@@ -13,6 +13,7 @@
 // touched slot (rocPRIM) followed by a segment-head walk in batch order; the
 // final state (max / OR) needs no atomics because each slot has one head.
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 #include <rocprim/device/device_radix_sort.hpp>
@@ -388,7 +389,10 @@ __device__ __forceinline__ void pfp_hash_impl(uint64_t n, const uint32_t *__rest
     static_assert(SK_PFP_EPB <= 2 * SK_PFP_WIN, "records fit the windows");
     uint64_t *lrec = &win[0][0];
     for (uint32_t b = threadIdx.x; b < NBK; b += SK_PFP_TPB) h[b] = 0;
-    if (blockIdx.x == 0 && threadIdx.x == 0) *big_alloc = 0;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        big_alloc[0] = 0;
+        if (LINE) big_alloc[1] = big_alloc[2] = 0; // the line plan's heavy / light counters
+    }
     constexpr int PER = SK_PFP_EPB / SK_PFP_TPB;
     const uint64_t base = uint64_t(blockIdx.x) * SK_PFP_EPB;
     const uint64_t rounds = (n - base + SK_PFP_TPB - 1) / SK_PFP_TPB;
@@ -1196,12 +1200,30 @@ __device__ __forceinline__ void pfl_chunk(const uint64_t *R, uint32_t cnt, uint1
         }
 }
 
+// Heavy fine buckets first: the apply's grid starts with hmax "heavy slots"; the plan lists the fine buckets of more
+// than one chunk (C1, a Zipf head's lines -- they run longest) in order[0..H), H = ctr[0], and heavy slot k applies
+// order[k].  The rest of the grid is the fine buckets in their own order; a heavy one there exits at once.  A
+// uniform call has H = 0: its heavy slots exit and nothing else is indirected.
+__global__ void __launch_bounds__(256) k_pfl_plan(const uint32_t *__restrict__ C, uint32_t ntile, uint32_t nf,
+                                                  uint32_t hmax, uint32_t *ctr, uint32_t *__restrict__ order) {
+    __shared__ uint32_t wsum[256 / 64], base;
+    const uint32_t f = blockIdx.x * 256 + threadIdx.x;
+    const bool heavy = f < nf && C[uint64_t(f) * ntile + ntile] - C[uint64_t(f) * ntile] > SK_PFL_CAP;
+    uint32_t th;
+    const uint32_t ph = block_exscan<256>(heavy ? 1u : 0u, wsum, &th);
+    if (threadIdx.x == 0) base = th ? atomicAdd(ctr, th) : 0u;
+    __syncthreads();
+    if (heavy && base + ph < hmax) order[base + ph] = f; // hmax bounds the heavy buckets (n / (CAP + 1))
+}
+
 __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const uint64_t *__restrict__ rec2,
                                                            const uint32_t *__restrict__ C, uint32_t ntile,
                                                            uint32_t nsub, uint32_t sh, PflPerm pm, uint32_t nslab,
                                                            uint8_t *arena,
                                                            uint8_t *__restrict__ changed, uint32_t *big_alloc,
-                                                           uint64_t *big_keys, uint32_t *big_vals, int probe) {
+                                                           uint64_t *big_keys, uint32_t *big_vals, int probe,
+                                                           uint32_t hmax, const uint32_t *order_n,
+                                                           const uint32_t *__restrict__ order) {
     constexpr uint32_t NL = 1u << SK_PFL_SH;
     constexpr uint32_t kWork = SK_PFL_CAP * 8 + SK_PFL_CAP * 2 + SK_PFL_HT * 4 + SK_PFL_CAP;
     constexpr uint32_t kBigL = 1024;       // LDS slots of the big-run table
@@ -1216,10 +1238,18 @@ __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const uint64_t *__res
     uint32_t *head = reinterpret_cast<uint32_t *>(nxt + SK_PFL_CAP);
     uint8_t *fin = reinterpret_cast<uint8_t *>(head + SK_PFL_HT);
 
-    const uint32_t f = blockIdx.x, b = f / nsub, sub = f % nsub;
+    uint32_t f;
+    if (blockIdx.x < hmax) { // a heavy slot
+        if (blockIdx.x >= order_n[0]) return; // uniform
+        f = order[blockIdx.x];
+    } else {
+        f = blockIdx.x - hmax;
+    }
+    const uint32_t b = f / nsub, sub = f % nsub;
     const uint64_t c0 = uint64_t(f) * ntile;
     const uint32_t start = C[c0], end = C[c0 + ntile], cnt = end - start;
     if (cnt == 0) return; // uniform
+    if (hmax && blockIdx.x >= hmax && cnt > SK_PFL_CAP) return; // applied by a heavy slot
     const uint32_t slab0 = sub << sh, nsl = 1u << sh; // permuted ids slab0 + i, i < nsl
     auto line = [&](uint32_t i) -> uint4 * {
         const uint32_t s = pm.inv(slab0 + i);
@@ -2658,10 +2688,20 @@ hipError_t launch_pfl_part(hipStream_t st, const PflDims &d, const uint64_t *chu
 
 hipError_t launch_pfl_apply(hipStream_t st, const PflDims &d, const uint64_t *rec2, const uint32_t *C, uint32_t nslab,
                             uint8_t *arena, uint8_t *changed, uint32_t *big_alloc, uint64_t *big_keys,
-                            uint32_t *big_vals, int flags) {
-    hipLaunchKernelGGL(k_pfl_apply, dim3(uint32_t(d.nf)), dim3(SK_PFL_ATPB), 0, st, rec2, C, d.ntile, d.nsub, d.sh,
+                            uint32_t *big_vals, int flags, uint32_t *order) {
+    // heavy slots: at most n / (CAP + 1) fine buckets hold more than one chunk
+    const uint32_t hmax = order ? uint32_t(std::min<uint64_t>(d.nf, uint64_t(d.nblk) * SK_PFP_EPB / (SK_PFL_CAP + 1)))
+                                : 0u;
+    if (order) {
+        hipLaunchKernelGGL(k_pfl_plan, dim3(uint32_t((d.nf + 255) / 256)), dim3(256), 0, st, C, d.ntile,
+                           uint32_t(d.nf), hmax, big_alloc + 1, order);
+        SK_LAUNCH_CHECK();
+    }
+    hipLaunchKernelGGL(k_pfl_apply, dim3(uint32_t(d.nf) + hmax), dim3(SK_PFL_ATPB), 0, st, rec2, C, d.ntile, d.nsub,
+                       d.sh,
                        PflPerm{d.pa, d.pai, d.pm_mask, d.nslab}, nslab,
-                       arena, changed, big_alloc, big_keys, big_vals, flags | (getenv("SK_PFL_PROBE") ? atoi(getenv("SK_PFL_PROBE")) : 0));
+                       arena, changed, big_alloc, big_keys, big_vals,
+                       flags | (getenv("SK_PFL_PROBE") ? atoi(getenv("SK_PFL_PROBE")) : 0), hmax, big_alloc + 1, order);
     SK_LAUNCH_CHECK();
     return hipSuccess;
 }

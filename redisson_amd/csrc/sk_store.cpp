@@ -289,7 +289,8 @@ struct sk_ctx {
     uint64_t pfl_min = 4u << 20;
     uint32_t pfl_tile = 0;      // hash blocks per run tile (SK_PFL_TILE, 0 = the kernel default)
     bool pfl_zero = true;       // replies pre-zeroed, the apply stores only the 1s (SK_PFL_ZERO)
-    DBuf pfl_chunks, pfl_S, pfl_C, pfl_sums, pfl_rec, pfl_bk, pfl_bv, pfl_ovf;
+    bool pfl_plan = true;       // heavy fine buckets dispatched first (SK_PFL_PLAN)
+    DBuf pfl_chunks, pfl_S, pfl_C, pfl_sums, pfl_rec, pfl_bk, pfl_bv, pfl_ovf, pfl_order;
 };
 
 namespace {
@@ -1005,6 +1006,7 @@ int pfadd_lines(sk_ctx *c, uint64_t n, const uint32_t *d_ids, const uint64_t *d_
     HIPCHK(c, c->pfl_bk.ensure(2 * n * 8));
     HIPCHK(c, c->pfl_bv.ensure(2 * n * 4));
     HIPCHK(c, c->pfl_ovf.ensure(64));
+    HIPCHK(c, c->pfl_order.ensure(d.nf * 4));
     { Prof p_(c, 24);
     HIPCHK(c, sk::launch_pfl_hash(c->st, n, d_ids, d_off, d_bytes, c->redis_major >= 5, c->pfl_chunks.as<uint64_t>(),
                                   c->pfl_S.as<uint32_t>(), c->pfl_ovf.as<uint32_t>())); }
@@ -1017,7 +1019,8 @@ int pfadd_lines(sk_ctx *c, uint64_t n, const uint32_t *d_ids, const uint64_t *d_
     { Prof p_(c, 26);
     HIPCHK(c, sk::launch_pfl_apply(c->st, d, c->pfl_rec.as<uint64_t>(), c->pfl_C.as<uint32_t>(), nslab, c->arena,
                                    d_changed, c->pfl_ovf.as<uint32_t>(), c->pfl_bk.as<uint64_t>(),
-                                   c->pfl_bv.as<uint32_t>(), c->pfl_zero ? 32 : 0)); }
+                                   c->pfl_bv.as<uint32_t>(), c->pfl_zero ? 32 : 0,
+                                   c->pfl_plan ? c->pfl_order.as<uint32_t>() : nullptr)); }
     if (getenv("SK_PFL_DEBUG")) { // dev: table entries the oversized runs took (2 per record of a min-seq table run)
         uint32_t big = 0;
         HIPCHK(c, hipMemcpyAsync(&big, c->pfl_ovf.p, 4, hipMemcpyDeviceToHost, c->st));
@@ -1186,6 +1189,7 @@ int sk_open(const sk_config *cfg, sk_ctx **out) {
     if (const char *e = getenv("SK_PFL_MIN")) c->pfl_min = strtoull(e, nullptr, 10);
     if (const char *e = getenv("SK_PFL_TILE")) c->pfl_tile = uint32_t(strtoul(e, nullptr, 10));
     if (const char *e = getenv("SK_PFL_ZERO")) c->pfl_zero = atoi(e) != 0;
+    if (const char *e = getenv("SK_PFL_PLAN")) c->pfl_plan = atoi(e) != 0;
     uint64_t cap = (cfg && cfg->hll_capacity) ? cfg->hll_capacity : 1024;
     if (hll_grow(c, cap) != SK_OK || c->misc.ensure(4096) != hipSuccess ||
         hipMalloc(&c->d_zero, 16) != hipSuccess || hipMemsetAsync(c->d_zero, 0, 16, c->st) != hipSuccess ||
@@ -1223,7 +1227,7 @@ int sk_close(sk_ctx *c) {
                     &c->hist_a, &c->hist_b, &c->ovf, &c->bloom_h, &c->rc_S, &c->rc_rec, &c->long_h,
                     &c->long_which, &c->long_plane, &c->long_flags, &c->ra_S, &c->ra_rec, &c->ra_flag, &c->ev, &c->ev_n,
                     &c->pfl_chunks, &c->pfl_S, &c->pfl_C, &c->pfl_sums, &c->pfl_rec, &c->pfl_bk, &c->pfl_bv,
-                    &c->pfl_ovf})
+                    &c->pfl_ovf, &c->pfl_order})
         b->release();
     for (auto &ps : c->pfs) {
         for (DBuf *b : {&ps.chunks, &ps.rep, &ps.S, &ps.big_k, &ps.big_v, &ps.ovf}) b->release();

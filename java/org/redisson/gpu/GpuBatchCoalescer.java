@@ -110,27 +110,6 @@ public final class GpuBatchCoalescer {
         SketchDispatch.worker(ctx).execute(task);
     }
 
-    static final double SKEW_SHARE = 0.02;
-    static final int SKEW_SAMPLE = 1 << 16, SKEW_SLICE = 1 << 20;
-
-    /** the most frequent key of a sample of the group holds more than SKEW_SHARE of it */
-    static boolean skewed(List<byte[]> keys) {
-        int n = keys.size();
-        if (n <= SKEW_SLICE) {
-            return false;
-        }
-        int step = Math.max(1, n / SKEW_SAMPLE), m = 0, top = 0;
-        java.util.HashMap<String, Integer> freq = new java.util.HashMap<String, Integer>();
-        for (int i = 0; i < n; i += step, m++) {
-            String k = new String(keys.get(i), SketchDispatch.ISO);
-            Integer c = freq.get(k);
-            int v = c == null ? 1 : c.intValue() + 1;
-            freq.put(k, v);
-            top = Math.max(top, v);
-        }
-        return top > SKEW_SHARE * m;
-    }
-
     private void execute(List<Req> group) {
         List<byte[]> keys = new ArrayList<byte[]>();
         List<byte[]> flat = new ArrayList<byte[]>();
@@ -148,30 +127,11 @@ public final class GpuBatchCoalescer {
         for (int i = 0; i < cnt.length; i++) {
             cnt[i] = counts.get(i);
         }
+        SketchDispatch.Packed k = new SketchDispatch.Packed(keys);
+        SketchDispatch.Packed e = new SketchDispatch.Packed(flat);
         byte[] out = new byte[keys.size()];
-        int st = SketchNative.SK_OK;
-        String err = null;
-        // a skewed group goes in slices below the engine's line-schedule threshold (few hot tenants would serialize
-        // on a handful of workgroups; DESIGN.md "PFADD group commit"); replies are the same, the order is kept
-        int slice = skewed(keys) ? SKEW_SLICE : keys.size();
-        int elemAt = 0;
-        for (int c0 = 0; c0 < keys.size(); c0 += slice) {
-            int c1 = Math.min(keys.size(), c0 + slice), ne = 0;
-            for (int c = c0; c < c1; c++) {
-                ne += cnt[c];
-            }
-            SketchDispatch.Packed k = new SketchDispatch.Packed(keys.subList(c0, c1));
-            SketchDispatch.Packed e = new SketchDispatch.Packed(flat.subList(elemAt, elemAt + ne));
-            byte[] part = new byte[c1 - c0];
-            int s = SketchNative.pfadd(ctx, k.off, k.bytes, java.util.Arrays.copyOfRange(cnt, c0, c1), e.off, e.bytes,
-                                       part);
-            System.arraycopy(part, 0, out, c0, part.length);
-            if (s != SketchNative.SK_OK && st == SketchNative.SK_OK) {
-                st = s;
-                err = SketchNative.lastError(ctx);
-            }
-            elemAt += ne;
-        }
+        int st = SketchNative.pfadd(ctx, k.off, k.bytes, cnt, e.off, e.bytes, out);
+        String err = st == SketchNative.SK_OK ? null : SketchNative.lastError(ctx);
         // the failed commands: keys that are still not HLLs after the call (WRONGTYPE / corrupt sparse string);
         // any other status fails every batch of the call
         Set<String> bad = new HashSet<String>();

@@ -21,8 +21,6 @@ import contextlib
 import threading
 from typing import List, Optional, Sequence
 
-import numpy as np
-
 from .redisson import Future
 
 
@@ -172,14 +170,6 @@ class BatchCoalescer:
     """One completion thread per client; `submit(batch)` enqueues an RBatch and returns the future of its result
     list (or its error, as RBatch.execute would raise it)."""
 
-    # A group whose keys are skewed is sent in slices below the engine's line-schedule threshold: the line schedule
-    # applies each fine bucket on one workgroup, so a few hot tenants serialize (C2 Zipf(1.1): 8-10 G/s as one
-    # 64 M call against 13 G/s in 1 M slices, DESIGN.md).  Skew = the most frequent key of a sample of the group's
-    # commands holds more than `skew_share` of it.
-    skew_share = 0.02
-    skew_sample = 1 << 16
-    skew_slice = 1 << 20
-
     def __init__(self, client, max_cmds: int = 1 << 26):
         self.client = client
         self.engine = client.engine
@@ -235,15 +225,6 @@ class BatchCoalescer:
                 self._run_pfadd(group)
             self.batches += len(group)
 
-    def _skewed(self, keys) -> bool:
-        n = len(keys)
-        if n <= self.skew_slice:
-            return False
-        step = max(1, n // self.skew_sample)
-        sample = keys[::step]
-        top = collections.Counter(sample).most_common(1)[0][1]
-        return top > self.skew_share * len(sample)
-
     def _run_one(self, r: _BatchReq):
         try:
             r.future._set(r.batch._execute_now())
@@ -255,17 +236,8 @@ class BatchCoalescer:
 
         cmds = [c for r in group for c in r.batch._cmds]
         keys = [c[0][1] for c in cmds]
-        elems = [c[0][2] for c in cmds]
-        if self._skewed(keys):
-            parts = [self.engine.pfadd_status(keys[i:i + self.skew_slice], elems[i:i + self.skew_slice])
-                     for i in range(0, len(keys), self.skew_slice)]
-            self.calls += len(parts)
-            bad_st = [p for p in parts if p[0] != 0]
-            st, msg = (bad_st[0][0], bad_st[0][2]) if bad_st else (0, "")
-            out = np.concatenate([p[1] for p in parts]) if parts else np.zeros(0, dtype=np.uint8)
-        else:
-            st, out, msg = self.engine.pfadd_status(keys, elems)
-            self.calls += 1
+        st, out, msg = self.engine.pfadd_status(keys, [c[0][2] for c in cmds])
+        self.calls += 1
         bad = set()
         if st != 0:
             # a command on a key of another type failed alone (the others were applied, pipeline semantics):

@@ -210,26 +210,3 @@ def test_coalesced_batches_on_engine(O):
     finally:
         cl.shutdown()
 
-
-def test_skewed_group_goes_in_slices():
-    """A merged group whose keys are skewed (one key holds > skew_share of a sample) is sent in slices below the
-    line-schedule threshold; replies and registers are still the sequential ones."""
-    from redisson_amd.coalesce import BatchCoalescer
-
-    def hot(b, s):
-        rng = np.random.default_rng(s)
-        for i in range(400):
-            b.getHyperLogLog("hot" if i % 3 else "t:%d" % rng.integers(0, 50)).addAsync(int(rng.integers(0, 1 << 62)))
-
-    specs = [lambda b, s=s: hot(b, s) for s in range(8)]
-    want, weng = _sequential(specs)
-    old = BatchCoalescer.skew_slice
-    BatchCoalescer.skew_slice = 1000
-    try:
-        got, geng, calls = _coalesced(specs)
-    finally:
-        BatchCoalescer.skew_slice = old
-    assert got == want
-    assert calls == 4 and geng.calls == 4          # 3200 commands in slices of 1000
-    for k in weng.ref.regs:
-        np.testing.assert_array_equal(geng.ref.regs[k], weng.ref.regs[k])

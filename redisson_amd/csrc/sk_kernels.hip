@@ -2689,6 +2689,7 @@ hipError_t launch_pfl_part(hipStream_t st, const PflDims &d, const uint64_t *chu
 hipError_t launch_pfl_apply(hipStream_t st, const PflDims &d, const uint64_t *rec2, const uint32_t *C, uint32_t nslab,
                             uint8_t *arena, uint8_t *changed, uint32_t *big_alloc, uint64_t *big_keys,
                             uint32_t *big_vals, int flags, uint32_t *order) {
+    static const int probe_flags = getenv("SK_PFL_PROBE") ? atoi(getenv("SK_PFL_PROBE")) : 0; // dev ablations (bit 4)
     // heavy slots: at most n / (CAP + 1) fine buckets hold more than one chunk
     const uint32_t hmax = order ? uint32_t(std::min<uint64_t>(d.nf, uint64_t(d.nblk) * SK_PFP_EPB / (SK_PFL_CAP + 1)))
                                 : 0u;
@@ -2701,7 +2702,7 @@ hipError_t launch_pfl_apply(hipStream_t st, const PflDims &d, const uint64_t *re
                        d.sh,
                        PflPerm{d.pa, d.pai, d.pm_mask, d.nslab}, nslab,
                        arena, changed, big_alloc, big_keys, big_vals,
-                       flags | (getenv("SK_PFL_PROBE") ? atoi(getenv("SK_PFL_PROBE")) : 0), hmax, big_alloc + 1, order);
+                       flags | probe_flags, hmax, big_alloc + 1, order);
     SK_LAUNCH_CHECK();
     return hipSuccess;
 }

@@ -174,3 +174,22 @@ def test_lines_agree_with_partition_path(O):
     regs, want = O.HLLStore().pfadd_bulk(kid, off, buf, nkeys)
     assert np.array_equal(res[1][0], want)
     assert np.array_equal(res[1][1], regs)
+
+
+def test_lines_host_buffer_batches(leng, O):
+    """Host-buffer PFADD (sk_pfadd by name, sk_pfadd_ids by slab id) of one-element commands goes through the line
+    schedule too (SK_PFL_MIN=1 here): replies and registers equal the oracle's."""
+    nkeys, n = 400, 60_000
+    names = [b"ln:h:%d" % i for i in range(nkeys)]
+    rng = np.random.default_rng(8)
+    off, buf = gen_jackson_longs(0x5EED1008, 2 * n)
+    els = [buf[off[i]:off[i + 1]].tobytes() for i in range(2 * n)]
+    kid = rng.integers(0, nkeys, 2 * n).astype(np.uint32)
+    ref = O.HLLStore()
+    got = leng.pfadd([names[k] for k in kid[:n]], [[e] for e in els[:n]])
+    assert got == ref.pfadd([names[k] for k in kid[:n]], [[e] for e in els[:n]])
+    ids = leng.hll_resolve(names)
+    got2 = leng.pfadd_ids(ids[kid[n:]], [[e] for e in els[n:]])
+    assert got2 == ref.pfadd([names[k] for k in kid[n:]], [[e] for e in els[n:]])
+    for nm in names:
+        np.testing.assert_array_equal(leng.hll_registers(nm), ref.regs[nm])

@@ -1267,7 +1267,18 @@ __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const uint64_t *__res
             if (q < nsl * LW && pm.inv(slab0 + q / LW) < nslab)
                 lv[j] = (probe & 4) ? make_uint4(0, 0, 0, 0) : line(q / LW)[q % LW];
         }
-        for (uint32_t u = threadIdx.x; u < cnt; u += SK_PFL_ATPB) R[u] = rec2[start + u];
+        constexpr int RU = SK_PFL_CAP / SK_PFL_ATPB; // every record load in flight at once
+        uint64_t rv[RU];
+#pragma unroll
+        for (int q = 0; q < RU; q++) {
+            const uint32_t u = q * SK_PFL_ATPB + threadIdx.x;
+            if (u < cnt) rv[q] = rec2[start + u];
+        }
+#pragma unroll
+        for (int q = 0; q < RU; q++) {
+            const uint32_t u = q * SK_PFL_ATPB + threadIdx.x;
+            if (u < cnt) R[u] = rv[q];
+        }
         __syncthreads();
         pfl_chunk(R, cnt, nxt, head, fin, reg, dirty, changed, probe, [&] {
 #pragma unroll

@@ -1,7 +1,8 @@
 """GPU parity of the PFADD line schedule (k_pfl_*: group-committed RBatches applied sketch-major with the registers
 in LDS) against the CPU oracle, bit-exact: replies of every command and every register.
 
-The engine is opened with SK_PFL_MIN=1 so that every device batch takes the line schedule, whatever its size.
+The engine is opened with SK_PFL_MIN=1 and SK_PFL_RATIO=0 so that every device batch takes the line schedule,
+whatever its size.
 Cases: uniform tenants over several fine buckets and run tiles, registers carried over from an earlier batch,
 one key receiving everything (fine buckets applied in chunks of runs), one element repeated past a chunk in one
 run (the (slot, rho) -> min seq table), Zipf-skewed tenants, slab ids above the last fine bucket's start, and the
@@ -20,10 +21,12 @@ def _engine(pfl_min="1"):
     from redisson_amd import SketchEngine
 
     os.environ["SK_PFL_MIN"] = pfl_min
+    os.environ["SK_PFL_RATIO"] = "0"   # every call of these tests takes the line schedule, whatever its size
     try:
         return SketchEngine(device=0, max_batch=1 << 23)
     finally:
         del os.environ["SK_PFL_MIN"]
+        del os.environ["SK_PFL_RATIO"]
 
 
 @pytest.fixture(scope="module")

@@ -140,7 +140,8 @@ int sk_pfadd_ids(sk_ctx *ctx, uint32_t n_cmds, const uint32_t *key_ids, const ui
  * existing); device-resident inputs.  d_out_changed u8[n] on device.
  * Replies are the sequential replies of the n commands in order, so a caller
  * may group-commit many RBatches into one call.  Calls of >= 4 M commands
- * (SK_PFL_MIN) are applied with the line schedule: register lines streamed
+ * (SK_PFL_MIN) and >= 160 per sketch of the store (SK_PFL_RATIO) are
+ * applied with the line schedule: register lines streamed
  * once per call instead of once per element (DESIGN.md "PFADD group commit"). */
 int sk_pfadd_dev(sk_ctx *ctx, uint64_t n, const uint32_t *d_key_ids, const uint64_t *d_elem_off,
                  const uint8_t *d_elem_bytes, uint64_t elem_bytes_len, uint8_t *d_out_changed);

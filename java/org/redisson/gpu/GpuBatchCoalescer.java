@@ -5,7 +5,8 @@
  * The reference sends every RBatch as its own pipeline (M:command/CommandBatchService.java:184-293) and
  * redis-server applies the batches one after another.  Here GpuSketchBatchService hands a batch whose commands are
  * all PFADDs on engine-held keys to this coalescer instead of running it alone.  The context's FIFO worker runs
- * each maximal sequence of such batches queued together (up to maxCmds commands) as ONE sk_pfadd call; at >= 4 M commands the engine applies it with the line schedule (register lines streamed
+ * each maximal sequence of such batches queued together (up to maxCmds commands) as ONE sk_pfadd call; at >= 4 M commands (and >= 160 per HLL key held) the engine applies it with the
+ * line schedule (register lines streamed
  * once per call instead of once per element).  The concatenation keeps FIFO order and PFADD replies depend only
  * on order, so every batch gets exactly the replies it would get run alone in that order.  A PFADD on a key of
  * another type fails that command alone inside the engine (pipeline semantics); its batch fails with the

@@ -82,7 +82,7 @@ class Config:
     # one completion thread merges FIFO runs into single engine calls
     bloom_coalesce: bool = False
     # group commit of concurrently executed RBatches (coalesce.BatchCoalescer): PFADD-only batches queued together
-    # become one engine call (the line schedule at >= 4 M commands), replies split back per batch
+    # become one engine call (the line schedule at >= 4 M commands and >= 160 per HLL key), replies split back per batch
     batch_coalesce: bool = False
 
 

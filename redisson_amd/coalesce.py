@@ -219,10 +219,20 @@ class BatchCoalescer:
                 if not self._q:
                     return
                 group = self._take()
-            if len(group) == 1 and not group[0].pfadd_only():
-                self._run_one(group[0])
-            else:
-                self._run_pfadd(group)
+            try:
+                if len(group) == 1 and not group[0].pfadd_only():
+                    self._run_one(group[0])
+                else:
+                    self._run_pfadd(group)
+            except Exception as e:  # noqa: BLE001 - packing / encoding / type lookup failed: fail the whole group,
+                # as BloomCoalescer._execute does; the completion thread lives on for the batches behind it
+                for r in group:
+                    r.batch._executed = True
+                    for (_c, _fn, _post, f) in r.batch._cmds:
+                        if not f.isDone():
+                            f._fail(e)
+                    if not r.future.isDone():
+                        r.future._fail(e)
             self.batches += len(group)
 
     def _run_one(self, r: _BatchReq):

@@ -46,27 +46,34 @@ hipError_t launch_pfp_apply(hipStream_t st, uint64_t n, const uint64_t *chunks, 
 hipError_t launch_pfp_reply(hipStream_t st, uint64_t n, const uint8_t *rep, const uint16_t *pos,
                             const uint32_t *cmd_of, uint8_t *changed);
 // PFADD line schedule (one element per command, n <= 2^26, <= pfl_max_slabs() sketches): hash into 128 line
-// buckets, partition each into runs of (bucket, 512 sketches, tile of hash blocks), apply with the lines in LDS
+// buckets, sort each (bucket, tile of hash blocks) region by fine bucket (2^sh sketches) in LDS, apply each fine
+// bucket with its lines in LDS
 struct PflDims {
-    uint32_t nblk, tb, ntile, nsub, nsums; // hash blocks, blocks per run tile, tiles, fine buckets per bucket
-    uint32_t sh;                           // 2^sh sketches per fine bucket
-    uint32_t pk, pa, pai, pm_mask;         // fine buckets by permuted slab id: slab * pa mod 2^pk
+    uint32_t nblk, tb, ntile, nsub;  // hash blocks, blocks per run tile, tiles, fine buckets per bucket
+    uint32_t sh;                     // 2^sh sketches per fine bucket
+    uint32_t pk, pa, pai, pm_mask;   // fine buckets by permuted slab id: slab * pa mod 2^pk
     uint32_t nslab;
-    uint64_t nf, ncount;         // fine buckets; run counts (C holds ncount + 1 words)
+    uint32_t rcap, nreg;             // records a region holds in LDS; regions (128 x ntile)
+    uint64_t nf;                     // fine buckets
+    uint64_t c_words;                // C: region totals, region bases (nreg each), then C2[nreg][nsub + 1]
     uint64_t chunk_bytes, S_bytes;
 };
 PflDims pfl_dims(uint64_t n, uint32_t nslab, uint32_t tile_blocks = 0); // 0: the default tile
+bool pfl_dims_ok(const PflDims &d);
 uint32_t pfl_max_slabs();
 hipError_t launch_pfl_hash(hipStream_t st, uint64_t n, const uint32_t *key_ids, const uint64_t *off,
                            const uint8_t *bytes, int v5, uint64_t *chunks, uint32_t *S, uint32_t *big_alloc);
-// count + scan + scatter; C u32[ncount + 1], sums u32[nsums + 1], rec2 u64[n]
+// region totals + region sort; C u32[c_words], rec2 u64[n]; dropped records (slab >= nslab) reply 0 in changed
 hipError_t launch_pfl_part(hipStream_t st, const PflDims &d, const uint64_t *chunks, const uint32_t *S, uint32_t *C,
-                           uint32_t *sums, uint64_t *rec2);
+                           uint64_t *rec2, uint8_t *changed);
+// replies pre-filled with the call's default reply (rc: u32[32] reply-mix counters, par: this call's parity)
+hipError_t launch_pfl_fill(hipStream_t st, uint8_t *changed, uint64_t n, uint32_t *rc, uint32_t par);
 // big tables: 2 entries per record of the call (u64 keys, u32 values)
 hipError_t launch_pfl_apply(hipStream_t st, const PflDims &d, const uint64_t *rec2, const uint32_t *C, uint32_t nslab,
                             uint8_t *arena, uint8_t *changed, uint32_t *big_alloc, uint64_t *big_keys,
-                            uint32_t *big_vals, int flags, // flags & 32: replies pre-zeroed, only 1s stored
-                            uint32_t *order);              // u32[nf]: dispatch order (heavy fine buckets first)
+                            uint32_t *big_vals, int flags, // flags & 32: replies pre-filled, only others stored
+                            uint32_t *order,               // u32[nf]: dispatch order (heavy fine buckets first)
+                            uint32_t *rc, uint32_t par);
 hipError_t sort_keys_size(uint64_t n, unsigned begin_bit, unsigned end_bit, size_t *bytes);
 hipError_t sort_keys(hipStream_t st, void *tmp, size_t tmp_bytes, const uint64_t *in, uint64_t *out, uint64_t n,
                      unsigned begin_bit, unsigned end_bit);

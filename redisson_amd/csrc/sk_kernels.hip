@@ -14,6 +14,7 @@
 // final state (max / OR) needs no atomics because each slot has one head.
 #include <hip/hip_runtime.h>
 #include <algorithm>
+#include <cmath>
 #include <cstdlib>
 #include <cstring>
 #include <rocprim/device/device_radix_sort.hpp>
@@ -893,37 +894,39 @@ __global__ void __launch_bounds__(SK_PFP_ATPB) __attribute__((amdgpu_waves_per_e
 // elements) registers are applied sketch-major with the registers held in LDS, instead of one random register
 // line read and written per element:
 //   k_pfl_hash     as k_pfp_hash, 128 coarse buckets: bucket b holds line (b - rot(s)) & 127 of every sketch s
-//   k_pfl_count    per (bucket, tile of hash blocks): records per fine bucket = (b, s >> sh)
-//   k_scan_*       exclusive scan of the counts (fine-bucket major, tile minor) -> each (fine bucket, tile) run
-//   k_pfl_scatter  records to their run: rec2 = slab_low << 46 | reg << 32 | rho << 26 | seq (26 bits)
-//   k_pfl_apply    one workgroup per fine bucket: its 256 lines (one per sketch, 32 KiB) into LDS with its
-//                  records, the records chained per register in LDS, the sequential replies (rho beats the
-//                  register and every earlier rho of it), the lines that changed stored back.
+//   k_pfl_tot      records per region = (coarse bucket b, tile of tb hash blocks), from the hash blocks' segments
+//   k_pfl_region   one workgroup per region: its segments into registers, counting-sorted in LDS by fine bucket
+//                  (b, p >> sh), written back as ONE contiguous region of rec2 (tile-major runs: region (b, t) holds
+//                  the runs (b, t, fine bucket) back to back) plus the region's fine-bucket starts C2[region][sub]
+//                  rec2 = slab_low << 46 | reg << 32 | rho << 26 | seq (26 bits)
+//   k_pfl_fill     replies pre-filled with the call's default (the majority reply of the previous call)
+//   k_pfl_apply    one workgroup per fine bucket: its 2^sh lines (one per sketch, 16 KiB) into LDS with its
+//                  records (one run per tile), the records chained per register in LDS, the sequential replies (rho
+//                  beats the register and every earlier rho of it; only replies != the default are stored), the
+//                  lines that changed stored back.
+// A region's records are binomial in the register index whatever the key skew (a sketch's 128 lines sit in 128
+// distinct coarse buckets), so at tb = 448 blocks (~14.3 k records) a region fits LDS; only a region swollen by one
+// element repeated thousands of times takes the two-pass streaming path.  The region layout replaces a global
+// count pass + scan + a scatter of partial-line pieces (0.77 ms per 64 M, r02) with one read and one contiguous
+// write of the records.
 // Runs are in tile order and tiles in batch order, so a fine bucket larger than one chunk is applied in chunks of
 // whole runs with the LDS registers carried over; a single run larger than a chunk is resolved with the (slot,
 // rho) -> min seq table of pfp_big_resolve, against the LDS registers.
 #define SK_PFL_SH 7        // largest fine bucket = 2^SH sketches (128 lines of 128 B = 16 KiB of registers); a call
                            // uses sh <= SH sketches per fine bucket, sized so a fine bucket expects <= ~768 records
-#define SK_PFL_TILE 1024   // hash blocks per run tile (default; SK_PFL_TILE)
-#define SK_PFL_BTPB 512    // count / scatter threads: 4 per hash block, 128 blocks per pass over the tile
-#define SK_PFL_ATPB 256    // apply threads (five apply workgroups per CU: 29 KiB of LDS each)
+#define SK_PFL_TILE 448    // hash blocks per run tile (default; SK_PFL_TILE): ~14.3 k records per region
+#define SK_PFL_RTPB 1024   // region threads: one hash-block segment each
+#define SK_PFL_RPER 16     // records per region thread held in registers
+#define SK_PFL_RCAP (SK_PFL_RTPB * SK_PFL_RPER) // most records of a one-piece region
+#define SK_PFL_ATPB 256    // apply threads (five apply workgroups per CU)
 #define SK_PFL_CAP 1024    // records per apply chunk
 #define SK_PFL_HT 1024     // chain heads per chunk
 #define SK_PFL_MAXSUB 8192 // fine buckets per coarse bucket (2^20 sketches)
-#define SK_PFL_TMAX 2048   // largest run tile (hash blocks)
+#define SK_PFL_TMAX 1024   // largest run tile (hash blocks): one segment per region thread
+#define SK_PFL_NTMAX 64    // most tiles per call (the apply's run table; 5 apply workgroups per CU need <= 32 KiB of LDS)
+#define SK_PFL_LDS (160 * 1024 - 9 * 1024) // dynamic LDS of a region workgroup: records + fine-bucket counts
 __device__ __forceinline__ uint32_t pfl_ht(uint64_t key) {
     return uint32_t((key * 0xC2B2AE3D27D4EB4Full) >> 54); // 10 bits
-}
-
-// (coarse bucket, tile) of this workgroup: workgroups are dispatched to the 8 XCDs round robin, so the ids are
-// dealt out such that one XCD takes consecutive tiles of a bucket -- the runs (f, tile) and (f, tile + 1) of a fine
-// bucket are adjacent in memory, and their partial lines then meet in the same L2 (speed only)
-__device__ __forceinline__ void pfl_bt(uint32_t ntile, uint32_t *b, uint32_t *tile) {
-    const uint32_t total = ntile * SK_PFL_NB, L = blockIdx.x;
-    uint32_t q = L;
-    if ((total & 7u) == 0) q = (L & 7u) * (total >> 3) + (L >> 3);
-    *b = q / ntile;
-    *tile = q % ntile;
 }
 
 // Fine buckets take sketches by a permuted slab id, p = slab * pa mod 2^pk (pa odd, a bijection): slabs are
@@ -931,241 +934,215 @@ __device__ __forceinline__ void pfl_bt(uint32_t ntile, uint32_t *b, uint32_t *ti
 // Zipf key space -- would otherwise share fine buckets and pile their records onto a few workgroups.
 struct PflPerm {
     uint32_t pa, pai, mask; // multiplier, its inverse mod 2^pk, 2^pk - 1
-    uint32_t nslab;         // slab ids >= nslab (never handed out) are dropped by count and scatter alike
+    uint32_t nslab;         // slab ids >= nslab (never handed out) are dropped, their replies 0
     __device__ __forceinline__ uint32_t fwd(uint32_t slab) const { return (slab * pa) & mask; }
     __device__ __forceinline__ uint32_t inv(uint32_t p) const { return (p * pai) & mask; }
 };
 
-__global__ void __launch_bounds__(SK_PFL_BTPB) k_pfl_count(const uint64_t *__restrict__ chunks,
-                                                           const uint32_t *__restrict__ S, uint32_t nblk, uint32_t tb,
-                                                           uint32_t ntile, uint32_t nsub, uint32_t sh, PflPerm pm,
-                                                           uint32_t *__restrict__ C) {
-    extern __shared__ uint32_t hist[]; // nsub words
-    for (uint32_t s = threadIdx.x; s < nsub; s += SK_PFL_BTPB) hist[s] = 0;
-    __syncthreads();
-    uint32_t b, tile;
-    pfl_bt(ntile, &b, &tile);
-    const uint32_t b0 = tile * tb, b1 = b0 + tb < nblk ? b0 + tb : nblk;
-    // 4 threads per block segment; the segment bounds of the thread's next block are loaded while this one is
-    // counted, and a segment's records are loaded 8 per thread before any is counted
-    uint32_t blk = b0 + (threadIdx.x >> 2);
-    uint32_t lo = 0, hi = 0;
-    if (blk < b1) lo = S[uint64_t(b) * nblk + blk], hi = S[uint64_t(b + 1) * nblk + blk];
-    for (; blk < b1; blk += SK_PFL_BTPB / 4) {
-        const uint32_t nx = blk + SK_PFL_BTPB / 4;
-        uint32_t lo2 = 0, hi2 = 0;
-        if (nx < b1) lo2 = S[uint64_t(b) * nblk + nx], hi2 = S[uint64_t(b + 1) * nblk + nx];
-        const uint64_t *seg = chunks + uint64_t(blk) * SK_PFP_EPB;
-        for (uint32_t t0 = lo + (threadIdx.x & 3u); t0 < hi; t0 += 32) {
-            uint32_t sl[8];
-#pragma unroll
-            for (int q = 0; q < 8; q++) {
-                const uint32_t t = t0 + 4 * q;
-                sl[q] = t < hi ? uint32_t(seg[t] >> 32) : 0xffffffffu;
-            }
-#pragma unroll
-            for (int q = 0; q < 8; q++) // ids beyond the store's slabs are dropped (both passes)
-                if (sl[q] < pm.nslab) atomicAdd(&hist[pm.fwd(sl[q]) >> sh], 1u);
-        }
-        lo = lo2;
-        hi = hi2;
-    }
-    __syncthreads();
-    for (uint32_t s = threadIdx.x; s < nsub; s += SK_PFL_BTPB)
-        C[(uint64_t(b) * nsub + s) * ntile + tile] = hist[s];
-}
-
-// The tile's records are taken in pieces of SK_PFL_PIECE (through the prefix of its block segments), each piece
-// counting-sorted by fine bucket in LDS and stored as one contiguous piece per run: consecutive lanes store
-// consecutive words of a run, so a store instruction writes whole pieces of lines (one record per lane into
-// hundreds of runs made every store a partial-line write).  Dynamic LDS: 2 * nsub words.
-#define SK_PFL_PIECE 4096
-__global__ void __launch_bounds__(SK_PFL_BTPB) k_pfl_scatter(const uint64_t *__restrict__ chunks,
-                                                             const uint32_t *__restrict__ S, uint32_t nblk,
-                                                             uint32_t tb, uint32_t ntile, uint32_t nsub, uint32_t sh,
-                                                             PflPerm pm, const uint32_t *__restrict__ C,
-                                                             uint64_t *__restrict__ rec2) {
-    constexpr int PER = SK_PFL_PIECE / SK_PFL_BTPB;
-    extern __shared__ uint32_t dyn[];
-    __shared__ uint32_t segp[SK_PFL_TMAX + 1]; // prefix of the tile's segment lengths
-    __shared__ uint32_t segs[SK_PFL_TMAX];     // each segment's start in its block chunk
-    __shared__ uint64_t sorted[SK_PFL_PIECE];
-    __shared__ uint32_t wsum[SK_PFL_BTPB / 64];
-    uint32_t *cur = dyn, *lcnt = dyn + nsub;
-    uint32_t b, tile;
-    pfl_bt(ntile, &b, &tile);
-    const uint32_t b0 = tile * tb, nb = (b0 + tb < nblk ? b0 + tb : nblk) - b0;
-    for (uint32_t x = threadIdx.x; x < nsub; x += SK_PFL_BTPB) {
-        cur[x] = C[(uint64_t(b) * nsub + x) * ntile + tile];
-        lcnt[x] = 0;
-    }
-    // segment prefix: tb <= SK_PFL_TMAX blocks, SK_PFL_TMAX / SK_PFL_BTPB per thread (consecutive)
-    constexpr int SP = SK_PFL_TMAX / SK_PFL_BTPB;
-    uint32_t sl[SP], ssum = 0;
-#pragma unroll
-    for (int q = 0; q < SP; q++) {
-        const uint32_t j = threadIdx.x * SP + q;
-        sl[q] = 0;
-        if (j < nb) {
-            const uint32_t st = S[uint64_t(b) * nblk + b0 + j];
-            sl[q] = S[uint64_t(b + 1) * nblk + b0 + j] - st;
-            segs[j] = st;
-        }
-        ssum += sl[q];
-    }
-    uint32_t total;
-    uint32_t ex = block_exscan<SK_PFL_BTPB>(ssum, wsum, &total);
-#pragma unroll
-    for (int q = 0; q < SP; q++) {
-        segp[threadIdx.x * SP + q] = ex;
-        ex += sl[q];
-    }
-    if (threadIdx.x == 0) segp[SK_PFL_TMAX] = total;
-    __syncthreads();
-    // a piece's record loads, all issued before any is used; the next piece's are issued while this one is sorted
-    auto load = [&](uint32_t base, uint64_t (&r)[PER], uint32_t (&bl)[PER]) {
-        const uint32_t m = total - base < SK_PFL_PIECE ? total - base : SK_PFL_PIECE;
-#pragma unroll
-        for (int q = 0; q < PER; q++) {
-            const uint32_t i = threadIdx.x + q * SK_PFL_BTPB;
-            r[q] = ~0ull;
-            bl[q] = 0;
-            if (i >= m) continue;
-            const uint32_t x = base + i;
-            uint32_t lo = 0, hi = nb; // segp[lo] <= x < segp[hi]
-            while (hi - lo > 1) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if (segp[mid] <= x) lo = mid;
-                else hi = mid;
-            }
-            bl[q] = b0 + lo;
-            r[q] = chunks[uint64_t(b0 + lo) * SK_PFP_EPB + segs[lo] + (x - segp[lo])];
-        }
-    };
-    uint64_t r[PER];
-    uint32_t bl[PER];
-    if (total) load(0, r, bl);
-    for (uint32_t base = 0; base < total; base += SK_PFL_PIECE) { // uniform
-        const uint32_t m = total - base < SK_PFL_PIECE ? total - base : SK_PFL_PIECE;
-        uint32_t rk[PER];
-#pragma unroll
-        for (int q = 0; q < PER; q++) {
-            const uint64_t rr = r[q];
-            const uint32_t blk = bl[q];
-            r[q] = ~0ull;
-            if (threadIdx.x + q * SK_PFL_BTPB >= m) continue;
-            if (uint32_t(rr >> 32) >= pm.nslab) continue; // ids beyond the store's slabs are dropped (both passes)
-            const uint32_t slab = pm.fwd(uint32_t(rr >> 32)), reg = uint32_t(rr >> 18) & 16383u,
-                           rho = uint32_t(rr >> 12) & 63u;
-            r[q] = (uint64_t(slab & ((1u << sh) - 1)) << 46) | (uint64_t(reg) << 32) | (uint64_t(rho) << 26) |
-                   (uint64_t(blk) * SK_PFP_EPB + (rr & 4095u));
-            rk[q] = atomicAdd(&lcnt[slab >> sh], 1u) | ((slab >> sh) << 13);
-        }
-        uint64_t rn[PER];
-        uint32_t bln[PER];
-        if (base + SK_PFL_PIECE < total) load(base + SK_PFL_PIECE, rn, bln);
-        __syncthreads();
-        // exclusive scan of the piece's counts over the fine buckets (in place), nsub <= SK_PFL_MAXSUB
-        uint32_t acc = 0;
-        for (uint32_t x0 = 0; x0 < nsub; x0 += SK_PFL_BTPB) {
-            const uint32_t x = x0 + threadIdx.x, v = x < nsub ? lcnt[x] : 0u;
-            uint32_t tot;
-            const uint32_t e = block_exscan<SK_PFL_BTPB>(v, wsum, &tot);
-            if (x < nsub) lcnt[x] = acc + e;
-            acc += tot;
-        }
-        __syncthreads();
-#pragma unroll
-        for (int q = 0; q < PER; q++)
-            if (r[q] != ~0ull) sorted[lcnt[rk[q] >> 13] + (rk[q] & 8191u)] = r[q];
-        __syncthreads();
-        const uint32_t kept = acc; // records of the piece that have a fine bucket
-        for (uint32_t i = threadIdx.x; i < kept; i += SK_PFL_BTPB) {
-            const uint64_t rr = sorted[i];
-            // fine bucket of sorted[i]: the record's sketch, relative to this coarse bucket's sub range
-            uint32_t lo = 0, hi = nsub; // lcnt[lo] <= i < lcnt[hi] (lcnt[nsub] = kept)
-            while (hi - lo > 1) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if (lcnt[mid] <= i) lo = mid;
-                else hi = mid;
-            }
-            rec2[cur[lo] + (i - lcnt[lo])] = rr;
-        }
-        __syncthreads();
-        // advance the runs' cursors by the piece's counts, clear the counts
-        for (uint32_t x = threadIdx.x; x < nsub; x += SK_PFL_BTPB) {
-            const uint32_t nx = (x + 1 < nsub ? lcnt[x + 1] : kept) - lcnt[x];
-            cur[x] += nx;
-        }
-        __syncthreads();
-        for (uint32_t x = threadIdx.x; x < nsub; x += SK_PFL_BTPB) lcnt[x] = 0;
-        __syncthreads();
-#pragma unroll
-        for (int q = 0; q < PER; q++) {
-            r[q] = rn[q];
-            bl[q] = bln[q];
-        }
-    }
-}
-
-// exclusive scan of u32[n] in place, total at [n]: block sums, one-workgroup scan of the sums, block scans
-#define SK_SCAN_TPB 1024
-#define SK_SCAN_PER 4
-#define SK_SCAN_ITEMS (SK_SCAN_TPB * SK_SCAN_PER)
-__global__ void __launch_bounds__(SK_SCAN_TPB) k_scan_reduce(uint64_t n, const uint32_t *__restrict__ v,
-                                                             uint32_t *__restrict__ sums) {
-    __shared__ uint32_t wsum[SK_SCAN_TPB / 64];
-    const uint64_t base = uint64_t(blockIdx.x) * SK_SCAN_ITEMS;
+// records of region (b, t) = sum over the tile's blocks of segment b's length; grid (ntile, 128)
+__global__ void __launch_bounds__(256) k_pfl_tot(const uint32_t *__restrict__ S, uint32_t nblk, uint32_t tb,
+                                                 uint32_t ntile, uint32_t *__restrict__ tot) {
+    __shared__ uint32_t wsum[256 / 64];
+    const uint32_t t = blockIdx.x, b = blockIdx.y, b0 = t * tb, b1 = b0 + tb < nblk ? b0 + tb : nblk;
     uint32_t s = 0;
-#pragma unroll
-    for (int q = 0; q < SK_SCAN_PER; q++) {
-        const uint64_t i = base + uint64_t(q) * SK_SCAN_TPB + threadIdx.x;
-        s += i < n ? v[i] : 0u;
-    }
-    uint32_t tot;
-    block_exscan<SK_SCAN_TPB>(s, wsum, &tot);
-    if (threadIdx.x == 0) sums[blockIdx.x] = tot;
+    for (uint32_t blk = b0 + threadIdx.x; blk < b1; blk += 256)
+        s += S[uint64_t(b + 1) * nblk + blk] - S[uint64_t(b) * nblk + blk];
+    uint32_t total;
+    block_exscan<256>(s, wsum, &total);
+    if (threadIdx.x == 0) tot[b * ntile + t] = total;
 }
-__global__ void __launch_bounds__(SK_SCAN_TPB) k_scan_sums(uint32_t nb, uint32_t *__restrict__ sums) {
-    __shared__ uint32_t wsum[SK_SCAN_TPB / 64];
-    uint32_t carry = 0;
-    for (uint32_t b0 = 0; b0 < nb; b0 += SK_SCAN_TPB) {
-        const uint32_t i = b0 + threadIdx.x, x = i < nb ? sums[i] : 0u;
-        uint32_t tot;
-        const uint32_t ex = block_exscan<SK_SCAN_TPB>(x, wsum, &tot);
-        if (i < nb) sums[i] = carry + ex;
-        carry += tot;
+
+// The region's record x: segment lo with segp[lo] <= x < segp[lo + 1] (binary search over the tile's prefix)
+__device__ __forceinline__ uint64_t pfl_region_rec(const uint64_t *__restrict__ chunks, const uint32_t *segp,
+                                                   const uint32_t *segs, uint32_t nb, uint32_t b0, uint32_t x,
+                                                   uint32_t *blk) {
+    uint32_t lo = 0, hi = nb;
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (segp[mid] <= x) lo = mid;
+        else hi = mid;
     }
-    if (threadIdx.x == 0) sums[nb] = carry;
+    *blk = b0 + lo;
+    return chunks[uint64_t(b0 + lo) * SK_PFP_EPB + segs[lo] + (x - segp[lo])];
 }
-__global__ void __launch_bounds__(SK_SCAN_TPB) k_scan_apply(uint64_t n, uint32_t *__restrict__ v,
-                                                            const uint32_t *__restrict__ sums) {
-    __shared__ uint32_t wsum[SK_SCAN_TPB / 64];
-    const uint64_t base = uint64_t(blockIdx.x) * SK_SCAN_ITEMS + uint64_t(threadIdx.x) * SK_SCAN_PER;
-    uint32_t x[SK_SCAN_PER], s = 0;
-#pragma unroll
-    for (int q = 0; q < SK_SCAN_PER; q++) {
-        x[q] = base + q < n ? v[base + q] : 0u;
-        s += x[q];
+
+// One workgroup per region g = b * ntile + t.  Dynamic LDS: cap records (u64) + nsub + 1 counts.
+// Outputs: rbase[g] (the region's first rec2 slot), C2[g][0..nsub] (exclusive starts of the fine buckets' runs
+// inside the region, [nsub] = records kept), rec2[rbase + ...] the runs; dropped records (slab >= nslab) reply 0.
+__global__ void __launch_bounds__(SK_PFL_RTPB) k_pfl_region(const uint64_t *__restrict__ chunks,
+                                                            const uint32_t *__restrict__ S, uint32_t nblk, uint32_t tb,
+                                                            uint32_t ntile, uint32_t nsub, uint32_t sh, PflPerm pm,
+                                                            uint32_t cap, const uint32_t *__restrict__ tot,
+                                                            uint32_t *__restrict__ rbase, uint32_t *__restrict__ C2,
+                                                            uint64_t *__restrict__ rec2,
+                                                            uint8_t *__restrict__ changed) {
+    extern __shared__ uint64_t dyn64[];
+    uint64_t *sorted = dyn64;
+    uint32_t *hist = reinterpret_cast<uint32_t *>(dyn64 + cap);
+    __shared__ uint32_t segp[SK_PFL_TMAX + 1], segs[SK_PFL_TMAX];
+    __shared__ uint32_t wsum[SK_PFL_RTPB / 64];
+    const uint32_t tid = threadIdx.x, g = blockIdx.x, b = g / ntile, t = g % ntile;
+    const uint32_t b0 = t * tb, nb = (b0 + tb < nblk ? b0 + tb : nblk) - b0;
+    // this region's base: the records of every region before it (b-major, tile minor)
+    uint32_t acc = 0;
+    for (uint32_t i = tid; i < g; i += SK_PFL_RTPB) acc += tot[i];
+    uint32_t base;
+    block_exscan<SK_PFL_RTPB>(acc, wsum, &base);
+    uint32_t st = 0, len = 0;
+    if (tid < nb) {
+        st = S[uint64_t(b) * nblk + b0 + tid];
+        len = S[uint64_t(b + 1) * nblk + b0 + tid] - st;
+        segs[tid] = st;
     }
-    uint32_t tot;
-    uint32_t ex = sums[blockIdx.x] + block_exscan<SK_SCAN_TPB>(s, wsum, &tot);
-#pragma unroll
-    for (int q = 0; q < SK_SCAN_PER; q++) {
-        if (base + q < n) v[base + q] = ex;
-        ex += x[q];
+    uint32_t m;
+    const uint32_t ex = block_exscan<SK_PFL_RTPB>(len, wsum, &m);
+    if (tid < nb) segp[tid] = ex;
+    for (uint32_t x = tid; x <= nsub; x += SK_PFL_RTPB) hist[x] = 0;
+    if (tid == 0) {
+        segp[nb] = m;
+        rbase[g] = base;
     }
-    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) v[n] = sums[gridDim.x];
+    __syncthreads();
+    uint32_t *C = C2 + uint64_t(g) * (nsub + 1);
+    // a record of the region -> its rec2 value (fine bucket in sub), or ~0 for a dropped record
+    auto conv = [&](uint64_t rr, uint32_t blk, uint32_t *sub) -> uint64_t {
+        const uint32_t seq = blk * SK_PFP_EPB + uint32_t(rr & 4095u);
+        if (uint32_t(rr >> 32) >= pm.nslab) { // ids beyond the store's slabs are dropped
+            if (changed) changed[seq] = 0;
+            return ~0ull;
+        }
+        const uint32_t slab = pm.fwd(uint32_t(rr >> 32)), reg = uint32_t(rr >> 18) & 16383u,
+                       rho = uint32_t(rr >> 12) & 63u;
+        *sub = slab >> sh;
+        return (uint64_t(slab & ((1u << sh) - 1)) << 46) | (uint64_t(reg) << 32) | (uint64_t(rho) << 26) | seq;
+    };
+    // exclusive scan of hist[0..nsub) in place (nsub <= 8 per thread), hist[nsub] = total; also written to C
+    auto scan_hist = [&]() {
+        constexpr int HP = SK_PFL_MAXSUB / SK_PFL_RTPB;
+        uint32_t v[HP], s = 0;
+#pragma unroll
+        for (int q = 0; q < HP; q++) {
+            const uint32_t x = tid * HP + q;
+            v[q] = x < nsub ? hist[x] : 0u;
+            s += v[q];
+        }
+        uint32_t total;
+        uint32_t e = block_exscan<SK_PFL_RTPB>(s, wsum, &total);
+#pragma unroll
+        for (int q = 0; q < HP; q++) {
+            const uint32_t x = tid * HP + q;
+            if (x < nsub) {
+                hist[x] = e;
+                C[x] = e;
+            }
+            e += v[q];
+        }
+        if (tid == 0) {
+            hist[nsub] = total;
+            C[nsub] = total;
+        }
+        __syncthreads();
+    };
+    if (m <= cap) { // one piece: every record in registers, ranked by its fine bucket, placed in LDS, written out
+        uint64_t r[SK_PFL_RPER];
+        uint32_t rk[SK_PFL_RPER];
+#pragma unroll
+        for (int q = 0; q < SK_PFL_RPER; q++) {
+            const uint32_t x = tid + q * SK_PFL_RTPB;
+            r[q] = ~0ull;
+            if (x < m) {
+                uint32_t blk;
+                r[q] = pfl_region_rec(chunks, segp, segs, nb, b0, x, &blk);
+                rk[q] = blk;
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < SK_PFL_RPER; q++) {
+            if (r[q] == ~0ull) continue;
+            uint32_t sub = 0;
+            r[q] = conv(r[q], rk[q], &sub);
+            if (r[q] != ~0ull) rk[q] = atomicAdd(&hist[sub], 1u) | (sub << 14);
+        }
+        __syncthreads();
+        scan_hist();
+#pragma unroll
+        for (int q = 0; q < SK_PFL_RPER; q++)
+            if (r[q] != ~0ull) sorted[hist[rk[q] >> 14] + (rk[q] & 16383u)] = r[q];
+        __syncthreads();
+        const uint32_t kept = hist[nsub];
+        uint64_t *dst = rec2 + base;
+        for (uint32_t i = tid; i < kept; i += SK_PFL_RTPB) dst[i] = sorted[i];
+        return;
+    }
+    // swollen region (one element repeated in many blocks): count every piece, then place every piece; the runs
+    // keep piece (= batch) order
+    for (uint32_t p0 = 0; p0 < m; p0 += cap) {
+#pragma unroll 4
+        for (int q = 0; q < SK_PFL_RPER; q++) {
+            const uint32_t x = p0 + tid + q * SK_PFL_RTPB;
+            if (x >= m || x - p0 >= cap) continue;
+            uint32_t blk, sub = 0;
+            const uint64_t rr = conv(pfl_region_rec(chunks, segp, segs, nb, b0, x, &blk), blk, &sub);
+            if (rr != ~0ull) atomicAdd(&hist[sub], 1u);
+        }
+    }
+    __syncthreads();
+    scan_hist();
+    uint32_t *lcnt = reinterpret_cast<uint32_t *>(sorted); // cap * 8 >= nsub * 4 bytes
+    for (uint32_t x = tid; x < nsub; x += SK_PFL_RTPB) lcnt[x] = 0;
+    __syncthreads();
+    for (uint32_t p0 = 0; p0 < m; p0 += cap) {
+#pragma unroll 4
+        for (int q = 0; q < SK_PFL_RPER; q++) {
+            const uint32_t x = p0 + tid + q * SK_PFL_RTPB;
+            if (x >= m || x - p0 >= cap) continue;
+            uint32_t blk, sub = 0;
+            const uint64_t rr = conv(pfl_region_rec(chunks, segp, segs, nb, b0, x, &blk), blk, &sub);
+            if (rr != ~0ull) rec2[base + hist[sub] + atomicAdd(&lcnt[sub], 1u)] = rr;
+        }
+        __syncthreads();
+        for (uint32_t x = tid; x < nsub; x += SK_PFL_RTPB) {
+            hist[x] += lcnt[x];
+            lcnt[x] = 0;
+        }
+        __syncthreads();
+    }
+}
+
+// Reply default: the apply stores only replies that differ from it, after k_pfl_fill wrote it everywhere.  It is
+// the majority reply of the previous call, from counters a sample of apply workgroups (1 in 16) kept: rc[16 p ..
+// 16 p + 8) ones and [16 p + 8, 16 p + 16) replies, parity p alternating per call (this call reads p and fills
+// p ^ 1, which its fill zeroed).
+__device__ __forceinline__ uint32_t pfl_dflt(const uint32_t *rc, uint32_t p) {
+    uint32_t ones = 0, all = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        ones += rc[16 * p + i];
+        all += rc[16 * p + 8 + i];
+    }
+    return 2 * ones > all ? 1u : 0u;
+}
+__global__ void __launch_bounds__(256) k_pfl_fill(uint8_t *__restrict__ changed, uint64_t n, uint32_t *rc,
+                                                  uint32_t p) {
+    const uint32_t v = pfl_dflt(rc, p) * 0x01010101u;
+    if (blockIdx.x == 0 && threadIdx.x < 16) rc[16 * (p ^ 1) + threadIdx.x] = 0;
+    const uint64_t a = (16 - (reinterpret_cast<uintptr_t>(changed) & 15)) & 15; // bytes before the first 16-B word
+    const uint64_t head = a < n ? a : n, nv = (n - head) >> 4;
+    const uint64_t i = uint64_t(blockIdx.x) * 256 + threadIdx.x, stride = uint64_t(gridDim.x) * 256;
+    uint4 *w = reinterpret_cast<uint4 *>(changed + head);
+    for (uint64_t j = i; j < nv; j += stride) w[j] = make_uint4(v, v, v, v);
+    if (i < head) changed[i] = uint8_t(v);
+    if (i < ((n - head) & 15)) changed[head + nv * 16 + i] = uint8_t(v);
 }
 
 // one chunk of records R[0..cnt) (every record of its registers with a smaller seq is in this chunk or was
 // applied to `reg` before): chains per register, sequential replies, final register values into `reg` (LDS).
 // Caller syncs before (R loaded, heads cleared) and after; `fill` runs between the chain build and the walk (the
-// caller's register lines, loaded into registers before, go to LDS while the chains are built).
-template <class Fill>
+// caller's register lines, loaded into registers before, go to LDS while the chains are built).  `put` stores a
+// reply (only those that differ from the call's default when the replies were pre-filled).
+template <class Fill, class Put>
 __device__ __forceinline__ void pfl_chunk(const uint64_t *R, uint32_t cnt, uint16_t *nxt, uint32_t *head,
-                                          uint8_t *fin, uint8_t *reg, uint8_t *dirty, uint8_t *__restrict__ changed,
-                                          int probe, Fill fill) {
+                                          uint8_t *fin, uint8_t *reg, uint8_t *dirty, Fill fill, Put put) {
     for (uint32_t u = threadIdx.x; u < cnt; u += SK_PFL_ATPB)
         nxt[u] = uint16_t(atomicExch(&head[pfl_ht(R[u] >> 32)], u));
     fill();
@@ -1187,8 +1164,7 @@ __device__ __forceinline__ void pfl_chunk(const uint64_t *R, uint32_t cnt, uint1
         }
         const uint32_t slotb = pfl_slotb(key);
         const uint32_t R0 = reg[slotb];
-        const uint8_t rep = rho > (R0 > p ? R0 : p);
-        if (!(probe & 32) || rep) changed[seq] = rep; // probe & 32: the replies were zeroed, only 1s are stored
+        put(uint32_t(seq), uint32_t(rho > (R0 > p ? R0 : p)));
         fin[u] = earliest && m > R0 ? uint8_t(m) : uint8_t(0);
     }
     __syncthreads();
@@ -1204,11 +1180,20 @@ __device__ __forceinline__ void pfl_chunk(const uint64_t *R, uint32_t cnt, uint1
 // than one chunk (C1, a Zipf head's lines -- they run longest) in order[0..H), H = ctr[0], and heavy slot k applies
 // order[k].  The rest of the grid is the fine buckets in their own order; a heavy one there exits at once.  A
 // uniform call has H = 0: its heavy slots exit and nothing else is indirected.
-__global__ void __launch_bounds__(256) k_pfl_plan(const uint32_t *__restrict__ C, uint32_t ntile, uint32_t nf,
-                                                  uint32_t hmax, uint32_t *ctr, uint32_t *__restrict__ order) {
+__global__ void __launch_bounds__(256) k_pfl_plan(const uint32_t *__restrict__ C2, uint32_t ntile, uint32_t nsub,
+                                                  uint32_t nf, uint32_t hmax, uint32_t *ctr,
+                                                  uint32_t *__restrict__ order) {
     __shared__ uint32_t wsum[256 / 64], base;
     const uint32_t f = blockIdx.x * 256 + threadIdx.x;
-    const bool heavy = f < nf && C[uint64_t(f) * ntile + ntile] - C[uint64_t(f) * ntile] > SK_PFL_CAP;
+    uint32_t cnt = 0;
+    if (f < nf) {
+        const uint32_t b = f / nsub, sub = f % nsub;
+        for (uint32_t t = 0; t < ntile; t++) {
+            const uint32_t *c = C2 + uint64_t(b * ntile + t) * (nsub + 1) + sub;
+            cnt += c[1] - c[0];
+        }
+    }
+    const bool heavy = cnt > SK_PFL_CAP;
     uint32_t th;
     const uint32_t ph = block_exscan<256>(heavy ? 1u : 0u, wsum, &th);
     if (threadIdx.x == 0) base = th ? atomicAdd(ctr, th) : 0u;
@@ -1217,13 +1202,15 @@ __global__ void __launch_bounds__(256) k_pfl_plan(const uint32_t *__restrict__ C
 }
 
 __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const uint64_t *__restrict__ rec2,
-                                                           const uint32_t *__restrict__ C, uint32_t ntile,
+                                                           const uint32_t *__restrict__ rbase,
+                                                           const uint32_t *__restrict__ C2, uint32_t ntile,
                                                            uint32_t nsub, uint32_t sh, PflPerm pm, uint32_t nslab,
                                                            uint8_t *arena,
                                                            uint8_t *__restrict__ changed, uint32_t *big_alloc,
                                                            uint64_t *big_keys, uint32_t *big_vals, int probe,
                                                            uint32_t hmax, const uint32_t *order_n,
-                                                           const uint32_t *__restrict__ order) {
+                                                           const uint32_t *__restrict__ order, uint32_t *rc,
+                                                           uint32_t par) {
     constexpr uint32_t NL = 1u << SK_PFL_SH;
     constexpr uint32_t kWork = SK_PFL_CAP * 8 + SK_PFL_CAP * 2 + SK_PFL_HT * 4 + SK_PFL_CAP;
     constexpr uint32_t kBigL = 1024;       // LDS slots of the big-run table
@@ -1232,6 +1219,8 @@ __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const uint64_t *__res
     __shared__ uint4 regs4[NL * LW];           // line of sketch slab0 + i at reg[i << SK_PFL_LB]
     __shared__ uint64_t work[(kWork + 7) / 8]; // chunk records, chains, final values (or the big-run table)
     __shared__ uint8_t dirty[NL];
+    __shared__ uint32_t rs[SK_PFL_NTMAX], rp[SK_PFL_NTMAX + 1]; // the fine bucket's run per tile: start, prefix
+    __shared__ uint32_t wsum[SK_PFL_ATPB / 64], s_ones;
     uint8_t *reg = reinterpret_cast<uint8_t *>(regs4);
     uint64_t *R = work;
     uint16_t *nxt = reinterpret_cast<uint16_t *>(R + SK_PFL_CAP);
@@ -1246,10 +1235,40 @@ __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const uint64_t *__res
         f = blockIdx.x - hmax;
     }
     const uint32_t b = f / nsub, sub = f % nsub;
-    const uint64_t c0 = uint64_t(f) * ntile;
-    const uint32_t start = C[c0], end = C[c0 + ntile], cnt = end - start;
+    uint32_t st = 0, len = 0;
+    if (threadIdx.x < ntile) {
+        const uint32_t g = b * ntile + threadIdx.x;
+        const uint32_t *c = C2 + uint64_t(g) * (nsub + 1) + sub;
+        const uint32_t c0 = c[0];
+        st = rbase[g] + c0;
+        len = c[1] - c0;
+        rs[threadIdx.x] = st;
+    }
+    uint32_t cnt;
+    const uint32_t ex = block_exscan<SK_PFL_ATPB>(len, wsum, &cnt);
     if (cnt == 0) return; // uniform
     if (hmax && blockIdx.x >= hmax && cnt > SK_PFL_CAP) return; // applied by a heavy slot
+    if (threadIdx.x < ntile) rp[threadIdx.x] = ex;
+    // record u of the fine bucket (u < cnt): run t with rp[t] <= u < rp[t + 1]
+    auto rec_at = [&](uint32_t u) -> uint64_t {
+        uint32_t lo = 0, hi = ntile;
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (rp[mid] <= u) lo = mid;
+            else hi = mid;
+        }
+        return rec2[rs[lo] + (u - rp[lo])];
+    };
+    const uint32_t dflt = (probe & 32) ? pfl_dflt(rc, par) : 2u; // 2: no default, every reply stored
+    const bool sample = (probe & 32) && (blockIdx.x & 15u) == 0;
+    uint32_t nrep = 0; // replies made by this thread (sampled workgroups)
+    auto put = [&](uint32_t seq, uint32_t rep) {
+        if (!(probe & 64) && rep != dflt) changed[seq] = uint8_t(rep); // probe & 64: dev ablation, no reply stores
+        if (sample) {
+            nrep++;
+            if (rep) atomicAdd(&s_ones, 1u);
+        }
+    };
     const uint32_t slab0 = sub << sh, nsl = 1u << sh; // permuted ids slab0 + i, i < nsl
     auto line = [&](uint32_t i) -> uint4 * {
         const uint32_t s = pm.inv(slab0 + i);
@@ -1257,6 +1276,10 @@ __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const uint64_t *__res
     };
     for (uint32_t i = threadIdx.x; i < NL; i += SK_PFL_ATPB) dirty[i] = 0;
     for (uint32_t t = threadIdx.x; t < SK_PFL_HT; t += SK_PFL_ATPB) head[t] = 0xffffu;
+    if (threadIdx.x == 0) {
+        rp[ntile] = cnt;
+        s_ones = 0;
+    }
     __syncthreads();
     if (cnt <= SK_PFL_CAP) { // the whole fine bucket is one chunk: records and lines in one round trip
         constexpr int LQ = (NL * LW + SK_PFL_ATPB - 1) / SK_PFL_ATPB;
@@ -1272,7 +1295,7 @@ __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const uint64_t *__res
 #pragma unroll
         for (int q = 0; q < RU; q++) {
             const uint32_t u = q * SK_PFL_ATPB + threadIdx.x;
-            if (u < cnt) rv[q] = rec2[start + u];
+            if (u < cnt) rv[q] = rec_at(u);
         }
 #pragma unroll
         for (int q = 0; q < RU; q++) {
@@ -1280,30 +1303,30 @@ __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const uint64_t *__res
             if (u < cnt) R[u] = rv[q];
         }
         __syncthreads();
-        pfl_chunk(R, cnt, nxt, head, fin, reg, dirty, changed, probe, [&] {
+        pfl_chunk(R, cnt, nxt, head, fin, reg, dirty, [&] {
 #pragma unroll
             for (int j = 0; j < LQ; j++) {
                 const uint32_t q = threadIdx.x + j * SK_PFL_ATPB;
                 if (q < nsl * LW && pm.inv(slab0 + q / LW) < nslab) regs4[q] = lv[j];
             }
-        });
+        }, put);
     } else {
         for (uint32_t q = threadIdx.x; q < nsl * LW; q += SK_PFL_ATPB)
             if (pm.inv(slab0 + q / LW) < nslab) regs4[q] = line(q / LW)[q % LW];
         __syncthreads();
         uint32_t t0 = 0;
         while (t0 < ntile) { // uniform: chunks of whole runs, in tile (= batch) order
-            const uint32_t a = C[c0 + t0];
+            const uint32_t a = rp[t0];
             uint32_t t1 = t0 + 1;
-            while (t1 < ntile && C[c0 + t1 + 1] - a <= SK_PFL_CAP) t1++;
-            const uint32_t z = C[c0 + t1], k = z - a;
+            while (t1 < ntile && rp[t1 + 1] - a <= SK_PFL_CAP) t1++;
+            const uint32_t k = rp[t1] - a;
             if (k <= SK_PFL_CAP) {
                 constexpr int CU = SK_PFL_CAP / SK_PFL_ATPB;
                 uint64_t rr[CU];
 #pragma unroll
                 for (int q = 0; q < CU; q++) {
                     const uint32_t u = q * SK_PFL_ATPB + threadIdx.x;
-                    if (u < k) rr[q] = rec2[a + u];
+                    if (u < k) rr[q] = rec_at(a + u);
                 }
 #pragma unroll
                 for (int q = 0; q < CU; q++) {
@@ -1311,8 +1334,9 @@ __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const uint64_t *__res
                     if (u < k) R[u] = rr[q];
                 }
                 __syncthreads();
-                pfl_chunk(R, k, nxt, head, fin, reg, dirty, changed, probe, [] {});
-            } else { // one run larger than a chunk (t1 == t0 + 1)
+                pfl_chunk(R, k, nxt, head, fin, reg, dirty, [] {}, put);
+            } else { // one run larger than a chunk (t1 == t0 + 1), contiguous from rs[t0]
+                const uint64_t *run = rec2 + rs[t0];
                 // only records above their register can rise, and only they can stop a later record from rising:
                 // the rest reply 0 now; the candidates are resolved as a chunk when they fit (a hot sketch whose
                 // registers are already high has few), else with the (slot, rho) -> min seq table
@@ -1325,7 +1349,7 @@ __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const uint64_t *__res
 #pragma unroll
                     for (int q = 0; q < FU; q++) {
                         const uint32_t u = u0 + q * SK_PFL_ATPB + threadIdx.x;
-                        rr[q] = u < k ? rec2[a + u] : ~0ull;
+                        rr[q] = u < k ? run[u] : ~0ull;
                     }
 #pragma unroll
                     for (int q = 0; q < FU; q++) {
@@ -1335,14 +1359,14 @@ __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const uint64_t *__res
                             const uint32_t i = atomicAdd(&ncand, 1u);
                             if (i < SK_PFL_CAP) R[i] = r;
                         } else {
-                            if (!(probe & 32)) changed[r & 0x3ffffffu] = 0;
+                            put(uint32_t(r & 0x3ffffffu), 0u);
                         }
                     }
                 }
                 __syncthreads();
                 const uint32_t nc = ncand;
                 if (nc <= SK_PFL_CAP) {
-                    pfl_chunk(R, nc, nxt, head, fin, reg, dirty, changed, probe, [] {});
+                    pfl_chunk(R, nc, nxt, head, fin, reg, dirty, [] {}, put);
                 } else {
                 __shared__ uint32_t gbase;
                 unsigned long long *lk = reinterpret_cast<unsigned long long *>(work);
@@ -1360,22 +1384,22 @@ __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const uint64_t *__res
                     return ((r >> 26) & 63u) > reg[pfl_slotb(key)];
                 };
                 for (uint32_t u = threadIdx.x; u < k; u += SK_PFL_ATPB) {
-                    const uint64_t r = rec2[a + u];
+                    const uint64_t r = run[u];
                     if (cand(r)) T.insert(((r >> 32) << 6) | ((r >> 26) & 63u), uint32_t(r & 0x3ffffffu));
                 }
                 __threadfence();
                 __syncthreads();
                 for (uint32_t u = threadIdx.x; u < k; u += SK_PFL_ATPB) { // replies (registers only read)
-                    const uint64_t r = rec2[a + u], key = r >> 32;
+                    const uint64_t r = run[u], key = r >> 32;
                     if (!cand(r)) continue;
                     const uint32_t rho = uint32_t(r >> 26) & 63u, seq = uint32_t(r & 0x3ffffffu);
                     bool first = true;
                     for (uint32_t v = rho; v < 52 && first; v++) first = T.find((key << 6) | v) >= seq;
-                    if (!(probe & 32) || first) changed[seq] = first ? 1 : 0;
+                    put(seq, first ? 1u : 0u);
                 }
                 __syncthreads();
                 for (uint32_t u = threadIdx.x; u < k; u += SK_PFL_ATPB) { // the register's writer: its top record
-                    const uint64_t r = rec2[a + u], key = r >> 32;
+                    const uint64_t r = run[u], key = r >> 32;
                     if (!cand(r)) continue;
                     const uint32_t rho = uint32_t(r >> 26) & 63u, seq = uint32_t(r & 0x3ffffffu);
                     if (T.find((key << 6) | rho) != seq) continue;
@@ -1396,6 +1420,15 @@ __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const uint64_t *__res
         }
     }
     __syncthreads();
+    if (sample) { // the reply mix of a sample of fine buckets decides the next call's default
+        uint32_t tot;
+        block_exscan<SK_PFL_ATPB>(nrep, wsum, &tot);
+        if (threadIdx.x == 0) {
+            const uint32_t sh8 = (blockIdx.x >> 4) & 7u, q = 16 * (par ^ 1);
+            atomicAdd(&rc[q + sh8], s_ones);
+            atomicAdd(&rc[q + 8 + sh8], tot);
+        }
+    }
     if (probe & 4) return;
     typedef unsigned int v4u __attribute__((ext_vector_type(4)));
     for (uint32_t q = threadIdx.x; q < nsl * LW; q += SK_PFL_ATPB)
@@ -2639,14 +2672,12 @@ hipError_t launch_pfp_reply(hipStream_t st, uint64_t n, const uint8_t *rep, cons
     return hipSuccess;
 }
 
-// line schedule: layout of one call's scratch (PflDims) and its five stages
+// line schedule: layout of one call's scratch (PflDims) and its stages
 PflDims pfl_dims(uint64_t n, uint32_t nslab, uint32_t tile_blocks) {
     PflDims d;
     d.nblk = pfp_blocks(n);
-    d.tb = tile_blocks ? tile_blocks : SK_PFL_TILE;
-    d.ntile = (d.nblk + d.tb - 1) / d.tb;
     // sketches per fine bucket: a fine bucket expects n * 2^sh / (128 * nslab) records; keep it near 768 (one
-    // chunk), within the LDS lines (2^SK_PFL_SH) and the scatter's fine-bucket arrays (SK_PFL_MAXSUB)
+    // chunk), within the LDS lines (2^SK_PFL_SH) and the region's fine-bucket counts (SK_PFL_MAXSUB)
     d.sh = SK_PFL_SH;
     while (d.sh > 0 && double(n) * double(1u << d.sh) > 768.0 * SK_PFL_NB * double(nslab ? nslab : 1) &&
            ((2 * uint64_t(nslab) + (1u << (d.sh - 1)) - 1) >> (d.sh - 1)) <= SK_PFL_MAXSUB)
@@ -2662,8 +2693,17 @@ PflDims pfl_dims(uint64_t n, uint32_t nslab, uint32_t tile_blocks) {
     d.nsub = uint32_t((uint64_t(d.pm_mask) + 1) >> d.sh);
     d.nslab = nslab;
     d.nf = uint64_t(SK_PFL_NB) * d.nsub;
-    d.ncount = d.nf * d.ntile;
-    d.nsums = uint32_t((d.ncount + SK_SCAN_ITEMS - 1) / SK_SCAN_ITEMS);
+    // region capacity in LDS: records (u64) + nsub + 1 counts; the tile keeps a region's binomial record count
+    // (mean 32 tb) 6 sigma below it
+    uint64_t cap = (uint64_t(SK_PFL_LDS) - 4ull * (d.nsub + 1)) / 8;
+    d.rcap = uint32_t(std::min<uint64_t>(cap & ~uint64_t(1023), SK_PFL_RCAP));
+    d.tb = tile_blocks ? tile_blocks : SK_PFL_TILE;
+    while (d.tb > 64 && 32.0 * d.tb + 6.0 * std::sqrt(32.0 * d.tb) > double(d.rcap)) d.tb -= 32;
+    if (d.tb > SK_PFL_TMAX) d.tb = SK_PFL_TMAX;
+    if (d.tb < (d.nblk + SK_PFL_NTMAX - 1) / SK_PFL_NTMAX) d.tb = (d.nblk + SK_PFL_NTMAX - 1) / SK_PFL_NTMAX;
+    d.ntile = (d.nblk + d.tb - 1) / d.tb;
+    d.nreg = SK_PFL_NB * d.ntile;
+    d.c_words = 2 * uint64_t(d.nreg) + uint64_t(d.nreg) * (d.nsub + 1);
     d.chunk_bytes = uint64_t(d.nblk) * SK_PFP_EPB * 8;
     d.S_bytes = uint64_t(SK_PFL_NB + 1) * d.nblk * 4;
     return d;
@@ -2680,40 +2720,53 @@ hipError_t launch_pfl_hash(hipStream_t st, uint64_t n, const uint32_t *key_ids, 
 }
 
 hipError_t launch_pfl_part(hipStream_t st, const PflDims &d, const uint64_t *chunks, const uint32_t *S, uint32_t *C,
-                           uint32_t *sums, uint64_t *rec2) {
-    if (d.nsub > SK_PFL_MAXSUB || d.tb > SK_PFL_TMAX || d.ncount >= (1ull << 32)) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_pfl_count, dim3(d.ntile * SK_PFL_NB), dim3(SK_PFL_BTPB), d.nsub * 4, st, chunks, S, d.nblk,
-                       d.tb, d.ntile, d.nsub, d.sh, PflPerm{d.pa, d.pai, d.pm_mask, d.nslab}, C);
+                           uint64_t *rec2, uint8_t *changed) {
+    if (d.nsub > SK_PFL_MAXSUB || d.tb > SK_PFL_TMAX || d.ntile > SK_PFL_NTMAX || d.rcap < SK_PFL_RTPB)
+        return hipErrorInvalidValue; // pfl_dims never produces these (the caller checks pfl_dims_ok)
+    uint32_t *tot = C, *rbase = C + d.nreg, *C2 = C + 2 * d.nreg;
+    hipLaunchKernelGGL(k_pfl_tot, dim3(d.ntile, SK_PFL_NB), dim3(256), 0, st, S, d.nblk, d.tb, d.ntile, tot);
     SK_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_scan_reduce, dim3(d.nsums), dim3(SK_SCAN_TPB), 0, st, d.ncount, C, sums);
+    const uint32_t lds = d.rcap * 8 + (d.nsub + 1) * 4;
+    static bool attr = false;
+    if (!attr) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_pfl_region),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, SK_PFL_LDS);
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
+    hipLaunchKernelGGL(k_pfl_region, dim3(d.nreg), dim3(SK_PFL_RTPB), lds, st, chunks, S, d.nblk, d.tb, d.ntile,
+                       d.nsub, d.sh, PflPerm{d.pa, d.pai, d.pm_mask, d.nslab}, d.rcap, tot, rbase, C2, rec2,
+                       changed);
     SK_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(SK_SCAN_TPB), 0, st, d.nsums, sums);
-    SK_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_scan_apply, dim3(d.nsums), dim3(SK_SCAN_TPB), 0, st, d.ncount, C, sums);
-    SK_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_pfl_scatter, dim3(d.ntile * SK_PFL_NB), dim3(SK_PFL_BTPB), 2 * d.nsub * 4, st, chunks, S,
-                       d.nblk, d.tb, d.ntile, d.nsub, d.sh, PflPerm{d.pa, d.pai, d.pm_mask, d.nslab}, C, rec2);
+    return hipSuccess;
+}
+bool pfl_dims_ok(const PflDims &d) {
+    return d.nsub <= SK_PFL_MAXSUB && d.tb <= SK_PFL_TMAX && d.ntile <= SK_PFL_NTMAX && d.rcap >= SK_PFL_RTPB;
+}
+
+hipError_t launch_pfl_fill(hipStream_t st, uint8_t *changed, uint64_t n, uint32_t *rc, uint32_t par) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k_pfl_fill, dim3(grid_for((n + 15) / 16, 256, 4096)), dim3(256), 0, st, changed, n, rc, par);
     SK_LAUNCH_CHECK();
     return hipSuccess;
 }
 
 hipError_t launch_pfl_apply(hipStream_t st, const PflDims &d, const uint64_t *rec2, const uint32_t *C, uint32_t nslab,
                             uint8_t *arena, uint8_t *changed, uint32_t *big_alloc, uint64_t *big_keys,
-                            uint32_t *big_vals, int flags, uint32_t *order) {
-    static const int probe_flags = getenv("SK_PFL_PROBE") ? atoi(getenv("SK_PFL_PROBE")) : 0; // dev ablations (bit 4)
+                            uint32_t *big_vals, int flags, uint32_t *order, uint32_t *rc, uint32_t par) {
+    static const int probe_flags = getenv("SK_PFL_PROBE") ? atoi(getenv("SK_PFL_PROBE")) : 0; // dev ablations
+    const uint32_t *rbase = C + d.nreg, *C2 = C + 2 * d.nreg;
     // heavy slots: at most n / (CAP + 1) fine buckets hold more than one chunk
     const uint32_t hmax = order ? uint32_t(std::min<uint64_t>(d.nf, uint64_t(d.nblk) * SK_PFP_EPB / (SK_PFL_CAP + 1)))
                                 : 0u;
     if (order) {
-        hipLaunchKernelGGL(k_pfl_plan, dim3(uint32_t((d.nf + 255) / 256)), dim3(256), 0, st, C, d.ntile,
+        hipLaunchKernelGGL(k_pfl_plan, dim3(uint32_t((d.nf + 255) / 256)), dim3(256), 0, st, C2, d.ntile, d.nsub,
                            uint32_t(d.nf), hmax, big_alloc + 1, order);
         SK_LAUNCH_CHECK();
     }
-    hipLaunchKernelGGL(k_pfl_apply, dim3(uint32_t(d.nf) + hmax), dim3(SK_PFL_ATPB), 0, st, rec2, C, d.ntile, d.nsub,
-                       d.sh,
-                       PflPerm{d.pa, d.pai, d.pm_mask, d.nslab}, nslab,
-                       arena, changed, big_alloc, big_keys, big_vals,
-                       flags | probe_flags, hmax, big_alloc + 1, order);
+    hipLaunchKernelGGL(k_pfl_apply, dim3(uint32_t(d.nf) + hmax), dim3(SK_PFL_ATPB), 0, st, rec2, rbase, C2, d.ntile,
+                       d.nsub, d.sh, PflPerm{d.pa, d.pai, d.pm_mask, d.nslab}, nslab, arena, changed, big_alloc,
+                       big_keys, big_vals, flags | probe_flags, hmax, big_alloc + 1, order, rc, par);
     SK_LAUNCH_CHECK();
     return hipSuccess;
 }

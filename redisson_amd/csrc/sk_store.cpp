@@ -58,8 +58,9 @@ struct DBuf {
     hipError_t ensure(size_t bytes) {
         if (bytes <= cap) return hipSuccess;
         // large buffers: 1/8 headroom in 2 MiB steps, so batches of slightly varying size do not reallocate (a
-        // hipFree synchronises the device and cost 28 ms once with a large keyspace resident); small ones exact
-        size_t nc = bytes;
+        // hipFree synchronises the device and cost 28 ms once with a large keyspace resident); small ones exact on
+        // the first allocation, then at least doubling (a slowly growing small request must not free every call)
+        size_t nc = cap ? std::max(bytes, cap * 2) : bytes;
         if (bytes >= (size_t(1) << 20)) {
             nc = std::max(bytes + bytes / 8, cap * 2);
             nc = (nc + (size_t(2) << 20) - 1) & ~((size_t(2) << 20) - 1);
@@ -208,6 +209,7 @@ struct sk_ctx {
     uint8_t *arena = nullptr;
     uint64_t hll_cap = 0, hll_next = 0;
     std::vector<uint32_t> hll_free;
+    uint64_t hll_retired = 0;      // slabs whose generation wrapped: never handed out again (stale handles stay stale)
     std::vector<uint8_t> hll_live; // slab id -> 1 while a key owns it (caller-cached ids are checked against it)
     std::vector<uint8_t> hll_gen;  // slab id -> generation, bumped when the slab is freed (top byte of a handle)
     std::vector<uint64_t> h_e0, h_off; // host PFADD staging, kept across calls (no page faults per batch)
@@ -291,7 +293,9 @@ struct sk_ctx {
     uint32_t pfl_tile = 0;      // hash blocks per run tile (SK_PFL_TILE, 0 = the kernel default)
     bool pfl_zero = true;       // replies pre-zeroed, the apply stores only the 1s (SK_PFL_ZERO)
     bool pfl_plan = true;       // heavy fine buckets dispatched first (SK_PFL_PLAN)
-    DBuf pfl_chunks, pfl_S, pfl_C, pfl_sums, pfl_rec, pfl_bk, pfl_bv, pfl_ovf, pfl_order;
+    DBuf pfl_chunks, pfl_S, pfl_C, pfl_rec, pfl_bk, pfl_bv, pfl_ovf, pfl_order;
+    DBuf pfl_rc;                // u32[32]: reply-mix counters that pick each call's reply default (two parities)
+    uint32_t pfl_par = 0;       // this call's parity
 };
 
 namespace {
@@ -813,7 +817,9 @@ int del_key(sk_ctx *c, const std::string &k, bool *removed) {
         HIPCHK(c, hipMemsetAsync(c->arena + uint64_t(e.id) * kHllBytes, 0, kHllBytes, c->st));
         c->hll_live[e.id] = 0;
         c->hll_gen[e.id] = uint8_t(c->hll_gen[e.id] + 1);
-        c->hll_free.push_back(e.id);
+        // a generation that wrapped would make a handle cached 256 frees ago live again: retire the slab instead
+        if (c->hll_gen[e.id] == 0) c->hll_retired++;
+        else c->hll_free.push_back(e.id);
         return SK_OK;
     }
     return str_free(c, e.id);
@@ -1002,35 +1008,44 @@ int pfadd_lines(sk_ctx *c, uint64_t n, const uint32_t *d_ids, const uint64_t *d_
     if (n > (1ull << 26)) return fail(c, SK_EINVAL, "PFADD line batch too large");
     const uint32_t nslab = uint32_t(c->hll_next);
     const sk::PflDims d = sk::pfl_dims(n, nslab, c->pfl_tile);
+    if (!sk::pfl_dims_ok(d))
+        return fail(c, SK_EINVAL, "PFADD line schedule: tile of %u hash blocks out of range (SK_PFL_TILE)", d.tb);
     HIPCHK(c, c->pfl_chunks.ensure(d.chunk_bytes));
     HIPCHK(c, c->pfl_S.ensure(d.S_bytes));
-    HIPCHK(c, c->pfl_C.ensure((d.ncount + 1) * 4));
-    HIPCHK(c, c->pfl_sums.ensure((uint64_t(d.nsums) + 1) * 4));
+    HIPCHK(c, c->pfl_C.ensure(d.c_words * 4));
     HIPCHK(c, c->pfl_rec.ensure(n * 8));
     HIPCHK(c, c->pfl_bk.ensure(2 * n * 8));
     HIPCHK(c, c->pfl_bv.ensure(2 * n * 4));
     HIPCHK(c, c->pfl_ovf.ensure(64));
     HIPCHK(c, c->pfl_order.ensure(d.nf * 4));
+    if (!c->pfl_rc.p) { // first call: no reply mix yet (default 0)
+        HIPCHK(c, c->pfl_rc.ensure(32 * 4));
+        HIPCHK(c, hipMemsetAsync(c->pfl_rc.p, 0, 32 * 4, c->st));
+    }
     { Prof p_(c, 24);
     HIPCHK(c, sk::launch_pfl_hash(c->st, n, d_ids, d_off, d_bytes, c->redis_major >= 5, c->pfl_chunks.as<uint64_t>(),
                                   c->pfl_S.as<uint32_t>(), c->pfl_ovf.as<uint32_t>())); }
     { Prof p_(c, 25);
     HIPCHK(c, sk::launch_pfl_part(c->st, d, c->pfl_chunks.as<uint64_t>(), c->pfl_S.as<uint32_t>(),
-                                  c->pfl_C.as<uint32_t>(), c->pfl_sums.as<uint32_t>(), c->pfl_rec.as<uint64_t>())); }
-    // replies: zeroed by one streaming memset, then the apply stores only the 1s (a register rise), instead of one
-    // scattered byte per element (SK_PFL_ZERO=0: every reply stored by the apply)
-    if (c->pfl_zero) HIPCHK(c, hipMemsetAsync(d_changed, 0, n, c->st));
+                                  c->pfl_C.as<uint32_t>(), c->pfl_rec.as<uint64_t>(), d_changed)); }
+    // replies: pre-filled with the call's default (the previous call's majority reply) by one streaming kernel, then
+    // the apply stores only the other replies, instead of one scattered byte per element (SK_PFL_ZERO=0: every
+    // reply stored by the apply)
+    const uint32_t par = c->pfl_par;
+    c->pfl_par ^= 1;
     { Prof p_(c, 26);
+    if (c->pfl_zero) HIPCHK(c, sk::launch_pfl_fill(c->st, d_changed, n, c->pfl_rc.as<uint32_t>(), par));
     HIPCHK(c, sk::launch_pfl_apply(c->st, d, c->pfl_rec.as<uint64_t>(), c->pfl_C.as<uint32_t>(), nslab, c->arena,
                                    d_changed, c->pfl_ovf.as<uint32_t>(), c->pfl_bk.as<uint64_t>(),
                                    c->pfl_bv.as<uint32_t>(), c->pfl_zero ? 32 : 0,
-                                   c->pfl_plan ? c->pfl_order.as<uint32_t>() : nullptr)); }
+                                   c->pfl_plan ? c->pfl_order.as<uint32_t>() : nullptr, c->pfl_rc.as<uint32_t>(),
+                                   par)); }
     if (getenv("SK_PFL_DEBUG")) { // dev: table entries the oversized runs took (2 per record of a min-seq table run)
         uint32_t big = 0;
         HIPCHK(c, hipMemcpyAsync(&big, c->pfl_ovf.p, 4, hipMemcpyDeviceToHost, c->st));
         HIPCHK(c, hipStreamSynchronize(c->st));
-        fprintf(stderr, "[pfl] n=%llu sh=%u nsub=%u ntile=%u big-table records=%u\n", (unsigned long long)n, d.sh,
-                d.nsub, d.ntile, big / 2);
+        fprintf(stderr, "[pfl] n=%llu sh=%u nsub=%u ntile=%u tb=%u rcap=%u big-table records=%u\n",
+                (unsigned long long)n, d.sh, d.nsub, d.ntile, d.tb, d.rcap, big / 2);
     }
     return SK_OK;
 }
@@ -1231,7 +1246,7 @@ int sk_close(sk_ctx *c) {
                     &c->in_ids, &c->in_cmd, &c->out_u8, &c->misc, &c->partial, &c->hist, &c->uni, &c->ptrs,
                     &c->hist_a, &c->hist_b, &c->ovf, &c->bloom_h, &c->rc_S, &c->rc_rec, &c->long_h,
                     &c->long_which, &c->long_plane, &c->long_flags, &c->ra_S, &c->ra_rec, &c->ra_flag, &c->ev, &c->ev_n,
-                    &c->pfl_chunks, &c->pfl_S, &c->pfl_C, &c->pfl_sums, &c->pfl_rec, &c->pfl_bk, &c->pfl_bv,
+                    &c->pfl_chunks, &c->pfl_S, &c->pfl_C, &c->pfl_rc, &c->pfl_rec, &c->pfl_bk, &c->pfl_bv,
                     &c->pfl_ovf, &c->pfl_order})
         b->release();
     for (auto &ps : c->pfs) {
@@ -1655,7 +1670,7 @@ int sk_pfadd_dev(sk_ctx *c, uint64_t n, const uint32_t *d_ids, const uint64_t *d
     }
     for (uint64_t s = 0; s < n; s += max_cmds) {
         uint64_t m = std::min(max_cmds, n - s);
-        uint64_t live = c->hll_next - c->hll_free.size(); // slabs in use bounds the touched sketches
+        uint64_t live = c->hll_next - c->hll_free.size() - c->hll_retired; // slabs in use bounds the touched sketches
         if (pfadd_uses_sort(c, m, live))
             HIPCHK(c, hipMemsetAsync(d_changed + s, 0, m, c->st)); // the sorted path sets only the 1s
         Prof p_(c, 20); // the whole PFADD chain of this batch
@@ -2722,7 +2737,7 @@ int sk_timer_elapsed(sk_ctx *c, int a, int b, float *ms) {
 int sk_hll_exact_strings(sk_ctx *c, int on) {
     std::lock_guard<std::mutex> g(c->mu);
     const bool want = on != 0;
-    if (want != c->hll_exact && c->hll_next - c->hll_free.size() != 0)
+    if (want != c->hll_exact && c->hll_next - c->hll_free.size() - c->hll_retired != 0)
         return fail(c, SK_EINVAL, "HLL string mode can change only while no HLL key exists");
     c->hll_exact = want;
     if (want) c->pfadd_path = 1; // the partition path logs the register rises

@@ -150,6 +150,32 @@ def test_wrongtype_fails_only_its_batch():
         np.testing.assert_array_equal(geng.ref.regs[k], weng.ref.regs[k])
 
 
+def test_group_error_fails_group_and_thread_survives():
+    """An exception inside the group's engine call (packing / encoding) fails every future of the group; the
+    completion thread keeps serving later batches."""
+
+    class Exploding(OracleHLLEngine):
+        def pfadd_status(self, keys, elems):
+            if any(k == "boom" for k in keys):
+                raise TypeError("cannot encode element")
+            return super().pfadd_status(keys, elems)
+
+    cl = FakeClient(Exploding())
+    try:
+        b1 = cl.createBatch()
+        _fill(b1, 1, 20, 3)
+        f_cmd = b1.getHyperLogLog("boom").addAsync(5)
+        f1 = b1.executeAsync()
+        with pytest.raises(TypeError):
+            f1.get(30)
+        assert f_cmd.isDone() and not f_cmd.isSuccess()
+        b2 = cl.createBatch()
+        _fill(b2, 2, 20, 3)
+        assert len(b2.executeAsync().get(30)) == 20
+    finally:
+        cl.close()
+
+
 def test_concurrent_threads_each_get_sequential_replies():
     """Threads execute batches concurrently; the coalescer linearizes them in FIFO order: replaying the batches in
     that order (the order the coalescer completed them in is not observable, so each batch is checked on its own

@@ -196,3 +196,24 @@ def test_lines_host_buffer_batches(leng, O):
     assert got2 == ref.pfadd([names[k] for k in kid[n:]], [[e] for e in els[n:]])
     for nm in names:
         np.testing.assert_array_equal(leng.hll_registers(nm), ref.regs[nm])
+
+
+def test_lines_reply_default_flips(leng, O):
+    """The apply stores only replies that differ from the call's default (the previous call's majority reply):
+    fresh elements (mostly 1s), the same elements again (all 0s), fresh again -- each call's replies equal the
+    oracle's whichever default it ran with."""
+    nkeys, n = 64, 400_000
+    names = [b"ln:d:%d" % i for i in range(nkeys)]
+    rng = np.random.default_rng(9)
+    regs = np.zeros((nkeys, 16384), dtype=np.uint8)
+    off, buf = gen_jackson_longs(0x5EED1009, n)
+    kid = rng.integers(0, nkeys, n).astype(np.uint32)
+    leng.hll_resolve(names)
+    for seed, (o, b, k) in enumerate([(off, buf, kid), (off, buf, kid),
+                                      (*gen_jackson_longs(0x5EED100A, n), kid[::-1].copy())]):
+        got = _run(leng, O, names, k, o, b)
+        regs, want = _oracle_from(O, regs, k, o, b, nkeys)
+        assert np.array_equal(got, want), "call %d" % seed
+        if seed == 1:
+            assert not want.any()
+    _check_regs(leng, names, regs)

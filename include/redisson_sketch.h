@@ -167,6 +167,13 @@ int sk_hll_union_dev(sk_ctx *ctx, uint64_t n, const uint32_t *d_key_ids, uint8_t
  * (replaces, per shard, the name resolution of M:RedissonHyperLogLog.java:86-97) */
 int sk_hll_union_keys(sk_ctx *ctx, uint32_t n, const uint64_t *key_off, const uint8_t *key_bytes, int32_t n_gpus,
                       int32_t rank, uint8_t *d_out, uint32_t *n_used);
+/* PFCOUNT of 16384 raw registers in device memory (multi-key PFCOUNT semantics: the union's estimate); the
+ * last step of the cross-GPU countWith after the MAX all-reduce (M:RedissonHyperLogLog.java:83-89) */
+int sk_hll_count_registers_dev(sk_ctx *ctx, const uint8_t *d_regs, int64_t *out_count);
+/* HLL keyspace epoch: changes whenever an HLL key is created or removed.  A caller that caches the slab ids
+ * of a key set on the device (the cross-GPU countWith of cluster.py through sk_hll_union_dev) re-resolves
+ * the set when the epoch moved: the ids then still name exactly the set's existing HLLs. */
+int sk_hll_epoch(sk_ctx *ctx, uint64_t *out_epoch);
 /* write 16384 unpacked registers (device pointer) into a key as max (PFMERGE of a raw array) */
 int sk_hll_merge_registers_dev(sk_ctx *ctx, const uint8_t *key, uint64_t len, const uint8_t *d_regs);
 /* parity readback: 16384 unpacked registers of an HLL key (zeros if missing) */

@@ -71,6 +71,8 @@ SIGNATURES = {
     "sk_hll_histogram_dev": (c_int, [P, c_uint64, _u32p, _u32p]),
     "sk_pfmerge": (c_int, [P, _u8p, c_uint64, c_uint32, _u64p, _u8p]),
     "sk_hll_union_dev": (c_int, [P, c_uint64, _u32p, _u8p]),
+    "sk_hll_epoch": (c_int, [P, P]),
+    "sk_hll_count_registers_dev": (c_int, [P, _u8p, _i64p]),
     "sk_hll_union_keys": (c_int, [P, c_uint32, _u64p, _u8p, c_int32, c_int32, _u8p, _u32p]),
     "sk_hll_merge_registers_dev": (c_int, [P, _u8p, c_uint64, _u8p]),
     "sk_hll_registers": (c_int, [P, _u8p, c_uint64, _u8p]),

@@ -142,40 +142,84 @@ class RcclCollective:
         return [flat[r * P:r * P + sizes[r]].tobytes() for r in range(self.world)]
 
 
-def global_union_registers(engine, keys, rank: int, world: int, coll: RcclCollective):
-    """Union (register max) of every key in `keys` (a sequence, or an engine.pack() result), wherever it lives;
-    result left in coll.buf on every rank.  Missing keys count as empty (PFCOUNT rule).  Local step: one
-    sk_hll_union_keys (owner filter + directory lookup on host threads, k_hll_union on the device); exchange:
-    RCCL u8 MAX all-reduce."""
-    engine.hll_union_keys(keys, world, rank, coll.buf)
-    coll.max_u8_dev(coll.buf)
-    return coll.buf
+class GlobalKeySet:
+    """The key set of a repeated global countWith / PFMERGE (C4), resolved once per rank: the slab ids of the
+    existing HLLs among `keys` that this rank owns (calcSlot % world), kept on the device.  Each union then streams
+    those slabs (sk_hll_union_dev) with no name resolution.  The set is resolved again when the engine's HLL
+    keyspace epoch moved (a key created or removed since), so it always names exactly the keys' existing HLLs:
+    missing keys count as empty and a key created later is included (PFCOUNT rule, M:RedissonHyperLogLog.java:
+    84-89)."""
+
+    def __init__(self, engine, keys, rank: int, world: int):
+        from .engine import pack
+
+        self.engine, self.rank, self.world = engine, rank, world
+        self.packed = keys if isinstance(keys, tuple) else pack([bytes(k) for k in keys])
+        self.n_keys = len(self.packed[0]) - 1
+        self.d_ids = None
+        self.epoch = None
+        self.n = 0
+        self.resolves = 0
+
+    def ids(self):
+        """(device slab ids, how many): the owned existing HLLs, re-resolved if the keyspace changed."""
+        ep = self.engine.hll_epoch()
+        if ep != self.epoch:
+            own = owners(self.packed, self.world) == self.rank
+            h = self.engine.hll_lookup(self.packed)
+            mine = np.ascontiguousarray(h[own & (h != 0xFFFFFFFF)], dtype=np.uint32)
+            if self.d_ids is not None:
+                self.d_ids.free()
+            self.d_ids = self.engine.to_device(mine) if len(mine) else None
+            self.n, self.epoch = len(mine), ep
+            self.resolves += 1
+        return self.d_ids, self.n
 
 
-def global_count_with(engine, keys: Sequence, rank: int, world: int, coll: RcclCollective,
-                      tmp_key: bytes = b"__sk_global_union__") -> int:
-    """countWith over GPU-sharded keys: exact PFCOUNT of the union (raw order)."""
-    d = global_union_registers(engine, keys, rank, world, coll)
-    engine.hll_merge_registers_dev(tmp_key, d)
-    try:
-        return engine.pfcount([[tmp_key, b"__sk_missing__"]])[0]   # multi-key PFCOUNT = raw-register union
-    finally:
-        engine.delete([tmp_key])
+def _union_buf(engine, coll):
+    """The 16 KiB device array a rank's union lands in (the RCCL collective's own buffer, else one per engine)."""
+    if hasattr(coll, "buf"):
+        return coll.buf
+    b = getattr(engine, "_sk_union_buf", None)
+    if b is None:
+        b = engine.alloc(HLL_REGISTERS)
+        engine._sk_union_buf = b
+    return b
 
 
-def global_merge(engine, dest, keys: Sequence, rank: int, world: int, coll: RcclCollective) -> None:
-    """PFMERGE dest keys... across GPUs: dest (on its owner) = max(dest, union)."""
-    if isinstance(keys, tuple):   # packed: append dest
-        off, buf = keys
-        n_, tot = len(off) - 1, int(off[-1])
-        off = np.concatenate([off, [tot + len(dest)]]).astype(np.uint64)
-        buf = np.concatenate([buf[:tot], np.frombuffer(bytes(dest), np.uint8), np.zeros(16, np.uint8)])
-        keys = (off, buf)
+def global_union_registers(engine, keys, rank: int, world: int, coll):
+    """Union (register max) of every key in `keys` -- a sequence, an engine.pack() result, or a GlobalKeySet --
+    wherever it lives; the result is left in a 16 KiB device array on every rank (returned).  Missing keys count
+    as empty (PFCOUNT rule).  Local step: a GlobalKeySet streams its cached device slab ids (sk_hll_union_dev);
+    names go through sk_hll_union_keys (owner filter + directory lookup on host threads, then k_hll_union).
+    Exchange: RCCL u8 MAX all-reduce on the device, or (HostCollective, gloo) the 16 KiB array through the host."""
+    out = _union_buf(engine, coll)
+    if isinstance(keys, GlobalKeySet):
+        d_ids, n = keys.ids()
+        if n:
+            engine.hll_union_dev(n, d_ids, out)
+        else:
+            out.zero()
     else:
-        keys = list(keys) + [dest]
+        engine.hll_union_keys(keys, world, rank, out)
+    if hasattr(coll, "max_u8_dev"):
+        coll.max_u8_dev(out)
+    else:
+        out.upload(coll.max_u8(out.download(np.uint8, HLL_REGISTERS)))
+    return out
+
+
+def global_count_with(engine, keys, rank: int, world: int, coll) -> int:
+    """countWith over GPU-sharded keys: exact PFCOUNT of the union (multi-key PFCOUNT: raw-register order), from
+    the all-reduced registers on the device -- no key is created or modified."""
+    return engine.hll_count_registers_dev(global_union_registers(engine, keys, rank, world, coll))
+
+
+def global_merge(engine, dest, keys, rank: int, world: int, coll) -> None:
+    """PFMERGE dest keys... across GPUs: dest (on its owner) = max(dest, union of keys)."""
     d = global_union_registers(engine, keys, rank, world, coll)
     if owner(dest, world) == rank:
-        engine.hll_merge_registers_dev(dest, d)
+        engine.hll_merge_registers_dev(dest, d)   # the max includes dest's own registers (pfmergeCommand)
 
 
 def host_global_count_with(local_regs: Dict, keys: Sequence, rank: int, world: int, coll: HostCollective,

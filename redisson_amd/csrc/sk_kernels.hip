@@ -1249,16 +1249,24 @@ __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const uint64_t *__res
     if (cnt == 0) return; // uniform
     if (hmax && blockIdx.x >= hmax && cnt > SK_PFL_CAP) return; // applied by a heavy slot
     if (threadIdx.x < ntile) rp[threadIdx.x] = ex;
-    // record u of the fine bucket (u < cnt): run t with rp[t] <= u < rp[t + 1]
+    if (probe & 256) return; // dev ablation: run table only
+    // record u of the fine bucket (u < cnt): run t with rp[t] <= u < rp[t + 1].  A one-chunk bucket reads t from
+    // run_of[u] (filled below, one LDS read per record); chunked buckets search rp (fixed steps, no branches)
+    static_assert(SK_PFL_NTMAX <= 64 && SK_PFL_NTMAX <= 256, "run_of holds u8 run numbers; 6 search steps");
+    __shared__ uint8_t run_of[SK_PFL_CAP];
     auto rec_at = [&](uint32_t u) -> uint64_t {
-        uint32_t lo = 0, hi = ntile;
-        while (hi - lo > 1) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (rp[mid] <= u) lo = mid;
-            else hi = mid;
-        }
+        uint32_t lo = 0;
+#pragma unroll
+        for (uint32_t step = 32; step; step >>= 1)
+            if (lo + step < ntile && rp[lo + step] <= u) lo += step;
         return rec2[rs[lo] + (u - rp[lo])];
     };
+    auto rec_one = [&](uint32_t u) -> uint64_t {
+        const uint32_t t = run_of[u];
+        return rec2[rs[t] + (u - rp[t])];
+    };
+    if (cnt <= SK_PFL_CAP && threadIdx.x < ntile)
+        for (uint32_t u = ex; u < ex + len; u++) run_of[u] = uint8_t(threadIdx.x);
     const uint32_t dflt = (probe & 32) ? pfl_dflt(rc, par) : 2u; // 2: no default, every reply stored
     const bool sample = (probe & 32) && (blockIdx.x & 15u) == 0;
     uint32_t nrep = 0; // replies made by this thread (sampled workgroups)
@@ -1295,7 +1303,7 @@ __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const uint64_t *__res
 #pragma unroll
         for (int q = 0; q < RU; q++) {
             const uint32_t u = q * SK_PFL_ATPB + threadIdx.x;
-            if (u < cnt) rv[q] = rec_at(u);
+            if (u < cnt) rv[q] = rec_one(u);
         }
 #pragma unroll
         for (int q = 0; q < RU; q++) {
@@ -1303,6 +1311,7 @@ __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const uint64_t *__res
             if (u < cnt) R[u] = rv[q];
         }
         __syncthreads();
+        if (probe & 128) return; // dev ablation: run table, lines and records loaded, nothing applied
         pfl_chunk(R, cnt, nxt, head, fin, reg, dirty, [&] {
 #pragma unroll
             for (int j = 0; j < LQ; j++) {

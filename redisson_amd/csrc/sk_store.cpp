@@ -209,7 +209,8 @@ struct sk_ctx {
     uint8_t *arena = nullptr;
     uint64_t hll_cap = 0, hll_next = 0;
     std::vector<uint32_t> hll_free;
-    uint64_t hll_retired = 0;      // slabs whose generation wrapped: never handed out again (stale handles stay stale)
+    uint64_t hll_retired = 0;
+    uint64_t hll_epoch = 0;        // bumped whenever an HLL key is created or removed (sk_hll_epoch: cached id sets)      // slabs whose generation wrapped: never handed out again (stale handles stay stale)
     std::vector<uint8_t> hll_live; // slab id -> 1 while a key owns it (caller-cached ids are checked against it)
     std::vector<uint8_t> hll_gen;  // slab id -> generation, bumped when the slab is freed (top byte of a handle)
     std::vector<uint64_t> h_e0, h_off; // host PFADD staging, kept across calls (no page faults per batch)
@@ -595,6 +596,7 @@ int hll_alloc(sk_ctx *c, uint32_t *id) {
         c->hll_gen.resize(n, 0);
     }
     c->hll_live[*id] = 1;
+    c->hll_epoch++;
     if (c->hll_exact) {
         if (c->hstr.size() <= *id) c->hstr.resize(std::max<size_t>(*id + 1, c->hstr.size() * 2));
         hll_str_init(c->hstr[*id]);
@@ -816,6 +818,7 @@ int del_key(sk_ctx *c, const std::string &k, bool *removed) {
     if (e.type == SK_TYPE_HLL) {
         HIPCHK(c, hipMemsetAsync(c->arena + uint64_t(e.id) * kHllBytes, 0, kHllBytes, c->st));
         c->hll_live[e.id] = 0;
+        c->hll_epoch++;
         c->hll_gen[e.id] = uint8_t(c->hll_gen[e.id] + 1);
         // a generation that wrapped would make a handle cached 256 frees ago live again: retire the slab instead
         if (c->hll_gen[e.id] == 0) c->hll_retired++;
@@ -1364,6 +1367,13 @@ int sk_del(sk_ctx *c, uint32_t n, const uint64_t *off, const uint8_t *bytes, uin
 
 // FLUSHALL / FLUSHDB: every key (HLL slabs re-zeroed and reused, strings
 // freed) and every Bloom config
+int sk_hll_epoch(sk_ctx *c, uint64_t *out) {
+    std::lock_guard<std::mutex> g(c->mu);
+    ENTER(c);
+    *out = c->hll_epoch;
+    return SK_OK;
+}
+
 int sk_flushall(sk_ctx *c) {
     std::lock_guard<std::mutex> g(c->mu);
     ENTER(c);
@@ -1824,6 +1834,19 @@ int sk_pfcount(sk_ctx *c, uint32_t n_cmds, const uint32_t *nkeys, const uint64_t
         if (rc) return rc;
     }
     return status;
+}
+
+// PFCOUNT of a raw register array in device memory, multi-key semantics (hllCount over the temporary raw
+// registers of pfcountCommand): the last step of a cross-GPU countWith after the MAX all-reduce, with no key
+int sk_hll_count_registers_dev(sk_ctx *c, const uint8_t *d_regs, int64_t *out) {
+    std::lock_guard<std::mutex> g(c->mu);
+    ENTER(c);
+    std::vector<uint32_t> h;
+    int r = hll_histograms(c, 1, c->d_zero, d_regs, h);
+    if (r) return r;
+    int rc;
+    *out = int64_t(estimate_host(c, h.data(), d_regs, true, &rc));
+    return rc;
 }
 
 int sk_hll_union_dev(sk_ctx *c, uint64_t n, const uint32_t *d_ids, uint8_t *d_out) {

@@ -243,11 +243,10 @@ class SketchEngine:
         return out.value
 
     def hll_lookup(self, keys: Sequence) -> np.ndarray:
-        """Handles of existing HLL keys (0xFFFFFFFF: missing), creating nothing."""
-        ks = [_b(k) for k in keys]
-        off, buf = pack(ks)
-        ids = np.zeros(len(ks), dtype=np.uint32)
-        self._check(self.lib.sk_hll_lookup(self.ctx, len(ks), _addr(off), _addr(buf), _addr(ids)))
+        """Handles of existing HLL keys (0xFFFFFFFF: missing), creating nothing; keys: a sequence or a pack()."""
+        off, buf = keys if isinstance(keys, tuple) else pack([_b(k) for k in keys])
+        ids = np.zeros(len(off) - 1, dtype=np.uint32)
+        self._check(self.lib.sk_hll_lookup(self.ctx, len(ids), _addr(off), _addr(buf), _addr(ids)))
         return ids
 
     def hll_resolve(self, keys: Sequence) -> np.ndarray:
@@ -325,6 +324,18 @@ class SketchEngine:
         self._check(self.lib.sk_hll_union_keys(self.ctx, n, _addr(off), _addr(buf), n_gpus, rank, _addr(d_out),
                                                ctypes.addressof(used)))
         return int(used.value)
+
+    def hll_count_registers_dev(self, d_regs) -> int:
+        """PFCOUNT (multi-key / raw semantics) of 16384 registers in device memory."""
+        v = ctypes.c_int64()
+        self._check(self.lib.sk_hll_count_registers_dev(self.ctx, _addr(d_regs), ctypes.addressof(v)))
+        return int(v.value)
+
+    def hll_epoch(self) -> int:
+        """HLL keyspace epoch: moves whenever an HLL key is created or removed (sk_hll_epoch)."""
+        v = ctypes.c_uint64()
+        self._check(self.lib.sk_hll_epoch(self.ctx, ctypes.addressof(v)))
+        return int(v.value)
 
     def hll_union_dev(self, n: int, d_ids, d_out):
         self._check(self.lib.sk_hll_union_dev(self.ctx, n, _addr(d_ids), _addr(d_out)))
@@ -495,10 +506,10 @@ def owner(key, n_gpus: int) -> int:
 
 
 def owners(keys: Sequence, n_gpus: int) -> np.ndarray:
-    """owner() of many keys in one call (int32; -1 where calcSlot throws)."""
-    off, buf = pack([_b(k) for k in keys])
-    out = np.zeros(len(keys), dtype=np.int32)
-    N.load().sk_owner_many(len(keys), _addr(off), _addr(buf), n_gpus, _addr(out))
+    """owner() of many keys in one call (int32; -1 where calcSlot throws); keys: a sequence or a pack()."""
+    off, buf = keys if isinstance(keys, tuple) else pack([_b(k) for k in keys])
+    out = np.zeros(len(off) - 1, dtype=np.int32)
+    N.load().sk_owner_many(len(out), _addr(off), _addr(buf), n_gpus, _addr(out))
     return out
 
 

@@ -15,6 +15,14 @@ def _offsets(seed, n):
     return np.random.default_rng(seed).integers(0, NBITS, n, dtype=np.uint64)
 
 
+HKEYS = [b"hk:%d" % i for i in range(24)]
+HN = [37 * i + 5 for i in range(24)]
+
+
+def _hll_elems(i):
+    return [b'["java.lang.Long",%d]' % (i * 100_003 + j) for j in range(HN[i])]
+
+
 def run_scenario(engine, rank, world, coll):
     from redisson_amd.cluster import ShardedBitSet, keyed_bitop
     from redisson_amd import owner
@@ -61,6 +69,30 @@ def run_scenario(engine, rank, world, coll):
         val = engine.get(dest) if owner(dest, world) == rank else None
         res[op] = (n, val)
     out["keyed"] = res
+
+    # C4: HLLs sharded by calcSlot % world, each rank adding only the keys it owns; global countWith / PFMERGE by
+    # local union + u8 MAX exchange, by key names and by a cached device slab-id set (GlobalKeySet)
+    from redisson_amd.cluster import GlobalKeySet, global_count_with, global_merge
+    for i, k in enumerate(HKEYS):
+        if owner(k, world) == rank:
+            engine.pfadd([k] * HN[i], [[e] for e in _hll_elems(i)])
+    hk = HKEYS + [b"hk:absent"]
+    out["count_with"] = global_count_with(engine, hk, rank, world, coll)
+    ks = GlobalKeySet(engine, hk, rank, world)
+    out["count_with_ids"] = [global_count_with(engine, ks, rank, world, coll) for _ in range(2)]
+    resolves = ks.resolves
+    extra = b"hk:late"                          # created after the set was resolved: the next call includes it
+    if owner(extra, world) == rank:
+        engine.pfadd([extra] * 50, [[b"late:%d" % j] for j in range(50)])
+    ks2 = GlobalKeySet(engine, hk + [extra], rank, world)
+    ks2.ids()
+    if owner(extra, world) == rank:
+        engine.pfadd([extra] * 50, [[b"late2:%d" % j] for j in range(50)])   # registers change, no new key
+    out["count_with_late"] = global_count_with(engine, ks2, rank, world, coll)
+    out["id_set_cached"] = resolves == 1 and ks2.resolves == 1
+    global_merge(engine, b"hk:dest", ks, rank, world, coll)
+    global_merge(engine, b"hk:dest", [HKEYS[0]], rank, world, coll)          # dest kept in the max
+    out["merge_dest"] = engine.hll_registers(b"hk:dest") if owner(b"hk:dest", world) == rank else None
 
     # one Bloom filter served by every rank (replicas): adds on all, contains split and gathered
     from redisson_amd.cluster import ReplicatedBloom
@@ -117,6 +149,17 @@ def expected():
         v = O.bitop(op, [keys.get(k) for k in srcs])
         res[op] = (len(v), v if v else None)
     out["keyed"] = res
+    h = O.HLLStore()
+    for i, k in enumerate(HKEYS):
+        h.pfadd([k] * HN[i], [[e] for e in _hll_elems(i)])
+    union = np.maximum.reduce([h.regs[k] for k in HKEYS])
+    out["count_with"] = O.count_regs(union, 2, 3)
+    out["count_with_ids"] = [out["count_with"]] * 2
+    h.pfadd([b"hk:late"] * 50, [[b"late:%d" % j] for j in range(50)])
+    h.pfadd([b"hk:late"] * 50, [[b"late2:%d" % j] for j in range(50)])
+    out["count_with_late"] = O.count_regs(np.maximum(union, h.regs[b"hk:late"]), 2, 3)
+    out["id_set_cached"] = True
+    out["merge_dest"] = union
     m = O.bloom_optimal_bits(20000, 0.01)
     kk = O.bloom_optimal_k(20000, m)
     b = O.BitString(16)
@@ -134,8 +177,10 @@ def check(got, want, rank, world):
     for k in ("set_a", "set_b", "clear_a", "get_a"):
         assert [int(x) for x in got[k]] == [int(x) for x in want[k]], k
     for k in ("card", "len", "size", "bytes_a", "and", "or", "xor", "not_b", "card_not_b", "bloom_add",
-              "bloom_contains"):
+              "bloom_contains", "count_with", "count_with_ids", "count_with_late", "id_set_cached"):
         assert got[k] == want[k], k
+    if owner(b"hk:dest", world) == rank:
+        np.testing.assert_array_equal(got["merge_dest"], want["merge_dest"])
     for op, (n, val) in want["keyed"].items():
         gn, gval = got["keyed"][op]
         assert gn == n, op
@@ -144,20 +189,106 @@ def check(got, want, rank, world):
             assert gval == val, op
 
 
+class HostBuf:
+    """A 'device buffer' of the oracle engine: host bytes with the DeviceBuffer methods the protocols use."""
+
+    def __init__(self, nbytes):
+        self.a = np.zeros(nbytes, dtype=np.uint8)
+
+    def upload(self, arr, offset=0):
+        b = np.ascontiguousarray(arr).view(np.uint8).ravel()
+        self.a[offset:offset + len(b)] = b
+
+    def download(self, dtype=np.uint8, count=-1, offset=0):
+        v = self.a[offset:].view(dtype)
+        return (v if count < 0 else v[:count]).copy()
+
+    def zero(self):
+        self.a[:] = 0
+
+    def free(self):
+        pass
+
+
 class OracleBitEngine:
-    """The engine methods the cluster protocols call, over oracle bit strings (CPU tests only)."""
+    """The engine methods the cluster protocols call, over oracle bit strings and HLLs (CPU tests only)."""
 
     def __init__(self):
         from oracle import oracle as O
 
         self.O = O
         self.s = {}
+        self.h = O.HLLStore()
+        self.epoch = 0
+        self.slab = {}          # HLL key -> slab id (index into self.slabs)
+        self.slabs = []
 
     def _bs(self, k):
         return self.s.setdefault(bytes(k), self.O.BitString(16))
 
     def key_type(self, k):
-        return 2 if bytes(k) in self.s else 0
+        return 2 if bytes(k) in self.s else (1 if bytes(k) in self.h.regs else 0)
+
+    # -------- HLL (SketchEngine signatures)
+    def _hll(self, k):
+        k = bytes(k)
+        if k not in self.slab:
+            self.slab[k] = len(self.slabs)
+            self.slabs.append(k)
+            self.epoch += 1
+        return k
+
+    def pfadd(self, keys, elems):
+        return self.h.pfadd([self._hll(k) for k in keys], elems)
+
+    def hll_registers(self, k):
+        return self.h.regs.get(bytes(k), np.zeros(16384, np.uint8)).copy()
+
+    def hll_epoch(self):
+        return self.epoch
+
+    def hll_lookup(self, keys):
+        if isinstance(keys, tuple):
+            off, buf = keys
+            keys = [buf[off[i]:off[i + 1]].tobytes() for i in range(len(off) - 1)]
+        return np.array([self.slab.get(bytes(k), 0xFFFFFFFF) for k in keys], dtype=np.uint32)
+
+    def alloc(self, nbytes):
+        return HostBuf(nbytes)
+
+    def to_device(self, arr):
+        b = HostBuf(np.ascontiguousarray(arr).nbytes)
+        b.upload(arr)
+        return b
+
+    def hll_union_dev(self, n, d_ids, d_out):
+        ids = d_ids.download(np.uint32, n)
+        u = np.zeros(16384, np.uint8)
+        for i in ids:
+            np.maximum(u, self.h.regs[self.slabs[int(i)]], out=u)
+        d_out.upload(u)
+
+    def hll_union_keys(self, keys, world, rank, d_out):
+        from redisson_amd import owner
+        if isinstance(keys, tuple):
+            off, buf = keys
+            keys = [buf[off[i]:off[i + 1]].tobytes() for i in range(len(off) - 1)]
+        u = np.zeros(16384, np.uint8)
+        used = 0
+        for k in keys:
+            if owner(k, world) == rank and bytes(k) in self.h.regs:
+                np.maximum(u, self.h.regs[bytes(k)], out=u)
+                used += 1
+        d_out.upload(u)
+        return used
+
+    def hll_count_registers_dev(self, d_regs):
+        return self.O.count_regs(d_regs.download(np.uint8, 16384), 2, 3)
+
+    def hll_merge_registers_dev(self, key, d_regs):
+        k = self._hll(key)
+        r = self.h.regs.setdefault(k, np.zeros(16384, np.uint8))
+        np.maximum(r, d_regs.download(np.uint8, 16384), out=r)
 
     def setbit(self, keys, offsets, values, want_old=True):
         vals = np.broadcast_to(np.asarray(values, dtype=np.uint8), (len(keys),))

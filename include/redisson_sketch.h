@@ -192,6 +192,22 @@ int sk_getbit(sk_ctx *ctx, uint32_t n, const uint64_t *key_off, const uint8_t *k
  * in-range bits are applied (a pipeline runs the other commands). */
 int sk_set_bit_range(sk_ctx *ctx, const uint8_t *key, uint64_t len, int64_t from, int64_t to, int value);
 /* single-key device-resident variants for the bulk path (C5) */
+/* SETBIT with one value per op (d_values u8[n], device); old bits in d_out_old (may be NULL) */
+int sk_setbit_values_dev(sk_ctx *ctx, const uint8_t *key, uint64_t len, uint64_t n, const uint64_t *d_offsets,
+                         const uint8_t *d_values, uint8_t *d_out_old);
+/* RBitSet range-sharded over the GPUs (C5 across GPUs; M:RedissonBitSet.java:53-81 GETBIT / SETBIT): shard s of
+ * `world` holds logical bits [s * shard_bits, (s + 1) * shard_bits).  sk_route_bits splits a device batch of logical
+ * offsets (n < 2^32) stably by shard: d_send = shard 0's ops, then shard 1's, ..., as shard-local offsets in batch
+ * order (d_send_values alongside when d_values != NULL), d_dst[i] = op i's slot, out_counts[s] = ops of shard s
+ * (host u64[world]); an offset >= world * shard_bits fails with SK_ERANGE.  sk_alltoallv exchanges the parts over
+ * the context's RCCL communicator (per-peer byte counts; displacements = their prefix sums), the owner applies its
+ * ops with sk_setbit_dev / sk_getbit_dev, the replies travel back the same way, and sk_unroute_u8 puts them in
+ * batch order: d_out[i] = d_rep[d_dst[i]]. */
+int sk_route_bits(sk_ctx *ctx, uint64_t n, const uint64_t *d_offsets, const uint8_t *d_values, uint64_t shard_bits,
+                  int32_t world, uint64_t *d_send, uint8_t *d_send_values, uint32_t *d_dst, uint64_t *out_counts);
+int sk_unroute_u8(sk_ctx *ctx, uint64_t n, const uint32_t *d_dst, const uint8_t *d_rep, uint8_t *d_out);
+int sk_alltoallv(sk_ctx *ctx, const void *d_send, const uint64_t *send_bytes, void *d_recv,
+                 const uint64_t *recv_bytes);
 int sk_setbit_dev(sk_ctx *ctx, const uint8_t *key, uint64_t len, uint64_t n, const uint64_t *d_offsets,
                   uint8_t value, uint8_t *d_out_old);
 int sk_getbit_dev(sk_ctx *ctx, const uint8_t *key, uint64_t len, uint64_t n, const uint64_t *d_offsets,

@@ -120,6 +120,10 @@ SIGNATURES = {
     "sk_allreduce_max_u8": (c_int, [P, P, c_uint64]),
     "sk_allreduce_sum_u64": (c_int, [P, P, c_uint64]),
     "sk_allgather": (c_int, [P, P, P, c_uint64]),
+    "sk_alltoallv": (c_int, [P, P, _u64p, P, _u64p]),
+    "sk_route_bits": (c_int, [P, c_uint64, _u64p, _u8p, c_uint64, c_int32, _u64p, _u8p, _u32p, _u64p]),
+    "sk_unroute_u8": (c_int, [P, c_uint64, _u32p, _u8p, _u8p]),
+    "sk_setbit_values_dev": (c_int, [P, _u8p, c_uint64, c_uint64, _u64p, _u8p, _u8p]),
 }
 
 _lib = None

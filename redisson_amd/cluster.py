@@ -81,6 +81,13 @@ class HostCollective:
         self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
         return int(t.item())
 
+    def alltoallv_bytes(self, parts: Sequence[bytes]) -> List[bytes]:
+        """parts[p] goes to rank p; returns what every rank sent to this one (gloo: through all_gather_object)."""
+        allp = [None] * self.world
+        self.dist.all_gather_object(allp, [bytes(x) for x in parts])
+        me = self.dist.get_rank()
+        return [allp[r][me] for r in range(self.world)]
+
 
 class RcclCollective:
     """RCCL over xGMI through the engine (device buffers, the context's stream)."""
@@ -97,6 +104,7 @@ class RcclCollective:
         self.u64 = engine.alloc(8)
 
         self.world = world
+        self.rank = rank
 
     def max_u8_dev(self, dbuf, n: int = HLL_REGISTERS):
         self.engine.allreduce_max_u8(dbuf, n)
@@ -115,6 +123,10 @@ class RcclCollective:
         out = d.download(np.uint8, len(a))
         d.free()
         return out
+
+    def alltoallv_dev(self, send, send_bytes, recv, recv_bytes):
+        """RCCL all-to-all with per-peer byte counts, device buffers (sk_alltoallv)."""
+        self.engine.alltoallv(send, send_bytes, recv, recv_bytes)
 
     def allgather_dev(self, send, recv, nbytes: int):
         """RCCL all-gather of nbytes per rank, device buffers (recv holds world * nbytes)."""
@@ -187,6 +199,23 @@ def _union_buf(engine, coll):
     return b
 
 
+def agree(coll, err: "Exception | None") -> None:
+    """SPMD failure agreement before a protocol's next collective: every rank learns whether any rank failed and all
+    of them raise (a failure on one rank alone would leave the others blocked in the collective).  The failing
+    rank re-raises its own error; the others raise RedisException naming the first failing rank."""
+    from .engine import RedisException
+
+    msg = b"" if err is None else ("%s: %s" % (type(err).__name__, err)).encode()[:1024]
+    msgs = coll.allgather_bytes(msg)
+    bad = [(r, m) for r, m in enumerate(msgs) if m]
+    if not bad:
+        return
+    if err is not None:
+        raise err
+    r, m = bad[0]
+    raise RedisException("rank %d failed: %s" % (r, m.decode(errors="replace")))
+
+
 def global_union_registers(engine, keys, rank: int, world: int, coll):
     """Union (register max) of every key in `keys` -- a sequence, an engine.pack() result, or a GlobalKeySet --
     wherever it lives; the result is left in a 16 KiB device array on every rank (returned).  Missing keys count
@@ -254,29 +283,139 @@ class ShardedBitSet:
         self.S = shard_bytes(nbits, world)
         self.lo = rank * self.S          # first byte of this rank's shard
 
-    def _mine(self, offsets):
-        offs = np.asarray(offsets, dtype=np.uint64)
-        byte = offs >> np.uint64(3)
-        mine = (byte >= np.uint64(self.lo)) & (byte < np.uint64(self.lo + self.S))
-        return offs, mine, offs[mine] - np.uint64(8 * self.lo)
+    def _device(self) -> bool:
+        return hasattr(self.coll, "alltoallv_dev") and hasattr(self.engine, "route_bits")
 
     def set(self, offsets, values) -> np.ndarray:
-        """SETBIT batch (RBitSet.set(i, v) in an RBatch): old bits in batch order, sequential semantics (each bit
-        lives on one rank, so per-bit order is that rank's order)."""
-        offs, mine, loc = self._mine(offsets)
-        vals = np.broadcast_to(np.asarray(values, dtype=np.uint8), offs.shape)
-        out = np.zeros(len(offs), dtype=np.uint8)
-        if mine.any():
-            out[mine] = self.engine.setbit([self.name] * int(mine.sum()), loc, vals[mine])
-        return self.coll.max_u8(out)
+        """SETBIT batch submitted on THIS rank (RBitSet.set(i, v) in an RBatch; M:RedissonBitSet.java:79-81): the old
+        bits in batch order.  SPMD: every rank calls it, each with its own batch (possibly empty).  Ops travel to
+        their shard's owner, which applies them in (submitting rank, batch position) order -- the same result as
+        the ranks' batches executed one after another on one redis-server -- and the replies come back; no rank
+        sees another shard's ops."""
+        offs = np.ascontiguousarray(offsets, dtype=np.uint64)
+        vals = np.ascontiguousarray(np.broadcast_to(np.asarray(values, dtype=np.uint8), offs.shape))
+        return self._routed("set", offs, vals)
 
     def get(self, offsets) -> np.ndarray:
-        """GETBIT batch (RBitSet.get(i))."""
-        offs, mine, loc = self._mine(offsets)
+        """GETBIT batch submitted on this rank (RBitSet.get(i), M:RedissonBitSet.java:53-56), routed as set()."""
+        return self._routed("get", np.ascontiguousarray(offsets, dtype=np.uint64), None)
+
+    def _routed(self, op, offs, vals) -> np.ndarray:
+        if self._device():
+            e = self.engine
+            n = len(offs)
+            bufs = [e.to_device(offs) if n else None, e.to_device(vals) if (n and vals is not None) else None,
+                    e.alloc(max(n, 1))]
+            try:
+                if op == "set":
+                    self.set_dev(n, bufs[0], bufs[2], d_values=bufs[1])
+                else:
+                    self.get_dev(n, bufs[0], bufs[2])
+                return bufs[2].download(np.uint8, n)
+            finally:
+                for b in bufs:
+                    if b is not None:
+                        b.free()
+        return self._routed_host(op, offs, vals)
+
+    def _routed_host(self, op, offs, vals) -> np.ndarray:
+        """The router over host arrays and a HostCollective (gloo): the same protocol as set_dev / get_dev."""
+        from .engine import RedisException
+
+        W, sb = self.world, 8 * self.S
+        sh = (offs // np.uint64(sb)).astype(np.int64) if len(offs) else np.zeros(0, np.int64)
+        err = RedisException("ERR bit offset is not an integer or out of range") if (sh >= W).any() else None
+        agree(self.coll, err)
+        order = np.argsort(sh, kind="stable")
+        cnt = np.bincount(sh, minlength=W)
+        loc = offs[order] - sh[order].astype(np.uint64) * np.uint64(sb)
+        cut = np.concatenate([[0], np.cumsum(cnt)])
+        parts = [loc[cut[p]:cut[p + 1]].tobytes() + (vals[order][cut[p]:cut[p + 1]].tobytes() if vals is not None
+                                                       else b"") for p in range(W)]
+        got = self.coll.alltoallv_bytes(parts)
+        # this rank's shard: every rank's ops in rank order, each in its batch order
+        ro, rv = [], []
+        for g in got:
+            k = len(g) // (9 if vals is not None else 8)
+            ro.append(np.frombuffer(g[:8 * k], dtype=np.uint64))
+            if vals is not None:
+                rv.append(np.frombuffer(g[8 * k:], dtype=np.uint8))
+        mo = np.concatenate(ro) if ro else np.zeros(0, np.uint64)
+        rep = np.zeros(len(mo), dtype=np.uint8)
+        err = None
+        try:
+            if len(mo):
+                if op == "set":
+                    rep = np.asarray(self.engine.setbit([self.name] * len(mo), mo, np.concatenate(rv)), dtype=np.uint8)
+                else:
+                    rep = np.asarray(self.engine.getbit([self.name] * len(mo), mo), dtype=np.uint8)
+        except Exception as e:  # noqa: BLE001 - agreed on below
+            err = e
+        agree(self.coll, err)
+        rc = np.concatenate([[0], np.cumsum([len(x) for x in ro])])
+        back = self.coll.alltoallv_bytes([rep[rc[r]:rc[r + 1]].tobytes() for r in range(W)])
+        mine = np.frombuffer(b"".join(back), dtype=np.uint8)
         out = np.zeros(len(offs), dtype=np.uint8)
-        if mine.any():
-            out[mine] = self.engine.getbit([self.name] * int(mine.sum()), loc)
-        return self.coll.max_u8(out)
+        out[order] = mine
+        return out
+
+    def set_dev(self, n: int, d_offsets, d_out, value: int = 1, d_values=None) -> None:
+        """SETBIT of a device batch submitted on this rank (RCCL collective): sk_route_bits splits it by shard on the
+        device, sk_alltoallv sends each owner its part (counts first, by an all-gather), the owner applies the ops
+        it received in (rank, position) order, the old bits travel back the same way and sk_unroute_u8 puts them in
+        batch order into d_out.  One value for every op, or one per op in d_values (u8, device).  d_out None:
+        SETBIT_VOID (RBitSet.set(i) with no reply, M:RedissonBitSet.java:79-81): nothing travels back."""
+        self._route_dev("set", n, d_offsets, d_out, value, d_values)
+
+    def get_dev(self, n: int, d_offsets, d_out) -> None:
+        """GETBIT of a device batch submitted on this rank, routed as set_dev."""
+        self._route_dev("get", n, d_offsets, d_out, 0, None)
+
+    def _route_dev(self, op, n, d_offsets, d_out, value, d_values) -> None:
+        e, W, me = self.engine, self.world, self.rank
+        send, dst = e.alloc(max(8 * n, 8)), e.alloc(max(4 * n, 4))
+        svals = e.alloc(max(n, 1)) if d_values is not None else None
+        tmp = [send, dst] + ([svals] if svals is not None else [])
+        try:
+            cnt, err = np.zeros(W, dtype=np.uint64), None
+            try:
+                cnt = e.route_bits(n, d_offsets, d_values, 8 * self.S, W, send, svals, dst)
+            except Exception as x:  # noqa: BLE001 - agreed on below
+                err = x
+            agree(self.coll, err)
+            allc = np.stack([np.frombuffer(b, dtype=np.uint64) for b in self.coll.allgather_bytes(cnt.tobytes())])
+            rcv = allc[:, me].copy()          # ops this rank owns, from each submitting rank
+            m = int(rcv.sum())
+            recv, rep = e.alloc(max(8 * m, 8)), e.alloc(max(m, 1))
+            tmp += [recv, rep]
+            self.coll.alltoallv_dev(send, cnt * 8, recv, rcv * 8)
+            rvals = None
+            if d_values is not None:
+                rvals = e.alloc(max(m, 1))
+                tmp.append(rvals)
+                self.coll.alltoallv_dev(svals, cnt, rvals, rcv)
+            err = None
+            try:
+                void = d_out is None
+                if m and op == "set" and rvals is not None:
+                    e.setbit_values_dev(self.name, m, recv, rvals, None if void else rep)
+                elif m and op == "set":
+                    e.setbit_dev(self.name, m, recv, int(value), None if void else rep)
+                elif m:
+                    e.getbit_dev(self.name, m, recv, rep)
+            except Exception as x:  # noqa: BLE001 - agreed on below
+                err = x
+            agree(self.coll, err)
+            if d_out is None:
+                return
+            back = e.alloc(max(n, 1))
+            tmp.append(back)
+            self.coll.alltoallv_dev(rep, rcv, back, cnt)
+            if n:
+                e.unroute_u8(n, dst, back, d_out)
+        finally:
+            for b in tmp:
+                b.free()
 
     def _local_len(self) -> int:
         return self.engine.strlen(self.name)

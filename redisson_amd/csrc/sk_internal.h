@@ -133,4 +133,15 @@ hipError_t gen_jackson_scan_size(uint64_t n, size_t *bytes);
 hipError_t launch_gen_jackson(hipStream_t st, uint64_t n, uint64_t seed, const uint64_t *idx, uint64_t first,
                               uint64_t *lens, void *tmp, size_t tmp_bytes, uint64_t *off, uint8_t *out);
 
+// range-sharded RBitSet routing: stable split of a batch by shard (offset / shard_bits < world <= route_max_world());
+// cnt u32[world * route_blocks(n) + 1] (the last word zero), base the same size; *bad = 1 for an offset past the
+// last shard; send u64[n] shard-local offsets grouped by shard, svals (if vals) alongside, dst u32[n] each op's slot
+uint32_t route_blocks(uint64_t n);
+uint32_t route_max_world();
+hipError_t route_scan_size(uint64_t m, size_t *bytes);
+hipError_t launch_route(hipStream_t st, uint64_t n, const uint64_t *offs, const uint8_t *vals, uint64_t shard_bits,
+                        uint32_t world, uint32_t *cnt, uint32_t *base, void *tmp, size_t tmp_bytes, uint32_t *bad,
+                        uint64_t *send, uint8_t *svals, uint32_t *dst);
+hipError_t launch_unroute(hipStream_t st, uint64_t n, const uint32_t *dst, const uint8_t *rep, uint8_t *out);
+
 } // namespace sk

@@ -919,14 +919,14 @@ __global__ void __launch_bounds__(SK_PFP_ATPB) __attribute__((amdgpu_waves_per_e
 #define SK_PFL_RPER 16     // records per region thread held in registers
 #define SK_PFL_RCAP (SK_PFL_RTPB * SK_PFL_RPER) // most records of a one-piece region
 #define SK_PFL_ATPB 256    // apply threads (five apply workgroups per CU)
-#define SK_PFL_CAP 1024    // records per apply chunk
-#define SK_PFL_HT 1024     // chain heads per chunk
+#define SK_PFL_CAP 768     // records per apply chunk (a fine bucket expects <= ~600: six apply workgroups per CU)
+#define SK_PFL_HT 256      // chain heads per chunk (LDS: six apply workgroups per CU)
 #define SK_PFL_MAXSUB 8192 // fine buckets per coarse bucket (2^20 sketches)
 #define SK_PFL_TMAX 1024   // largest run tile (hash blocks): one segment per region thread
 #define SK_PFL_NTMAX 64    // most tiles per call (the apply's run table; 5 apply workgroups per CU need <= 32 KiB of LDS)
 #define SK_PFL_LDS (160 * 1024 - 9 * 1024) // dynamic LDS of a region workgroup: records + fine-bucket counts
 __device__ __forceinline__ uint32_t pfl_ht(uint64_t key) {
-    return uint32_t((key * 0xC2B2AE3D27D4EB4Full) >> 54); // 10 bits
+    return uint32_t((key * 0xC2B2AE3D27D4EB4Full) >> 56); // 8 bits
 }
 
 // Fine buckets take sketches by a permuted slab id, p = slab * pa mod 2^pk (pa odd, a bijection): slabs are
@@ -975,7 +975,7 @@ __global__ void __launch_bounds__(SK_PFL_RTPB) k_pfl_region(const uint64_t *__re
                                                             uint32_t cap, const uint32_t *__restrict__ tot,
                                                             uint32_t *__restrict__ rbase, uint32_t *__restrict__ C2,
                                                             uint64_t *__restrict__ rec2,
-                                                            uint8_t *__restrict__ changed) {
+                                                            uint8_t *__restrict__ changed, int probe) {
     extern __shared__ uint64_t dyn64[];
     uint64_t *sorted = dyn64;
     uint32_t *hist = reinterpret_cast<uint32_t *>(dyn64 + cap);
@@ -1052,6 +1052,11 @@ __global__ void __launch_bounds__(SK_PFL_RTPB) k_pfl_region(const uint64_t *__re
             r[q] = ~0ull;
             if (x < m) {
                 uint32_t blk;
+                if (probe & 2048) { // dev ablation: no record loads (a record of block b0, timing only)
+                    r[q] = (uint64_t(x % pm.nslab) << 32) | (uint64_t(x & 16383) << 18) | (1u << 12) | (x & 4095);
+                    rk[q] = b0;
+                    continue;
+                }
                 r[q] = pfl_region_rec(chunks, segp, segs, nb, b0, x, &blk);
                 rk[q] = blk;
             }
@@ -1071,6 +1076,7 @@ __global__ void __launch_bounds__(SK_PFL_RTPB) k_pfl_region(const uint64_t *__re
         __syncthreads();
         const uint32_t kept = hist[nsub];
         uint64_t *dst = rec2 + base;
+        if (probe & 1024) return; // dev ablation: no write-out
         for (uint32_t i = tid; i < kept; i += SK_PFL_RTPB) dst[i] = sorted[i];
         return;
     }
@@ -1213,7 +1219,7 @@ __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const uint64_t *__res
                                                            uint32_t par) {
     constexpr uint32_t NL = 1u << SK_PFL_SH;
     constexpr uint32_t kWork = SK_PFL_CAP * 8 + SK_PFL_CAP * 2 + SK_PFL_HT * 4 + SK_PFL_CAP;
-    constexpr uint32_t kBigL = 1024;       // LDS slots of the big-run table
+    constexpr uint32_t kBigL = 512;        // LDS slots of the big-run table
     static_assert(kWork >= kBigL * 12, "the big-run table shares the chunk LDS");
     constexpr uint32_t LW = (1u << SK_PFL_LB) / 16; // 16-B words per line
     __shared__ uint4 regs4[NL * LW];           // line of sketch slab0 + i at reg[i << SK_PFL_LB]
@@ -1253,7 +1259,7 @@ __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const uint64_t *__res
     // record u of the fine bucket (u < cnt): run t with rp[t] <= u < rp[t + 1].  A one-chunk bucket reads t from
     // run_of[u] (filled below, one LDS read per record); chunked buckets search rp (fixed steps, no branches)
     static_assert(SK_PFL_NTMAX <= 64 && SK_PFL_NTMAX <= 256, "run_of holds u8 run numbers; 6 search steps");
-    __shared__ uint8_t run_of[SK_PFL_CAP];
+    uint8_t *run_of = fin; // the records' run numbers (u < cnt), read before the chunk's walk writes fin
     auto rec_at = [&](uint32_t u) -> uint64_t {
         uint32_t lo = 0;
 #pragma unroll
@@ -2558,6 +2564,95 @@ __global__ void __launch_bounds__(256) k_gen_write(uint64_t n, uint64_t seed, co
     p[18 + L] = ']';
 }
 
+// -------------------------------------------------------------- range-sharded RBitSet routing (C5 across GPUs)
+// A SETBIT / GETBIT batch submitted on one rank is split by owner shard (shard s holds bits [s * shard_bits,
+// (s + 1) * shard_bits) of the logical string) into ONE buffer: shard 0's ops, then shard 1's, ..., each in batch
+// order, as shard-local offsets.  Blocks of SK_RT_EPB ops; a thread takes SK_RT_PER consecutive ops, so the stable
+// rank of an op inside its block is the thread's exclusive prefix for its shard plus its running count.  The
+// replies come back in the same layout and k_unroute gathers them to batch order (each block reads one contiguous
+// segment per shard).
+#define SK_RT_TPB 256
+#define SK_RT_PER 16
+#define SK_RT_EPB (SK_RT_TPB * SK_RT_PER)
+#define SK_RT_MAXW 8
+__device__ __forceinline__ uint32_t rt_shard(uint64_t off, uint64_t shard_bits, uint32_t world) {
+    const uint64_t s = off / shard_bits;
+    return s < world ? uint32_t(s) : world; // world: out of range
+}
+// ops per (shard, block) -> cnt[s * nblk + blk]; *bad = 1 if an offset is past the last shard
+__global__ void __launch_bounds__(SK_RT_TPB) k_route_count(uint64_t n, const uint64_t *__restrict__ offs,
+                                                           uint64_t shard_bits, uint32_t world, uint32_t nblk,
+                                                           uint32_t *__restrict__ cnt, uint32_t *bad) {
+    __shared__ uint32_t h[SK_RT_MAXW + 1];
+    if (threadIdx.x <= SK_RT_MAXW) h[threadIdx.x] = 0;
+    __syncthreads();
+    const uint64_t i0 = uint64_t(blockIdx.x) * SK_RT_EPB + uint64_t(threadIdx.x) * SK_RT_PER;
+    uint32_t c[SK_RT_MAXW + 1] = {};
+#pragma unroll
+    for (int q = 0; q < SK_RT_PER; q++) {
+        const uint64_t i = i0 + q;
+        if (i < n) {
+            const uint32_t sh = rt_shard(offs[i], shard_bits, world);
+#pragma unroll
+            for (int w = 0; w <= SK_RT_MAXW; w++) c[w] += sh == uint32_t(w);
+        }
+    }
+#pragma unroll
+    for (int w = 0; w <= SK_RT_MAXW; w++)
+        if (c[w]) atomicAdd(&h[w], c[w]);
+    __syncthreads();
+    if (threadIdx.x < world) cnt[uint64_t(threadIdx.x) * nblk + blockIdx.x] = h[threadIdx.x];
+    if (threadIdx.x == 0 && h[world]) *bad = 1;
+}
+// base = exclusive scan of cnt (shard-major); send[base + rank] = shard-local offset (values alongside if given),
+// dst[i] = the op's slot in send
+__global__ void __launch_bounds__(SK_RT_TPB) k_route_scatter(uint64_t n, const uint64_t *__restrict__ offs,
+                                                             const uint8_t *__restrict__ vals, uint64_t shard_bits,
+                                                             uint32_t world, uint32_t nblk,
+                                                             const uint32_t *__restrict__ base,
+                                                             uint64_t *__restrict__ send, uint8_t *__restrict__ svals,
+                                                             uint32_t *__restrict__ dst) {
+    __shared__ uint32_t wsum[SK_RT_TPB / 64];
+    const uint64_t i0 = uint64_t(blockIdx.x) * SK_RT_EPB + uint64_t(threadIdx.x) * SK_RT_PER;
+    uint64_t o[SK_RT_PER];
+    uint32_t c[SK_RT_MAXW] = {};
+#pragma unroll
+    for (int q = 0; q < SK_RT_PER; q++) {
+        const uint64_t i = i0 + q;
+        o[q] = i < n ? offs[i] : ~0ull;
+        const uint32_t sh = i < n ? rt_shard(o[q], shard_bits, world) : world;
+#pragma unroll
+        for (int w = 0; w < SK_RT_MAXW; w++) c[w] += sh == uint32_t(w);
+    }
+    uint32_t pre[SK_RT_MAXW];
+#pragma unroll
+    for (int w = 0; w < SK_RT_MAXW; w++) {
+        uint32_t tot;
+        pre[w] = uint32_t(w) < world ? base[uint64_t(w) * nblk + blockIdx.x] + block_exscan<SK_RT_TPB>(c[w], wsum, &tot)
+                                     : 0u;
+    }
+#pragma unroll
+    for (int q = 0; q < SK_RT_PER; q++) {
+        const uint64_t i = i0 + q;
+        if (i >= n) continue;
+        const uint32_t sh = rt_shard(o[q], shard_bits, world);
+        if (sh >= world) continue;
+        uint32_t d = 0;
+#pragma unroll
+        for (int w = 0; w < SK_RT_MAXW; w++)
+            if (sh == uint32_t(w)) d = pre[w]++;
+        send[d] = o[q] - uint64_t(sh) * shard_bits;
+        if (vals) svals[d] = vals[i];
+        dst[i] = d;
+    }
+}
+// out[i] = rep[dst[i]]: replies back to batch order
+__global__ void __launch_bounds__(256) k_unroute(uint64_t n, const uint32_t *__restrict__ dst,
+                                                 const uint8_t *__restrict__ rep, uint8_t *__restrict__ out) {
+    for (uint64_t i = uint64_t(blockIdx.x) * 256 + threadIdx.x; i < n; i += uint64_t(gridDim.x) * 256)
+        out[i] = rep[dst[i]];
+}
+
 // ================================================================ launchers
 #define SK_LAUNCH_CHECK()                                                                                              \
     do {                                                                                                               \
@@ -2685,15 +2780,17 @@ hipError_t launch_pfp_reply(hipStream_t st, uint64_t n, const uint8_t *rep, cons
 PflDims pfl_dims(uint64_t n, uint32_t nslab, uint32_t tile_blocks) {
     PflDims d;
     d.nblk = pfp_blocks(n);
-    // sketches per fine bucket: a fine bucket expects n * 2^sh / (128 * nslab) records; keep it near 768 (one
-    // chunk), within the LDS lines (2^SK_PFL_SH) and the region's fine-bucket counts (SK_PFL_MAXSUB)
+    // permutation over 2^pk >= nslab ids (>= one fine bucket); a fine bucket = 2^sh consecutive permuted ids, of which
+    // nslab / 2^pk are live: it expects n * 2^sh / (128 * 2^pk) records.  Keep that <= ~600 (one chunk of
+    // SK_PFL_CAP with margin), within the LDS lines (2^SK_PFL_SH) and the region's fine-bucket counts (MAXSUB)
+    uint32_t pk0 = 0;
+    while (pk0 < 32 && (1ull << pk0) < nslab) pk0++;
     d.sh = SK_PFL_SH;
-    while (d.sh > 0 && double(n) * double(1u << d.sh) > 768.0 * SK_PFL_NB * double(nslab ? nslab : 1) &&
-           ((2 * uint64_t(nslab) + (1u << (d.sh - 1)) - 1) >> (d.sh - 1)) <= SK_PFL_MAXSUB)
+    while (d.sh > 0 && double(n) * double(1u << d.sh) > 600.0 * SK_PFL_NB * double(1ull << std::max(pk0, d.sh)) &&
+           (1ull << (std::max(pk0, d.sh - 1) - (d.sh - 1))) <= SK_PFL_MAXSUB)
         d.sh--;
-    // permutation over 2^pk >= nslab ids (>= one fine bucket); the inverse of an odd pa mod 2^32 by Newton steps
-    d.pk = d.sh;
-    while (d.pk < 32 && (1ull << d.pk) < nslab) d.pk++;
+    // the inverse of an odd pa mod 2^32 by Newton steps
+    d.pk = std::max(pk0, d.sh);
     d.pm_mask = d.pk >= 32 ? 0xffffffffu : uint32_t((1ull << d.pk) - 1);
     d.pa = 0x9E3779B1u;
     uint32_t inv = d.pa; // x <- x (2 - a x): correct bits double each step
@@ -2743,9 +2840,10 @@ hipError_t launch_pfl_part(hipStream_t st, const PflDims &d, const uint64_t *chu
         if (e != hipSuccess) return e;
         attr = true;
     }
+    static const int probe_flags = getenv("SK_PFL_PROBE") ? atoi(getenv("SK_PFL_PROBE")) : 0; // dev ablations
     hipLaunchKernelGGL(k_pfl_region, dim3(d.nreg), dim3(SK_PFL_RTPB), lds, st, chunks, S, d.nblk, d.tb, d.ntile,
                        d.nsub, d.sh, PflPerm{d.pa, d.pai, d.pm_mask, d.nslab}, d.rcap, tot, rbase, C2, rec2,
-                       changed);
+                       changed, probe_flags);
     SK_LAUNCH_CHECK();
     return hipSuccess;
 }
@@ -3060,6 +3158,41 @@ hipError_t launch_gen_jackson(hipStream_t st, uint64_t n, uint64_t seed, const u
     e = rocprim::inclusive_scan(tmp, sz, lens, off + 1, size_t(n), rocprim::plus<uint64_t>(), st);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_gen_write, dim3(grid_for(n, 256)), dim3(256), 0, st, n, seed, idx, first, off, out);
+    SK_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+
+// routing: cnt u32[world * nblk + 1] scratch, tmp rocprim scratch; base written in place of cnt
+uint32_t route_blocks(uint64_t n) { return uint32_t((n + SK_RT_EPB - 1) / SK_RT_EPB); }
+uint32_t route_max_world() { return SK_RT_MAXW; }
+hipError_t route_scan_size(uint64_t m, size_t *bytes) {
+    size_t sz = 0;
+    hipError_t e = rocprim::exclusive_scan(nullptr, sz, (const uint32_t *)nullptr, (uint32_t *)nullptr, 0u, size_t(m),
+                                           rocprim::plus<uint32_t>());
+    *bytes = sz;
+    return e;
+}
+hipError_t launch_route(hipStream_t st, uint64_t n, const uint64_t *offs, const uint8_t *vals, uint64_t shard_bits,
+                        uint32_t world, uint32_t *cnt, uint32_t *base, void *tmp, size_t tmp_bytes, uint32_t *bad,
+                        uint64_t *send, uint8_t *svals, uint32_t *dst) {
+    if (!n) return hipSuccess;
+    if (world > SK_RT_MAXW || !world) return hipErrorInvalidValue;
+    const uint32_t nblk = route_blocks(n);
+    hipLaunchKernelGGL(k_route_count, dim3(nblk), dim3(SK_RT_TPB), 0, st, n, offs, shard_bits, world, nblk, cnt, bad);
+    SK_LAUNCH_CHECK();
+    size_t sz = tmp_bytes;
+    hipError_t e = rocprim::exclusive_scan(tmp, sz, cnt, base, 0u, size_t(world) * nblk + 1, rocprim::plus<uint32_t>(),
+                                           st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_route_scatter, dim3(nblk), dim3(SK_RT_TPB), 0, st, n, offs, vals, shard_bits, world, nblk,
+                       base, send, svals, dst);
+    SK_LAUNCH_CHECK();
+    return hipSuccess;
+}
+hipError_t launch_unroute(hipStream_t st, uint64_t n, const uint32_t *dst, const uint8_t *rep, uint8_t *out) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k_unroute, dim3(grid_for(n, 256, 8192)), dim3(256), 0, st, n, dst, rep, out);
     SK_LAUNCH_CHECK();
     return hipSuccess;
 }

@@ -239,6 +239,8 @@ struct sk_ctx {
 
     // cross-GPU exchange (RCCL over xGMI)
     ncclComm_t comm = nullptr;
+    int comm_rank = 0, comm_size = 0;
+    DBuf rt_cnt;                // range-sharded RBitSet routing: per-(shard, block) counts, then their scan
 
     bool async_dev = false;     // sk_set_async: _dev calls return without a final sync
     int pfadd_path = 1;         // 0 claim/commit, 1 partition, 2 sorted (SK_PFADD_PATH); dense batches use 2
@@ -1249,7 +1251,7 @@ int sk_close(sk_ctx *c) {
                     &c->in_ids, &c->in_cmd, &c->out_u8, &c->misc, &c->partial, &c->hist, &c->uni, &c->ptrs,
                     &c->hist_a, &c->hist_b, &c->ovf, &c->bloom_h, &c->rc_S, &c->rc_rec, &c->long_h,
                     &c->long_which, &c->long_plane, &c->long_flags, &c->ra_S, &c->ra_rec, &c->ra_flag, &c->ev, &c->ev_n,
-                    &c->pfl_chunks, &c->pfl_S, &c->pfl_C, &c->pfl_rc, &c->pfl_rec, &c->pfl_bk, &c->pfl_bv,
+                    &c->pfl_chunks, &c->pfl_S, &c->pfl_C, &c->pfl_rc, &c->rt_cnt, &c->pfl_rec, &c->pfl_bk, &c->pfl_bv,
                     &c->pfl_ovf, &c->pfl_order})
         b->release();
     for (auto &ps : c->pfs) {
@@ -2124,6 +2126,85 @@ int sk_setbit_dev(sk_ctx *c, const uint8_t *key, uint64_t len, uint64_t n, const
     return sync(c);
 }
 
+// Range-sharded RBitSet routing (cluster.py ShardedBitSet.set_dev / get_dev): a device batch of logical bit offsets
+// split by owner shard (offset / shard_bits) into d_send -- shard 0's ops, then shard 1's, ..., each in batch order,
+// as shard-local offsets (d_send_values alongside when d_values is given) -- and d_dst[i] = op i's slot there.
+// out_counts[s] = ops for shard s (host).  An offset past the last shard fails the batch with SK_ERANGE.
+int sk_route_bits(sk_ctx *c, uint64_t n, const uint64_t *d_offsets, const uint8_t *d_values, uint64_t shard_bits,
+                  int32_t world, uint64_t *d_send, uint8_t *d_send_values, uint32_t *d_dst, uint64_t *out_counts) {
+    std::lock_guard<std::mutex> g(c->mu);
+    ENTER(c);
+    if (world <= 0 || uint32_t(world) > sk::route_max_world())
+        return fail(c, SK_EINVAL, "route: world %d outside 1..%u", world, sk::route_max_world());
+    if (!shard_bits) return fail(c, SK_EINVAL, "route: shard_bits is 0");
+    if (n >= (1ull << 32)) return fail(c, SK_EINVAL, "route: batch of %llu ops (< 2^32)", (unsigned long long)n);
+    for (int s = 0; s < world; s++) out_counts[s] = 0;
+    if (!n) return SK_OK;
+    const uint32_t nblk = sk::route_blocks(n);
+    const uint64_t m = uint64_t(world) * nblk + 1;
+    size_t tmp;
+    HIPCHK(c, sk::route_scan_size(m, &tmp));
+    HIPCHK(c, c->sort_tmp.ensure(std::max<size_t>(tmp, 16)));
+    HIPCHK(c, c->rt_cnt.ensure(2 * m * 4));
+    uint32_t *cnt = c->rt_cnt.as<uint32_t>(), *base = cnt + m;
+    HIPCHK(c, hipMemsetAsync(cnt + (m - 1), 0, 4, c->st));
+    HIPCHK(c, hipMemsetAsync(c->misc.p, 0, 4, c->st));
+    HIPCHK(c, sk::launch_route(c->st, n, d_offsets, d_values, shard_bits, uint32_t(world), cnt, base, c->sort_tmp.p,
+                               c->sort_tmp.cap, c->misc.as<uint32_t>(), d_send, d_send_values, d_dst));
+    std::vector<uint32_t> b(world + 1);
+    for (int s = 0; s <= world; s++)
+        HIPCHK(c, hipMemcpyAsync(&b[s], base + uint64_t(s) * nblk, 4, hipMemcpyDeviceToHost, c->st));
+    uint32_t bad = 0;
+    HIPCHK(c, hipMemcpyAsync(&bad, c->misc.p, 4, hipMemcpyDeviceToHost, c->st));
+    int r = sync(c);
+    if (r) return r;
+    if (bad) return fail(c, SK_ERANGE, "%s", kRange);
+    for (int s = 0; s < world; s++) out_counts[s] = b[s + 1] - b[s];
+    return SK_OK;
+}
+
+// replies of a routed batch back to batch order: d_out[i] = d_rep[d_dst[i]]
+int sk_unroute_u8(sk_ctx *c, uint64_t n, const uint32_t *d_dst, const uint8_t *d_rep, uint8_t *d_out) {
+    std::lock_guard<std::mutex> g(c->mu);
+    ENTER(c);
+    HIPCHK(c, sk::launch_unroute(c->st, n, d_dst, d_rep, d_out));
+    return sync(c);
+}
+
+// SETBIT of a device batch with one value per op (d_values u8[n]); replies (old bits) in d_out_old when given
+int sk_setbit_values_dev(sk_ctx *c, const uint8_t *key, uint64_t len, uint64_t n, const uint64_t *d_offsets,
+                         const uint8_t *d_values, uint8_t *d_out_old) {
+    std::lock_guard<std::mutex> g(c->mu);
+    ENTER(c);
+    if (!n) return SK_OK;
+    uint64_t mx;
+    int r = dev_max_offset(c, n, d_offsets, &mx);
+    if (r) return r;
+    if (mx >= c->max_bit_offset) return fail(c, SK_ERANGE, "%s", kRange);
+    uint32_t id;
+    if ((r = str_get(c, key_of(key, len), true, (mx >> 3) + 1, &id))) return r;
+    uint64_t need = (mx >> 3) + 1, cur;
+    if ((r = str_reserve(c, id, need))) return r;
+    if ((r = str_len(c, id, &cur))) return r;
+    if (need > cur && (r = str_set_len(c, id, need))) return r;
+    size_t tmp;
+    HIPCHK(c, sk::sort_pairs_size(n, 0, 36, &tmp));
+    HIPCHK(c, c->sort_tmp.ensure(tmp));
+    HIPCHK(c, c->keys_a.ensure(n * 8));
+    HIPCHK(c, c->keys_b.ensure(n * 8));
+    HIPCHK(c, c->vals_a.ensure(n * 4));
+    HIPCHK(c, c->vals_b.ensure(n * 4));
+    DirEnt one{c->strs[id].ptr, 0, c->strs[id].cap};
+    HIPCHK(c, c->ptrs.ensure(sizeof(DirEnt)));
+    HIPCHK(c, hipMemcpyAsync(c->ptrs.p, &one, sizeof one, hipMemcpyHostToDevice, c->st));
+    HIPCHK(c, sk::launch_setbit_keys(c->st, n, nullptr, d_offsets, c->keys_a.as<uint64_t>(), c->vals_a.as<uint32_t>()));
+    HIPCHK(c, sk::sort_pairs(c->st, c->sort_tmp.p, c->sort_tmp.cap, c->keys_a.as<uint64_t>(), c->keys_b.as<uint64_t>(),
+                             c->vals_a.as<uint32_t>(), c->vals_b.as<uint32_t>(), n, 0, 36));
+    HIPCHK(c, sk::launch_setbit_apply(c->st, n, c->keys_b.as<uint64_t>(), c->vals_b.as<uint32_t>(), d_values, 0,
+                                      c->ptrs.p, d_out_old));
+    return sync(c);
+}
+
 // RBitSet.set(from, to) / clear(from, to): the reference sends one SETBIT_VOID
 // per bit in one pipeline (M:RedissonBitSet.java:202-228).  Each SETBIT grows
 // the string (sdsgrowzero) whatever the value; an out-of-range offset fails
@@ -2889,7 +2970,35 @@ int sk_comm_init(sk_ctx *c, int nranks, int rank, const uint8_t *id128) {
     if (c->comm) NCCLCHK(c, ncclCommDestroy(c->comm));
     c->comm = nullptr;
     NCCLCHK(c, ncclCommInitRank(&c->comm, nranks, id, rank));
+    c->comm_rank = rank;
+    c->comm_size = nranks;
     return SK_OK;
+}
+// all-to-all with per-peer byte counts (send / recv displacements = prefix sums of the counts): the exchange step
+// of the range-sharded RBitSet router (cluster.py ShardedBitSet.set_dev / get_dev).  Peers in one RCCL group;
+// the rank's own part is a device copy.
+int sk_alltoallv(sk_ctx *c, const void *d_send, const uint64_t *send_bytes, void *d_recv, const uint64_t *recv_bytes) {
+    std::lock_guard<std::mutex> g(c->mu);
+    ENTER(c);
+    if (!c->comm) return fail(c, SK_EINVAL, "sk_comm_init first");
+    const int W = c->comm_size, me = c->comm_rank;
+    std::vector<uint64_t> so(W + 1, 0), ro(W + 1, 0);
+    for (int p = 0; p < W; p++) {
+        so[p + 1] = so[p] + send_bytes[p];
+        ro[p + 1] = ro[p] + recv_bytes[p];
+    }
+    if (send_bytes[me] != recv_bytes[me]) return fail(c, SK_EINVAL, "alltoallv: own send and receive sizes differ");
+    const uint8_t *sb = static_cast<const uint8_t *>(d_send);
+    uint8_t *rb = static_cast<uint8_t *>(d_recv);
+    if (send_bytes[me]) HIPCHK(c, hipMemcpyAsync(rb + ro[me], sb + so[me], send_bytes[me], hipMemcpyDeviceToDevice, c->st));
+    NCCLCHK(c, ncclGroupStart());
+    for (int p = 0; p < W; p++) {
+        if (p == me) continue;
+        if (send_bytes[p]) NCCLCHK(c, ncclSend(sb + so[p], send_bytes[p], ncclUint8, p, c->comm, c->st));
+        if (recv_bytes[p]) NCCLCHK(c, ncclRecv(rb + ro[p], recv_bytes[p], ncclUint8, p, c->comm, c->st));
+    }
+    NCCLCHK(c, ncclGroupEnd());
+    return sync(c);
 }
 // cross-GPU PFMERGE / countWith: register-wise max of 16384-byte arrays
 int sk_allreduce_max_u8(sk_ctx *c, uint8_t *d_buf, uint64_t n) {

@@ -381,6 +381,28 @@ class SketchEngine:
         k = _b(key)
         self._check(self.lib.sk_getbit_dev(self.ctx, k, len(k), n, _addr(d_offsets), _addr(d_out)))
 
+    def setbit_values_dev(self, key, n: int, d_offsets, d_values, d_out_old=None):
+        """SETBIT of a device batch with one value per op (u8); old bits in d_out_old if given."""
+        k = _b(key)
+        self._check(self.lib.sk_setbit_values_dev(self.ctx, k, len(k), n, _addr(d_offsets), _addr(d_values),
+                                                  _addr(d_out_old)))
+
+    def route_bits(self, n: int, d_offsets, d_values, shard_bits: int, world: int, d_send, d_send_values,
+                   d_dst) -> np.ndarray:
+        """Split a device batch of logical bit offsets by owner shard (sk_route_bits): ops per shard (u64)."""
+        out = np.zeros(world, dtype=np.uint64)
+        self._check(self.lib.sk_route_bits(self.ctx, n, _addr(d_offsets), _addr(d_values), int(shard_bits), world,
+                                           _addr(d_send), _addr(d_send_values), _addr(d_dst), _addr(out)))
+        return out
+
+    def unroute_u8(self, n: int, d_dst, d_rep, d_out):
+        self._check(self.lib.sk_unroute_u8(self.ctx, n, _addr(d_dst), _addr(d_rep), _addr(d_out)))
+
+    def alltoallv(self, d_send, send_bytes, d_recv, recv_bytes):
+        sb = np.ascontiguousarray(send_bytes, dtype=np.uint64)
+        rb = np.ascontiguousarray(recv_bytes, dtype=np.uint64)
+        self._check(self.lib.sk_alltoallv(self.ctx, _addr(d_send), _addr(sb), _addr(d_recv), _addr(rb)))
+
     def set_bit_range(self, key, frm: int, to: int, value: int):
         """RBitSet.set(from, to) / clear(from, to): bits [from, to) := value."""
         k = _b(key)

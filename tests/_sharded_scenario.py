@@ -33,24 +33,38 @@ def run_scenario(engine, rank, world, coll):
     c = ShardedBitSet(engine, b"sb:c", NBITS, rank, world, coll)
     oa = _offsets(1, 3000)
     oa[0] = NBITS - 1                       # the last byte of the string
-    out["set_a"] = a.set(oa, 1).tolist()     # repeats inside the batch: second SETBIT of a bit replies 1
-    out["set_b"] = b.set(_offsets(2, 2000)[:1000], 1).tolist()   # b ends early: shorter than a
-    out["clear_a"] = a.set(oa[:500], 0).tolist()
-    out["get_a"] = a.get(np.concatenate([oa[:800], _offsets(3, 800)])).tolist()
+
+    def mine(x):                            # this rank's part of a batch: rank r submits the r-th slice
+        return x[rank * len(x) // world:(rank + 1) * len(x) // world]
+
+    def gathered(rep):                      # every rank's replies, in rank order (= the whole batch's order)
+        return [int(v) for part in coll.allgather_bytes(np.asarray(rep, np.uint8).tobytes()) for v in part]
+
+    out["set_a"] = gathered(a.set(mine(oa), 1))      # repeats inside the batch: second SETBIT of a bit replies 1
+    out["set_b"] = gathered(b.set(mine(_offsets(2, 2000)[:1000]), 1))   # b ends early: shorter than a
+    vals = (np.arange(500) % 3 == 0).astype(np.uint8)   # clear most of them, set every third again
+    out["clear_a"] = gathered(a.set(mine(oa[:500]), mine(vals)))
+    out["get_a"] = gathered(a.get(mine(np.concatenate([oa[:800], _offsets(3, 800)]))))
+    try:
+        a.set(mine(np.array([NBITS + 8 * 64 * world], dtype=np.uint64)) if rank == world - 1 else [], 1)
+        out["range_err"] = False
+    except Exception as e:                  # one rank's bad offset fails the call on every rank, none blocks
+        out["range_err"] = "out of range" in str(e) or "failed" in str(e)
+    out["range_err"] = all(x == b"1" for x in coll.allgather_bytes(b"1" if out["range_err"] else b"0"))
     out["card"] = [a.cardinality(), b.cardinality(), c.cardinality()]
     out["len"] = [a.length_bytes(), b.length_bytes(), c.length_bytes()]
     out["size"] = a.size()
     out["bytes_a"] = a.to_bytes()
     a2 = ShardedBitSet(engine, b"sb:a2", NBITS, rank, world, coll)
-    a2.set(oa[500:], 1)
+    a2.set(mine(oa[500:]), 1)
     a2.op("AND", [b])
     out["and"] = a2.to_bytes()
     a3 = ShardedBitSet(engine, b"sb:a3", NBITS, rank, world, coll)
-    a3.set(oa[500:], 1)
+    a3.set(mine(oa[500:]), 1)
     a3.op("OR", [b, c])                      # c is empty (missing on every rank)
     out["or"] = a3.to_bytes()
     a4 = ShardedBitSet(engine, b"sb:a4", NBITS, rank, world, coll)
-    a4.set(_offsets(2, 2000)[:1000], 1)
+    a4.set(mine(_offsets(2, 2000)[:1000]), 1)
     a4.op("XOR", [b])                        # equal strings: an all-zero result of b's length
     out["xor"] = a4.to_bytes()
     b.op("NOT")                              # shards before b's last byte are padded, then inverted
@@ -123,7 +137,9 @@ def expected():
     out["set_a"] = setbits(b"a", oa, 1)
     ob = _offsets(2, 2000)[:1000]
     out["set_b"] = setbits(b"b", ob, 1)
-    out["clear_a"] = setbits(b"a", oa[:500], 0)
+    vals = (np.arange(500) % 3 == 0).astype(np.uint8)
+    out["clear_a"] = [bs(b"a").setbit(int(o), int(v)) for o, v in zip(oa[:500], vals)]
+    out["range_err"] = True
     out["get_a"] = [bs(b"a").getbit(int(o)) for o in np.concatenate([oa[:800], _offsets(3, 800)])]
     out["card"] = [bs(b"a").bitcount(), bs(b"b").bitcount(), 0]
     out["len"] = [len(bs(b"a").bytes()), len(bs(b"b").bytes()), 0]
@@ -174,6 +190,7 @@ def expected():
 def check(got, want, rank, world):
     from redisson_amd import owner
 
+    assert got["range_err"], "an out-of-range offset on one rank must fail the call on every rank"
     for k in ("set_a", "set_b", "clear_a", "get_a"):
         assert [int(x) for x in got[k]] == [int(x) for x in want[k]], k
     for k in ("card", "len", "size", "bytes_a", "and", "or", "xor", "not_b", "card_not_b", "bloom_add",

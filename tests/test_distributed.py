@@ -203,3 +203,36 @@ def test_rccl_single_rank_exchange(engine, O):
         parts.append(got)
         d.free()
     np.testing.assert_array_equal(np.maximum.reduce(parts), ref.regs[b"g4:dest"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [3, 8])
+def test_route_bits_device_partition(engine, world):
+    """sk_route_bits (the range-sharded RBitSet router's device step) at world 3 and 8 on one GPU: a stable split
+    by shard with shard-local offsets and values alongside, counts per shard, and sk_unroute_u8 restoring batch
+    order -- against numpy; an offset past the last shard fails with the range error."""
+    from redisson_amd.engine import RedisException
+
+    rng = np.random.default_rng(world)
+    shard_bits = 8 * 4096 * 3
+    n = 300_001
+    offs = rng.integers(0, world * shard_bits, n, dtype=np.uint64)
+    offs[:5000] = offs[0]                        # a hot bit: order inside a shard must stay batch order
+    vals = rng.integers(0, 2, n, dtype=np.uint8)
+    d = [engine.to_device(offs), engine.to_device(vals), engine.alloc(8 * n), engine.alloc(n), engine.alloc(4 * n)]
+    cnt = engine.route_bits(n, d[0], d[1], shard_bits, world, d[2], d[3], d[4])
+    sh = (offs // np.uint64(shard_bits)).astype(np.int64)
+    order = np.argsort(sh, kind="stable")
+    np.testing.assert_array_equal(cnt, np.bincount(sh, minlength=world))
+    np.testing.assert_array_equal(d[2].download(np.uint64, n), offs[order] - sh[order].astype(np.uint64) *
+                                  np.uint64(shard_bits))
+    np.testing.assert_array_equal(d[3].download(np.uint8, n), vals[order])
+    rep = engine.to_device(np.arange(n, dtype=np.uint64)[order].astype(np.uint8))   # reply j = low byte of its op
+    out = engine.alloc(n)
+    engine.unroute_u8(n, d[4], rep, out)
+    np.testing.assert_array_equal(out.download(np.uint8, n), np.arange(n, dtype=np.uint64).astype(np.uint8))
+    bad = engine.to_device(np.array([0, world * shard_bits], dtype=np.uint64))
+    with pytest.raises(RedisException):
+        engine.route_bits(2, bad, None, shard_bits, world, d[2], None, d[4])
+    for x in d + [rep, out, bad]:
+        x.free()

@@ -396,6 +396,19 @@ def host(eng, args):
     ct(0)
     t_ct = timed(eng, lambda: [ct(r) for r in range(reps)]) / reps
     h2d_bl = eoffs[0].nbytes + probe[0][1].nbytes
+    # group commit through the host ABI (what GpuBatchCoalescer sends): G RBatches of 1M one-element PFADDs as ONE
+    # sk_pfadd_ids call over cached slab ids, pageable inputs staged by the library through its pinned double buffer
+    G = 32
+    gof, gbuf = gen_jackson_longs(0x5EED0034, B * G)
+    gids = np.ascontiguousarray(eng.hll_resolve(names)[rng.integers(0, nt, B * G)], dtype=np.uint32)
+    gcounts = np.ones(B * G, dtype=np.uint32)
+    gout = np.zeros(B * G, dtype=np.uint8)
+
+    def grp():
+        eng._check(lib.sk_pfadd_ids(ctx, B * G, gids.ctypes.data, gcounts.ctypes.data, gof.ctypes.data,
+                                    gbuf.ctypes.data, gout.ctypes.data))
+    grp()
+    t_grp = timed(eng, grp, reps=2)
     # the same PFADD batch with inputs already on the device (diagnostic: device share of the host path)
     dk, do_, db, dout = (eng.to_device(kids), eng.to_device(batches[1][0]), eng.to_device(batches[1][1], pad=16),
                          eng.alloc(B))
@@ -409,6 +422,9 @@ def host(eng, args):
           "value": 2 * B / (t_pfi + t_ct), "unit": "ops/s",
           "config": {"workload": "host", "batch": B, "tenants": nt, "bloom_bits": size, "bloom_k": k},
           "pfadd_host_per_s": B / t_pf, "pfadd_ids_host_per_s": B / t_pfi,
+          "group_commit_ids_host_per_s": B * G / t_grp,
+          "group_commit": "%d RBatches of 1M PFADDs as one sk_pfadd_ids call (host buffers, cached slab ids; the "
+                          "library stages pageable inputs through two pinned buffers)" % G,
           "pfadd_ids_ms_per_batch": t_pfi * 1e3, "bloom_add_host_per_s": B / t_add, "bloom_contains_host_per_s": B / t_ct,
           "pfadd_ms_per_batch": t_pf * 1e3, "bloom_contains_ms_per_batch": t_ct * 1e3,
           "pfadd_h2d_bytes": int(h2d_pf), "pageable_h2d_GBps": raw.nbytes / t_h2d / 1e9,

@@ -105,6 +105,8 @@ uint64_t sk_hll_estimate_hist(const uint32_t *hist64, int redis_major);
 /* ---- key directory (one keyspace per context, like one redis db) ---- */
 /* type of key (SK_TYPE_*) */
 int sk_type(sk_ctx *ctx, const uint8_t *key, uint64_t len, int *out_type);
+/* types of n keys in one call (SK_TYPE_*; 3 = a Bloom filter's name) */
+int sk_type_many(sk_ctx *ctx, uint32_t n, const uint64_t *key_off, const uint8_t *key_bytes, int32_t *out_types);
 /* DEL k1..kn -> number removed (RedissonObject.delete / RBitSet.clear, M:RedissonBitSet.java:250) */
 int sk_del(sk_ctx *ctx, uint32_t n, const uint64_t *key_off, const uint8_t *key_bytes, uint64_t *out_removed);
 /* FLUSHALL: remove every key and Bloom config of the context */
@@ -170,6 +172,11 @@ int sk_hll_union_keys(sk_ctx *ctx, uint32_t n, const uint64_t *key_off, const ui
 /* PFCOUNT of 16384 raw registers in device memory (multi-key PFCOUNT semantics: the union's estimate); the
  * last step of the cross-GPU countWith after the MAX all-reduce (M:RedissonHyperLogLog.java:83-89) */
 int sk_hll_count_registers_dev(sk_ctx *ctx, const uint8_t *d_regs, int64_t *out_count);
+/* pinned host memory (hipHostMalloc) for inputs the caller fills in place -- the JNI side wraps it in a direct
+ * ByteBuffer for the group-commit coalescer -- so their H2D needs no staging copy.  Pageable inputs of >= 4 MiB
+ * are staged by the library through two pinned buffers (host threads fill one while the other is copied). */
+int sk_host_alloc(sk_ctx *ctx, uint64_t bytes, void **out_ptr);
+int sk_host_free(sk_ctx *ctx, void *ptr);
 /* HLL keyspace epoch: changes whenever an HLL key is created or removed.  A caller that caches the slab ids
  * of a key set on the device (the cross-GPU countWith of cluster.py through sk_hll_union_dev) re-resolves
  * the set when the epoch moved: the ids then still name exactly the set's existing HLLs. */

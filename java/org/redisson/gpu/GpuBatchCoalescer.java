@@ -5,9 +5,10 @@
  * The reference sends every RBatch as its own pipeline (M:command/CommandBatchService.java:184-293) and
  * redis-server applies the batches one after another.  Here GpuSketchBatchService hands a batch whose commands are
  * all PFADDs on engine-held keys to this coalescer instead of running it alone.  The context's FIFO worker runs
- * each maximal sequence of such batches queued together (up to maxCmds commands) as ONE sk_pfadd call; at >= 4 M commands (and >= 160 per HLL key held) the engine applies it with the
- * line schedule (register lines streamed
- * once per call instead of once per element).  The concatenation keeps FIFO order and PFADD replies depend only
+ * each maximal sequence of such batches queued together (up to maxCmds commands) as ONE sk_pfadd_ids call over
+ * slab handles cached per tenant (names are typed and resolved only on a cache miss, SK_ESTALE drops the cache);
+ * at >= 4 M commands (and >= 160 per HLL key held) the engine applies it with the line schedule (register lines
+ * streamed once per call instead of once per element).  The concatenation keeps FIFO order and PFADD replies depend only
  * on order, so every batch gets exactly the replies it would get run alone in that order.  A PFADD on a key of
  * another type fails that command alone inside the engine (pipeline semantics); its batch fails with the
  * engine's error and every other batch of the call completes normally.  Groups run as tasks of the context's FIFO
@@ -111,52 +112,153 @@ public final class GpuBatchCoalescer {
         SketchDispatch.worker(ctx).execute(task);
     }
 
+    /* key -> slab handle (sk_hll_resolve), touched only by the context's worker thread (groups run there); valid
+     * until the key is deleted or replaced, which the engine reports as SK_ESTALE without writing anything */
+    private final java.util.HashMap<String, Integer> ids = new java.util.HashMap<String, Integer>();
+
+    /* The group's keys without a cached handle: typed in ONE sk_type_many call, the non-string ones resolved
+     * (created) in one sk_hll_resolve call; a key holding a plain string is resolved on its own (adopted when it
+     * holds a valid HLL string), else its commands fail.  Returns key -> error text of the failing keys; created
+     * collects the keys this resolution created (their first PFADD replies 1). */
+    private java.util.Map<String, String> resolve(List<byte[]> keys, Set<String> created) {
+        java.util.LinkedHashMap<String, byte[]> miss = new java.util.LinkedHashMap<String, byte[]>();
+        for (byte[] k : keys) {
+            String s = new String(k, SketchDispatch.ISO);
+            if (!ids.containsKey(s)) {
+                miss.put(s, k);
+            }
+        }
+        java.util.Map<String, String> bad = new java.util.HashMap<String, String>();
+        if (miss.isEmpty()) {
+            return bad;
+        }
+        List<byte[]> mk = new ArrayList<byte[]>(miss.values());
+        SketchDispatch.Packed pk = new SketchDispatch.Packed(mk);
+        int[] types = new int[mk.size()];
+        check(SketchNative.typeMany(ctx, pk.off, pk.bytes, types));
+        List<byte[]> plain = new ArrayList<byte[]>();
+        List<byte[]> strings = new ArrayList<byte[]>();
+        for (int i = 0; i < types.length; i++) {
+            (types[i] == SketchNative.SK_TYPE_NONE || types[i] == SketchNative.SK_TYPE_HLL ? plain : strings)
+                    .add(mk.get(i));
+        }
+        if (!plain.isEmpty()) {
+            SketchDispatch.Packed pp = new SketchDispatch.Packed(plain);
+            int[] h = new int[plain.size()];
+            byte[] cr = new byte[plain.size()];
+            check(SketchNative.hllResolve(ctx, pp.off, pp.bytes, h, cr));
+            for (int i = 0; i < h.length; i++) {
+                String s = new String(plain.get(i), SketchDispatch.ISO);
+                ids.put(s, h[i]);
+                if (cr[i] != 0) {
+                    created.add(s);
+                }
+            }
+        }
+        for (byte[] k : strings) {
+            List<byte[]> one = new ArrayList<byte[]>();
+            one.add(k);
+            SketchDispatch.Packed p1 = new SketchDispatch.Packed(one);
+            int[] h = new int[1];
+            String s = new String(k, SketchDispatch.ISO);
+            if (SketchNative.hllResolve(ctx, p1.off, p1.bytes, h, null) == SketchNative.SK_OK) {
+                ids.put(s, h[0]);
+            } else {
+                bad.put(s, SketchNative.lastError(ctx));
+            }
+        }
+        return bad;
+    }
+
+    private void check(int st) {
+        if (st != SketchNative.SK_OK) {
+            throw new RedisException(SketchNative.lastError(ctx));
+        }
+    }
+
+    /* The group as ONE sk_pfadd_ids call over cached slab handles: no name resolution on the hot path, the
+     * library's liveness check and host threads over the ids, and pageable inputs staged through its pinned
+     * double buffer (H2D of one piece overlaps the host copy of the next).  A stale cache is dropped and the group
+     * resolved again once. */
     private void execute(List<Req> group) {
         List<byte[]> keys = new ArrayList<byte[]>();
-        List<byte[]> flat = new ArrayList<byte[]>();
-        List<Integer> counts = new ArrayList<Integer>();
         for (Req r : group) {
             keys.addAll(r.keys);
-            for (byte[][] es : r.elems) {
-                counts.add(es.length);
-                for (byte[] x : es) {
-                    flat.add(x);
-                }
-            }
         }
-        int[] cnt = new int[counts.size()];
-        for (int i = 0; i < cnt.length; i++) {
-            cnt[i] = counts.get(i);
-        }
-        SketchDispatch.Packed k = new SketchDispatch.Packed(keys);
-        SketchDispatch.Packed e = new SketchDispatch.Packed(flat);
+        int st = SketchNative.SK_OK;
+        String err = null;
         byte[] out = new byte[keys.size()];
-        int st = SketchNative.pfadd(ctx, k.off, k.bytes, cnt, e.off, e.bytes, out);
-        String err = st == SketchNative.SK_OK ? null : SketchNative.lastError(ctx);
-        // the failed commands: keys that are still not HLLs after the call (WRONGTYPE / corrupt sparse string);
-        // any other status fails every batch of the call
-        Set<String> bad = new HashSet<String>();
-        boolean all = st != SketchNative.SK_OK && st != SketchNative.SK_EWRONGTYPE && st != SketchNative.SK_ECORRUPT;
-        if (st == SketchNative.SK_EWRONGTYPE || st == SketchNative.SK_ECORRUPT) {
-            int[] t = new int[1];
-            for (byte[] key : keys) {
-                if (SketchNative.type(ctx, key, t) != SketchNative.SK_OK || t[0] != SketchNative.SK_TYPE_HLL) {
-                    bad.add(new String(key, SketchDispatch.ISO));
+        java.util.Map<String, String> bad = null;
+        Set<String> created = new HashSet<String>();
+        for (int attempt = 0; attempt < 2; attempt++) {
+            created.clear();
+            bad = resolve(keys, created);
+            List<Integer> okIds = new ArrayList<Integer>();
+            List<byte[]> flat = new ArrayList<byte[]>();
+            List<Integer> counts = new ArrayList<Integer>();
+            int c = 0;
+            for (Req r : group) {
+                for (int j = 0; j < r.keys.size(); j++, c++) {
+                    String s = new String(r.keys.get(j), SketchDispatch.ISO);
+                    if (bad.containsKey(s)) {
+                        continue;
+                    }
+                    okIds.add(ids.get(s));
+                    byte[][] es = r.elems.get(j);
+                    counts.add(es.length);
+                    for (byte[] x : es) {
+                        flat.add(x);
+                    }
                 }
             }
+            int[] idv = new int[okIds.size()];
+            int[] cnt = new int[okIds.size()];
+            for (int i = 0; i < idv.length; i++) {
+                idv[i] = okIds.get(i);
+                cnt[i] = counts.get(i);
+            }
+            SketchDispatch.Packed e = new SketchDispatch.Packed(flat);
+            byte[] sub = new byte[idv.length];
+            st = idv.length == 0 ? SketchNative.SK_OK : SketchNative.pfaddIds(ctx, idv, cnt, e.off, e.bytes, sub);
+            if (st == SketchNative.SK_ESTALE && attempt == 0) {
+                ids.clear();
+                continue;
+            }
+            err = st == SketchNative.SK_OK ? null : SketchNative.lastError(ctx);
+            // scatter the sub-batch's replies back; the command that created its key replies 1
+            Set<String> seen = new HashSet<String>();
+            int p = 0;
+            c = 0;
+            for (Req r : group) {
+                for (int j = 0; j < r.keys.size(); j++, c++) {
+                    String s = new String(r.keys.get(j), SketchDispatch.ISO);
+                    if (bad.containsKey(s)) {
+                        continue;
+                    }
+                    out[c] = sub[p++];
+                    if (created.contains(s) && seen.add(s)) {
+                        out[c] = 1;
+                    }
+                    seen.add(s);
+                }
+            }
+            break;
         }
+        // a device / capacity error fails every batch of the call; a key of another type fails its batches only
+        boolean all = st != SketchNative.SK_OK;
+        String badMsg = bad.isEmpty() ? null : bad.values().iterator().next();
         int p = 0;
         for (Req r : group) {
             boolean failed = all;
             boolean[] rep = new boolean[r.keys.size()];
             for (int c = 0; c < rep.length; c++, p++) {
                 rep[c] = out[p] != 0;
-                if (!failed && !bad.isEmpty() && bad.contains(new String(r.keys.get(c), SketchDispatch.ISO))) {
+                if (!failed && bad.containsKey(new String(r.keys.get(c), SketchDispatch.ISO))) {
                     failed = true;
                 }
             }
             if (failed) {
-                r.promise.tryFailure(new RedisException(err));
+                r.promise.tryFailure(new RedisException(all ? err : badMsg));
             } else {
                 r.promise.trySuccess(rep);
             }

@@ -45,6 +45,8 @@ public final class SketchNative {
     public static native int bitop(long ctx, int op, byte[] dest, long[] srcOff, byte[] srcs, long[] outLen);
     public static final int SK_TYPE_NONE = 0, SK_TYPE_HLL = 1, SK_TYPE_STRING = 2;
     public static native int type(long ctx, byte[] key, int[] outType);
+    /** sk_type_many: types of many keys in one call (outTypes[i] = SK_TYPE_*; 3 = a Bloom filter's name). */
+    public static native int typeMany(long ctx, long[] keyOff, byte[] keys, int[] outTypes);
     public static native byte[] get(long ctx, byte[] key); // null when the key does not exist
     public static native int set(long ctx, byte[] key, byte[] value);
     public static native int bitsetLength(long ctx, byte[] key, long[] out);

@@ -180,6 +180,15 @@ int main(void) {
     jintArray ty = jints(1, NULL);
     st = Java_org_redisson_gpu_SketchNative_type(env, cls, ctx, jbytes("jd:a"), ty);
     pr_i32("type_hll", st, ty);
+    {   /* typeMany: an HLL, a bit string, a missing key */
+        const char *tk[] = {"jd:a", "jd:s", "jd:none"};
+        jlongArray tko;
+        jbyteArray tkb;
+        packed(3, tk, &tko, &tkb);
+        jintArray tt = jints(3, NULL);
+        st = Java_org_redisson_gpu_SketchNative_typeMany(env, cls, ctx, tko, tkb, tt);
+        pr_i32("typeMany", st, tt);
+    }
     pr_i64("bitsetLength", Java_org_redisson_gpu_SketchNative_bitsetLength(env, cls, ctx, jbytes("jd:s"), o1), o1);
     /* Bloom: tryInit(100, 0.03) -> 729 bits, k 5 (T:RedissonBloomFilterTest.java:12-16) */
     jintArray ok = jints(1, NULL);

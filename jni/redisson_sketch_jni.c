@@ -90,6 +90,17 @@ JNIEXPORT jint JNICALL Java_org_redisson_gpu_SketchNative_hllLookup(JNIEnv *env,
     return st;
 }
 
+/* sk_type_many: the group-commit coalescer types every key it holds no cached slab id for in one call */
+JNIEXPORT jint JNICALL Java_org_redisson_gpu_SketchNative_typeMany(JNIEnv *env, jclass cls, jlong ctx, jlongArray koff,
+                                                                   jbyteArray keys, jintArray out) {
+    (void)cls;
+    jsize n = LEN(out);
+    void *ko = PIN(koff), *k = PIN(keys), *r = PIN(out);
+    jint st = sk_type_many(CTX(ctx), (uint32_t)n, (const uint64_t *)ko, (const uint8_t *)k, (int32_t *)r);
+    UNPIN(out, r, 0); UNPIN(keys, k, JNI_ABORT); UNPIN(koff, ko, JNI_ABORT);
+    return st;
+}
+
 /* sk_pfadd_ids: keys resolved once per tenant (SketchNative.hllResolve) and cached on the Java side */
 JNIEXPORT jint JNICALL Java_org_redisson_gpu_SketchNative_pfaddIds(JNIEnv *env, jclass cls, jlong ctx, jintArray ids,
                                                                    jintArray counts, jlongArray eoff,

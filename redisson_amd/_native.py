@@ -60,6 +60,7 @@ SIGNATURES = {
     "sk_bloom_optimal_k": (c_int32, [c_int64, c_int64]),
     "sk_hll_estimate_hist": (c_uint64, [_u32p, c_int]),
     "sk_type": (c_int, [P, _u8p, c_uint64, P]),
+    "sk_type_many": (c_int, [P, c_uint32, _u64p, _u8p, _i32p]),
     "sk_del": (c_int, [P, c_uint32, _u64p, _u8p, _u64p]),
     "sk_hll_resolve": (c_int, [P, c_uint32, _u64p, _u8p, _u32p, _u8p]),
     "sk_hll_lookup": (c_int, [P, c_uint32, _u64p, _u8p, _u32p]),
@@ -72,6 +73,8 @@ SIGNATURES = {
     "sk_pfmerge": (c_int, [P, _u8p, c_uint64, c_uint32, _u64p, _u8p]),
     "sk_hll_union_dev": (c_int, [P, c_uint64, _u32p, _u8p]),
     "sk_hll_epoch": (c_int, [P, P]),
+    "sk_host_alloc": (c_int, [P, c_uint64, P]),
+    "sk_host_free": (c_int, [P, P]),
     "sk_hll_count_registers_dev": (c_int, [P, _u8p, _i64p]),
     "sk_hll_union_keys": (c_int, [P, c_uint32, _u64p, _u8p, c_int32, c_int32, _u8p, _u32p]),
     "sk_hll_merge_registers_dev": (c_int, [P, _u8p, c_uint64, _u8p]),

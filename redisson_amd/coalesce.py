@@ -21,6 +21,8 @@ import contextlib
 import threading
 from typing import List, Optional, Sequence
 
+import numpy as np
+
 from .redisson import Future
 
 
@@ -180,6 +182,8 @@ class BatchCoalescer:
         self._held = 0
         self.calls = 0       # engine PFADD calls made for merged groups
         self.batches = 0     # batches completed
+        self._ids = {}       # key -> slab handle (sk_hll_resolve), valid until the key is deleted / replaced
+        self._created = set()
         self._t = threading.Thread(target=self._loop, name="sk-batch-coalescer", daemon=True)
         self._t.start()
 
@@ -241,23 +245,66 @@ class BatchCoalescer:
         except Exception as e:  # noqa: BLE001 - the batch's own error, as execute() raises it
             r.future._fail(e)
 
+    def _resolve(self, keys) -> "tuple[dict, set]":
+        """Slab handles of the group's distinct keys: from the coalescer's cache (the Java executor's per-tenant
+        cache), else typed in ONE call and resolved (created) in one call.  A key holding a plain string is
+        resolved on its own: it is adopted if it holds a valid HLL string, otherwise its commands fail (WRONGTYPE).
+        Returns ({key: handle}, {key: error text of the keys whose commands fail}) and records created keys."""
+        from . import _native as N
+        from .engine import RedisException
+
+        miss = [k for k in dict.fromkeys(keys) if k not in self._ids]
+        bad = {}
+        if miss:
+            t = self.engine.key_types(miss)
+            plain = [k for k, ty in zip(miss, t) if ty in (N.SK_TYPE_NONE, N.SK_TYPE_HLL)]
+            if plain:
+                h, cr = self.engine.hll_resolve(plain, with_created=True)
+                for k, hk, c in zip(plain, h, cr):
+                    self._ids[k] = int(hk)
+                    if c:
+                        self._created.add(k)
+            for k, ty in zip(miss, t):
+                if ty in (N.SK_TYPE_NONE, N.SK_TYPE_HLL):
+                    continue
+                try:
+                    self._ids[k] = int(self.engine.hll_resolve([k])[0])
+                except RedisException as e:
+                    bad[k] = str(e)
+        return self._ids, bad
+
     def _run_pfadd(self, group: List[_BatchReq]):
+        """The group as ONE sk_pfadd_ids call over cached slab handles (names are resolved only on a cache miss);
+        a stale cache (a key deleted or replaced since) is dropped and resolved again once."""
+        from . import _native as N
         from .engine import RedisException
 
         cmds = [c for r in group for c in r.batch._cmds]
         keys = [c[0][1] for c in cmds]
-        st, out, msg = self.engine.pfadd_status(keys, [c[0][2] for c in cmds])
+        for attempt in range(2):
+            self._created = set()
+            ids, bad_msg = self._resolve(keys)
+            ok = [i for i, k in enumerate(keys) if k not in bad_msg]
+            out = np.zeros(len(keys), dtype=np.uint8)
+            st, sub, msg = self.engine.pfadd_ids_status(np.array([ids[keys[i]] for i in ok], dtype=np.uint32),
+                                                        [cmds[i][0][2] for i in ok]) if ok else (N.SK_OK, out[:0], "")
+            if st == N.SK_ESTALE and attempt == 0:
+                self._ids.clear()
+                continue
+            break
         self.calls += 1
-        bad = set()
-        if st != 0:
-            # a command on a key of another type failed alone (the others were applied, pipeline semantics):
-            # those keys are still not HLLs after the call; any other error fails every command of the group
-            from . import _native as N
-
-            if st in (N.SK_EWRONGTYPE, N.SK_ECORRUPT):
-                bad = {k for k in set(keys) if self.engine.key_type(k) != N.SK_TYPE_HLL}
-            else:
-                bad = set(keys)
+        out[ok] = sub
+        seen = set()
+        for i in ok:                          # PFADD replies 1 on the command that created its key
+            k = keys[i]
+            if k in self._created and k not in seen:
+                out[i] = 1
+            seen.add(k)
+        bad = set(bad_msg)
+        if bad:
+            msg = next(iter(bad_msg.values()))
+        if st != N.SK_OK:                     # a device / capacity error fails every command of the group
+            bad = set(keys)
         p = 0
         for r in group:
             r.batch._executed = True

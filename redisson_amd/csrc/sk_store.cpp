@@ -241,6 +241,10 @@ struct sk_ctx {
     ncclComm_t comm = nullptr;
     int comm_rank = 0, comm_size = 0;
     DBuf rt_cnt;                // range-sharded RBitSet routing: per-(shard, block) counts, then their scan
+    // host -> device staging of caller host buffers (stage_h2d): two pinned buffers, filled by host threads in turn
+    uint8_t *stage[2] = {nullptr, nullptr};
+    hipEvent_t stage_ev[2] = {nullptr, nullptr};
+    bool stage_on = true;       // SK_STAGE=0: plain pageable copies
 
     bool async_dev = false;     // sk_set_async: _dev calls return without a final sync
     int pfadd_path = 1;         // 0 claim/commit, 1 partition, 2 sorted (SK_PFADD_PATH); dense batches use 2
@@ -581,6 +585,48 @@ void hll_str_merged(sk_ctx *c, uint32_t slab) {
     c->hstr[slab].hdr[15] |= 0x80;
 }
 
+// H2D of a caller's host range, asynchronous on c->st.  Large pageable ranges go through two pinned staging
+// buffers: host threads copy piece p into buffer p % 2 while the device copies piece p - 1 out of the other one at
+// the link's rate (a pageable hipMemcpyAsync is staged by the runtime and returns only once it has been copied).  A
+// buffer is refilled only after the event of its previous copy completed.  Pinned caller memory (a buffer the JNI
+// side allocated with sk_host_alloc) is copied directly.
+constexpr uint64_t kStagePiece = 32ull << 20;
+int stage_h2d(sk_ctx *c, void *dst, const void *src, uint64_t bytes) {
+    if (!bytes) return SK_OK;
+    hipPointerAttribute_t at;
+    const bool pinned = hipPointerGetAttributes(&at, src) == hipSuccess && at.type == hipMemoryTypeHost;
+    (void)hipGetLastError(); // pageable memory reports an error here
+    if (!c->stage_on || pinned || bytes < (4ull << 20)) {
+        HIPCHK(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->st));
+        return SK_OK;
+    }
+    for (int k = 0; k < 2; k++)
+        if (!c->stage[k]) {
+            HIPCHK(c, hipHostMalloc((void **)&c->stage[k], kStagePiece, hipHostMallocDefault));
+            HIPCHK(c, hipEventCreateWithFlags(&c->stage_ev[k], hipEventDisableTiming));
+            HIPCHK(c, hipEventRecord(c->stage_ev[k], c->st));
+        }
+    const unsigned T = std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
+    const uint8_t *s8 = static_cast<const uint8_t *>(src);
+    uint8_t *d8 = static_cast<uint8_t *>(dst);
+    for (uint64_t o = 0, p = 0; o < bytes; o += kStagePiece, p++) {
+        const int k = int(p & 1);
+        const uint64_t len = std::min(kStagePiece, bytes - o);
+        HIPCHK(c, hipEventSynchronize(c->stage_ev[k])); // the buffer's previous copy is done
+        std::vector<std::thread> th;
+        for (unsigned t = 1; t < T; t++)
+            th.emplace_back([&, t] {
+                const uint64_t a = len * t / T, b = len * (t + 1) / T;
+                std::memcpy(c->stage[k] + a, s8 + o + a, b - a);
+            });
+        std::memcpy(c->stage[k], s8 + o, len / T);
+        for (auto &x : th) x.join();
+        HIPCHK(c, hipMemcpyAsync(d8 + o, c->stage[k], len, hipMemcpyHostToDevice, c->st));
+        HIPCHK(c, hipEventRecord(c->stage_ev[k], c->st));
+    }
+    return SK_OK;
+}
+
 int hll_alloc(sk_ctx *c, uint32_t *id) {
     if (!c->hll_free.empty()) {
         *id = c->hll_free.back();
@@ -613,6 +659,28 @@ uint32_t hll_handle(const sk_ctx *c, uint32_t id) { return id | (uint32_t(c->hll
 bool hll_handle_live(const sk_ctx *c, uint32_t h) {
     uint32_t id = h & kSlabMask;
     return id < c->hll_live.size() && c->hll_live[id] && c->hll_gen[id] == (h >> 24);
+}
+// index of the first handle of ids[0..n) that is not live, or n: on host threads for large batches (the check of
+// caller-cached handles must not cost more than the batch's H2D)
+uint64_t first_dead_handle(const sk_ctx *c, uint64_t n, const uint32_t *ids) {
+    const unsigned T = n >= (1u << 18) ? std::max(1u, std::min(16u, std::thread::hardware_concurrency())) : 1u;
+    std::vector<uint64_t> bad(T, n);
+    auto work = [&](unsigned t) {
+        const uint64_t i0 = n * t / T, i1 = n * (t + 1) / T;
+        for (uint64_t i = i0; i < i1; i++)
+            if (!hll_handle_live(c, ids[i])) {
+                bad[t] = i;
+                return;
+            }
+    };
+    if (T == 1) {
+        work(0);
+    } else {
+        std::vector<std::thread> th;
+        for (unsigned t = 0; t < T; t++) th.emplace_back(work, t);
+        for (auto &x : th) x.join();
+    }
+    return *std::min_element(bad.begin(), bad.end());
 }
 
 int str_len(sk_ctx *c, uint32_t id, uint64_t *len);
@@ -1215,6 +1283,7 @@ int sk_open(const sk_config *cfg, sk_ctx **out) {
     if (const char *e = getenv("SK_PFL_TILE")) c->pfl_tile = uint32_t(strtoul(e, nullptr, 10));
     if (const char *e = getenv("SK_PFL_ZERO")) c->pfl_zero = atoi(e) != 0;
     if (const char *e = getenv("SK_PFL_PLAN")) c->pfl_plan = atoi(e) != 0;
+    if (const char *e = getenv("SK_STAGE")) c->stage_on = atoi(e) != 0;
     uint64_t cap = (cfg && cfg->hll_capacity) ? cfg->hll_capacity : 1024;
     if (hll_grow(c, cap) != SK_OK || c->misc.ensure(4096) != hipSuccess ||
         hipMalloc(&c->d_zero, 16) != hipSuccess || hipMemsetAsync(c->d_zero, 0, 16, c->st) != hipSuccess ||
@@ -1247,6 +1316,10 @@ int sk_close(sk_ctx *c) {
     if (c->d_dir) (void)hipFree(c->d_dir);
     if (c->d_zero) (void)hipFree(c->d_zero);
     if (c->h_cnt) (void)hipHostFree(c->h_cnt);
+    for (int k = 0; k < 2; k++) {
+        if (c->stage[k]) (void)hipHostFree(c->stage[k]);
+        if (c->stage_ev[k]) (void)hipEventDestroy(c->stage_ev[k]);
+    }
     for (DBuf *b : {&c->keys_a, &c->keys_b, &c->vals_a, &c->vals_b, &c->sort_tmp, &c->in_off, &c->in_bytes,
                     &c->in_ids, &c->in_cmd, &c->out_u8, &c->misc, &c->partial, &c->hist, &c->uni, &c->ptrs,
                     &c->hist_a, &c->hist_b, &c->ovf, &c->bloom_h, &c->rc_S, &c->rc_rec, &c->long_h,
@@ -1344,6 +1417,17 @@ uint64_t sk_hll_estimate_hist(const uint32_t *hist, int redis_major) {
     return estimate_v3(E, int(hist[0]));
 }
 
+// types of n keys in one call (the group-commit coalescers' check of the keys they have no cached slab id for)
+int sk_type_many(sk_ctx *c, uint32_t n, const uint64_t *off, const uint8_t *bytes, int32_t *out) {
+    std::lock_guard<std::mutex> g(c->mu);
+    for (uint32_t i = 0; i < n; i++) {
+        std::string k = key_of(bytes + off[i], off[i + 1] - off[i]);
+        auto it = c->keys.find(k);
+        out[i] = it != c->keys.end() ? int32_t(it->second.type) : (c->bloom.count(k) ? 3 : SK_TYPE_NONE);
+    }
+    return SK_OK;
+}
+
 int sk_type(sk_ctx *c, const uint8_t *key, uint64_t len, int *out) {
     std::lock_guard<std::mutex> g(c->mu);
     std::string k = key_of(key, len);
@@ -1369,6 +1453,22 @@ int sk_del(sk_ctx *c, uint32_t n, const uint64_t *off, const uint8_t *bytes, uin
 
 // FLUSHALL / FLUSHDB: every key (HLL slabs re-zeroed and reused, strings
 // freed) and every Bloom config
+// pinned host memory for callers that fill their inputs in place (the JNI side's direct ByteBuffers): H2D from it
+// runs at the link's rate with no staging copy
+int sk_host_alloc(sk_ctx *c, uint64_t bytes, void **out) {
+    std::lock_guard<std::mutex> g(c->mu);
+    ENTER(c);
+    *out = nullptr;
+    HIPCHK(c, hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault));
+    return SK_OK;
+}
+int sk_host_free(sk_ctx *c, void *p) {
+    std::lock_guard<std::mutex> g(c->mu);
+    ENTER(c);
+    if (p) HIPCHK(c, hipHostFree(p));
+    return SK_OK;
+}
+
 int sk_hll_epoch(sk_ctx *c, uint64_t *out) {
     std::lock_guard<std::mutex> g(c->mu);
     ENTER(c);
@@ -1471,16 +1571,18 @@ static int pfadd_host_batch(sk_ctx *c, uint32_t n_cmds, const uint32_t *cmd_key,
         }
         uint64_t e0 = cmd_e0(c0), b0 = elem_off[e0], b1 = elem_off[cmd_e0(c1)];
         const uint32_t *ids_src, *cmd_src = nullptr;
+        const uint64_t *off_src;
         const uint8_t *bytes_src;
-        uint64_t m, nbytes;
+        uint64_t m, nbytes, shift = 0; // simple chunks: the caller's offsets as they are, the bytes from b0 down to
+                                       // a 16-B boundary, and the device byte pointer moved back by that base
         if (!simple) off2.clear();
         if (simple) {
             m = c1 - c0;
-            if (off2.size() < m + 1) off2.resize(m + 1);
-            for (uint64_t j = 0; j <= m; j++) off2[j] = elem_off[e0 + j] - b0;
+            shift = b0 & ~uint64_t(15);
+            off_src = elem_off + e0;
             ids_src = cmd_key + c0;
-            bytes_src = elem_bytes + b0;
-            nbytes = b1 - b0;
+            bytes_src = elem_bytes + shift;
+            nbytes = b1 - shift;
         } else {
             h_ids.clear();
             h_cmd.clear();
@@ -1499,6 +1601,7 @@ static int pfadd_host_batch(sk_ctx *c, uint32_t n_cmds, const uint32_t *cmd_key,
             }
             off2.push_back(t);
             m = h_ids.size();
+            off_src = off2.data();
             ids_src = h_ids.data();
             cmd_src = h_cmd.data();
             bytes_src = bytes2.data();
@@ -1512,13 +1615,14 @@ static int pfadd_host_batch(sk_ctx *c, uint32_t n_cmds, const uint32_t *cmd_key,
             HIPCHK(c, c->in_off.ensure((m + 1) * 8));
             HIPCHK(c, c->in_bytes.ensure(nbytes + 16));
             HIPCHK(c, c->out_u8.ensure(c1 - c0));
-            HIPCHK(c, hipMemcpyAsync(c->in_ids.p, ids_src, m * 4, hipMemcpyHostToDevice, c->st));
+            int sr;
+            if ((sr = stage_h2d(c, c->in_ids.p, ids_src, m * 4))) return sr;
             if (cmd_src) {
                 HIPCHK(c, c->in_cmd.ensure(m * 4));
-                HIPCHK(c, hipMemcpyAsync(c->in_cmd.p, cmd_src, m * 4, hipMemcpyHostToDevice, c->st));
+                if ((sr = stage_h2d(c, c->in_cmd.p, cmd_src, m * 4))) return sr;
             }
-            HIPCHK(c, hipMemcpyAsync(c->in_off.p, off2.data(), (m + 1) * 8, hipMemcpyHostToDevice, c->st));
-            if (nbytes) HIPCHK(c, hipMemcpyAsync(c->in_bytes.p, bytes_src, nbytes, hipMemcpyHostToDevice, c->st));
+            if ((sr = stage_h2d(c, c->in_off.p, off_src, (m + 1) * 8))) return sr;
+            if ((sr = stage_h2d(c, c->in_bytes.p, bytes_src, nbytes))) return sr;
             HIPCHK(c, hipMemsetAsync(c->in_bytes.as<uint8_t>() + nbytes, 0, 16, c->st)); // padding contract
             HIPCHK(c, hipMemsetAsync(c->out_u8.p, 0, c1 - c0, c->st));
             uint64_t touched = 0; // distinct sketches: only the density heuristic of the non-default paths uses it
@@ -1533,10 +1637,10 @@ static int pfadd_host_batch(sk_ctx *c, uint32_t n_cmds, const uint32_t *cmd_key,
                 std::vector<uint32_t> which, first_wg{0};
                 std::vector<uint64_t> poff{0};
                 for (uint64_t j = 0; j < m; j++)
-                    if (off2[j + 1] - off2[j] >= sk::long_elem_bytes()) {
+                    if (off_src[j + 1] - off_src[j] >= sk::long_elem_bytes()) {
                         which.push_back(uint32_t(j));
-                        first_wg.push_back(first_wg.back() + sk::murmur_long_wgs(off2[j + 1] - off2[j]));
-                        poff.push_back(poff.back() + sk::murmur_long_plane_words(off2[j + 1] - off2[j]));
+                        first_wg.push_back(first_wg.back() + sk::murmur_long_wgs(off_src[j + 1] - off_src[j]));
+                        poff.push_back(poff.back() + sk::murmur_long_plane_words(off_src[j + 1] - off_src[j]));
                     }
                 if (!which.empty()) {
                     const uint32_t nl = uint32_t(which.size()), nwg = first_wg.back();
@@ -1552,7 +1656,7 @@ static int pfadd_host_batch(sk_ctx *c, uint32_t n_cmds, const uint32_t *cmd_key,
                     HIPCHK(c, hipMemcpyAsync(c->long_which.p, which.data(), which.size() * 4, hipMemcpyHostToDevice,
                                              c->st));
                     { Prof p_(c, 21);
-                    HIPCHK(c, sk::launch_murmur_long(c->st, nl, nwg, c->in_bytes.as<uint8_t>(),
+                    HIPCHK(c, sk::launch_murmur_long(c->st, nl, nwg, c->in_bytes.as<uint8_t>() - shift,
                                                      c->in_off.as<uint64_t>(), c->long_which.as<uint32_t>(),
                                                      c->long_plane.as<uint32_t>(), c->long_flags.as<uint32_t>(),
                                                      c->long_h.as<uint64_t>())); }
@@ -1564,7 +1668,7 @@ static int pfadd_host_batch(sk_ctx *c, uint32_t n_cmds, const uint32_t *cmd_key,
                     d_pre = c->long_h.as<uint64_t>();
                 }
             }
-            int r = pfadd_device(c, m, c->in_ids.as<uint32_t>(), c->in_off.as<uint64_t>(), c->in_bytes.as<uint8_t>(),
+            int r = pfadd_device(c, m, c->in_ids.as<uint32_t>(), c->in_off.as<uint64_t>(), c->in_bytes.as<uint8_t>() - shift,
                                  cmd_src ? c->in_cmd.as<uint32_t>() : nullptr, c1 - c0, c->out_u8.as<uint8_t>(),
                                  touched, d_pre);
             if (r) return r;
@@ -1647,10 +1751,10 @@ int sk_pfadd_ids(sk_ctx *c, uint32_t n_cmds, const uint32_t *key_ids, const uint
     std::lock_guard<std::mutex> g(c->mu);
     ENTER(c);
     if (!n_cmds) return SK_OK;
-    for (uint32_t i = 0; i < n_cmds; i++)
-        if (!hll_handle_live(c, key_ids[i]))
-            return fail(c, SK_ESTALE, "PFADD: slab id %u is not held by a key (deleted, replaced or never resolved)",
-                        key_ids[i]);
+    const uint64_t d = first_dead_handle(c, n_cmds, key_ids);
+    if (d < n_cmds)
+        return fail(c, SK_ESTALE, "PFADD: slab id %u is not held by a key (deleted, replaced or never resolved)",
+                    key_ids[d]);
     return pfadd_host_batch(c, n_cmds, key_ids, nullptr, elem_counts, elem_off, elem_bytes, out_changed);
 }
 
@@ -1741,10 +1845,10 @@ int sk_pfcount_ids(sk_ctx *c, uint64_t n, const uint32_t *key_ids, int64_t *out)
     std::lock_guard<std::mutex> g(c->mu);
     ENTER(c);
     if (!n) return SK_OK;
-    for (uint64_t i = 0; i < n; i++)
-        if (!hll_handle_live(c, key_ids[i]))
-            return fail(c, SK_ESTALE, "PFCOUNT: slab id %u is not held by a key (deleted, replaced or never resolved)",
-                        key_ids[i]);
+    const uint64_t d = first_dead_handle(c, n, key_ids);
+    if (d < n)
+        return fail(c, SK_ESTALE, "PFCOUNT: slab id %u is not held by a key (deleted, replaced or never resolved)",
+                    key_ids[d]);
     HIPCHK(c, c->in_ids.ensure(n * 4));
     HIPCHK(c, hipMemcpyAsync(c->in_ids.p, key_ids, n * 4, hipMemcpyHostToDevice, c->st));
     std::vector<uint32_t> h;
@@ -2672,8 +2776,9 @@ static int stage_elems(sk_ctx *c, uint32_t n, const uint64_t *off, const uint8_t
     for (uint32_t i = 0; i <= n; i++) o[i] = off[i] - off[0];
     HIPCHK(c, c->in_off.ensure((n + 1) * 8ull));
     HIPCHK(c, c->in_bytes.ensure(tot + 16));
-    HIPCHK(c, hipMemcpyAsync(c->in_off.p, o.data(), (n + 1) * 8ull, hipMemcpyHostToDevice, c->st));
-    if (tot) HIPCHK(c, hipMemcpyAsync(c->in_bytes.p, bytes + off[0], tot, hipMemcpyHostToDevice, c->st));
+    int sr;
+    if ((sr = stage_h2d(c, c->in_off.p, o.data(), (n + 1) * 8ull))) return sr;
+    if ((sr = stage_h2d(c, c->in_bytes.p, bytes + off[0], tot))) return sr;
     HIPCHK(c, hipMemsetAsync(c->in_bytes.as<uint8_t>() + tot, 0, 16, c->st));
     return sync(c); // o is a host vector
 }

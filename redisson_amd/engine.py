@@ -235,6 +235,24 @@ class SketchEngine:
         self._check(self.lib.sk_type(self.ctx, k, len(k), ctypes.addressof(t)))
         return t.value
 
+    def key_types(self, keys) -> np.ndarray:
+        """key_type of many keys in one call (int32); keys: a sequence or a pack()."""
+        off, buf = keys if isinstance(keys, tuple) else pack([_b(k) for k in keys])
+        out = np.zeros(len(off) - 1, dtype=np.int32)
+        self._check(self.lib.sk_type_many(self.ctx, len(out), _addr(off), _addr(buf), _addr(out)))
+        return out
+
+    def pfadd_ids_status(self, key_ids, elems: Sequence[Sequence[bytes]]):
+        """sk_pfadd_ids without raising: (status, replies u8[n], error text)."""
+        ids = np.ascontiguousarray(key_ids, dtype=np.uint32)
+        n = len(ids)
+        counts = np.fromiter((len(e) for e in elems), dtype=np.uint32, count=n)
+        eoff, ebuf = pack([x for e in elems for x in e])
+        out = np.zeros(n, dtype=np.uint8)
+        st = self.lib.sk_pfadd_ids(self.ctx, n, _addr(ids), _addr(counts), _addr(eoff), _addr(ebuf), _addr(out))
+        msg = (self.lib.sk_last_error(self.ctx) or b"").decode("utf-8", "replace") if st != N.SK_OK else ""
+        return st, out, msg
+
     def delete(self, keys: Iterable) -> int:
         ks = [_b(k) for k in keys]
         off, buf = pack(ks)
@@ -249,12 +267,14 @@ class SketchEngine:
         self._check(self.lib.sk_hll_lookup(self.ctx, len(ids), _addr(off), _addr(buf), _addr(ids)))
         return ids
 
-    def hll_resolve(self, keys: Sequence) -> np.ndarray:
+    def hll_resolve(self, keys: Sequence, with_created: bool = False):
+        """Slab handles of HLL keys, creating empty HLLs for missing names; with_created: (handles, created u8[])."""
         ks = [_b(k) for k in keys]
         off, buf = pack(ks)
         ids = np.zeros(len(ks), dtype=np.uint32)
-        self._check(self.lib.sk_hll_resolve(self.ctx, len(ks), _addr(off), _addr(buf), _addr(ids), None))
-        return ids
+        cr = np.zeros(len(ks), dtype=np.uint8)
+        self._check(self.lib.sk_hll_resolve(self.ctx, len(ks), _addr(off), _addr(buf), _addr(ids), _addr(cr)))
+        return (ids, cr) if with_created else ids
 
     # ------------------------------------------------------------ HLL
     def pfadd(self, keys: Sequence, elems: Sequence[Sequence[bytes]]) -> List[bool]:

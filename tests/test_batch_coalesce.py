@@ -1,7 +1,8 @@
 """Group commit of concurrently executed RBatches (redisson_amd/coalesce.py BatchCoalescer).
 
-CPU tests run the coalescer over an oracle-backed engine stand-in (pfadd / pfadd_status / pfcount / key_type with
-the engine's pipeline semantics: a PFADD on a key of another type fails that command alone).  Expected results
+CPU tests run the coalescer over an oracle-backed engine stand-in (pfadd / pfadd_status / pfcount / key_type, and the
+slab-id path the coalescer takes: key_types, hll_resolve, pfadd_ids_status; a PFADD on a key of another type fails
+that command alone).  Expected results
 come from running the same batches one after another through the oracle, in the FIFO order they were submitted:
 merged PFADD-only batches must give every batch exactly its sequential replies, a batch with another command runs
 on its own, and a WRONGTYPE command fails only the batch that holds it."""
@@ -45,6 +46,35 @@ class OracleHLLEngine:
 
     def key_type(self, k):
         return N.SK_TYPE_STRING if k in self.strings else (N.SK_TYPE_HLL if k in self.ref.regs else N.SK_TYPE_NONE)
+
+    # the slab-id path the coalescer uses (sk_type_many, sk_hll_resolve, sk_pfadd_ids)
+    def key_types(self, keys):
+        return np.array([self.key_type(k) for k in keys], dtype=np.int32)
+
+    def hll_resolve(self, keys, with_created=False):
+        self.slabs = getattr(self, "slabs", [])
+        ids, cr = [], []
+        for k in keys:
+            if k in self.strings:
+                raise RedisException("WRONGTYPE Key is not a valid HyperLogLog string value.")
+            cr.append(k not in self.ref.regs)
+            if cr[-1]:
+                self.ref.regs[k] = np.zeros(16384, dtype=np.uint8)
+                self.slabs.append(k)
+            ids.append(self.slabs.index(k) if k in self.slabs else self._adopt(k))
+        ids = np.array(ids, dtype=np.uint32)
+        return (ids, np.array(cr, dtype=np.uint8)) if with_created else ids
+
+    def _adopt(self, k):
+        self.slabs.append(k)
+        return len(self.slabs) - 1
+
+    def pfadd_ids_status(self, ids, elems):
+        self.calls += 1
+        keys = [self.slabs[int(i)] for i in ids]
+        if any(k not in self.ref.regs for k in keys):
+            return N.SK_ESTALE, np.zeros(len(keys), np.uint8), "stale"
+        return N.SK_OK, np.array(self.ref.pfadd(keys, elems), dtype=np.uint8), ""
 
 
 class FakeClient:
@@ -155,10 +185,10 @@ def test_group_error_fails_group_and_thread_survives():
     completion thread keeps serving later batches."""
 
     class Exploding(OracleHLLEngine):
-        def pfadd_status(self, keys, elems):
-            if any(k == "boom" for k in keys):
+        def pfadd_ids_status(self, ids, elems):
+            if any(self.slabs[int(i)] == "boom" for i in ids):
                 raise TypeError("cannot encode element")
-            return super().pfadd_status(keys, elems)
+            return super().pfadd_ids_status(ids, elems)
 
     cl = FakeClient(Exploding())
     try:
@@ -172,6 +202,31 @@ def test_group_error_fails_group_and_thread_survives():
         b2 = cl.createBatch()
         _fill(b2, 2, 20, 3)
         assert len(b2.executeAsync().get(30)) == 20
+    finally:
+        cl.close()
+
+
+def test_cached_ids_survive_and_recover_from_delete():
+    """Groups after the first use cached slab handles (no name resolution); a key deleted between groups makes
+    the cached handle stale: the coalescer drops its cache, resolves again, and the command that re-creates the
+    key replies 1 (PFADD on a missing key creates it)."""
+    eng = OracleHLLEngine()
+    cl = FakeClient(eng)
+    try:
+        b = cl.createBatch()
+        _fill(b, 7, 50, 4)
+        b.executeAsync().get(30)
+        n_slabs = len(eng.slabs)
+        b = cl.createBatch()
+        _fill(b, 8, 50, 4)
+        b.executeAsync().get(30)
+        assert len(eng.slabs) == n_slabs            # every key came from the cache
+        del eng.ref.regs["t:1"]                     # DEL t:1 behind the coalescer's back
+        b = cl.createBatch()
+        f = b.getHyperLogLog("t:1").addAsync(12345)
+        b.getHyperLogLog("t:1").addAsync(12345)
+        b.executeAsync().get(30)
+        assert f.get() is True and "t:1" in eng.ref.regs
     finally:
         cl.close()
 

@@ -781,3 +781,21 @@ def test_pfadd_long_elements_workgroup_hash(O):
             np.testing.assert_array_equal(e.hll_registers(k), ref.regs[k])
     finally:
         e.close()
+
+
+def test_stale_handle_after_generation_wrap(engine):
+    """A slab whose 8-bit generation would wrap is retired instead of reused: a handle cached before
+    300 delete / re-create cycles of its key is still refused with SK_ESTALE, and no cycle reuses its slab."""
+    from redisson_amd.engine import RedisException
+
+    k = b"wrap:key"
+    h0 = engine.hll_resolve([k])[0]
+    seen = set()
+    for _ in range(300):
+        engine.delete([k])
+        h = int(engine.hll_resolve([k])[0])
+        seen.add(h)
+        with pytest.raises(RedisException, match="not held by a key"):
+            engine.pfadd_ids(np.array([h0], dtype=np.uint32), [[b"e"]])
+    assert int(h0) not in seen
+    engine.delete([k])

@@ -61,6 +61,7 @@ def test_jni_drive_every_entry_point(O):
     assert out["get_missing"] == ["1"]
     assert out["set_getbit"] == ["0", "1", "1"]
     assert out["type_hll"] == ["0", "1"]
+    assert out["typeMany"] == ["0", "1", "2", "0"]
     assert out["bitsetLength"] == ["0", "101"]
     assert out["bloomTryInit"] == ["0", "1"]
     assert out["bloomConfig"] == ["0", "729", "100", "5", "0.0300"]

@@ -141,6 +141,12 @@ def c2zipf(eng, args):
     eng.prof_enable(False)
     n_l, ms = eng.prof_read("hll_hist")
     k_ms = ms / max(n_l, 1)
+    d_sum = eng.alloc(nt * 16)
+    eng.prof_reset(); eng.prof_enable(True)
+    timed(eng, lambda: eng.hll_sum_dev(nt, d_all, d_sum), reps=3)
+    eng.prof_enable(False)
+    n_s, ms_s = eng.prof_read("hll_sum")
+    s_ms = ms_s / max(n_s, 1)
     t_c = timed(eng, lambda: eng.pfcount([[nm] for nm in names]))
     t_ci = timed(eng, lambda: eng.pfcount_ids(ids))                  # slab ids cached by the caller
     gbs = nt * 16384 / (k_ms * 1e-3) / 1e9
@@ -151,8 +157,12 @@ def c2zipf(eng, args):
           "group_commit_inserts_per_s": B * G / t_g, "group_commit_kernel_ms": g_ms,
           "group_commit": "%d fresh 1M batches as one call (line schedule), host-timed" % G,
           "pfcount_keys_per_s": nt / t_c, "pfcount_ids_keys_per_s": nt / t_ci, "hist_keys_per_s_host_timed": nt / t_h,
-          "roofline": {"kernel": "hll_hist", "bound": "hbm", "achieved": gbs, "peak": PEAK, "unit": "GB/s",
-                       "frac": gbs / PEAK, "bytes_per_unit": 16384, "avg_launch_ms": k_ms}})
+          "hll_hist": {"achieved_GBps": gbs, "frac": gbs / PEAK, "avg_launch_ms": k_ms,
+                       "note": "64-bin histograms (sk_hll_histogram_dev; the redis >= 5 estimator's input)"},
+          "roofline": {"kernel": "hll_sum (PFCOUNT, redis 3.x: exact register sums)", "bound": "hbm",
+                       "achieved": nt * 16384 / (s_ms * 1e-3) / 1e9, "peak": PEAK, "unit": "GB/s",
+                       "frac": nt * 16384 / (s_ms * 1e-3) / 1e9 / PEAK, "bytes_per_unit": 16384,
+                       "avg_launch_ms": s_ms}})
 
 
 def c4(eng, args):
@@ -409,6 +419,22 @@ def host(eng, args):
                                     gbuf.ctypes.data, gout.ctypes.data))
     grp()
     t_grp = timed(eng, grp, reps=2)
+    # the same group from pinned host buffers (sk_host_alloc: what the JNI side's direct ByteBuffers would be)
+    pin = eng.host_alloc(gids.nbytes + gcounts.nbytes + gof.nbytes + gbuf.nbytes + 64)
+    views, at = [], 0
+    for a in (gids, gcounts, gof, gbuf):
+        v = pin[at:at + a.nbytes].view(a.dtype)
+        v[:] = a
+        views.append(v)
+        at += (a.nbytes + 15) // 16 * 16
+    pids, pcnt, poff, pbuf = views
+
+    def grp_pinned():
+        eng._check(lib.sk_pfadd_ids(ctx, B * G, pids.ctypes.data, pcnt.ctypes.data, poff.ctypes.data,
+                                    pbuf.ctypes.data, gout.ctypes.data))
+    t_grp_pin = timed(eng, grp_pinned, reps=2)
+    del views, pids, pcnt, poff, pbuf
+    eng.host_free(pin)
     # the same PFADD batch with inputs already on the device (diagnostic: device share of the host path)
     dk, do_, db, dout = (eng.to_device(kids), eng.to_device(batches[1][0]), eng.to_device(batches[1][1], pad=16),
                          eng.alloc(B))
@@ -422,9 +448,9 @@ def host(eng, args):
           "value": 2 * B / (t_pfi + t_ct), "unit": "ops/s",
           "config": {"workload": "host", "batch": B, "tenants": nt, "bloom_bits": size, "bloom_k": k},
           "pfadd_host_per_s": B / t_pf, "pfadd_ids_host_per_s": B / t_pfi,
-          "group_commit_ids_host_per_s": B * G / t_grp,
+          "group_commit_ids_host_per_s": B * G / t_grp, "group_commit_ids_pinned_per_s": B * G / t_grp_pin,
           "group_commit": "%d RBatches of 1M PFADDs as one sk_pfadd_ids call (host buffers, cached slab ids; the "
-                          "library stages pageable inputs through two pinned buffers)" % G,
+                          "pinned: the same inputs in sk_host_alloc memory)" % G,
           "pfadd_ids_ms_per_batch": t_pfi * 1e3, "bloom_add_host_per_s": B / t_add, "bloom_contains_host_per_s": B / t_ct,
           "pfadd_ms_per_batch": t_pf * 1e3, "bloom_contains_ms_per_batch": t_ct * 1e3,
           "pfadd_h2d_bytes": int(h2d_pf), "pageable_h2d_GBps": raw.nbytes / t_h2d / 1e9,

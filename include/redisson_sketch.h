@@ -156,6 +156,11 @@ int sk_pfcount(sk_ctx *ctx, uint32_t n_cmds, const uint32_t *nkeys, const uint64
  * out[i] = PFCOUNT of key_ids[i].  One histogram launch, estimates on host
  * threads.  Ids no key holds fail with SK_ESTALE (as for sk_pfadd_ids). */
 int sk_pfcount_ids(sk_ctx *ctx, uint64_t n, const uint32_t *key_ids, int64_t *out);
+/* per-key exact register sums for slab ids (device in / device out u64[2n]): d_out[2i] = sum of 2^(40 - r) over the
+ * registers, d_out[2i+1] = zero registers | (a register >= 40) << 32.  Without such a register,
+ * E = d_out[2i] * 2^-40 is bit-identical to redis 3.x hllDenseSum (the PFCOUNT path of sk_pfcount /
+ * sk_pfcount_ids under redis_major 3); with one, d_out[2i] is not meaningful */
+int sk_hll_sum_dev(sk_ctx *ctx, uint64_t n, const uint32_t *d_key_ids, uint64_t *d_out);
 /* per-key 64-bin register histograms for slab ids (device in / device out u32[n*64]) */
 int sk_hll_histogram_dev(sk_ctx *ctx, uint64_t n, const uint32_t *d_key_ids, uint32_t *d_hist);
 /* PFMERGE dest src1..srcn (dest included in the max, becomes dense) */

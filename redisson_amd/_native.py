@@ -70,6 +70,7 @@ SIGNATURES = {
     "sk_pfcount": (c_int, [P, c_uint32, _u32p, _u64p, _u8p, _i64p]),
     "sk_pfcount_ids": (c_int, [P, c_uint64, _u32p, _i64p]),
     "sk_hll_histogram_dev": (c_int, [P, c_uint64, _u32p, _u32p]),
+    "sk_hll_sum_dev": (c_int, [P, c_uint64, _u32p, _u64p]),
     "sk_pfmerge": (c_int, [P, _u8p, c_uint64, c_uint32, _u64p, _u8p]),
     "sk_hll_union_dev": (c_int, [P, c_uint64, _u32p, _u8p]),
     "sk_hll_epoch": (c_int, [P, P]),

@@ -83,6 +83,8 @@ hipError_t sort_pairs64(hipStream_t st, void *tmp, size_t tmp_bytes, const uint6
 hipError_t sort_pairs_size(uint64_t n, unsigned begin_bit, unsigned end_bit, size_t *bytes);
 hipError_t sort_pairs(hipStream_t st, void *tmp, size_t tmp_bytes, const uint64_t *kin, uint64_t *kout,
                       const uint32_t *vin, uint32_t *vout, uint64_t n, unsigned begin_bit, unsigned end_bit);
+// per key: out[2k] = sum 2^(40 - r) over the registers, out[2k+1] = zeros | (a register >= 40) << 32 (PFCOUNT 3.x)
+hipError_t launch_hll_sum(hipStream_t st, uint64_t n, const uint32_t *ids, const uint8_t *arena, uint64_t *out);
 hipError_t launch_hll_hist(hipStream_t st, uint64_t n, const uint32_t *ids, const uint8_t *arena, uint32_t *hist);
 hipError_t launch_hll_union(hipStream_t st, uint64_t n, const uint32_t *ids, const uint8_t *arena, uint8_t *partial,
                             uint64_t max_groups, uint8_t *out, int include_out);

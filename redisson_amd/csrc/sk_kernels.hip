@@ -916,17 +916,28 @@ __global__ void __launch_bounds__(SK_PFP_ATPB) __attribute__((amdgpu_waves_per_e
                            // uses sh <= SH sketches per fine bucket, sized so a fine bucket expects <= ~768 records
 #define SK_PFL_TILE 448    // hash blocks per run tile (default; SK_PFL_TILE): ~14.3 k records per region
 #define SK_PFL_RTPB 1024   // region threads: one hash-block segment each
+#ifndef SK_PFL_RPER
 #define SK_PFL_RPER 16     // records per region thread held in registers
+#endif
 #define SK_PFL_RCAP (SK_PFL_RTPB * SK_PFL_RPER) // most records of a one-piece region
+#ifndef SK_PFL_ATPB
 #define SK_PFL_ATPB 256    // apply threads (five apply workgroups per CU)
+#endif
+#ifndef SK_PFL_CAP
 #define SK_PFL_CAP 768     // records per apply chunk (a fine bucket expects <= ~600: six apply workgroups per CU)
+#endif
+#ifndef SK_PFL_HT
 #define SK_PFL_HT 256      // chain heads per chunk (LDS: six apply workgroups per CU)
+#endif
 #define SK_PFL_MAXSUB 8192 // fine buckets per coarse bucket (2^20 sketches)
 #define SK_PFL_TMAX 1024   // largest run tile (hash blocks): one segment per region thread
+#ifndef SK_PFL_NTMAX
 #define SK_PFL_NTMAX 64    // most tiles per call (the apply's run table; 5 apply workgroups per CU need <= 32 KiB of LDS)
+#endif
 #define SK_PFL_LDS (160 * 1024 - 9 * 1024) // dynamic LDS of a region workgroup: records + fine-bucket counts
 __device__ __forceinline__ uint32_t pfl_ht(uint64_t key) {
-    return uint32_t((key * 0xC2B2AE3D27D4EB4Full) >> 56); // 8 bits
+    static_assert((SK_PFL_HT & (SK_PFL_HT - 1)) == 0, "power-of-two chain heads");
+    return uint32_t((key * 0xC2B2AE3D27D4EB4Full) >> (64 - __builtin_ctz(SK_PFL_HT)));
 }
 
 // Fine buckets take sketches by a permuted slab id, p = slab * pa mod 2^pk (pa odd, a bijection): slabs are
@@ -1258,12 +1269,12 @@ __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const uint64_t *__res
     if (probe & 256) return; // dev ablation: run table only
     // record u of the fine bucket (u < cnt): run t with rp[t] <= u < rp[t + 1].  A one-chunk bucket reads t from
     // run_of[u] (filled below, one LDS read per record); chunked buckets search rp (fixed steps, no branches)
-    static_assert(SK_PFL_NTMAX <= 64 && SK_PFL_NTMAX <= 256, "run_of holds u8 run numbers; 6 search steps");
+    static_assert(SK_PFL_NTMAX <= 128, "run_of holds u8 run numbers; 7 search steps");
     uint8_t *run_of = fin; // the records' run numbers (u < cnt), read before the chunk's walk writes fin
     auto rec_at = [&](uint32_t u) -> uint64_t {
         uint32_t lo = 0;
 #pragma unroll
-        for (uint32_t step = 32; step; step >>= 1)
+        for (uint32_t step = 64; step; step >>= 1)
             if (lo + step < ntile && rp[lo + step] <= u) lo += step;
         return rec2[rs[lo] + (u - rp[lo])];
     };
@@ -1463,6 +1474,49 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ uint4 ld_nt(const uint4 *p) {
     u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p));
     return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+// -------------------------------------------------------------- exact register sums (PFCOUNT, redis 3.x)
+// The 3.x estimator needs only E = sum 2^-r[j] and the zero count (hllDenseSum).  With every register <= 39 each
+// partial sum of E is exact in double (multiples of 2^-39 below 2^14), so E = S * 2^-40 with the integer
+// S = sum 2^(40 - r[j]) (< 2^55) is bit-identical to Redis's sum in any order.  One wave per key, no LDS: a lane sums
+// 256 registers (16 x 16-B loads in flight), the wave reduces with shuffles.  out[2k] = S, out[2k + 1] = zeros |
+// (a register >= 40) << 32: the host then takes Redis's register-order sum instead (S is not used).
+// Per byte: extract, 40 - r (the 64-bit shift takes it mod 64: garbage only for r > 40, which the flag catches),
+// a 64-bit shift and add; per word the zero count and the >= 40 test (r + 24 reaches bit 6 iff r >= 40, r <= 63).
+__global__ void __launch_bounds__(256) k_hll_sum(uint64_t n, const uint32_t *__restrict__ ids,
+                                                 const uint8_t *__restrict__ arena, uint64_t *__restrict__ out) {
+    const uint32_t lane = threadIdx.x & 63u;
+    for (uint64_t key = uint64_t(blockIdx.x) * 4 + (threadIdx.x >> 6); key < n; key += uint64_t(gridDim.x) * 4) {
+        const uint4 *base = reinterpret_cast<const uint4 *>(arena + (uint64_t(ids[key] & SK_SLAB_MASK) << 14));
+        uint4 v[16];
+#pragma unroll
+        for (int it = 0; it < 16; it++) v[it] = ld_nt(base + it * 64 + lane);
+        uint64_t S = 0;
+        uint32_t zeros = 0, ge40 = 0;
+#pragma unroll
+        for (int it = 0; it < 16; it++) {
+            const uint32_t ws[4] = {v[it].x, v[it].y, v[it].z, v[it].w};
+#pragma unroll
+            for (int w = 0; w < 4; w++) {
+                const uint32_t x = ws[w] & 0x3f3f3f3fu;
+                zeros += __popc(~(((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x | 0x7f7f7f7fu));
+                ge40 |= (x + 0x18181818u) & 0x40404040u;
+#pragma unroll
+                for (int b = 0; b < 4; b++) S += 1ull << ((40u - ((x >> (8 * b)) & 63u)) & 63u);
+            }
+        }
+#pragma unroll
+        for (int o = 32; o; o >>= 1) {
+            S += __shfl_xor(S, o);
+            zeros += __shfl_xor(zeros, o);
+            ge40 |= __shfl_xor(ge40, o);
+        }
+        if (lane == 0) {
+            out[2 * key] = S;
+            out[2 * key + 1] = uint64_t(zeros) | (uint64_t(ge40 ? 1u : 0u) << 32);
+        }
+    }
 }
 
 // -------------------------------------------------------------- histogram
@@ -2922,6 +2976,13 @@ hipError_t sort_pairs64(hipStream_t st, void *tmp, size_t tmp_bytes, const uint6
     if (!n) return hipSuccess;
     size_t sz = tmp_bytes;
     return rocprim::radix_sort_pairs(tmp, sz, kin, kout, vin, vout, size_t(n), 0, 64, st);
+}
+
+hipError_t launch_hll_sum(hipStream_t st, uint64_t n, const uint32_t *ids, const uint8_t *arena, uint64_t *out) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k_hll_sum, dim3(grid_for((n + 3) / 4, 1, 4096)), dim3(256), 0, st, n, ids, arena, out);
+    SK_LAUNCH_CHECK();
+    return hipSuccess;
 }
 
 hipError_t launch_hll_hist(hipStream_t st, uint64_t n, const uint32_t *ids, const uint8_t *arena, uint32_t *hist) {

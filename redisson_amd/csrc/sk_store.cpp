@@ -244,7 +244,7 @@ struct sk_ctx {
     // host -> device staging of caller host buffers (stage_h2d): two pinned buffers, filled by host threads in turn
     uint8_t *stage[2] = {nullptr, nullptr};
     hipEvent_t stage_ev[2] = {nullptr, nullptr};
-    bool stage_on = true;       // SK_STAGE=0: plain pageable copies
+    bool stage_on = false;      // SK_STAGE=1: stage pageable inputs (measured no faster than HIP's own pageable path)
 
     bool async_dev = false;     // sk_set_async: _dev calls return without a final sync
     int pfadd_path = 1;         // 0 claim/commit, 1 partition, 2 sorted (SK_PFADD_PATH); dense batches use 2
@@ -365,7 +365,7 @@ const char *kPhaseNames[] = {"pfadd_hash",  "pfadd_sort",   "pfadd_apply", "hll_
                              "getbit",      "bitcount",     "bitop",       "pfadd_claim", "pfadd_commit",
                              "pfp_hash",    "pfp_apply",    "pfp_reply",   "bloom_rc_hash", "bloom_rc_probe", "pfadd",
                              "pfadd_long",  "bloom_ra_hash", "bloom_ra_apply", "pfl_hash",   "pfl_part",
-                             "pfl_apply"};
+                             "pfl_apply",   "hll_sum"};
 constexpr int kNumPhases = sizeof(kPhaseNames) / sizeof(kPhaseNames[0]);
 
 hipEvent_t ev_get(sk_ctx *c) {
@@ -606,7 +606,8 @@ int stage_h2d(sk_ctx *c, void *dst, const void *src, uint64_t bytes) {
             HIPCHK(c, hipEventCreateWithFlags(&c->stage_ev[k], hipEventDisableTiming));
             HIPCHK(c, hipEventRecord(c->stage_ev[k], c->st));
         }
-    const unsigned T = std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
+    static const unsigned TT = getenv("SK_STAGE_THREADS") ? unsigned(atoi(getenv("SK_STAGE_THREADS"))) : 16u;
+    const unsigned T = std::max(1u, std::min(TT, std::thread::hardware_concurrency()));
     const uint8_t *s8 = static_cast<const uint8_t *>(src);
     uint8_t *d8 = static_cast<uint8_t *>(dst);
     for (uint64_t o = 0, p = 0; o < bytes; o += kStagePiece, p++) {
@@ -1797,6 +1798,14 @@ int sk_pfadd_dev(sk_ctx *c, uint64_t n, const uint32_t *d_ids, const uint64_t *d
 }
 
 // --------------------------------------------------------------- PFCOUNT
+int sk_hll_sum_dev(sk_ctx *c, uint64_t n, const uint32_t *d_ids, uint64_t *d_out) {
+    std::lock_guard<std::mutex> g(c->mu);
+    ENTER(c);
+    { Prof p_(c, 27);
+    HIPCHK(c, sk::launch_hll_sum(c->st, n, d_ids, c->arena, d_out)); }
+    return sync(c);
+}
+
 int sk_hll_histogram_dev(sk_ctx *c, uint64_t n, const uint32_t *d_ids, uint32_t *d_hist) {
     std::lock_guard<std::mutex> g(c->mu);
     ENTER(c);
@@ -1808,6 +1817,45 @@ int sk_hll_histogram_dev(sk_ctx *c, uint64_t n, const uint32_t *d_ids, uint32_t 
 // Estimates of many single-key counts: exact-sum histograms (every register
 // < 40, and every redis >= 5 estimate) in parallel threads, the rest (the
 // register-order sum needs a register readback) in order afterwards.
+// Single-key counts under the 3.x estimator from the device's exact register sums (k_hll_sum): E = S * 2^-40 when
+// no register is >= 40 (bit-identical to hllDenseSum, see the kernel), else Redis's register-order sum.
+static int estimate_many_sums(sk_ctx *c, uint64_t n, const uint64_t *s2, const uint32_t *ids, int64_t *out) {
+    std::vector<uint8_t> slow(n, 0);
+    auto work = [&](uint64_t i0, uint64_t i1) {
+        for (uint64_t i = i0; i < i1; i++) {
+            const uint32_t zeros = uint32_t(s2[2 * i + 1]), ge40 = uint32_t(s2[2 * i + 1] >> 32);
+            if (!ge40) out[i] = int64_t(estimate_v3(std::ldexp(double(s2[2 * i]), -40), int(zeros)));
+            else slow[i] = 1;
+        }
+    };
+    unsigned T = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    if (const char *e = getenv("OMP_NUM_THREADS")) T = std::max(1, std::min(int(T), atoi(e)));
+    if (n < 65536) T = 1;
+    std::vector<std::thread> th;
+    uint64_t per = (n + T - 1) / T;
+    for (unsigned t = 1; t < T && t * per < n; t++) th.emplace_back(work, t * per, std::min<uint64_t>(n, (t + 1) * per));
+    work(0, std::min<uint64_t>(n, per));
+    for (auto &x : th) x.join();
+    for (uint64_t i = 0; i < n; i++) {
+        if (!slow[i]) continue;
+        std::vector<uint8_t> regs(kHllBytes);
+        HIPCHK(c, hipMemcpy(regs.data(), c->arena + uint64_t(ids[i] & kSlabMask) * kHllBytes, kHllBytes,
+                            hipMemcpyDeviceToHost));
+        int ez;
+        const double E = dense_sum(regs.data(), &ez);
+        out[i] = int64_t(estimate_v3(E, ez));
+    }
+    return SK_OK;
+}
+int hll_sums(sk_ctx *c, uint64_t n, const uint32_t *d_ids, std::vector<uint64_t> &s2) {
+    HIPCHK(c, c->hist.ensure(n * 16));
+    { Prof p_(c, 27);
+    HIPCHK(c, sk::launch_hll_sum(c->st, n, d_ids, c->arena, c->hist.as<uint64_t>())); }
+    s2.resize(n * 2);
+    HIPCHK(c, hipMemcpyAsync(s2.data(), c->hist.p, n * 16, hipMemcpyDeviceToHost, c->st));
+    return sync(c);
+}
+
 static int estimate_many(sk_ctx *c, uint64_t n, const uint32_t *h, const uint32_t *ids, int64_t *out) {
     std::vector<uint8_t> slow(n, 0);
     auto work = [&](uint64_t i0, uint64_t i1) {
@@ -1851,10 +1899,18 @@ int sk_pfcount_ids(sk_ctx *c, uint64_t n, const uint32_t *key_ids, int64_t *out)
                     key_ids[d]);
     HIPCHK(c, c->in_ids.ensure(n * 4));
     HIPCHK(c, hipMemcpyAsync(c->in_ids.p, key_ids, n * 4, hipMemcpyHostToDevice, c->st));
-    std::vector<uint32_t> h;
-    int r = hll_histograms(c, n, c->in_ids.as<uint32_t>(), c->arena, h);
-    if (r) return r;
-    int r2 = estimate_many(c, n, h.data(), key_ids, out);
+    int r2;
+    if (c->redis_major < 5) { // exact register sums on the device (k_hll_sum)
+        std::vector<uint64_t> s2;
+        int r = hll_sums(c, n, c->in_ids.as<uint32_t>(), s2);
+        if (r) return r;
+        r2 = estimate_many_sums(c, n, s2.data(), key_ids, out);
+    } else {
+        std::vector<uint32_t> h;
+        int r = hll_histograms(c, n, c->in_ids.as<uint32_t>(), c->arena, h);
+        if (r) return r;
+        r2 = estimate_many(c, n, h.data(), key_ids, out);
+    }
     if (r2 || !c->hll_exact) return r2;
     for (uint64_t i = 0; i < n; i++) hll_card_cache(c, key_ids[i] & kSlabMask, &out[i]);
     return SK_OK;
@@ -1917,10 +1973,16 @@ int sk_pfcount(sk_ctx *c, uint32_t n_cmds, const uint32_t *nkeys, const uint64_t
     if (!single_ids.empty()) {
         HIPCHK(c, c->in_ids.ensure(single_ids.size() * 4));
         HIPCHK(c, hipMemcpyAsync(c->in_ids.p, single_ids.data(), single_ids.size() * 4, hipMemcpyHostToDevice, c->st));
-        int r = hll_histograms(c, single_ids.size(), c->in_ids.as<uint32_t>(), c->arena, h);
-        if (r) return r;
         std::vector<int64_t> est(single_ids.size());
-        if ((r = estimate_many(c, single_ids.size(), h.data(), single_ids.data(), est.data()))) return r;
+        int r;
+        if (c->redis_major < 5) { // exact register sums on the device (k_hll_sum)
+            std::vector<uint64_t> s2;
+            if ((r = hll_sums(c, single_ids.size(), c->in_ids.as<uint32_t>(), s2))) return r;
+            if ((r = estimate_many_sums(c, single_ids.size(), s2.data(), single_ids.data(), est.data()))) return r;
+        } else {
+            if ((r = hll_histograms(c, single_ids.size(), c->in_ids.as<uint32_t>(), c->arena, h))) return r;
+            if ((r = estimate_many(c, single_ids.size(), h.data(), single_ids.data(), est.data()))) return r;
+        }
         for (size_t i = 0; i < single_ids.size(); i++) {
             out[single_cmd[i]] = est[i];
             hll_card_cache(c, single_ids[i], &out[single_cmd[i]]);

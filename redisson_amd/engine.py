@@ -144,6 +144,17 @@ class SketchEngine:
         self._check(self.lib.sk_sync(self.ctx))
 
     # ------------------------------------------------------------ device memory / timing / RCCL
+    def host_alloc(self, nbytes: int) -> np.ndarray:
+        """Pinned host memory (sk_host_alloc) as a u8 array; freed with host_free.  Inputs the caller builds in it are
+        copied to the device at the link's rate with no staging (the JNI side's direct ByteBuffers)."""
+        p = ctypes.c_void_p()
+        self._check(self.lib.sk_host_alloc(self.ctx, int(nbytes), ctypes.addressof(p)))
+        arr = np.ctypeslib.as_array((ctypes.c_uint8 * max(int(nbytes), 1)).from_address(p.value))
+        return arr[:nbytes]
+
+    def host_free(self, arr: np.ndarray):
+        self._check(self.lib.sk_host_free(self.ctx, arr.ctypes.data))
+
     def alloc(self, nbytes: int) -> DeviceBuffer:
         return DeviceBuffer(self, nbytes)
 
@@ -331,6 +342,10 @@ class SketchEngine:
         d = _b(dest)
         soff, sbuf = pack([_b(s) for s in srcs])
         self._check(self.lib.sk_pfmerge(self.ctx, d, len(d), len(srcs), _addr(soff), _addr(sbuf)))
+
+    def hll_sum_dev(self, n: int, d_ids, d_out):
+        """Per-key exact register sums (k_hll_sum): d_out u64[2n] = (sum 2^(40-r), zeros | (any r >= 40) << 32)."""
+        self._check(self.lib.sk_hll_sum_dev(self.ctx, n, _addr(d_ids), _addr(d_out)))
 
     def hll_histogram_dev(self, n: int, d_ids, d_hist):
         self._check(self.lib.sk_hll_histogram_dev(self.ctx, n, _addr(d_ids), _addr(d_hist)))

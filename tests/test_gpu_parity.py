@@ -799,3 +799,31 @@ def test_stale_handle_after_generation_wrap(engine):
             engine.pfadd_ids(np.array([h0], dtype=np.uint32), [[b"e"]])
     assert int(h0) not in seen
     engine.delete([k])
+
+
+def test_hll_sum_kernel_exact(engine, O):
+    """k_hll_sum (the PFCOUNT path under redis 3.x): per-key S = sum 2^(40-r), zero count and the register >= 40
+    flag against numpy on keys with every register value 0..63; PFCOUNT of each key equals the oracle (the keys
+    holding a register >= 40 take the register-order sum)."""
+    rng = np.random.default_rng(77)
+    names = [b"hsum:%d" % i for i in range(40)]
+    ids = engine.hll_resolve(names)
+    regs = []
+    for i, nm in enumerate(names):
+        top = 20 if i % 4 else 63                      # every 4th key reaches registers >= 40
+        r = rng.integers(0, top + 1, 16384, dtype=np.uint8)
+        r[rng.random(16384) < (i % 5) / 5] = 0
+        d = engine.to_device(r)
+        engine.hll_merge_registers_dev(nm, d)
+        d.free()
+        regs.append(r)
+    d_ids, d_out = engine.to_device(ids), engine.alloc(16 * len(names))
+    engine.hll_sum_dev(len(names), d_ids, d_out)
+    got = d_out.download(np.uint64, 2 * len(names))
+    for i, r in enumerate(regs):
+        assert int(got[2 * i + 1]) & 0xffffffff == int((r == 0).sum())
+        assert int(got[2 * i + 1]) >> 32 == int(r.max() >= 40)
+        if r.max() < 40:
+            assert int(got[2 * i]) == int(sum(1 << (40 - int(v)) for v in r))
+    assert [int(x) for x in engine.pfcount_ids(ids)] == [O.count_regs(r, 1) for r in regs]
+    d_ids.free(); d_out.free()

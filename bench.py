@@ -89,6 +89,7 @@ def main():
     ap.add_argument("--bloom-n", type=int, default=425_000_000)
     ap.add_argument("--bloom-p", type=float, default=0.008)
     ap.add_argument("--bloom-fill", type=int, default=1_000_000_000, help="elements added before contains (C3: 1B)")
+    ap.add_argument("--add-chunk", type=int, default=1 << 23, help="elements per Bloom add call of the fill")
     ap.add_argument("--overlap", action="store_true",
                     help="contains on the engine's read stream beside the PFADD stream (default: one stream, chains "
                          "back to back -- overlapping them gains ~2 %% and makes each chain's launch time measure "
@@ -138,7 +139,7 @@ def main():
     eng.bloom_try_init(bloom, args.bloom_n, args.bloom_p)
     size, k, _, _ = eng.bloom_config(bloom)
     seed_b = 0x5EED0003
-    chunk = 1 << 23
+    chunk = args.add_chunk
     d_add_out = eng.alloc(chunk)
     add_s = 0.0      # the add batches only (input generation excluded), host-timed around each call
     for s in range(0, fill, chunk):
@@ -351,7 +352,7 @@ def per_unit_bytes(mean_len_h, mean_len_b, k, size, CB, nr, tenants, group):
     touched = lines * (1.0 - math.exp(-group / lines))   # this many of them (uniform tenants)
     return {
         "pfl_hash": mean_len_h + 8 + 4 + 8,            # key bytes + offset + slab id in, record out
-        "pfl_part": 8 + 8 + 8,                         # records read by count and scatter, written once
+        "pfl_part": 8 + 8,                             # records read once and written once (tile-major region sort)
         "pfl_apply": 8 + 1 + 2 * 128 * touched / group,  # record + reply + each touched line in and out once
         "pfp_hash": mean_len_h + 8 + 4 + 8,            # key bytes + offset + slab id in, record out
         "pfp_apply": 8 + 64 + 64 + 1,                  # record + register sector load (R0) + store + reply
@@ -377,8 +378,7 @@ def pmc_traffic(phase):
     kern = {"bloom_contains": "sk::k_bloom_contains", "pfadd_claim": "sk::k_pfadd_claim",
             "pfadd_commit": "sk::k_pfadd_commit", "pfp_hash": "sk::k_pfp_hash", "pfp_apply": "sk::k_pfp_apply",
             "pfp_reply": "sk::k_pfp_reply", "bloom_rc_hash": "sk::k_bloom_rc_hash<false>", "pfl_hash": "sk::k_pfl_hash",
-            "pfl_apply": "sk::k_pfl_apply", "pfl_part": "sk::k_pfl_count+sk::k_pfl_scatter+sk::k_scan_reduce+"
-                                                      "sk::k_scan_sums+sk::k_scan_apply",
+            "pfl_apply": "sk::k_pfl_fill+sk::k_pfl_plan+sk::k_pfl_apply", "pfl_part": "sk::k_pfl_tot+sk::k_pfl_region",
             "bloom_rc_probe": "sk::k_bloom_rc_probe"}.get(phase)
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_summary.json")))
     if not kern or not files:

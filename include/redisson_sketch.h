@@ -292,9 +292,12 @@ int sk_timer_elapsed(sk_ctx *ctx, int slot_a, int slot_b, float *ms);
  * "hll_union", "bloom_contains", "bloom_probes", "bloom_sort", "bloom_apply",
  * "setbit", "getbit", "bitcount", "bitop", "pfadd_claim", "pfadd_commit",
  * "pfp_hash", "pfp_apply", "pfp_reply", "bloom_rc_hash", "bloom_rc_probe",
- * "pfadd_long", "bloom_ra_hash", "bloom_ra_apply";
+ * "pfadd_long", "bloom_ra_hash", "bloom_ra_apply", "pfl_hash", "pfl_part",
+ * "pfl_apply", "hll_sum";
  * chains: "bloom_contains" (every kernel of one contains call), "pfadd" (every
- * kernel of one sk_pfadd_dev batch) */
+ * kernel of one sk_pfadd_dev batch).  "pfadd_long_fallback" is a count, not a
+ * time: calls whose long elements (>= 64 KiB) were re-hashed per thread because
+ * a look-back wait of the bit-round scan ran out (the call still succeeds) */
 int sk_prof_enable(sk_ctx *ctx, int on);
 /* time only the named phases while profiling is on ("a,b,c"; NULL: every phase) */
 int sk_prof_only(sk_ctx *ctx, const char *phase);

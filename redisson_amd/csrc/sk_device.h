@@ -25,8 +25,13 @@ namespace sk {
 #define SK_LONG_ELEM (uint64_t(1) << 16)
 
 __device__ __forceinline__ uint64_t funnel(uint64_t lo, uint64_t hi, unsigned sh) {
-    // (lo >> sh) | (hi << (64 - sh)), correct for sh == 0 (two shifts < 64)
-    return (lo >> sh) | ((hi << 1) << (63 - sh));
+    // (lo >> sh) | (hi << (64 - sh)) for sh = 8 * (0..7): the 32-bit word pair picked by sh >= 32, then two
+    // byte-aligned 32-bit funnel shifts (v_alignbyte_b32) -- full-rate 32-bit ops instead of three 64-bit shifts
+    const bool up = sh & 32u;
+    const uint32_t w1 = uint32_t(lo >> 32), w2 = uint32_t(hi);
+    const uint32_t a0 = up ? w1 : uint32_t(lo), a1 = up ? w2 : w1, a2 = up ? uint32_t(hi >> 32) : w2;
+    const uint32_t b = (sh >> 3) & 3u;
+    return uint64_t(__builtin_amdgcn_alignbyte(a1, a0, b)) | (uint64_t(__builtin_amdgcn_alignbyte(a2, a1, b)) << 32);
 }
 
 // unaligned little-endian 8-byte load (over-reads < 16 B past p)

@@ -73,7 +73,9 @@ hipError_t launch_pfl_apply(hipStream_t st, const PflDims &d, const uint64_t *re
                             uint8_t *arena, uint8_t *changed, uint32_t *big_alloc, uint64_t *big_keys,
                             uint32_t *big_vals, int flags, // flags & 32: replies pre-filled, only others stored
                             uint32_t *order,               // u32[nf]: dispatch order (heavy fine buckets first)
-                            uint32_t *rc, uint32_t par);
+                            uint32_t *rc, uint32_t par,
+                            void *rt);                     // pfl_rt_bytes(d): the fine-bucket-major run table
+uint64_t pfl_rt_bytes(const PflDims &d);
 hipError_t sort_keys_size(uint64_t n, unsigned begin_bit, unsigned end_bit, size_t *bytes);
 hipError_t sort_keys(hipStream_t st, void *tmp, size_t tmp_bytes, const uint64_t *in, uint64_t *out, uint64_t n,
                      unsigned begin_bit, unsigned end_bit);

@@ -578,7 +578,7 @@ __global__ void __launch_bounds__(SK_MS_TPB) k_ms_rounds(const uint8_t *__restri
                                                          const uint32_t *__restrict__ meta, uint32_t n_long,
                                                          uint32_t n_wg, const uint32_t *__restrict__ plane,
                                                          uint32_t *__restrict__ flags, uint64_t seed,
-                                                         uint64_t *__restrict__ out_h) {
+                                                         uint64_t *__restrict__ out_h, uint32_t spin_max) {
     const uint64_t m = 0xc6a4a7935bd1e995ull;
     __shared__ uint32_t s_id, s_wpar[2][SK_MS_TPB / 64], s_ex[2];
     uint32_t *ctr = flags + uint64_t(n_wg) * 64, *err = ctr + 1;
@@ -649,7 +649,7 @@ __global__ void __launch_bounds__(SK_MS_TPB) k_ms_rounds(const uint8_t *__restri
                     const uint32_t stop = inc_b ? uint32_t(__ffsll((long long)inc_b)) - 1u : 64u;
                     const uint64_t need = stop >= 63 ? ~0ull : ((2ull << stop) - 1ull);
                     if ((rdy & need) != need) {
-                        if (++spins > SK_MS_SPIN) { // a predecessor never published: report, do not hang
+                        if (++spins > spin_max) { // a predecessor never published: report, do not hang
                             if (lane == 0) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                             break;
                         }
@@ -994,17 +994,18 @@ __global__ void __launch_bounds__(SK_PFL_RTPB) k_pfl_region(const uint64_t *__re
     __shared__ uint32_t wsum[SK_PFL_RTPB / 64];
     const uint32_t tid = threadIdx.x, g = blockIdx.x, b = g / ntile, t = g % ntile;
     const uint32_t b0 = t * tb, nb = (b0 + tb < nblk ? b0 + tb : nblk) - b0;
+    // the segment table loads first (independent of the region base below)
+    uint32_t st = 0, len = 0;
+    if (tid < nb) {
+        st = S[uint64_t(b) * nblk + b0 + tid];
+        len = S[uint64_t(b + 1) * nblk + b0 + tid] - st;
+    }
     // this region's base: the records of every region before it (b-major, tile minor)
     uint32_t acc = 0;
     for (uint32_t i = tid; i < g; i += SK_PFL_RTPB) acc += tot[i];
     uint32_t base;
     block_exscan<SK_PFL_RTPB>(acc, wsum, &base);
-    uint32_t st = 0, len = 0;
-    if (tid < nb) {
-        st = S[uint64_t(b) * nblk + b0 + tid];
-        len = S[uint64_t(b + 1) * nblk + b0 + tid] - st;
-        segs[tid] = st;
-    }
+    if (tid < nb) segs[tid] = st;
     uint32_t m;
     const uint32_t ex = block_exscan<SK_PFL_RTPB>(len, wsum, &m);
     if (tid < nb) segp[tid] = ex;
@@ -1055,6 +1056,13 @@ __global__ void __launch_bounds__(SK_PFL_RTPB) k_pfl_region(const uint64_t *__re
         __syncthreads();
     };
     if (m <= cap) { // one piece: every record in registers, ranked by its fine bucket, placed in LDS, written out
+        // each record's segment from a u16 map in the (still free) sort area: one LDS read instead of a binary
+        // search over the tile's segments
+        static_assert(SK_PFL_TMAX <= 65536, "seg_of: u16 segment numbers");
+        uint16_t *seg_of = reinterpret_cast<uint16_t *>(sorted); // m <= cap records: 2 m of the 8 cap bytes
+        if (tid < nb)
+            for (uint32_t u = ex; u < ex + len; u++) seg_of[u] = uint16_t(tid);
+        __syncthreads();
         uint64_t r[SK_PFL_RPER];
         uint32_t rk[SK_PFL_RPER];
 #pragma unroll
@@ -1062,14 +1070,14 @@ __global__ void __launch_bounds__(SK_PFL_RTPB) k_pfl_region(const uint64_t *__re
             const uint32_t x = tid + q * SK_PFL_RTPB;
             r[q] = ~0ull;
             if (x < m) {
-                uint32_t blk;
                 if (probe & 2048) { // dev ablation: no record loads (a record of block b0, timing only)
                     r[q] = (uint64_t(x % pm.nslab) << 32) | (uint64_t(x & 16383) << 18) | (1u << 12) | (x & 4095);
                     rk[q] = b0;
                     continue;
                 }
-                r[q] = pfl_region_rec(chunks, segp, segs, nb, b0, x, &blk);
-                rk[q] = blk;
+                const uint32_t lo = seg_of[x];
+                r[q] = chunks[uint64_t(b0 + lo) * SK_PFP_EPB + segs[lo] + (x - segp[lo])];
+                rk[q] = b0 + lo;
             }
         }
 #pragma unroll
@@ -1193,23 +1201,34 @@ __device__ __forceinline__ void pfl_chunk(const uint64_t *R, uint32_t cnt, uint1
         }
 }
 
+// The run table, fine-bucket major: RT[f * ntile + t] = the rec2 start of fine bucket f's run in tile t | the records of
+// f in tiles before t << 32, FC[f] = f's records.  The apply reads its row as one contiguous piece (296 B at 37 tiles)
+// instead of 2 x ntile scattered words of the region-major C2 (one line each), and learns its count from one word.
 // Heavy fine buckets first: the apply's grid starts with hmax "heavy slots"; the plan lists the fine buckets of more
 // than one chunk (C1, a Zipf head's lines -- they run longest) in order[0..H), H = ctr[0], and heavy slot k applies
 // order[k].  The rest of the grid is the fine buckets in their own order; a heavy one there exits at once.  A
-// uniform call has H = 0: its heavy slots exit and nothing else is indirected.
-__global__ void __launch_bounds__(256) k_pfl_plan(const uint32_t *__restrict__ C2, uint32_t ntile, uint32_t nsub,
-                                                  uint32_t nf, uint32_t hmax, uint32_t *ctr,
-                                                  uint32_t *__restrict__ order) {
+// uniform call has H = 0: its heavy slots exit and nothing else is indirected.  hmax = 0: no heavy slots.
+__global__ void __launch_bounds__(256) k_pfl_plan(const uint32_t *__restrict__ C2, const uint32_t *__restrict__ rbase,
+                                                  uint32_t ntile, uint32_t nsub, uint32_t nf, uint32_t hmax,
+                                                  uint32_t *ctr, uint32_t *__restrict__ order,
+                                                  uint64_t *__restrict__ RT, uint32_t *__restrict__ FC) {
     __shared__ uint32_t wsum[256 / 64], base;
     const uint32_t f = blockIdx.x * 256 + threadIdx.x;
     uint32_t cnt = 0;
     if (f < nf) {
         const uint32_t b = f / nsub, sub = f % nsub;
+        uint64_t *row = RT + uint64_t(f) * ntile;
+#pragma unroll 4
         for (uint32_t t = 0; t < ntile; t++) {
-            const uint32_t *c = C2 + uint64_t(b * ntile + t) * (nsub + 1) + sub;
-            cnt += c[1] - c[0];
+            const uint32_t g = b * ntile + t;
+            const uint32_t *c = C2 + uint64_t(g) * (nsub + 1) + sub;
+            const uint32_t c0 = c[0];
+            row[t] = uint64_t(rbase[g] + c0) | (uint64_t(cnt) << 32);
+            cnt += c[1] - c0;
         }
+        FC[f] = cnt;
     }
+    if (!hmax) return; // uniform
     const bool heavy = cnt > SK_PFL_CAP;
     uint32_t th;
     const uint32_t ph = block_exscan<256>(heavy ? 1u : 0u, wsum, &th);
@@ -1219,8 +1238,8 @@ __global__ void __launch_bounds__(256) k_pfl_plan(const uint32_t *__restrict__ C
 }
 
 __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const uint64_t *__restrict__ rec2,
-                                                           const uint32_t *__restrict__ rbase,
-                                                           const uint32_t *__restrict__ C2, uint32_t ntile,
+                                                           const uint64_t *__restrict__ RT,
+                                                           const uint32_t *__restrict__ FC, uint32_t ntile,
                                                            uint32_t nsub, uint32_t sh, PflPerm pm, uint32_t nslab,
                                                            uint8_t *arena,
                                                            uint8_t *__restrict__ changed, uint32_t *big_alloc,
@@ -1251,21 +1270,36 @@ __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const uint64_t *__res
     } else {
         f = blockIdx.x - hmax;
     }
-    const uint32_t b = f / nsub, sub = f % nsub;
-    uint32_t st = 0, len = 0;
-    if (threadIdx.x < ntile) {
-        const uint32_t g = b * ntile + threadIdx.x;
-        const uint32_t *c = C2 + uint64_t(g) * (nsub + 1) + sub;
-        const uint32_t c0 = c[0];
-        st = rbase[g] + c0;
-        len = c[1] - c0;
-        rs[threadIdx.x] = st;
-    }
-    uint32_t cnt;
-    const uint32_t ex = block_exscan<SK_PFL_ATPB>(len, wsum, &cnt);
-    if (cnt == 0) return; // uniform
+    const uint32_t cnt = FC[f]; // uniform
+    if (cnt == 0) return;
     if (hmax && blockIdx.x >= hmax && cnt > SK_PFL_CAP) return; // applied by a heavy slot
-    if (threadIdx.x < ntile) rp[threadIdx.x] = ex;
+    const uint32_t b = f / nsub, sub = f % nsub;
+    const uint32_t slab0 = sub << sh, nsl = 1u << sh; // permuted ids slab0 + i, i < nsl
+    auto line = [&](uint32_t i) -> uint4 * {
+        const uint32_t s = pm.inv(slab0 + i);
+        return reinterpret_cast<uint4 *>(arena + (uint64_t(s) << 14) + (((b - pfl_rot(s)) & (SK_PFL_NB - 1)) << SK_PFL_LB));
+    };
+    // a one-chunk bucket's lines are issued first: they do not depend on the run table
+    constexpr int LQ = (NL * LW + SK_PFL_ATPB - 1) / SK_PFL_ATPB;
+    uint4 lv[LQ];
+    if (cnt <= SK_PFL_CAP) {
+#pragma unroll
+        for (int j = 0; j < LQ; j++) {
+            const uint32_t q = threadIdx.x + j * SK_PFL_ATPB;
+            if (q < nsl * LW && pm.inv(slab0 + q / LW) < nslab)
+                lv[j] = (probe & 4) ? make_uint4(0, 0, 0, 0) : line(q / LW)[q % LW];
+        }
+    }
+    uint32_t ex = 0, len = 0;
+    if (threadIdx.x < ntile) {
+        const uint64_t *row = RT + uint64_t(f) * ntile;
+        const uint64_t e0 = row[threadIdx.x];
+        const uint32_t nx = threadIdx.x + 1 < ntile ? uint32_t(row[threadIdx.x + 1] >> 32) : cnt;
+        ex = uint32_t(e0 >> 32);
+        len = nx - ex;
+        rs[threadIdx.x] = uint32_t(e0);
+        rp[threadIdx.x] = ex;
+    }
     if (probe & 256) return; // dev ablation: run table only
     // record u of the fine bucket (u < cnt): run t with rp[t] <= u < rp[t + 1].  A one-chunk bucket reads t from
     // run_of[u] (filled below, one LDS read per record); chunked buckets search rp (fixed steps, no branches)
@@ -1294,11 +1328,6 @@ __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const uint64_t *__res
             if (rep) atomicAdd(&s_ones, 1u);
         }
     };
-    const uint32_t slab0 = sub << sh, nsl = 1u << sh; // permuted ids slab0 + i, i < nsl
-    auto line = [&](uint32_t i) -> uint4 * {
-        const uint32_t s = pm.inv(slab0 + i);
-        return reinterpret_cast<uint4 *>(arena + (uint64_t(s) << 14) + (((b - pfl_rot(s)) & (SK_PFL_NB - 1)) << SK_PFL_LB));
-    };
     for (uint32_t i = threadIdx.x; i < NL; i += SK_PFL_ATPB) dirty[i] = 0;
     for (uint32_t t = threadIdx.x; t < SK_PFL_HT; t += SK_PFL_ATPB) head[t] = 0xffffu;
     if (threadIdx.x == 0) {
@@ -1306,15 +1335,7 @@ __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const uint64_t *__res
         s_ones = 0;
     }
     __syncthreads();
-    if (cnt <= SK_PFL_CAP) { // the whole fine bucket is one chunk: records and lines in one round trip
-        constexpr int LQ = (NL * LW + SK_PFL_ATPB - 1) / SK_PFL_ATPB;
-        uint4 lv[LQ];
-#pragma unroll
-        for (int j = 0; j < LQ; j++) {
-            const uint32_t q = threadIdx.x + j * SK_PFL_ATPB;
-            if (q < nsl * LW && pm.inv(slab0 + q / LW) < nslab)
-                lv[j] = (probe & 4) ? make_uint4(0, 0, 0, 0) : line(q / LW)[q % LW];
-        }
+    if (cnt <= SK_PFL_CAP) { // the whole fine bucket is one chunk: records loaded while the lines are in flight
         constexpr int RU = SK_PFL_CAP / SK_PFL_ATPB; // every record load in flight at once
         uint64_t rv[RU];
 #pragma unroll
@@ -2017,6 +2038,9 @@ __device__ __forceinline__ void rc_test(const uint8_t *fb, uint32_t x, uint8_t *
 // stream); then the record vectors of RC_JB segments are loaded one step ahead of the segments being tested,
 // so a lane always has a step of loads in flight while it tests from LDS.
 #define RC_SMAX 8 // blocks per thread: pieces of <= 32 M elements = 8192 blocks
+#ifndef RC_PF
+#define RC_PF 3   // steps of segment loads in flight per thread (2: one step ahead)
+#endif
 __device__ __forceinline__ void rc_load_seg(const uint32_t *chunks, uint64_t CH, uint32_t j, uint32_t seg,
                                             uint4 (&w)[RC_SEGV]) {
     uint32_t st = seg & 0xffffu, cnt = seg >> 16;
@@ -2068,18 +2092,23 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_rc_probe(uint32_t NB, uint32_t
             uint32_t j = threadIdx.x + u * RC_TPB;
             seg0[u] = j < NB ? S[uint64_t(r) * NB + j] : 0u; // coalesced: S is region-major
         }
+        // a ring of RC_PF steps of segment vectors: the first RC_PF - 1 steps are issued before the region's bits
+        // land in LDS, and each step then issues the loads RC_PF - 1 steps ahead of the one it tests
+        const uint64_t CH = uint64_t(RC_EPB) * P;
+        uint4 w[RC_PF][RC_SEGV];
+#pragma unroll
+        for (int u = 0; u < RC_PF - 1; u++) rc_load_seg(chunks, CH, threadIdx.x + u * RC_TPB, seg0[u], w[u]);
 #pragma unroll
         for (uint32_t q = 0; q < VPT; q++) filt[threadIdx.x + q * RC_TPB] = fv[q];
         __syncthreads();
         const uint8_t *fb = reinterpret_cast<const uint8_t *>(filt);
-        const uint64_t CH = uint64_t(RC_EPB) * P;
-        uint4 wa[RC_SEGV], wb[RC_SEGV];
-        rc_load_seg(chunks, CH, threadIdx.x, seg0[0], wa);
 #pragma unroll
         for (int u = 0; u < RC_SMAX; u++) {
             if (uint32_t(u) * RC_TPB >= NB) break; // no thread has a block at this step (uniform)
-            if (u + 1 < RC_SMAX) rc_load_seg(chunks, CH, threadIdx.x + (u + 1) * RC_TPB, seg0[u + 1], (u & 1) ? wa : wb);
-            rc_test_seg(fb, chunks, CH, threadIdx.x + u * RC_TPB, seg0[u], (u & 1) ? wb : wa, out);
+            if (u + RC_PF - 1 < RC_SMAX)
+                rc_load_seg(chunks, CH, threadIdx.x + (u + RC_PF - 1) * RC_TPB, seg0[u + RC_PF - 1],
+                            w[(u + RC_PF - 1) % RC_PF]);
+            rc_test_seg(fb, chunks, CH, threadIdx.x + u * RC_TPB, seg0[u], w[u % RC_PF], out);
         }
     }
 }
@@ -2104,11 +2133,13 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_rc_probe(uint32_t NB, uint32_t
 #define RA_CAP 8192   // records per window (LDS)
 #define RA_HT 4096    // chain heads
 #define RA_DENSE 1024 // records from which the region's bits are staged in LDS
+#ifndef RA_JPT
 #define RA_JPT 4      // blocks per thread (block j = q * RC_TPB + thread): pieces of <= 4096 blocks (8 M elements)
+#endif
 #define RA_NONE 0xffffffffu
 #define RA_RPT (RA_CAP / RC_TPB)
 static_assert(RA_CAP >= 2 * RA_SEGMAX && RA_CAP % RC_TPB == 0 && RA_CAP < 0xffff, "windows: u16 links");
-static_assert(RA_JPT * RC_TPB <= 8192, "block numbers: 13 bits of the order key");
+static_assert(RA_JPT * RC_TPB <= 65536, "block numbers: u16 in the window, 16 bits of the order key");
 
 __device__ __forceinline__ uint32_t ra_mask(uint32_t b) { return (0x80u >> (b & 7u)) << (((b >> 3) & 3u) * 8u); }
 __device__ __forceinline__ uint32_t ra_key(uint32_t blk, uint32_t x) { return (blk << 11) | ((x >> 1) & 0x7ffu); }
@@ -2791,8 +2822,11 @@ hipError_t launch_murmur_long(hipStream_t st, uint32_t n_long, uint32_t n_wg, co
     if (r != hipSuccess) return r;
     hipLaunchKernelGGL(k_ms_planes, dim3(n_wg), dim3(SK_MS_TPB), 0, st, bytes, off, meta, n_long, plane);
     SK_LAUNCH_CHECK();
+    // SK_MS_SPIN_DEV: a test-only lower wait bound, so the host's recompute path is exercised
+    static const uint32_t spin = getenv("SK_MS_SPIN_DEV") ? uint32_t(strtoul(getenv("SK_MS_SPIN_DEV"), nullptr, 10))
+                                                          : SK_MS_SPIN;
     hipLaunchKernelGGL(k_ms_rounds, dim3(n_wg), dim3(SK_MS_TPB), 0, st, bytes, off, meta, n_long, n_wg,
-                       (const uint32_t *)plane, flags, 0xadc83b19ull, out_h);
+                       (const uint32_t *)plane, flags, 0xadc83b19ull, out_h, spin);
     SK_LAUNCH_CHECK();
     return hipSuccess;
 }
@@ -2912,20 +2946,22 @@ hipError_t launch_pfl_fill(hipStream_t st, uint8_t *changed, uint64_t n, uint32_
     return hipSuccess;
 }
 
+uint64_t pfl_rt_bytes(const PflDims &d) { return ((d.nf * 4 + 15) & ~uint64_t(15)) + d.nf * d.ntile * 8; }
+
 hipError_t launch_pfl_apply(hipStream_t st, const PflDims &d, const uint64_t *rec2, const uint32_t *C, uint32_t nslab,
                             uint8_t *arena, uint8_t *changed, uint32_t *big_alloc, uint64_t *big_keys,
-                            uint32_t *big_vals, int flags, uint32_t *order, uint32_t *rc, uint32_t par) {
+                            uint32_t *big_vals, int flags, uint32_t *order, uint32_t *rc, uint32_t par, void *rt) {
     static const int probe_flags = getenv("SK_PFL_PROBE") ? atoi(getenv("SK_PFL_PROBE")) : 0; // dev ablations
     const uint32_t *rbase = C + d.nreg, *C2 = C + 2 * d.nreg;
+    uint32_t *FC = static_cast<uint32_t *>(rt);
+    uint64_t *RT = reinterpret_cast<uint64_t *>(static_cast<uint8_t *>(rt) + ((d.nf * 4 + 15) & ~uint64_t(15)));
     // heavy slots: at most n / (CAP + 1) fine buckets hold more than one chunk
     const uint32_t hmax = order ? uint32_t(std::min<uint64_t>(d.nf, uint64_t(d.nblk) * SK_PFP_EPB / (SK_PFL_CAP + 1)))
                                 : 0u;
-    if (order) {
-        hipLaunchKernelGGL(k_pfl_plan, dim3(uint32_t((d.nf + 255) / 256)), dim3(256), 0, st, C2, d.ntile, d.nsub,
-                           uint32_t(d.nf), hmax, big_alloc + 1, order);
-        SK_LAUNCH_CHECK();
-    }
-    hipLaunchKernelGGL(k_pfl_apply, dim3(uint32_t(d.nf) + hmax), dim3(SK_PFL_ATPB), 0, st, rec2, rbase, C2, d.ntile,
+    hipLaunchKernelGGL(k_pfl_plan, dim3(uint32_t((d.nf + 255) / 256)), dim3(256), 0, st, C2, rbase, d.ntile, d.nsub,
+                       uint32_t(d.nf), hmax, big_alloc + 1, order, RT, FC);
+    SK_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_pfl_apply, dim3(uint32_t(d.nf) + hmax), dim3(SK_PFL_ATPB), 0, st, rec2, RT, FC, d.ntile,
                        d.nsub, d.sh, PflPerm{d.pa, d.pai, d.pm_mask, d.nslab}, nslab, arena, changed, big_alloc,
                        big_keys, big_vals, flags | probe_flags, hmax, big_alloc + 1, order, rc, par);
     SK_LAUNCH_CHECK();

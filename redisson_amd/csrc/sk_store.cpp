@@ -209,8 +209,8 @@ struct sk_ctx {
     uint8_t *arena = nullptr;
     uint64_t hll_cap = 0, hll_next = 0;
     std::vector<uint32_t> hll_free;
-    uint64_t hll_retired = 0;
-    uint64_t hll_epoch = 0;        // bumped whenever an HLL key is created or removed (sk_hll_epoch: cached id sets)      // slabs whose generation wrapped: never handed out again (stale handles stay stale)
+    uint64_t hll_retired = 0;      // slabs whose generation wrapped: never handed out again (stale handles stay stale)
+    uint64_t hll_epoch = 0;        // bumped whenever an HLL key is created or removed (sk_hll_epoch: cached id sets)
     std::vector<uint8_t> hll_live; // slab id -> 1 while a key owns it (caller-cached ids are checked against it)
     std::vector<uint8_t> hll_gen;  // slab id -> generation, bumped when the slab is freed (top byte of a handle)
     std::vector<uint64_t> h_e0, h_off; // host PFADD staging, kept across calls (no page faults per batch)
@@ -274,6 +274,7 @@ struct sk_ctx {
     DBuf rc_S, rc_rec;          // Bloom contains region schedule: segment table + probe records (contains only)
     DBuf long_h, long_which;    // PFADD: hashes of long elements (k_ms_rounds) and their element indexes + layout
     DBuf long_plane, long_flags; // their k bit planes and look-back flags
+    uint64_t long_fallbacks = 0; // calls whose long elements were re-hashed per thread (look-back wait ran out)
     // device PFADD batches, pipelined (SK_PFP_PIPE, default on): batch i+1's k_pfp_hash runs on st3 while batch i's
     // k_pfp_apply runs on st; two scratch sets alternate, events order hash -> apply and apply -> reuse
     struct PfpSet {
@@ -300,7 +301,7 @@ struct sk_ctx {
     uint32_t pfl_tile = 0;      // hash blocks per run tile (SK_PFL_TILE, 0 = the kernel default)
     bool pfl_zero = true;       // replies pre-zeroed, the apply stores only the 1s (SK_PFL_ZERO)
     bool pfl_plan = true;       // heavy fine buckets dispatched first (SK_PFL_PLAN)
-    DBuf pfl_chunks, pfl_S, pfl_C, pfl_rec, pfl_bk, pfl_bv, pfl_ovf, pfl_order;
+    DBuf pfl_chunks, pfl_S, pfl_C, pfl_rec, pfl_bk, pfl_bv, pfl_ovf, pfl_order, pfl_rt;
     DBuf pfl_rc;                // u32[32]: reply-mix counters that pick each call's reply default (two parities)
     uint32_t pfl_par = 0;       // this call's parity
 };
@@ -1092,6 +1093,7 @@ int pfadd_lines(sk_ctx *c, uint64_t n, const uint32_t *d_ids, const uint64_t *d_
     HIPCHK(c, c->pfl_bv.ensure(2 * n * 4));
     HIPCHK(c, c->pfl_ovf.ensure(64));
     HIPCHK(c, c->pfl_order.ensure(d.nf * 4));
+    HIPCHK(c, c->pfl_rt.ensure(sk::pfl_rt_bytes(d)));
     if (!c->pfl_rc.p) { // first call: no reply mix yet (default 0)
         HIPCHK(c, c->pfl_rc.ensure(32 * 4));
         HIPCHK(c, hipMemsetAsync(c->pfl_rc.p, 0, 32 * 4, c->st));
@@ -1113,7 +1115,7 @@ int pfadd_lines(sk_ctx *c, uint64_t n, const uint32_t *d_ids, const uint64_t *d_
                                    d_changed, c->pfl_ovf.as<uint32_t>(), c->pfl_bk.as<uint64_t>(),
                                    c->pfl_bv.as<uint32_t>(), c->pfl_zero ? 32 : 0,
                                    c->pfl_plan ? c->pfl_order.as<uint32_t>() : nullptr, c->pfl_rc.as<uint32_t>(),
-                                   par)); }
+                                   par, c->pfl_rt.p)); }
     if (getenv("SK_PFL_DEBUG")) { // dev: table entries the oversized runs took (2 per record of a min-seq table run)
         uint32_t big = 0;
         HIPCHK(c, hipMemcpyAsync(&big, c->pfl_ovf.p, 4, hipMemcpyDeviceToHost, c->st));
@@ -1326,7 +1328,7 @@ int sk_close(sk_ctx *c) {
                     &c->hist_a, &c->hist_b, &c->ovf, &c->bloom_h, &c->rc_S, &c->rc_rec, &c->long_h,
                     &c->long_which, &c->long_plane, &c->long_flags, &c->ra_S, &c->ra_rec, &c->ra_flag, &c->ev, &c->ev_n,
                     &c->pfl_chunks, &c->pfl_S, &c->pfl_C, &c->pfl_rc, &c->rt_cnt, &c->pfl_rec, &c->pfl_bk, &c->pfl_bv,
-                    &c->pfl_ovf, &c->pfl_order})
+                    &c->pfl_ovf, &c->pfl_order, &c->pfl_rt})
         b->release();
     for (auto &ps : c->pfs) {
         for (DBuf *b : {&ps.chunks, &ps.rep, &ps.S, &ps.big_k, &ps.big_v, &ps.ovf}) b->release();
@@ -1665,8 +1667,11 @@ static int pfadd_host_batch(sk_ctx *c, uint32_t n_cmds, const uint32_t *cmd_key,
                     HIPCHK(c, hipMemcpyAsync(&lerr, c->long_flags.as<uint32_t>() + uint64_t(nwg) * 64 + 1, 4,
                                              hipMemcpyDeviceToHost, c->st));
                     HIPCHK(c, hipStreamSynchronize(c->st)); // `which` is a host vector
-                    if (lerr) return fail(c, SK_EDEVICE, "long-element hash: look-back wait ran out");
-                    d_pre = c->long_h.as<uint64_t>();
+                    // a look-back wait that ran out (a predecessor workgroup delayed, e.g. on a shared GPU) leaves
+                    // these hashes invalid: the hash kernels then hash the long elements per thread instead (slow,
+                    // no waits), so the call still succeeds
+                    c->long_fallbacks += lerr ? 1 : 0;
+                    d_pre = lerr ? nullptr : c->long_h.as<uint64_t>();
                 }
             }
             int r = pfadd_device(c, m, c->in_ids.as<uint32_t>(), c->in_off.as<uint64_t>(), c->in_bytes.as<uint8_t>() - shift,
@@ -3107,6 +3112,11 @@ int sk_prof_reset(sk_ctx *c) {
 }
 int sk_prof_read(sk_ctx *c, const char *phase, uint64_t *launches, double *total_ms) {
     std::lock_guard<std::mutex> g(c->mu);
+    if (!std::strcmp(phase, "pfadd_long_fallback")) { // a count, not a timed phase: calls whose long elements were
+        *launches = c->long_fallbacks;                // re-hashed per thread after a look-back wait ran out
+        *total_ms = 0;
+        return SK_OK;
+    }
     prof_collect(c);
     for (int i = 0; i < kNumPhases; i++)
         if (!std::strcmp(phase, kPhaseNames[i])) {

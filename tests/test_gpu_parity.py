@@ -742,6 +742,44 @@ def test_stale_slab_id_rejected(O):
         e.close()
 
 
+_LONG_FALLBACK = r"""
+import sys, numpy as np
+sys.path.insert(0, sys.argv[1])
+from oracle import oracle as O
+from redisson_amd import SketchEngine
+e = SketchEngine(device=0)
+ref = O.HLLStore()
+rng = np.random.default_rng(5)
+elems = [rng.integers(0, 256, int(n), dtype=np.uint8).tobytes()
+         for n in (3_000_003, 37, 1_048_583, 65_536, 2_500_000, 5)]
+keys = [b"lf:%d" % (i % 2) for i in range(len(elems))]
+assert e.pfadd(keys, [[x] for x in elems]) == ref.pfadd(keys, [[x] for x in elems])
+for k in set(keys):
+    np.testing.assert_array_equal(e.hll_registers(k), ref.regs[k])
+n_fb, _ = e.prof_read("pfadd_long_fallback")
+e.close()
+print("fallbacks", n_fb)
+"""
+
+
+def test_pfadd_long_elements_lookback_fallback():
+    """a look-back wait of the bit-round scan that runs out (a delayed predecessor workgroup, e.g. on a
+    GPU shared by two processes) must not fail the PFADD.  A child process forces a zero wait bound
+    (SK_MS_SPIN_DEV=0): the long elements are then re-hashed per thread, and replies and registers still equal the
+    oracle's."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, SK_MS_SPIN_DEV="0")
+    r = subprocess.run([sys.executable, "-c", _LONG_FALLBACK, root], env=env, capture_output=True, text=True,
+                       timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    n_fb = int(r.stdout.split("fallbacks")[1])
+    assert n_fb >= 1, r.stdout   # the zero bound made some workgroup give up waiting
+
+
 def test_pfadd_long_elements_workgroup_hash(O):
     """C1's addAll (quirk Q1: ONE element = the Jackson array of 1M Longs, ~40 MB) and a batch mixing elements
     of 64 KiB .. 3 MB with short ones: elements >= 64 KiB are hashed by the bit-round scan (k_ms_planes +

@@ -12,7 +12,7 @@ for rep in 1 2; do
 import json,sys
 d=json.load(open(sys.argv[1]))
 k=d['kernels']
-print('%-8s value %.3f G  ' % (sys.argv[2], d['value']/1e9) + '  '.join('%s %.3f' % (n, v['ms_isolated']) for n, v in k.items()) + '  chain %.3f' % d['chains']['pfadd']['ms_isolated'])
+print('%-8s value %.3f G add %.2f G/s ' % (sys.argv[2], d['value']/1e9, (d.get('bloom_add_per_s') or 0)/1e9) + '  '.join('%s %.3f' % (n, v['ms_isolated']) for n, v in k.items()) + '  chain %.3f' % d['chains']['pfadd']['ms_isolated'])
 PY
   done
 done

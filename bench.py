@@ -249,6 +249,14 @@ def main():
     avg_ms = tot_ms / max(n_launch, 1)
     # SURVEY 8(d) per-unit bytes of each chain (53 B per PFADD element at C2; len + 9 + 64(k-1) per contains)
     s8 = {"pfadd": mean_len_h + 12 + 2.5, "bloom_contains": mean_len_b + 8 + 1 + 64 * (k - 1)}
+    # the schedule's own minimum HBM bytes per unit (a second roofline, DESIGN.md "Measurement"): what the chain
+    # must move as built -- inputs, replies, its intermediate records written and read back, the register lines or
+    # the bit array once per pass -- so that a chain which beats SURVEY 8(d)'s per-probe pricing still reads < 1
+    lines = 128.0 * len(mine)
+    touched = lines * (1.0 - math.exp(-(G * B) / lines))
+    piece = min(CB, 32 << 20)                         # contains pieces of <= 32 M elements (sk_store.cpp)
+    own = {"pfadd": mean_len_h + 8 + 4 + 1 + 4 * 8 + 2 * 128 * touched / (G * B),
+           "bloom_contains": mean_len_b + 8 + 1 + 2 * 4 * (k - 1) + 2 * 4.0 * nr / 4096 + (size / 8.0) / piece}
     achieved = s8[dom] * upl[dom] / (avg_ms * 1e-3) / 1e9
     # PMC bytes per dispatch x dispatches of each kernel per launch of the chain (a 64 M contains call is two
     # 32 M pieces)
@@ -277,6 +285,8 @@ def main():
                       "units_per_s_isolated": u / (ms * 1e-3),
                       "s8d_GBps_isolated": s8[ch] * u / (ms * 1e-3) / 1e9,
                       "s8d_frac_isolated": s8[ch] * u / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                      "schedule_min_bytes_per_unit": own[ch],
+                      "schedule_min_frac_isolated": own[ch] * u / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                       "ms_overlapped": over.get(ch, (0, None))[1]}
     hll_ms = iso["pfadd"][1] if "pfadd" in iso else None
     bl_ms = iso["bloom_contains"][1] if "bloom_contains" in iso else None
@@ -323,6 +333,8 @@ def main():
                      "traffic_source": "newest profiles/*_pmc_summary.json: 2 x FETCH_SIZE (gfx950) + WRITE_SIZE per "
                                        "dispatch, times dispatches per chain launch, summed over the chain's kernels",
                      "bytes_per_unit": s8[dom], "bytes_per_unit_source": "SURVEY 8(d)",
+                     "schedule_min_bytes_per_unit": own[dom],
+                     "schedule_min_frac": own[dom] * upl[dom] / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                      "units_per_launch": upl[dom], "avg_launch_ms": avg_ms, "launches_timed": n_launch,
                      "kernel_ms_isolated": {p_: iso[p_][1] for p_ in chain_kernels[dom] if p_ in iso},
                      "kernel_ms_overlapped": {p_: over[p_][1] for p_ in chain_kernels[dom] if p_ in over},

@@ -463,23 +463,42 @@ class ShardedBitSet:
 
 
 def _owned_lengths(engine, keys: Sequence, rank: int, world: int, coll) -> List[int]:
-    """Byte length of every key (-1: missing), each reported by its owner."""
+    """Byte length of every key (-1: missing), each reported by its owner.  SPMD: a failure on one rank raises on
+    every rank (cluster.agree) before the all-gather."""
     mine = np.full(len(keys), -2, dtype=np.int64)
-    for i, k in enumerate(keys):
-        if owner(k, world) == rank:
-            t = engine.key_type(k)
-            mine[i] = engine.strlen(k) if t else -1
+    err = None
+    try:
+        for i, k in enumerate(keys):
+            if owner(k, world) == rank:
+                t = engine.key_type(k)
+                mine[i] = engine.strlen(k) if t else -1
+    except Exception as e:  # noqa: BLE001 - agreed on below
+        err = e
+    agree(coll, err)
     parts = coll.allgather_bytes(mine.tobytes())
     allv = np.stack([np.frombuffer(p, dtype=np.int64) for p in parts])
     return [int(allv[owner(k, world), i]) for i, k in enumerate(keys)]
+
+
+def _source_to_dev(engine, key, buf, at: int, n: int) -> None:
+    """The first n bytes of a BITOP source into device buffer `buf` at byte `at`: a bit string device to device; any
+    other string (an HLL reads as its Redis encoding, as BITOP on redis-server takes it) through the host."""
+    from . import _native as N
+
+    if engine.key_type(key) == N.SK_TYPE_STRING:
+        engine.get_dev(key, buf.ptr + at, n)
+    else:
+        buf.upload(np.frombuffer((engine.get(key) or b"")[:n], dtype=np.uint8), at)
 
 
 def keyed_bitop(engine, op: str, dest, srcs: Sequence, rank: int, world: int, coll,
                 tmp_prefix: bytes = b"__sk_bitop_src__:") -> int:
     """BITOP op dest srcs... where every key lives whole on its owner (calcSlot % world): each rank contributes the
     sources it owns to one all-gather, and dest's owner runs the local BITOP over the gathered copies (missing
-    sources are empty strings, as in Redis).  Returns the result length on every rank.  A Bloom filter union is
-    keyed_bitop("OR", ...) over the filters' names (same size and k)."""
+    sources are empty strings, as in Redis; an HLL source reads as its Redis string).  Returns the result length on
+    every rank.  A Bloom filter union is keyed_bitop("OR", ...) over the filters' names (same size and k).  SPMD:
+    a failure on any rank (reading a source, the destination's BITOP) raises on every rank (cluster.agree) instead
+    of leaving the others in a collective."""
     if op.upper() == "NOT" and len(srcs) != 1:
         raise ValueError("BITOP NOT must be called with a single source key.")
     lens = _owned_lengths(engine, srcs, rank, world, coll)
@@ -501,32 +520,47 @@ def keyed_bitop(engine, op: str, dest, srcs: Sequence, rank: int, world: int, co
                 q += max(lens[i], 0)
     d_owner = owner(dest, world)
     tmp = [tmp_prefix + b"%d" % i for i in range(len(srcs))]
-    if hasattr(coll, "allgather_dev"):        # GPUs: the operands never leave HBM
+    if hasattr(coll, "allgather_dev"):        # GPUs: bit-string operands never leave HBM
         send, recv = engine.alloc(P), engine.alloc(P * world)
-        for i in mine:
-            if lens[i] > 0:
-                engine.get_dev(srcs[i], send.ptr + base[i], lens[i])
-        coll.allgather_dev(send, recv, P)
-        if rank == d_owner:
-            for i in range(len(srcs)):
-                if lens[i] >= 0:
-                    engine.set_dev(tmp[i], recv.ptr + where[i], lens[i])
-        send.free()
-        recv.free()
+        try:
+            err = None
+            try:
+                for i in mine:
+                    if lens[i] > 0:
+                        _source_to_dev(engine, srcs[i], send, base[i], lens[i])
+            except Exception as e:  # noqa: BLE001 - agreed on below
+                err = e
+            agree(coll, err)
+            coll.allgather_dev(send, recv, P)
+            if rank == d_owner:
+                for i in range(len(srcs)):
+                    if lens[i] >= 0:
+                        engine.set_dev(tmp[i], recv.ptr + where[i], lens[i])
+        finally:
+            send.free()
+            recv.free()
     else:
-        blob = b"".join((engine.get(srcs[i]) or b"") for i in mine)
+        blob, err = b"", None
+        try:
+            blob = b"".join((engine.get(srcs[i]) or b"") for i in mine)
+        except Exception as e:  # noqa: BLE001 - agreed on below
+            err = e
+        agree(coll, err)
         parts = coll.allgather_bytes(blob)
         flat = b"".join(p + b"\0" * (P - len(p)) for p in parts)
         if rank == d_owner:
             for i in range(len(srcs)):
                 if lens[i] >= 0:
                     engine.set(tmp[i], flat[where[i]:where[i] + lens[i]])
-    n = 0
+    n, err = 0, None
     if rank == d_owner:
         try:
             n = engine.bitop(op, dest, tmp)
+        except Exception as e:  # noqa: BLE001 - agreed on below
+            err = e
         finally:
             engine.delete(tmp)
+    agree(coll, err)
     return max(coll.allgather_u64(n))
 
 

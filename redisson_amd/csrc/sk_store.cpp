@@ -1819,9 +1819,6 @@ int sk_hll_histogram_dev(sk_ctx *c, uint64_t n, const uint32_t *d_ids, uint32_t 
     return sync(c);
 }
 
-// Estimates of many single-key counts: exact-sum histograms (every register
-// < 40, and every redis >= 5 estimate) in parallel threads, the rest (the
-// register-order sum needs a register readback) in order afterwards.
 // Single-key counts under the 3.x estimator from the device's exact register sums (k_hll_sum): E = S * 2^-40 when
 // no register is >= 40 (bit-identical to hllDenseSum, see the kernel), else Redis's register-order sum.
 static int estimate_many_sums(sk_ctx *c, uint64_t n, const uint64_t *s2, const uint32_t *ids, int64_t *out) {
@@ -1861,6 +1858,9 @@ int hll_sums(sk_ctx *c, uint64_t n, const uint32_t *d_ids, std::vector<uint64_t>
     return sync(c);
 }
 
+// Estimates of many single-key counts from 64-bin histograms: exact-sum histograms (every register < 40, and every
+// redis >= 5 estimate) in parallel threads, the rest (the register-order sum needs a register readback) in order
+// afterwards.
 static int estimate_many(sk_ctx *c, uint64_t n, const uint32_t *h, const uint32_t *ids, int64_t *out) {
     std::vector<uint8_t> slow(n, 0);
     auto work = [&](uint64_t i0, uint64_t i1) {

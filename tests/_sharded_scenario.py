@@ -84,6 +84,27 @@ def run_scenario(engine, rank, world, coll):
         res[op] = (n, val)
     out["keyed"] = res
 
+    # a failure on one rank only (the owner of KEYS[0] cannot read its length) raises on every rank instead of
+    # leaving the other ranks in the next collective (cluster.agree)
+    class _FailOn:
+        def __init__(self, e, key):
+            self.e, self.key = e, key
+
+        def __getattr__(self, a):
+            return getattr(self.e, a)
+
+        def strlen(self, k):
+            if bytes(k) == self.key:
+                raise RuntimeError("injected strlen failure")
+            return self.e.strlen(k)
+
+    try:
+        keyed_bitop(_FailOn(engine, KEYS[0]), "OR", b"kd:fail", KEYS[:3], rank, world, coll)
+        out["keyed_agree"] = False
+    except Exception as e:  # noqa: BLE001 - both the failing rank and the others must raise
+        out["keyed_agree"] = "injected" in str(e)
+    out["keyed_after"] = keyed_bitop(engine, "OR", b"kd:or2", KEYS[:2], rank, world, coll)   # still in step
+
     # C4: HLLs sharded by calcSlot % world, each rank adding only the keys it owns; global countWith / PFMERGE by
     # local union + u8 MAX exchange, by key names and by a cached device slab-id set (GlobalKeySet)
     from redisson_amd.cluster import GlobalKeySet, global_count_with, global_merge
@@ -165,6 +186,8 @@ def expected():
         v = O.bitop(op, [keys.get(k) for k in srcs])
         res[op] = (len(v), v if v else None)
     out["keyed"] = res
+    out["keyed_agree"] = True
+    out["keyed_after"] = len(O.bitop("OR", [keys.get(k) for k in KEYS[:2]]))
     h = O.HLLStore()
     for i, k in enumerate(HKEYS):
         h.pfadd([k] * HN[i], [[e] for e in _hll_elems(i)])
@@ -194,7 +217,8 @@ def check(got, want, rank, world):
     for k in ("set_a", "set_b", "clear_a", "get_a"):
         assert [int(x) for x in got[k]] == [int(x) for x in want[k]], k
     for k in ("card", "len", "size", "bytes_a", "and", "or", "xor", "not_b", "card_not_b", "bloom_add",
-              "bloom_contains", "count_with", "count_with_ids", "count_with_late", "id_set_cached"):
+              "bloom_contains", "count_with", "count_with_ids", "count_with_late", "id_set_cached", "keyed_agree",
+              "keyed_after"):
         assert got[k] == want[k], k
     if owner(b"hk:dest", world) == rank:
         np.testing.assert_array_equal(got["merge_dest"], want["merge_dest"])

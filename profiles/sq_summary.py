@@ -25,7 +25,8 @@ CUS, SIMDS = 256, 1024
 
 def main(d, tag, stats_csv, clock_ghz=2.1):
     means = {}
-    for f in sorted(sum((glob.glob(os.path.join(x, "*", "pmc_means.json")) for x in d.split(",")), [])):
+    # directories in the given order, later ones overriding a counter both collected (the newer build's pass last)
+    for f in sum((sorted(glob.glob(os.path.join(x, "*", "pmc_means.json"))) for x in d.split(",")), []):
         for k, cs in json.load(open(f)).items():
             means.setdefault(k, {}).update({c: v for c, v in cs.items() if c != "dispatches"})
     dur = {}

@@ -73,9 +73,7 @@ hipError_t launch_pfl_apply(hipStream_t st, const PflDims &d, const uint64_t *re
                             uint8_t *arena, uint8_t *changed, uint32_t *big_alloc, uint64_t *big_keys,
                             uint32_t *big_vals, int flags, // flags & 32: replies pre-filled, only others stored
                             uint32_t *order,               // u32[nf]: dispatch order (heavy fine buckets first)
-                            uint32_t *rc, uint32_t par,
-                            void *rt);                     // pfl_rt_bytes(d): the fine-bucket-major run table
-uint64_t pfl_rt_bytes(const PflDims &d);
+                            uint32_t *rc, uint32_t par);
 hipError_t sort_keys_size(uint64_t n, unsigned begin_bit, unsigned end_bit, size_t *bytes);
 hipError_t sort_keys(hipStream_t st, void *tmp, size_t tmp_bytes, const uint64_t *in, uint64_t *out, uint64_t n,
                      unsigned begin_bit, unsigned end_bit);
@@ -109,6 +107,7 @@ uint32_t ra_blocks(uint64_t n);
 uint32_t ra_regions(uint64_t size);
 uint64_t ra_piece();
 uint64_t ra_chunk_words(int k);
+uint32_t ra_max_probes();
 hipError_t launch_bloom_ra_hash(hipStream_t st, uint64_t n, const uint64_t *off, const uint8_t *bytes, uint64_t size,
                                 uint64_t magic, int k, uint32_t *S, uint32_t *recs, uint32_t *stop, uint32_t piece);
 hipError_t launch_bloom_ra_apply(hipStream_t st, uint64_t n, uint64_t size, int k, const uint32_t *S,

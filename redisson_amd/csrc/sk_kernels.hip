@@ -931,6 +931,9 @@ __global__ void __launch_bounds__(SK_PFP_ATPB) __attribute__((amdgpu_waves_per_e
 #endif
 #define SK_PFL_MAXSUB 8192 // fine buckets per coarse bucket (2^20 sketches)
 #define SK_PFL_TMAX 1024   // largest run tile (hash blocks): one segment per region thread
+#ifndef SK_PFL_LF
+#define SK_PFL_LF 0        // 1: the apply issues its register lines before the run table (speculative)
+#endif
 #ifndef SK_PFL_NTMAX
 #define SK_PFL_NTMAX 64    // most tiles per call (the apply's run table; 5 apply workgroups per CU need <= 32 KiB of LDS)
 #endif
@@ -1201,34 +1204,23 @@ __device__ __forceinline__ void pfl_chunk(const uint64_t *R, uint32_t cnt, uint1
         }
 }
 
-// The run table, fine-bucket major: RT[f * ntile + t] = the rec2 start of fine bucket f's run in tile t | the records of
-// f in tiles before t << 32, FC[f] = f's records.  The apply reads its row as one contiguous piece (296 B at 37 tiles)
-// instead of 2 x ntile scattered words of the region-major C2 (one line each), and learns its count from one word.
 // Heavy fine buckets first: the apply's grid starts with hmax "heavy slots"; the plan lists the fine buckets of more
 // than one chunk (C1, a Zipf head's lines -- they run longest) in order[0..H), H = ctr[0], and heavy slot k applies
 // order[k].  The rest of the grid is the fine buckets in their own order; a heavy one there exits at once.  A
-// uniform call has H = 0: its heavy slots exit and nothing else is indirected.  hmax = 0: no heavy slots.
-__global__ void __launch_bounds__(256) k_pfl_plan(const uint32_t *__restrict__ C2, const uint32_t *__restrict__ rbase,
-                                                  uint32_t ntile, uint32_t nsub, uint32_t nf, uint32_t hmax,
-                                                  uint32_t *ctr, uint32_t *__restrict__ order,
-                                                  uint64_t *__restrict__ RT, uint32_t *__restrict__ FC) {
+// uniform call has H = 0: its heavy slots exit and nothing else is indirected.
+__global__ void __launch_bounds__(256) k_pfl_plan(const uint32_t *__restrict__ C2, uint32_t ntile, uint32_t nsub,
+                                                  uint32_t nf, uint32_t hmax, uint32_t *ctr,
+                                                  uint32_t *__restrict__ order) {
     __shared__ uint32_t wsum[256 / 64], base;
     const uint32_t f = blockIdx.x * 256 + threadIdx.x;
     uint32_t cnt = 0;
     if (f < nf) {
         const uint32_t b = f / nsub, sub = f % nsub;
-        uint64_t *row = RT + uint64_t(f) * ntile;
-#pragma unroll 4
         for (uint32_t t = 0; t < ntile; t++) {
-            const uint32_t g = b * ntile + t;
-            const uint32_t *c = C2 + uint64_t(g) * (nsub + 1) + sub;
-            const uint32_t c0 = c[0];
-            row[t] = uint64_t(rbase[g] + c0) | (uint64_t(cnt) << 32);
-            cnt += c[1] - c0;
+            const uint32_t *c = C2 + uint64_t(b * ntile + t) * (nsub + 1) + sub;
+            cnt += c[1] - c[0];
         }
-        FC[f] = cnt;
     }
-    if (!hmax) return; // uniform
     const bool heavy = cnt > SK_PFL_CAP;
     uint32_t th;
     const uint32_t ph = block_exscan<256>(heavy ? 1u : 0u, wsum, &th);
@@ -1238,8 +1230,8 @@ __global__ void __launch_bounds__(256) k_pfl_plan(const uint32_t *__restrict__ C
 }
 
 __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const uint64_t *__restrict__ rec2,
-                                                           const uint64_t *__restrict__ RT,
-                                                           const uint32_t *__restrict__ FC, uint32_t ntile,
+                                                           const uint32_t *__restrict__ rbase,
+                                                           const uint32_t *__restrict__ C2, uint32_t ntile,
                                                            uint32_t nsub, uint32_t sh, PflPerm pm, uint32_t nslab,
                                                            uint8_t *arena,
                                                            uint8_t *__restrict__ changed, uint32_t *big_alloc,
@@ -1270,36 +1262,39 @@ __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const uint64_t *__res
     } else {
         f = blockIdx.x - hmax;
     }
-    const uint32_t cnt = FC[f]; // uniform
-    if (cnt == 0) return;
-    if (hmax && blockIdx.x >= hmax && cnt > SK_PFL_CAP) return; // applied by a heavy slot
     const uint32_t b = f / nsub, sub = f % nsub;
     const uint32_t slab0 = sub << sh, nsl = 1u << sh; // permuted ids slab0 + i, i < nsl
     auto line = [&](uint32_t i) -> uint4 * {
         const uint32_t s = pm.inv(slab0 + i);
         return reinterpret_cast<uint4 *>(arena + (uint64_t(s) << 14) + (((b - pfl_rot(s)) & (SK_PFL_NB - 1)) << SK_PFL_LB));
     };
-    // a one-chunk bucket's lines are issued first: they do not depend on the run table
     constexpr int LQ = (NL * LW + SK_PFL_ATPB - 1) / SK_PFL_ATPB;
     uint4 lv[LQ];
-    if (cnt <= SK_PFL_CAP) {
+    auto load_lines = [&] {
 #pragma unroll
         for (int j = 0; j < LQ; j++) {
             const uint32_t q = threadIdx.x + j * SK_PFL_ATPB;
             if (q < nsl * LW && pm.inv(slab0 + q / LW) < nslab)
                 lv[j] = (probe & 4) ? make_uint4(0, 0, 0, 0) : line(q / LW)[q % LW];
         }
-    }
-    uint32_t ex = 0, len = 0;
+    };
+#if SK_PFL_LF
+    load_lines(); // speculative: issued before the run table, used when the bucket turns out to be one chunk
+#endif
+    uint32_t st = 0, len = 0;
     if (threadIdx.x < ntile) {
-        const uint64_t *row = RT + uint64_t(f) * ntile;
-        const uint64_t e0 = row[threadIdx.x];
-        const uint32_t nx = threadIdx.x + 1 < ntile ? uint32_t(row[threadIdx.x + 1] >> 32) : cnt;
-        ex = uint32_t(e0 >> 32);
-        len = nx - ex;
-        rs[threadIdx.x] = uint32_t(e0);
-        rp[threadIdx.x] = ex;
+        const uint32_t g = b * ntile + threadIdx.x;
+        const uint32_t *c = C2 + uint64_t(g) * (nsub + 1) + sub;
+        const uint32_t c0 = c[0];
+        st = rbase[g] + c0;
+        len = c[1] - c0;
+        rs[threadIdx.x] = st;
     }
+    uint32_t cnt;
+    const uint32_t ex = block_exscan<SK_PFL_ATPB>(len, wsum, &cnt);
+    if (cnt == 0) return; // uniform
+    if (hmax && blockIdx.x >= hmax && cnt > SK_PFL_CAP) return; // applied by a heavy slot
+    if (threadIdx.x < ntile) rp[threadIdx.x] = ex;
     if (probe & 256) return; // dev ablation: run table only
     // record u of the fine bucket (u < cnt): run t with rp[t] <= u < rp[t + 1].  A one-chunk bucket reads t from
     // run_of[u] (filled below, one LDS read per record); chunked buckets search rp (fixed steps, no branches)
@@ -1335,7 +1330,10 @@ __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const uint64_t *__res
         s_ones = 0;
     }
     __syncthreads();
-    if (cnt <= SK_PFL_CAP) { // the whole fine bucket is one chunk: records loaded while the lines are in flight
+    if (cnt <= SK_PFL_CAP) { // the whole fine bucket is one chunk: records and lines in one round trip
+#if !SK_PFL_LF
+        load_lines();
+#endif
         constexpr int RU = SK_PFL_CAP / SK_PFL_ATPB; // every record load in flight at once
         uint64_t rv[RU];
 #pragma unroll
@@ -1883,16 +1881,23 @@ __global__ void __launch_bounds__(256) k_bloom_contains_q(uint64_t n, const uint
 #define RC_PMAX 8                     // probes per element handled here (k <= 9)
 #define RC_NRMAX 4096                 // regions (bit arrays <= 2^32 bits)
 #define RC_ROUNDS (RC_EPB / RC_TPB)
-#define RA_EPB 2048                   // add: elements per hash block (11-bit element-in-block, 1-bit last probe)
+#ifndef RA_EPB
+#define RA_EPB 2048                   // add: elements per hash block (element-in-block < 4096, 1-bit last probe)
+#endif
+#ifndef RA_PMAX
+#define RA_PMAX RC_PMAX               // add: probes per element handled here (k <= RA_PMAX)
+#endif
+#define RA_EB (RA_EPB == 4096 ? 12 : 11) // log2 RA_EPB
 #define RA_RB 19                      // add: region = 2^19 bits = 64 KiB (the apply keeps a window of records too)
 #define RA_NRMAX 8192
-#define RA_BUFW 12288                 // add: u64 words: two key windows, then the block's records (RA_EPB*RC_PMAX u32)
+#define RA_BUFW (RA_EPB * RA_PMAX / 2 > 2 * SK_PFP_WIN ? RA_EPB * RA_PMAX / 2 : 2 * SK_PFP_WIN) // add: u64 words:
+                                      // two key windows, then the block's records (RA_EPB * RA_PMAX u32)
 #define RA_SEGMAX 512                 // add: longest (block, region) segment the apply's windows take
 #define RC_BUFW 16384                 // u64 words: two key windows, then the block's records (RC_EPB*RC_PMAX u32)
 static_assert(2 * SK_PFP_WIN <= RC_BUFW && RC_EPB * RC_PMAX * 4 <= RC_BUFW * 8, "hash block LDS");
 static_assert(RC_EPB * RC_PMAX < 65536, "segment starts/counts are u16");
-static_assert(RA_EPB * 2 <= 8192 && RA_EPB % RC_TPB == 0, "add records: bit << 13 | element << 1 | last");
-static_assert(2 * SK_PFP_WIN <= RA_BUFW && RA_EPB * RC_PMAX * 4 <= RA_BUFW * 8, "add hash block LDS");
+static_assert((RA_EPB == 2048 || RA_EPB == 4096) && RA_EPB % RC_TPB == 0, "add records: bit << 13 | element << 1 | last");
+static_assert(2 * SK_PFP_WIN <= RA_BUFW && RA_EPB * RA_PMAX * 4 <= RA_BUFW * 8 && RA_PMAX <= RC_PMAX, "add hash block LDS");
 static_assert(RC_TPB == SK_PFP_TPB, "key windows sized for SK_PFP_TPB threads");
 
 template <bool ADD>
@@ -1964,7 +1969,7 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_rc_hash(uint64_t n, const uint
             if (!ADD) out[i] = 1;
             BloomIdx bi(h1, h2, size, magic);
 #pragma unroll
-            for (int p = 0; p < RC_PMAX; p++) {
+            for (int p = 0; p < (ADD ? RA_PMAX : RC_PMAX); p++) {
                 if (uint32_t(p) >= P) break;
                 uint32_t idx = uint32_t(bi.r);
                 ix[e][p] = idx;
@@ -2142,7 +2147,7 @@ static_assert(RA_CAP >= 2 * RA_SEGMAX && RA_CAP % RC_TPB == 0 && RA_CAP < 0xffff
 static_assert(RA_JPT * RC_TPB <= 65536, "block numbers: u16 in the window, 16 bits of the order key");
 
 __device__ __forceinline__ uint32_t ra_mask(uint32_t b) { return (0x80u >> (b & 7u)) << (((b >> 3) & 3u) * 8u); }
-__device__ __forceinline__ uint32_t ra_key(uint32_t blk, uint32_t x) { return (blk << 11) | ((x >> 1) & 0x7ffu); }
+__device__ __forceinline__ uint32_t ra_key(uint32_t blk, uint32_t x) { return (blk << RA_EB) | ((x >> 1) & (RA_EPB - 1)); }
 
 __global__ void __launch_bounds__(RC_TPB) k_bloom_ra_apply(uint32_t NB, uint32_t NR, const uint32_t *__restrict__ S,
                                                            const uint32_t *__restrict__ chunks, uint32_t P,
@@ -2278,7 +2283,7 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_ra_apply(uint32_t NB, uint32_t
             }
             if (!f) continue;
             first |= 1u << q;
-            if (!(xu & 1u)) out[uint64_t(blk[u]) * RA_EPB + ((xu >> 1) & 0x7ffu)] = 1;
+            if (!(xu & 1u)) out[uint64_t(blk[u]) * RA_EPB + ((xu >> 1) & (RA_EPB - 1))] = 1;
         }
         __syncthreads(); // every probe of the window has read the bits
 #pragma unroll 1
@@ -2946,22 +2951,20 @@ hipError_t launch_pfl_fill(hipStream_t st, uint8_t *changed, uint64_t n, uint32_
     return hipSuccess;
 }
 
-uint64_t pfl_rt_bytes(const PflDims &d) { return ((d.nf * 4 + 15) & ~uint64_t(15)) + d.nf * d.ntile * 8; }
-
 hipError_t launch_pfl_apply(hipStream_t st, const PflDims &d, const uint64_t *rec2, const uint32_t *C, uint32_t nslab,
                             uint8_t *arena, uint8_t *changed, uint32_t *big_alloc, uint64_t *big_keys,
-                            uint32_t *big_vals, int flags, uint32_t *order, uint32_t *rc, uint32_t par, void *rt) {
+                            uint32_t *big_vals, int flags, uint32_t *order, uint32_t *rc, uint32_t par) {
     static const int probe_flags = getenv("SK_PFL_PROBE") ? atoi(getenv("SK_PFL_PROBE")) : 0; // dev ablations
     const uint32_t *rbase = C + d.nreg, *C2 = C + 2 * d.nreg;
-    uint32_t *FC = static_cast<uint32_t *>(rt);
-    uint64_t *RT = reinterpret_cast<uint64_t *>(static_cast<uint8_t *>(rt) + ((d.nf * 4 + 15) & ~uint64_t(15)));
     // heavy slots: at most n / (CAP + 1) fine buckets hold more than one chunk
     const uint32_t hmax = order ? uint32_t(std::min<uint64_t>(d.nf, uint64_t(d.nblk) * SK_PFP_EPB / (SK_PFL_CAP + 1)))
                                 : 0u;
-    hipLaunchKernelGGL(k_pfl_plan, dim3(uint32_t((d.nf + 255) / 256)), dim3(256), 0, st, C2, rbase, d.ntile, d.nsub,
-                       uint32_t(d.nf), hmax, big_alloc + 1, order, RT, FC);
-    SK_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_pfl_apply, dim3(uint32_t(d.nf) + hmax), dim3(SK_PFL_ATPB), 0, st, rec2, RT, FC, d.ntile,
+    if (order) {
+        hipLaunchKernelGGL(k_pfl_plan, dim3(uint32_t((d.nf + 255) / 256)), dim3(256), 0, st, C2, d.ntile, d.nsub,
+                           uint32_t(d.nf), hmax, big_alloc + 1, order);
+        SK_LAUNCH_CHECK();
+    }
+    hipLaunchKernelGGL(k_pfl_apply, dim3(uint32_t(d.nf) + hmax), dim3(SK_PFL_ATPB), 0, st, rec2, rbase, C2, d.ntile,
                        d.nsub, d.sh, PflPerm{d.pa, d.pai, d.pm_mask, d.nslab}, nslab, arena, changed, big_alloc,
                        big_keys, big_vals, flags | probe_flags, hmax, big_alloc + 1, order, rc, par);
     SK_LAUNCH_CHECK();
@@ -3096,6 +3099,7 @@ uint32_t ra_blocks(uint64_t n) { return uint32_t((n + RA_EPB - 1) / RA_EPB); }
 uint32_t ra_regions(uint64_t size) { return uint32_t((size + (1ull << RA_RB) - 1) >> RA_RB); }
 uint64_t ra_piece() { return uint64_t(RA_JPT) * RC_TPB * RA_EPB; }
 uint64_t ra_chunk_words(int k) { return uint64_t(RA_EPB) * uint64_t(k); }
+uint32_t ra_max_probes() { return RA_PMAX; }
 
 // Bloom add, region schedule: records u32[ra_blocks(n) * ra_chunk_words(k)], S u32[regions * blocks], *flag = 0 before
 hipError_t launch_bloom_ra_hash(hipStream_t st, uint64_t n, const uint64_t *off, const uint8_t *bytes, uint64_t size,

@@ -301,7 +301,7 @@ struct sk_ctx {
     uint32_t pfl_tile = 0;      // hash blocks per run tile (SK_PFL_TILE, 0 = the kernel default)
     bool pfl_zero = true;       // replies pre-zeroed, the apply stores only the 1s (SK_PFL_ZERO)
     bool pfl_plan = true;       // heavy fine buckets dispatched first (SK_PFL_PLAN)
-    DBuf pfl_chunks, pfl_S, pfl_C, pfl_rec, pfl_bk, pfl_bv, pfl_ovf, pfl_order, pfl_rt;
+    DBuf pfl_chunks, pfl_S, pfl_C, pfl_rec, pfl_bk, pfl_bv, pfl_ovf, pfl_order;
     DBuf pfl_rc;                // u32[32]: reply-mix counters that pick each call's reply default (two parities)
     uint32_t pfl_par = 0;       // this call's parity
 };
@@ -1093,7 +1093,6 @@ int pfadd_lines(sk_ctx *c, uint64_t n, const uint32_t *d_ids, const uint64_t *d_
     HIPCHK(c, c->pfl_bv.ensure(2 * n * 4));
     HIPCHK(c, c->pfl_ovf.ensure(64));
     HIPCHK(c, c->pfl_order.ensure(d.nf * 4));
-    HIPCHK(c, c->pfl_rt.ensure(sk::pfl_rt_bytes(d)));
     if (!c->pfl_rc.p) { // first call: no reply mix yet (default 0)
         HIPCHK(c, c->pfl_rc.ensure(32 * 4));
         HIPCHK(c, hipMemsetAsync(c->pfl_rc.p, 0, 32 * 4, c->st));
@@ -1115,7 +1114,7 @@ int pfadd_lines(sk_ctx *c, uint64_t n, const uint32_t *d_ids, const uint64_t *d_
                                    d_changed, c->pfl_ovf.as<uint32_t>(), c->pfl_bk.as<uint64_t>(),
                                    c->pfl_bv.as<uint32_t>(), c->pfl_zero ? 32 : 0,
                                    c->pfl_plan ? c->pfl_order.as<uint32_t>() : nullptr, c->pfl_rc.as<uint32_t>(),
-                                   par, c->pfl_rt.p)); }
+                                   par)); }
     if (getenv("SK_PFL_DEBUG")) { // dev: table entries the oversized runs took (2 per record of a min-seq table run)
         uint32_t big = 0;
         HIPCHK(c, hipMemcpyAsync(&big, c->pfl_ovf.p, 4, hipMemcpyDeviceToHost, c->st));
@@ -1328,7 +1327,7 @@ int sk_close(sk_ctx *c) {
                     &c->hist_a, &c->hist_b, &c->ovf, &c->bloom_h, &c->rc_S, &c->rc_rec, &c->long_h,
                     &c->long_which, &c->long_plane, &c->long_flags, &c->ra_S, &c->ra_rec, &c->ra_flag, &c->ev, &c->ev_n,
                     &c->pfl_chunks, &c->pfl_S, &c->pfl_C, &c->pfl_rc, &c->rt_cnt, &c->pfl_rec, &c->pfl_bk, &c->pfl_bv,
-                    &c->pfl_ovf, &c->pfl_order, &c->pfl_rt})
+                    &c->pfl_ovf, &c->pfl_order})
         b->release();
     for (auto &ps : c->pfs) {
         for (DBuf *b : {&ps.chunks, &ps.rep, &ps.S, &ps.big_k, &ps.big_v, &ps.ovf}) b->release();
@@ -2726,14 +2725,14 @@ static int bloom_add_sorted(sk_ctx *c, uint32_t id, int64_t size, int32_t k, uin
 // schedule (sk_kernels.hip "Bloom add, region schedule") in pieces of <= ra_piece() elements, all enqueued without
 // a host wait; a hash pass that finds a segment longer than RA_SEGMAX (one element repeated hundreds of times in a
 // block) lowers the device word `stop` to its piece number, every apply from that piece on does nothing, and the
-// host -- one read at the end -- redoes those pieces on the sort path in order.  k > rc_max_probes() takes the
+// host -- one read at the end -- redoes those pieces on the sort path in order.  k > ra_max_probes() takes the
 // sort path whole.
 static int bloom_add_device(sk_ctx *c, uint32_t id, int64_t size, int32_t k, uint64_t n, const uint64_t *d_off,
                             const uint8_t *d_bytes, uint8_t *d_out) {
     if (!n) return SK_OK;
     HIPCHK(c, hipMemsetAsync(d_out, 0, n, c->st));
     const uint64_t usize = uint64_t(size);
-    if (!(c->bloom_ra_min && n >= c->bloom_ra_min && k >= 1 && uint32_t(k) <= sk::rc_max_probes()))
+    if (!(c->bloom_ra_min && n >= c->bloom_ra_min && k >= 1 && uint32_t(k) <= sk::ra_max_probes()))
         return bloom_add_sorted(c, id, size, k, n, d_off, d_bytes, d_out);
     const uint64_t magic = magic_for(usize), piece = sk::ra_piece();
     const uint64_t nb = sk::ra_blocks(std::min(n, piece)), nr = sk::ra_regions(usize);

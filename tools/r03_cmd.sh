@@ -1,8 +1,13 @@
 set -o pipefail
-mkdir -p gpurun_out/r03a
-timeout -k 10 900 python3 -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests/test_gpu_lines.py tests/test_gpu_region.py tests/test_full_size.py tests/test_gpu_parity.py tests/test_distributed.py -k "lines or region or full or long or engine or rccl or route" > gpurun_out/r03a/tests.log 2>&1 || { echo TESTS FAILED; tail -30 gpurun_out/r03a/tests.log; exit 1; }
-tail -2 gpurun_out/r03a/tests.log
-bash tools/gpu_ab.sh r03a "h0 base pf2 ra16" "--steps 5 --warmup 1 --no-cpu-baseline --add-chunk 33554432" || exit 1
-bash tools/r03_lds.sh r03lds || exit 1
-timeout -k 10 600 python3 -u bench_configs.py > gpurun_out/r03a/configs.jsonl 2> gpurun_out/r03a/configs.err || { echo configs failed; tail -5 gpurun_out/r03a/configs.err; exit 1; }
+O=gpurun_out/r03c; mkdir -p $O
+T="python3 -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu"
+timeout -k 10 900 $T tests/test_gpu_lines.py tests/test_gpu_region.py tests/test_full_size.py tests/test_gpu_parity.py -k "lines or region or full or long" > $O/tests.log 2>&1 || { echo TESTS FAILED; tail -30 $O/tests.log; exit 1; }
+tail -1 $O/tests.log
+SK_LIB_PATH=$PWD/redisson_amd/var_ra4k.so timeout -k 10 600 $T tests/test_gpu_region.py tests/test_full_size.py -k "region or c3" > $O/tests_ra4k.log 2>&1 || { echo RA4K TESTS FAILED; tail -30 $O/tests_ra4k.log; exit 1; }
+tail -1 $O/tests_ra4k.log
+SK_LIB_PATH=$PWD/redisson_amd/var_lf.so timeout -k 10 600 $T tests/test_gpu_lines.py > $O/tests_lf.log 2>&1 || { echo LF TESTS FAILED; tail -30 $O/tests_lf.log; exit 1; }
+tail -1 $O/tests_lf.log
+bash tools/gpu_ab.sh r03c "h0 base lf ra4k" "--steps 5 --warmup 1 --no-cpu-baseline --add-chunk 33554432" || exit 1
+SK_HOST_TIMING=1 timeout -k 10 300 python3 -u bench_configs.py --configs host > $O/host.jsonl 2> $O/host.err || { echo host failed; tail -5 $O/host.err; exit 1; }
+SK_STAGE=1 timeout -k 10 300 python3 -u bench_configs.py --configs host > $O/host_stage.jsonl 2> $O/host_stage.err || { echo host2 failed; tail -5 $O/host_stage.err; exit 1; }
 echo all done

@@ -2142,6 +2142,12 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_rc_probe(uint32_t NB, uint32_t
 #define RA_JPT 4      // blocks per thread (block j = q * RC_TPB + thread): pieces of <= 4096 blocks (8 M elements)
 #endif
 #define RA_NONE 0xffffffffu
+#ifndef RA_GQ
+#define RA_GQ 8       // record loads in flight per thread in a window's gather (RA_RPT: all of them)
+#endif
+#ifndef RA_SKIPSET
+#define RA_SKIPSET 1  // records on bits already set are not chained
+#endif
 #define RA_RPT (RA_CAP / RC_TPB)
 static_assert(RA_CAP >= 2 * RA_SEGMAX && RA_CAP % RC_TPB == 0 && RA_CAP < 0xffff, "windows: u16 links");
 static_assert(RA_JPT * RC_TPB <= 65536, "block numbers: u16 in the window, 16 bits of the order key");
@@ -2248,19 +2254,23 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_ra_apply(uint32_t NB, uint32_t
         __syncthreads();
         const uint32_t nw = base == RA_NONE ? 0u : wend - base; // <= W + RA_SEGMAX = RA_CAP
 #pragma unroll 1
-        for (uint32_t g = 0; g < RA_RPT; g += 4) { // this thread's records of the window, 4 loads in flight
-            uint32_t x[4];
+        for (uint32_t g = 0; g < RA_RPT; g += RA_GQ) { // this thread's records of the window, RA_GQ loads in flight
+            uint32_t x[RA_GQ];
 #pragma unroll
-            for (uint32_t q = 0; q < 4; q++) {
+            for (uint32_t q = 0; q < RA_GQ; q++) {
                 const uint32_t u = threadIdx.x + (g + q) * RC_TPB;
                 x[q] = u < nw ? chunks[rec[u]] : 0u;
             }
 #pragma unroll
-            for (uint32_t q = 0; q < 4; q++) {
+            for (uint32_t q = 0; q < RA_GQ; q++) {
                 const uint32_t u = threadIdx.x + (g + q) * RC_TPB;
                 if (u < nw) {
                     rec[u] = x[q];
-                    nxt[u] = uint16_t(atomicExch(&head[(x[q] >> 13) & (RA_HT - 1)], u));
+                    const uint32_t b = x[q] >> 13;
+                    // a record on a bit already set (before the batch or by an earlier window) is never a setter, and
+                    // a record on an unset bit only looks for smaller keys on its own bit: it stays off the chains
+                    if (RA_SKIPSET && dense && (filt[b >> 5] & ra_mask(b))) nxt[u] = 0xffffu;
+                    else nxt[u] = uint16_t(atomicExch(&head[b & (RA_HT - 1)], u));
                 }
             }
         }

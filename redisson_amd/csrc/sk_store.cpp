@@ -11,7 +11,10 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <functional>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -24,11 +27,93 @@
 #include <vector>
 
 #include <rccl/rccl.h>
+#include <unistd.h>
 
 #include "../../include/redisson_sketch.h"
 #include "sk_internal.h"
 
 namespace {
+
+// Host worker threads, started once per process.  The host passes that run on every large call (handle liveness
+// checks, directory lookups, estimator tails, staging copies) used to spawn and join up to 16 std::threads per call
+// (~20-50 us each); the pool keeps them parked on a condition variable.  run(parts, fn) calls fn(0..parts-1) on the
+// workers and the caller and returns when all are done; one parallel section at a time (contexts share the pool).
+class HostPool {
+  public:
+    static HostPool &get() {
+        // never destroyed: parked workers end with the process.  A forked child has none of the parent's threads,
+        // so it starts its own pool.
+        static std::mutex m;
+        static HostPool *p = nullptr;
+        static pid_t pid = 0;
+        std::lock_guard<std::mutex> l(m);
+        if (!p || pid != getpid()) {
+            p = new HostPool();
+            pid = getpid();
+        }
+        return *p;
+    }
+    unsigned threads() const { return unsigned(workers_.size()) + 1; }
+    void run(unsigned parts, const std::function<void(unsigned)> &fn) {
+        if (parts <= 1 || workers_.empty()) {
+            for (unsigned t = 0; t < parts; t++) fn(t);
+            return;
+        }
+        std::lock_guard<std::mutex> one(run_mu_);
+        {
+            std::lock_guard<std::mutex> l(mu_);
+            job_ = &fn;
+            parts_ = parts;
+            next_.store(0);
+            active_ = unsigned(workers_.size());
+            gen_++;
+        }
+        cv_.notify_all();
+        for (unsigned t; (t = next_.fetch_add(1)) < parts;) fn(t);
+        std::unique_lock<std::mutex> l(mu_);
+        done_.wait(l, [&] { return active_ == 0; });
+        job_ = nullptr;
+    }
+
+  private:
+    HostPool() {
+        unsigned T = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+        if (const char *e = getenv("OMP_NUM_THREADS")) T = std::max(1, std::min(int(T), atoi(e)));
+        for (unsigned i = 1; i < T; i++) workers_.emplace_back([this] { loop(); });
+        for (auto &w : workers_) w.detach();
+    }
+    void loop() {
+        uint64_t seen = 0;
+        for (;;) {
+            std::unique_lock<std::mutex> l(mu_);
+            cv_.wait(l, [&] { return gen_ != seen; });
+            seen = gen_;
+            const std::function<void(unsigned)> *j = job_;
+            const unsigned P = parts_;
+            l.unlock();
+            for (unsigned t; (t = next_.fetch_add(1)) < P;) (*j)(t);
+            l.lock();
+            if (--active_ == 0) done_.notify_one();
+        }
+    }
+    std::vector<std::thread> workers_;
+    std::mutex run_mu_, mu_;
+    std::condition_variable cv_, done_;
+    const std::function<void(unsigned)> *job_ = nullptr;
+    unsigned parts_ = 0, active_ = 0;
+    std::atomic<unsigned> next_{0};
+    uint64_t gen_ = 0;
+};
+// parallel for over [0, n) in `parts` contiguous ranges (parts = the pool's threads unless n is small)
+void host_for(uint64_t n, uint64_t min_per_thread, const std::function<void(uint64_t, uint64_t)> &fn) {
+    HostPool &p = HostPool::get();
+    const unsigned T = n >= 2 * min_per_thread ? unsigned(std::min<uint64_t>(p.threads(), n / min_per_thread)) : 1u;
+    if (T <= 1) {
+        fn(0, n);
+        return;
+    }
+    p.run(T, [&](unsigned t) { fn(n * t / T, n * (t + 1) / T); });
+}
 
 constexpr uint64_t kHllBytes = 16384;
 constexpr int64_t kBloomMaxSize = 2LL * 2147483647LL; // M:RedissonBloomFilter.java:52
@@ -607,22 +692,13 @@ int stage_h2d(sk_ctx *c, void *dst, const void *src, uint64_t bytes) {
             HIPCHK(c, hipEventCreateWithFlags(&c->stage_ev[k], hipEventDisableTiming));
             HIPCHK(c, hipEventRecord(c->stage_ev[k], c->st));
         }
-    static const unsigned TT = getenv("SK_STAGE_THREADS") ? unsigned(atoi(getenv("SK_STAGE_THREADS"))) : 16u;
-    const unsigned T = std::max(1u, std::min(TT, std::thread::hardware_concurrency()));
     const uint8_t *s8 = static_cast<const uint8_t *>(src);
     uint8_t *d8 = static_cast<uint8_t *>(dst);
     for (uint64_t o = 0, p = 0; o < bytes; o += kStagePiece, p++) {
         const int k = int(p & 1);
         const uint64_t len = std::min(kStagePiece, bytes - o);
         HIPCHK(c, hipEventSynchronize(c->stage_ev[k])); // the buffer's previous copy is done
-        std::vector<std::thread> th;
-        for (unsigned t = 1; t < T; t++)
-            th.emplace_back([&, t] {
-                const uint64_t a = len * t / T, b = len * (t + 1) / T;
-                std::memcpy(c->stage[k] + a, s8 + o + a, b - a);
-            });
-        std::memcpy(c->stage[k], s8 + o, len / T);
-        for (auto &x : th) x.join();
+        host_for(len, 1u << 20, [&](uint64_t a, uint64_t b) { std::memcpy(c->stage[k] + a, s8 + o + a, b - a); });
         HIPCHK(c, hipMemcpyAsync(d8 + o, c->stage[k], len, hipMemcpyHostToDevice, c->st));
         HIPCHK(c, hipEventRecord(c->stage_ev[k], c->st));
     }
@@ -665,24 +741,17 @@ bool hll_handle_live(const sk_ctx *c, uint32_t h) {
 // index of the first handle of ids[0..n) that is not live, or n: on host threads for large batches (the check of
 // caller-cached handles must not cost more than the batch's H2D)
 uint64_t first_dead_handle(const sk_ctx *c, uint64_t n, const uint32_t *ids) {
-    const unsigned T = n >= (1u << 18) ? std::max(1u, std::min(16u, std::thread::hardware_concurrency())) : 1u;
-    std::vector<uint64_t> bad(T, n);
-    auto work = [&](unsigned t) {
-        const uint64_t i0 = n * t / T, i1 = n * (t + 1) / T;
+    std::atomic<uint64_t> bad{n};
+    host_for(n, 1u << 16, [&](uint64_t i0, uint64_t i1) {
         for (uint64_t i = i0; i < i1; i++)
             if (!hll_handle_live(c, ids[i])) {
-                bad[t] = i;
+                uint64_t cur = bad.load();
+                while (i < cur && !bad.compare_exchange_weak(cur, i)) {
+                }
                 return;
             }
-    };
-    if (T == 1) {
-        work(0);
-    } else {
-        std::vector<std::thread> th;
-        for (unsigned t = 0; t < T; t++) th.emplace_back(work, t);
-        for (auto &x : th) x.join();
-    }
-    return *std::min_element(bad.begin(), bad.end());
+    });
+    return bad.load();
 }
 
 int str_len(sk_ctx *c, uint32_t id, uint64_t *len);
@@ -1697,10 +1766,8 @@ static int pfadd_host_batch(sk_ctx *c, uint32_t n_cmds, const uint32_t *cmd_key,
 // so creation order and error text are those of the serial lookup.
 static void find_hlls_parallel(sk_ctx *c, uint32_t n, const uint64_t *key_off, const uint8_t *key_bytes,
                                uint32_t *ids, uint8_t *found) {
-    unsigned T = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-    if (const char *e = getenv("OMP_NUM_THREADS")) T = std::max(1, std::min(int(T), atoi(e)));
-    if (n < 65536 || T == 1) return;
-    auto work = [&](uint32_t i0, uint32_t i1) {
+    if (n < 65536 || HostPool::get().threads() == 1) return;
+    auto work = [&](uint64_t i0, uint64_t i1) {
         std::string k;
         for (uint32_t i = i0; i < i1; i++) {
             k.assign(reinterpret_cast<const char *>(key_bytes + key_off[i]), key_off[i + 1] - key_off[i]);
@@ -1711,11 +1778,7 @@ static void find_hlls_parallel(sk_ctx *c, uint32_t n, const uint64_t *key_off, c
             }
         }
     };
-    std::vector<std::thread> th;
-    uint32_t per = (n + T - 1) / T;
-    for (unsigned t = 1; t < T && t * per < n; t++) th.emplace_back(work, t * per, std::min<uint32_t>(n, (t + 1) * per));
-    work(0, std::min(n, per));
-    for (auto &x : th) x.join();
+    host_for(n, 4096, work);
 }
 
 int sk_pfadd(sk_ctx *c, uint32_t n_cmds, const uint64_t *key_off, const uint8_t *key_bytes,
@@ -1829,14 +1892,7 @@ static int estimate_many_sums(sk_ctx *c, uint64_t n, const uint64_t *s2, const u
             else slow[i] = 1;
         }
     };
-    unsigned T = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-    if (const char *e = getenv("OMP_NUM_THREADS")) T = std::max(1, std::min(int(T), atoi(e)));
-    if (n < 65536) T = 1;
-    std::vector<std::thread> th;
-    uint64_t per = (n + T - 1) / T;
-    for (unsigned t = 1; t < T && t * per < n; t++) th.emplace_back(work, t * per, std::min<uint64_t>(n, (t + 1) * per));
-    work(0, std::min<uint64_t>(n, per));
-    for (auto &x : th) x.join();
+    host_for(n, 32768, work);
     for (uint64_t i = 0; i < n; i++) {
         if (!slow[i]) continue;
         std::vector<uint8_t> regs(kHllBytes);
@@ -1876,14 +1932,7 @@ static int estimate_many(sk_ctx *c, uint64_t n, const uint32_t *h, const uint32_
             }
         }
     };
-    unsigned T = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-    if (const char *e = getenv("OMP_NUM_THREADS")) T = std::max(1, std::min(int(T), atoi(e)));
-    if (n < 32768) T = 1;
-    std::vector<std::thread> th;
-    uint64_t per = (n + T - 1) / T;
-    for (unsigned t = 1; t < T && t * per < n; t++) th.emplace_back(work, t * per, std::min<uint64_t>(n, (t + 1) * per));
-    work(0, std::min<uint64_t>(n, per));
-    for (auto &x : th) x.join();
+    host_for(n, 16384, work);
     for (uint64_t i = 0; i < n; i++) {
         if (!slow[i]) continue;
         int rc;
@@ -2040,14 +2089,9 @@ int sk_hll_union_keys(sk_ctx *c, uint32_t n, const uint64_t *off, const uint8_t 
     ENTER(c);
     std::vector<int32_t> own(n);
     {
-        unsigned T = n >= 65536 ? std::max(1u, std::min(16u, std::thread::hardware_concurrency())) : 1u;
-        std::vector<std::thread> th;
-        for (unsigned t = 0; t < T; t++)
-            th.emplace_back([&, t] {
-                for (uint64_t i = uint64_t(n) * t / T; i < uint64_t(n) * (t + 1) / T; i++)
-                    own[i] = sk_owner(bytes + off[i], off[i + 1] - off[i], n_gpus);
-            });
-        for (auto &x : th) x.join();
+        host_for(n, 32768, [&](uint64_t i0, uint64_t i1) {
+            for (uint64_t i = i0; i < i1; i++) own[i] = sk_owner(bytes + off[i], off[i + 1] - off[i], n_gpus);
+        });
     }
     std::vector<uint64_t> so(1, 0); // the owned keys, packed
     std::vector<uint8_t> sb;

@@ -937,7 +937,9 @@ __global__ void __launch_bounds__(SK_PFP_ATPB) __attribute__((amdgpu_waves_per_e
 #ifndef SK_PFL_NTMAX
 #define SK_PFL_NTMAX 64    // most tiles per call (the apply's run table; 5 apply workgroups per CU need <= 32 KiB of LDS)
 #endif
+#ifndef SK_PFL_LDS
 #define SK_PFL_LDS (160 * 1024 - 9 * 1024) // dynamic LDS of a region workgroup: records + fine-bucket counts
+#endif
 __device__ __forceinline__ uint32_t pfl_ht(uint64_t key) {
     static_assert((SK_PFL_HT & (SK_PFL_HT - 1)) == 0, "power-of-two chain heads");
     return uint32_t((key * 0xC2B2AE3D27D4EB4Full) >> (64 - __builtin_ctz(SK_PFL_HT)));

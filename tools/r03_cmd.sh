@@ -7,7 +7,9 @@ SK_LIB_PATH=$PWD/redisson_amd/var_ra4k.so timeout -k 10 600 $T tests/test_gpu_re
 tail -1 $O/tests_ra4k.log
 SK_LIB_PATH=$PWD/redisson_amd/var_lf.so timeout -k 10 600 $T tests/test_gpu_lines.py > $O/tests_lf.log 2>&1 || { echo LF TESTS FAILED; tail -30 $O/tests_lf.log; exit 1; }
 tail -1 $O/tests_lf.log
-bash tools/gpu_ab.sh r03c "h0 base lf ra4k ra0" "--steps 5 --warmup 1 --no-cpu-baseline --add-chunk 33554432" || exit 1
+SK_LIB_PATH=$PWD/redisson_amd/var_r2.so timeout -k 10 600 $T tests/test_gpu_lines.py > $O/tests_r2.log 2>&1 || { echo R2 TESTS FAILED; tail -30 $O/tests_r2.log; exit 1; }
+tail -1 $O/tests_r2.log
+bash tools/gpu_ab.sh r03c "h0 base lf ra4k ra0 r2" "--steps 5 --warmup 1 --no-cpu-baseline --add-chunk 33554432" || exit 1
 SK_HOST_TIMING=1 timeout -k 10 300 python3 -u bench_configs.py --configs host > $O/host.jsonl 2> $O/host.err || { echo host failed; tail -5 $O/host.err; exit 1; }
 SK_STAGE=1 timeout -k 10 300 python3 -u bench_configs.py --configs host > $O/host_stage.jsonl 2> $O/host_stage.err || { echo host2 failed; tail -5 $O/host_stage.err; exit 1; }
 echo all done

@@ -103,9 +103,9 @@ hipError_t launch_bloom_rc_hash(hipStream_t st, uint64_t n, const uint64_t *off,
 hipError_t launch_bloom_rc_probe(hipStream_t st, uint64_t n, uint64_t size, int k, const uint32_t *S,
                                  const uint32_t *recs, const uint8_t *bits, uint64_t cap_bytes, uint8_t *out);
 // Bloom add, region schedule: pieces of <= ra_piece() elements; k <= rc_max_probes()
-uint32_t ra_blocks(uint64_t n);
+uint32_t ra_blocks(uint64_t n, int k);
 uint32_t ra_regions(uint64_t size);
-uint64_t ra_piece();
+uint64_t ra_piece(int k);
 uint64_t ra_chunk_words(int k);
 uint32_t ra_max_probes();
 hipError_t launch_bloom_ra_hash(hipStream_t st, uint64_t n, const uint64_t *off, const uint8_t *bytes, uint64_t size,

@@ -1883,33 +1883,34 @@ __global__ void __launch_bounds__(256) k_bloom_contains_q(uint64_t n, const uint
 #define RC_PMAX 8                     // probes per element handled here (k <= 9)
 #define RC_NRMAX 4096                 // regions (bit arrays <= 2^32 bits)
 #define RC_ROUNDS (RC_EPB / RC_TPB)
-#ifndef RA_EPB
-#define RA_EPB 2048                   // add: elements per hash block (element-in-block < 4096, 1-bit last probe)
-#endif
-#ifndef RA_PMAX
-#define RA_PMAX RC_PMAX               // add: probes per element handled here (k <= RA_PMAX)
-#endif
-#define RA_EB (RA_EPB == 4096 ? 12 : 11) // log2 RA_EPB
+// add: elements per hash block.  4096 while the block's records (4096 x k u32) fit LDS beside the key windows and
+// the region counts (k <= RA_K4), else 2048: twice the records per (block, region) segment and half the segment
+// table -- the apply's cost is per record and per segment (C3 fill: 5.5 vs 3.9 G adds/s, r03)
+#define RA_K4 7
+__host__ __device__ constexpr uint32_t ra_bufw(uint32_t epb, uint32_t pmax) { // u64 words: two key windows, then
+    return epb * pmax / 2 > 2 * SK_PFP_WIN ? epb * pmax / 2 : 2 * SK_PFP_WIN;  // the block's records (epb x pmax u32)
+}
 #define RA_RB 19                      // add: region = 2^19 bits = 64 KiB (the apply keeps a window of records too)
 #define RA_NRMAX 8192
-#define RA_BUFW (RA_EPB * RA_PMAX / 2 > 2 * SK_PFP_WIN ? RA_EPB * RA_PMAX / 2 : 2 * SK_PFP_WIN) // add: u64 words:
-                                      // two key windows, then the block's records (RA_EPB * RA_PMAX u32)
 #define RA_SEGMAX 512                 // add: longest (block, region) segment the apply's windows take
 #define RC_BUFW 16384                 // u64 words: two key windows, then the block's records (RC_EPB*RC_PMAX u32)
 static_assert(2 * SK_PFP_WIN <= RC_BUFW && RC_EPB * RC_PMAX * 4 <= RC_BUFW * 8, "hash block LDS");
 static_assert(RC_EPB * RC_PMAX < 65536, "segment starts/counts are u16");
-static_assert((RA_EPB == 2048 || RA_EPB == 4096) && RA_EPB % RC_TPB == 0, "add records: bit << 13 | element << 1 | last");
-static_assert(2 * SK_PFP_WIN <= RA_BUFW && RA_EPB * RA_PMAX * 4 <= RA_BUFW * 8 && RA_PMAX <= RC_PMAX, "add hash block LDS");
+static_assert(4096 * 2 <= 8192, "add records: bit << 13 | element << 1 | last (element < 4096)");
+static_assert(ra_bufw(4096, RA_K4) * 8 + RA_NRMAX * 4 <= 150 * 1024 && RA_K4 <= RC_PMAX, "add hash block LDS");
 static_assert(RC_TPB == SK_PFP_TPB, "key windows sized for SK_PFP_TPB threads");
 
-template <bool ADD>
+// ADD: AEPB = the add's elements per block (4096 for k <= RA_K4, else 2048)
+template <bool ADD, uint32_t AEPB = 2048>
 __global__ void __launch_bounds__(RC_TPB) k_bloom_rc_hash(uint64_t n, const uint64_t *__restrict__ off,
                                                           const uint8_t *__restrict__ bytes, uint64_t size,
                                                           uint64_t magic, uint32_t P, uint32_t NR, uint32_t NB,
                                                           uint32_t *__restrict__ S, uint32_t *__restrict__ chunks,
                                                           uint8_t *__restrict__ out, uint32_t *__restrict__ flag,
                                                           uint32_t piece) {
-    constexpr uint32_t EPB = ADD ? RA_EPB : RC_EPB;
+    constexpr uint32_t EPB = ADD ? AEPB : RC_EPB;
+    constexpr uint32_t PM = ADD ? (AEPB == 4096 ? RA_K4 : RC_PMAX) : RC_PMAX; // probes per element held
+    static_assert(!ADD || AEPB == 2048 || AEPB == 4096, "add blocks");
     constexpr int ROUNDS = int(EPB / RC_TPB);
     constexpr uint32_t RB = ADD ? RA_RB : RC_RB, NRMAX = ADD ? RA_NRMAX : RC_NRMAX, RPT = NRMAX / RC_TPB;
     __shared__ uint32_t hist[NRMAX];
@@ -1918,7 +1919,7 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_rc_hash(uint64_t n, const uint
     const uint32_t jq = (NB + 7) / 8, jb = (blockIdx.x & 7u) * jq + (blockIdx.x >> 3);
     if (jb >= NB) return; // uniform
     __shared__ uint32_t wsum[RC_TPB / 64];
-    __shared__ uint64_t buf[ADD ? RA_BUFW : RC_BUFW];
+    __shared__ uint64_t buf[ADD ? ra_bufw(AEPB, PM) : RC_BUFW];
     uint64_t *win[2] = {buf, buf + SK_PFP_WIN};
     uint32_t *lrec = reinterpret_cast<uint32_t *>(buf); // after the last hash round
     for (uint32_t r = threadIdx.x; r < NR; r += RC_TPB) hist[r] = 0;
@@ -1971,7 +1972,7 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_rc_hash(uint64_t n, const uint
             if (!ADD) out[i] = 1;
             BloomIdx bi(h1, h2, size, magic);
 #pragma unroll
-            for (int p = 0; p < (ADD ? RA_PMAX : RC_PMAX); p++) {
+            for (int p = 0; p < int(PM); p++) {
                 if (uint32_t(p) >= P) break;
                 uint32_t idx = uint32_t(bi.r);
                 ix[e][p] = idx;
@@ -2123,7 +2124,7 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_rc_probe(uint32_t NB, uint32_t
 // ---------------------------------------------- Bloom add, region schedule
 // The add side of the region schedule (the rocPRIM sort path is left for k > RC_PMAX and for the rare piece with
 // a segment longer than RA_SEGMAX, i.e. one element repeated hundreds of times in one block):
-//   k_bloom_rc_hash<true>  as for contains, with all k probes, RA_EPB elements per block and records
+//   k_bloom_rc_hash<true>  as for contains, with all k probes, 4096 (k <= RA_K4) or 2048 elements per block, records
 //                          bit-in-region << 12 | element-in-block << 1 | (probe == k-1); a segment longer than
 //                          RA_SEGMAX raises *flag, and the host then takes the sort path for that piece.
 //   k_bloom_ra_apply       one workgroup per region.  Reference semantics (M:RedissonBloomFilter.java:94-113,
@@ -2155,8 +2156,11 @@ static_assert(RA_CAP >= 2 * RA_SEGMAX && RA_CAP % RC_TPB == 0 && RA_CAP < 0xffff
 static_assert(RA_JPT * RC_TPB <= 65536, "block numbers: u16 in the window, 16 bits of the order key");
 
 __device__ __forceinline__ uint32_t ra_mask(uint32_t b) { return (0x80u >> (b & 7u)) << (((b >> 3) & 3u) * 8u); }
-__device__ __forceinline__ uint32_t ra_key(uint32_t blk, uint32_t x) { return (blk << RA_EB) | ((x >> 1) & (RA_EPB - 1)); }
+template <uint32_t AEPB> __device__ __forceinline__ uint32_t ra_key(uint32_t blk, uint32_t x) {
+    return (blk << (AEPB == 4096 ? 12 : 11)) | ((x >> 1) & (AEPB - 1));
+}
 
+template <uint32_t AEPB>
 __global__ void __launch_bounds__(RC_TPB) k_bloom_ra_apply(uint32_t NB, uint32_t NR, const uint32_t *__restrict__ S,
                                                            const uint32_t *__restrict__ chunks, uint32_t P,
                                                            uint8_t *bits, uint64_t cap_bytes,
@@ -2187,7 +2191,7 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_ra_apply(uint32_t NB, uint32_t
             if (!ok) t[q] = make_uint4(0, 0, 0, 0);
         }
     }
-    const uint32_t CH = RA_EPB * P; // words per block chunk (NB * CH < 2^32: pieces of <= 16 M elements)
+    const uint32_t CH = AEPB * P; // words per block chunk (NB * CH < 2^32: pieces of <= 16 M elements)
     uint32_t sg[RA_JPT], pre[RA_JPT], total = 0;
 #pragma unroll
     for (int q = 0; q < RA_JPT; q++) {
@@ -2287,15 +2291,15 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_ra_apply(uint32_t NB, uint32_t
             const uint32_t w = dense ? filt[b >> 5]
                                      : __hip_atomic_load(gw + (b >> 5), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (w & ra_mask(b)) continue; // set before this probe: not a setter
-            const uint32_t key = ra_key(blk[u], xu);
+            const uint32_t key = ra_key<AEPB>(blk[u], xu);
             bool f = true;
             for (uint32_t v = head[b & (RA_HT - 1)]; v < RA_CAP && f; v = nxt[v]) { // RA_NONE / 0xffff end a chain
                 const uint32_t xv = rec[v];
-                if ((xv >> 13) == b && ra_key(blk[v], xv) < key) f = false;
+                if ((xv >> 13) == b && ra_key<AEPB>(blk[v], xv) < key) f = false;
             }
             if (!f) continue;
             first |= 1u << q;
-            if (!(xu & 1u)) out[uint64_t(blk[u]) * RA_EPB + ((xu >> 1) & (RA_EPB - 1))] = 1;
+            if (!(xu & 1u)) out[uint64_t(blk[u]) * AEPB + ((xu >> 1) & (AEPB - 1))] = 1;
         }
         __syncthreads(); // every probe of the window has read the bits
 #pragma unroll 1
@@ -3107,19 +3111,24 @@ uint32_t rc_regions(uint64_t size) { return uint32_t((size + (1ull << RC_RB) - 1
 uint32_t rc_max_probes() { return RC_PMAX; }
 uint64_t rc_chunk_words(int k) { return uint64_t(RC_EPB) * uint64_t(k - 1); }
 
-uint32_t ra_blocks(uint64_t n) { return uint32_t((n + RA_EPB - 1) / RA_EPB); }
+static uint32_t ra_epb(int k) { return k <= RA_K4 ? 4096u : 2048u; }
+uint32_t ra_blocks(uint64_t n, int k) { return uint32_t((n + ra_epb(k) - 1) / ra_epb(k)); }
 uint32_t ra_regions(uint64_t size) { return uint32_t((size + (1ull << RA_RB) - 1) >> RA_RB); }
-uint64_t ra_piece() { return uint64_t(RA_JPT) * RC_TPB * RA_EPB; }
-uint64_t ra_chunk_words(int k) { return uint64_t(RA_EPB) * uint64_t(k); }
-uint32_t ra_max_probes() { return RA_PMAX; }
+uint64_t ra_piece(int k) { return uint64_t(RA_JPT) * RC_TPB * ra_epb(k); }
+uint64_t ra_chunk_words(int k) { return uint64_t(ra_epb(k)) * uint64_t(k); }
+uint32_t ra_max_probes() { return RC_PMAX; }
 
 // Bloom add, region schedule: records u32[ra_blocks(n) * ra_chunk_words(k)], S u32[regions * blocks], *flag = 0 before
 hipError_t launch_bloom_ra_hash(hipStream_t st, uint64_t n, const uint64_t *off, const uint8_t *bytes, uint64_t size,
                                 uint64_t magic, int k, uint32_t *S, uint32_t *recs, uint32_t *stop, uint32_t piece) {
     if (!n) return hipSuccess;
-    uint32_t NB = ra_blocks(n);
-    hipLaunchKernelGGL(k_bloom_rc_hash<true>, dim3(8 * ((NB + 7) / 8)), dim3(RC_TPB), 0, st, n, off, bytes, size,
-                       magic, uint32_t(k), ra_regions(size), NB, S, recs, nullptr, stop, piece);
+    uint32_t NB = ra_blocks(n, k);
+    if (ra_epb(k) == 4096)
+        hipLaunchKernelGGL((k_bloom_rc_hash<true, 4096>), dim3(8 * ((NB + 7) / 8)), dim3(RC_TPB), 0, st, n, off, bytes,
+                           size, magic, uint32_t(k), ra_regions(size), NB, S, recs, nullptr, stop, piece);
+    else
+        hipLaunchKernelGGL((k_bloom_rc_hash<true, 2048>), dim3(8 * ((NB + 7) / 8)), dim3(RC_TPB), 0, st, n, off, bytes,
+                           size, magic, uint32_t(k), ra_regions(size), NB, S, recs, nullptr, stop, piece);
     SK_LAUNCH_CHECK();
     return hipSuccess;
 }
@@ -3131,9 +3140,14 @@ hipError_t launch_bloom_ra_apply(hipStream_t st, uint64_t n, uint64_t size, int 
     uint32_t NR = ra_regions(size);
     // every region of a big piece expects >= RA_DENSE records: its bits are loaded up front
     const int big = n * uint64_t(k) >= uint64_t(2 * RA_DENSE) * NR;
-    hipLaunchKernelGGL(k_bloom_ra_apply, dim3(8 * ((NR + 7) / 8)), dim3(RC_TPB), 0, st, ra_blocks(n), NR, S, recs,
-                       uint32_t(k), bits, cap_bytes, reinterpret_cast<unsigned long long *>(d_len), out, stop, piece,
-                       big);
+    if (ra_epb(k) == 4096)
+        hipLaunchKernelGGL(k_bloom_ra_apply<4096>, dim3(8 * ((NR + 7) / 8)), dim3(RC_TPB), 0, st, ra_blocks(n, k), NR, S,
+                           recs, uint32_t(k), bits, cap_bytes, reinterpret_cast<unsigned long long *>(d_len), out,
+                           stop, piece, big);
+    else
+        hipLaunchKernelGGL(k_bloom_ra_apply<2048>, dim3(8 * ((NR + 7) / 8)), dim3(RC_TPB), 0, st, ra_blocks(n, k), NR, S,
+                           recs, uint32_t(k), bits, cap_bytes, reinterpret_cast<unsigned long long *>(d_len), out,
+                           stop, piece, big);
     SK_LAUNCH_CHECK();
     return hipSuccess;
 }

@@ -2778,8 +2778,8 @@ static int bloom_add_device(sk_ctx *c, uint32_t id, int64_t size, int32_t k, uin
     const uint64_t usize = uint64_t(size);
     if (!(c->bloom_ra_min && n >= c->bloom_ra_min && k >= 1 && uint32_t(k) <= sk::ra_max_probes()))
         return bloom_add_sorted(c, id, size, k, n, d_off, d_bytes, d_out);
-    const uint64_t magic = magic_for(usize), piece = sk::ra_piece();
-    const uint64_t nb = sk::ra_blocks(std::min(n, piece)), nr = sk::ra_regions(usize);
+    const uint64_t magic = magic_for(usize), piece = sk::ra_piece(k);
+    const uint64_t nb = sk::ra_blocks(std::min(n, piece), k), nr = sk::ra_regions(usize);
     HIPCHK(c, c->ra_S.ensure(nb * nr * 4));
     HIPCHK(c, c->ra_rec.ensure(nb * sk::ra_chunk_words(k) * 4));
     HIPCHK(c, c->ra_flag.ensure(4));

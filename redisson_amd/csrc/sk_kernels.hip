@@ -931,6 +931,9 @@ __global__ void __launch_bounds__(SK_PFP_ATPB) __attribute__((amdgpu_waves_per_e
 #endif
 #define SK_PFL_MAXSUB 8192 // fine buckets per coarse bucket (2^20 sketches)
 #define SK_PFL_TMAX 1024   // largest run tile (hash blocks): one segment per region thread
+#ifndef SK_PFL_MARK
+#define SK_PFL_MARK 0      // 1: registers with one record of the chunk skip the chains (marks in the register bytes)
+#endif
 #ifndef SK_PFL_LF
 #define SK_PFL_LF 0        // 1: the apply issues its register lines before the run table (speculative)
 #endif
@@ -1173,6 +1176,60 @@ __global__ void __launch_bounds__(256) k_pfl_fill(uint8_t *__restrict__ changed,
 template <class Fill, class Put>
 __device__ __forceinline__ void pfl_chunk(const uint64_t *R, uint32_t cnt, uint16_t *nxt, uint32_t *head,
                                           uint8_t *fin, uint8_t *reg, uint8_t *dirty, Fill fill, Put put) {
+#if SK_PFL_MARK
+    // Marks instead of chains for the common case: a fine bucket's registers are exactly its LDS lines, and a
+    // register value is <= 63, so bits 6 / 7 of its byte can say "one record" / "two or more".  A register with
+    // one record (~98 % at 600 records over ~12.5 k registers) needs no order: its record replies rho > R and
+    // writes max(R, rho).  Only the records of registers marked twice are chained and walked as before.
+    fill();
+    __syncthreads();
+    uint32_t *regw = reinterpret_cast<uint32_t *>(reg);
+    for (uint32_t u = threadIdx.x; u < cnt; u += SK_PFL_ATPB) {
+        const uint32_t sb = pfl_slotb(R[u] >> 32), sh = (sb & 3u) * 8u;
+        const uint32_t old = atomicOr(&regw[sb >> 2], 0x40u << sh);
+        if ((old >> sh) & 0x40u) atomicOr(&regw[sb >> 2], 0x80u << sh);
+    }
+    __syncthreads();
+    for (uint32_t u = threadIdx.x; u < cnt; u += SK_PFL_ATPB)
+        if (reg[pfl_slotb(R[u] >> 32)] & 0x80u) nxt[u] = uint16_t(atomicExch(&head[pfl_ht(R[u] >> 32)], u));
+    __syncthreads();
+    for (uint32_t u = threadIdx.x; u < cnt; u += SK_PFL_ATPB) {
+        const uint64_t rt = R[u], key = rt >> 32, seq = rt & 0x3ffffffu;
+        const uint32_t rho = uint32_t(rt >> 26) & 63u, byte = reg[pfl_slotb(key)], R0 = byte & 63u;
+        if (!(byte & 0x80u)) { // the register's only record
+            put(uint32_t(seq), uint32_t(rho > R0));
+            fin[u] = rho > R0 ? uint8_t(rho) : uint8_t(0);
+            continue;
+        }
+        uint32_t p = 0, m = rho;
+        bool earliest = true;
+        for (uint32_t w = head[pfl_ht(key)]; w != 0xffffu; w = nxt[w]) {
+            const uint64_t rw = R[w];
+            if ((rw >> 32) != key) continue;
+            const uint32_t rhow = uint32_t(rw >> 26) & 63u;
+            m = rhow > m ? rhow : m;
+            if ((rw & 0x3ffffffu) < seq) {
+                p = rhow > p ? rhow : p;
+                earliest = false;
+            }
+        }
+        put(uint32_t(seq), uint32_t(rho > (R0 > p ? R0 : p)));
+        fin[u] = earliest && m > R0 ? uint8_t(m) : uint8_t(0);
+    }
+    __syncthreads();
+    for (uint32_t u = threadIdx.x; u < cnt; u += SK_PFL_ATPB) { // marks off (every writer writes the same byte)
+        const uint32_t sb = pfl_slotb(R[u] >> 32);
+        reg[sb] = reg[sb] & 63u;
+    }
+    __syncthreads();
+    for (uint32_t u = threadIdx.x; u < cnt; u += SK_PFL_ATPB)
+        if (fin[u]) {
+            const uint64_t key = R[u] >> 32;
+            reg[pfl_slotb(key)] = fin[u];
+            dirty[uint32_t(key >> 14)] = 1;
+        }
+    return;
+#endif
     for (uint32_t u = threadIdx.x; u < cnt; u += SK_PFL_ATPB)
         nxt[u] = uint16_t(atomicExch(&head[pfl_ht(R[u] >> 32)], u));
     fill();
@@ -2148,6 +2205,12 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_rc_probe(uint32_t NB, uint32_t
 #ifndef RA_GQ
 #define RA_GQ 8       // record loads in flight per thread in a window's gather (RA_RPT: all of them)
 #endif
+#ifndef RA_OWNER
+#define RA_OWNER 0    // 1: the segments' owners load and chain their records (no separate index pass)
+#endif
+#ifndef RA_OQ
+#define RA_OQ 4       // records per segment an owner loads at once
+#endif
 #ifndef RA_SKIPSET
 #define RA_SKIPSET 1  // records on bits already set are not chained
 #endif
@@ -2229,22 +2292,72 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_ra_apply(uint32_t NB, uint32_t
     bool anyset = false;
     constexpr uint32_t W = RA_CAP - RA_SEGMAX;
     for (uint32_t lo = 0; lo < total; lo += W) {
-        if (threadIdx.x == 0) {
-            wbase = RA_NONE;
-            wend = 0;
-        }
-        __syncthreads(); // (first window: bits staged, heads cleared)
-        // the window = the segments starting in [lo, lo + W), laid out from the first one's start (a segment that
-        // starts in the previous window belongs to it whole)
+        if (total <= W) { // one window: [0, total), known without the atomics (the usual case)
+            if (threadIdx.x == 0) {
+                wbase = 0;
+                wend = total;
+            }
+            __syncthreads(); // bits staged, heads cleared
+        } else {
+            if (threadIdx.x == 0) {
+                wbase = RA_NONE;
+                wend = 0;
+            }
+            __syncthreads(); // (first window: bits staged, heads cleared)
+            // the window = the segments starting in [lo, lo + W), laid out from the first one's start (a segment that
+            // starts in the previous window belongs to it whole)
 #pragma unroll
-        for (int q = 0; q < RA_JPT; q++) {
-            const uint32_t cnt = sg[q] >> 16;
-            if (cnt == 0 || pre[q] < lo || pre[q] >= lo + W) continue;
-            atomicMin(&wbase, pre[q]);
-            atomicMax(&wend, pre[q] + cnt);
+            for (int q = 0; q < RA_JPT; q++) {
+                const uint32_t cnt = sg[q] >> 16;
+                if (cnt == 0 || pre[q] < lo || pre[q] >= lo + W) continue;
+                atomicMin(&wbase, pre[q]);
+                atomicMax(&wend, pre[q] + cnt);
+            }
+            __syncthreads();
         }
-        __syncthreads();
         const uint32_t base = wbase; // RA_NONE: no segment starts here (wend = 0, nw = 0)
+        const uint32_t nw = base == RA_NONE ? 0u : wend - base; // <= W + RA_SEGMAX = RA_CAP
+        // a record whose bit is already set (before the batch or by an earlier window) is never a setter, and a
+        // record on an unset bit only looks for smaller keys on its own bit: the former stay off the chains
+        auto link = [&](uint32_t u, uint32_t x) {
+            const uint32_t b = x >> 13;
+            if (RA_SKIPSET && dense && (filt[b >> 5] & ra_mask(b))) nxt[u] = 0xffffu;
+            else nxt[u] = uint16_t(atomicExch(&head[b & (RA_HT - 1)], u));
+        };
+#if RA_OWNER
+        { // the segments' owners load their records (the first RA_OQ of every segment at once) and chain them
+            uint32_t xs[RA_JPT][RA_OQ];
+#pragma unroll
+            for (int q = 0; q < RA_JPT; q++) {
+                const uint32_t cnt = sg[q] >> 16;
+                const bool in = cnt != 0 && pre[q] >= lo && pre[q] < lo + W;
+                const uint32_t *cs = chunks + (uint32_t(q) * RC_TPB + threadIdx.x) * CH + (sg[q] & 0xffffu);
+#pragma unroll
+                for (int u = 0; u < RA_OQ; u++) xs[q][u] = in && uint32_t(u) < cnt ? cs[u] : 0u;
+            }
+#pragma unroll
+            for (int q = 0; q < RA_JPT; q++) {
+                const uint32_t cnt = sg[q] >> 16;
+                if (cnt == 0 || pre[q] < lo || pre[q] >= lo + W) continue;
+                const uint32_t j = uint32_t(q) * RC_TPB + threadIdx.x, d = pre[q] - base;
+#pragma unroll
+                for (int u = 0; u < RA_OQ; u++)
+                    if (uint32_t(u) < cnt) {
+                        rec[d + u] = xs[q][u];
+                        blk[d + u] = uint16_t(j);
+                        link(d + u, xs[q][u]);
+                    }
+                const uint32_t *cs = chunks + j * CH + (sg[q] & 0xffffu);
+#pragma unroll 1
+                for (uint32_t u = RA_OQ; u < cnt; u++) { // long segment (rare): the rest one by one
+                    const uint32_t x = cs[u];
+                    rec[d + u] = x;
+                    blk[d + u] = uint16_t(j);
+                    link(d + u, x);
+                }
+            }
+        }
+#else
 #pragma unroll
         for (int q = 0; q < RA_JPT; q++) { // owners write each record's chunk word index
             const uint32_t cnt = sg[q] >> 16;
@@ -2258,7 +2371,6 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_ra_apply(uint32_t NB, uint32_t
             }
         }
         __syncthreads();
-        const uint32_t nw = base == RA_NONE ? 0u : wend - base; // <= W + RA_SEGMAX = RA_CAP
 #pragma unroll 1
         for (uint32_t g = 0; g < RA_RPT; g += RA_GQ) { // this thread's records of the window, RA_GQ loads in flight
             uint32_t x[RA_GQ];
@@ -2272,14 +2384,11 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_ra_apply(uint32_t NB, uint32_t
                 const uint32_t u = threadIdx.x + (g + q) * RC_TPB;
                 if (u < nw) {
                     rec[u] = x[q];
-                    const uint32_t b = x[q] >> 13;
-                    // a record on a bit already set (before the batch or by an earlier window) is never a setter, and
-                    // a record on an unset bit only looks for smaller keys on its own bit: it stays off the chains
-                    if (RA_SKIPSET && dense && (filt[b >> 5] & ra_mask(b))) nxt[u] = 0xffffu;
-                    else nxt[u] = uint16_t(atomicExch(&head[b & (RA_HT - 1)], u));
+                    link(u, x[q]);
                 }
             }
         }
+#endif
         __syncthreads();
         uint32_t first = 0; // bit q: record q of this thread sets its bit
 #pragma unroll 1

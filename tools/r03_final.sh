@@ -19,4 +19,9 @@ timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "sk::" --o
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "sk::" --output-format csv -d $O/pmc_write -o run -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline > $O/write.json 2> $O/write.err || { echo write failed; exit 1; }
 cd $R && python3 profiles/summarize.py $O $T --into $O/summary > /dev/null && rm -f $O/trace/run_kernel_trace.csv $O/pmc_*/run_counter_collection.csv
 timeout -k 10 900 python3 -u bench_configs.py > $O/configs.jsonl 2> $O/configs.err || { echo configs failed; tail -5 $O/configs.err; exit 1; }
+if [ -n "$EXTRA" ]; then
+  timeout -k 10 300 python3 -u bench.py --overlap --no-cpu-baseline > $O/bench_overlap.json 2> $O/bench_overlap.err || { echo overlap failed; exit 1; }
+  timeout -k 10 400 python3 -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 \
+    bench.py --gpus 2 --no-cpu-baseline > $O/bench_n2_shared_gpu.json 2> $O/bench_n2.err || { echo n2 failed; tail -5 $O/bench_n2.err; exit 1; }
+fi
 echo all done

@@ -931,6 +931,9 @@ __global__ void __launch_bounds__(SK_PFP_ATPB) __attribute__((amdgpu_waves_per_e
 #endif
 #define SK_PFL_MAXSUB 8192 // fine buckets per coarse bucket (2^20 sketches)
 #define SK_PFL_TMAX 1024   // largest run tile (hash blocks): one segment per region thread
+#ifndef SK_PFL_ONEB
+#define SK_PFL_ONEB 0      // 1: the chunk resolve reads registers before its one barrier and writes maxima in the walk
+#endif
 #ifndef SK_PFL_MARK
 #define SK_PFL_MARK 0      // 1: registers with one record of the chunk skip the chains (marks in the register bytes)
 #endif
@@ -1230,6 +1233,50 @@ __device__ __forceinline__ void pfl_chunk(const uint64_t *R, uint32_t cnt, uint1
         }
     return;
 #endif
+#if SK_PFL_ONEB
+    // One barrier: every record reads its register's value before the barrier (the lines are in LDS already: the
+    // caller stored them before its own barrier), so the earliest record of a register can write the final max
+    // during the walk -- nobody reads a register after the barrier
+    constexpr int CQ = SK_PFL_CAP / SK_PFL_ATPB;
+    uint32_t r0[CQ];
+    fill();
+#pragma unroll
+    for (int q = 0; q < CQ; q++) {
+        const uint32_t u = threadIdx.x + q * SK_PFL_ATPB;
+        if (u < cnt) {
+            const uint64_t key = R[u] >> 32;
+            nxt[u] = uint16_t(atomicExch(&head[pfl_ht(key)], u));
+            r0[q] = reg[pfl_slotb(key)];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < CQ; q++) {
+        const uint32_t u = threadIdx.x + q * SK_PFL_ATPB;
+        if (u >= cnt) continue;
+        const uint64_t rt = R[u], key = rt >> 32, seq = rt & 0x3ffffffu;
+        const uint32_t rho = uint32_t(rt >> 26) & 63u, R0 = r0[q];
+        uint32_t p = 0, m = rho;
+        bool earliest = true;
+        for (uint32_t w = head[pfl_ht(key)]; w != 0xffffu; w = nxt[w]) {
+            const uint64_t rw = R[w];
+            if ((rw >> 32) != key) continue;
+            const uint32_t rhow = uint32_t(rw >> 26) & 63u;
+            m = rhow > m ? rhow : m;
+            if ((rw & 0x3ffffffu) < seq) {
+                p = rhow > p ? rhow : p;
+                earliest = false;
+            }
+        }
+        put(uint32_t(seq), uint32_t(rho > (R0 > p ? R0 : p)));
+        if (earliest && m > R0) {
+            reg[pfl_slotb(key)] = uint8_t(m);
+            dirty[uint32_t(key >> 14)] = 1;
+        }
+    }
+    (void)fin;
+    return;
+#endif
     for (uint32_t u = threadIdx.x; u < cnt; u += SK_PFL_ATPB)
         nxt[u] = uint16_t(atomicExch(&head[pfl_ht(R[u] >> 32)], u));
     fill();
@@ -1405,15 +1452,23 @@ __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const uint64_t *__res
             const uint32_t u = q * SK_PFL_ATPB + threadIdx.x;
             if (u < cnt) R[u] = rv[q];
         }
-        __syncthreads();
-        if (probe & 128) return; // dev ablation: run table, lines and records loaded, nothing applied
-        pfl_chunk(R, cnt, nxt, head, fin, reg, dirty, [&] {
+        auto fill_lines = [&] {
 #pragma unroll
             for (int j = 0; j < LQ; j++) {
                 const uint32_t q = threadIdx.x + j * SK_PFL_ATPB;
                 if (q < nsl * LW && pm.inv(slab0 + q / LW) < nslab) regs4[q] = lv[j];
             }
-        }, put);
+        };
+#if SK_PFL_ONEB
+        fill_lines(); // the lines reach LDS before the barrier (pfl_chunk reads registers before its own)
+        __syncthreads();
+        if (probe & 128) return; // dev ablation: run table, lines and records loaded, nothing applied
+        pfl_chunk(R, cnt, nxt, head, fin, reg, dirty, [] {}, put);
+#else
+        __syncthreads();
+        if (probe & 128) return; // dev ablation: run table, lines and records loaded, nothing applied
+        pfl_chunk(R, cnt, nxt, head, fin, reg, dirty, fill_lines, put);
+#endif
     } else {
         for (uint32_t q = threadIdx.x; q < nsl * LW; q += SK_PFL_ATPB)
             if (pm.inv(slab0 + q / LW) < nslab) regs4[q] = line(q / LW)[q % LW];

@@ -931,15 +931,6 @@ __global__ void __launch_bounds__(SK_PFP_ATPB) __attribute__((amdgpu_waves_per_e
 #endif
 #define SK_PFL_MAXSUB 8192 // fine buckets per coarse bucket (2^20 sketches)
 #define SK_PFL_TMAX 1024   // largest run tile (hash blocks): one segment per region thread
-#ifndef SK_PFL_ONEB
-#define SK_PFL_ONEB 0      // 1: the chunk resolve reads registers before its one barrier and writes maxima in the walk
-#endif
-#ifndef SK_PFL_MARK
-#define SK_PFL_MARK 0      // 1: registers with one record of the chunk skip the chains (marks in the register bytes)
-#endif
-#ifndef SK_PFL_LF
-#define SK_PFL_LF 0        // 1: the apply issues its register lines before the run table (speculative)
-#endif
 #ifndef SK_PFL_NTMAX
 #define SK_PFL_NTMAX 64    // most tiles per call (the apply's run table; 5 apply workgroups per CU need <= 32 KiB of LDS)
 #endif
@@ -1179,104 +1170,6 @@ __global__ void __launch_bounds__(256) k_pfl_fill(uint8_t *__restrict__ changed,
 template <class Fill, class Put>
 __device__ __forceinline__ void pfl_chunk(const uint64_t *R, uint32_t cnt, uint16_t *nxt, uint32_t *head,
                                           uint8_t *fin, uint8_t *reg, uint8_t *dirty, Fill fill, Put put) {
-#if SK_PFL_MARK
-    // Marks instead of chains for the common case: a fine bucket's registers are exactly its LDS lines, and a
-    // register value is <= 63, so bits 6 / 7 of its byte can say "one record" / "two or more".  A register with
-    // one record (~98 % at 600 records over ~12.5 k registers) needs no order: its record replies rho > R and
-    // writes max(R, rho).  Only the records of registers marked twice are chained and walked as before.
-    fill();
-    __syncthreads();
-    uint32_t *regw = reinterpret_cast<uint32_t *>(reg);
-    for (uint32_t u = threadIdx.x; u < cnt; u += SK_PFL_ATPB) {
-        const uint32_t sb = pfl_slotb(R[u] >> 32), sh = (sb & 3u) * 8u;
-        const uint32_t old = atomicOr(&regw[sb >> 2], 0x40u << sh);
-        if ((old >> sh) & 0x40u) atomicOr(&regw[sb >> 2], 0x80u << sh);
-    }
-    __syncthreads();
-    for (uint32_t u = threadIdx.x; u < cnt; u += SK_PFL_ATPB)
-        if (reg[pfl_slotb(R[u] >> 32)] & 0x80u) nxt[u] = uint16_t(atomicExch(&head[pfl_ht(R[u] >> 32)], u));
-    __syncthreads();
-    for (uint32_t u = threadIdx.x; u < cnt; u += SK_PFL_ATPB) {
-        const uint64_t rt = R[u], key = rt >> 32, seq = rt & 0x3ffffffu;
-        const uint32_t rho = uint32_t(rt >> 26) & 63u, byte = reg[pfl_slotb(key)], R0 = byte & 63u;
-        if (!(byte & 0x80u)) { // the register's only record
-            put(uint32_t(seq), uint32_t(rho > R0));
-            fin[u] = rho > R0 ? uint8_t(rho) : uint8_t(0);
-            continue;
-        }
-        uint32_t p = 0, m = rho;
-        bool earliest = true;
-        for (uint32_t w = head[pfl_ht(key)]; w != 0xffffu; w = nxt[w]) {
-            const uint64_t rw = R[w];
-            if ((rw >> 32) != key) continue;
-            const uint32_t rhow = uint32_t(rw >> 26) & 63u;
-            m = rhow > m ? rhow : m;
-            if ((rw & 0x3ffffffu) < seq) {
-                p = rhow > p ? rhow : p;
-                earliest = false;
-            }
-        }
-        put(uint32_t(seq), uint32_t(rho > (R0 > p ? R0 : p)));
-        fin[u] = earliest && m > R0 ? uint8_t(m) : uint8_t(0);
-    }
-    __syncthreads();
-    for (uint32_t u = threadIdx.x; u < cnt; u += SK_PFL_ATPB) { // marks off (every writer writes the same byte)
-        const uint32_t sb = pfl_slotb(R[u] >> 32);
-        reg[sb] = reg[sb] & 63u;
-    }
-    __syncthreads();
-    for (uint32_t u = threadIdx.x; u < cnt; u += SK_PFL_ATPB)
-        if (fin[u]) {
-            const uint64_t key = R[u] >> 32;
-            reg[pfl_slotb(key)] = fin[u];
-            dirty[uint32_t(key >> 14)] = 1;
-        }
-    return;
-#endif
-#if SK_PFL_ONEB
-    // One barrier: every record reads its register's value before the barrier (the lines are in LDS already: the
-    // caller stored them before its own barrier), so the earliest record of a register can write the final max
-    // during the walk -- nobody reads a register after the barrier
-    constexpr int CQ = SK_PFL_CAP / SK_PFL_ATPB;
-    uint32_t r0[CQ];
-    fill();
-#pragma unroll
-    for (int q = 0; q < CQ; q++) {
-        const uint32_t u = threadIdx.x + q * SK_PFL_ATPB;
-        if (u < cnt) {
-            const uint64_t key = R[u] >> 32;
-            nxt[u] = uint16_t(atomicExch(&head[pfl_ht(key)], u));
-            r0[q] = reg[pfl_slotb(key)];
-        }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int q = 0; q < CQ; q++) {
-        const uint32_t u = threadIdx.x + q * SK_PFL_ATPB;
-        if (u >= cnt) continue;
-        const uint64_t rt = R[u], key = rt >> 32, seq = rt & 0x3ffffffu;
-        const uint32_t rho = uint32_t(rt >> 26) & 63u, R0 = r0[q];
-        uint32_t p = 0, m = rho;
-        bool earliest = true;
-        for (uint32_t w = head[pfl_ht(key)]; w != 0xffffu; w = nxt[w]) {
-            const uint64_t rw = R[w];
-            if ((rw >> 32) != key) continue;
-            const uint32_t rhow = uint32_t(rw >> 26) & 63u;
-            m = rhow > m ? rhow : m;
-            if ((rw & 0x3ffffffu) < seq) {
-                p = rhow > p ? rhow : p;
-                earliest = false;
-            }
-        }
-        put(uint32_t(seq), uint32_t(rho > (R0 > p ? R0 : p)));
-        if (earliest && m > R0) {
-            reg[pfl_slotb(key)] = uint8_t(m);
-            dirty[uint32_t(key >> 14)] = 1;
-        }
-    }
-    (void)fin;
-    return;
-#endif
     for (uint32_t u = threadIdx.x; u < cnt; u += SK_PFL_ATPB)
         nxt[u] = uint16_t(atomicExch(&head[pfl_ht(R[u] >> 32)], u));
     fill();
@@ -1384,9 +1277,6 @@ __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const uint64_t *__res
                 lv[j] = (probe & 4) ? make_uint4(0, 0, 0, 0) : line(q / LW)[q % LW];
         }
     };
-#if SK_PFL_LF
-    load_lines(); // speculative: issued before the run table, used when the bucket turns out to be one chunk
-#endif
     uint32_t st = 0, len = 0;
     if (threadIdx.x < ntile) {
         const uint32_t g = b * ntile + threadIdx.x;
@@ -1437,9 +1327,7 @@ __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const uint64_t *__res
     }
     __syncthreads();
     if (cnt <= SK_PFL_CAP) { // the whole fine bucket is one chunk: records and lines in one round trip
-#if !SK_PFL_LF
         load_lines();
-#endif
         constexpr int RU = SK_PFL_CAP / SK_PFL_ATPB; // every record load in flight at once
         uint64_t rv[RU];
 #pragma unroll
@@ -1459,16 +1347,9 @@ __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const uint64_t *__res
                 if (q < nsl * LW && pm.inv(slab0 + q / LW) < nslab) regs4[q] = lv[j];
             }
         };
-#if SK_PFL_ONEB
-        fill_lines(); // the lines reach LDS before the barrier (pfl_chunk reads registers before its own)
-        __syncthreads();
-        if (probe & 128) return; // dev ablation: run table, lines and records loaded, nothing applied
-        pfl_chunk(R, cnt, nxt, head, fin, reg, dirty, [] {}, put);
-#else
         __syncthreads();
         if (probe & 128) return; // dev ablation: run table, lines and records loaded, nothing applied
         pfl_chunk(R, cnt, nxt, head, fin, reg, dirty, fill_lines, put);
-#endif
     } else {
         for (uint32_t q = threadIdx.x; q < nsl * LW; q += SK_PFL_ATPB)
             if (pm.inv(slab0 + q / LW) < nslab) regs4[q] = line(q / LW)[q % LW];
@@ -2260,12 +2141,6 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_rc_probe(uint32_t NB, uint32_t
 #ifndef RA_GQ
 #define RA_GQ 8       // record loads in flight per thread in a window's gather (RA_RPT: all of them)
 #endif
-#ifndef RA_OWNER
-#define RA_OWNER 0    // 1: the segments' owners load and chain their records (no separate index pass)
-#endif
-#ifndef RA_OQ
-#define RA_OQ 4       // records per segment an owner loads at once
-#endif
 #ifndef RA_SKIPSET
 #define RA_SKIPSET 1  // records on bits already set are not chained
 #endif
@@ -2379,40 +2254,6 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_ra_apply(uint32_t NB, uint32_t
             if (RA_SKIPSET && dense && (filt[b >> 5] & ra_mask(b))) nxt[u] = 0xffffu;
             else nxt[u] = uint16_t(atomicExch(&head[b & (RA_HT - 1)], u));
         };
-#if RA_OWNER
-        { // the segments' owners load their records (the first RA_OQ of every segment at once) and chain them
-            uint32_t xs[RA_JPT][RA_OQ];
-#pragma unroll
-            for (int q = 0; q < RA_JPT; q++) {
-                const uint32_t cnt = sg[q] >> 16;
-                const bool in = cnt != 0 && pre[q] >= lo && pre[q] < lo + W;
-                const uint32_t *cs = chunks + (uint32_t(q) * RC_TPB + threadIdx.x) * CH + (sg[q] & 0xffffu);
-#pragma unroll
-                for (int u = 0; u < RA_OQ; u++) xs[q][u] = in && uint32_t(u) < cnt ? cs[u] : 0u;
-            }
-#pragma unroll
-            for (int q = 0; q < RA_JPT; q++) {
-                const uint32_t cnt = sg[q] >> 16;
-                if (cnt == 0 || pre[q] < lo || pre[q] >= lo + W) continue;
-                const uint32_t j = uint32_t(q) * RC_TPB + threadIdx.x, d = pre[q] - base;
-#pragma unroll
-                for (int u = 0; u < RA_OQ; u++)
-                    if (uint32_t(u) < cnt) {
-                        rec[d + u] = xs[q][u];
-                        blk[d + u] = uint16_t(j);
-                        link(d + u, xs[q][u]);
-                    }
-                const uint32_t *cs = chunks + j * CH + (sg[q] & 0xffffu);
-#pragma unroll 1
-                for (uint32_t u = RA_OQ; u < cnt; u++) { // long segment (rare): the rest one by one
-                    const uint32_t x = cs[u];
-                    rec[d + u] = x;
-                    blk[d + u] = uint16_t(j);
-                    link(d + u, x);
-                }
-            }
-        }
-#else
 #pragma unroll
         for (int q = 0; q < RA_JPT; q++) { // owners write each record's chunk word index
             const uint32_t cnt = sg[q] >> 16;
@@ -2443,7 +2284,6 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_ra_apply(uint32_t NB, uint32_t
                 }
             }
         }
-#endif
         __syncthreads();
         uint32_t first = 0; // bit q: record q of this thread sets its bit
 #pragma unroll 1

@@ -1,3 +1,5 @@
+#!/bin/bash
+# Dev scratch: the last A/B command sent to the GPU box this round (parity of the variants, then tools/gpu_ab.sh).
 set -o pipefail
 O=gpurun_out/r03e; mkdir -p $O
 T="python3 -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu"

@@ -1534,68 +1534,57 @@ __global__ void __launch_bounds__(256) k_hll_sum(uint64_t n, const uint32_t *__r
 }
 
 // -------------------------------------------------------------- histogram
-// 64-bin register histogram per key (the input of the PFCOUNT estimator).
-// Most registers of a tenant HLL share a value (0 in a sparse one), so shared
-// bins would serialise LDS atomics.  Zero registers are counted in registers
-// (zero-byte popcount); every other value bumps the lane's own column of a
-// bin-major LDS table with a return-less LDS add (ds_add_u32: the wave never
-// waits on a read-modify-write chain; two bins share a u32, u16 halves, a lane
-// counts <= 64 registers per key), conflict-free whatever the values.  The
-// columns are reduced with a rotated walk and cleared for the next key.
-// Workgroups loop over keys; the next key's 16 KiB is loaded while the current
-// one is reduced.  (Plain u16 read-modify-write columns: 3.6 TB/s at C2;
-// return-less adds: 4.95 TB/s, profiles/r01_ab/stream/.)
-#define SK_HH_TPB 256
-__global__ void __launch_bounds__(SK_HH_TPB) k_hll_hist(uint64_t n, const uint32_t *__restrict__ ids,
-                                                        const uint8_t *__restrict__ arena,
-                                                        uint32_t *__restrict__ hist) {
-    __shared__ uint32_t h[32][SK_HH_TPB];
-    __shared__ uint32_t part[SK_HH_TPB / 64][64];
-    const unsigned t = threadIdx.x, bin = t & 63u, q = t >> 6;
-    for (int b = 0; b < 32; b++) h[b][t] = 0;
-    auto load = [&](uint64_t key, uint4 (&v)[4]) {
+// 64-bin register histogram per key, one wave per key and no barriers (the input of the >= 5.0 estimator).
+// Each lane owns a column of a bin-major LDS table h[64][64] (u32, 16 KiB per wave) and counts its 256 registers
+// into it with return-less LDS adds: the address is bin * 256 + lane * 4, so the 64 lanes of one add always hit
+// 64 different banks whatever the values, zeros included (no branch).  Lane b then sums row b (bin b) with 16-B
+// reads, rotated per lane, and clears it.  LDS instructions of one wave execute in order, so the next key's adds
+// land after this key's reads.  The next key's 16 KiB loads while the table is summed (a second key in registers,
+// loading while this one is counted, measured the same: the adds, ~7 cycles per wave instruction per CU, bound it).
+__global__ void __launch_bounds__(64) k_hll_hist(uint64_t n, const uint32_t *__restrict__ ids,
+                                                   const uint8_t *__restrict__ arena, uint32_t *__restrict__ hist) {
+    __shared__ uint4 h4[64 * 16];
+    uint32_t *h = reinterpret_cast<uint32_t *>(h4);
+    const uint32_t lane = threadIdx.x;
+#pragma unroll
+    for (int j = 0; j < 16; j++) h4[lane + 64 * j] = make_uint4(0, 0, 0, 0);
+    auto load = [&](uint64_t key, uint4 (&v)[16]) {
         const uint4 *base = reinterpret_cast<const uint4 *>(arena + (uint64_t(ids[key] & SK_SLAB_MASK) << 14));
 #pragma unroll
-        for (int it = 0; it < 4; it++) v[it] = ld_nt(base + it * SK_HH_TPB + t);
+        for (int it = 0; it < 16; it++) v[it] = ld_nt(base + it * 64 + lane);
     };
-    uint4 v[4];
+    auto count = [&](uint64_t key, const uint4 (&v)[16]) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int it = 0; it < 16; it++) {
+            const uint32_t ws[4] = {v[it].x, v[it].y, v[it].z, v[it].w};
+#pragma unroll
+            for (int w = 0; w < 4; w++)
+#pragma unroll
+                for (int b = 0; b < 4; b++)
+                    __hip_atomic_fetch_add(&h[((ws[w] >> (8 * b)) & 63u) * 64 + lane], 1u, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_WAVEFRONT);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        uint32_t c = 0;
+#pragma unroll
+        for (int j = 0; j < 16; j++) {
+            const uint32_t q = lane * 16 + ((j + lane) & 15u);
+            const uint4 x = h4[q];
+            c += x.x + x.y + x.z + x.w;
+            h4[q] = make_uint4(0, 0, 0, 0);
+        }
+        hist[key * 64 + lane] = c;
+    };
+    const uint64_t G = gridDim.x;
+    uint4 v[16];
     uint64_t key = blockIdx.x;
     if (key < n) load(key, v);
-    for (; key < n; key += gridDim.x) {
-        uint32_t zeros = 0;
-#pragma unroll
-        for (int it = 0; it < 4; it++) {
-            uint32_t ws[4] = {v[it].x, v[it].y, v[it].z, v[it].w};
-#pragma unroll
-            for (int w = 0; w < 4; w++) {
-                uint32_t x = ws[w] & 0x3f3f3f3fu;
-                zeros += __popc(~(((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x | 0x7f7f7f7fu));
-                if (x == 0) continue;
-#pragma unroll
-                for (int b = 0; b < 4; b++) {
-                    uint32_t r = (x >> (8 * b)) & 63u;
-                    if (r) __hip_atomic_fetch_add(&h[r >> 1][t], 1u << ((r & 1u) * 16u), __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_WORKGROUP);
-                }
-            }
-        }
-        __hip_atomic_fetch_add(&h[0][t], zeros, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        __syncthreads();
-        if (key + gridDim.x < n) load(key + gridDim.x, v);
-        uint32_t sum = 0;
-        for (unsigned i = 0; i < 64; i++) {
-            unsigned lane = q * 64 + ((i + bin) & 63u);
-            sum += (h[bin >> 1][lane] >> ((bin & 1u) * 16u)) & 0xffffu;
-        }
-        part[q][bin] = sum;
-        __syncthreads(); // every half is read before the columns are cleared
-        for (int b = 0; b < 32; b++) h[b][t] = 0;
-        if (t < 64) {
-            uint32_t c = 0;
-#pragma unroll
-            for (int qq = 0; qq < SK_HH_TPB / 64; qq++) c += part[qq][t];
-            hist[key * 64 + t] = c;
-        }
+    for (; key < n; key += G) {
+        count(key, v);
+        if (key + G < n) load(key + G, v);
     }
 }
 
@@ -3046,7 +3035,7 @@ hipError_t launch_hll_sum(hipStream_t st, uint64_t n, const uint32_t *ids, const
 
 hipError_t launch_hll_hist(hipStream_t st, uint64_t n, const uint32_t *ids, const uint8_t *arena, uint32_t *hist) {
     if (!n) return hipSuccess;
-    hipLaunchKernelGGL(k_hll_hist, dim3(grid_for(n, 1, 2048)), dim3(SK_HH_TPB), 0, st, n, ids, arena, hist);
+    hipLaunchKernelGGL(k_hll_hist, dim3(grid_for(n, 1, 8192)), dim3(64), 0, st, n, ids, arena, hist);
     SK_LAUNCH_CHECK();
     return hipSuccess;
 }

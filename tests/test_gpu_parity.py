@@ -129,7 +129,29 @@ def test_pfadd_dev_path(engine, O):
     engine.hll_histogram_dev(nkeys, engine.to_device(ids), d_hist)
     h = d_hist.download(np.uint32).reshape(nkeys, 64)
     for i in range(nkeys):
+        assert np.array_equal(h[i], np.bincount(regs[i], minlength=64)), i
         assert engine.estimate_hist(h[i]) == O.count_regs(regs[i], 1)
+
+
+def test_hll_histogram_many_keys(engine, O):
+    """More keys than histogram workgroups (each loops over keys and reuses its cleared LDS table), with the ids
+    in a shuffled order and repeated: every row equals np.bincount of the key's registers."""
+    n, nkeys = 600_000, 20_000
+    off, buf = gen_jackson_longs(0x5EED0021, n)
+    rng = np.random.default_rng(21)
+    kid = rng.integers(0, nkeys, n).astype(np.uint32)
+    names = [b"hh:%d" % i for i in range(nkeys)]
+    ids = engine.hll_resolve(names)
+    d_out = engine.alloc(n)
+    engine.pfadd_dev(n, engine.to_device(ids[kid]), engine.to_device(off), engine.to_device(buf, pad=16),
+                     int(off[-1]), d_out)
+    regs, _ = O.HLLStore().pfadd_bulk(kid, off, buf, nkeys)
+    order = np.concatenate([rng.permutation(nkeys), rng.integers(0, nkeys, 3000)]).astype(np.int64)
+    d_hist = engine.alloc(len(order) * 64 * 4)
+    engine.hll_histogram_dev(len(order), engine.to_device(ids[order]), d_hist)
+    h = d_hist.download(np.uint32).reshape(len(order), 64)
+    want = np.stack([np.bincount(regs[i], minlength=64) for i in order]).astype(np.uint32)
+    np.testing.assert_array_equal(h, want)
 
 
 # ------------------------------------------------------------------- Bloom

@@ -421,7 +421,8 @@ def host(eng, args):
     t_ct = timed(eng, lambda: [ct(r) for r in range(reps)]) / reps
     h2d_bl = eoffs[0].nbytes + probe[0][1].nbytes
     # group commit through the host ABI (what GpuBatchCoalescer sends): G RBatches of 1M one-element PFADDs as ONE
-    # sk_pfadd_ids call over cached slab ids, pageable inputs staged by the library through its pinned double buffer
+    # sk_pfadd_ids call over cached slab ids; pageable inputs go through HIP's own pageable copy (the library's pinned
+    # double buffer is opt-in, SK_STAGE=1)
     G = 32
     gof, gbuf = gen_jackson_longs(0x5EED0034, B * G)
     gids = np.ascontiguousarray(eng.hll_resolve(names)[rng.integers(0, nt, B * G)], dtype=np.uint32)

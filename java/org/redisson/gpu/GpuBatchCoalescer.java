@@ -176,10 +176,10 @@ public final class GpuBatchCoalescer {
         }
     }
 
-    /* The group as ONE sk_pfadd_ids call over cached slab handles: no name resolution on the hot path, the
-     * library's liveness check and host threads over the ids, and pageable inputs staged through its pinned
-     * double buffer (H2D of one piece overlaps the host copy of the next).  A stale cache is dropped and the group
-     * resolved again once. */
+    /* The group as ONE sk_pfadd_ids call over cached slab handles: no name resolution on the hot path and the
+     * library's liveness check on host threads over the ids.  Pageable inputs take HIP's own pageable copy (the
+     * library's pinned double buffer is opt-in, SK_STAGE=1); inputs in sk_host_alloc memory are copied directly.
+     * A stale cache is dropped and the group resolved again once. */
     private void execute(List<Req> group) {
         List<byte[]> keys = new ArrayList<byte[]>();
         for (Req r : group) {

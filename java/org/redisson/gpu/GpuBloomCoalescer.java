@@ -62,6 +62,7 @@ public final class GpuBloomCoalescer implements Runnable {
         this.thread = new Thread(this, "sk-bloom-coalescer");
         this.thread.setDaemon(true);
         this.thread.start();
+        GpuSketch.track(ctx, this); // closed by GpuSketch.close(ctx) before the context itself
     }
 
     /** Enqueue; never blocks on the device.  The promise gets one reply per element. */

@@ -26,6 +26,7 @@ import org.redisson.client.RedisException;
 import org.redisson.client.codec.Codec;
 import org.redisson.client.protocol.RedisCommand;
 import org.redisson.client.protocol.RedisCommands;
+import org.redisson.client.protocol.convertor.VoidReplayConvertor;
 import org.redisson.command.CommandBatchService;
 import org.redisson.connection.ConnectionManager;
 import org.redisson.connection.NodeSource;
@@ -169,6 +170,26 @@ public class GpuSketchBatchService extends CommandBatchService {
         return result;
     }
 
+    /* RBitSet range set/clear (M:RedissonBitSet.java:202-228) and RedissonBloomFilter's pipelines finish their
+     * batch with executeAsyncVoid, which in the reference walks the per-slot queues directly
+     * (M:command/CommandBatchService.java:117-140) and would never see this class's sketch queue: route it through
+     * executeAsync and drop the result list. */
+    @Override
+    public Future<Void> executeAsyncVoid() {
+        final Promise<Void> done = getConnectionManager().newPromise();
+        executeAsync().addListener(new FutureListener<List<?>>() {
+            @Override
+            public void operationComplete(Future<List<?>> f) throws Exception {
+                if (f.isSuccess()) {
+                    done.trySuccess(null);
+                } else {
+                    done.tryFailure(f.cause());
+                }
+            }
+        });
+        return done;
+    }
+
     boolean pfaddOnly() {
         if (redisUsed || sketch.isEmpty()) {
             return false;
@@ -266,6 +287,34 @@ public class GpuSketchBatchService extends CommandBatchService {
         });
     }
 
+    /* A run of SETBIT_VOID on one key, one value and consecutive offsets -- what RBitSet.set(from, to) and
+     * clear(from, to) queue, one SETBIT per bit (M:RedissonBitSet.java:202-228) -- is applied by ONE range kernel
+     * with the same string growth and final bits (k_bit_range).  The replies are Void, so nothing else is owed;
+     * an out-of-range offset fails the run after the in-range bits are set, as the pipeline would. */
+    boolean bitRange(List<Cmd> run) {
+        if (run.size() < 64) {
+            return false;
+        }
+        Cmd first = run.get(0);
+        String key = first.params[0].toString();
+        String val = first.params[2].toString();
+        long from = Long.parseLong(first.params[1].toString());
+        for (int c = 0; c < run.size(); c++) {
+            Cmd cmd = run.get(c);
+            if (!(cmd.command.getConvertor() instanceof VoidReplayConvertor) || !key.equals(cmd.params[0].toString())
+                    || !val.equals(cmd.params[2].toString())
+                    || Long.parseLong(cmd.params[1].toString()) != from + c) {
+                return false;
+            }
+        }
+        byte[] k = GpuSketchCommandService.encodeParam(first.codec, first.command, first.params[0], 1);
+        SketchDispatch.check(ctx, SketchNative.setBitRange(ctx, k, from, from + run.size(), !"0".equals(val)));
+        for (Cmd cmd : run) {
+            cmd.promise.setSuccess(null);
+        }
+        return true;
+    }
+
     static boolean runnable(String kind) {
         return "PFADD".equals(kind) || "GETBIT".equals(kind) || "SETBIT".equals(kind) || "PFCOUNT".equals(kind);
     }
@@ -319,6 +368,8 @@ public class GpuSketchBatchService extends CommandBatchService {
                 }
                 SketchDispatch.Packed e = new SketchDispatch.Packed(elems);
                 SketchDispatch.pfaddRun(ctx, keys, k, counts, e, out);
+            } else if ("SETBIT".equals(kind) && bitRange(run)) {
+                return; // one range kernel (sk_set_bit_range) for the whole run
             } else {
                 long[] offs = new long[n];
                 byte[] vals = new byte[n];

@@ -68,12 +68,21 @@ public final class SketchDispatch {
         return w;
     }
 
-    /** Before sk_close(ctx): queued work finishes, later submissions are refused. */
-    public static void shutdownWorker(long ctx) {
+    /** Before sk_close(ctx): queued work finishes (this waits for it), later submissions are refused. */
+    public static void shutdownWorker(long ctx) throws InterruptedException {
         ExecutorService w = WORKERS.remove(ctx);
         if (w != null) {
             w.shutdown();
+            while (!w.awaitTermination(1, java.util.concurrent.TimeUnit.SECONDS)) {
+                // engine calls in flight: a device batch may take seconds; keep waiting
+            }
         }
+    }
+
+    /** Drop every per-context table (slab-handle cache) once the context is closed: a later context opened at the
+     * same address starts from nothing (ADVICE r3). */
+    static void forget(long ctx) {
+        SLAB_IDS.remove(ctx);
     }
 
     /* Per-context HLL name -> slab handle cache (INTEGRATION.md "Caching slab ids").  Filled after a run's

@@ -371,15 +371,39 @@ class ShardedBitSet:
         """GETBIT of a device batch submitted on this rank, routed as set_dev."""
         self._route_dev("get", n, d_offsets, d_out, 0, None)
 
+    _OPS = {"set": 1, "get": 2}
+
     def _route_dev(self, op, n, d_offsets, d_out, value, d_values) -> None:
+        """The device router.  Every rank's call shape travels with its per-shard counts in ONE all-gather (ADVICE
+        r3): op, value, whether it passed per-op values and whether it wants replies.  So the collective sequence
+        below is decided from the same gathered words on every rank: per-op values travel whenever any rank passed
+        them or the ranks' values differ (a rank with one value sends it per op), replies travel back whenever any
+        rank wants them, and ranks that called different operations all raise instead of mismatching RCCL calls."""
+        from .engine import RedisException
+
         e, W, me = self.engine, self.world, self.rank
         send, dst = e.alloc(max(8 * n, 8)), e.alloc(max(4 * n, 4))
-        svals = e.alloc(max(n, 1)) if d_values is not None else None
-        tmp = [send, dst] + ([svals] if svals is not None else [])
+        tmp = [send, dst]
         try:
+            hdr = np.array([self._OPS[op], int(value) & 1, d_values is not None, d_out is not None], dtype=np.uint64)
+            gathered = [np.frombuffer(b, dtype=np.uint64)
+                        for b in self.coll.allgather_bytes(hdr.tobytes())]
+            hdrs = np.stack(gathered)
+            if len(set(hdrs[:, 0].tolist())) != 1:
+                raise RedisException("ranks called different routed operations on %r: %s"
+                                     % (self.name, sorted({k for k, v in self._OPS.items() if v in hdrs[:, 0]})))
+            per_op = op == "set" and (bool(hdrs[:, 2].any()) or len(set(hdrs[:, 1].tolist())) != 1)
+            want = bool(hdrs[:, 3].any())
+            svals = None
+            if per_op:
+                svals = e.alloc(max(n, 1))
+                tmp.append(svals)
+                if d_values is None and n:        # this rank's one value, per op
+                    d_values = e.to_device(np.full(n, int(value) & 1, dtype=np.uint8))
+                    tmp.append(d_values)
             cnt, err = np.zeros(W, dtype=np.uint64), None
             try:
-                cnt = e.route_bits(n, d_offsets, d_values, 8 * self.S, W, send, svals, dst)
+                cnt = e.route_bits(n, d_offsets, d_values if per_op else None, 8 * self.S, W, send, svals, dst)
             except Exception as x:  # noqa: BLE001 - agreed on below
                 err = x
             agree(self.coll, err)
@@ -390,28 +414,27 @@ class ShardedBitSet:
             tmp += [recv, rep]
             self.coll.alltoallv_dev(send, cnt * 8, recv, rcv * 8)
             rvals = None
-            if d_values is not None:
+            if per_op:
                 rvals = e.alloc(max(m, 1))
                 tmp.append(rvals)
                 self.coll.alltoallv_dev(svals, cnt, rvals, rcv)
             err = None
             try:
-                void = d_out is None
-                if m and op == "set" and rvals is not None:
-                    e.setbit_values_dev(self.name, m, recv, rvals, None if void else rep)
+                if m and op == "set" and per_op:
+                    e.setbit_values_dev(self.name, m, recv, rvals, rep if want else None)
                 elif m and op == "set":
-                    e.setbit_dev(self.name, m, recv, int(value), None if void else rep)
+                    e.setbit_dev(self.name, m, recv, int(hdrs[0, 1]), rep if want else None)
                 elif m:
                     e.getbit_dev(self.name, m, recv, rep)
             except Exception as x:  # noqa: BLE001 - agreed on below
                 err = x
             agree(self.coll, err)
-            if d_out is None:
+            if not want:
                 return
             back = e.alloc(max(n, 1))
             tmp.append(back)
             self.coll.alltoallv_dev(rep, rcv, back, cnt)
-            if n:
+            if n and d_out is not None:
                 e.unroute_u8(n, dst, back, d_out)
         finally:
             for b in tmp:

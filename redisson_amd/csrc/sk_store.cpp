@@ -20,6 +20,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <exception>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -54,8 +55,12 @@ class HostPool {
         return *p;
     }
     unsigned threads() const { return unsigned(workers_.size()) + 1; }
+    // An exception thrown by fn (bad_alloc in a lookup pass ...) is caught where it is thrown, the section still
+    // waits until every worker has left fn -- which references the caller's frame -- and then the first exception is
+    // rethrown on the caller.  A run() nested inside a section (fn calling host_for) runs inline on the
+    // calling thread instead of waiting on run_mu_, which its own section holds.
     void run(unsigned parts, const std::function<void(unsigned)> &fn) {
-        if (parts <= 1 || workers_.empty()) {
+        if (parts <= 1 || workers_.empty() || in_section()) {
             for (unsigned t = 0; t < parts; t++) fn(t);
             return;
         }
@@ -66,16 +71,39 @@ class HostPool {
             parts_ = parts;
             next_.store(0);
             active_ = unsigned(workers_.size());
+            err_ = nullptr;
             gen_++;
         }
         cv_.notify_all();
-        for (unsigned t; (t = next_.fetch_add(1)) < parts;) fn(t);
+        in_section() = true;
+        work(fn, parts);
+        in_section() = false;
         std::unique_lock<std::mutex> l(mu_);
         done_.wait(l, [&] { return active_ == 0; });
         job_ = nullptr;
+        std::exception_ptr e = err_;
+        err_ = nullptr;
+        l.unlock();
+        if (e) std::rethrow_exception(e);
     }
 
   private:
+    static bool &in_section() {
+        static thread_local bool b = false;
+        return b;
+    }
+    // take parts until none is left; an exception is recorded (first one wins) and the remaining parts are skipped
+    void work(const std::function<void(unsigned)> &fn, unsigned P) {
+        for (unsigned t; (t = next_.fetch_add(1)) < P;) {
+            try {
+                fn(t);
+            } catch (...) {
+                std::lock_guard<std::mutex> l(mu_);
+                if (!err_) err_ = std::current_exception();
+                next_.store(P);
+            }
+        }
+    }
     HostPool() {
         unsigned T = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
         if (const char *e = getenv("OMP_NUM_THREADS")) T = std::max(1, std::min(int(T), atoi(e)));
@@ -84,6 +112,7 @@ class HostPool {
     }
     void loop() {
         uint64_t seen = 0;
+        in_section() = true; // a worker is only ever inside a section
         for (;;) {
             std::unique_lock<std::mutex> l(mu_);
             cv_.wait(l, [&] { return gen_ != seen; });
@@ -91,7 +120,7 @@ class HostPool {
             const std::function<void(unsigned)> *j = job_;
             const unsigned P = parts_;
             l.unlock();
-            for (unsigned t; (t = next_.fetch_add(1)) < P;) (*j)(t);
+            work(*j, P);
             l.lock();
             if (--active_ == 0) done_.notify_one();
         }
@@ -103,6 +132,7 @@ class HostPool {
     unsigned parts_ = 0, active_ = 0;
     std::atomic<unsigned> next_{0};
     uint64_t gen_ = 0;
+    std::exception_ptr err_;
 };
 // parallel for over [0, n) in `parts` contiguous ranges (parts = the pool's threads unless n is small)
 void host_for(uint64_t n, uint64_t min_per_thread, const std::function<void(uint64_t, uint64_t)> &fn) {
@@ -1169,16 +1199,18 @@ int pfadd_lines(sk_ctx *c, uint64_t n, const uint32_t *d_ids, const uint64_t *d_
     { Prof p_(c, 24);
     HIPCHK(c, sk::launch_pfl_hash(c->st, n, d_ids, d_off, d_bytes, c->redis_major >= 5, c->pfl_chunks.as<uint64_t>(),
                                   c->pfl_S.as<uint32_t>(), c->pfl_ovf.as<uint32_t>())); }
-    { Prof p_(c, 25);
-    HIPCHK(c, sk::launch_pfl_part(c->st, d, c->pfl_chunks.as<uint64_t>(), c->pfl_S.as<uint32_t>(),
-                                  c->pfl_C.as<uint32_t>(), c->pfl_rec.as<uint64_t>(), d_changed)); }
     // replies: pre-filled with the call's default (the previous call's majority reply) by one streaming kernel, then
     // the apply stores only the other replies, instead of one scattered byte per element (SK_PFL_ZERO=0: every
-    // reply stored by the apply)
+    // reply stored by the apply).  The fill runs before the region pass, which stores 0 for the records it drops
+    // (slab id >= nslab: no register, reply 0), so the default never overwrites those.
     const uint32_t par = c->pfl_par;
     c->pfl_par ^= 1;
     { Prof p_(c, 26);
-    if (c->pfl_zero) HIPCHK(c, sk::launch_pfl_fill(c->st, d_changed, n, c->pfl_rc.as<uint32_t>(), par));
+    if (c->pfl_zero) HIPCHK(c, sk::launch_pfl_fill(c->st, d_changed, n, c->pfl_rc.as<uint32_t>(), par)); }
+    { Prof p_(c, 25);
+    HIPCHK(c, sk::launch_pfl_part(c->st, d, c->pfl_chunks.as<uint64_t>(), c->pfl_S.as<uint32_t>(),
+                                  c->pfl_C.as<uint32_t>(), c->pfl_rec.as<uint64_t>(), d_changed)); }
+    { Prof p_(c, 26);
     HIPCHK(c, sk::launch_pfl_apply(c->st, d, c->pfl_rec.as<uint64_t>(), c->pfl_C.as<uint32_t>(), nslab, c->arena,
                                    d_changed, c->pfl_ovf.as<uint32_t>(), c->pfl_bk.as<uint64_t>(),
                                    c->pfl_bv.as<uint32_t>(), c->pfl_zero ? 32 : 0,

@@ -384,3 +384,117 @@ class OracleBitEngine:
         else:
             self.s.pop(bytes(dest), None)
         return len(v)
+
+    # -------- the device router's engine steps (sk_route_bits / sk_unroute_u8 / *_dev), over HostBufs
+    def route_bits(self, n, d_offsets, d_values, shard_bits, world, d_send, d_send_values, d_dst):
+        from redisson_amd.engine import RedisException
+        offs = d_offsets.download(np.uint64, n) if n else np.zeros(0, np.uint64)
+        sh = (offs // np.uint64(shard_bits)).astype(np.int64)
+        if (sh >= world).any():
+            raise RedisException("ERR bit offset is not an integer or out of range")
+        order = np.argsort(sh, kind="stable")
+        if n:
+            d_send.upload(offs[order] - sh[order].astype(np.uint64) * np.uint64(shard_bits))
+            if d_values is not None:
+                d_send_values.upload(d_values.download(np.uint8, n)[order])
+            pos = np.empty(n, dtype=np.uint32)
+            pos[order] = np.arange(n, dtype=np.uint32)
+            d_dst.upload(pos)
+        return np.bincount(sh, minlength=world).astype(np.uint64)
+
+    def unroute_u8(self, n, d_dst, d_rep, d_out):
+        d_out.upload(d_rep.download(np.uint8, -1)[d_dst.download(np.uint32, n)])
+
+    def setbit_dev(self, key, n, d_offsets, value, d_out_old=None):
+        old = self.setbit([key] * n, d_offsets.download(np.uint64, n), [value] * n)
+        if d_out_old is not None:
+            d_out_old.upload(np.asarray(old, np.uint8))
+
+    def setbit_values_dev(self, key, n, d_offsets, d_values, d_out_old=None):
+        old = self.setbit([key] * n, d_offsets.download(np.uint64, n), d_values.download(np.uint8, n))
+        if d_out_old is not None:
+            d_out_old.upload(np.asarray(old, np.uint8))
+
+    def getbit_dev(self, key, n, d_offsets, d_out):
+        d_out.upload(np.asarray(self.getbit([key] * n, d_offsets.download(np.uint64, n)), np.uint8))
+
+
+class HostDevCollective:
+    """HostCollective plus the RCCL collective's alltoallv_dev over HostBufs (gloo underneath), so the CPU tests run
+    ShardedBitSet's device router (set_dev / get_dev) on an OracleBitEngine."""
+
+    def __init__(self, dist):
+        from redisson_amd.cluster import HostCollective
+        self.h = HostCollective(dist)
+
+    def __getattr__(self, a):
+        return getattr(self.h, a)
+
+    def alltoallv_dev(self, send, send_bytes, recv, recv_bytes):
+        sb = np.asarray(send_bytes, dtype=np.int64)
+        cut = np.concatenate([[0], np.cumsum(sb)])
+        got = self.h.alltoallv_bytes([send.a[cut[p]:cut[p + 1]].tobytes() for p in range(len(sb))])
+        assert [len(g) for g in got] == [int(x) for x in recv_bytes], "alltoallv sizes disagree"
+        flat = b"".join(got)
+        if flat:
+            recv.upload(np.frombuffer(flat, np.uint8))
+
+
+def run_route_mix(engine, rank, world, coll):
+    """ranks calling the device router with different call shapes.  Rank r sets (r even) or clears (r odd)
+    its slice of one offset list; then rank 0 asks for no replies while the others do; then rank 0 passes per-op
+    values while the others pass one value.  Every rank's replies are gathered in rank order."""
+    from redisson_amd.cluster import ShardedBitSet
+
+    bs = ShardedBitSet(engine, b"sb:mix", NBITS, rank, world, coll)
+    offs = _offsets(21, 2400)
+    offs[:300] = offs[300:600]                    # bits touched by both ranks' slices
+    mine = offs[rank * len(offs) // world:(rank + 1) * len(offs) // world]
+    out = {}
+
+    def run(value, d_values=None, want=True):
+        n = len(mine)
+        d_off, d_rep = engine.to_device(mine), engine.alloc(max(n, 1))
+        dv = engine.to_device(d_values) if d_values is not None else None
+        bs.set_dev(n, d_off, d_rep if want else None, value=value, d_values=dv)
+        rep = d_rep.download(np.uint8, n) if want else np.zeros(0, np.uint8)
+        for b in (d_off, d_rep, dv):
+            if b is not None:
+                b.free()
+        return [int(v) for part in coll.allgather_bytes(rep.tobytes()) for v in part]
+
+    out["mixed_values"] = run(1 if rank % 2 == 0 else 0)
+    out["void_on_rank0"] = run(1, want=rank != 0)
+    pv = (np.arange(len(mine)) % 2).astype(np.uint8)
+    out["per_op_on_rank0"] = run(0, d_values=pv if rank == 0 else None)
+    out["bytes"] = bs.to_bytes()
+    try:
+        if rank == 0:
+            bs.get_dev(0, engine.alloc(8), engine.alloc(8))
+        else:
+            bs.set_dev(0, engine.alloc(8), engine.alloc(8))
+        out["op_mismatch"] = False
+    except Exception as e:  # noqa: BLE001 - every rank must raise
+        out["op_mismatch"] = "different routed operations" in str(e)
+    return out
+
+
+def expected_route_mix(world):
+    from oracle import oracle as O
+
+    b = O.BitString(NBITS // 8 + 16)
+    offs = _offsets(21, 2400)
+    offs[:300] = offs[300:600]
+    slices = [offs[r * len(offs) // world:(r + 1) * len(offs) // world] for r in range(world)]
+    out = {"mixed_values": [], "void_on_rank0": [], "per_op_on_rank0": []}
+    for r, s in enumerate(slices):                # owners apply in (submitting rank, position) order
+        out["mixed_values"] += [b.setbit(int(o), 1 if r % 2 == 0 else 0) for o in s]
+    for r, s in enumerate(slices):
+        rep = [b.setbit(int(o), 1) for o in s]
+        out["void_on_rank0"] += rep if r != 0 else []
+    for r, s in enumerate(slices):
+        vals = (np.arange(len(s)) % 2).astype(np.uint8) if r == 0 else np.zeros(len(s), np.uint8)
+        out["per_op_on_rank0"] += [b.setbit(int(o), int(v)) for o, v in zip(s, vals)]
+    out["bytes"] = b.bytes()
+    out["op_mismatch"] = world > 1
+    return out

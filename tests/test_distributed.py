@@ -84,13 +84,14 @@ def test_global_countwith_and_bitcount_two_ranks(O):
     assert sum(ret[0][2]) == len(keys)
 
 
-def _bitset_worker(rank, world, port, ret, use_gpu):
+def _bitset_worker(rank, world, port, ret, use_gpu, scenario="main"):
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     import torch.distributed as dist
 
     from redisson_amd.cluster import HostCollective
-    from tests._sharded_scenario import OracleBitEngine, check, expected, run_scenario
+    from tests._sharded_scenario import (HostDevCollective, OracleBitEngine, check, expected, expected_route_mix,
+                                         run_route_mix, run_scenario)
 
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -101,8 +102,14 @@ def _bitset_worker(rank, world, port, ret, use_gpu):
     else:
         eng = OracleBitEngine()
     try:
-        got = run_scenario(eng, rank, world, HostCollective(dist))
-        check(got, expected(), rank, world)
+        if scenario == "route_mix":
+            coll = HostCollective(dist) if use_gpu else HostDevCollective(dist)
+            got, want = run_route_mix(eng, rank, world, coll), expected_route_mix(world)
+            for k in want:
+                assert got[k] == want[k], k
+        else:
+            got = run_scenario(eng, rank, world, HostCollective(dist))
+            check(got, expected(), rank, world)
         ret[rank] = "ok"
     except Exception as e:  # reported through the manager: the assertion text reaches the parent
         import traceback
@@ -113,12 +120,12 @@ def _bitset_worker(rank, world, port, ret, use_gpu):
         dist.destroy_process_group()
 
 
-def _run_world(world, use_gpu):
+def _run_world(world, use_gpu, scenario="main"):
     port = _free_port()
     ctx = mp.get_context("spawn")
     mgr = ctx.Manager()
     ret = mgr.dict()
-    procs = [ctx.Process(target=_bitset_worker, args=(r, world, port, ret, use_gpu)) for r in range(world)]
+    procs = [ctx.Process(target=_bitset_worker, args=(r, world, port, ret, use_gpu, scenario)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
@@ -132,6 +139,25 @@ def test_sharded_bitset_and_keyed_bitop_two_ranks():
     """C5 across GPUs, protocol on CPU: a 2^20-bit RBitSet range-sharded over 2 ranks and BITOP over keys owned by
     different ranks give one oracle store's replies and strings."""
     _run_world(2, False)
+
+
+def test_routed_bitset_mixed_call_shapes_two_ranks():
+    """the device router (set_dev / get_dev) on CPU at world 2 with ranks that set vs clear, want replies
+    vs not, pass per-op values vs one value -- one oracle store's replies and string; different operations raise on
+    every rank instead of mismatching the collectives."""
+    _run_world(2, False, "route_mix")
+
+
+@pytest.mark.gpu
+def test_routed_bitset_mixed_call_shapes_rccl_world1(engine):
+    """The same call shapes through the engine's RCCL communicator at world 1 (sk_route_bits + sk_alltoallv)."""
+    from redisson_amd.cluster import RcclCollective
+    from tests._sharded_scenario import expected_route_mix, run_route_mix
+
+    coll = RcclCollective(engine, 0, 1)
+    got, want = run_route_mix(engine, 0, 1, coll), expected_route_mix(1)
+    for k in want:
+        assert got[k] == want[k], k
 
 
 @pytest.mark.gpu

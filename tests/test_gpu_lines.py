@@ -217,3 +217,35 @@ def test_lines_reply_default_flips(leng, O):
         if seed == 1:
             assert not want.any()
     _check_regs(leng, names, regs)
+
+
+def test_lines_dropped_ids_reply_zero_after_majority_one(leng, O):
+    """a slab id the store never handed out is dropped by the region pass and replies 0, also when the
+    call's default reply (the previous call's majority) is 1 -- the default fill runs before the region pass."""
+    nkeys, n = 64, 400_000
+    names = [b"ln:x:%d" % i for i in range(nkeys)]
+    rng = np.random.default_rng(10)
+    regs = np.zeros((nkeys, 16384), dtype=np.uint8)
+    ids = leng.hll_resolve(names)
+    for call, seed in enumerate((0x5EED100B, 0x5EED100C)):
+        off, buf = gen_jackson_longs(seed, n)
+        kid = rng.integers(0, nkeys, n).astype(np.uint32)
+        dev_ids = ids[kid].astype(np.uint32)
+        bad = np.zeros(n, dtype=bool)
+        if call == 1:                                  # fresh elements again: the default is 1 from call 0
+            bad[rng.choice(n, 5000, replace=False)] = True
+            dev_ids[bad] = 0x00FFFFF0                  # a slab id far above every slab handed out
+        d = [leng.to_device(dev_ids), leng.to_device(off), leng.to_device(buf, pad=16), leng.alloc(n)]
+        leng.pfadd_dev(n, d[0], d[1], d[2], int(off[-1]), d[3])
+        got = d[3].download(np.uint8, n)
+        for x in d:
+            x.free()
+        keep = ~bad
+        sub_off = np.concatenate([np.zeros(1, np.uint64), np.cumsum(np.diff(off)[keep], dtype=np.uint64)])
+        sub_buf = np.concatenate([buf[off[i]:off[i + 1]] for i in np.flatnonzero(keep)] + [np.zeros(16, np.uint8)])
+        regs, want = _oracle_from(O, regs, kid[keep], sub_off, sub_buf, nkeys)
+        if call == 0:
+            assert want.mean() > 0.5, "the first call must leave a majority of 1 replies"
+        assert not got[bad].any(), "dropped ids must reply 0"
+        assert np.array_equal(got[keep], want), "call %d" % call
+    _check_regs(leng, names, regs)

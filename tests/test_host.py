@@ -149,3 +149,32 @@ def test_jni_shim_typechecks_against_the_abi():
     exported = set(re.findall(r"Java_org_redisson_gpu_SketchNative_(\w+)", shim))
     exported |= set(re.findall(r"(?:BLOOM_OP|KEY_U64_OUT)\((\w+),", shim))
     assert natives <= exported, natives - exported
+
+
+def test_java_executors_cover_every_reference_executor_family():
+    """SURVEY 8(b) callers: one engine executor per executor class the reference constructs (CommandSyncService for
+    Redisson, CommandReactiveService for RedissonReactive, CommandBatchService for RBatch / RBatchReactive / the
+    internal batches), all routed by SketchRouter; the RBitSet.length() script digest the Java router matches is the
+    one the RESP front-end matches (no JDK here: source-level checks)."""
+    import re
+
+    gpu = os.path.join(ROOT, "java", "org", "redisson", "gpu")
+
+    def src(name):
+        return open(os.path.join(gpu, name)).read()
+
+    assert re.search(r"class GpuSketchCommandService extends CommandSyncService implements SketchRouter\.RedisPath",
+                     src("GpuSketchCommandService.java"))
+    assert re.search(r"class GpuSketchReactiveService extends CommandReactiveService implements "
+                     r"SketchRouter\.RedisPath", src("GpuSketchReactiveService.java"))
+    assert re.search(r"class GpuSketchBatchService extends CommandBatchService", src("GpuSketchBatchService.java"))
+    for f in ("GpuSketchCommandService.java", "GpuSketchReactiveService.java"):
+        assert "SketchRouter.submit(ctx, this," in src(f), f
+    assert "public Future<Void> executeAsyncVoid()" in src("GpuSketchBatchService.java")
+    digest = re.search(r'LENGTH_SCRIPT_SHA1 = "([0-9a-f]{40})"', src("SketchRouter.java")).group(1)
+    resp = open(os.path.join(ROOT, "redisson_amd", "csrc", "sk_resp.cpp")).read()
+    assert re.search(r'kScriptBitsetLength = "%s"' % digest, resp)
+    integ = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    for site in ("M:Redisson.java:118", "M:RedissonReactive.java:106", "M:RedissonBatch.java:61",
+                 "M:reactive/RedissonBatchReactive.java:51", "M:RedissonBitSet.java:204,223"):
+        assert site in integ, site

@@ -176,29 +176,8 @@ __device__ __forceinline__ uint64_t xmerge(uint64_t acc, uint64_t v) {
     return acc * SK_XP1 + SK_XP4;
 }
 
-template <class R> __device__ __forceinline__ uint64_t xxh64_r(const R &rd, uint32_t len) {
-    const uint64_t seed = 0;
-    uint64_t h;
-    uint32_t pos = 0, rem = len;
-    if (len >= 32) {
-        uint64_t v1 = seed + SK_XP1 + SK_XP2, v2 = seed + SK_XP2, v3 = seed, v4 = seed - SK_XP1;
-        do {
-            v1 = xround(v1, rd.u64(pos));
-            v2 = xround(v2, rd.u64(pos + 8));
-            v3 = xround(v3, rd.u64(pos + 16));
-            v4 = xround(v4, rd.u64(pos + 24));
-            pos += 32;
-            rem -= 32;
-        } while (rem >= 32);
-        h = rotl(v1, 1) + rotl(v2, 7) + rotl(v3, 12) + rotl(v4, 18);
-        h = xmerge(h, v1);
-        h = xmerge(h, v2);
-        h = xmerge(h, v3);
-        h = xmerge(h, v4);
-    } else {
-        h = seed + SK_XP5;
-    }
-    h += len;
+// the part after the stripes: h already holds the stripes' merge (or seed + P5) plus len; bytes [pos, pos + rem)
+template <class R> __device__ __forceinline__ uint64_t xxh64_tail(const R &rd, uint64_t h, uint32_t pos, uint32_t rem) {
     while (rem >= 8) {
         h ^= xround(0, rd.u64(pos));
         h = rotl(h, 27) * SK_XP1 + SK_XP4;
@@ -226,6 +205,30 @@ template <class R> __device__ __forceinline__ uint64_t xxh64_r(const R &rd, uint
     h *= SK_XP3;
     h ^= h >> 32;
     return h;
+}
+template <class R> __device__ __forceinline__ uint64_t xxh64_r(const R &rd, uint32_t len) {
+    const uint64_t seed = 0;
+    uint64_t h;
+    uint32_t pos = 0, rem = len;
+    if (len >= 32) {
+        uint64_t v1 = seed + SK_XP1 + SK_XP2, v2 = seed + SK_XP2, v3 = seed, v4 = seed - SK_XP1;
+        do {
+            v1 = xround(v1, rd.u64(pos));
+            v2 = xround(v2, rd.u64(pos + 8));
+            v3 = xround(v3, rd.u64(pos + 16));
+            v4 = xround(v4, rd.u64(pos + 24));
+            pos += 32;
+            rem -= 32;
+        } while (rem >= 32);
+        h = rotl(v1, 1) + rotl(v2, 7) + rotl(v3, 12) + rotl(v4, 18);
+        h = xmerge(h, v1);
+        h = xmerge(h, v2);
+        h = xmerge(h, v3);
+        h = xmerge(h, v4);
+    } else {
+        h = seed + SK_XP5;
+    }
+    return xxh64_tail(rd, h + len, pos, rem);
 }
 __device__ __forceinline__ uint64_t xxh64(const uint8_t *p, uint32_t len) { return xxh64_r(GlobalReader{p}, len); }
 
@@ -311,8 +314,9 @@ __device__ __forceinline__ uint64_t uo_H(uint64_t x, uint64_t y, uint64_t mul, i
     return rotr(b, r) * mul;
 }
 
-// farmhashuo::Hash64WithSeeds(s, len, 81, 0) for len > 64
-template <class R> __device__ __noinline__ uint64_t farm_uo_long(const R &rd, uint32_t len) {
+// farmhashuo::Hash64WithSeeds(s, len, 81, 0) for len > 64 (inlined into the out-of-line pair below; called from
+// the other kernels through farm_uo_long)
+template <class R> __device__ __forceinline__ uint64_t farm_uo_long_body(const R &rd, uint32_t len) {
     uint32_t s = 0;
     const uint64_t seed0 = 81, seed1 = 0;
     uint64_t x = seed0;
@@ -385,11 +389,80 @@ template <class R> __device__ __noinline__ uint64_t farm_uo_long(const R &rd, ui
                 mul, 31);
 }
 
+template <class R> __device__ __noinline__ uint64_t farm_uo_long(const R rd, uint32_t len) {
+    return farm_uo_long_body(rd, len);
+}
 template <class R> __device__ __forceinline__ uint64_t farm_uo64_r(const R &rd, uint32_t len) {
     return len <= 64 ? farm_na_short(rd, len) : farm_uo_long(rd, len);
 }
 __device__ __forceinline__ uint64_t farm_uo64(const uint8_t *s, uint32_t len) {
     return farm_uo64_r(GlobalReader{s}, len);
+}
+
+// ---------------------------------------------------------------- Bloom hash pair, shared 16-byte prefix
+// Codec-encoded elements share their first bytes: every Jackson Long is `["java.lang.Long",<digits>]`, 20-39 B
+// (SURVEY A3), and a typed object starts with its class name.  For 33 <= len <= 63, XXH64 runs one 32-byte stripe,
+// whose lanes v1 / v2 take bytes 0-15 alone, and farmhashna's 33-64 path multiplies bytes 0-7 by K2 and combines
+// them with bytes 8-15 before anything else.  So an element whose first 16 bytes equal a block-uniform pattern
+// (taken from the block's first element, precomputed on the scalar unit) reuses v1, v2, their merge terms and
+// farm's prefix terms: 9 of its ~40 64-bit multiplies.  Any other element takes the full functions.  Results are
+// identical either way (the same arithmetic, evaluated once per block instead of once per element).
+struct BloomPre {
+    uint64_t w0, w1;       // the pattern: bytes 0-7 and 8-15
+    uint64_t R12, M1, M2;  // XXH64: rotl(v1, 1) + rotl(v2, 7); xround(0, v1); xround(0, v2)
+    uint64_t FA, FY0, FZ0; // farmhashna 33-64: a = w0 * K2; rotr(a + w1, 43); a + rotr(w1 + K2, 18)
+};
+__device__ __forceinline__ uint64_t uniform64(uint64_t x) {
+    return uint64_t(__builtin_amdgcn_readfirstlane(uint32_t(x))) |
+           (uint64_t(__builtin_amdgcn_readfirstlane(uint32_t(x >> 32))) << 32);
+}
+// w0 / w1: the same 16 bytes in every lane of the wave (the block's first element, read by every lane)
+__device__ __forceinline__ BloomPre bloom_pre(uint64_t w0, uint64_t w1) {
+    BloomPre p;
+    p.w0 = uniform64(w0);
+    p.w1 = uniform64(w1);
+    const uint64_t v1 = xround(SK_XP1 + SK_XP2, p.w0), v2 = xround(SK_XP2, p.w1);
+    p.R12 = rotl(v1, 1) + rotl(v2, 7);
+    p.M1 = xround(0, v1);
+    p.M2 = xround(0, v2);
+    p.FA = p.w0 * SK_K2;
+    p.FY0 = rotr(p.FA + p.w1, 43);
+    p.FZ0 = p.FA + rotr(p.w1 + SK_K2, 18);
+    return p;
+}
+// the generic pair, out of line: elements off the shared prefix are rare in a codec's batch, and keeping this code
+// out of the hash kernels' round loop keeps the loop unrolled and its registers spill-free
+template <class R> __device__ __noinline__ P2 bloom_hash_pair(const R rd, uint32_t len) {
+    return P2{xxh64_r(rd, len), len <= 64 ? farm_na_short(rd, len) : farm_uo_long_body(rd, len)}; // a leaf: no stack
+}
+template <class R>
+__device__ __forceinline__ void bloom_hashes_pre(const R &rd, uint32_t len, const BloomPre &pre, uint64_t *h1,
+                                                 uint64_t *h2) {
+    if (len >= 33 && len <= 63 && rd.u64(0) == pre.w0 && rd.u64(8) == pre.w1) {
+        // XXH64 (xxh64_r): one stripe with v1 / v2 from the pattern
+        const uint64_t b2 = rd.u64(16), b3 = rd.u64(24);
+        const uint64_t v3 = xround(0, b2), v4 = xround(0 - SK_XP1, b3);
+        uint64_t h = pre.R12 + rotl(v3, 12) + rotl(v4, 18);
+        h = (h ^ pre.M1) * SK_XP1 + SK_XP4; // xmerge(h, v1)
+        h = (h ^ pre.M2) * SK_XP1 + SK_XP4; // xmerge(h, v2)
+        h = xmerge(h, v3);
+        h = xmerge(h, v4);
+        *h1 = xxh64_tail(rd, h + len, 32, len - 32);
+        // farmhashna::Hash64, 33 <= len <= 64 (farm_na_short) with a / b from the pattern
+        const uint64_t mul = SK_K2 + uint64_t(len) * 2;
+        const uint64_t c = rd.u64(len - 8) * mul;
+        const uint64_t d = rd.u64(len - 16) * SK_K2;
+        const uint64_t y = pre.FY0 + rotr(c, 30) + d;
+        const uint64_t z = hl16(y, pre.FZ0 + c, mul);
+        const uint64_t e = b2 * mul, f = b3;
+        const uint64_t g = (y + rd.u64(len - 32)) * mul;
+        const uint64_t hh = (z + rd.u64(len - 24)) * mul;
+        *h2 = hl16(rotr(e + f, 43) + rotr(g, 30) + hh, e + rotr(f + pre.FA, 18) + g, mul);
+        return;
+    }
+    const P2 h = bloom_hash_pair(rd, len);
+    *h1 = h.first;
+    *h2 = h.second;
 }
 
 // ---------------------------------------------------------------- misc

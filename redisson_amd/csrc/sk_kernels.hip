@@ -1860,6 +1860,9 @@ __global__ void __launch_bounds__(256) k_bloom_contains_q(uint64_t n, const uint
 // Regions of one XCD are consecutive (blockIdx % 8 -> XCD under round-robin
 // dispatch; speed only, never correctness): the ~32 workgroups an XCD runs at
 // once read neighbouring segments of each block chunk, which share lines.
+#ifndef SK_BLOOM_PRE
+#define SK_BLOOM_PRE 1                // shared-prefix hash path (sk_device.h bloom_hashes_pre)
+#endif
 #define RC_RB 20                      // region = 2^20 bits = 128 KiB
 #define RC_TPB 1024
 #define RC_EPB 4096                   // elements per hash block (12-bit element-in-block)
@@ -1884,7 +1887,9 @@ static_assert(ra_bufw(4096, RA_K4) * 8 + RA_NRMAX * 4 <= 150 * 1024 && RA_K4 <= 
 static_assert(RC_TPB == SK_PFP_TPB, "key windows sized for SK_PFP_TPB threads");
 
 // ADD: AEPB = the add's elements per block (4096 for k <= RA_K4, else 2048)
-template <bool ADD, uint32_t AEPB = 2048>
+// CPM: contains probes held per element (6 for k <= 7, the bench's C3 filter; else RC_PMAX): the probes' indexes
+// and ranks stay in registers across the block's rounds, so holding no more than needed keeps the kernel spill-free
+template <bool ADD, uint32_t AEPB = 2048, uint32_t CPM = RC_PMAX>
 __global__ void __launch_bounds__(RC_TPB) k_bloom_rc_hash(uint64_t n, const uint64_t *__restrict__ off,
                                                           const uint8_t *__restrict__ bytes, uint64_t size,
                                                           uint64_t magic, uint32_t P, uint32_t NR, uint32_t NB,
@@ -1892,7 +1897,8 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_rc_hash(uint64_t n, const uint
                                                           uint8_t *__restrict__ out, uint32_t *__restrict__ flag,
                                                           uint32_t piece) {
     constexpr uint32_t EPB = ADD ? AEPB : RC_EPB;
-    constexpr uint32_t PM = ADD ? (AEPB == 4096 ? RA_K4 : RC_PMAX) : RC_PMAX; // probes per element held
+    constexpr uint32_t PM = ADD ? (AEPB == 4096 ? RA_K4 : RC_PMAX) : CPM; // probes per element held
+    static_assert(PM <= RC_PMAX, "probes held");
     static_assert(!ADD || AEPB == 2048 || AEPB == 4096, "add blocks");
     constexpr int ROUNDS = int(EPB / RC_TPB);
     constexpr uint32_t RB = ADD ? RA_RB : RC_RB, NRMAX = ADD ? RA_NRMAX : RC_NRMAX, RPT = NRMAX / RC_TPB;
@@ -1909,48 +1915,71 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_rc_hash(uint64_t n, const uint
     const uint64_t base = uint64_t(jb) * EPB;
     const uint64_t rounds = (n - base + RC_TPB - 1) / RC_TPB;
     const int nr = rounds < ROUNDS ? int(rounds) : ROUNDS;
-    uint64_t wb[ROUNDS + 1], oa[ROUNDS], ob[ROUNDS];
+    uint64_t wb[ROUNDS + 1];
 #pragma unroll
     for (int e = 0; e <= ROUNDS; e++) {
         uint64_t i0 = base + uint64_t(e) * RC_TPB;
         wb[e] = off[i0 < n ? i0 : n];
     }
-#pragma unroll
-    for (int e = 0; e < ROUNDS; e++) {
-        uint64_t i = base + uint64_t(e) * RC_TPB + threadIdx.x;
-        oa[e] = ob[e] = 0;
+    // this thread's element offsets, one round ahead (the next round's are loaded while this round hashes; holding
+    // all rounds' offsets in registers made the kernel spill)
+    uint64_t oa_c = 0, ob_c = 0;
+    {
+        const uint64_t i = base + threadIdx.x;
         if (i < n) {
-            oa[e] = off[i];
-            ob[e] = off[i + 1];
+            oa_c = off[i];
+            ob_c = off[i + 1];
         }
     }
     uint4 v[SK_PFP_WVEC];
-    if (pfp_win_fits(wb[0], wb[1])) {
+    const bool fit0 = pfp_win_fits(wb[0], wb[1]);
+    if (fit0) {
         pfp_win_load(bytes, wb[0], wb[1], v);
         pfp_win_store(wb[0], wb[1], v, win[0]);
     }
     __syncthreads(); // hist zeroed, window 0 staged
+#if SK_BLOOM_PRE
+    // the block's first element's 16 leading bytes: the shared-prefix pattern (bloom_hashes_pre)
+    const BloomPre bpre = fit0 ? bloom_pre(LdsReader{win[0], uint32_t(wb[0] & 15u)}.u64(0),
+                                          LdsReader{win[0], uint32_t(wb[0] & 15u)}.u64(8))
+                              : bloom_pre(ldu64(bytes + wb[0]), ldu64(bytes + wb[0] + 8));
+#endif
     // probe p of round e: bit index (< 2^32: sizes <= 4,294,967,294) and its rank in its region
-    uint32_t ix[ROUNDS][RC_PMAX], rk[ROUNDS][RC_PMAX / 2]; // u16 ranks, two per word
+    uint32_t ix[ROUNDS][PM], rk[ROUNDS][(PM + 1) / 2]; // u16 ranks, two per word
 #pragma unroll
     for (int e = 0; e < ROUNDS; e++) {
 #pragma unroll
-        for (int q = 0; q < RC_PMAX; q++) ix[e][q] = 0;
+        for (int q = 0; q < int(PM); q++) ix[e][q] = 0;
 #pragma unroll
-        for (int q = 0; q < RC_PMAX / 2; q++) rk[e][q] = 0;
+        for (int q = 0; q < int(PM + 1) / 2; q++) rk[e][q] = 0;
         if (e >= nr) continue; // uniform
         bool pre = e + 1 < nr && pfp_win_fits(wb[e + 1], wb[e + 2]);
         if (pre) pfp_win_load(bytes, wb[e + 1], wb[e + 2], v);
+        uint64_t oa_n = 0, ob_n = 0;
+        if (e + 1 < nr) {
+            const uint64_t i1 = base + uint64_t(e + 1) * RC_TPB + threadIdx.x;
+            if (i1 < n) {
+                oa_n = off[i1];
+                ob_n = off[i1 + 1];
+            }
+        }
+        const uint64_t oa = oa_c, ob = ob_c;
+        oa_c = oa_n;
+        ob_c = ob_n;
         uint64_t i = base + uint64_t(e) * RC_TPB + threadIdx.x;
         if (i < n) {
-            uint32_t len = uint32_t(ob[e] - oa[e]);
+            uint32_t len = uint32_t(ob - oa);
             uint64_t h1, h2;
             if (pfp_win_fits(wb[e], wb[e + 1])) {
-                LdsReader rd{win[e & 1], uint32_t(wb[e] & 15u) + uint32_t(oa[e] - wb[e])};
+                LdsReader rd{win[e & 1], uint32_t(wb[e] & 15u) + uint32_t(oa - wb[e])};
+#if SK_BLOOM_PRE
+                bloom_hashes_pre(rd, len, bpre, &h1, &h2);
+#else
                 h1 = xxh64_r(rd, len);
                 h2 = farm_uo64_r(rd, len);
+#endif
             } else {
-                bloom_hashes(bytes + oa[e], len, &h1, &h2);
+                bloom_hashes(bytes + oa, len, &h1, &h2);
             }
             if (!ADD) out[i] = 1;
             BloomIdx bi(h1, h2, size, magic);
@@ -1993,7 +2022,7 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_rc_hash(uint64_t n, const uint
         uint64_t i = base + uint64_t(e) * RC_TPB + threadIdx.x;
         if (e >= nr || i >= n) continue;
 #pragma unroll
-        for (int p = 0; p < RC_PMAX; p++) {
+        for (int p = 0; p < int(PM); p++) {
             if (uint32_t(p) >= P) break;
             uint32_t idx = ix[e][p], rank = (rk[e][p >> 1] >> ((p & 1) * 16)) & 0xffffu;
             const uint32_t el = uint32_t(e) * RC_TPB + threadIdx.x;
@@ -3151,8 +3180,12 @@ hipError_t launch_bloom_rc_hash(hipStream_t st, uint64_t n, const uint64_t *off,
                                 uint64_t magic, int k, uint32_t *S, uint32_t *recs, uint8_t *out) {
     if (!n) return hipSuccess;
     uint32_t NB = rc_blocks(n);
-    hipLaunchKernelGGL(k_bloom_rc_hash<false>, dim3(8 * ((NB + 7) / 8)), dim3(RC_TPB), 0, st, n, off, bytes, size,
-                       magic, uint32_t(k - 1), rc_regions(size), NB, S, recs, out, nullptr, 0u);
+    if (k - 1 <= 6)
+        hipLaunchKernelGGL((k_bloom_rc_hash<false, 2048, 6>), dim3(8 * ((NB + 7) / 8)), dim3(RC_TPB), 0, st, n, off,
+                           bytes, size, magic, uint32_t(k - 1), rc_regions(size), NB, S, recs, out, nullptr, 0u);
+    else
+        hipLaunchKernelGGL(k_bloom_rc_hash<false>, dim3(8 * ((NB + 7) / 8)), dim3(RC_TPB), 0, st, n, off, bytes, size,
+                           magic, uint32_t(k - 1), rc_regions(size), NB, S, recs, out, nullptr, 0u);
     SK_LAUNCH_CHECK();
     return hipSuccess;
 }

@@ -247,3 +247,45 @@ def test_region_add_late_piece_falls_back_in_order(O):
             x.free()
     finally:
         eng.close()
+
+
+def test_region_shared_prefix_mixed_elements(O, monkeypatch):
+    """The hash blocks' shared-prefix path (sk_device.h bloom_hashes_pre): elements that match the block's 16-byte
+    pattern with every length around the 33..63 window, elements differing in one byte of the pattern, and blocks
+    whose first element is not a Jackson Long (the pattern is someone else's bytes) -- add replies, contains replies
+    and the bit array equal the oracle's on the region schedule (forced for every batch size)."""
+    monkeypatch.setenv("SK_BLOOM_RC_MIN", "1")
+    monkeypatch.setenv("SK_BLOOM_RA_MIN", "1")
+    rng = np.random.default_rng(77)
+    pref = b'["java.lang.Long",'
+    elems = []
+    for i in range(30000):
+        r = i % 6
+        if r == 0:
+            elems.append(b'["java.lang.Long",%d]' % int(rng.integers(-(1 << 63), 1 << 63)))
+        elif r == 1:   # the pattern, then any length 16..80
+            elems.append(pref[:16] + bytes(rng.integers(48, 58, int(rng.integers(0, 65)), dtype=np.uint8)))
+        elif r == 2:   # one byte of the 16 differs
+            e = bytearray(b'["java.lang.Long",%d]' % int(rng.integers(0, 1 << 62)))
+            e[int(rng.integers(0, 16))] ^= 0x20
+            elems.append(bytes(e))
+        elif r == 3:   # random bytes, 0..90
+            elems.append(rng.integers(0, 256, int(rng.integers(0, 91)), dtype=np.uint8).tobytes())
+        elif r == 4:   # quoted strings (the String codec form)
+            elems.append(b'"%s"' % (b"k" * int(rng.integers(0, 60))))
+        else:
+            elems.append(b'["java.lang.Long",%d]' % int(rng.integers(0, 1000)))
+    order = rng.permutation(len(elems))
+    elems = [elems[i] for i in order]
+    eng = _engine()
+    try:
+        assert eng.bloom_try_init("pref", 40000, 0.01)
+        size, k, _, _ = eng.bloom_config("pref")
+        ref = O.BitString(16)
+        half = len(elems) // 2
+        assert eng.bloom_add("pref", size, k, elems[:half]) == ref.bloom_add(size, k, elems[:half])
+        probe = elems[half // 2:] + [e + b"x" for e in elems[:2000]]
+        assert eng.bloom_contains("pref", size, k, probe) == ref.bloom_contains(size, k, probe)
+        assert eng.get("pref") == ref.bytes()
+    finally:
+        eng.close()

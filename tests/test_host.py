@@ -178,3 +178,37 @@ def test_java_executors_cover_every_reference_executor_family():
     for site in ("M:Redisson.java:118", "M:RedissonReactive.java:106", "M:RedissonBatch.java:61",
                  "M:reactive/RedissonBatchReactive.java:51", "M:RedissonBitSet.java:204,223"):
         assert site in integ, site
+
+
+def test_hot_path_kernels_use_no_scratch():
+    """Every engine kernel on the bench's paths (PFADD, Bloom, PFCOUNT / union) runs without private (scratch) memory:
+    their per-element state stays in registers and LDS.  A round-4 build whose Bloom hash kernels spilled (272 B per
+    lane) faulted the GPU, so a spill in these kernels is refused at build time.  Reads the gfx950 code object's
+    AMDGPU metadata out of the built object (clang-offload-bundler + llvm-readelf; no GPU)."""
+    import re
+    import subprocess
+    import tempfile
+
+    import yaml
+
+    obj = os.path.join(ROOT, "build", "obj", "sk_kernels.o")
+    if not os.path.exists(obj):
+        pytest.skip("engine not built")
+    llvm = "/opt/rocm/lib/llvm/bin"
+    with tempfile.TemporaryDirectory() as d:
+        fb, co = os.path.join(d, "fb.bin"), os.path.join(d, "k.co")
+        subprocess.run([f"{llvm}/llvm-objcopy", f"--dump-section=.hip_fatbin={fb}", obj, os.path.join(d, "x.o")],
+                       check=True)
+        subprocess.run([f"{llvm}/clang-offload-bundler", "--unbundle", "--type=o", f"--input={fb}",
+                        "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"], check=True)
+        notes = subprocess.run([f"{llvm}/llvm-readelf", "--notes", co], check=True, capture_output=True,
+                               text=True).stdout
+    meta = yaml.safe_load(notes[notes.index("---"):notes.rindex("...")])
+    hot = re.compile(r"k_(bloom_rc|bloom_ra|pfl_|pfp_|hll_sum|hll_hist|hll_union|getbit|setbit|bitcount|bitop)")
+    seen = 0
+    for k in meta["amdhsa.kernels"]:
+        if hot.search(k[".name"]):
+            seen += 1
+            assert k[".private_segment_fixed_size"] == 0, (k[".name"], k[".private_segment_fixed_size"])
+            assert not k.get(".uses_dynamic_stack", False), k[".name"]
+    assert seen >= 20, seen

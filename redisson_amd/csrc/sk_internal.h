@@ -101,7 +101,11 @@ uint64_t rc_chunk_words(int k);
 hipError_t launch_bloom_rc_hash(hipStream_t st, uint64_t n, const uint64_t *off, const uint8_t *bytes, uint64_t size,
                                 uint64_t magic, int k, uint32_t *S, uint32_t *recs, uint8_t *out);
 hipError_t launch_bloom_rc_probe(hipStream_t st, uint64_t n, uint64_t size, int k, const uint32_t *S,
-                                 const uint32_t *recs, const uint8_t *bits, uint64_t cap_bytes, uint8_t *out);
+                                 const uint32_t *recs, const uint8_t *bits, uint64_t cap_bytes, uint8_t *out,
+                                 uint32_t *Z, uint32_t *GT);
+// contains zero lists (k_bloom_rc_probe -> k_bloom_rc_zero): u32 words of the per-region lists and the group table
+uint64_t rc_zero_list_words(uint64_t size);
+uint64_t rc_group_table_words(uint64_t size);
 // Bloom add, region schedule: pieces of <= ra_piece() elements; k <= rc_max_probes()
 uint32_t ra_blocks(uint64_t n, int k);
 uint32_t ra_regions(uint64_t size);

@@ -1972,7 +1972,11 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_rc_hash(uint64_t n, const uint
             uint64_t h1, h2;
             if (pfp_win_fits(wb[e], wb[e + 1])) {
                 LdsReader rd{win[e & 1], uint32_t(wb[e] & 15u) + uint32_t(oa - wb[e])};
-#if SK_BLOOM_PRE
+#if SK_RC_ABL & 8
+                (void)rd;
+                h1 = (oa + len) * 0x9e3779b97f4a7c15ull;
+                h2 = (h1 ^ (h1 >> 29)) * 0xbf58476d1ce4e5b9ull;
+#elif SK_BLOOM_PRE
                 bloom_hashes_pre(rd, len, bpre, &h1, &h2);
 #else
                 h1 = xxh64_r(rd, len);
@@ -2050,9 +2054,12 @@ __device__ __forceinline__ uint32_t rc_region(uint32_t b, uint32_t NR) {
 // LDS while they are in flight.
 #define RC_SEGV 4
 #define RC_JB 2
+#ifndef SK_RC_ABL
+#define SK_RC_ABL 0 // dev ablations (results discarded): 1 no reply stores, 2 no record loads, 4 no region load, 8 no hash
+#endif
 __device__ __forceinline__ void rc_test(const uint8_t *fb, uint32_t x, uint8_t *ob) {
     uint32_t bit = x >> 12;
-    if (!((fb[bit >> 3] >> (7u - (bit & 7u))) & 1u)) ob[x & 0xfffu] = 0;
+    if (!((fb[bit >> 3] >> (7u - (bit & 7u))) & 1u) && (!(SK_RC_ABL & 1) || x == 0xffffffffu)) ob[x & 0xfffu] = 0;
 }
 // Per thread: the segment-table words of every block it serves are loaded up front (with the region's own
 // stream); then the record vectors of RC_JB segments are loaded one step ahead of the segments being tested,
@@ -2066,8 +2073,17 @@ __device__ __forceinline__ void rc_load_seg(const uint32_t *chunks, uint64_t CH,
     uint32_t st = seg & 0xffffu, cnt = seg >> 16;
     const uint4 *cv = reinterpret_cast<const uint4 *>(chunks + uint64_t(j) * CH) + (st >> 2);
     uint32_t nv = ((st & 3u) + cnt + 3u) >> 2; // vectors covering the segment
+#if SK_RC_ABL & 2
+    (void)cv;
+#pragma unroll
+    for (int q = 0; q < RC_SEGV; q++) {
+        const uint32_t h = (seg ^ j) * 2654435761u + uint32_t(q) * 0x9e3779b9u;
+        w[q] = uint32_t(q) < nv ? make_uint4(h, h * 3u, h * 5u, h * 7u) : make_uint4(0, 0, 0, 0);
+    }
+#else
 #pragma unroll
     for (int q = 0; q < RC_SEGV; q++) w[q] = uint32_t(q) < nv ? cv[q] : make_uint4(0, 0, 0, 0);
+#endif
 }
 __device__ __forceinline__ void rc_test_seg(const uint8_t *fb, const uint32_t *chunks, uint64_t CH, uint32_t j,
                                             uint32_t seg, const uint4 (&w)[RC_SEGV], uint8_t *out) {
@@ -2088,14 +2104,92 @@ __device__ __forceinline__ void rc_test_seg(const uint8_t *fb, const uint32_t *c
         for (uint32_t s = inreg; s < cnt; s++) rc_test(fb, cs[s], ob);
     }
 }
+// Zero lists (SK_RC_ZL): a probe on a 0 bit no longer stores its element's reply byte (one random byte store per
+// zero hit: ~19 M per 32 M piece at C3, a third of the probe's time, r04 ablation).  The workgroup appends the
+// element's piece-local index to an LDS list instead (one LDS atomic per wave and step); at the end it counting-
+// sorts the list by reply group (RC_GB hash blocks) into the free region area and writes it as one contiguous run
+// per region, Z[region][...], with the row GT[region][group] = start | count << 16.  k_bloom_rc_zero then takes
+// one reply group per workgroup: the group's zero entries from every region go into an LDS byte map, and the
+// replies are ANDed in as coalesced 16-B vectors.  A region with more zero hits than the list holds (a sparse
+// filter) stores the rest directly, as before; the AND keeps those.
+#ifndef SK_RC_ZL
+#define SK_RC_ZL 1
+#endif
+#define RC_GB 16                         // hash blocks per reply group: 64 Ki replies, a 64 KiB LDS map
+#define RC_NG (RC_SMAX * RC_TPB / RC_GB) // reply groups per piece (<= 512)
+#define RC_ZCAP 7424                     // zero-list entries per region (LDS beside the 128 KiB region)
+static_assert((1u << (RC_RB - 3)) >= RC_ZCAP * 4, "the sorted list fits the region area");
+// the zero hits of one segment (the words the unrolled test found on 0 bits): the wave's counts are scanned, one
+// lane reserves the wave's slots, and every lane writes its entries; entries past the list's end store directly
+__device__ __forceinline__ void rc_test_seg_zl(const uint8_t *fb, const uint32_t *chunks, uint64_t CH, uint32_t j,
+                                               uint32_t seg, const uint4 (&w)[RC_SEGV], uint8_t *out, uint32_t *zl,
+                                               uint32_t *zn) {
+    const uint32_t st = seg & 0xffffu, cnt = seg >> 16, o = st & 3u;
+    constexpr uint32_t NW = 4 * RC_SEGV;
+    const uint32_t end = o + cnt < NW ? o + cnt : NW, inreg = end - o;
+    auto zero = [&](uint32_t x) {
+        const uint32_t bit = x >> 12;
+        return !((fb[bit >> 3] >> (7u - (bit & 7u))) & 1u);
+    };
+    uint32_t mask = 0;
+#pragma unroll
+    for (int q = 0; q < RC_SEGV; q++) {
+        const uint32_t t = 4u * uint32_t(q);
+        if (t >= o && t < end && zero(w[q].x)) mask |= 1u << t;
+        if (t + 1 >= o && t + 1 < end && zero(w[q].y)) mask |= 2u << t;
+        if (t + 2 >= o && t + 2 < end && zero(w[q].z)) mask |= 4u << t;
+        if (t + 3 >= o && t + 3 < end && zero(w[q].w)) mask |= 8u << t;
+    }
+    const uint32_t k = __popc(mask), lane = threadIdx.x & 63u;
+    uint32_t x = k;
+#pragma unroll
+    for (int s2 = 1; s2 < 64; s2 <<= 1) {
+        const uint32_t y = __shfl_up(x, s2);
+        if (lane >= uint32_t(s2)) x += y;
+    }
+    uint32_t base = 0;
+    if (lane == 63 && x) base = atomicAdd(zn, x);
+    base = __shfl(base, 63) + (x - k);
+    const uint32_t e0 = j * RC_EPB;
+    uint8_t *ob = out + uint64_t(j) * RC_EPB;
+    auto put = [&](uint32_t word) {
+        const uint32_t el = word & 0xfffu;
+        if (base < RC_ZCAP) zl[base] = e0 + el;
+        else ob[el] = 0;
+        base++;
+    };
+#pragma unroll
+    for (int q = 0; q < RC_SEGV; q++) {
+        const uint32_t t = 4u * uint32_t(q);
+        if (mask & (1u << t)) put(w[q].x);
+        if (mask & (2u << t)) put(w[q].y);
+        if (mask & (4u << t)) put(w[q].z);
+        if (mask & (8u << t)) put(w[q].w);
+    }
+    if (cnt > inreg) { // long segment (rare): the rest word by word, direct stores
+        const uint32_t *cs = chunks + uint64_t(j) * CH + st;
+        for (uint32_t s2 = inreg; s2 < cnt; s2++) rc_test(fb, cs[s2], ob);
+    }
+}
 __global__ void __launch_bounds__(RC_TPB) k_bloom_rc_probe(uint32_t NB, uint32_t NR, const uint32_t *__restrict__ S,
                                                            const uint32_t *__restrict__ chunks, uint32_t P,
                                                            const uint8_t *__restrict__ bits, uint64_t cap_bytes,
-                                                           uint8_t *__restrict__ out) {
+                                                           uint8_t *__restrict__ out, uint32_t *__restrict__ Z,
+                                                           uint32_t *__restrict__ GT) {
     __shared__ uint4 filt[(1u << (RC_RB - 3)) / 16];
     constexpr uint32_t NV = (1u << (RC_RB - 3)) / 16, VPT = NV / RC_TPB;
     const uint32_t r = rc_region(blockIdx.x, NR);
     if (r >= NR) return; // uniform
+#if SK_RC_ZL
+    __shared__ uint32_t zl[RC_ZCAP];
+    __shared__ uint32_t gcnt[RC_NG];
+    __shared__ uint32_t zn, wsum[RC_TPB / 64];
+    if (threadIdx.x == 0) zn = 0;
+    for (uint32_t g = threadIdx.x; g < RC_NG; g += RC_TPB) gcnt[g] = 0;
+#else
+    (void)Z;
+    (void)GT;
+#endif
     const uint64_t b0 = uint64_t(r) << (RC_RB - 3);
     const uint4 *src = reinterpret_cast<const uint4 *>(bits + b0);
     {
@@ -2103,7 +2197,12 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_rc_probe(uint32_t NB, uint32_t
 #pragma unroll
         for (uint32_t q = 0; q < VPT; q++) { // bytes past the buffer read as 0 (they are past the string)
             uint32_t v = threadIdx.x + q * RC_TPB;
+#if SK_RC_ABL & 4
+            fv[q] = make_uint4(v * 2654435761u, v, ~v, r);
+            (void)src;
+#else
             fv[q] = b0 + uint64_t(v) * 16 < cap_bytes ? ld_nt(src + v) : make_uint4(0, 0, 0, 0);
+#endif
         }
         // NB <= RC_SMAX * RC_TPB (the host cuts batches into pieces)
         uint32_t seg0[RC_SMAX];
@@ -2128,8 +2227,80 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_rc_probe(uint32_t NB, uint32_t
             if (u + RC_PF - 1 < RC_SMAX)
                 rc_load_seg(chunks, CH, threadIdx.x + (u + RC_PF - 1) * RC_TPB, seg0[u + RC_PF - 1],
                             w[(u + RC_PF - 1) % RC_PF]);
+#if SK_RC_ZL
+            rc_test_seg_zl(fb, chunks, CH, threadIdx.x + u * RC_TPB, seg0[u], w[u % RC_PF], out, zl, &zn);
+#else
             rc_test_seg(fb, chunks, CH, threadIdx.x + u * RC_TPB, seg0[u], w[u % RC_PF], out);
+#endif
         }
+    }
+#if SK_RC_ZL
+    __syncthreads(); // every test done: the list is complete and the region area is free
+    const uint32_t nz = zn < RC_ZCAP ? zn : RC_ZCAP;
+    constexpr uint32_t ZPT = (RC_ZCAP + RC_TPB - 1) / RC_TPB;
+    constexpr uint32_t GSH = 12 + 4; // log2(RC_EPB * RC_GB)
+    static_assert((RC_EPB * RC_GB) == (1u << GSH), "reply group size");
+    uint32_t zv[ZPT], zr[ZPT];
+#pragma unroll
+    for (uint32_t q = 0; q < ZPT; q++) { // rank of each entry inside its group
+        const uint32_t i = threadIdx.x + q * RC_TPB;
+        zv[q] = i < nz ? zl[i] : 0u;
+        zr[q] = i < nz ? atomicAdd(&gcnt[zv[q] >> GSH], 1u) : 0u;
+    }
+    __syncthreads();
+    const uint32_t ng = (NB + RC_GB - 1) / RC_GB;
+    const uint32_t c = threadIdx.x < ng ? gcnt[threadIdx.x] : 0u;
+    uint32_t tot;
+    const uint32_t gs = block_exscan<RC_TPB>(c, wsum, &tot);
+    if (threadIdx.x < ng) {
+        gcnt[threadIdx.x] = gs;
+        GT[uint64_t(r) * RC_NG + threadIdx.x] = gs | (c << 16);
+    }
+    __syncthreads();
+    uint32_t *sorted = reinterpret_cast<uint32_t *>(filt);
+#pragma unroll
+    for (uint32_t q = 0; q < ZPT; q++) {
+        const uint32_t i = threadIdx.x + q * RC_TPB;
+        if (i < nz) sorted[gcnt[zv[q] >> GSH] + zr[q]] = zv[q];
+    }
+    __syncthreads();
+    uint32_t *zdst = Z + uint64_t(r) * RC_ZCAP;
+    for (uint32_t i = threadIdx.x; i < nz; i += RC_TPB) zdst[i] = sorted[i];
+#endif
+}
+
+// One reply group (RC_GB hash blocks, 64 Ki elements) per workgroup: its zero entries from every region's list
+// (GT[region][group] names the run) clear bytes of an LDS map of the group's replies, which is then ANDed into out
+// with 16-B vectors.  Groups of one XCD are consecutive (speed only): their runs of one region are neighbours.
+__global__ void __launch_bounds__(RC_TPB) k_bloom_rc_zero(uint32_t NB, uint32_t NR, uint64_t n,
+                                                          const uint32_t *__restrict__ Z,
+                                                          const uint32_t *__restrict__ GT,
+                                                          uint8_t *__restrict__ out) {
+    constexpr uint32_t GE = RC_EPB * RC_GB; // replies per group
+    __shared__ uint4 mapv[GE / 16];
+    const uint32_t ng = (NB + RC_GB - 1) / RC_GB;
+    const uint32_t g = rc_region(blockIdx.x, ng);
+    if (g >= ng) return; // uniform
+    for (uint32_t v = threadIdx.x; v < GE / 16; v += RC_TPB) mapv[v] = make_uint4(~0u, ~0u, ~0u, ~0u);
+    __syncthreads();
+    uint8_t *map = reinterpret_cast<uint8_t *>(mapv);
+    for (uint32_t rr = threadIdx.x; rr < NR; rr += RC_TPB) {
+        const uint32_t t = GT[uint64_t(rr) * RC_NG + g], st = t & 0xffffu, c = t >> 16;
+        const uint32_t *zs = Z + uint64_t(rr) * RC_ZCAP + st;
+        for (uint32_t i = 0; i < c; i++) map[zs[i] & (GE - 1)] = 0;
+    }
+    __syncthreads();
+    const uint64_t e0 = uint64_t(g) * GE;
+    const uint64_t ne = n - e0 < GE ? n - e0 : GE;
+    uint8_t *ob = out + e0;
+    if ((reinterpret_cast<uintptr_t>(ob) & 15u) == 0) {
+        for (uint32_t v = threadIdx.x; v < ne / 16; v += RC_TPB) {
+            uint4 a = reinterpret_cast<const uint4 *>(ob)[v], b = mapv[v];
+            reinterpret_cast<uint4 *>(ob)[v] = make_uint4(a.x & b.x, a.y & b.y, a.z & b.z, a.w & b.w);
+        }
+        for (uint32_t i = uint32_t(ne / 16) * 16 + threadIdx.x; i < ne; i += RC_TPB) ob[i] &= map[i];
+    } else {
+        for (uint32_t i = threadIdx.x; i < ne; i += RC_TPB) ob[i] &= map[i];
     }
 }
 
@@ -3190,14 +3361,22 @@ hipError_t launch_bloom_rc_hash(hipStream_t st, uint64_t n, const uint64_t *off,
     return hipSuccess;
 }
 hipError_t launch_bloom_rc_probe(hipStream_t st, uint64_t n, uint64_t size, int k, const uint32_t *S,
-                                 const uint32_t *recs, const uint8_t *bits, uint64_t cap_bytes, uint8_t *out) {
+                                 const uint32_t *recs, const uint8_t *bits, uint64_t cap_bytes, uint8_t *out,
+                                 uint32_t *Z, uint32_t *GT) {
     if (!n) return hipSuccess;
-    uint32_t NR = rc_regions(size);
-    hipLaunchKernelGGL(k_bloom_rc_probe, dim3(8 * ((NR + 7) / 8)), dim3(RC_TPB), 0, st, rc_blocks(n), NR, S, recs,
-                       uint32_t(k - 1), bits, cap_bytes, out);
+    uint32_t NR = rc_regions(size), NB = rc_blocks(n);
+    hipLaunchKernelGGL(k_bloom_rc_probe, dim3(8 * ((NR + 7) / 8)), dim3(RC_TPB), 0, st, NB, NR, S, recs,
+                       uint32_t(k - 1), bits, cap_bytes, out, Z, GT);
     SK_LAUNCH_CHECK();
+#if SK_RC_ZL
+    const uint32_t ng = (NB + RC_GB - 1) / RC_GB;
+    hipLaunchKernelGGL(k_bloom_rc_zero, dim3(8 * ((ng + 7) / 8)), dim3(RC_TPB), 0, st, NB, NR, n, Z, GT, out);
+    SK_LAUNCH_CHECK();
+#endif
     return hipSuccess;
 }
+uint64_t rc_zero_list_words(uint64_t size) { return SK_RC_ZL ? uint64_t(rc_regions(size)) * RC_ZCAP : 1; }
+uint64_t rc_group_table_words(uint64_t size) { return SK_RC_ZL ? uint64_t(rc_regions(size)) * RC_NG : 1; }
 
 hipError_t launch_bloom_probes(hipStream_t st, uint64_t n, const uint64_t *off, const uint8_t *bytes, uint64_t size,
                                uint64_t magic, int k, uint64_t *keys) {

@@ -384,6 +384,7 @@ struct sk_ctx {
     DBuf keys_a, keys_b, vals_a, vals_b, sort_tmp, in_off, in_bytes, in_ids, in_cmd, out_u8, misc, partial, hist,
         uni, ptrs, hist_a, hist_b, ovf, bloom_h;
     DBuf rc_S, rc_rec;          // Bloom contains region schedule: segment table + probe records (contains only)
+    DBuf rc_Z, rc_GT;           // ... and its zero lists: per-region lists + the (region, reply group) run table
     DBuf long_h, long_which;    // PFADD: hashes of long elements (k_ms_rounds) and their element indexes + layout
     DBuf long_plane, long_flags; // their k bit planes and look-back flags
     uint64_t long_fallbacks = 0; // calls whose long elements were re-hashed per thread (look-back wait ran out)
@@ -1275,7 +1276,7 @@ int sk_close(sk_ctx *c) {
     }
     for (DBuf *b : {&c->keys_a, &c->keys_b, &c->vals_a, &c->vals_b, &c->sort_tmp, &c->in_off, &c->in_bytes,
                     &c->in_ids, &c->in_cmd, &c->out_u8, &c->misc, &c->partial, &c->hist, &c->uni, &c->ptrs,
-                    &c->hist_a, &c->hist_b, &c->ovf, &c->bloom_h, &c->rc_S, &c->rc_rec, &c->long_h,
+                    &c->hist_a, &c->hist_b, &c->ovf, &c->bloom_h, &c->rc_S, &c->rc_rec, &c->rc_Z, &c->rc_GT, &c->long_h,
                     &c->long_which, &c->long_plane, &c->long_flags, &c->ra_S, &c->ra_rec, &c->ra_flag, &c->ev, &c->ev_n,
                     &c->pfl_chunks, &c->pfl_S, &c->pfl_C, &c->pfl_rc, &c->rt_cnt, &c->pfl_rec, &c->pfl_bk, &c->pfl_bv,
                     &c->pfl_ovf, &c->pfl_order})
@@ -2732,6 +2733,8 @@ static int bloom_contains_launch(sk_ctx *c, hipStream_t s, uint32_t id, int64_t 
     const uint64_t nb = sk::rc_blocks(std::min(n, piece)), nr = sk::rc_regions(usize);
     HIPCHK(c, c->rc_S.ensure(nb * nr * 4));
     HIPCHK(c, c->rc_rec.ensure(nb * sk::rc_chunk_words(k) * 4));
+    HIPCHK(c, c->rc_Z.ensure(sk::rc_zero_list_words(usize) * 4));
+    HIPCHK(c, c->rc_GT.ensure(sk::rc_group_table_words(usize) * 4));
     for (uint64_t s0 = 0; s0 < n; s0 += piece) {
         uint64_t m = std::min(piece, n - s0);
         { Prof q_(c, 18, s);
@@ -2739,7 +2742,8 @@ static int bloom_contains_launch(sk_ctx *c, hipStream_t s, uint32_t id, int64_t 
                                            c->rc_rec.as<uint32_t>(), d_out + s0)); }
         { Prof q_(c, 19, s);
         HIPCHK(c, sk::launch_bloom_rc_probe(s, m, usize, k, c->rc_S.as<uint32_t>(), c->rc_rec.as<uint32_t>(),
-                                            c->strs[id].ptr, c->strs[id].cap, d_out + s0)); }
+                                            c->strs[id].ptr, c->strs[id].cap, d_out + s0, c->rc_Z.as<uint32_t>(),
+                                            c->rc_GT.as<uint32_t>())); }
     }
     return SK_OK;
 }

@@ -105,6 +105,7 @@ SIGNATURES = {
     "sk_dev_free": (c_int, [P, P]),
     "sk_h2d": (c_int, [P, P, P, c_uint64]),
     "sk_d2h": (c_int, [P, P, P, c_uint64]),
+    "sk_d2d": (c_int, [P, P, P, c_uint64]),
     "sk_dev_memset": (c_int, [P, P, c_int, c_uint64]),
     "sk_timer_record": (c_int, [P, c_int]),
     "sk_timer_elapsed": (c_int, [P, c_int, c_int, P]),
@@ -127,6 +128,8 @@ SIGNATURES = {
     "sk_alltoallv": (c_int, [P, P, _u64p, P, _u64p]),
     "sk_route_bits": (c_int, [P, c_uint64, _u64p, _u8p, c_uint64, c_int32, _u64p, _u8p, _u32p, _u64p]),
     "sk_unroute_u8": (c_int, [P, c_uint64, _u32p, _u8p, _u8p]),
+    "sk_bloom_indexes_dev": (c_int, [P, c_uint64, _u64p, _u8p, c_int64, c_int32, c_int32, _u64p]),
+    "sk_reduce_groups_u8": (c_int, [P, c_uint64, c_uint32, c_uint32, c_int, _u8p, _u8p]),
     "sk_setbit_values_dev": (c_int, [P, _u8p, c_uint64, c_uint64, _u64p, _u8p, _u8p]),
 }
 

@@ -20,6 +20,12 @@ only exchange steps are the global ones:
   operands it owns to ONE all-gather (RCCL, device buffers), and the owner of
   the destination runs the local BITOP over the gathered copies
   (north_star: "Bloom/BitSet union uses all-gather plus a local OR").
+* One RBloomFilter over several GPUs: ``RangeShardedBloom`` splits its bit
+  array by range (the RBitSet shards above): the probe indexes of a batch are
+  computed on the submitting GPU and routed to each bit's owner, so capacity
+  and add rate grow with the GPUs; ``ReplicatedBloom`` keeps a full copy on
+  every GPU (adds on all, contains split and all-gathered, device path
+  ``contains_dev``).
 
 The collective is a small interface so the same protocol runs with the
 engine's RCCL communicator on GPUs and with torch.distributed/gloo on host
@@ -617,3 +623,145 @@ class ReplicatedBloom:
         mine = self.engine.bloom_contains(self.name, size, k, list(elems[lo:hi])) if hi > lo else []
         parts = self.coll.allgather_bytes(bytes(int(x) for x in mine))
         return [bool(b) for p in parts for b in p]
+
+    def add_dev(self, n: int, d_off, d_bytes, bytes_len: int, d_out) -> None:
+        """add of a device batch (the same batch on every rank): applied to every replica, the same exact replies."""
+        self.engine.bloom_add_dev(self.name, n, d_off, d_bytes, bytes_len, d_out)
+
+    def contains_dev(self, n: int, d_off, d_bytes, bytes_len: int, d_out) -> None:
+        """contains of a device batch held by every rank, with no host copy: rank r answers elements [r*P, (r+1)*P)
+        (P = ceil(n / world)) on its replica, and one RCCL all-gather of the P-byte reply pieces lays the replies out
+        in batch order on every rank (into d_out, n bytes)."""
+        W, r = self.world, self.rank
+        P = max((n + W - 1) // W, 1)
+        lo, hi = min(r * P, n), min((r + 1) * P, n)
+        e = self.engine
+        part, recv = e.alloc(P), e.alloc(P * W)
+        try:
+            err = None
+            try:
+                if hi > lo:
+                    e.bloom_contains_dev(self.name, hi - lo, d_off.view(8 * lo), d_bytes, bytes_len, part)
+            except Exception as x:  # noqa: BLE001 - agreed on below
+                err = x
+            agree(self.coll, err)
+            self.coll.allgather_dev(part, recv, P)
+            if n:
+                e.d2d(d_out, recv, n)
+        finally:
+            part.free()
+            recv.free()
+
+
+def java_int(x: float) -> int:
+    """Java's (int) of a double: NaN -> 0, saturating, else truncation toward zero."""
+    if x != x:
+        return 0
+    if x >= 2147483647.0:
+        return 2147483647
+    if x <= -2147483648.0:
+        return -2147483648
+    return int(x)
+
+
+class RangeShardedBloom:
+    """One RBloomFilter whose bit array is range-sharded over the GPUs: rank r holds bits [r*S, (r+1)*S) of the
+    m-bit array as its local bit string `name` (the RBitSet shards of ShardedBitSet).  add / contains of a device
+    batch submitted on any rank (M:RedissonBloomFilter.java:80-168):
+      1. the probe bit indexes are computed on the submitting GPU (sk_bloom_indexes_dev: k for add, the k-1 that
+         decide contains for contains -- Q2), element-major;
+      2. they travel to the owner of each bit through the RBitSet router (sk_route_bits + RCCL all-to-all), which
+         applies them in (submitting rank, element, probe) order -- SETBIT with old-bit replies for add, GETBIT for
+         contains -- so every reply is the one redis-server gives when the ranks' batches run one after another;
+      3. the per-probe replies come back in element order and sk_reduce_groups_u8 makes one reply per element:
+         contains = AND of probes 0..k-2, add = one of probes 0..k-2 was 0.
+    Each GPU holds 1/N of the array and applies 1/N of every batch's probes, so the filter's capacity and its add
+    rate grow with N; ReplicatedBloom instead applies every add on every GPU.  Every method is SPMD: all ranks call
+    it (an empty batch is fine) with the same filter configuration."""
+
+    def __init__(self, engine, name, rank: int, world: int, coll):
+        self.engine, self.name, self.rank, self.world, self.coll = engine, name, rank, world, coll
+        self.size = self.k = 0
+        self.bits = None
+
+    def try_init(self, expected: int, fpp: float) -> bool:
+        """RedissonBloomFilter.tryInit sizing (:69-78, :223-252): False when already initialized (config replaced,
+        Q6); IllegalArgumentException above 4,294,967,294 bits (Q4)."""
+        from .engine import IllegalArgumentException, bloom_optimal_bits, bloom_optimal_k
+
+        m = bloom_optimal_bits(expected, fpp)
+        if m > 2 * 2147483647:
+            raise IllegalArgumentException("Bloom filter can't be greater than %d. But calculated size is %d"
+                                           % (2 * 2147483647, m))
+        fresh = self.bits is None
+        self.size, self.k = int(m), int(bloom_optimal_k(expected, m))
+        self.bits = ShardedBitSet(self.engine, self.name, self.size, self.rank, self.world, self.coll)
+        return fresh
+
+    def _check(self):
+        from .engine import IllegalStateException
+
+        if self.bits is None:
+            raise IllegalStateException("Bloom filter is not initialized!")
+
+    def add_dev(self, n: int, d_off, d_bytes, d_out=None) -> None:
+        """add of n device elements submitted on this rank; d_out: one reply per element (None: no replies)."""
+        self._check()
+        e, k = self.engine, self.k
+        idx, rep = e.alloc(max(8 * n * k, 8)), e.alloc(max(n * k, 1))
+        try:
+            e.bloom_indexes_dev(n, d_off, d_bytes, self.size, k, k, idx)
+            self.bits.set_dev(n * k, idx, rep if d_out is not None else None, value=1)
+            if d_out is not None and n:
+                e.reduce_groups_u8(n, k, k - 1, True, rep, d_out)
+        finally:
+            idx.free()
+            rep.free()
+
+    def contains_dev(self, n: int, d_off, d_bytes, d_out) -> None:
+        """contains of n device elements submitted on this rank (one reply per element in d_out)."""
+        self._check()
+        e, np_ = self.engine, self.k - 1
+        idx, rep = e.alloc(max(8 * n * np_, 8)), e.alloc(max(n * np_, 1))
+        try:
+            e.bloom_indexes_dev(n, d_off, d_bytes, self.size, self.k, np_, idx)
+            self.bits.get_dev(n * np_, idx, rep)
+            if n:
+                e.reduce_groups_u8(n, np_, np_, False, rep, d_out)
+        finally:
+            idx.free()
+            rep.free()
+
+    def _host(self, op, elems: Sequence[bytes]) -> List[bool]:
+        from .engine import pack
+
+        e, n = self.engine, len(elems)
+        off, buf = pack([bytes(x) for x in elems])
+        d_off, d_bytes, d_out = e.to_device(off), e.to_device(buf, pad=16), e.alloc(max(n, 1))
+        try:
+            (self.add_dev if op == "add" else self.contains_dev)(n, d_off, d_bytes, d_out)
+            return [bool(x) for x in d_out.download(np.uint8, n)]
+        finally:
+            for b in (d_off, d_bytes, d_out):
+                b.free()
+
+    def add(self, elems: Sequence[bytes]) -> List[bool]:
+        return self._host("add", elems)
+
+    def contains(self, elems: Sequence[bytes]) -> List[bool]:
+        return self._host("contains", elems)
+
+    def count(self) -> int:
+        """RedissonBloomFilter.count (:188-199): BITCOUNT over every shard, then -m/k * ln(1 - bits/m) as a Java int."""
+        import math
+
+        self._check()
+        c = self.bits.cardinality()
+        x = 1 - c / self.size
+        v = (-self.size / self.k) * (math.log(x) if x > 0 else float("-inf"))
+        return java_int(v)
+
+    def to_bytes(self) -> bytes:
+        """GET of the filter's bit array (the Redis string: every shard's bytes, up to the last non-empty one)."""
+        self._check()
+        return self.bits.to_bytes()

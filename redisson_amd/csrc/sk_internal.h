@@ -103,6 +103,10 @@ hipError_t launch_bloom_rc_hash(hipStream_t st, uint64_t n, const uint64_t *off,
 hipError_t launch_bloom_rc_probe(hipStream_t st, uint64_t n, uint64_t size, int k, const uint32_t *S,
                                  const uint32_t *recs, const uint8_t *bits, uint64_t cap_bytes, uint8_t *out,
                                  uint32_t *Z, uint32_t *GT);
+hipError_t launch_bloom_indexes(hipStream_t st, uint64_t n, const uint64_t *off, const uint8_t *bytes, uint64_t size,
+                                uint64_t magic, int np, uint64_t *idx);
+hipError_t launch_reduce_groups_u8(hipStream_t st, uint64_t n, uint32_t group, uint32_t take, uint32_t invert,
+                                   const uint8_t *in, uint8_t *out);
 // contains zero lists (k_bloom_rc_probe -> k_bloom_rc_zero): u32 words of the per-region lists and the group table
 uint64_t rc_zero_list_words(uint64_t size);
 uint64_t rc_group_table_words(uint64_t size);

@@ -1863,6 +1863,11 @@ __global__ void __launch_bounds__(256) k_bloom_contains_q(uint64_t n, const uint
 #ifndef SK_BLOOM_PRE
 #define SK_BLOOM_PRE 1                // shared-prefix hash path (sk_device.h bloom_hashes_pre)
 #endif
+#ifndef SK_RC_ABL
+// dev ablations of the contains chain (results discarded): 1 no reply stores, 2 no record loads, 4 no region load,
+// 8 no hash arithmetic, 16 no segment-table stores, 32 no record stores
+#define SK_RC_ABL 0
+#endif
 #define RC_RB 20                      // region = 2^20 bits = 128 KiB
 #define RC_TPB 1024
 #define RC_EPB 4096                   // elements per hash block (12-bit element-in-block)
@@ -2016,7 +2021,7 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_rc_hash(uint64_t n, const uint
         if (r < NR) {
             if (ADD && c4[q] > RA_SEGMAX) atomicMin(flag, piece); // the apply's windows assume short segments
             hist[r] = st;
-            S[uint64_t(r) * NB + jb] = st | (c4[q] << 16);
+            if (!(SK_RC_ABL & 16) || ADD) S[uint64_t(r) * NB + jb] = st | (c4[q] << 16);
         }
         st += c4[q];
     }
@@ -2037,7 +2042,8 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_rc_hash(uint64_t n, const uint
     __syncthreads();
     uint4 *dst = reinterpret_cast<uint4 *>(chunks + uint64_t(jb) * EPB * P);
     const uint4 *src = reinterpret_cast<const uint4 *>(lrec);
-    for (uint32_t t = threadIdx.x; t < (tot + 3) / 4; t += RC_TPB) dst[t] = src[t];
+    if (!(SK_RC_ABL & 32) || ADD)
+        for (uint32_t t = threadIdx.x; t < (tot + 3) / 4; t += RC_TPB) dst[t] = src[t];
 }
 
 // regions of XCD group x = blockIdx % 8 are [x*q, (x+1)*q), taken in order
@@ -2054,9 +2060,6 @@ __device__ __forceinline__ uint32_t rc_region(uint32_t b, uint32_t NR) {
 // LDS while they are in flight.
 #define RC_SEGV 4
 #define RC_JB 2
-#ifndef SK_RC_ABL
-#define SK_RC_ABL 0 // dev ablations (results discarded): 1 no reply stores, 2 no record loads, 4 no region load, 8 no hash
-#endif
 __device__ __forceinline__ void rc_test(const uint8_t *fb, uint32_t x, uint8_t *ob) {
     uint32_t bit = x >> 12;
     if (!((fb[bit >> 3] >> (7u - (bit & 7u))) & 1u) && (!(SK_RC_ABL & 1) || x == 0xffffffffu)) ob[x & 0xfffu] = 0;
@@ -2547,6 +2550,47 @@ __global__ void __launch_bounds__(256) k_bloom_probes(uint64_t n, const uint64_t
     for (int j = 0; j < k; j++) {
         keys[pos + j] = (bi.r << 32) | (pos + j);
         bi.next(j);
+    }
+}
+
+// Probe bit indexes of n elements, element-major: idx[i * np + j] = probe j of element i (RedissonBloomFilter.hash,
+// M:RedissonBloomFilter.java:116-131), np <= k.  The input of the range-sharded filter's router
+// (redisson_amd/cluster.py RangeShardedBloom): every probe travels to the GPU that owns its bit.
+__global__ void __launch_bounds__(256) k_bloom_indexes(uint64_t n, const uint64_t *__restrict__ off,
+                                                       const uint8_t *__restrict__ bytes, uint64_t size,
+                                                       uint64_t magic, int np, uint64_t *__restrict__ idx) {
+    __shared__ uint64_t lds[SK_STAGE_WORDS];
+    uint64_t e0 = uint64_t(blockIdx.x) * blockDim.x, e1 = e0 + blockDim.x < n ? e0 + blockDim.x : n;
+    uint64_t lo = off[e0], hi = off[e1];
+    bool staged = stage_fits(lo, hi);
+    uint32_t wbase = staged ? stage_keys(bytes, lo, hi, lds) : 0u;
+    uint64_t i = e0 + threadIdx.x;
+    if (i >= n) return;
+    uint64_t o = off[i];
+    uint32_t len = uint32_t(off[i + 1] - o);
+    uint64_t h1, h2;
+    if (staged) {
+        LdsReader rd{lds, wbase + uint32_t(o - lo)};
+        h1 = xxh64_r(rd, len);
+        h2 = farm_uo64_r(rd, len);
+    } else {
+        bloom_hashes(bytes + o, len, &h1, &h2);
+    }
+    BloomIdx bi(h1, h2, size, magic);
+    for (int j = 0; j < np; j++) {
+        idx[i * uint64_t(np) + j] = bi.r;
+        bi.next(j);
+    }
+}
+// out[i] = AND(in[i * group .. i * group + take)) ^ invert: a contains reply (AND of probes 0..k-2) or an add reply
+// (one of probes 0..k-2 replied 0) from per-probe bits in element-major order
+__global__ void __launch_bounds__(256) k_reduce_groups_u8(uint64_t n, uint32_t group, uint32_t take, uint32_t invert,
+                                                          const uint8_t *__restrict__ in, uint8_t *__restrict__ out) {
+    for (uint64_t i = uint64_t(blockIdx.x) * 256 + threadIdx.x; i < n; i += uint64_t(gridDim.x) * 256) {
+        const uint8_t *p = in + i * group;
+        uint32_t a = 1;
+        for (uint32_t j = 0; j < take; j++) a &= p[j] ? 1u : 0u;
+        out[i] = uint8_t(a ^ invert);
     }
 }
 
@@ -3382,6 +3426,22 @@ hipError_t launch_bloom_probes(hipStream_t st, uint64_t n, const uint64_t *off, 
                                uint64_t magic, int k, uint64_t *keys) {
     if (!n) return hipSuccess;
     hipLaunchKernelGGL(k_bloom_probes, dim3(grid_for(n, 256)), dim3(256), 0, st, n, off, bytes, size, magic, k, keys);
+    SK_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+hipError_t launch_bloom_indexes(hipStream_t st, uint64_t n, const uint64_t *off, const uint8_t *bytes, uint64_t size,
+                                uint64_t magic, int np, uint64_t *idx) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k_bloom_indexes, dim3(grid_for(n, 256)), dim3(256), 0, st, n, off, bytes, size, magic, np, idx);
+    SK_LAUNCH_CHECK();
+    return hipSuccess;
+}
+hipError_t launch_reduce_groups_u8(hipStream_t st, uint64_t n, uint32_t group, uint32_t take, uint32_t invert,
+                                   const uint8_t *in, uint8_t *out) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k_reduce_groups_u8, dim3(grid_for(n, 256, 8192)), dim3(256), 0, st, n, group, take, invert, in,
+                       out);
     SK_LAUNCH_CHECK();
     return hipSuccess;
 }

@@ -2268,6 +2268,28 @@ int sk_unroute_u8(sk_ctx *c, uint64_t n, const uint32_t *d_dst, const uint8_t *d
     return sync(c);
 }
 
+// The range-sharded Bloom filter's device steps (redisson_amd/cluster.py RangeShardedBloom): the probe indexes of
+// a batch, routed like SETBIT / GETBIT, and the per-element reduction of the probes' replies
+int sk_bloom_indexes_dev(sk_ctx *c, uint64_t n, const uint64_t *d_off, const uint8_t *d_bytes, int64_t size, int32_t k,
+                         int32_t nprobe, uint64_t *d_idx) {
+    std::lock_guard<std::mutex> g(c->mu);
+    ENTER(c);
+    if (size <= 0 || k <= 0 || nprobe < 0 || nprobe > k)
+        return fail(c, SK_EINVAL, "bloom indexes: size %lld, k %d, nprobe %d", (long long)size, k, nprobe);
+    if (!n || !nprobe) return SK_OK;
+    HIPCHK(c, sk::launch_bloom_indexes(c->st, n, d_off, d_bytes, uint64_t(size), magic_for(uint64_t(size)), nprobe,
+                                       d_idx));
+    return sync(c);
+}
+int sk_reduce_groups_u8(sk_ctx *c, uint64_t n, uint32_t group, uint32_t take, int invert, const uint8_t *d_in,
+                        uint8_t *d_out) {
+    std::lock_guard<std::mutex> g(c->mu);
+    ENTER(c);
+    if (take > group) return fail(c, SK_EINVAL, "reduce groups: take %u > group %u", take, group);
+    HIPCHK(c, sk::launch_reduce_groups_u8(c->st, n, group, take, invert ? 1u : 0u, d_in, d_out));
+    return sync(c);
+}
+
 // SETBIT of a device batch with one value per op (d_values u8[n]); replies (old bits) in d_out_old when given
 int sk_setbit_values_dev(sk_ctx *c, const uint8_t *key, uint64_t len, uint64_t n, const uint64_t *d_offsets,
                          const uint8_t *d_values, uint8_t *d_out_old) {
@@ -2904,6 +2926,11 @@ int sk_h2d(sk_ctx *c, void *dst, const void *src, uint64_t n) {
 int sk_d2h(sk_ctx *c, void *dst, const void *src, uint64_t n) {
     std::lock_guard<std::mutex> g(c->mu);
     if (n) HIPCHK(c, hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, c->st));
+    return sync(c);
+}
+int sk_d2d(sk_ctx *c, void *dst, const void *src, uint64_t n) {
+    std::lock_guard<std::mutex> g(c->mu);
+    if (n) HIPCHK(c, hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToDevice, c->st));
     return sync(c);
 }
 int sk_dev_memset(sk_ctx *c, void *p, int v, uint64_t n) {

@@ -76,11 +76,28 @@ class DeviceBuffer:
             self.engine.lib.sk_dev_free(self.engine.ctx, self.ptr)
         self.ptr = 0
 
+    def view(self, offset: int, nbytes: int = -1) -> "DeviceView":
+        """Bytes [offset, offset + nbytes) of this allocation, without ownership (freeing a view is a no-op)."""
+        return DeviceView(self.engine, self.ptr + offset, self.nbytes - offset if nbytes < 0 else nbytes)
+
     def __del__(self):
         try:
             self.free()
         except Exception:
             pass
+
+
+class DeviceView(DeviceBuffer):
+    """A range of an engine allocation (DeviceBuffer.view): the same upload / download / zero, no ownership."""
+
+    def __init__(self, engine: "SketchEngine", ptr: int, nbytes: int):  # noqa: D107 - no allocation
+        self.engine, self.ptr, self.nbytes = engine, int(ptr), int(nbytes)
+
+    def free(self):
+        self.ptr = 0
+
+    def __del__(self):
+        pass
 
 
 def pack(items: Sequence[bytes]):
@@ -429,6 +446,19 @@ class SketchEngine:
         self._check(self.lib.sk_route_bits(self.ctx, n, _addr(d_offsets), _addr(d_values), int(shard_bits), world,
                                            _addr(d_send), _addr(d_send_values), _addr(d_dst), _addr(out)))
         return out
+
+    def bloom_indexes_dev(self, n: int, d_off, d_bytes, size: int, k: int, nprobe: int, d_idx):
+        """Probe bit indexes of n device elements, element-major u64[n * nprobe] (sk_bloom_indexes_dev)."""
+        self._check(self.lib.sk_bloom_indexes_dev(self.ctx, n, _addr(d_off), _addr(d_bytes), int(size), int(k),
+                                                  int(nprobe), _addr(d_idx)))
+
+    def reduce_groups_u8(self, n: int, group: int, take: int, invert: bool, d_in, d_out):
+        """d_out[i] = AND(d_in[i * group .. i * group + take)) ^ invert (sk_reduce_groups_u8)."""
+        self._check(self.lib.sk_reduce_groups_u8(self.ctx, n, group, take, 1 if invert else 0, _addr(d_in),
+                                                 _addr(d_out)))
+
+    def d2d(self, d_dst, d_src, n: int):
+        self._check(self.lib.sk_d2d(self.ctx, _addr(d_dst), _addr(d_src), n))
 
     def unroute_u8(self, n: int, d_dst, d_rep, d_out):
         self._check(self.lib.sk_unroute_u8(self.ctx, n, _addr(d_dst), _addr(d_rep), _addr(d_out)))

@@ -246,9 +246,15 @@ class HostBuf:
 
     def zero(self):
         self.a[:] = 0
+        return self
 
     def free(self):
         pass
+
+    def view(self, offset, nbytes=-1):
+        v = HostBuf(0)
+        v.a = self.a[offset:] if nbytes < 0 else self.a[offset:offset + nbytes]
+        return v
 
 
 class OracleBitEngine:
@@ -297,10 +303,33 @@ class OracleBitEngine:
     def alloc(self, nbytes):
         return HostBuf(nbytes)
 
-    def to_device(self, arr):
-        b = HostBuf(np.ascontiguousarray(arr).nbytes)
+    def to_device(self, arr, pad=0):
+        b = HostBuf(np.ascontiguousarray(arr).nbytes + pad)
         b.upload(arr)
         return b
+
+    def d2d(self, dst, src, n):
+        dst.a[:n] = src.a[:n]
+
+    # -------- the range-sharded / replicated Bloom filter's device steps
+    @staticmethod
+    def _elems(n, d_off, d_bytes):
+        off = d_off.download(np.uint64, n + 1)
+        raw = d_bytes.a
+        return [raw[int(off[i]):int(off[i + 1])].tobytes() for i in range(n)]
+
+    def bloom_indexes_dev(self, n, d_off, d_bytes, size, k, nprobe, d_idx):
+        if n and nprobe:
+            idx = [self.O.bloom_indexes(e, k, size)[:nprobe] for e in self._elems(n, d_off, d_bytes)]
+            d_idx.upload(np.asarray(idx, dtype=np.uint64).ravel())
+
+    def reduce_groups_u8(self, n, group, take, invert, d_in, d_out):
+        v = d_in.download(np.uint8, n * group).reshape(n, group)[:, :take] if group else np.zeros((n, 0), np.uint8)
+        d_out.upload((v.all(axis=1) ^ bool(invert)).astype(np.uint8))
+
+    def bloom_contains_dev(self, name, n, d_off, d_bytes, bytes_len, d_out):
+        size, k, _, _ = self.bloom_config(name)
+        d_out.upload(np.asarray(self.bloom_contains(name, size, k, self._elems(n, d_off, d_bytes)), np.uint8))
 
     def hll_union_dev(self, n, d_ids, d_out):
         ids = d_ids.download(np.uint32, n)
@@ -420,8 +449,9 @@ class OracleBitEngine:
 
 
 class HostDevCollective:
-    """HostCollective plus the RCCL collective's alltoallv_dev over HostBufs (gloo underneath), so the CPU tests run
-    ShardedBitSet's device router (set_dev / get_dev) on an OracleBitEngine."""
+    """HostCollective plus the RCCL collective's device-buffer calls (alltoallv_dev, allgather_dev) through the
+    buffers' download / upload and gloo, so the device protocols (ShardedBitSet's router, RangeShardedBloom,
+    ReplicatedBloom.contains_dev) run on an OracleBitEngine on the CPU and on engine contexts sharing one GPU."""
 
     def __init__(self, dist):
         from redisson_amd.cluster import HostCollective
@@ -433,11 +463,16 @@ class HostDevCollective:
     def alltoallv_dev(self, send, send_bytes, recv, recv_bytes):
         sb = np.asarray(send_bytes, dtype=np.int64)
         cut = np.concatenate([[0], np.cumsum(sb)])
-        got = self.h.alltoallv_bytes([send.a[cut[p]:cut[p + 1]].tobytes() for p in range(len(sb))])
+        flat_send = send.download(np.uint8, int(cut[-1])) if cut[-1] else np.zeros(0, np.uint8)
+        got = self.h.alltoallv_bytes([flat_send[cut[p]:cut[p + 1]].tobytes() for p in range(len(sb))])
         assert [len(g) for g in got] == [int(x) for x in recv_bytes], "alltoallv sizes disagree"
         flat = b"".join(got)
         if flat:
             recv.upload(np.frombuffer(flat, np.uint8))
+
+    def allgather_dev(self, send, recv, nbytes):
+        parts = self.h.allgather_bytes(send.download(np.uint8, nbytes).tobytes())
+        recv.upload(np.frombuffer(b"".join(parts), np.uint8))
 
 
 def run_route_mix(engine, rank, world, coll):
@@ -497,4 +532,61 @@ def expected_route_mix(world):
         out["per_op_on_rank0"] += [b.setbit(int(o), int(v)) for o, v in zip(s, vals)]
     out["bytes"] = b.bytes()
     out["op_mismatch"] = world > 1
+    return out
+
+
+BLOOM_ADDS = [b'["java.lang.Long",%d]' % (i * 7919) for i in range(3000)]
+BLOOM_PROBE = [b'["java.lang.Long",%d]' % (i * 7919) for i in range(0, 6000, 3)] + [b'"x%d"' % i for i in range(500)]
+
+
+def run_bloom_shard(engine, rank, world, coll):
+    """one filter range-sharded over the ranks (RangeShardedBloom: adds and contains submitted on
+    every rank, routed to the bits' owners) and one replicated filter answering a device batch (contains_dev)."""
+    from redisson_amd.cluster import RangeShardedBloom, ReplicatedBloom
+    from redisson_amd.engine import pack
+
+    def mine(x):
+        return x[rank * len(x) // world:(rank + 1) * len(x) // world]
+
+    def gathered(rep):
+        return [bool(v) for part in coll.allgather_bytes(np.asarray(rep, np.uint8).tobytes()) for v in part]
+
+    out = {}
+    rb = RangeShardedBloom(engine, b"rsb:c3", rank, world, coll)
+    out["init"] = [rb.try_init(20000, 0.01), rb.try_init(20000, 0.01)]
+    out["cfg"] = (rb.size, rb.k)
+    out["add1"] = gathered(rb.add(mine(BLOOM_ADDS[:2000])))
+    out["add2"] = gathered(rb.add(mine(BLOOM_ADDS[1000:])))   # repeats reply False
+    out["contains"] = gathered(rb.contains(mine(BLOOM_PROBE)))
+    out["empty"] = rb.contains([])                            # an empty batch on every rank
+    out["bytes"] = rb.to_bytes()
+    out["count"] = rb.count()
+    rp = ReplicatedBloom(engine, b"rpb:c3", rank, world, coll)
+    rp.try_init(20000, 0.01)
+    rp.add(BLOOM_ADDS[:1500])
+    off, buf = pack(BLOOM_PROBE)
+    d_off, d_bytes, d_out = engine.to_device(off), engine.to_device(buf, pad=16), engine.alloc(len(BLOOM_PROBE))
+    rp.contains_dev(len(BLOOM_PROBE), d_off, d_bytes, int(off[-1]), d_out)
+    out["rep_contains_dev"] = [bool(v) for v in d_out.download(np.uint8, len(BLOOM_PROBE))]
+    for b in (d_off, d_bytes, d_out):
+        b.free()
+    return out
+
+
+def expected_bloom_shard():
+    from oracle import oracle as O
+
+    m = O.bloom_optimal_bits(20000, 0.01)
+    k = O.bloom_optimal_k(20000, m)
+    b = O.BitString(16)
+    out = {"init": [True, False], "cfg": (m, k)}
+    out["add1"] = [bool(x) for x in b.bloom_add(m, k, BLOOM_ADDS[:2000])]
+    out["add2"] = [bool(x) for x in b.bloom_add(m, k, BLOOM_ADDS[1000:])]
+    out["contains"] = [bool(x) for x in b.bloom_contains(m, k, BLOOM_PROBE)]
+    out["empty"] = []
+    out["bytes"] = b.bytes()
+    out["count"] = O.bloom_count(m, k, b.bitcount())
+    r = O.BitString(16)
+    r.bloom_add(m, k, BLOOM_ADDS[:1500])
+    out["rep_contains_dev"] = [bool(x) for x in r.bloom_contains(m, k, BLOOM_PROBE)]
     return out

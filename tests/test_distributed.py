@@ -90,8 +90,8 @@ def _bitset_worker(rank, world, port, ret, use_gpu, scenario="main"):
     import torch.distributed as dist
 
     from redisson_amd.cluster import HostCollective
-    from tests._sharded_scenario import (HostDevCollective, OracleBitEngine, check, expected, expected_route_mix,
-                                         run_route_mix, run_scenario)
+    from tests._sharded_scenario import (HostDevCollective, OracleBitEngine, check, expected, expected_bloom_shard,
+                                         expected_route_mix, run_bloom_shard, run_route_mix, run_scenario)
 
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -102,7 +102,12 @@ def _bitset_worker(rank, world, port, ret, use_gpu, scenario="main"):
     else:
         eng = OracleBitEngine()
     try:
-        if scenario == "route_mix":
+        if scenario == "bloom_shard":
+            coll = HostDevCollective(dist)
+            got, want = run_bloom_shard(eng, rank, world, coll), expected_bloom_shard()
+            for k in want:
+                assert got[k] == want[k], k
+        elif scenario == "route_mix":
             coll = HostCollective(dist) if use_gpu else HostDevCollective(dist)
             got, want = run_route_mix(eng, rank, world, coll), expected_route_mix(world)
             for k in want:
@@ -146,6 +151,32 @@ def test_routed_bitset_mixed_call_shapes_two_ranks():
     vs not, pass per-op values vs one value -- one oracle store's replies and string; different operations raise on
     every rank instead of mismatching the collectives."""
     _run_world(2, False, "route_mix")
+
+
+def test_range_sharded_bloom_two_ranks():
+    """VERDICT r3 item 6, protocol on CPU: one RBloomFilter range-sharded over 2 ranks (probe indexes routed to the
+    bits' owners, replies reduced per element) gives one oracle filter's add / contains replies, bit array and count;
+    a replicated filter answers a device batch split over the ranks and all-gathered."""
+    _run_world(2, False, "bloom_shard")
+
+
+@pytest.mark.gpu
+def test_range_sharded_bloom_engine_two_ranks_one_gpu():
+    """The same on two engine contexts (two processes sharing the GPU; device buffers exchanged over gloo)."""
+    _run_world(2, True, "bloom_shard")
+
+
+@pytest.mark.gpu
+def test_range_sharded_bloom_rccl_world1(engine):
+    """The same through the engine's RCCL communicator at world 1 (sk_bloom_indexes_dev, sk_route_bits,
+    sk_alltoallv, sk_reduce_groups_u8, the all-gather of contains_dev)."""
+    from redisson_amd.cluster import RcclCollective
+    from tests._sharded_scenario import expected_bloom_shard, run_bloom_shard
+
+    coll = RcclCollective(engine, 0, 1)
+    got, want = run_bloom_shard(engine, 0, 1, coll), expected_bloom_shard()
+    for k in want:
+        assert got[k] == want[k], k
 
 
 @pytest.mark.gpu

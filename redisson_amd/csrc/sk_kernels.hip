@@ -1865,7 +1865,7 @@ __global__ void __launch_bounds__(256) k_bloom_contains_q(uint64_t n, const uint
 #endif
 #ifndef SK_RC_ABL
 // dev ablations of the contains chain (results discarded): 1 no reply stores, 2 no record loads, 4 no region load,
-// 8 no hash arithmetic, 16 no segment-table stores, 32 no record stores
+// 8 no hash arithmetic, 16 no segment-table stores, 32 no record stores, 64 no add reply stores
 #define SK_RC_ABL 0
 #endif
 #define RC_RB 20                      // region = 2^20 bits = 128 KiB
@@ -2273,37 +2273,56 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_rc_probe(uint32_t NB, uint32_t
 }
 
 // One reply group (RC_GB hash blocks, 64 Ki elements) per workgroup: its zero entries from every region's list
-// (GT[region][group] names the run) clear bytes of an LDS map of the group's replies, which is then ANDed into out
-// with 16-B vectors.  Groups of one XCD are consecutive (speed only): their runs of one region are neighbours.
-__global__ void __launch_bounds__(RC_TPB) k_bloom_rc_zero(uint32_t NB, uint32_t NR, uint64_t n,
-                                                          const uint32_t *__restrict__ Z,
-                                                          const uint32_t *__restrict__ GT,
-                                                          uint8_t *__restrict__ out) {
+// (GT[region][group] names the run) clear bits of an 8 KiB LDS bitmap of the group's replies, which is then ANDed
+// into out with 16-B vectors.  Each thread's run descriptors are loaded up front (independent loads in flight), and
+// groups of one XCD are consecutive (speed only): their runs of one region are neighbours.
+#define RC_ZTPB 512
+__global__ void __launch_bounds__(RC_ZTPB) k_bloom_rc_zero(uint32_t NB, uint32_t NR, uint64_t n,
+                                                           const uint32_t *__restrict__ Z,
+                                                           const uint32_t *__restrict__ GT,
+                                                           uint8_t *__restrict__ out) {
     constexpr uint32_t GE = RC_EPB * RC_GB; // replies per group
-    __shared__ uint4 mapv[GE / 16];
+    constexpr uint32_t RPT = RC_NRMAX / RC_ZTPB;
+    __shared__ uint32_t bm[GE / 32];
     const uint32_t ng = (NB + RC_GB - 1) / RC_GB;
     const uint32_t g = rc_region(blockIdx.x, ng);
     if (g >= ng) return; // uniform
-    for (uint32_t v = threadIdx.x; v < GE / 16; v += RC_TPB) mapv[v] = make_uint4(~0u, ~0u, ~0u, ~0u);
+    uint32_t t[RPT];
+#pragma unroll
+    for (uint32_t q = 0; q < RPT; q++) {
+        const uint32_t rr = threadIdx.x + q * RC_ZTPB;
+        t[q] = rr < NR ? GT[uint64_t(rr) * RC_NG + g] : 0u;
+    }
+    for (uint32_t v = threadIdx.x; v < GE / 32; v += RC_ZTPB) bm[v] = ~0u;
     __syncthreads();
-    uint8_t *map = reinterpret_cast<uint8_t *>(mapv);
-    for (uint32_t rr = threadIdx.x; rr < NR; rr += RC_TPB) {
-        const uint32_t t = GT[uint64_t(rr) * RC_NG + g], st = t & 0xffffu, c = t >> 16;
+#pragma unroll
+    for (uint32_t q = 0; q < RPT; q++) {
+        const uint32_t rr = threadIdx.x + q * RC_ZTPB, st = t[q] & 0xffffu, c = t[q] >> 16;
         const uint32_t *zs = Z + uint64_t(rr) * RC_ZCAP + st;
-        for (uint32_t i = 0; i < c; i++) map[zs[i] & (GE - 1)] = 0;
+        for (uint32_t i = 0; i < c; i++) {
+            const uint32_t e = zs[i] & (GE - 1);
+            atomicAnd(&bm[e >> 5], ~(1u << (e & 31u)));
+        }
     }
     __syncthreads();
     const uint64_t e0 = uint64_t(g) * GE;
     const uint64_t ne = n - e0 < GE ? n - e0 : GE;
     uint8_t *ob = out + e0;
+    // reply byte i &= bit i: 16 replies per 16-B vector from one 16-bit piece of the bitmap
+    auto spread = [](uint32_t b4) { // 4 bits -> 4 bytes of 0 / 1
+        return (b4 & 1u) | ((b4 & 2u) << 7) | ((b4 & 4u) << 14) | ((b4 & 8u) << 21);
+    };
     if ((reinterpret_cast<uintptr_t>(ob) & 15u) == 0) {
-        for (uint32_t v = threadIdx.x; v < ne / 16; v += RC_TPB) {
-            uint4 a = reinterpret_cast<const uint4 *>(ob)[v], b = mapv[v];
-            reinterpret_cast<uint4 *>(ob)[v] = make_uint4(a.x & b.x, a.y & b.y, a.z & b.z, a.w & b.w);
+        for (uint32_t v = threadIdx.x; v < ne / 16; v += RC_ZTPB) {
+            const uint32_t w16 = (bm[v >> 1] >> ((v & 1u) * 16u)) & 0xffffu;
+            const uint4 a = reinterpret_cast<const uint4 *>(ob)[v];
+            reinterpret_cast<uint4 *>(ob)[v] = make_uint4(a.x & spread(w16 & 15u), a.y & spread((w16 >> 4) & 15u),
+                                                          a.z & spread((w16 >> 8) & 15u), a.w & spread(w16 >> 12));
         }
-        for (uint32_t i = uint32_t(ne / 16) * 16 + threadIdx.x; i < ne; i += RC_TPB) ob[i] &= map[i];
+        for (uint32_t i = uint32_t(ne / 16) * 16 + threadIdx.x; i < ne; i += RC_ZTPB)
+            ob[i] &= uint8_t((bm[i >> 5] >> (i & 31u)) & 1u);
     } else {
-        for (uint32_t i = threadIdx.x; i < ne; i += RC_TPB) ob[i] &= map[i];
+        for (uint32_t i = threadIdx.x; i < ne; i += RC_ZTPB) ob[i] &= uint8_t((bm[i >> 5] >> (i & 31u)) & 1u);
     }
 }
 
@@ -2496,7 +2515,7 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_ra_apply(uint32_t NB, uint32_t
             }
             if (!f) continue;
             first |= 1u << q;
-            if (!(xu & 1u)) out[uint64_t(blk[u]) * AEPB + ((xu >> 1) & (AEPB - 1))] = 1;
+            if (!(xu & 1u) && (!(SK_RC_ABL & 64) || xu == 0xfffffffeu)) out[uint64_t(blk[u]) * AEPB + ((xu >> 1) & (AEPB - 1))] = 1;
         }
         __syncthreads(); // every probe of the window has read the bits
 #pragma unroll 1
@@ -3414,7 +3433,7 @@ hipError_t launch_bloom_rc_probe(hipStream_t st, uint64_t n, uint64_t size, int 
     SK_LAUNCH_CHECK();
 #if SK_RC_ZL
     const uint32_t ng = (NB + RC_GB - 1) / RC_GB;
-    hipLaunchKernelGGL(k_bloom_rc_zero, dim3(8 * ((ng + 7) / 8)), dim3(RC_TPB), 0, st, NB, NR, n, Z, GT, out);
+    hipLaunchKernelGGL(k_bloom_rc_zero, dim3(8 * ((ng + 7) / 8)), dim3(RC_ZTPB), 0, st, NB, NR, n, Z, GT, out);
     SK_LAUNCH_CHECK();
 #endif
     return hipSuccess;

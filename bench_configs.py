@@ -456,6 +456,57 @@ def host(eng, args):
     t_dev = timed(eng, lambda: eng.pfadd_dev(B, dk, do_, db, int(batches[1][0][-1]), dout), reps=3)
     for x in (dk, do_, db, dout):
         x.free()
+    # the prefix form (what the Java coalescers send for a codec's shared type header): the same batches with the
+    # 18-byte Jackson Long header sent once and only the suffixes + u32 offsets per element
+    plen = 18
+
+    def suffix_form(eoff, ebuf):
+        n_ = len(eoff) - 1
+        mask = np.zeros(len(ebuf), dtype=bool)
+        mask[(eoff[:-1, None].astype(np.int64) + np.arange(plen)).ravel()] = True
+        mask[int(eoff[-1]):] = True
+        sbuf = np.concatenate([ebuf[~mask], np.zeros(16, np.uint8)])
+        soff = (eoff.astype(np.int64) - np.arange(n_ + 1) * plen).astype(np.uint32)
+        return soff, sbuf
+    preb = np.frombuffer(batches[1][1][int(batches[1][0][0]):int(batches[1][0][0]) + plen].tobytes(), np.uint8).copy()
+    sforms = [suffix_form(*b) for b in batches]
+
+    def pfx(r):
+        soff, sbuf = sforms[r]
+        eng._check(lib.sk_pfadd_ids_prefix(ctx, B, kids.ctypes.data, preb.ctypes.data, plen, soff.ctypes.data,
+                                           sbuf.ctypes.data, out.ctypes.data))
+    pfx(0)
+    t_pfx = timed(eng, lambda: [pfx(r) for r in range(1, reps + 1)]) / reps
+    gsoff, gsbuf = suffix_form(gof, gbuf)
+
+    def grp_pfx():
+        eng._check(lib.sk_pfadd_ids_prefix(ctx, B * G, gids.ctypes.data, preb.ctypes.data, plen, gsoff.ctypes.data,
+                                           gsbuf.ctypes.data, gout.ctypes.data))
+    grp_pfx()
+    t_grp_pfx = timed(eng, grp_pfx, reps=2)
+    pin = eng.host_alloc(gids.nbytes + gsoff.nbytes + gsbuf.nbytes + 64)
+    views, at = [], 0
+    for a in (gids, gsoff, gsbuf):
+        v = pin[at:at + a.nbytes].view(a.dtype)
+        v[:] = a
+        views.append(v)
+        at += (a.nbytes + 15) // 16 * 16
+    pids, psoff, psbuf = views
+
+    def grp_pfx_pinned():
+        eng._check(lib.sk_pfadd_ids_prefix(ctx, B * G, pids.ctypes.data, preb.ctypes.data, plen, psoff.ctypes.data,
+                                           psbuf.ctypes.data, gout.ctypes.data))
+    t_grp_pfx_pin = timed(eng, grp_pfx_pinned, reps=2)
+    del views, pids, psoff, psbuf
+    eng.host_free(pin)
+    pforms = [suffix_form(*p_) for p_ in probe]
+
+    def ctp(r):
+        soff, sbuf = pforms[r]
+        eng._check(lib.sk_bloom_contains_prefix(ctx, nm, len(nm), size, k, B, preb.ctypes.data, plen,
+                                                soff.ctypes.data, sbuf.ctypes.data, out.ctypes.data))
+    ctp(0)
+    t_ctp = timed(eng, lambda: [ctp(r) for r in range(reps)]) / reps
     # raw pageable H2D rate of one PFADD batch's element bytes (diagnostic for the rates above)
     raw = batches[1][1]
     t_h2d = timed(eng, lambda: eng.to_device(raw).free(), reps=3)
@@ -466,7 +517,12 @@ def host(eng, args):
           "group_commit_ids_host_per_s": B * G / t_grp, "group_commit_ids_pinned_per_s": B * G / t_grp_pin,
           "group_commit": "%d RBatches of 1M PFADDs as one sk_pfadd_ids call (host buffers, cached slab ids; the "
                           "pinned: the same inputs in sk_host_alloc memory)" % G,
-          "pfadd_ids_ms_per_batch": t_pfi * 1e3, "bloom_add_host_per_s": B / t_add, "bloom_contains_host_per_s": B / t_ct,
+          "pfadd_ids_ms_per_batch": t_pfi * 1e3,
+          "prefix_form": "the same inputs with the 18-B Jackson Long header sent once (sk_pfadd_ids_prefix, "
+                         "sk_bloom_contains_prefix): suffixes + u32 offsets cross the link",
+          "pfadd_ids_prefix_host_per_s": B / t_pfx, "pfadd_ids_prefix_ms_per_batch": t_pfx * 1e3,
+          "group_commit_prefix_host_per_s": B * G / t_grp_pfx, "group_commit_prefix_pinned_per_s": B * G / t_grp_pfx_pin,
+          "bloom_contains_prefix_host_per_s": B / t_ctp, "bloom_add_host_per_s": B / t_add, "bloom_contains_host_per_s": B / t_ct,
           "pfadd_ms_per_batch": t_pf * 1e3, "bloom_contains_ms_per_batch": t_ct * 1e3,
           "pfadd_h2d_bytes": int(h2d_pf), "pageable_h2d_GBps": raw.nbytes / t_h2d / 1e9,
           "pfadd_dev_ms_per_batch": t_dev * 1e3, "contains_h2d_bytes": int(h2d_bl),

@@ -138,6 +138,14 @@ int sk_pfadd(sk_ctx *ctx, uint32_t n_cmds, const uint64_t *key_off, const uint8_
  * round trip of M:RedissonHyperLogLog.java:66-68 / M:RedissonBatch.java:76-83. */
 int sk_pfadd_ids(sk_ctx *ctx, uint32_t n_cmds, const uint32_t *key_ids, const uint32_t *elem_counts,
                  const uint64_t *elem_off, const uint8_t *elem_bytes, uint8_t *out_changed);
+/* Host ingress in prefix form (the group-commit path of GpuBatchCoalescer and the Bloom coalescer): n one-element
+ * commands whose elements share the byte prefix prefix[0..prefix_len) (prefix_len <= 255: a codec's type header --
+ * every Jackson Long is ["java.lang.Long",<digits>]); element i = prefix followed by suffix bytes
+ * [suffix_off[i], suffix_off[i+1]) (u32 offsets into suffix_bytes, which keeps >= 16 B of readable padding).  Only
+ * the suffixes and the u32 offsets cross the host link; the elements are rebuilt on the device and the replies are
+ * those of the same commands through sk_pfadd_ids / sk_bloom_add / sk_bloom_contains. */
+int sk_pfadd_ids_prefix(sk_ctx *ctx, uint32_t n, const uint32_t *key_ids, const uint8_t *prefix, uint32_t prefix_len,
+                        const uint32_t *suffix_off, const uint8_t *suffix_bytes, uint8_t *out_changed);
 /* PFADD of one element per command, keys pre-resolved to slab ids (all
  * existing); device-resident inputs.  d_out_changed u8[n] on device.
  * Replies are the sequential replies of the n commands in order, so a caller
@@ -266,6 +274,12 @@ int sk_bloom_add(sk_ctx *ctx, const uint8_t *name, uint64_t len, int64_t size, i
                  const uint64_t *elem_off, const uint8_t *elem_bytes, uint8_t *out);
 int sk_bloom_contains(sk_ctx *ctx, const uint8_t *name, uint64_t len, int64_t size, int32_t k, uint32_t n,
                       const uint64_t *elem_off, const uint8_t *elem_bytes, uint8_t *out);
+int sk_bloom_add_prefix(sk_ctx *ctx, const uint8_t *name, uint64_t len, int64_t size, int32_t k, uint32_t n,
+                        const uint8_t *prefix, uint32_t prefix_len, const uint32_t *suffix_off,
+                        const uint8_t *suffix_bytes, uint8_t *out);
+int sk_bloom_contains_prefix(sk_ctx *ctx, const uint8_t *name, uint64_t len, int64_t size, int32_t k, uint32_t n,
+                             const uint8_t *prefix, uint32_t prefix_len, const uint32_t *suffix_off,
+                             const uint8_t *suffix_bytes, uint8_t *out);
 int sk_bloom_add_dev(sk_ctx *ctx, const uint8_t *name, uint64_t len, uint64_t n, const uint64_t *d_elem_off,
                      const uint8_t *d_elem_bytes, uint64_t elem_bytes_len, uint8_t *d_out);
 int sk_bloom_contains_dev(sk_ctx *ctx, const uint8_t *name, uint64_t len, uint64_t n, const uint64_t *d_elem_off,

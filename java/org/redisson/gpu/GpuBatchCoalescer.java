@@ -217,9 +217,18 @@ public final class GpuBatchCoalescer {
                 idv[i] = okIds.get(i);
                 cnt[i] = counts.get(i);
             }
-            SketchDispatch.Packed e = new SketchDispatch.Packed(flat);
             byte[] sub = new byte[idv.length];
-            st = idv.length == 0 ? SketchNative.SK_OK : SketchNative.pfaddIds(ctx, idv, cnt, e.off, e.bytes, sub);
+            // one-element commands sharing a codec prefix (every Jackson Long): the prefix form ships only the
+            // suffixes and u32 offsets over the host link (sk_pfadd_ids_prefix); anything else the full form
+            SketchDispatch.PrefixPacked pp = flat.size() == idv.length ? SketchDispatch.PrefixPacked.of(flat, 8) : null;
+            if (idv.length == 0) {
+                st = SketchNative.SK_OK;
+            } else if (pp != null) {
+                st = SketchNative.pfaddIdsPrefix(ctx, idv, pp.prefix, pp.off, pp.suffixes, sub);
+            } else {
+                SketchDispatch.Packed e = new SketchDispatch.Packed(flat);
+                st = SketchNative.pfaddIds(ctx, idv, cnt, e.off, e.bytes, sub);
+            }
             if (st == SketchNative.SK_ESTALE && attempt == 0) {
                 ids.clear();
                 continue;

@@ -121,10 +121,20 @@ public final class GpuBloomCoalescer implements Runnable {
         for (Req r : run) {
             all.addAll(Arrays.asList(r.elems));
         }
-        SketchDispatch.Packed e = new SketchDispatch.Packed(all);
         byte[] out = new byte[all.size()];
-        int st = head.add ? SketchNative.bloomAdd(ctx, head.name, head.size, head.k, e.off, e.bytes, out)
-                : SketchNative.bloomContains(ctx, head.name, head.size, head.k, e.off, e.bytes, out);
+        // elements sharing a codec prefix go in prefix form (only the suffixes cross the host link)
+        SketchDispatch.PrefixPacked pp = SketchDispatch.PrefixPacked.of(all, 8);
+        int st;
+        if (pp != null) {
+            st = head.add ? SketchNative.bloomAddPrefix(ctx, head.name, head.size, head.k, pp.prefix, pp.off,
+                                                        pp.suffixes, out)
+                    : SketchNative.bloomContainsPrefix(ctx, head.name, head.size, head.k, pp.prefix, pp.off,
+                                                       pp.suffixes, out);
+        } else {
+            SketchDispatch.Packed e = new SketchDispatch.Packed(all);
+            st = head.add ? SketchNative.bloomAdd(ctx, head.name, head.size, head.k, e.off, e.bytes, out)
+                    : SketchNative.bloomContains(ctx, head.name, head.size, head.k, e.off, e.bytes, out);
+        }
         if (st != SketchNative.SK_OK) {
             RuntimeException ex = st == SketchNative.SK_ENOTINIT ? new IllegalStateException(SketchNative.lastError(ctx))
                     : new RedisException(SketchNative.lastError(ctx));

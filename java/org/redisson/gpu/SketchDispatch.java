@@ -41,6 +41,51 @@ public final class SketchDispatch {
         }
     }
 
+    /* Elements in prefix form (sk_pfadd_ids_prefix / sk_bloom_*_prefix): the longest prefix every element shares
+     * (<= 255 bytes; a codec's type header such as ["java.lang.Long",) and the suffixes with u32 offsets.  Only the
+     * suffixes cross the host link; the engine rebuilds the elements on the device. */
+    public static final class PrefixPacked {
+        public final byte[] prefix;
+        public final int[] off;
+        public final byte[] suffixes;
+
+        PrefixPacked(List<byte[]> items, int plen) {
+            prefix = java.util.Arrays.copyOf(items.get(0), plen);
+            off = new int[items.size() + 1];
+            int tot = 0;
+            for (byte[] x : items) {
+                tot += x.length - plen;
+            }
+            suffixes = new byte[tot + 16]; // device padding contract
+            int p = 0;
+            for (int i = 0; i < items.size(); i++) {
+                byte[] x = items.get(i);
+                off[i] = p;
+                System.arraycopy(x, plen, suffixes, p, x.length - plen);
+                p += x.length - plen;
+            }
+            off[items.size()] = p;
+        }
+
+        /** The prefix form when the items share at least minPrefix bytes, else null. */
+        public static PrefixPacked of(List<byte[]> items, int minPrefix) {
+            if (items.isEmpty()) {
+                return null;
+            }
+            byte[] first = items.get(0);
+            int plen = Math.min(first.length, 255);
+            for (int i = 1; i < items.size() && plen >= minPrefix; i++) {
+                byte[] x = items.get(i);
+                int m = Math.min(plen, x.length), j = 0;
+                while (j < m && x[j] == first[j]) {
+                    j++;
+                }
+                plen = j;
+            }
+            return plen >= minPrefix ? new PrefixPacked(items, plen) : null;
+        }
+    }
+
     static final Charset ISO = Charset.forName("ISO-8859-1"); // bytes <-> String one to one
 
     /* One FIFO worker thread per engine context (SURVEY 8b: no event-loop thread waits on the device).  Single

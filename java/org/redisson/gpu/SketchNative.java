@@ -33,6 +33,9 @@ public final class SketchNative {
     /** sk_pfadd_ids: slab handles from a cached sk_hll_resolve; SK_ESTALE once the key was deleted / replaced. */
     public static native int pfaddIds(long ctx, int[] keyIds, int[] elemCounts, long[] elemOff, byte[] elems,
                                       byte[] outChanged);
+    /* sk_pfadd_ids_prefix: one-element PFADDs whose elements are prefix + suffixes[suffixOff[i] .. suffixOff[i+1]) */
+    public static native int pfaddIdsPrefix(long ctx, int[] keyIds, byte[] prefix, int[] suffixOff, byte[] suffixes,
+                                            byte[] outChanged);
     public static native int pfcount(long ctx, int[] nkeys, long[] keyOff, byte[] keys, long[] outCounts);
     /** sk_pfcount_ids: RHyperLogLog.count of many keys by cached slab id. */
     public static native int pfcountIds(long ctx, int[] keyIds, long[] outCounts);
@@ -57,6 +60,10 @@ public final class SketchNative {
                                       byte[] out);
     public static native int bloomContains(long ctx, byte[] name, long size, int k, long[] elemOff, byte[] elems,
                                            byte[] out);
+    public static native int bloomAddPrefix(long ctx, byte[] name, long size, int k, byte[] prefix, int[] suffixOff,
+                                            byte[] suffixes, byte[] out);
+    public static native int bloomContainsPrefix(long ctx, byte[] name, long size, int k, byte[] prefix,
+                                                 int[] suffixOff, byte[] suffixes, byte[] out);
     public static native int bloomCount(long ctx, byte[] name, int[] out);
 
     // RBitSet.set(from, to) / clear(from, to) as one device fill (M:RedissonBitSet.java:194-228)

@@ -132,6 +132,16 @@ int main(void) {
     jbyteArray out2 = f_newbytes(env, 2);
     pr_u8("pfaddIds", Java_org_redisson_gpu_SketchNative_pfaddIds(env, cls, ctx, ids, jints(2, one), eo, eb, out2),
           out2);
+    /* the same handles in prefix form: elements "pre" + "q2" / "pre" + "r2" */
+    {
+        FakeArr *so = arr_new(3, 4);
+        int32_t *sov = (int32_t *)(void *)so->data;
+        sov[0] = 0, sov[1] = 2, sov[2] = 4;
+        FakeArr *sb = arr_new(4 + 16, 1);
+        memcpy(sb->data, "q2r2", 4);
+        pr_u8("pfaddIdsPrefix", Java_org_redisson_gpu_SketchNative_pfaddIdsPrefix(env, cls, ctx, ids, jbytes("pre"),
+                                                                                   A(so), A(sb), out2), out2);
+    }
     const char *ck[] = {"jd:a", "jd:b", "jd:a", "jd:b", "jd:missing"};
     int nk[] = {1, 1, 3};
     packed(5, ck, &ko, &kb);
@@ -211,6 +221,21 @@ int main(void) {
           Java_org_redisson_gpu_SketchNative_bloomContains(env, cls, ctx, jbytes("jd:bf"), 729, 5, eo, eb, bco), bco);
     printf("bloomContains_changed %d\n",
            Java_org_redisson_gpu_SketchNative_bloomContains(env, cls, ctx, jbytes("jd:bf"), 730, 5, eo, eb, bco));
+    {   /* contains of "\"e1\"" and "\"e3\"" in prefix form: prefix "\"e", suffixes 1", 3" */
+        FakeArr *so = arr_new(3, 4);
+        int32_t *sov = (int32_t *)(void *)so->data;
+        sov[0] = 0, sov[1] = 2, sov[2] = 4;
+        FakeArr *sb = arr_new(4 + 16, 1);
+        memcpy(sb->data, "1\"3\"", 4);
+        jbyteArray pco = f_newbytes(env, 2);
+        pr_u8("bloomContainsPrefix", Java_org_redisson_gpu_SketchNative_bloomContainsPrefix(
+                                         env, cls, ctx, jbytes("jd:bf"), 729, 5, jbytes("\"e"), A(so), A(sb), pco), pco);
+        FakeArr *sb2 = arr_new(4 + 16, 1);
+        memcpy(sb2->data, "4\"5\"", 4);
+        jbyteArray pao = f_newbytes(env, 2);
+        pr_u8("bloomAddPrefix", Java_org_redisson_gpu_SketchNative_bloomAddPrefix(
+                                    env, cls, ctx, jbytes("jd:bf"), 729, 5, jbytes("\"e"), A(so), A(sb2), pao), pao);
+    }
     jintArray bn = jints(1, NULL);
     pr_i32("bloomCount", Java_org_redisson_gpu_SketchNative_bloomCount(env, cls, ctx, jbytes("jd:bf"), bn), bn);
     /* range set, async tickets */

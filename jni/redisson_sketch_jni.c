@@ -115,6 +115,21 @@ JNIEXPORT jint JNICALL Java_org_redisson_gpu_SketchNative_pfaddIds(JNIEnv *env, 
     return st;
 }
 
+/* group commit in prefix form: elements = prefix + suffixes (sk_pfadd_ids_prefix) */
+JNIEXPORT jint JNICALL Java_org_redisson_gpu_SketchNative_pfaddIdsPrefix(JNIEnv *env, jclass cls, jlong ctx,
+                                                                         jintArray ids, jbyteArray prefix,
+                                                                         jintArray soff, jbyteArray sbytes,
+                                                                         jbyteArray out) {
+    (void)cls;
+    jsize n = LEN(ids), pl = LEN(prefix);
+    void *i = PIN(ids), *p = PIN(prefix), *so = PIN(soff), *sb = PIN(sbytes), *r = PIN(out);
+    jint st = sk_pfadd_ids_prefix(CTX(ctx), (uint32_t)n, (const uint32_t *)i, (const uint8_t *)p, (uint32_t)pl,
+                                  (const uint32_t *)so, (const uint8_t *)sb, (uint8_t *)r);
+    UNPIN(out, r, 0); UNPIN(sbytes, sb, JNI_ABORT); UNPIN(soff, so, JNI_ABORT);
+    UNPIN(prefix, p, JNI_ABORT); UNPIN(ids, i, JNI_ABORT);
+    return st;
+}
+
 JNIEXPORT jint JNICALL Java_org_redisson_gpu_SketchNative_pfcountIds(JNIEnv *env, jclass cls, jlong ctx,
                                                                      jintArray ids, jlongArray out) {
     (void)cls;
@@ -272,6 +287,22 @@ JNIEXPORT jint JNICALL Java_org_redisson_gpu_SketchNative_bloomConfig(JNIEnv *en
     }
 BLOOM_OP(bloomAdd, sk_bloom_add)
 BLOOM_OP(bloomContains, sk_bloom_contains)
+
+#define BLOOM_PREFIX_OP(name, fn)                                                                            \
+    JNIEXPORT jint JNICALL Java_org_redisson_gpu_SketchNative_##name(                                        \
+        JNIEnv *env, jclass cls, jlong ctx, jbyteArray nmArr, jlong size, jint k, jbyteArray prefix,         \
+        jintArray soff, jbyteArray sbytes, jbyteArray out) {                                                 \
+        (void)cls;                                                                                           \
+        jsize nn = LEN(nmArr), n = LEN(soff) - 1, pl = LEN(prefix);                                          \
+        void *nm = PIN(nmArr), *p = PIN(prefix), *so = PIN(soff), *sb = PIN(sbytes), *r = PIN(out);          \
+        jint st = fn(CTX(ctx), (const uint8_t *)nm, (uint64_t)nn, size, k, (uint32_t)n, (const uint8_t *)p,  \
+                     (uint32_t)pl, (const uint32_t *)so, (const uint8_t *)sb, (uint8_t *)r);                 \
+        UNPIN(out, r, 0); UNPIN(sbytes, sb, JNI_ABORT); UNPIN(soff, so, JNI_ABORT);                          \
+        UNPIN(prefix, p, JNI_ABORT); UNPIN(nmArr, nm, JNI_ABORT);                                            \
+        return st;                                                                                           \
+    }
+BLOOM_PREFIX_OP(bloomAddPrefix, sk_bloom_add_prefix)
+BLOOM_PREFIX_OP(bloomContainsPrefix, sk_bloom_contains_prefix)
 
 JNIEXPORT jint JNICALL Java_org_redisson_gpu_SketchNative_bloomCount(JNIEnv *env, jclass cls, jlong ctx,
                                                                      jbyteArray name, jintArray out) {

@@ -99,6 +99,10 @@ SIGNATURES = {
     "sk_bloom_add_dev": (c_int, [P, _u8p, c_uint64, c_uint64, _u64p, _u8p, c_uint64, _u8p]),
     "sk_bloom_contains_dev": (c_int, [P, _u8p, c_uint64, c_uint64, _u64p, _u8p, c_uint64, _u8p]),
     "sk_bloom_count": (c_int, [P, _u8p, c_uint64, P]),
+    "sk_pfadd_ids_prefix": (c_int, [P, c_uint32, _u32p, _u8p, c_uint32, _u32p, _u8p, _u8p]),
+    "sk_bloom_add_prefix": (c_int, [P, _u8p, c_uint64, c_int64, c_int32, c_uint32, _u8p, c_uint32, _u32p, _u8p, _u8p]),
+    "sk_bloom_contains_prefix": (c_int, [P, _u8p, c_uint64, c_int64, c_int32, c_uint32, _u8p, c_uint32, _u32p, _u8p,
+                                         _u8p]),
     "sk_gen_jackson_longs": (c_int, [c_uint64, c_uint64, _u64p, _u8p]),
     "sk_gen_jackson_longs_dev": (c_int, [P, c_uint64, P, c_uint64, c_uint64, P, P]),
     "sk_dev_alloc": (c_int, [P, c_uint64, P]),

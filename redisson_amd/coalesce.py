@@ -132,7 +132,14 @@ class BloomCoalescer:
         elems = [e for r in run for e in r.elems]
         fn = self.engine.bloom_add if head.kind == "add" else self.engine.bloom_contains
         try:
-            res = fn(head.name, head.size, head.k, elems) if elems else []
+            from .engine import common_prefix
+
+            plen = common_prefix(elems) if elems else 0
+            if plen >= 8:   # a shared codec prefix: prefix form, only the suffixes cross the host link
+                res = self.engine.bloom_prefix(head.kind, head.name, head.size, head.k, bytes(elems[0])[:plen],
+                                               [bytes(e)[plen:] for e in elems])
+            else:
+                res = fn(head.name, head.size, head.k, elems) if elems else []
         except Exception as e:  # noqa: BLE001 - every request of the run sees the engine's error
             for r in run:
                 r.future._fail(e)

@@ -103,6 +103,13 @@ hipError_t launch_bloom_rc_hash(hipStream_t st, uint64_t n, const uint64_t *off,
 hipError_t launch_bloom_rc_probe(hipStream_t st, uint64_t n, uint64_t size, int k, const uint32_t *S,
                                  const uint32_t *recs, const uint8_t *bits, uint64_t cap_bytes, uint8_t *out,
                                  uint32_t *Z, uint32_t *GT);
+// a shared element prefix (host ingress in prefix form), passed by value to the expand kernel
+struct SkPrefix {
+    uint64_t w[32]; // prefix bytes, <= 255
+    uint32_t len;
+};
+hipError_t launch_expand_prefix(hipStream_t st, uint64_t n, const SkPrefix &pre, const uint32_t *soff,
+                                const uint8_t *sbytes, uint64_t *off, uint8_t *bytes);
 hipError_t launch_bloom_indexes(hipStream_t st, uint64_t n, const uint64_t *off, const uint8_t *bytes, uint64_t size,
                                 uint64_t magic, int np, uint64_t *idx);
 hipError_t launch_reduce_groups_u8(hipStream_t st, uint64_t n, uint32_t group, uint32_t take, uint32_t invert,

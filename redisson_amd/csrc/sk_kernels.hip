@@ -2601,6 +2601,24 @@ __global__ void __launch_bounds__(256) k_bloom_indexes(uint64_t n, const uint64_
         bi.next(j);
     }
 }
+// Host ingress in prefix form (sk_pfadd_ids_prefix, sk_bloom_*_prefix): element i = prefix ‖ suffix bytes
+// [soff[i], soff[i+1]) (u32 offsets, relative to soff[0]); rebuilt here into the (u64 offsets, bytes) form every hash
+// kernel reads.  One thread per element.
+__global__ void __launch_bounds__(256) k_expand_prefix(uint64_t n, SkPrefix pre, const uint32_t *__restrict__ soff,
+                                                       const uint8_t *__restrict__ sbytes, uint64_t *__restrict__ off,
+                                                       uint8_t *__restrict__ bytes) {
+    const uint64_t i = uint64_t(blockIdx.x) * 256 + threadIdx.x;
+    if (i > n) return;
+    const uint32_t s0 = soff[0], a = soff[i] - s0;
+    const uint64_t o = i * pre.len + a;
+    off[i] = o;
+    if (i == n) return;
+    const uint32_t b = soff[i + 1] - s0;
+    const uint8_t *pp = reinterpret_cast<const uint8_t *>(pre.w);
+    for (uint32_t j = 0; j < pre.len; j++) bytes[o + j] = pp[j];
+    for (uint32_t j = a; j < b; j++) bytes[o + pre.len + (j - a)] = sbytes[j];
+}
+
 // out[i] = AND(in[i * group .. i * group + take)) ^ invert: a contains reply (AND of probes 0..k-2) or an add reply
 // (one of probes 0..k-2 replied 0) from per-probe bits in element-major order
 __global__ void __launch_bounds__(256) k_reduce_groups_u8(uint64_t n, uint32_t group, uint32_t take, uint32_t invert,
@@ -3453,6 +3471,12 @@ hipError_t launch_bloom_indexes(hipStream_t st, uint64_t n, const uint64_t *off,
                                 uint64_t magic, int np, uint64_t *idx) {
     if (!n) return hipSuccess;
     hipLaunchKernelGGL(k_bloom_indexes, dim3(grid_for(n, 256)), dim3(256), 0, st, n, off, bytes, size, magic, np, idx);
+    SK_LAUNCH_CHECK();
+    return hipSuccess;
+}
+hipError_t launch_expand_prefix(hipStream_t st, uint64_t n, const SkPrefix &pre, const uint32_t *soff,
+                                const uint8_t *sbytes, uint64_t *off, uint8_t *bytes) {
+    hipLaunchKernelGGL(k_expand_prefix, dim3(grid_for(n + 1, 256)), dim3(256), 0, st, n, pre, soff, sbytes, off, bytes);
     SK_LAUNCH_CHECK();
     return hipSuccess;
 }

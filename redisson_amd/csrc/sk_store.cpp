@@ -354,9 +354,11 @@ struct sk_ctx {
     int comm_rank = 0, comm_size = 0;
     DBuf rt_cnt;                // range-sharded RBitSet routing: per-(shard, block) counts, then their scan
     // host -> device staging of caller host buffers (stage_h2d): two pinned buffers, filled by host threads in turn
-    uint8_t *stage[2] = {nullptr, nullptr};
-    hipEvent_t stage_ev[2] = {nullptr, nullptr};
-    bool stage_on = false;      // SK_STAGE=1: stage pageable inputs (measured no faster than HIP's own pageable path)
+    uint8_t *stage[8] = {};
+    hipEvent_t stage_ev[8] = {};
+    bool stage_on = false;      // SK_STAGE=1: stage pageable inputs through the ring below
+    uint64_t stage_piece = 4ull << 20; // bytes per staged piece (SK_STAGE_PIECE_KB)
+    uint32_t stage_bufs = 4;    // pinned buffers in the ring (SK_STAGE_BUFS, <= 8)
 
     bool async_dev = false;     // sk_set_async: _dev calls return without a final sync
     int pfadd_path = 1;         // 0 claim/commit, 1 partition, 2 sorted (SK_PFADD_PATH); dense batches use 2
@@ -385,6 +387,7 @@ struct sk_ctx {
         uni, ptrs, hist_a, hist_b, ovf, bloom_h;
     DBuf rc_S, rc_rec;          // Bloom contains region schedule: segment table + probe records (contains only)
     DBuf rc_Z, rc_GT;           // ... and its zero lists: per-region lists + the (region, reply group) run table
+    DBuf in_soff, in_sbytes;    // host ingress in prefix form: suffix offsets (u32) and bytes, before the rebuild
     DBuf long_h, long_which;    // PFADD: hashes of long elements (k_ms_rounds) and their element indexes + layout
     DBuf long_plane, long_flags; // their k bit planes and look-back flags
     uint64_t long_fallbacks = 0; // calls whose long elements were re-hashed per thread (look-back wait ran out)
@@ -592,29 +595,31 @@ void hll_str_merged(sk_ctx *c, uint32_t slab) {
 // the link's rate (a pageable hipMemcpyAsync is staged by the runtime and returns only once it has been copied).  A
 // buffer is refilled only after the event of its previous copy completed.  Pinned caller memory (a buffer the JNI
 // side allocated with sk_host_alloc) is copied directly.
-constexpr uint64_t kStagePiece = 32ull << 20;
 int stage_h2d(sk_ctx *c, void *dst, const void *src, uint64_t bytes) {
     if (!bytes) return SK_OK;
     hipPointerAttribute_t at;
     const bool pinned = hipPointerGetAttributes(&at, src) == hipSuccess && at.type == hipMemoryTypeHost;
     (void)hipGetLastError(); // pageable memory reports an error here
-    if (!c->stage_on || pinned || bytes < (4ull << 20)) {
+    if (!c->stage_on || pinned || bytes < 2 * c->stage_piece) {
         HIPCHK(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->st));
         return SK_OK;
     }
-    for (int k = 0; k < 2; k++)
+    const uint32_t nb = c->stage_bufs;
+    for (uint32_t k = 0; k < nb; k++)
         if (!c->stage[k]) {
-            HIPCHK(c, hipHostMalloc((void **)&c->stage[k], kStagePiece, hipHostMallocDefault));
+            HIPCHK(c, hipHostMalloc((void **)&c->stage[k], c->stage_piece, hipHostMallocDefault));
             HIPCHK(c, hipEventCreateWithFlags(&c->stage_ev[k], hipEventDisableTiming));
             HIPCHK(c, hipEventRecord(c->stage_ev[k], c->st));
         }
+    // a ring of nb pinned buffers: host threads fill piece p into buffer p % nb while the DMA engine copies the
+    // pieces before it; a buffer is refilled once the event of its previous copy completed
     const uint8_t *s8 = static_cast<const uint8_t *>(src);
     uint8_t *d8 = static_cast<uint8_t *>(dst);
-    for (uint64_t o = 0, p = 0; o < bytes; o += kStagePiece, p++) {
-        const int k = int(p & 1);
-        const uint64_t len = std::min(kStagePiece, bytes - o);
-        HIPCHK(c, hipEventSynchronize(c->stage_ev[k])); // the buffer's previous copy is done
-        host_for(len, 1u << 20, [&](uint64_t a, uint64_t b) { std::memcpy(c->stage[k] + a, s8 + o + a, b - a); });
+    for (uint64_t o = 0, p = 0; o < bytes; o += c->stage_piece, p++) {
+        const uint32_t k = uint32_t(p % nb);
+        const uint64_t len = std::min(c->stage_piece, bytes - o);
+        HIPCHK(c, hipEventSynchronize(c->stage_ev[k]));
+        host_for(len, 256u << 10, [&](uint64_t a, uint64_t b) { std::memcpy(c->stage[k] + a, s8 + o + a, b - a); });
         HIPCHK(c, hipMemcpyAsync(d8 + o, c->stage[k], len, hipMemcpyHostToDevice, c->st));
         HIPCHK(c, hipEventRecord(c->stage_ev[k], c->st));
     }
@@ -1238,6 +1243,8 @@ int sk_open(const sk_config *cfg, sk_ctx **out) {
     if (const char *e = getenv("SK_PFL_ZERO")) c->pfl_zero = atoi(e) != 0;
     if (const char *e = getenv("SK_PFL_PLAN")) c->pfl_plan = atoi(e) != 0;
     if (const char *e = getenv("SK_STAGE")) c->stage_on = atoi(e) != 0;
+    if (const char *e = getenv("SK_STAGE_PIECE_KB")) c->stage_piece = std::max<uint64_t>(64, strtoull(e, nullptr, 10)) << 10;
+    if (const char *e = getenv("SK_STAGE_BUFS")) c->stage_bufs = uint32_t(std::min(8, std::max(2, atoi(e))));
     uint64_t cap = (cfg && cfg->hll_capacity) ? cfg->hll_capacity : 1024;
     if (hll_grow(c, cap) != SK_OK || c->misc.ensure(4096) != hipSuccess ||
         hipMalloc(&c->d_zero, 16) != hipSuccess || hipMemsetAsync(c->d_zero, 0, 16, c->st) != hipSuccess ||
@@ -1270,13 +1277,13 @@ int sk_close(sk_ctx *c) {
     if (c->d_dir) (void)hipFree(c->d_dir);
     if (c->d_zero) (void)hipFree(c->d_zero);
     if (c->h_cnt) (void)hipHostFree(c->h_cnt);
-    for (int k = 0; k < 2; k++) {
+    for (int k = 0; k < 8; k++) {
         if (c->stage[k]) (void)hipHostFree(c->stage[k]);
         if (c->stage_ev[k]) (void)hipEventDestroy(c->stage_ev[k]);
     }
     for (DBuf *b : {&c->keys_a, &c->keys_b, &c->vals_a, &c->vals_b, &c->sort_tmp, &c->in_off, &c->in_bytes,
                     &c->in_ids, &c->in_cmd, &c->out_u8, &c->misc, &c->partial, &c->hist, &c->uni, &c->ptrs,
-                    &c->hist_a, &c->hist_b, &c->ovf, &c->bloom_h, &c->rc_S, &c->rc_rec, &c->rc_Z, &c->rc_GT, &c->long_h,
+                    &c->hist_a, &c->hist_b, &c->ovf, &c->bloom_h, &c->rc_S, &c->rc_rec, &c->rc_Z, &c->rc_GT, &c->in_soff, &c->in_sbytes, &c->long_h,
                     &c->long_which, &c->long_plane, &c->long_flags, &c->ra_S, &c->ra_rec, &c->ra_flag, &c->ev, &c->ev_n,
                     &c->pfl_chunks, &c->pfl_S, &c->pfl_C, &c->pfl_rc, &c->rt_cnt, &c->pfl_rec, &c->pfl_bk, &c->pfl_bv,
                     &c->pfl_ovf, &c->pfl_order})
@@ -2792,6 +2799,118 @@ static int stage_elems(sk_ctx *c, uint32_t n, const uint64_t *off, const uint8_t
     if ((sr = stage_h2d(c, c->in_bytes.p, bytes + off[0], tot))) return sr;
     HIPCHK(c, hipMemsetAsync(c->in_bytes.as<uint8_t>() + tot, 0, 16, c->st));
     return sync(c); // o is a host vector
+}
+
+// Host ingress in prefix form: element i = prefix ‖ suffix bytes [soff[i], soff[i+1]).  Only the suffixes and u32
+// offsets cross the host link (a Jackson Long ships ~21 of its ~39 bytes and 4 instead of 8 offset bytes); the
+// elements are rebuilt on the device into in_off / in_bytes (k_expand_prefix).
+static int prefix_check(sk_ctx *c, const uint8_t *prefix, uint32_t plen, sk::SkPrefix *pre) {
+    if (plen > 255 || (plen && !prefix)) return fail(c, SK_EINVAL, "element prefix of %u bytes (<= 255)", plen);
+    std::memset(pre, 0, sizeof *pre);
+    if (plen) std::memcpy(pre->w, prefix, plen);
+    pre->len = plen;
+    return SK_OK;
+}
+static int stage_prefixed(sk_ctx *c, uint32_t n, const sk::SkPrefix &pre, const uint32_t *soff, const uint8_t *sbytes) {
+    const uint64_t tot_s = uint64_t(soff[n] - soff[0]), tot = uint64_t(n) * pre.len + tot_s;
+    HIPCHK(c, c->in_soff.ensure((n + 1) * 4ull));
+    HIPCHK(c, c->in_sbytes.ensure(tot_s + 16));
+    HIPCHK(c, c->in_off.ensure((n + 1) * 8ull));
+    HIPCHK(c, c->in_bytes.ensure(tot + 16));
+    int sr;
+    if ((sr = stage_h2d(c, c->in_soff.p, soff, (n + 1) * 4ull))) return sr;
+    if ((sr = stage_h2d(c, c->in_sbytes.p, sbytes + soff[0], tot_s))) return sr;
+    HIPCHK(c, sk::launch_expand_prefix(c->st, n, pre, c->in_soff.as<uint32_t>(), c->in_sbytes.as<uint8_t>(),
+                                       c->in_off.as<uint64_t>(), c->in_bytes.as<uint8_t>()));
+    HIPCHK(c, hipMemsetAsync(c->in_bytes.as<uint8_t>() + tot, 0, 16, c->st)); // padding contract
+    return SK_OK;
+}
+static uint32_t longest_suffix(uint32_t n, const uint32_t *soff) {
+    uint32_t m = 0;
+    for (uint32_t i = 0; i < n; i++) m = std::max(m, soff[i + 1] - soff[i]);
+    return m;
+}
+
+int sk_pfadd_ids_prefix(sk_ctx *c, uint32_t n, const uint32_t *key_ids, const uint8_t *prefix, uint32_t plen,
+                        const uint32_t *soff, const uint8_t *sbytes, uint8_t *out_changed) {
+    std::lock_guard<std::mutex> g(c->mu);
+    ENTER(c);
+    if (!n) return SK_OK;
+    sk::SkPrefix pre;
+    int r = prefix_check(c, prefix, plen, &pre);
+    if (r) return r;
+    const uint64_t d = first_dead_handle(c, n, key_ids);
+    if (d < n)
+        return fail(c, SK_ESTALE,
+                    "PFADD: slab id %u is not held by a key (deleted, replaced or never resolved)", key_ids[d]);
+    if (plen + uint64_t(longest_suffix(n, soff)) >= sk::long_elem_bytes()) {
+        // a long element (addAll's one-element array): the bit-round scan of the full-element path; rebuilt here
+        std::vector<uint64_t> off(uint64_t(n) + 1);
+        std::vector<uint8_t> bytes;
+        bytes.reserve(uint64_t(n) * plen + (soff[n] - soff[0]) + 16);
+        for (uint32_t i = 0; i < n; i++) {
+            off[i] = bytes.size();
+            bytes.insert(bytes.end(), prefix, prefix + plen);
+            bytes.insert(bytes.end(), sbytes + soff[i], sbytes + soff[i + 1]);
+        }
+        off[n] = bytes.size();
+        bytes.resize(bytes.size() + 16);
+        std::vector<uint32_t> ones(n, 1);
+        return pfadd_host_batch(c, n, key_ids, nullptr, ones.data(), off.data(), bytes.data(), out_changed);
+    }
+    const uint64_t chunk = std::max<uint64_t>(c->max_batch, 1);
+    for (uint64_t c0 = 0; c0 < n; c0 += chunk) {
+        const uint32_t m = uint32_t(std::min<uint64_t>(chunk, n - c0));
+        HIPCHK(c, c->in_ids.ensure(m * 4ull));
+        HIPCHK(c, c->out_u8.ensure(m));
+        if ((r = stage_h2d(c, c->in_ids.p, key_ids + c0, m * 4ull))) return r;
+        if ((r = stage_prefixed(c, m, pre, soff + c0, sbytes))) return r;
+        HIPCHK(c, hipMemsetAsync(c->out_u8.p, 0, m, c->st));
+        if ((r = pfadd_device(c, m, c->in_ids.as<uint32_t>(), c->in_off.as<uint64_t>(), c->in_bytes.as<uint8_t>(),
+                              nullptr, m, c->out_u8.as<uint8_t>(), 0)))
+            return r;
+        HIPCHK(c, hipMemcpyAsync(out_changed + c0, c->out_u8.p, m, hipMemcpyDeviceToHost, c->st));
+        if ((r = sync(c))) return r;
+    }
+    return SK_OK;
+}
+
+int sk_bloom_add_prefix(sk_ctx *c, const uint8_t *name, uint64_t len, int64_t size, int32_t k, uint32_t n,
+                        const uint8_t *prefix, uint32_t plen, const uint32_t *soff, const uint8_t *sbytes,
+                        uint8_t *out) {
+    std::lock_guard<std::mutex> g(c->mu);
+    ENTER(c);
+    sk::SkPrefix pre;
+    int r = prefix_check(c, prefix, plen, &pre);
+    if (r) return r;
+    uint32_t id;
+    if ((r = bloom_prepare(c, key_of(name, len), size, k, true, &id)) || !n) return r;
+    if ((r = stage_prefixed(c, n, pre, soff, sbytes))) return r;
+    HIPCHK(c, c->out_u8.ensure(n));
+    if ((r = bloom_add_device(c, id, size, k, n, c->in_off.as<uint64_t>(), c->in_bytes.as<uint8_t>(),
+                              c->out_u8.as<uint8_t>())))
+        return r;
+    HIPCHK(c, hipMemcpyAsync(out, c->out_u8.p, n, hipMemcpyDeviceToHost, c->st));
+    return sync(c);
+}
+
+int sk_bloom_contains_prefix(sk_ctx *c, const uint8_t *name, uint64_t len, int64_t size, int32_t k, uint32_t n,
+                             const uint8_t *prefix, uint32_t plen, const uint32_t *soff, const uint8_t *sbytes,
+                             uint8_t *out) {
+    std::lock_guard<std::mutex> g(c->mu);
+    ENTER(c);
+    sk::SkPrefix pre;
+    int r = prefix_check(c, prefix, plen, &pre);
+    if (r) return r;
+    uint32_t id;
+    if ((r = bloom_prepare(c, key_of(name, len), size, k, false, &id)) || !n) return r;
+    if ((r = stage_prefixed(c, n, pre, soff, sbytes))) return r;
+    HIPCHK(c, c->out_u8.ensure(n));
+    if ((r = bloom_contains_launch(c, c->st, id, size, k, n, c->in_off.as<uint64_t>(), c->in_bytes.as<uint8_t>(),
+                                   c->out_u8.as<uint8_t>())))
+        return r;
+    HIPCHK(c, hipMemcpyAsync(out, c->out_u8.p, n, hipMemcpyDeviceToHost, c->st));
+    return sync(c);
 }
 
 int sk_bloom_add(sk_ctx *c, const uint8_t *name, uint64_t len, int64_t size, int32_t k, uint32_t n,

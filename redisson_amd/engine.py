@@ -114,6 +114,33 @@ def pack(items: Sequence[bytes]):
     return off, buf
 
 
+def common_prefix(items: Sequence[bytes], cap: int = 255) -> int:
+    """Length of the longest byte prefix every item shares (<= cap): the prefix form's shared part."""
+    if not items:
+        return 0
+    first = bytes(items[0])[:cap]
+    plen = len(first)
+    for x in items[1:]:
+        x = bytes(x)
+        m = min(plen, len(x))
+        j = 0
+        while j < m and x[j] == first[j]:
+            j += 1
+        plen = j
+        if plen == 0:
+            break
+    return plen
+
+
+def pack_u32(items: Sequence[bytes]):
+    """(u32 offsets[n+1], bytes + 16 B of padding): the suffix form of the prefix-form entry points."""
+    lens = np.fromiter((len(x) for x in items), dtype=np.uint32, count=len(items))
+    off = np.zeros(len(items) + 1, dtype=np.uint32)
+    np.cumsum(lens, out=off[1:])
+    buf = np.frombuffer(b"".join(bytes(x) for x in items) + b"\0" * 16, dtype=np.uint8)
+    return off, buf
+
+
 def _b(x) -> bytes:
     return x.encode("utf-8") if isinstance(x, str) else bytes(x)
 
@@ -271,12 +298,23 @@ class SketchEngine:
         return out
 
     def pfadd_ids_status(self, key_ids, elems: Sequence[Sequence[bytes]]):
-        """sk_pfadd_ids without raising: (status, replies u8[n], error text)."""
+        """sk_pfadd_ids without raising: (status, replies u8[n], error text).  One-element commands whose elements
+        share a codec prefix of >= 8 bytes go in prefix form (sk_pfadd_ids_prefix: only the suffixes cross the host
+        link), as the Java group commit does."""
         ids = np.ascontiguousarray(key_ids, dtype=np.uint32)
         n = len(ids)
+        out = np.zeros(n, dtype=np.uint8)
+        flat = [e[0] for e in elems] if all(len(e) == 1 for e in elems) else None
+        plen = common_prefix(flat) if flat else 0
+        if plen >= 8:
+            soff, sbuf = pack_u32([bytes(x)[plen:] for x in flat])
+            pre = np.frombuffer(bytes(flat[0])[:plen], dtype=np.uint8)
+            st = self.lib.sk_pfadd_ids_prefix(self.ctx, n, _addr(ids), _addr(pre), plen, _addr(soff), _addr(sbuf),
+                                              _addr(out))
+            msg = (self.lib.sk_last_error(self.ctx) or b"").decode("utf-8", "replace") if st != N.SK_OK else ""
+            return st, out, msg
         counts = np.fromiter((len(e) for e in elems), dtype=np.uint32, count=n)
         eoff, ebuf = pack([x for e in elems for x in e])
-        out = np.zeros(n, dtype=np.uint8)
         st = self.lib.sk_pfadd_ids(self.ctx, n, _addr(ids), _addr(counts), _addr(eoff), _addr(ebuf), _addr(out))
         msg = (self.lib.sk_last_error(self.ctx) or b"").decode("utf-8", "replace") if st != N.SK_OK else ""
         return st, out, msg
@@ -334,6 +372,16 @@ class SketchEngine:
         out = np.zeros(n, dtype=np.uint8)
         self._check(self.lib.sk_pfadd_ids(self.ctx, n, _addr(ids), _addr(counts), _addr(eoff), _addr(ebuf),
                                           _addr(out)))
+        return [bool(x) for x in out]
+
+    def pfadd_ids_prefix(self, key_ids, prefix: bytes, suffixes: Sequence[bytes]) -> List[bool]:
+        """One-element PFADDs by slab handle whose elements are prefix + suffixes[i] (sk_pfadd_ids_prefix)."""
+        ids = np.ascontiguousarray(key_ids, dtype=np.uint32)
+        soff, sbuf = pack_u32(suffixes)
+        pre = np.frombuffer(bytes(prefix) or b"\0", dtype=np.uint8)
+        out = np.zeros(len(ids), dtype=np.uint8)
+        self._check(self.lib.sk_pfadd_ids_prefix(self.ctx, len(ids), _addr(ids), _addr(pre), len(prefix),
+                                                 _addr(soff), _addr(sbuf), _addr(out)))
         return [bool(x) for x in out]
 
     def pfadd_dev(self, n: int, d_key_ids, d_elem_off, d_elem_bytes, bytes_len: int, d_out):
@@ -565,6 +613,17 @@ class SketchEngine:
         nm = _b(name)
         self._check(self.lib.sk_bloom_contains_dev(self.ctx, nm, len(nm), n, _addr(d_off), _addr(d_bytes),
                                                    bytes_len, _addr(d_out)))
+
+    def bloom_prefix(self, op: str, name, size: int, k: int, prefix: bytes, suffixes: Sequence[bytes]) -> List[bool]:
+        """add / contains of elements prefix + suffixes[i] (sk_bloom_add_prefix / sk_bloom_contains_prefix)."""
+        nm = _b(name)
+        soff, sbuf = pack_u32(suffixes)
+        pre = np.frombuffer(bytes(prefix) or b"\0", dtype=np.uint8)
+        out = np.zeros(len(suffixes), dtype=np.uint8)
+        fn = self.lib.sk_bloom_add_prefix if op == "add" else self.lib.sk_bloom_contains_prefix
+        self._check(fn(self.ctx, nm, len(nm), size, k, len(suffixes), _addr(pre), len(prefix), _addr(soff),
+                       _addr(sbuf), _addr(out)))
+        return [bool(x) for x in out]
 
     def bloom_count(self, name) -> int:
         nm = _b(name)

@@ -41,6 +41,11 @@ class OracleBloomEngine:
         b = self.bits.get(name)
         return b.bloom_contains(size, k, elems) if b else [False] * len(elems)
 
+    def bloom_prefix(self, op, name, size, k, prefix, suffixes):  # the prefix form: elements = prefix + suffix
+        self.prefix_calls = getattr(self, "prefix_calls", 0) + 1
+        elems = [prefix + x for x in suffixes]
+        return (self.bloom_add if op == "add" else self.bloom_contains)(name, size, k, elems)
+
 
 def _elem(t, i):
     return b'["java.lang.Long",%d]' % (t * 1_000_003 + i)

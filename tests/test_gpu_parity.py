@@ -887,3 +887,51 @@ def test_hll_sum_kernel_exact(engine, O):
             assert int(got[2 * i]) == int(sum(1 << (40 - int(v)) for v in r))
     assert [int(x) for x in engine.pfcount_ids(ids)] == [O.count_regs(r, 1) for r in regs]
     d_ids.free(); d_out.free()
+
+
+def test_prefix_form_ingress_matches_oracle(O):
+    """Host ingress in prefix form (sk_pfadd_ids_prefix, sk_bloom_add_prefix, sk_bloom_contains_prefix: element =
+    shared prefix + suffix, rebuilt on the device) gives the oracle's replies, registers and bit array: Jackson Longs
+    split at their type header, an empty suffix, an empty prefix, a batch over several device batches (max_batch), a
+    long element (the full-element fallback) and a stale handle."""
+    from redisson_amd import SketchEngine
+    from redisson_amd.engine import RedisException
+    e = SketchEngine(device=0, max_batch=3000)
+    try:
+        rng = np.random.default_rng(505)
+        names = [b"pfx:%d" % i for i in range(29)]
+        ref = O.HLLStore()
+        ref.pfadd(names, [[] for _ in names])
+        ids = e.hll_resolve(names)
+        els = _elems(0x5EED0505, 8000)
+        pre = b'["java.lang.Long",'
+        assert all(x.startswith(pre) for x in els)
+        kid = rng.integers(0, len(names), 8000)
+        got = e.pfadd_ids_prefix(ids[kid], pre, [x[len(pre):] for x in els])
+        assert got == ref.pfadd([names[k] for k in kid], [[x] for x in els])
+        # an empty suffix, an empty prefix, repeats
+        odd = [pre, pre + b"1]", els[0]]
+        kid2 = rng.integers(0, len(names), len(odd))
+        assert e.pfadd_ids_prefix(ids[kid2], pre, [x[len(pre):] for x in odd]) == \
+            ref.pfadd([names[k] for k in kid2], [[x] for x in odd])
+        assert e.pfadd_ids_prefix(ids[kid2], b"", odd) == ref.pfadd([names[k] for k in kid2], [[x] for x in odd])
+        # a long element (>= 64 KiB: the bit-round scan of the full-element path)
+        big = b"[" + b",".join(b"%d" % i for i in range(20000)) + b"]"
+        assert e.pfadd_ids_prefix(ids[:1], b"[0,1,2", [big[6:]]) == ref.pfadd(names[:1], [[big]])
+        for nm in names:
+            np.testing.assert_array_equal(e.hll_registers(nm), ref.regs[nm])
+        with pytest.raises(RedisException, match="not held by a key"):
+            e.pfadd_ids_prefix(np.array([1 << 20], dtype=np.uint32), pre, [b"1]"])
+        # Bloom add / contains in prefix form
+        assert e.bloom_try_init("pfx:bf", 50000, 0.01)
+        size, k, _, _ = e.bloom_config("pfx:bf")
+        bits = O.BitString()
+        assert e.bloom_prefix("add", "pfx:bf", size, k, pre, [x[len(pre):] for x in els[:5000]]) == \
+            bits.bloom_add(size, k, els[:5000])
+        probe = els[2500:] + odd
+        assert e.bloom_prefix("contains", "pfx:bf", size, k, b"", probe) == bits.bloom_contains(size, k, probe)
+        assert e.bloom_prefix("contains", "pfx:bf", size, k, pre, [x[len(pre):] for x in els[2500:]]) == \
+            bits.bloom_contains(size, k, els[2500:])
+        assert e.get("pfx:bf") == bits.bytes()
+    finally:
+        e.close()

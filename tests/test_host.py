@@ -147,7 +147,7 @@ def test_jni_shim_typechecks_against_the_abi():
     natives = set(re.findall(r"native\s+[\w\[\]]+\s+(\w+)\s*\(", java))
     shim = open(src).read()
     exported = set(re.findall(r"Java_org_redisson_gpu_SketchNative_(\w+)", shim))
-    exported |= set(re.findall(r"(?:BLOOM_OP|KEY_U64_OUT)\((\w+),", shim))
+    exported |= set(re.findall(r"(?:BLOOM_OP|BLOOM_PREFIX_OP|KEY_U64_OUT)\((\w+),", shim))
     assert natives <= exported, natives - exported
 
 

@@ -44,6 +44,8 @@ def test_jni_drive_every_entry_point(O):
     assert out["resolve_created"] == ["0", "0", "0"]
     assert out["lookup"] == ["0", "1", "-1"]
     assert out["pfaddIds"] == ["0"] + [str(int(x)) for x in ref.pfadd([b"jd:a", b"jd:b"], [[b"q"], [b"r"]])]
+    assert out["pfaddIdsPrefix"] == ["0"] + [str(int(x)) for x in ref.pfadd([b"jd:a", b"jd:b"],
+                                                                             [[b"preq2"], [b"prer2"]])]
     ca, cb, cab = ref.count([b"jd:a"]), ref.count([b"jd:b"]), ref.count([b"jd:a", b"jd:b"])
     assert out["pfcount"] == ["0", str(ca), str(cb), str(cab)]
     assert out["pfcountIds"] == ["0", str(ca), str(cb)]
@@ -70,7 +72,9 @@ def test_jni_drive_every_entry_point(O):
     assert out["bloomAdd"] == ["0"] + [str(int(x)) for x in adds]
     assert out["bloomContains"] == ["0"] + [str(int(x)) for x in bs.bloom_contains(729, 5, [b'"e1"', b'"e3"'])]
     assert out["bloomContains_changed"] == ["-3"]
-    assert out["bloomCount"] == ["0", str(O.bloom_count(729, 5, bs.bitcount()))]
+    assert out["bloomContainsPrefix"] == out["bloomContains"]
+    assert out["bloomAddPrefix"] == ["0"] + [str(int(x)) for x in bs.bloom_add(729, 5, [b'"e4"', b'"e5"'])]
+    assert out["bloomCount"] == ["0", str(O.bloom_count(729, 5, bs.bitcount()))]  # after the prefix-form adds
     assert out["setBitRange_bitcount"] == ["0", "18"]
     assert out["ticket"] == ["1", "0"]
     assert out["del"] == ["0", "1"]

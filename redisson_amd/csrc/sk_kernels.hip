@@ -912,8 +912,13 @@ __global__ void __launch_bounds__(SK_PFP_ATPB) __attribute__((amdgpu_waves_per_e
 // Runs are in tile order and tiles in batch order, so a fine bucket larger than one chunk is applied in chunks of
 // whole runs with the LDS registers carried over; a single run larger than a chunk is resolved with the (slot,
 // rho) -> min seq table of pfp_big_resolve, against the LDS registers.
+#ifndef SK_PFL_SH
 #define SK_PFL_SH 7        // largest fine bucket = 2^SH sketches (128 lines of 128 B = 16 KiB of registers); a call
                            // uses sh <= SH sketches per fine bucket, sized so a fine bucket expects <= ~768 records
+#endif
+#ifndef SK_PFL_EXP
+#define SK_PFL_EXP 600     // records a fine bucket is sized to expect (one chunk of SK_PFL_CAP with margin)
+#endif
 #define SK_PFL_TILE 448    // hash blocks per run tile (default; SK_PFL_TILE): ~14.3 k records per region
 #define SK_PFL_RTPB 1024   // region threads: one hash-block segment each
 #ifndef SK_PFL_RPER
@@ -3170,7 +3175,7 @@ PflDims pfl_dims(uint64_t n, uint32_t nslab, uint32_t tile_blocks) {
     uint32_t pk0 = 0;
     while (pk0 < 32 && (1ull << pk0) < nslab) pk0++;
     d.sh = SK_PFL_SH;
-    while (d.sh > 0 && double(n) * double(1u << d.sh) > 600.0 * SK_PFL_NB * double(1ull << std::max(pk0, d.sh)) &&
+    while (d.sh > 0 && double(n) * double(1u << d.sh) > double(SK_PFL_EXP) * SK_PFL_NB * double(1ull << std::max(pk0, d.sh)) &&
            (1ull << (std::max(pk0, d.sh - 1) - (d.sh - 1))) <= SK_PFL_MAXSUB)
         d.sh--;
     // the inverse of an odd pa mod 2^32 by Newton steps

@@ -353,7 +353,7 @@ struct sk_ctx {
     ncclComm_t comm = nullptr;
     int comm_rank = 0, comm_size = 0;
     DBuf rt_cnt;                // range-sharded RBitSet routing: per-(shard, block) counts, then their scan
-    // host -> device staging of caller host buffers (stage_h2d): two pinned buffers, filled by host threads in turn
+    // host -> device staging of caller host buffers (stage_h2d): a ring of stage_bufs pinned buffers
     uint8_t *stage[8] = {};
     hipEvent_t stage_ev[8] = {};
     bool stage_on = false;      // SK_STAGE=1: stage pageable inputs through the ring below
@@ -590,11 +590,12 @@ void hll_str_merged(sk_ctx *c, uint32_t slab) {
     c->hstr[slab].hdr[15] |= 0x80;
 }
 
-// H2D of a caller's host range, asynchronous on c->st.  Large pageable ranges go through two pinned staging
-// buffers: host threads copy piece p into buffer p % 2 while the device copies piece p - 1 out of the other one at
-// the link's rate (a pageable hipMemcpyAsync is staged by the runtime and returns only once it has been copied).  A
-// buffer is refilled only after the event of its previous copy completed.  Pinned caller memory (a buffer the JNI
-// side allocated with sk_host_alloc) is copied directly.
+// H2D of a caller's host range, asynchronous on c->st.  With SK_STAGE=1, large pageable ranges go through a ring of
+// stage_bufs pinned buffers of stage_piece bytes (SK_STAGE_BUFS, SK_STAGE_PIECE_KB): host threads copy piece p into
+// buffer p % stage_bufs while the device copies the pieces before it at the link's rate.  A buffer is refilled only
+// after the event of its previous copy completed.  Off by default: measured, the runtime's own staging of a pageable
+// hipMemcpyAsync was as fast or faster (host ingress).  Pinned caller memory (a buffer the JNI side
+// allocated with sk_host_alloc) is always copied directly.
 int stage_h2d(sk_ctx *c, void *dst, const void *src, uint64_t bytes) {
     if (!bytes) return SK_OK;
     hipPointerAttribute_t at;

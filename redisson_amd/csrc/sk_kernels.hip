@@ -1870,7 +1870,8 @@ __global__ void __launch_bounds__(256) k_bloom_contains_q(uint64_t n, const uint
 #endif
 #ifndef SK_RC_ABL
 // dev ablations of the contains chain (results discarded): 1 no reply stores, 2 no record loads, 4 no region load,
-// 8 no hash arithmetic, 16 no segment-table stores, 32 no record stores, 64 no add reply stores
+// 8 no hash arithmetic, 16 no segment-table stores, 32 no record stores, 64 no add reply stores; of the add apply:
+// 128 records gathered from one contiguous run, 256 no windows (region and segment table only), 512 no chain walk
 #define SK_RC_ABL 0
 #endif
 #define RC_RB 20                      // region = 2^20 bits = 128 KiB
@@ -2438,7 +2439,7 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_ra_apply(uint32_t NB, uint32_t
     uint32_t mymax = 0;
     bool anyset = false;
     constexpr uint32_t W = RA_CAP - RA_SEGMAX;
-    for (uint32_t lo = 0; lo < total; lo += W) {
+    for (uint32_t lo = 0; lo < ((SK_RC_ABL & 256) ? 0u : total); lo += W) {
         if (total <= W) { // one window: [0, total), known without the atomics (the usual case)
             if (threadIdx.x == 0) {
                 wbase = 0;
@@ -2490,7 +2491,11 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_ra_apply(uint32_t NB, uint32_t
 #pragma unroll
             for (uint32_t q = 0; q < RA_GQ; q++) {
                 const uint32_t u = threadIdx.x + (g + q) * RC_TPB;
+#if SK_RC_ABL & 128
+                x[q] = u < nw ? chunks[(uint64_t(r) * W + lo + u) % (uint64_t(NB) * CH)] : 0u;
+#else
                 x[q] = u < nw ? chunks[rec[u]] : 0u;
+#endif
             }
 #pragma unroll
             for (uint32_t q = 0; q < RA_GQ; q++) {
@@ -2514,7 +2519,7 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_ra_apply(uint32_t NB, uint32_t
             if (w & ra_mask(b)) continue; // set before this probe: not a setter
             const uint32_t key = ra_key<AEPB>(blk[u], xu);
             bool f = true;
-            for (uint32_t v = head[b & (RA_HT - 1)]; v < RA_CAP && f; v = nxt[v]) { // RA_NONE / 0xffff end a chain
+            for (uint32_t v = (SK_RC_ABL & 512) ? RA_NONE : head[b & (RA_HT - 1)]; v < RA_CAP && f; v = nxt[v]) { // RA_NONE / 0xffff end a chain
                 const uint32_t xv = rec[v];
                 if ((xv >> 13) == b && ra_key<AEPB>(blk[v], xv) < key) f = false;
             }

@@ -1252,7 +1252,7 @@ __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const uint64_t *__res
     __shared__ uint64_t work[(kWork + 7) / 8]; // chunk records, chains, final values (or the big-run table)
     __shared__ uint8_t dirty[NL];
     __shared__ uint32_t rs[SK_PFL_NTMAX], rp[SK_PFL_NTMAX + 1]; // the fine bucket's run per tile: start, prefix
-    __shared__ uint32_t wsum[SK_PFL_ATPB / 64], s_ones;
+    __shared__ uint32_t wsum[SK_PFL_ATPB / 64];
     uint8_t *reg = reinterpret_cast<uint8_t *>(regs4);
     uint64_t *R = work;
     uint16_t *nxt = reinterpret_cast<uint16_t *>(R + SK_PFL_CAP);
@@ -1316,20 +1316,17 @@ __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const uint64_t *__res
         for (uint32_t u = ex; u < ex + len; u++) run_of[u] = uint8_t(threadIdx.x);
     const uint32_t dflt = (probe & 32) ? pfl_dflt(rc, par) : 2u; // 2: no default, every reply stored
     const bool sample = (probe & 32) && (blockIdx.x & 15u) == 0;
-    uint32_t nrep = 0; // replies made by this thread (sampled workgroups)
+    uint32_t nrep = 0, nones = 0; // replies made by this thread and how many were 1 (sampled workgroups)
     auto put = [&](uint32_t seq, uint32_t rep) {
         if (!(probe & 64) && rep != dflt) changed[seq] = uint8_t(rep); // probe & 64: dev ablation, no reply stores
         if (sample) {
             nrep++;
-            if (rep) atomicAdd(&s_ones, 1u);
+            nones += rep;
         }
     };
     for (uint32_t i = threadIdx.x; i < NL; i += SK_PFL_ATPB) dirty[i] = 0;
     for (uint32_t t = threadIdx.x; t < SK_PFL_HT; t += SK_PFL_ATPB) head[t] = 0xffffu;
-    if (threadIdx.x == 0) {
-        rp[ntile] = cnt;
-        s_ones = 0;
-    }
+    if (threadIdx.x == 0) rp[ntile] = cnt;
     __syncthreads();
     if (cnt <= SK_PFL_CAP) { // the whole fine bucket is one chunk: records and lines in one round trip
         load_lines();
@@ -1466,11 +1463,12 @@ __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const uint64_t *__res
     }
     __syncthreads();
     if (sample) { // the reply mix of a sample of fine buckets decides the next call's default
-        uint32_t tot;
+        uint32_t tot, ones;
         block_exscan<SK_PFL_ATPB>(nrep, wsum, &tot);
+        block_exscan<SK_PFL_ATPB>(nones, wsum, &ones);
         if (threadIdx.x == 0) {
             const uint32_t sh8 = (blockIdx.x >> 4) & 7u, q = 16 * (par ^ 1);
-            atomicAdd(&rc[q + sh8], s_ones);
+            atomicAdd(&rc[q + sh8], ones);
             atomicAdd(&rc[q + 8 + sh8], tot);
         }
     }
@@ -2366,6 +2364,22 @@ __global__ void __launch_bounds__(RC_ZTPB) k_bloom_rc_zero(uint32_t NB, uint32_t
 static_assert(RA_CAP >= 2 * RA_SEGMAX && RA_CAP % RC_TPB == 0 && RA_CAP < 0xffff, "windows: u16 links");
 static_assert(RA_JPT * RC_TPB <= 65536, "block numbers: u16 in the window, 16 bits of the order key");
 
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint32_t w = __shfl_xor(v, o);
+        v = w < v ? w : v;
+    }
+    return v;
+}
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint32_t w = __shfl_xor(v, o);
+        v = w > v ? w : v;
+    }
+    return v;
+}
 __device__ __forceinline__ uint32_t ra_mask(uint32_t b) { return (0x80u >> (b & 7u)) << (((b >> 3) & 3u) * 8u); }
 template <uint32_t AEPB> __device__ __forceinline__ uint32_t ra_key(uint32_t blk, uint32_t x) {
     return (blk << (AEPB == 4096 ? 12 : 11)) | ((x >> 1) & (AEPB - 1));
@@ -2453,13 +2467,21 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_ra_apply(uint32_t NB, uint32_t
             }
             __syncthreads(); // (first window: bits staged, heads cleared)
             // the window = the segments starting in [lo, lo + W), laid out from the first one's start (a segment that
-            // starts in the previous window belongs to it whole)
+            // starts in the previous window belongs to it whole).  Reduced per thread, then per wave, then one LDS
+            // atomic per wave: one atomic per segment on the same two words serialized ~8 k LDS atomics per window
+            uint32_t mn = RA_NONE, mx = 0;
 #pragma unroll
             for (int q = 0; q < RA_JPT; q++) {
                 const uint32_t cnt = sg[q] >> 16;
                 if (cnt == 0 || pre[q] < lo || pre[q] >= lo + W) continue;
-                atomicMin(&wbase, pre[q]);
-                atomicMax(&wend, pre[q] + cnt);
+                mn = pre[q] < mn ? pre[q] : mn;
+                mx = pre[q] + cnt > mx ? pre[q] + cnt : mx;
+            }
+            mn = wave_min_u32(mn);
+            mx = wave_max_u32(mx);
+            if ((threadIdx.x & 63u) == 0 && mx) {
+                atomicMin(&wbase, mn);
+                atomicMax(&wend, mx);
             }
             __syncthreads();
         }
@@ -2541,7 +2563,8 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_ra_apply(uint32_t NB, uint32_t
             head[b & (RA_HT - 1)] = RA_NONE;
         }
     }
-    atomicMax(&maxb, mymax);
+    mymax = wave_max_u32(mymax);
+    if ((threadIdx.x & 63u) == 0) atomicMax(&maxb, mymax);
     const bool changed = __syncthreads_or(anyset);
     if (threadIdx.x == 0) atomicMax(d_len, (unsigned long long)(b0 + (maxb >> 3) + 1));
     if (dense && changed) {

@@ -987,7 +987,10 @@ __device__ __forceinline__ uint64_t pfl_region_rec(const uint64_t *__restrict__ 
 // One workgroup per region g = b * ntile + t.  Dynamic LDS: cap records (u64) + nsub + 1 counts.
 // Outputs: rbase[g] (the region's first rec2 slot), C2[g][0..nsub] (exclusive starts of the fine buckets' runs
 // inside the region, [nsub] = records kept), rec2[rbase + ...] the runs; dropped records (slab >= nslab) reply 0.
-__global__ void __launch_bounds__(SK_PFL_RTPB) k_pfl_region(const uint64_t *__restrict__ chunks,
+#ifndef SK_PFL_RWPE
+#define SK_PFL_RWPE 4      // region waves per SIMD the register budget is sized for (one 1024-thread workgroup per CU)
+#endif
+__global__ void __launch_bounds__(SK_PFL_RTPB) __attribute__((amdgpu_waves_per_eu(SK_PFL_RWPE))) k_pfl_region(const uint64_t *__restrict__ chunks,
                                                             const uint32_t *__restrict__ S, uint32_t nblk, uint32_t tb,
                                                             uint32_t ntile, uint32_t nsub, uint32_t sh, PflPerm pm,
                                                             uint32_t cap, const uint32_t *__restrict__ tot,
@@ -1872,6 +1875,17 @@ __global__ void __launch_bounds__(256) k_bloom_contains_q(uint64_t n, const uint
 // 128 records gathered from one contiguous run, 256 no windows (region and segment table only), 512 no chain walk
 #define SK_RC_ABL 0
 #endif
+#ifndef SK_RC_STILE
+// The hash blocks write their segment entries interleaved by SK_RC_STILE regions, St[(r / T * NB + block) * T + r % T]:
+// a block's entries for T consecutive regions are one 128-B line (coalesced stores; a region-major row per region
+// made every entry a separate partial line, 0.12 ms of the contains hash per 32 M).  k_rc_stranspose then turns
+// them into the region-major rows S[r * NB + block] the probe / apply stream (their rows read as columns of the
+// interleaved table cost the probe 0.15 ms).  1: the hash writes the rows itself, no transpose.
+#define SK_RC_STILE 32
+#endif
+__host__ __device__ __forceinline__ uint64_t rc_sidx(uint32_t r, uint32_t j, uint32_t NB) {
+    return (uint64_t(r / SK_RC_STILE) * NB + j) * SK_RC_STILE + (r % SK_RC_STILE);
+}
 #define RC_RB 20                      // region = 2^20 bits = 128 KiB
 #define RC_TPB 1024
 #define RC_EPB 4096                   // elements per hash block (12-bit element-in-block)
@@ -2025,7 +2039,7 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_rc_hash(uint64_t n, const uint
         if (r < NR) {
             if (ADD && c4[q] > RA_SEGMAX) atomicMin(flag, piece); // the apply's windows assume short segments
             hist[r] = st;
-            if (!(SK_RC_ABL & 16) || ADD) S[uint64_t(r) * NB + jb] = st | (c4[q] << 16);
+            if (!(SK_RC_ABL & 16) || ADD) S[rc_sidx(r, jb, NB)] = st | (c4[q] << 16);
         }
         st += c4[q];
     }
@@ -2048,6 +2062,24 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_rc_hash(uint64_t n, const uint
     const uint4 *src = reinterpret_cast<const uint4 *>(lrec);
     if (!(SK_RC_ABL & 32) || ADD)
         for (uint32_t t = threadIdx.x; t < (tot + 3) / 4; t += RC_TPB) dst[t] = src[t];
+}
+
+// St (interleaved by SK_RC_STILE regions) -> S (region-major rows): one 32 x T tile of (block, region) entries per
+// workgroup, both sides read / written as 128-B lines
+__global__ void __launch_bounds__(256) k_rc_stranspose(const uint32_t *__restrict__ St, uint32_t *__restrict__ S,
+                                                       uint32_t NB, uint32_t NR) {
+    constexpr uint32_t T = SK_RC_STILE, TJ = 32;
+    __shared__ uint32_t tile[TJ][T + 1];
+    const uint32_t j0 = blockIdx.x * TJ, rt = blockIdx.y;
+    for (uint32_t e = threadIdx.x; e < TJ * T; e += 256) {
+        const uint32_t jj = e / T, rr = e % T;
+        if (j0 + jj < NB) tile[jj][rr] = St[(uint64_t(rt) * NB + j0 + jj) * T + rr];
+    }
+    __syncthreads();
+    for (uint32_t e = threadIdx.x; e < TJ * T; e += 256) {
+        const uint32_t rr = e / TJ, jj = e % TJ, r = rt * T + rr;
+        if (r < NR && j0 + jj < NB) S[uint64_t(r) * NB + j0 + jj] = tile[jj][rr];
+    }
 }
 
 // regions of XCD group x = blockIdx % 8 are [x*q, (x+1)*q), taken in order
@@ -2489,11 +2521,6 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_ra_apply(uint32_t NB, uint32_t
         const uint32_t nw = base == RA_NONE ? 0u : wend - base; // <= W + RA_SEGMAX = RA_CAP
         // a record whose bit is already set (before the batch or by an earlier window) is never a setter, and a
         // record on an unset bit only looks for smaller keys on its own bit: the former stay off the chains
-        auto link = [&](uint32_t u, uint32_t x) {
-            const uint32_t b = x >> 13;
-            if (RA_SKIPSET && dense && (filt[b >> 5] & ra_mask(b))) nxt[u] = 0xffffu;
-            else nxt[u] = uint16_t(atomicExch(&head[b & (RA_HT - 1)], u));
-        };
 #pragma unroll
         for (int q = 0; q < RA_JPT; q++) { // owners write each record's chunk word index
             const uint32_t cnt = sg[q] >> 16;
@@ -2507,38 +2534,45 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_ra_apply(uint32_t NB, uint32_t
             }
         }
         __syncthreads();
-#pragma unroll 1
-        for (uint32_t g = 0; g < RA_RPT; g += RA_GQ) { // this thread's records of the window, RA_GQ loads in flight
-            uint32_t x[RA_GQ];
+        // this thread's records u = thread + q * RC_TPB stay in registers (xs) with their bit's word (ws) from the
+        // link to the set: the scan and the set read no record back, and every load of a step is in flight at once
+        uint32_t xs[RA_RPT], ws[RA_RPT];
+#pragma unroll
+        for (uint32_t g = 0; g < RA_RPT; g += RA_GQ) { // RA_GQ gathers in flight
 #pragma unroll
             for (uint32_t q = 0; q < RA_GQ; q++) {
                 const uint32_t u = threadIdx.x + (g + q) * RC_TPB;
 #if SK_RC_ABL & 128
-                x[q] = u < nw ? chunks[(uint64_t(r) * W + lo + u) % (uint64_t(NB) * CH)] : 0u;
+                xs[g + q] = u < nw ? chunks[(uint64_t(r) * W + lo + u) % (uint64_t(NB) * CH)] : 0u;
 #else
-                x[q] = u < nw ? chunks[rec[u]] : 0u;
+                xs[g + q] = u < nw ? chunks[rec[u]] : 0u;
 #endif
             }
 #pragma unroll
             for (uint32_t q = 0; q < RA_GQ; q++) {
-                const uint32_t u = threadIdx.x + (g + q) * RC_TPB;
+                const uint32_t u = threadIdx.x + (g + q) * RC_TPB, b = xs[g + q] >> 13;
+                ws[g + q] = ~0u;
                 if (u < nw) {
-                    rec[u] = x[q];
-                    link(u, x[q]);
+                    rec[u] = xs[g + q];
+                    ws[g + q] = dense ? filt[b >> 5]
+                                      : __hip_atomic_load(gw + (b >> 5), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
+            }
+#pragma unroll
+            for (uint32_t q = 0; q < RA_GQ; q++) {
+                const uint32_t u = threadIdx.x + (g + q) * RC_TPB, b = xs[g + q] >> 13;
+                if (u >= nw) continue;
+                mymax = b > mymax ? b : mymax;
+                if (RA_SKIPSET && (ws[g + q] & ra_mask(b))) nxt[u] = 0xffffu;
+                else nxt[u] = uint16_t(atomicExch(&head[b & (RA_HT - 1)], u));
             }
         }
         __syncthreads();
         uint32_t first = 0; // bit q: record q of this thread sets its bit
-#pragma unroll 1
+#pragma unroll
         for (uint32_t q = 0; q < RA_RPT; q++) {
-            const uint32_t u = threadIdx.x + q * RC_TPB;
-            if (u >= nw) break;
-            const uint32_t xu = rec[u], b = xu >> 13;
-            mymax = b > mymax ? b : mymax;
-            const uint32_t w = dense ? filt[b >> 5]
-                                     : __hip_atomic_load(gw + (b >> 5), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (w & ra_mask(b)) continue; // set before this probe: not a setter
+            const uint32_t u = threadIdx.x + q * RC_TPB, xu = xs[q], b = xu >> 13;
+            if (u >= nw || (ws[q] & ra_mask(b))) continue; // set before this probe: not a setter
             const uint32_t key = ra_key<AEPB>(blk[u], xu);
             bool f = true;
             for (uint32_t v = (SK_RC_ABL & 512) ? RA_NONE : head[b & (RA_HT - 1)]; v < RA_CAP && f; v = nxt[v]) { // RA_NONE / 0xffff end a chain
@@ -2550,11 +2584,10 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_ra_apply(uint32_t NB, uint32_t
             if (!(xu & 1u) && (!(SK_RC_ABL & 64) || xu == 0xfffffffeu)) out[uint64_t(blk[u]) * AEPB + ((xu >> 1) & (AEPB - 1))] = 1;
         }
         __syncthreads(); // every probe of the window has read the bits
-#pragma unroll 1
+#pragma unroll
         for (uint32_t q = 0; q < RA_RPT; q++) {
-            const uint32_t u = threadIdx.x + q * RC_TPB;
-            if (u >= nw) break;
-            const uint32_t b = rec[u] >> 13;
+            const uint32_t u = threadIdx.x + q * RC_TPB, b = xs[q] >> 13;
+            if (u >= nw) continue;
             if (first & (1u << q)) {
                 anyset = true;
                 if (dense) atomicOr(&filt[b >> 5], ra_mask(b));
@@ -3421,6 +3454,17 @@ uint64_t rc_chunk_words(int k) { return uint64_t(RC_EPB) * uint64_t(k - 1); }
 
 static uint32_t ra_epb(int k) { return k <= RA_K4 ? 4096u : 2048u; }
 uint32_t ra_blocks(uint64_t n, int k) { return uint32_t((n + ra_epb(k) - 1) / ra_epb(k)); }
+uint64_t rc_seg_words(uint32_t nb, uint32_t nr) {
+    return uint64_t(nb) * ((nr + SK_RC_STILE - 1) / SK_RC_STILE * SK_RC_STILE);
+}
+bool rc_seg_interleaved() { return SK_RC_STILE > 1; }
+hipError_t launch_rc_stranspose(hipStream_t st, uint32_t nb, uint32_t nr, const uint32_t *St, uint32_t *S) {
+    if (SK_RC_STILE == 1) return hipSuccess;
+    hipLaunchKernelGGL(k_rc_stranspose, dim3((nb + 31) / 32, (nr + SK_RC_STILE - 1) / SK_RC_STILE), dim3(256), 0, st,
+                       St, S, nb, nr);
+    SK_LAUNCH_CHECK();
+    return hipSuccess;
+}
 uint32_t ra_regions(uint64_t size) { return uint32_t((size + (1ull << RA_RB) - 1) >> RA_RB); }
 uint64_t ra_piece(int k) { return uint64_t(RA_JPT) * RC_TPB * ra_epb(k); }
 uint64_t ra_chunk_words(int k) { return uint64_t(ra_epb(k)) * uint64_t(k); }

@@ -385,7 +385,7 @@ struct sk_ctx {
     uint32_t *d_zero = nullptr; // device u32[4] zeros: id 0 / empty length
     DBuf keys_a, keys_b, vals_a, vals_b, sort_tmp, in_off, in_bytes, in_ids, in_cmd, out_u8, misc, partial, hist,
         uni, ptrs, hist_a, hist_b, ovf, bloom_h;
-    DBuf rc_S, rc_rec;          // Bloom contains region schedule: segment table + probe records (contains only)
+    DBuf rc_S, rc_St, rc_rec;   // Bloom contains region schedule: segment table (+ the hash's interleaved one), records
     DBuf rc_Z, rc_GT;           // ... and its zero lists: per-region lists + the (region, reply group) run table
     DBuf in_soff, in_sbytes;    // host ingress in prefix form: suffix offsets (u32) and bytes, before the rebuild
     DBuf long_h, long_which;    // PFADD: hashes of long elements (k_ms_rounds) and their element indexes + layout
@@ -408,7 +408,7 @@ struct sk_ctx {
     std::vector<HllStr> hstr;
     DBuf ev, ev_n;
     uint64_t bloom_ra_min = 1;  // add batches >= this use the region schedule (SK_BLOOM_RA_MIN, 0 = never: sort path)
-    DBuf ra_S, ra_rec, ra_flag;
+    DBuf ra_S, ra_St, ra_rec, ra_flag;
     uint64_t bloom_rc_min = 2u << 20; // contains batches >= this use the region schedule (SK_BLOOM_RC_MIN, 0 = never)
     // PFADD line schedule (sketch-major group apply with the registers in LDS) for device batches of at least
     // pfl_min one-element commands (SK_PFL_MIN, 0 = never): scratch of one call
@@ -1284,8 +1284,8 @@ int sk_close(sk_ctx *c) {
     }
     for (DBuf *b : {&c->keys_a, &c->keys_b, &c->vals_a, &c->vals_b, &c->sort_tmp, &c->in_off, &c->in_bytes,
                     &c->in_ids, &c->in_cmd, &c->out_u8, &c->misc, &c->partial, &c->hist, &c->uni, &c->ptrs,
-                    &c->hist_a, &c->hist_b, &c->ovf, &c->bloom_h, &c->rc_S, &c->rc_rec, &c->rc_Z, &c->rc_GT, &c->in_soff, &c->in_sbytes, &c->long_h,
-                    &c->long_which, &c->long_plane, &c->long_flags, &c->ra_S, &c->ra_rec, &c->ra_flag, &c->ev, &c->ev_n,
+                    &c->hist_a, &c->hist_b, &c->ovf, &c->bloom_h, &c->rc_S, &c->rc_St, &c->rc_rec, &c->rc_Z, &c->rc_GT, &c->in_soff, &c->in_sbytes, &c->long_h,
+                    &c->long_which, &c->long_plane, &c->long_flags, &c->ra_S, &c->ra_St, &c->ra_rec, &c->ra_flag, &c->ev, &c->ev_n,
                     &c->pfl_chunks, &c->pfl_S, &c->pfl_C, &c->pfl_rc, &c->rt_cnt, &c->pfl_rec, &c->pfl_bk, &c->pfl_bv,
                     &c->pfl_ovf, &c->pfl_order})
         b->release();
@@ -2687,6 +2687,8 @@ static int bloom_add_device(sk_ctx *c, uint32_t id, int64_t size, int32_t k, uin
     const uint64_t magic = magic_for(usize), piece = sk::ra_piece(k);
     const uint64_t nb = sk::ra_blocks(std::min(n, piece), k), nr = sk::ra_regions(usize);
     HIPCHK(c, c->ra_S.ensure(nb * nr * 4));
+    if (sk::rc_seg_interleaved()) HIPCHK(c, c->ra_St.ensure(sk::rc_seg_words(nb, nr) * 4));
+    uint32_t *St = sk::rc_seg_interleaved() ? c->ra_St.as<uint32_t>() : c->ra_S.as<uint32_t>();
     HIPCHK(c, c->ra_rec.ensure(nb * sk::ra_chunk_words(k) * 4));
     HIPCHK(c, c->ra_flag.ensure(4));
     uint32_t *stop = c->ra_flag.as<uint32_t>();
@@ -2695,8 +2697,9 @@ static int bloom_add_device(sk_ctx *c, uint32_t id, int64_t size, int32_t k, uin
     for (uint64_t s0 = 0; s0 < n; s0 += piece, np++) {
         const uint64_t m = std::min(piece, n - s0);
         { Prof q_(c, 22);
-        HIPCHK(c, sk::launch_bloom_ra_hash(c->st, m, d_off + s0, d_bytes, usize, magic, k, c->ra_S.as<uint32_t>(),
-                                           c->ra_rec.as<uint32_t>(), stop, np)); }
+        HIPCHK(c, sk::launch_bloom_ra_hash(c->st, m, d_off + s0, d_bytes, usize, magic, k, St,
+                                           c->ra_rec.as<uint32_t>(), stop, np));
+        HIPCHK(c, sk::launch_rc_stranspose(c->st, sk::ra_blocks(m, k), uint32_t(nr), St, c->ra_S.as<uint32_t>())); }
         { Prof q_(c, 23);
         HIPCHK(c, sk::launch_bloom_ra_apply(c->st, m, usize, k, c->ra_S.as<uint32_t>(), c->ra_rec.as<uint32_t>(),
                                             c->strs[id].ptr, c->strs[id].cap, &c->d_dir[id].len, d_out + s0, stop,
@@ -2762,14 +2765,17 @@ static int bloom_contains_launch(sk_ctx *c, hipStream_t s, uint32_t id, int64_t 
     const uint64_t piece = uint64_t(32) << 20; // k_bloom_rc_probe serves <= RC_SMAX * RC_TPB blocks
     const uint64_t nb = sk::rc_blocks(std::min(n, piece)), nr = sk::rc_regions(usize);
     HIPCHK(c, c->rc_S.ensure(nb * nr * 4));
+    if (sk::rc_seg_interleaved()) HIPCHK(c, c->rc_St.ensure(sk::rc_seg_words(nb, nr) * 4));
+    uint32_t *St = sk::rc_seg_interleaved() ? c->rc_St.as<uint32_t>() : c->rc_S.as<uint32_t>();
     HIPCHK(c, c->rc_rec.ensure(nb * sk::rc_chunk_words(k) * 4));
     HIPCHK(c, c->rc_Z.ensure(sk::rc_zero_list_words(usize) * 4));
     HIPCHK(c, c->rc_GT.ensure(sk::rc_group_table_words(usize) * 4));
     for (uint64_t s0 = 0; s0 < n; s0 += piece) {
         uint64_t m = std::min(piece, n - s0);
         { Prof q_(c, 18, s);
-        HIPCHK(c, sk::launch_bloom_rc_hash(s, m, d_off + s0, d_bytes, usize, magic, k, c->rc_S.as<uint32_t>(),
-                                           c->rc_rec.as<uint32_t>(), d_out + s0)); }
+        HIPCHK(c, sk::launch_bloom_rc_hash(s, m, d_off + s0, d_bytes, usize, magic, k, St,
+                                           c->rc_rec.as<uint32_t>(), d_out + s0));
+        HIPCHK(c, sk::launch_rc_stranspose(s, sk::rc_blocks(m), uint32_t(nr), St, c->rc_S.as<uint32_t>())); }
         { Prof q_(c, 19, s);
         HIPCHK(c, sk::launch_bloom_rc_probe(s, m, usize, k, c->rc_S.as<uint32_t>(), c->rc_rec.as<uint32_t>(),
                                             c->strs[id].ptr, c->strs[id].cap, d_out + s0, c->rc_Z.as<uint32_t>(),

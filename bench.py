@@ -389,9 +389,10 @@ def pmc_traffic(phase):
 
     kern = {"bloom_contains": "sk::k_bloom_contains", "pfadd_claim": "sk::k_pfadd_claim",
             "pfadd_commit": "sk::k_pfadd_commit", "pfp_hash": "sk::k_pfp_hash", "pfp_apply": "sk::k_pfp_apply",
-            "pfp_reply": "sk::k_pfp_reply", "bloom_rc_hash": "sk::k_bloom_rc_hash<false>", "pfl_hash": "sk::k_pfl_hash",
+            "pfp_reply": "sk::k_pfp_reply", "bloom_rc_hash": "sk::k_bloom_rc_hash<false>+sk::k_rc_stranspose",
+            "pfl_hash": "sk::k_pfl_hash",
             "pfl_apply": "sk::k_pfl_fill+sk::k_pfl_plan+sk::k_pfl_apply", "pfl_part": "sk::k_pfl_tot+sk::k_pfl_region",
-            "bloom_rc_probe": "sk::k_bloom_rc_probe"}.get(phase)
+            "bloom_rc_probe": "sk::k_bloom_rc_probe+sk::k_bloom_rc_zero"}.get(phase)
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_summary.json")))
     if not kern or not files:
         return None

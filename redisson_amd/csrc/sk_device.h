@@ -507,6 +507,37 @@ struct BloomIdx {
     }
 };
 
+// The same walk for sizes < 2^32 (every Redis bit string: Bloom sizes are <= 4,294,967,294), the index arithmetic
+// in 32-bit words: r + A < 2 size is reduced with one conditional subtraction (its carry out of 32 bits included),
+// then C is taken off modulo size.  Only the 63-bit m stays 64-bit.
+struct BloomIdx32 {
+    uint64_t m, D1, D2;
+    uint32_t r, A1, A2, C, size;
+    __device__ __forceinline__ BloomIdx32(uint64_t h1, uint64_t h2, uint64_t size_, uint64_t magic)
+        : size(uint32_t(size_)) {
+        const uint64_t MAXL = 0x7fffffffffffffffull;
+        D1 = h1 & MAXL;
+        D2 = h2 & MAXL;
+        A1 = uint32_t(mod_invariant(D1, size_, magic));
+        A2 = uint32_t(mod_invariant(D2, size_, magic));
+        uint64_t c = mod_invariant(MAXL, size_, magic) + 1; // 2^63 mod size (uniform)
+        C = c == size_ ? 0u : uint32_t(c);
+        m = D1;
+        r = A1;
+    }
+    __device__ __forceinline__ void next(int p) {
+        const uint64_t D = (p & 1) ? D1 : D2;
+        const uint32_t A = (p & 1) ? A1 : A2;
+        const uint64_t s = m + D;
+        const bool w = (s >> 63) != 0;
+        m = s & 0x7fffffffffffffffull;
+        uint32_t x = r + A;
+        x = (x < r || x >= size) ? x - size : x; // (r + A) mod size
+        const uint32_t c = w ? C : 0u;
+        r = x >= c ? x - c : x - c + size;       // (x - c) mod size
+    }
+};
+
 // Redis bit strings are MSB-first: bit i lives in byte i>>3 at mask 0x80>>(i&7)
 __device__ __forceinline__ int get_bit(const uint8_t *buf, uint64_t len, uint64_t idx) {
     uint64_t byte = idx >> 3;

@@ -2009,7 +2009,7 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_rc_hash(uint64_t n, const uint
                 bloom_hashes(bytes + oa, len, &h1, &h2);
             }
             if (!ADD) out[i] = 1;
-            BloomIdx bi(h1, h2, size, magic);
+            BloomIdx32 bi(h1, h2, size, magic); // sizes < 2^32 (the records hold 32-bit indexes)
 #pragma unroll
             for (int p = 0; p < int(PM); p++) {
                 if (uint32_t(p) >= P) break;
@@ -2064,11 +2064,12 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_rc_hash(uint64_t n, const uint
         for (uint32_t t = threadIdx.x; t < (tot + 3) / 4; t += RC_TPB) dst[t] = src[t];
 }
 
-// St (interleaved by SK_RC_STILE regions) -> S (region-major rows): one 32 x T tile of (block, region) entries per
-// workgroup, both sides read / written as 128-B lines
+// St (interleaved by SK_RC_STILE regions) -> S (region-major rows): one 128 x T tile of (block, region) entries per
+// workgroup (16 KiB: a 4 KiB tile per workgroup left the copy launch-bound), both sides read / written as 128-B lines
+#define RC_STJ 128
 __global__ void __launch_bounds__(256) k_rc_stranspose(const uint32_t *__restrict__ St, uint32_t *__restrict__ S,
                                                        uint32_t NB, uint32_t NR) {
-    constexpr uint32_t T = SK_RC_STILE, TJ = 32;
+    constexpr uint32_t T = SK_RC_STILE, TJ = RC_STJ;
     __shared__ uint32_t tile[TJ][T + 1];
     const uint32_t j0 = blockIdx.x * TJ, rt = blockIdx.y;
     for (uint32_t e = threadIdx.x; e < TJ * T; e += 256) {
@@ -3460,7 +3461,7 @@ uint64_t rc_seg_words(uint32_t nb, uint32_t nr) {
 bool rc_seg_interleaved() { return SK_RC_STILE > 1; }
 hipError_t launch_rc_stranspose(hipStream_t st, uint32_t nb, uint32_t nr, const uint32_t *St, uint32_t *S) {
     if (SK_RC_STILE == 1) return hipSuccess;
-    hipLaunchKernelGGL(k_rc_stranspose, dim3((nb + 31) / 32, (nr + SK_RC_STILE - 1) / SK_RC_STILE), dim3(256), 0, st,
+    hipLaunchKernelGGL(k_rc_stranspose, dim3((nb + RC_STJ - 1) / RC_STJ, (nr + SK_RC_STILE - 1) / SK_RC_STILE), dim3(256), 0, st,
                        St, S, nb, nr);
     SK_LAUNCH_CHECK();
     return hipSuccess;

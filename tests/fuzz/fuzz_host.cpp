@@ -298,6 +298,14 @@ void fuzz_hash(Rng &r, long it) {
         check(bi.r == uint64_t(want[q]), "BloomIdx == or_bloom_indexes", it);
         bi.next(q);
     }
+    // BloomIdx32 (the region schedule's walk, sizes < 2^32), sizes drawn up to the largest Bloom size
+    const uint64_t s32 = r.below(4) == 0 ? 4294967294ull - r.below(3) : r.below(2) ? 4271038538ull : 1 + r.below(~0u - 2);
+    or_bloom_indexes(reinterpret_cast<const uint8_t *>(key.data()), len, k, int64_t(s32), want);
+    sk::BloomIdx32 b32(x, f, s32, ~0ull / s32);
+    for (int q = 0; q < k; q++) {
+        check(uint64_t(b32.r) == uint64_t(want[q]), "BloomIdx32 == or_bloom_indexes", it);
+        b32.next(q);
+    }
 }
 
 } // namespace

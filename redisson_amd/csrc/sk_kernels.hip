@@ -2065,21 +2065,39 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_rc_hash(uint64_t n, const uint
 }
 
 // St (interleaved by SK_RC_STILE regions) -> S (region-major rows): one 128 x T tile of (block, region) entries per
-// workgroup (16 KiB: a 4 KiB tile per workgroup left the copy launch-bound), both sides read / written as 128-B lines
+// workgroup (16 KiB: a 4 KiB tile per workgroup left the copy launch-bound), both sides moved as 16-B vectors
+// (4 consecutive entries of a block's T-region line in, 4 consecutive blocks of a region's row out; scalar when
+// NB is not a multiple of 4, i.e. a small last piece)
 #define RC_STJ 128
 __global__ void __launch_bounds__(256) k_rc_stranspose(const uint32_t *__restrict__ St, uint32_t *__restrict__ S,
                                                        uint32_t NB, uint32_t NR) {
     constexpr uint32_t T = SK_RC_STILE, TJ = RC_STJ;
+    static_assert(T % 4 == 0 && TJ % 4 == 0, "16-B vectors on both sides");
     __shared__ uint32_t tile[TJ][T + 1];
     const uint32_t j0 = blockIdx.x * TJ, rt = blockIdx.y;
-    for (uint32_t e = threadIdx.x; e < TJ * T; e += 256) {
-        const uint32_t jj = e / T, rr = e % T;
-        if (j0 + jj < NB) tile[jj][rr] = St[(uint64_t(rt) * NB + j0 + jj) * T + rr];
+    for (uint32_t e = threadIdx.x; e < TJ * T / 4; e += 256) {
+        const uint32_t jj = (4 * e) / T, rr = (4 * e) % T;
+        if (j0 + jj < NB) {
+            const uint4 v = *reinterpret_cast<const uint4 *>(St + (uint64_t(rt) * NB + j0 + jj) * T + rr);
+            tile[jj][rr] = v.x;
+            tile[jj][rr + 1] = v.y;
+            tile[jj][rr + 2] = v.z;
+            tile[jj][rr + 3] = v.w;
+        }
     }
     __syncthreads();
-    for (uint32_t e = threadIdx.x; e < TJ * T; e += 256) {
-        const uint32_t rr = e / TJ, jj = e % TJ, r = rt * T + rr;
-        if (r < NR && j0 + jj < NB) S[uint64_t(r) * NB + j0 + jj] = tile[jj][rr];
+    if ((NB & 3u) == 0) {
+        for (uint32_t e = threadIdx.x; e < TJ * T / 4; e += 256) {
+            const uint32_t rr = (4 * e) / TJ, jj = (4 * e) % TJ, r = rt * T + rr;
+            if (r < NR && j0 + jj < NB) // NB, j0 and jj are multiples of 4: the 4 blocks are all < NB
+                *reinterpret_cast<uint4 *>(S + uint64_t(r) * NB + j0 + jj) =
+                    make_uint4(tile[jj][rr], tile[jj + 1][rr], tile[jj + 2][rr], tile[jj + 3][rr]);
+        }
+    } else {
+        for (uint32_t e = threadIdx.x; e < TJ * T; e += 256) {
+            const uint32_t rr = e / TJ, jj = e % TJ, r = rt * T + rr;
+            if (r < NR && j0 + jj < NB) S[uint64_t(r) * NB + j0 + jj] = tile[jj][rr];
+        }
     }
 }
 

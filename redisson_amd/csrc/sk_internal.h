@@ -128,9 +128,13 @@ uint64_t ra_chunk_words(int k);
 uint32_t ra_max_probes();
 hipError_t launch_bloom_ra_hash(hipStream_t st, uint64_t n, const uint64_t *off, const uint8_t *bytes, uint64_t size,
                                 uint64_t magic, int k, uint32_t *S, uint32_t *recs, uint32_t *stop, uint32_t piece);
+// Z u32[ra_chunk_words(k) x blocks] (one lists, <= the records), zalloc u32 scratch counter,
+// GT u64[ra_group_table_words(size)] (one-list run table); out must be zeroed before (a stopped piece writes nothing)
+uint64_t ra_group_table_words(uint64_t size);
 hipError_t launch_bloom_ra_apply(hipStream_t st, uint64_t n, uint64_t size, int k, const uint32_t *S,
                                  const uint32_t *recs, uint8_t *bits, uint64_t cap_bytes, uint64_t *d_len,
-                                 uint8_t *out, const uint32_t *stop, uint32_t piece);
+                                 uint8_t *out, const uint32_t *stop, uint32_t piece, uint32_t *Z, uint32_t *zalloc,
+                                 uint64_t *GT);
 hipError_t launch_bloom_probes(hipStream_t st, uint64_t n, const uint64_t *off, const uint8_t *bytes, uint64_t size,
                                uint64_t magic, int k, uint64_t *keys);
 hipError_t launch_bloom_apply(hipStream_t st, uint64_t m, const uint64_t *keys, uint8_t *bits, uint64_t *d_len, int k,

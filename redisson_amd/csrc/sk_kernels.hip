@@ -2412,7 +2412,13 @@ __global__ void __launch_bounds__(RC_ZTPB) k_bloom_rc_zero(uint32_t NB, uint32_t
 #define RA_SKIPSET 1  // records on bits already set are not chained
 #endif
 #define RA_RPT (RA_CAP / RC_TPB)
+#ifndef SK_RA_OL
+#define SK_RA_OL 1    // add replies through one lists (k_bloom_ra_one) instead of a random byte store per new element
+#endif
+#define RA_GSH 16     // one list groups: 64 Ki elements of the piece (the reply bytes one k_bloom_ra_one workgroup writes)
+#define RA_NG 256     // groups per piece (<= 4096 blocks x 4096 elements / 64 Ki)
 static_assert(RA_CAP >= 2 * RA_SEGMAX && RA_CAP % RC_TPB == 0 && RA_CAP < 0xffff, "windows: u16 links");
+static_assert(RA_JPT * RC_TPB * 4096ull <= (uint64_t(RA_NG) << RA_GSH), "one-list groups of a piece");
 static_assert(RA_JPT * RC_TPB <= 65536, "block numbers: u16 in the window, 16 bits of the order key");
 
 __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
@@ -2441,8 +2447,9 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_ra_apply(uint32_t NB, uint32_t
                                                            const uint32_t *__restrict__ chunks, uint32_t P,
                                                            uint8_t *bits, uint64_t cap_bytes,
                                                            unsigned long long *d_len, uint8_t *__restrict__ out,
-                                                           const uint32_t *__restrict__ stop, uint32_t piece,
-                                                           int big) {
+                                                           const uint32_t *stop, uint32_t piece,
+                                                           int big, uint32_t *__restrict__ Z, uint32_t *zalloc,
+                                                           uint64_t *__restrict__ GT) {
     constexpr uint32_t NW = 1u << (RA_RB - 5); // u32 words per region
     __shared__ uint32_t filt[NW];
     __shared__ uint32_t rec[RA_CAP];
@@ -2451,6 +2458,15 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_ra_apply(uint32_t NB, uint32_t
     __shared__ uint32_t head[RA_HT];
     __shared__ uint32_t wsum[RC_TPB / 64];
     __shared__ uint32_t wbase, wend, maxb;
+#if SK_RA_OL
+    // one list: the piece-local indexes of the elements this region makes "new" (a setter among probes 0..k-2), in
+    // record order = block order, so each reply group is one run of the region's list (gfirst / glast); the run
+    // table GT[group][region] tells k_bloom_ra_one where.  The list lives in Z from a slot range the workgroup
+    // reserves (<= its records).
+    __shared__ uint32_t wc[RA_RPT * (RC_TPB / 64)], gfirst[RA_NG], glast[RA_NG], zbase, wtot;
+    uint32_t zn = 0, lastg = RA_NONE; // the region's list so far and its last entry's group (uniform, per thread)
+    const uint32_t ng = uint32_t((uint64_t(NB) * AEPB + (1u << RA_GSH) - 1) >> RA_GSH);
+#endif
     const uint32_t r = rc_region(blockIdx.x, NR);
     if (r >= NR || *stop <= piece) return; // uniform (stop: a hash pass of this or an earlier piece saw a long segment)
     const uint64_t b0 = uint64_t(r) << (RA_RB - 3);
@@ -2482,7 +2498,16 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_ra_apply(uint32_t NB, uint32_t
         pre[q] = total + e;
         total += tq;
     }
-    if (total == 0) return; // uniform: no probe in this region
+    if (total == 0) { // uniform: no probe in this region
+#if SK_RA_OL
+        for (uint32_t g = threadIdx.x; g < ng; g += RC_TPB) GT[uint64_t(g) * NR + r] = 0;
+#endif
+        return;
+    }
+#if SK_RA_OL
+    for (uint32_t g = threadIdx.x; g < RA_NG; g += RC_TPB) gfirst[g] = RA_NONE;
+    if (threadIdx.x == 0) zbase = atomicAdd(zalloc, total);
+#endif
     const bool dense = big || total >= RA_DENSE;
     if (dense) { // bytes past the buffer read as 0 and are not written back
         uint4 *fv = reinterpret_cast<uint4 *>(filt);
@@ -2588,21 +2613,42 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_ra_apply(uint32_t NB, uint32_t
         }
         __syncthreads();
         uint32_t first = 0; // bit q: record q of this thread sets its bit
+#if SK_RA_OL
+        uint32_t one = 0; // bit q: record q makes its element new
+#endif
 #pragma unroll
         for (uint32_t q = 0; q < RA_RPT; q++) {
             const uint32_t u = threadIdx.x + q * RC_TPB, xu = xs[q], b = xu >> 13;
             if (u >= nw || (ws[q] & ra_mask(b))) continue; // set before this probe: not a setter
             const uint32_t key = ra_key<AEPB>(blk[u], xu);
             bool f = true;
+            uint32_t steps = 0; // a chain holds <= nw records: a longer walk is a broken chain, reported, never a hang
             for (uint32_t v = (SK_RC_ABL & 512) ? RA_NONE : head[b & (RA_HT - 1)]; v < RA_CAP && f; v = nxt[v]) { // RA_NONE / 0xffff end a chain
                 const uint32_t xv = rec[v];
                 if ((xv >> 13) == b && ra_key<AEPB>(blk[v], xv) < key) f = false;
+                if (++steps > RA_CAP) {
+                    atomicOr(const_cast<uint32_t *>(stop) + 2, 1u);
+                    break;
+                }
             }
             if (!f) continue;
             first |= 1u << q;
+#if SK_RA_OL
+            if (!(xu & 1u)) one |= 1u << q;
+#else
             if (!(xu & 1u) && (!(SK_RC_ABL & 64) || xu == 0xfffffffeu)) out[uint64_t(blk[u]) * AEPB + ((xu >> 1) & (AEPB - 1))] = 1;
+#endif
         }
         __syncthreads(); // every probe of the window has read the bits
+#if SK_RA_OL
+        const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+        const uint64_t below = (1ull << lane) - 1ull;
+#pragma unroll
+        for (uint32_t q = 0; q < RA_RPT; q++) { // this window's new elements per (record row q, wave)
+            const uint64_t bal = __ballot((one >> q) & 1u);
+            if (lane == 0) wc[q * (RC_TPB / 64) + wv] = uint32_t(__popcll(bal));
+        }
+#endif
 #pragma unroll
         for (uint32_t q = 0; q < RA_RPT; q++) {
             const uint32_t u = threadIdx.x + q * RC_TPB, b = xs[q] >> 13;
@@ -2614,10 +2660,53 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_ra_apply(uint32_t NB, uint32_t
             }
             head[b & (RA_HT - 1)] = RA_NONE;
         }
+#if SK_RA_OL
+        __syncthreads(); // the (row, wave) counts are in; the window's records are no longer read: rec is free
+        if (threadIdx.x < 64) { // exclusive scan of the 128 counts in (row, wave) = record order
+            const uint32_t a = wc[2 * threadIdx.x], c = wc[2 * threadIdx.x + 1];
+            uint32_t x = a + c;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(x, o);
+                if (threadIdx.x >= uint32_t(o)) x += y;
+            }
+            wc[2 * threadIdx.x] = x - a - c;
+            wc[2 * threadIdx.x + 1] = x - c;
+            if (threadIdx.x == 63) wtot = x;
+        }
+        __syncthreads();
+#pragma unroll
+        for (uint32_t q = 0; q < RA_RPT; q++) { // the window's new elements in record order into rec
+            const uint64_t bal = __ballot((one >> q) & 1u);
+            const uint32_t u = threadIdx.x + q * RC_TPB; // blk[] holds the window's blocks until its next fill
+            if ((one >> q) & 1u)
+                rec[wc[q * (RC_TPB / 64) + wv] + uint32_t(__popcll(bal & below))] =
+                    uint32_t(blk[u]) * AEPB + ((xs[q] >> 1) & (AEPB - 1));
+        }
+        __syncthreads();
+        { // appended to the list, group runs marked; rec is rewritten only after the next window's first barrier
+            const uint32_t nt = wtot;
+            for (uint32_t i = threadIdx.x; i < nt; i += RC_TPB) {
+                const uint32_t e = rec[i], g = e >> RA_GSH;
+                Z[zbase + zn + i] = e;
+                if (i == 0 ? (zn == 0 || lastg != g) : (rec[i - 1] >> RA_GSH) != g) gfirst[g] = zn + i;
+                if (i + 1 == nt || (rec[i + 1] >> RA_GSH) != g) glast[g] = zn + i + 1;
+            }
+            if (nt) {
+                lastg = rec[nt - 1] >> RA_GSH;
+                zn += nt;
+            }
+        }
+#endif
     }
     mymax = wave_max_u32(mymax);
     if ((threadIdx.x & 63u) == 0) atomicMax(&maxb, mymax);
     const bool changed = __syncthreads_or(anyset);
+#if SK_RA_OL
+    for (uint32_t g = threadIdx.x; g < ng; g += RC_TPB)
+        GT[uint64_t(g) * NR + r] = gfirst[g] == RA_NONE ? 0ull
+                                                        : uint64_t(zbase + gfirst[g]) | uint64_t(glast[g] - gfirst[g]) << 32;
+#endif
     if (threadIdx.x == 0) atomicMax(d_len, (unsigned long long)(b0 + (maxb >> 3) + 1));
     if (dense && changed) {
         uint4 *dst = reinterpret_cast<uint4 *>(gw);
@@ -2625,6 +2714,69 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_ra_apply(uint32_t NB, uint32_t
 #pragma unroll
         for (uint32_t v = threadIdx.x; v < NW / 4; v += RC_TPB)
             if (b0 + uint64_t(v) * 16 < cap_bytes) dst[v] = fv[v];
+    }
+}
+
+// One reply group (64 Ki elements of the piece) per workgroup: every region's run of the group's new elements sets
+// bits of an 8 KiB LDS bitmap, then the group's reply bytes are written whole (16-B vectors: no partial lines).
+// Replaces one random byte store per new element in k_bloom_ra_apply (their partial-line write-backs were ~1.5 GB
+// of the apply's 2.1 GB written per 16 M piece).  A stopped piece (sort-path fallback) is left to the host.
+#define RA_OTPB 1024
+__global__ void __launch_bounds__(RA_OTPB) k_bloom_ra_one(uint32_t NR, uint64_t n, const uint32_t *__restrict__ Z,
+                                                          uint64_t zcap, const uint64_t *__restrict__ GT,
+                                                          uint8_t *__restrict__ out, const uint32_t *stop,
+                                                          uint32_t piece) {
+    constexpr uint32_t GE = 1u << RA_GSH, RPT = RA_NRMAX / RA_OTPB;
+    __shared__ uint32_t bm[GE / 32];
+    const uint32_t ng = uint32_t((n + GE - 1) >> RA_GSH), g = rc_region(blockIdx.x, ng);
+    if (g >= ng || *stop <= piece) return; // uniform
+    uint64_t t[RPT]; // this thread's run descriptors, every load in flight before the first run is read
+#pragma unroll
+    for (uint32_t q = 0; q < RPT; q++) {
+        const uint32_t rr = threadIdx.x + q * RA_OTPB;
+        t[q] = rr < NR ? GT[uint64_t(g) * NR + rr] : 0ull;
+    }
+    for (uint32_t v = threadIdx.x; v < GE / 32; v += RA_OTPB) bm[v] = 0;
+    __syncthreads();
+#pragma unroll
+    for (uint32_t q = 0; q < RPT; q++) {
+        const uint32_t st = uint32_t(t[q]);
+        uint32_t c = uint32_t(t[q] >> 32);
+        if (uint64_t(st) + c > zcap) { // a run past the lists: reported, never read
+            atomicOr(const_cast<uint32_t *>(stop) + 2, 2u);
+            c = 0;
+        }
+        const uint32_t *zs = Z + st;
+        uint32_t i = 0;
+        for (; i + 4 <= c; i += 4) { // four loads in flight
+            const uint32_t a0 = zs[i], a1 = zs[i + 1], a2 = zs[i + 2], a3 = zs[i + 3];
+            atomicOr(&bm[(a0 & (GE - 1)) >> 5], 1u << (a0 & 31u));
+            atomicOr(&bm[(a1 & (GE - 1)) >> 5], 1u << (a1 & 31u));
+            atomicOr(&bm[(a2 & (GE - 1)) >> 5], 1u << (a2 & 31u));
+            atomicOr(&bm[(a3 & (GE - 1)) >> 5], 1u << (a3 & 31u));
+        }
+        for (; i < c; i++) {
+            const uint32_t e = zs[i] & (GE - 1);
+            atomicOr(&bm[e >> 5], 1u << (e & 31u));
+        }
+    }
+    __syncthreads();
+    const uint64_t e0 = uint64_t(g) * GE;
+    const uint64_t ne = n - e0 < GE ? n - e0 : GE;
+    uint8_t *ob = out + e0;
+    auto spread = [](uint32_t b4) { // 4 bits -> 4 bytes of 0 / 1
+        return (b4 & 1u) | ((b4 & 2u) << 7) | ((b4 & 4u) << 14) | ((b4 & 8u) << 21);
+    };
+    if ((reinterpret_cast<uintptr_t>(ob) & 15u) == 0) {
+        for (uint32_t v = threadIdx.x; v < ne / 16; v += RA_OTPB) {
+            const uint32_t w16 = (bm[v >> 1] >> ((v & 1u) * 16u)) & 0xffffu;
+            reinterpret_cast<uint4 *>(ob)[v] = make_uint4(spread(w16 & 15u), spread((w16 >> 4) & 15u),
+                                                          spread((w16 >> 8) & 15u), spread(w16 >> 12));
+        }
+        for (uint32_t i = uint32_t(ne / 16) * 16 + threadIdx.x; i < ne; i += RA_OTPB)
+            ob[i] = uint8_t((bm[i >> 5] >> (i & 31u)) & 1u);
+    } else {
+        for (uint32_t i = threadIdx.x; i < ne; i += RA_OTPB) ob[i] = uint8_t((bm[i >> 5] >> (i & 31u)) & 1u);
     }
 }
 
@@ -3504,22 +3656,34 @@ hipError_t launch_bloom_ra_hash(hipStream_t st, uint64_t n, const uint64_t *off,
     return hipSuccess;
 }
 
+uint64_t ra_group_table_words(uint64_t size) { return uint64_t(RA_NG) * ra_regions(size); }
 hipError_t launch_bloom_ra_apply(hipStream_t st, uint64_t n, uint64_t size, int k, const uint32_t *S,
                                  const uint32_t *recs, uint8_t *bits, uint64_t cap_bytes, uint64_t *d_len,
-                                 uint8_t *out, const uint32_t *stop, uint32_t piece) {
+                                 uint8_t *out, const uint32_t *stop, uint32_t piece, uint32_t *Z, uint32_t *zalloc,
+                                 uint64_t *GT) {
     if (!n) return hipSuccess;
     uint32_t NR = ra_regions(size);
     // every region of a big piece expects >= RA_DENSE records: its bits are loaded up front
     const int big = n * uint64_t(k) >= uint64_t(2 * RA_DENSE) * NR;
+#if SK_RA_OL
+    hipError_t e = hipMemsetAsync(zalloc, 0, 4, st);
+    if (e != hipSuccess) return e;
+#endif
     if (ra_epb(k) == 4096)
         hipLaunchKernelGGL(k_bloom_ra_apply<4096>, dim3(8 * ((NR + 7) / 8)), dim3(RC_TPB), 0, st, ra_blocks(n, k), NR, S,
                            recs, uint32_t(k), bits, cap_bytes, reinterpret_cast<unsigned long long *>(d_len), out,
-                           stop, piece, big);
+                           stop, piece, big, Z, zalloc, GT);
     else
         hipLaunchKernelGGL(k_bloom_ra_apply<2048>, dim3(8 * ((NR + 7) / 8)), dim3(RC_TPB), 0, st, ra_blocks(n, k), NR, S,
                            recs, uint32_t(k), bits, cap_bytes, reinterpret_cast<unsigned long long *>(d_len), out,
-                           stop, piece, big);
+                           stop, piece, big, Z, zalloc, GT);
     SK_LAUNCH_CHECK();
+#if SK_RA_OL
+    const uint32_t ng = uint32_t((n + (1u << RA_GSH) - 1) >> RA_GSH);
+    hipLaunchKernelGGL(k_bloom_ra_one, dim3(8 * ((ng + 7) / 8)), dim3(RA_OTPB), 0, st, NR, n, Z,
+                       uint64_t(ra_blocks(n, k)) * ra_chunk_words(k), GT, out, stop, piece);
+    SK_LAUNCH_CHECK();
+#endif
     return hipSuccess;
 }
 

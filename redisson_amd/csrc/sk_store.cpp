@@ -408,7 +408,7 @@ struct sk_ctx {
     std::vector<HllStr> hstr;
     DBuf ev, ev_n;
     uint64_t bloom_ra_min = 1;  // add batches >= this use the region schedule (SK_BLOOM_RA_MIN, 0 = never: sort path)
-    DBuf ra_S, ra_St, ra_rec, ra_flag;
+    DBuf ra_S, ra_St, ra_rec, ra_flag, ra_Z, ra_GT; // Bloom add region schedule (+ its one lists and their run table)
     uint64_t bloom_rc_min = 2u << 20; // contains batches >= this use the region schedule (SK_BLOOM_RC_MIN, 0 = never)
     // PFADD line schedule (sketch-major group apply with the registers in LDS) for device batches of at least
     // pfl_min one-element commands (SK_PFL_MIN, 0 = never): scratch of one call
@@ -1285,7 +1285,7 @@ int sk_close(sk_ctx *c) {
     for (DBuf *b : {&c->keys_a, &c->keys_b, &c->vals_a, &c->vals_b, &c->sort_tmp, &c->in_off, &c->in_bytes,
                     &c->in_ids, &c->in_cmd, &c->out_u8, &c->misc, &c->partial, &c->hist, &c->uni, &c->ptrs,
                     &c->hist_a, &c->hist_b, &c->ovf, &c->bloom_h, &c->rc_S, &c->rc_St, &c->rc_rec, &c->rc_Z, &c->rc_GT, &c->in_soff, &c->in_sbytes, &c->long_h,
-                    &c->long_which, &c->long_plane, &c->long_flags, &c->ra_S, &c->ra_St, &c->ra_rec, &c->ra_flag, &c->ev, &c->ev_n,
+                    &c->long_which, &c->long_plane, &c->long_flags, &c->ra_S, &c->ra_St, &c->ra_rec, &c->ra_flag, &c->ra_Z, &c->ra_GT, &c->ev, &c->ev_n,
                     &c->pfl_chunks, &c->pfl_S, &c->pfl_C, &c->pfl_rc, &c->rt_cnt, &c->pfl_rec, &c->pfl_bk, &c->pfl_bv,
                     &c->pfl_ovf, &c->pfl_order})
         b->release();
@@ -2690,9 +2690,12 @@ static int bloom_add_device(sk_ctx *c, uint32_t id, int64_t size, int32_t k, uin
     if (sk::rc_seg_interleaved()) HIPCHK(c, c->ra_St.ensure(sk::rc_seg_words(nb, nr) * 4));
     uint32_t *St = sk::rc_seg_interleaved() ? c->ra_St.as<uint32_t>() : c->ra_S.as<uint32_t>();
     HIPCHK(c, c->ra_rec.ensure(nb * sk::ra_chunk_words(k) * 4));
-    HIPCHK(c, c->ra_flag.ensure(4));
+    HIPCHK(c, c->ra_flag.ensure(12)); // [0] the first stopped piece, [1] the one-list slot counter, [2] guard bits
+    HIPCHK(c, c->ra_Z.ensure(nb * sk::ra_chunk_words(k) * 4));
+    HIPCHK(c, c->ra_GT.ensure(sk::ra_group_table_words(usize) * 8));
     uint32_t *stop = c->ra_flag.as<uint32_t>();
     HIPCHK(c, hipMemsetAsync(stop, 0xff, 4, c->st));
+    HIPCHK(c, hipMemsetAsync(stop + 2, 0, 4, c->st));
     uint32_t np = 0;
     for (uint64_t s0 = 0; s0 < n; s0 += piece, np++) {
         const uint64_t m = std::min(piece, n - s0);
@@ -2703,12 +2706,14 @@ static int bloom_add_device(sk_ctx *c, uint32_t id, int64_t size, int32_t k, uin
         { Prof q_(c, 23);
         HIPCHK(c, sk::launch_bloom_ra_apply(c->st, m, usize, k, c->ra_S.as<uint32_t>(), c->ra_rec.as<uint32_t>(),
                                             c->strs[id].ptr, c->strs[id].cap, &c->d_dir[id].len, d_out + s0, stop,
-                                            np)); }
+                                            np, c->ra_Z.as<uint32_t>(), stop + 1, c->ra_GT.as<uint64_t>())); }
     }
-    uint32_t first_bad = 0;
-    HIPCHK(c, hipMemcpyAsync(&first_bad, stop, 4, hipMemcpyDeviceToHost, c->st));
+    uint32_t flags[3] = {0, 0, 0};
+    HIPCHK(c, hipMemcpyAsync(flags, stop, 12, hipMemcpyDeviceToHost, c->st));
     int r = sync(c);
     if (r) return r;
+    if (flags[2]) return fail(c, SK_EDEVICE, "Bloom add apply guard tripped (%u): a broken chain or one-list run", flags[2]);
+    const uint32_t first_bad = flags[0];
     for (uint64_t p = first_bad; p < np; p++) { // (first_bad = 0xffffffff: every piece was applied)
         const uint64_t s0 = p * piece, m = std::min(piece, n - s0);
         if ((r = bloom_add_sorted(c, id, size, k, m, d_off + s0, d_bytes, d_out + s0))) return r;

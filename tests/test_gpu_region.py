@@ -136,9 +136,12 @@ def _add_case(O, eng, name, n_exp, k, batches):
     for b in batches:
         got = eng.bloom_add(name, size, k, b)
         want = ref.bloom_add(size, k, b)
-        assert got == want, "k=%d add replies differ at %s" % (
-            k, [i for i, (g, w) in enumerate(zip(got, want)) if g != w][:8])
-    assert eng.get(name) == ref.bytes()
+        bad = [i for i, (g, w) in enumerate(zip(got, want)) if g != w]  # no pytest diff of 10^5-element lists
+        assert len(got) == len(want) and not bad, "k=%d add replies differ at %d places, first %s (got %s)" % (
+            k, len(bad), bad[:8], [got[i] for i in bad[:8]])
+    gb, wb = eng.get(name), ref.bytes()
+    assert len(gb) == len(wb) and gb == wb, "bit string differs: %d vs %d bytes, first byte %s" % (
+        len(gb), len(wb), next((i for i, (x, y) in enumerate(zip(gb, wb)) if x != y), None))
     return size
 
 

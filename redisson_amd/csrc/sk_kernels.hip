@@ -1621,21 +1621,25 @@ __global__ void __launch_bounds__(256) k_hll_union_partial(uint64_t n, const uin
     if (k1 > n) k1 = n;
     uint4 acc = make_uint4(0, 0, 0, 0);
     uint64_t k = k0;
-#define SK_SRC(kk) (reinterpret_cast<const uint4 *>(base + ((ids ? uint64_t(ids[kk] & SK_SLAB_MASK) : uint64_t(kk)) << 14)))
+    // the next step's slab ids are loaded while this step's 8 vectors are in flight (the id loads used to sit in
+    // front of every step's vector loads)
+    auto idof = [&](uint64_t kk) -> uint64_t { return ids ? uint64_t(ids[kk] & SK_SLAB_MASK) : kk; };
+    auto src = [&](uint64_t id) { return reinterpret_cast<const uint4 *>(base + (id << 14)) + lane16; };
+    uint64_t idn[8];
+    if (k + 8 <= k1)
+#pragma unroll
+        for (int j = 0; j < 8; j++) idn[j] = idof(k + j);
     for (; k + 8 <= k1; k += 8) { // 8 independent 16 B loads in flight per lane
-        uint4 a0 = ld_nt(SK_SRC(k) + lane16),
-              a1 = ld_nt(SK_SRC(k + 1) + lane16),
-              a2 = ld_nt(SK_SRC(k + 2) + lane16),
-              a3 = ld_nt(SK_SRC(k + 3) + lane16),
-              a4 = ld_nt(SK_SRC(k + 4) + lane16),
-              a5 = ld_nt(SK_SRC(k + 5) + lane16),
-              a6 = ld_nt(SK_SRC(k + 6) + lane16),
-              a7 = ld_nt(SK_SRC(k + 7) + lane16);
-        acc = bytemax4(acc, bytemax4(bytemax4(bytemax4(a0, a1), bytemax4(a2, a3)),
-                                     bytemax4(bytemax4(a4, a5), bytemax4(a6, a7))));
+        uint4 a[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) a[j] = ld_nt(src(idn[j]));
+        if (k + 16 <= k1)
+#pragma unroll
+            for (int j = 0; j < 8; j++) idn[j] = idof(k + 8 + j);
+        acc = bytemax4(acc, bytemax4(bytemax4(bytemax4(a[0], a[1]), bytemax4(a[2], a[3])),
+                                     bytemax4(bytemax4(a[4], a[5]), bytemax4(a[6], a[7]))));
     }
-    for (; k < k1; k++) acc = bytemax4(acc, SK_SRC(k)[lane16]);
-#undef SK_SRC
+    for (; k < k1; k++) acc = bytemax4(acc, *src(idof(k)));
     reinterpret_cast<uint4 *>(partial + g * 16384)[lane16] = acc;
 }
 

@@ -2390,7 +2390,8 @@ int sk_bitcount(sk_ctx *c, const uint8_t *key, uint64_t len, uint64_t *out) {
     if (id == kNoId) return SK_OK;
     uint64_t l;
     if ((r = str_len(c, id, &l))) return r;
-    HIPCHK(c, sk::launch_bitcount(c->st, c->strs[id].ptr, l, c->misc.as<uint64_t>()));
+    { Prof p_(c, 11);
+    HIPCHK(c, sk::launch_bitcount(c->st, c->strs[id].ptr, l, c->misc.as<uint64_t>())); }
     HIPCHK(c, hipMemcpyAsync(out, c->misc.p, 8, hipMemcpyDeviceToHost, c->st));
     return sync(c);
 }
@@ -2471,8 +2472,9 @@ int sk_bitop(sk_ctx *c, int op, const uint8_t *dest, uint64_t dest_len, uint32_t
     std::memcpy(blob.data(), ptrs.data(), n_src * 8);
     std::memcpy(blob.data() + n_src * 8, lens.data(), n_src * 8);
     HIPCHK(c, hipMemcpyAsync(c->ptrs.p, blob.data(), blob.size(), hipMemcpyHostToDevice, c->st));
+    { Prof p_(c, 12);
     HIPCHK(c, sk::launch_bitop(c->st, op, n_src, reinterpret_cast<const uint8_t *const *>(c->ptrs.p),
-                               reinterpret_cast<const uint64_t *>(c->ptrs.as<uint8_t>() + n_src * 8), maxlen, dst));
+                               reinterpret_cast<const uint64_t *>(c->ptrs.as<uint8_t>() + n_src * 8), maxlen, dst)); }
     if ((r = sync(c))) return r;
     if (did == kNoId) { // create / replace the destination (BITOP overwrites any type)
         bool removed;

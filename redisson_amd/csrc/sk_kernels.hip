@@ -2117,7 +2117,9 @@ __device__ __forceinline__ uint32_t rc_region(uint32_t b, uint32_t NR) {
 // segment that does not fit them (rare: > 13 records) finishes word by word.
 // The region's own stream is issued before the segment loads and lands in
 // LDS while they are in flight.
+#ifndef RC_SEGV
 #define RC_SEGV 4
+#endif
 #define RC_JB 2
 __device__ __forceinline__ void rc_test(const uint8_t *fb, uint32_t x, uint8_t *ob) {
     uint32_t bit = x >> 12;

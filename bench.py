@@ -55,7 +55,18 @@ def dist_setup():
     if world > 1:
         import torch.distributed as dist  # gloo only: CPU-side rendezvous / barrier / max
 
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        # gloo prints its peer-connection notice on the C-level stdout: send it to stderr, so that rank 0's stdout
+        # carries the one JSON line the driver parses
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+            dist.barrier()
+        finally:
+            sys.stdout.flush()
+            os.dup2(saved, 1)
+            os.close(saved)
         pg = dist
     return world, rank, local, pg
 

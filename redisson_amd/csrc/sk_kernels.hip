@@ -2337,7 +2337,9 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_rc_probe(uint32_t NB, uint32_t
 // (GT[region][group] names the run) clear bits of an 8 KiB LDS bitmap of the group's replies, which is then ANDed
 // into out with 16-B vectors.  Each thread's run descriptors are loaded up front (independent loads in flight), and
 // groups of one XCD are consecutive (speed only): their runs of one region are neighbours.
+#ifndef RC_ZTPB
 #define RC_ZTPB 512
+#endif
 __global__ void __launch_bounds__(RC_ZTPB) k_bloom_rc_zero(uint32_t NB, uint32_t NR, uint64_t n,
                                                            const uint32_t *__restrict__ Z,
                                                            const uint32_t *__restrict__ GT,
@@ -2360,7 +2362,16 @@ __global__ void __launch_bounds__(RC_ZTPB) k_bloom_rc_zero(uint32_t NB, uint32_t
     for (uint32_t q = 0; q < RPT; q++) {
         const uint32_t rr = threadIdx.x + q * RC_ZTPB, st = t[q] & 0xffffu, c = t[q] >> 16;
         const uint32_t *zs = Z + uint64_t(rr) * RC_ZCAP + st;
-        for (uint32_t i = 0; i < c; i++) {
+        uint32_t i = 0;
+        for (; i + 4 <= c; i += 4) { // four list loads in flight
+            const uint32_t a0 = zs[i] & (GE - 1), a1 = zs[i + 1] & (GE - 1), a2 = zs[i + 2] & (GE - 1),
+                           a3 = zs[i + 3] & (GE - 1);
+            atomicAnd(&bm[a0 >> 5], ~(1u << (a0 & 31u)));
+            atomicAnd(&bm[a1 >> 5], ~(1u << (a1 & 31u)));
+            atomicAnd(&bm[a2 >> 5], ~(1u << (a2 & 31u)));
+            atomicAnd(&bm[a3 >> 5], ~(1u << (a3 & 31u)));
+        }
+        for (; i < c; i++) {
             const uint32_t e = zs[i] & (GE - 1);
             atomicAnd(&bm[e >> 5], ~(1u << (e & 31u)));
         }

@@ -39,6 +39,9 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 HLL_KERNELS = ["pfp_hash", "pfp_apply", "pfp_reply", "pfl_hash", "pfl_part", "pfl_apply", "pfadd_claim",
                "pfadd_commit", "pfadd_hash", "pfadd_apply"]
 BLOOM_KERNELS = ["bloom_rc_hash", "bloom_rc_probe"]
+# the kernels each timed phase launches (the roofline label names them all)
+PHASE_KERNELS = {"bloom_rc_hash": "k_bloom_rc_hash + k_rc_stranspose", "bloom_rc_probe": "k_bloom_rc_probe + k_bloom_rc_zero",
+                 "pfl_part": "k_pfl_tot + k_pfl_region", "pfl_apply": "k_pfl_fill + k_pfl_plan + k_pfl_apply"}
 CHAINS = ["pfadd", "bloom_contains"]
 PHASES = HLL_KERNELS + ["pfadd_sort"] + BLOOM_KERNELS + CHAINS
 
@@ -337,7 +340,8 @@ def main():
         "bloom_add_per_s": fill / add_s if add_s else None,
         "device_ms_timed_region": dev_ms,
         "host_enqueue_ms_per_step": t_enq / K * 1e3,
-        "roofline": {"kernel": "%s chain (%s)" % (dom, " + ".join("k_" + p_ for p_ in chain_kernels[dom])),
+        "roofline": {"kernel": "%s chain (%s)" % (dom, " + ".join(PHASE_KERNELS.get(p_, "k_" + p_)
+                                                                 for p_ in chain_kernels[dom])),
                      "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "traffic_GBps": traffic / (avg_ms * 1e-3) / 1e9 if traffic else None,

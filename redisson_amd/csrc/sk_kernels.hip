@@ -1876,7 +1876,9 @@ __global__ void __launch_bounds__(256) k_bloom_contains_q(uint64_t n, const uint
 #ifndef SK_RC_ABL
 // dev ablations of the contains chain (results discarded): 1 no reply stores, 2 no record loads, 4 no region load,
 // 8 no hash arithmetic, 16 no segment-table stores, 32 no record stores, 64 no add reply stores; of the add apply:
-// 128 records gathered from one contiguous run, 256 no windows (region and segment table only), 512 no chain walk
+// 128 records gathered from one contiguous run, 256 no windows (region and segment table only), 512 no chain walk;
+// 1024: the probe reads each (block, region) segment from a region-major position ((r * NB + j) * CH / NR words,
+// as a region-major record arena would place it: a wave's segments adjacent) -- a timing probe, results discarded
 #define SK_RC_ABL 0
 #endif
 #ifndef SK_RC_STILE
@@ -2133,9 +2135,20 @@ __device__ __forceinline__ void rc_test(const uint8_t *fb, uint32_t x, uint8_t *
 #define RC_PF 3   // steps of segment loads in flight per thread (2: one step ahead)
 #endif
 __device__ __forceinline__ void rc_load_seg(const uint32_t *chunks, uint64_t CH, uint32_t j, uint32_t seg,
-                                            uint4 (&w)[RC_SEGV]) {
+                                            uint4 (&w)[RC_SEGV], uint32_t r = 0, uint32_t NB = 0, uint32_t NR = 1) {
     uint32_t st = seg & 0xffffu, cnt = seg >> 16;
+#if SK_RC_ABL & 1024
+    uint64_t w0 = (uint64_t(r) * NB + j) * CH / NR;
+    const uint64_t wmax = uint64_t(NB) * CH - 4 * RC_SEGV - 4;
+    w0 = (w0 < wmax ? w0 : wmax) & ~uint64_t(3);
+    const uint4 *cv = reinterpret_cast<const uint4 *>(chunks + w0);
+    if (j >= NB) cv = reinterpret_cast<const uint4 *>(chunks); // seg == 0: nothing read
+#else
+    (void)r;
+    (void)NB;
+    (void)NR;
     const uint4 *cv = reinterpret_cast<const uint4 *>(chunks + uint64_t(j) * CH) + (st >> 2);
+#endif
     uint32_t nv = ((st & 3u) + cnt + 3u) >> 2; // vectors covering the segment
 #if SK_RC_ABL & 2
     (void)cv;
@@ -2280,7 +2293,8 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_rc_probe(uint32_t NB, uint32_t
         const uint64_t CH = uint64_t(RC_EPB) * P;
         uint4 w[RC_PF][RC_SEGV];
 #pragma unroll
-        for (int u = 0; u < RC_PF - 1; u++) rc_load_seg(chunks, CH, threadIdx.x + u * RC_TPB, seg0[u], w[u]);
+        for (int u = 0; u < RC_PF - 1; u++)
+            rc_load_seg(chunks, CH, threadIdx.x + u * RC_TPB, seg0[u], w[u], r, NB, NR);
 #pragma unroll
         for (uint32_t q = 0; q < VPT; q++) filt[threadIdx.x + q * RC_TPB] = fv[q];
         __syncthreads();
@@ -2290,7 +2304,7 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_rc_probe(uint32_t NB, uint32_t
             if (uint32_t(u) * RC_TPB >= NB) break; // no thread has a block at this step (uniform)
             if (u + RC_PF - 1 < RC_SMAX)
                 rc_load_seg(chunks, CH, threadIdx.x + (u + RC_PF - 1) * RC_TPB, seg0[u + RC_PF - 1],
-                            w[(u + RC_PF - 1) % RC_PF]);
+                            w[(u + RC_PF - 1) % RC_PF], r, NB, NR);
 #if SK_RC_ZL
             rc_test_seg_zl(fb, chunks, CH, threadIdx.x + u * RC_TPB, seg0[u], w[u % RC_PF], out, zl, &zn);
 #else

@@ -417,7 +417,7 @@ def pmc_traffic(phase):
         def find(k_):   # template kernels may carry more arguments in newer builds (k_bloom_rc_hash<false, 2048u>)
             if k_ in ks:
                 return ks[k_]
-            stem = k_[:-1] + "," if k_.endswith(">") else None
+            stem = k_[:-1] + "," if k_.endswith(">") else k_ + "<"   # or a kernel that became a template
             hit = [v for n_, v in ks.items() if stem and n_.startswith(stem)]
             return hit[0] if len(hit) == 1 else None
         parts = [find(k_) for k_ in kern.split("+")]   # a phase of several launches: their sum

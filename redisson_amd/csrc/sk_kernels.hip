@@ -1937,7 +1937,7 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_rc_hash(uint64_t n, const uint
     const uint32_t jq = (NB + 7) / 8, jb = (blockIdx.x & 7u) * jq + (blockIdx.x >> 3);
     if (jb >= NB) return; // uniform
     __shared__ uint32_t wsum[RC_TPB / 64];
-    __shared__ uint64_t buf[ADD ? ra_bufw(AEPB, PM) : RC_BUFW];
+    __shared__ uint64_t buf[ra_bufw(EPB, PM)]; // two key windows, then the block's records (EPB x PM u32)
     uint64_t *win[2] = {buf, buf + SK_PFP_WIN};
     uint32_t *lrec = reinterpret_cast<uint32_t *>(buf); // after the last hash round
     for (uint32_t r = threadIdx.x; r < NR; r += RC_TPB) hist[r] = 0;

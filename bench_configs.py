@@ -218,13 +218,21 @@ def c5(eng, args):
     chunk = 1 << 26
     keys = [b"bs5:%d" % i for i in range(4)]
     t_set = t_get = 0.0
+    set_dev_ms = 0.0
     d_out = eng.alloc(chunk)
+    eng.setbit([keys[0]], [bits - 1], [1])   # the string created at full length untimed (a 2 GiB allocation)
     for key in keys:
         for s in range(0, n if key == keys[0] else n // 16, chunk):
             m = min(chunk, n - s)
             d_off = eng.to_device(rng.integers(0, bits, m, dtype=np.uint64))
+            if key == keys[0]:
+                eng.prof_reset()
+                eng.prof_enable(True)
             dt = timed(eng, lambda: eng.setbit_dev(key, m, d_off, 1))
             if key == keys[0]:
+                eng.prof_enable(False)
+                k_, ms_ = eng.prof_read("setbit")
+                set_dev_ms += ms_ if k_ else 0.0
                 t_set += dt
                 t_get += timed(eng, lambda: eng.getbit_dev(key, m, d_off, d_out))
             d_off.free()
@@ -247,6 +255,9 @@ def c5(eng, args):
           "value": 2 * n / (t_set + t_get), "unit": "ops/s",
           "config": {"workload": "c5", "bits": bits, "ops": n},
           "setbit_per_s": n / t_set, "getbit_per_s": n / t_get,
+          "setbit_device_per_s": n / (set_dev_ms * 1e-3) if set_dev_ms else None,
+          "setbit": "SETBIT_VOID (RBitSet.set(i)) in 64 M-op calls on the full-length string (created untimed); a dense "
+                    "call (>= 2 ops per 128-B line) takes the region path (radix sort by 32 KiB region + k_sbv_apply)",
           "bitcount_GBps": nbytes / t_bc / 1e9, "bitop_and4_GBps": 5 * nbytes / t_and / 1e9,
           "bitop_or2_GBps": 3 * nbytes / t_or / 1e9,
           "device_GBps": {"bitcount": gbps(nbytes, d_bc), "bitop_and4": gbps(5 * nbytes, d_and),

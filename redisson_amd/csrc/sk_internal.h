@@ -148,6 +148,10 @@ hipError_t launch_setbit_keys(hipStream_t st, uint64_t n, const uint32_t *sid, c
 hipError_t launch_setbit_apply(hipStream_t st, uint64_t n, const uint64_t *keys, const uint32_t *vals,
                                const uint8_t *values, uint8_t value_all, void *dir, uint8_t *out_old);
 hipError_t launch_setbit_void(hipStream_t st, uint64_t n, const uint64_t *offs, uint8_t *buf, uint32_t value);
+// dense SETBIT_VOID: keys = the offsets grouped by 2^sbv_region_bits()-bit region (ascending), start u32[regions + 1]
+uint32_t sbv_region_bits();
+hipError_t launch_setbit_void_regions(hipStream_t st, uint64_t n, const uint64_t *keys, uint64_t max_off,
+                                      uint32_t *start, uint8_t *buf, uint64_t cap, uint32_t value);
 hipError_t launch_bit_range(hipStream_t st, uint8_t *buf, uint64_t from, uint64_t to, uint32_t value);
 hipError_t launch_max_u64(hipStream_t st, uint64_t n, const uint64_t *v, uint64_t *out);
 hipError_t launch_bitcount(hipStream_t st, const uint8_t *buf, uint64_t len, uint64_t *out);

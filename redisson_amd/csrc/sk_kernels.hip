@@ -3014,6 +3014,54 @@ __global__ void __launch_bounds__(256) k_setbit_void(uint64_t n, const uint64_t 
     }
 }
 
+// SETBIT_VOID in bulk (a dense batch: >= 2 ops per 128-B line of the string, C5's 64 M ops on 2^34 bits give 4): the
+// ops sorted by 32 KiB region (a radix sort on the offset's region bits only), then one workgroup per region with
+// ops stages the region in LDS, ORs (ANDs) its ops in with LDS atomics and writes it back.  The string streams in
+// and out once instead of taking one random device-scope atomic per op; the result is the same set of bits (one
+// value, so the ops commute).
+#define SBV_RB 18   // region = 2^18 bits = 32 KiB of LDS
+#define SBV_TPB 256
+__global__ void __launch_bounds__(256) k_sbv_starts(uint64_t n, const uint64_t *__restrict__ keys, uint32_t NR,
+                                                    uint32_t *__restrict__ start) {
+    const uint64_t i = uint64_t(blockIdx.x) * 256 + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t r = uint32_t(keys[i] >> SBV_RB);
+    const uint32_t rp = i ? uint32_t(keys[i - 1] >> SBV_RB) + 1u : 0u; // regions rp..r start at op i
+    for (uint32_t q = rp; q <= r; q++) start[q] = uint32_t(i);
+    if (i == n - 1)
+        for (uint32_t q = r + 1; q <= NR; q++) start[q] = uint32_t(n);
+}
+__global__ void __launch_bounds__(SBV_TPB) k_sbv_apply(const uint64_t *__restrict__ keys,
+                                                       const uint32_t *__restrict__ start, uint8_t *buf, uint64_t cap,
+                                                       uint32_t value) {
+    constexpr uint32_t RBYTES = 1u << (SBV_RB - 3), NV = RBYTES / 16, VPT = NV / SBV_TPB;
+    __shared__ uint4 reg4[NV];
+    const uint32_t r = blockIdx.x, lo = start[r], hi = start[r + 1];
+    if (lo == hi) return; // uniform: no op in this region
+    const uint64_t b0 = uint64_t(r) * RBYTES; // < cap: an op's byte lies in the region
+    uint4 *src = reinterpret_cast<uint4 *>(buf + b0);
+    const uint32_t nv = cap - b0 >= RBYTES ? NV : uint32_t((cap - b0) / 16); // cap is a multiple of 16
+    if (nv == NV) { // a whole region: every load issued before the first LDS store
+        uint4 t[VPT];
+#pragma unroll
+        for (uint32_t q = 0; q < VPT; q++) t[q] = src[threadIdx.x + q * SBV_TPB];
+#pragma unroll
+        for (uint32_t q = 0; q < VPT; q++) reg4[threadIdx.x + q * SBV_TPB] = t[q];
+    } else {
+        for (uint32_t v = threadIdx.x; v < nv; v += SBV_TPB) reg4[v] = src[v];
+    }
+    __syncthreads();
+    uint32_t *w = reinterpret_cast<uint32_t *>(reg4);
+    for (uint32_t i = lo + threadIdx.x; i < hi; i += SBV_TPB) {
+        const uint32_t lb = uint32_t(keys[i] - (uint64_t(r) << SBV_RB));
+        const uint32_t byte = lb >> 3, mask = 1u << ((byte & 3u) * 8u + (7u - (lb & 7u))); // bit_word's layout
+        if (value) atomicOr(&w[byte >> 2], mask);
+        else atomicAnd(&w[byte >> 2], ~mask);
+    }
+    __syncthreads();
+    for (uint32_t v = threadIdx.x; v < nv; v += SBV_TPB) src[v] = reg4[v];
+}
+
 // RBitSet.set(from, to) / clear(from, to) (M:RedissonBitSet.java:202-228:
 // one SETBIT_VOID per bit): bits [from, to) of an MSB-first string set to
 // `value`.  One lane per 16-B vector; vectors inside the range are stored
@@ -3827,6 +3875,18 @@ hipError_t launch_setbit_apply(hipStream_t st, uint64_t n, const uint64_t *keys,
 hipError_t launch_setbit_void(hipStream_t st, uint64_t n, const uint64_t *offs, uint8_t *buf, uint32_t value) {
     if (!n) return hipSuccess;
     hipLaunchKernelGGL(k_setbit_void, dim3(grid_for(n, 256)), dim3(256), 0, st, n, offs, buf, value);
+    SK_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+uint32_t sbv_region_bits() { return SBV_RB; }
+hipError_t launch_setbit_void_regions(hipStream_t st, uint64_t n, const uint64_t *keys, uint64_t max_off,
+                                      uint32_t *start, uint8_t *buf, uint64_t cap, uint32_t value) {
+    if (!n) return hipSuccess;
+    const uint32_t NR = uint32_t(max_off >> SBV_RB) + 1;
+    hipLaunchKernelGGL(k_sbv_starts, dim3(grid_for(n, 256)), dim3(256), 0, st, n, keys, NR, start);
+    SK_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_sbv_apply, dim3(NR), dim3(SBV_TPB), 0, st, keys, start, buf, cap, value);
     SK_LAUNCH_CHECK();
     return hipSuccess;
 }

@@ -363,6 +363,7 @@ struct sk_ctx {
     bool async_dev = false;     // sk_set_async: _dev calls return without a final sync
     int pfadd_path = 1;         // 0 claim/commit, 1 partition, 2 sorted (SK_PFADD_PATH); dense batches use 2
     bool pfp_direct = true;     // partition path, one element per command: apply writes replies (SK_PFP_DIRECT)
+    uint64_t sbv_min = 1u << 20; // SETBIT_VOID batches from which a dense one takes the region path (SK_SBV_MIN)
     int claim_all = 1;          // PFADD claim: 1 = every element claims (R0 from the atomic), 0 = load first, claim candidates (SK_PFADD_CLAIM)
     int read_stream = 1;        // async Bloom contains on the read stream st2 (SK_READ_STREAM=0: main stream)
     int bloom_sched = 0;        // contains kernel (SK_BLOOM_SCHED): 0 one element per thread; 1 probe queue, 4/lane; 3 split hash / probe passes
@@ -1233,6 +1234,7 @@ int sk_open(const sk_config *cfg, sk_ctx **out) {
     if (const char *e = getenv("SK_PFADD_CLAIM")) c->claim_all = atoi(e);
     if (const char *e = getenv("SK_PFADD_PATH")) c->pfadd_path = atoi(e);
     if (const char *e = getenv("SK_PFP_DIRECT")) c->pfp_direct = atoi(e) != 0;
+    if (const char *e = getenv("SK_SBV_MIN")) c->sbv_min = strtoull(e, nullptr, 10);
     if (const char *e = getenv("SK_BLOOM_RC_MIN")) c->bloom_rc_min = strtoull(e, nullptr, 10);
     if (const char *e = getenv("SK_BLOOM_RA_MIN")) c->bloom_ra_min = strtoull(e, nullptr, 10);
     if (const char *e = getenv("SK_HLL_EXACT_STRINGS")) c->hll_exact = atoi(e) != 0;
@@ -2207,8 +2209,29 @@ int sk_setbit_dev(sk_ctx *c, const uint8_t *key, uint64_t len, uint64_t n, const
     if ((r = str_len(c, id, &cur))) return r;
     if (need > cur && (r = str_set_len(c, id, need))) return r;
     if (!d_out_old) {
-        { Prof p_(c, 9);
-        HIPCHK(c, sk::launch_setbit_void(c->st, n, d_offsets, c->strs[id].ptr, value & 1)); }
+        // a dense batch (>= 2 ops per 128-B line of the string) streams the string through LDS region by region
+        // instead of one random atomic per op (k_sbv_apply); same bits, the ops of one value commute
+        const unsigned rb = sk::sbv_region_bits(), eb = 64u - unsigned(__builtin_clzll(mx | 1));
+        const uint64_t nr = (mx >> rb) + 1; // regions up to the highest op; >= 256 of them to fill the GPU
+        if (n >= c->sbv_min && n < (uint64_t(1) << 32) && n * 64 >= need && nr >= 256) {
+            const uint64_t *keys = d_offsets;
+            HIPCHK(c, c->vals_a.ensure((nr + 1) * 4));
+            Prof p_(c, 9);
+            if (eb > rb) { // more than one region: group the ops by region
+                size_t tmp;
+                HIPCHK(c, sk::sort_keys_size(n, rb, eb, &tmp));
+                HIPCHK(c, c->sort_tmp.ensure(tmp));
+                HIPCHK(c, c->keys_b.ensure(n * 8));
+                HIPCHK(c, sk::sort_keys(c->st, c->sort_tmp.p, c->sort_tmp.cap, d_offsets, c->keys_b.as<uint64_t>(), n,
+                                        rb, eb));
+                keys = c->keys_b.as<uint64_t>();
+            }
+            HIPCHK(c, sk::launch_setbit_void_regions(c->st, n, keys, mx, c->vals_a.as<uint32_t>(), c->strs[id].ptr,
+                                                     c->strs[id].cap, value & 1));
+        } else {
+            Prof p_(c, 9);
+            HIPCHK(c, sk::launch_setbit_void(c->st, n, d_offsets, c->strs[id].ptr, value & 1));
+        }
         return sync(c);
     }
     size_t tmp;

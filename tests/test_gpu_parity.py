@@ -258,6 +258,29 @@ def test_bulk_setbit_getbit_dev(engine):
     assert o[:100].all() and not o[100:200].any()
 
 
+def test_dense_setbit_void_regions(engine):
+    """A dense SETBIT_VOID batch (>= 2 ops per 128-B line, >= 256 regions of 32 KiB: the region path, k_sbv_apply)
+    sets and then clears exactly the bits the per-op atomics would: repeated offsets, the first and last bit of the
+    string, a last region cut short by the string's length, and a clear batch over a set string."""
+    rng = np.random.default_rng(8)
+    nbits = (1 << 27) - 12345                     # 16 MiB string: 512 regions, the last one partial
+    offs = rng.integers(0, nbits, 3 << 20).astype(np.uint64)
+    offs[:3] = [0, nbits - 1, 0]
+    offs[3:1000] = offs[1000:1997]                # repeats
+    engine.setbit_dev(b"dense", len(offs), engine.to_device(offs), 1)
+    want = np.zeros((nbits + 7) // 8, dtype=np.uint8)
+    np.bitwise_or.at(want, (offs >> np.uint64(3)).astype(np.int64),
+                     (np.uint8(1) << (np.uint8(7) - (offs & np.uint64(7)).astype(np.uint8))).astype(np.uint8))
+    assert engine.strlen(b"dense") == len(want)
+    assert np.array_equal(np.frombuffer(engine.get(b"dense"), np.uint8), want)
+    clr = np.concatenate([offs[: 1 << 20], rng.integers(0, nbits, 1 << 20).astype(np.uint64)])
+    engine.setbit_dev(b"dense", len(clr), engine.to_device(clr), 0)
+    np.bitwise_and.at(want, (clr >> np.uint64(3)).astype(np.int64),
+                      (~(np.uint8(1) << (np.uint8(7) - (clr & np.uint64(7)).astype(np.uint8)))).astype(np.uint8))
+    assert np.array_equal(np.frombuffer(engine.get(b"dense"), np.uint8), want)
+    assert engine.bitcount(b"dense") == int(np.bitwise_count(want).sum(dtype=np.uint64))
+
+
 def test_async_pfadd_and_read_stream(engine, O):
     """Async mode: PFADD batches (one overflowing the in-LDS conflict replay)
     interleaved with Bloom contains on the read stream and Bloom adds; the

@@ -3093,10 +3093,38 @@ __global__ void __launch_bounds__(256) k_bit_range(uint8_t *buf, uint64_t from, 
 }
 
 // max of a u64 array (offset validation / capacity sizing)
+// 16-B loads, SK_MX_UNROLL in flight per lane (one element by itself when v is not 16-B aligned, and an odd last one)
+#define SK_MX_UNROLL 4
 __global__ void __launch_bounds__(256) k_max_u64(uint64_t n, const uint64_t *__restrict__ v, uint64_t *out) {
+    constexpr uint32_t U = SK_MX_UNROLL;
     uint64_t m = 0;
-    for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += uint64_t(gridDim.x) * blockDim.x)
-        m = v[i] > m ? v[i] : m;
+    const uint64_t lead = (reinterpret_cast<uintptr_t>(v) & 15u) && n ? 1u : 0u;
+    const uint64_t nv = (n - lead) / 2; // 16-B pairs after the lead element
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        if (lead) m = v[0];
+        if ((n - lead) & 1u) m = v[n - 1] > m ? v[n - 1] : m;
+    }
+    const ulonglong2 *w = reinterpret_cast<const ulonglong2 *>(v + lead);
+    const uint64_t step = uint64_t(gridDim.x) * (256 * U);
+    uint64_t i = uint64_t(blockIdx.x) * (256 * U) + threadIdx.x;
+    for (; i + 256 * (U - 1) < nv; i += step) {
+        ulonglong2 x[U];
+#pragma unroll
+        for (uint32_t u = 0; u < U; u++) x[u] = w[i + 256 * u];
+#pragma unroll
+        for (uint32_t u = 0; u < U; u++) {
+            const uint64_t a = x[u].x > x[u].y ? x[u].x : x[u].y;
+            m = a > m ? a : m;
+        }
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < U; u++) { // this lane's part of the last, partial chunk (later chunks start past nv)
+        const uint64_t t = i + 256 * u;
+        if (t < nv) {
+            const uint64_t a = w[t].x > w[t].y ? w[t].x : w[t].y;
+            m = a > m ? a : m;
+        }
+    }
     for (int s = 32; s > 0; s >>= 1) {
         uint64_t o = __shfl_xor(m, s);
         m = o > m ? o : m;
@@ -3902,7 +3930,7 @@ hipError_t launch_bit_range(hipStream_t st, uint8_t *buf, uint64_t from, uint64_
 hipError_t launch_max_u64(hipStream_t st, uint64_t n, const uint64_t *v, uint64_t *out) {
     hipError_t e = hipMemsetAsync(out, 0, sizeof(uint64_t), st);
     if (e != hipSuccess || !n) return e;
-    hipLaunchKernelGGL(k_max_u64, dim3(grid_for(n, 256, 1024)), dim3(256), 0, st, n, v, out);
+    hipLaunchKernelGGL(k_max_u64, dim3(grid_for((n + 1) / 2, 256 * SK_MX_UNROLL, 2048)), dim3(256), 0, st, n, v, out);
     SK_LAUNCH_CHECK();
     return hipSuccess;
 }

@@ -258,6 +258,23 @@ def test_bulk_setbit_getbit_dev(engine):
     assert o[:100].all() and not o[100:200].any()
 
 
+def test_setbit_dev_max_offset_any_alignment(engine):
+    """The batch's max offset (string growth, range check) is found with 16-B loads: at every start alignment and
+    odd / even counts the string grows to exactly the highest op's byte."""
+    rng = np.random.default_rng(12)
+    for n in (1, 2, 3, 64, 1001, 100000):
+        offs = rng.integers(0, 1 << 20, n + 1).astype(np.uint64)
+        for lead in (0, 1):
+            hi = int(rng.integers(1 << 21, 1 << 22))
+            o = offs.copy()
+            o[lead + int(rng.integers(0, n))] = hi          # the max somewhere in the n ops
+            d = engine.to_device(o)
+            key = b"mx:%d:%d" % (n, lead)
+            engine.setbit_dev(key, n, d.ptr + 8 * lead, 1)
+            assert engine.strlen(key) == hi // 8 + 1, (n, lead)
+            d.free()
+
+
 def test_dense_setbit_void_regions(engine):
     """A dense SETBIT_VOID batch (>= 2 ops per 128-B line, >= 256 regions of 32 KiB: the region path, k_sbv_apply)
     sets and then clears exactly the bits the per-op atomics would: repeated offsets, the first and last bit of the

@@ -43,6 +43,13 @@ BLOOM_KERNELS = ["bloom_rc_hash", "bloom_rc_probe"]
 PHASE_KERNELS = {"bloom_rc_hash": "k_bloom_rc_hash + k_rc_stranspose", "bloom_rc_probe": "k_bloom_rc_probe + k_bloom_rc_zero",
                  "pfl_part": "k_pfl_tot + k_pfl_region", "pfl_apply": "k_pfl_fill + k_pfl_plan + k_pfl_apply"}
 CHAINS = ["pfadd", "bloom_contains"]
+# rocprof names of the kernels each phase launches (PMC / SQ summaries)
+PMC_KERNELS = {"bloom_contains": "sk::k_bloom_contains", "pfadd_claim": "sk::k_pfadd_claim",
+               "pfadd_commit": "sk::k_pfadd_commit", "pfp_hash": "sk::k_pfp_hash", "pfp_apply": "sk::k_pfp_apply",
+               "pfp_reply": "sk::k_pfp_reply", "bloom_rc_hash": "sk::k_bloom_rc_hash<false>+sk::k_rc_stranspose",
+               "pfl_hash": "sk::k_pfl_hash",
+               "pfl_apply": "sk::k_pfl_fill+sk::k_pfl_plan+sk::k_pfl_apply", "pfl_part": "sk::k_pfl_tot+sk::k_pfl_region",
+               "bloom_rc_probe": "sk::k_bloom_rc_probe+sk::k_bloom_rc_zero"}
 PHASES = HLL_KERNELS + ["pfadd_sort"] + BLOOM_KERNELS + CHAINS
 
 
@@ -271,11 +278,20 @@ def main():
     piece = min(CB, 32 << 20)                         # contains pieces of <= 32 M elements (sk_store.cpp)
     own = {"pfadd": mean_len_h + 8 + 4 + 1 + 4 * 8 + 2 * 128 * touched / (G * B),
            "bloom_contains": mean_len_b + 8 + 1 + 2 * 4 * (k - 1) + 2 * 4.0 * nr / 4096 + (size / 8.0) / piece}
-    achieved = s8[dom] * upl[dom] / (avg_ms * 1e-3) / 1e9
     # PMC bytes per dispatch x dispatches of each kernel per launch of the chain (a 64 M contains call is two
     # 32 M pieces)
     tr_parts = [(pmc_traffic(p_), iso[p_][0] / iso[dom][0]) for p_ in chain_kernels[dom] if p_ in iso]
     traffic = sum(t * f for t, f in tr_parts) if tr_parts and all(t is not None for t, _ in tr_parts) else None
+    # The headline roofline is the bytes the chain's kernels actually move (rocprofv3 FETCH/WRITE counters of this
+    # build, per launch) over the chain's launch time measured here.  SURVEY 8(d) charges one random 64-B sector
+    # per Bloom probe, which the region schedule never pays (probes are sorted into LDS-resident regions), so its
+    # bytes over the same time are an "effective" bandwidth that can exceed the HBM peak; it is reported beside it.
+    eff_gbs = s8[dom] * upl[dom] / (avg_ms * 1e-3) / 1e9
+    if traffic:
+        achieved, a_src = traffic / (avg_ms * 1e-3) / 1e9, "pmc"
+    else:   # no counter summary for this build: the schedule's own minimum bytes
+        achieved, a_src = own[dom] * upl[dom] / (avg_ms * 1e-3) / 1e9, "schedule_min"
+    valu = sq_valu(dom_chain_kernel(dom, iso, chain_kernels))
 
     kernels = {}
     for p_, (lps, ms) in iso.items():
@@ -344,10 +360,13 @@ def main():
                                                                  for p_ in chain_kernels[dom])),
                      "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "traffic_GBps": traffic / (avg_ms * 1e-3) / 1e9 if traffic else None,
+                     "achieved_source": a_src,
                      "traffic_source": "newest profiles/*_pmc_summary.json: 2 x FETCH_SIZE (gfx950) + WRITE_SIZE per "
                                        "dispatch, times dispatches per chain launch, summed over the chain's kernels",
-                     "bytes_per_unit": s8[dom], "bytes_per_unit_source": "SURVEY 8(d)",
+                     "traffic_bytes_per_unit": traffic / upl[dom] if traffic else None,
+                     "effective_GBps": eff_gbs, "effective_frac_s8d": eff_gbs / HBM_PEAK_GBS,
+                     "effective_bytes_per_unit": s8[dom], "effective_bytes_source": "SURVEY 8(d) (one 64-B sector "
+                     "per decisive probe; the region schedule does not pay it, so this can exceed the peak)",
                      "schedule_min_bytes_per_unit": own[dom],
                      "schedule_min_frac": own[dom] * upl[dom] / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                      "units_per_launch": upl[dom], "avg_launch_ms": avg_ms, "launches_timed": n_launch,
@@ -356,11 +375,12 @@ def main():
                      "dominant_kernel": {"kernel": dom_kernel, "line_bytes_per_unit": bpu.get(dom_kernel),
                                          "ms_isolated": iso[dom_kernel][1],
                                          "launches_per_step": iso[dom_kernel][0]},
-                     "note": "unit = the chain with the most device time per step, run alone; avg_launch_ms = "
-                             "HIP events around each launch of the chain on its stream inside the timed region "
-                             "(PFADD: the per-batch period, hash of batch i+1 overlapping apply of batch i); "
-                             "kernel times alone and overlapped from the breakdown passes; line-level bytes per "
-                             "kernel: DESIGN.md kernel table"},
+                     "valu_frac": valu,
+                     "note": "frac = PMC bytes of the chain per launch / avg_launch_ms / 8 TB/s.  avg_launch_ms = HIP "
+                             "events around each launch of the chain on its stream inside the timed region (PFADD: "
+                             "the per-batch period); valu_frac = SQ_ACTIVE_INST_VALU / (SIMDs x dispatch cycles) of "
+                             "the chain's longest kernel from the newest profiles/*_sq_summary.json (that kernel is "
+                             "VALU-bound, not HBM-bound); line-level bytes per kernel: DESIGN.md kernel table"},
         "kernels": kernels,
         "chains": chains,
         "cpu_baseline": cpu,
@@ -398,29 +418,52 @@ def per_unit_bytes(mean_len_h, mean_len_b, k, size, CB, nr, tenants, group):
     }
 
 
+def _summary_find(ks, k_):
+    """a kernel's entry in a summary; template kernels may carry more arguments in newer builds"""
+    if k_ in ks:
+        return ks[k_]
+    stem = k_[:-1] + "," if k_.endswith(">") else k_ + "<"   # or a kernel that became a template
+    hit = [v for n_, v in ks.items() if stem and n_.startswith(stem)]
+    return hit[0] if len(hit) == 1 else None
+
+
+def dom_chain_kernel(dom, iso, chain_kernels):
+    """the phase of the chain with the most device time per chain launch"""
+    ps = [p_ for p_ in chain_kernels[dom] if p_ in iso]
+    return max(ps, key=lambda p_: iso[p_][0] * iso[p_][1]) if ps else None
+
+
+def sq_valu(phase):
+    """VALU busy fraction of the phase's first kernel from the newest committed SQ summary (or None)"""
+    import glob
+
+    if not phase or phase not in PMC_KERNELS:
+        return None
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_sq_summary.json")))
+    if not files:
+        return None
+    try:
+        d = _summary_find(json.load(open(files[-1]))["kernels"], PMC_KERNELS[phase].split("+")[0])
+        return {"kernel": PMC_KERNELS[phase].split("+")[0], "valu_frac": d["valu_util"],
+                "lds_conflict_share": d.get("lds_conflict_share"),
+                "valu_insts_per_dispatch": d["counters"]["SQ_INSTS_VALU"],
+                "source": os.path.relpath(files[-1], ROOT)} if d else None
+    except (OSError, ValueError, KeyError):
+        return None
+
+
 def pmc_traffic(phase):
     """HBM bytes per launch of the phase's kernel from the newest committed PMC summary (or None)."""
     import glob
 
-    kern = {"bloom_contains": "sk::k_bloom_contains", "pfadd_claim": "sk::k_pfadd_claim",
-            "pfadd_commit": "sk::k_pfadd_commit", "pfp_hash": "sk::k_pfp_hash", "pfp_apply": "sk::k_pfp_apply",
-            "pfp_reply": "sk::k_pfp_reply", "bloom_rc_hash": "sk::k_bloom_rc_hash<false>+sk::k_rc_stranspose",
-            "pfl_hash": "sk::k_pfl_hash",
-            "pfl_apply": "sk::k_pfl_fill+sk::k_pfl_plan+sk::k_pfl_apply", "pfl_part": "sk::k_pfl_tot+sk::k_pfl_region",
-            "bloom_rc_probe": "sk::k_bloom_rc_probe+sk::k_bloom_rc_zero"}.get(phase)
+    kern = PMC_KERNELS.get(phase)
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_summary.json")))
     if not kern or not files:
         return None
     try:
         ks = json.load(open(files[-1]))["kernels"]
 
-        def find(k_):   # template kernels may carry more arguments in newer builds (k_bloom_rc_hash<false, 2048u>)
-            if k_ in ks:
-                return ks[k_]
-            stem = k_[:-1] + "," if k_.endswith(">") else k_ + "<"   # or a kernel that became a template
-            hit = [v for n_, v in ks.items() if stem and n_.startswith(stem)]
-            return hit[0] if len(hit) == 1 else None
-        parts = [find(k_) for k_ in kern.split("+")]   # a phase of several launches: their sum
+        parts = [_summary_find(ks, k_) for k_ in kern.split("+")]   # a phase of several launches: their sum
         return sum(d["traffic_bytes_per_launch"] for d in parts) if all(parts) else None
     except (OSError, ValueError, KeyError):
         return None

@@ -220,6 +220,13 @@ def c5(eng, args):
     t_set = t_get = 0.0
     set_dev_ms = 0.0
     d_out = eng.alloc(chunk)
+    # the cold form as well -- a first 64 M-op call on a key that does not exist yet, timed with the
+    # string's creation and growth to full length inside the call (rounds <= 3 timed C5 this way)
+    m0 = min(chunk, n)
+    d_off = eng.to_device(rng.integers(0, bits, m0, dtype=np.uint64))
+    t_cold = timed(eng, lambda: eng.setbit_dev(b"bs5:cold", m0, d_off, 1))
+    d_off.free()
+    eng.delete([b"bs5:cold"])
     eng.setbit([keys[0]], [bits - 1], [1])   # the string created at full length untimed (a 2 GiB allocation)
     for key in keys:
         for s in range(0, n if key == keys[0] else n // 16, chunk):
@@ -256,6 +263,8 @@ def c5(eng, args):
           "config": {"workload": "c5", "bits": bits, "ops": n},
           "setbit_per_s": n / t_set, "getbit_per_s": n / t_get,
           "setbit_device_per_s": n / (set_dev_ms * 1e-3) if set_dev_ms else None,
+          "setbit_cold_first_call_per_s": m0 / t_cold,
+          "setbit_cold": "one %d-op call on a missing key: the 2 GiB string's creation and growth timed inside it" % m0,
           "setbit": "SETBIT_VOID (RBitSet.set(i)) in 64 M-op calls on the full-length string (created untimed); a dense "
                     "call (>= 2 ops per 128-B line) takes the region path (radix sort by 32 KiB region + k_sbv_apply)",
           "bitcount_GBps": nbytes / t_bc / 1e9, "bitop_and4_GBps": 5 * nbytes / t_and / 1e9,

@@ -9,6 +9,9 @@
  *                   :162-166 is kept verbatim (the engine checks size / k as the EVAL of addConfigCheck did)
  *   count        -> sk_bloom_count (:188-199)
  *   delete       -> DEL name {name}__config, both on the engine (:201-203)
+ * Every engine call runs on the coalescer's FIFO completion thread: add / contains as merged runs, and tryInit,
+ * the config read, count, the getters and delete as tasks in their FIFO place (submitTask), so no caller thread
+ * makes a JNI call and a delete never overtakes a queued add / contains (tests/test_coalesce.py, Python twin).
  * It lives in org.redisson next to RedissonBloomFilter (RedissonExpirable's constructors are package-private);
  * Redisson.getBloomFilter returns it when the engine is configured (INTEGRATION.md).  Source only here.
  */
@@ -87,13 +90,11 @@ public class GpuBloomFilter<T> extends RedissonExpirable implements RBloomFilter
         }
     }
 
-    /** Non-blocking form for event-loop callers: completes from the coalescer's thread. */
+    /** Non-blocking form for event-loop callers: completes from the coalescer's thread.  With no config read yet
+     *  the request carries size 0 and the coalescer reads the config in FIFO order (never on the caller's thread). */
     public Future<boolean[]> containsAllAsync(byte[][] encoded) {
-        if (size == 0) {
-            readConfig();
-        }
         Promise<boolean[]> p = executor.getConnectionManager().newPromise();
-        coalescer.submit(nameBytes(), false, size, hashIterations, encoded, p);
+        coalescer.submit(nameBytes(), false, size, size == 0 ? 0 : hashIterations, encoded, p);
         return p;
     }
 
@@ -107,72 +108,120 @@ public class GpuBloomFilter<T> extends RedissonExpirable implements RBloomFilter
         return call(false, object);
     }
 
-    @Override
-    public boolean tryInit(long expectedInsertions, double falseProbability) {
-        int[] ok = new int[1];
-        SketchDispatch.check(ctx, SketchNative.bloomTryInit(ctx, nameBytes(), expectedInsertions, falseProbability,
-                ok));
-        readConfig();
-        return ok[0] == 1;
+    /** Every other engine call of the filter goes through the coalescer's FIFO thread too (VERDICT r4 item 8):
+     *  it runs after every add / contains queued before it, and no caller thread makes a JNI call. */
+    private <R> Future<R> onWorker(GpuBloomCoalescer.Task<R> task) {
+        Promise<R> p = executor.getConnectionManager().newPromise();
+        coalescer.submitTask(task, p);
+        return p;
     }
 
-    private long[] config(int[] k, double[] fpp) {
-        long[] sizeExpected = new long[2];
-        SketchDispatch.check(ctx, SketchNative.bloomConfig(ctx, nameBytes(), sizeExpected, k, fpp));
-        return sizeExpected;
+    /** The sync API's blocking wait (RedissonObject.get): user threads only, as in the reference. */
+    private <R> R await(Future<R> f) {
+        try {
+            return f.get();
+        } catch (ExecutionException e) {
+            Throwable c = e.getCause();
+            if (c instanceof RuntimeException) {
+                throw (RuntimeException) c;
+            }
+            throw new RedisException(c.getMessage(), c);
+        } catch (InterruptedException e) {
+            Thread.currentThread().interrupt();
+            throw new RedisException("interrupted", e);
+        }
+    }
+
+    @Override
+    public boolean tryInit(final long expectedInsertions, final double falseProbability) {
+        final byte[] name = nameBytes();
+        boolean ok = await(onWorker(new GpuBloomCoalescer.Task<Boolean>() {
+            public Boolean call(long c) {
+                int[] out = new int[1];
+                SketchDispatch.check(c, SketchNative.bloomTryInit(c, name, expectedInsertions, falseProbability, out));
+                return out[0] == 1;
+            }
+        }));
+        readConfig();
+        return ok;
+    }
+
+    /** {size, expectedInsertions} with k and fpp, read on the worker. */
+    private static final class Cfg {
+        long size;
+        long expected;
+        int k;
+        double fpp;
+    }
+
+    private Cfg config() {
+        final byte[] name = nameBytes();
+        return await(onWorker(new GpuBloomCoalescer.Task<Cfg>() {
+            public Cfg call(long c) {
+                long[] se = new long[2];
+                int[] k = new int[1];
+                double[] fpp = new double[1];
+                SketchDispatch.check(c, SketchNative.bloomConfig(c, name, se, k, fpp));
+                Cfg r = new Cfg();
+                r.size = se[0];
+                r.expected = se[1];
+                r.k = k[0];
+                r.fpp = fpp[0];
+                return r;
+            }
+        }));
     }
 
     private void readConfig() {
-        int[] k = new int[1];
-        long[] se = config(k, new double[1]);
-        size = se[0];
-        hashIterations = k[0];
+        Cfg c = config();
+        size = c.size;
+        hashIterations = c.k;
     }
 
     @Override
     public long getExpectedInsertions() {
-        return config(new int[1], new double[1])[1];
+        return config().expected;
     }
 
     @Override
     public double getFalseProbability() {
-        double[] fpp = new double[1];
-        config(new int[1], fpp);
-        return fpp[0];
+        return config().fpp;
     }
 
     @Override
     public long getSize() {
-        return config(new int[1], new double[1])[0];
+        return config().size;
     }
 
     @Override
     public int getHashIterations() {
-        int[] k = new int[1];
-        config(k, new double[1]);
-        return k[0];
+        return config().k;
     }
 
     @Override
     public int count() {
-        int[] out = new int[1];
-        SketchDispatch.check(ctx, SketchNative.bloomCount(ctx, nameBytes(), out));
-        return out[0];
+        final byte[] name = nameBytes();
+        return await(onWorker(new GpuBloomCoalescer.Task<Integer>() {
+            public Integer call(long c) {
+                int[] out = new int[1];
+                SketchDispatch.check(c, SketchNative.bloomCount(c, name, out));
+                return out[0];
+            }
+        }));
     }
 
+    /** DEL name {name}__config (:201-203), completed by the coalescer's thread after every request queued before it
+     *  (a delete issued after a containsAllAsync on the same thread never overtakes it). */
     @Override
     public Future<Boolean> deleteAsync() {
-        java.util.List<byte[]> keys = java.util.Arrays.asList(nameBytes(),
-                ("{" + getName() + "}__config").getBytes(UTF8));
-        SketchDispatch.Packed k = new SketchDispatch.Packed(keys);
-        long[] removed = new long[1];
-        int st = SketchNative.del(ctx, k.off, k.bytes, removed);
-        Promise<Boolean> p = executor.getConnectionManager().newPromise();
-        if (st != SketchNative.SK_OK) {
-            p.setFailure(new RedisException(SketchNative.lastError(ctx)));
-        } else {
-            p.setSuccess(removed[0] > 0);
-        }
-        return p;
+        final SketchDispatch.Packed k = new SketchDispatch.Packed(java.util.Arrays.asList(nameBytes(),
+                ("{" + getName() + "}__config").getBytes(UTF8)));
+        return onWorker(new GpuBloomCoalescer.Task<Boolean>() {
+            public Boolean call(long c) {
+                long[] removed = new long[1];
+                SketchDispatch.check(c, SketchNative.del(c, k.off, k.bytes, removed));
+                return removed[0] > 0;
+            }
+        });
     }
 }

@@ -26,6 +26,11 @@ import io.netty.util.concurrent.Promise;
 
 public final class GpuBloomCoalescer implements Runnable {
 
+    /** Any other engine call of a filter (tryInit, the config read, count, delete), run in its FIFO place. */
+    public interface Task<T> {
+        T call(long ctx);
+    }
+
     static final class Req {
         final byte[] name;
         final boolean add;
@@ -33,6 +38,8 @@ public final class GpuBloomCoalescer implements Runnable {
         final int k;
         final byte[][] elems;
         final Promise<boolean[]> promise;
+        final Task<Object> task;
+        final Promise<Object> taskPromise;
 
         Req(byte[] name, boolean add, long size, int k, byte[][] elems, Promise<boolean[]> promise) {
             this.name = name;
@@ -41,10 +48,25 @@ public final class GpuBloomCoalescer implements Runnable {
             this.k = k;
             this.elems = elems;
             this.promise = promise;
+            this.task = null;
+            this.taskPromise = null;
+        }
+
+        Req(Task<Object> task, Promise<Object> taskPromise) {
+            this.name = null;
+            this.add = false;
+            this.size = 0;
+            this.k = 0;
+            this.elems = new byte[0][];
+            this.promise = null;
+            this.task = task;
+            this.taskPromise = taskPromise;
         }
 
         boolean sameRun(Req o) {
-            return add == o.add && size == o.size && k == o.k && Arrays.equals(name, o.name);
+            // a task is a run of its own: it never merges, and nothing merges across it
+            return task == null && o.task == null && add == o.add && size == o.size && k == o.k
+                    && Arrays.equals(name, o.name);
         }
     }
 
@@ -65,14 +87,27 @@ public final class GpuBloomCoalescer implements Runnable {
         GpuSketch.track(ctx, this); // closed by GpuSketch.close(ctx) before the context itself
     }
 
-    /** Enqueue; never blocks on the device.  The promise gets one reply per element. */
+    /** Enqueue; never blocks on the device.  The promise gets one reply per element.  size = 0: the filter's
+     *  config is read on the completion thread right before the engine call (the non-blocking callers' form). */
     public void submit(byte[] name, boolean add, long size, int k, byte[][] elems, Promise<boolean[]> promise) {
+        enqueue(new Req(name, add, size, k, elems, promise), promise);
+    }
+
+    /** Enqueue any other engine call of a filter: it runs on the completion thread after every request queued
+     *  before it, so it neither blocks the caller's (event-loop) thread on the device nor overtakes a queued
+     *  add / contains.  The promise completes from that thread. */
+    @SuppressWarnings("unchecked")
+    public <T> void submitTask(Task<T> task, Promise<T> promise) {
+        enqueue(new Req((Task<Object>) (Task<?>) task, (Promise<Object>) (Promise<?>) promise), promise);
+    }
+
+    private void enqueue(Req r, Promise<?> promise) {
         synchronized (queue) {
             if (stop) {
                 promise.tryFailure(new IllegalStateException("coalescer closed"));
                 return;
             }
-            queue.addLast(new Req(name, add, size, k, elems, promise));
+            queue.addLast(r);
             queue.notify();
         }
     }
@@ -117,6 +152,36 @@ public final class GpuBloomCoalescer implements Runnable {
 
     private void execute(List<Req> run) {
         Req head = run.get(0);
+        if (head.task != null) {
+            try {
+                head.taskPromise.trySuccess(head.task.call(ctx));
+            } catch (RuntimeException e) {
+                head.taskPromise.tryFailure(e);
+            }
+            calls++;
+            requests++;
+            return;
+        }
+        long size = head.size;
+        int k = head.k;
+        if (size == 0) { // config read here, in FIFO order
+            long[] se = new long[2];
+            int[] kk = new int[1];
+            int cs = SketchNative.bloomConfig(ctx, head.name, se, kk, new double[1]);
+            if (cs != SketchNative.SK_OK) {
+                RuntimeException ex = cs == SketchNative.SK_ENOTINIT
+                        ? new IllegalStateException(SketchNative.lastError(ctx))
+                        : new RedisException(SketchNative.lastError(ctx));
+                for (Req r : run) {
+                    r.promise.tryFailure(ex);
+                }
+                calls++;
+                requests += run.size();
+                return;
+            }
+            size = se[0];
+            k = kk[0];
+        }
         List<byte[]> all = new ArrayList<byte[]>();
         for (Req r : run) {
             all.addAll(Arrays.asList(r.elems));
@@ -126,14 +191,12 @@ public final class GpuBloomCoalescer implements Runnable {
         SketchDispatch.PrefixPacked pp = SketchDispatch.PrefixPacked.of(all, 8);
         int st;
         if (pp != null) {
-            st = head.add ? SketchNative.bloomAddPrefix(ctx, head.name, head.size, head.k, pp.prefix, pp.off,
-                                                        pp.suffixes, out)
-                    : SketchNative.bloomContainsPrefix(ctx, head.name, head.size, head.k, pp.prefix, pp.off,
-                                                       pp.suffixes, out);
+            st = head.add ? SketchNative.bloomAddPrefix(ctx, head.name, size, k, pp.prefix, pp.off, pp.suffixes, out)
+                    : SketchNative.bloomContainsPrefix(ctx, head.name, size, k, pp.prefix, pp.off, pp.suffixes, out);
         } else {
             SketchDispatch.Packed e = new SketchDispatch.Packed(all);
-            st = head.add ? SketchNative.bloomAdd(ctx, head.name, head.size, head.k, e.off, e.bytes, out)
-                    : SketchNative.bloomContains(ctx, head.name, head.size, head.k, e.off, e.bytes, out);
+            st = head.add ? SketchNative.bloomAdd(ctx, head.name, size, k, e.off, e.bytes, out)
+                    : SketchNative.bloomContains(ctx, head.name, size, k, e.off, e.bytes, out);
         }
         if (st != SketchNative.SK_OK) {
             RuntimeException ex = st == SketchNative.SK_ENOTINIT ? new IllegalStateException(SketchNative.lastError(ctx))

@@ -695,7 +695,19 @@ class RangeShardedBloom:
                                            % (2 * 2147483647, m))
         fresh = self.bits is None
         self.size, self.k = int(m), int(bloom_optimal_k(expected, m))
-        self.bits = ShardedBitSet(self.engine, self.name, self.size, self.rank, self.world, self.coll)
+        if fresh:
+            self.bits = ShardedBitSet(self.engine, self.name, self.size, self.rank, self.world, self.coll)
+        elif self.size > 8 * self.bits.S * self.world:
+            # Q6 keeps the one global bit string and only replaces the config: bit i stays bit i.  The first layout
+            # is kept while it covers the new size; a larger filter gets a wider layout, and the existing bits are
+            # moved to their new owners (every rank holds the logical string after to_bytes, then keeps its part)
+            whole = self.bits.to_bytes()
+            self.bits = ShardedBitSet(self.engine, self.name, self.size, self.rank, self.world, self.coll)
+            mine = whole[self.bits.lo:self.bits.lo + self.bits.S]
+            if mine:
+                self.engine.set(self.name, mine)
+            else:
+                self.engine.delete([self.name])
         return fresh
 
     def _check(self):

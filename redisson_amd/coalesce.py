@@ -51,14 +51,15 @@ class WaitFuture(Future):
 
 
 class _Req:
-    __slots__ = ("name", "kind", "size", "k", "elems", "future")
+    __slots__ = ("name", "kind", "size", "k", "elems", "future", "fn")
 
-    def __init__(self, name, kind, size, k, elems):
-        self.name, self.kind, self.size, self.k, self.elems = name, kind, size, k, elems
+    def __init__(self, name, kind, size, k, elems, fn=None):
+        self.name, self.kind, self.size, self.k, self.elems, self.fn = name, kind, size, k, elems, fn
         self.future = WaitFuture()
 
     def key(self):
-        return (self.name, self.kind, self.size, self.k)
+        # a task is a run of its own: it never merges, and nothing merges across it
+        return (self.name, self.kind, self.size, self.k) if self.fn is None else self
 
 
 class BloomCoalescer:
@@ -79,9 +80,19 @@ class BloomCoalescer:
         self._t.start()
 
     def submit(self, name, kind: str, size: int, k: int, elems: Sequence[bytes]) -> WaitFuture:
+        """An add / contains request.  size = 0: the filter's config is read on the completion thread right before
+        the engine call (the non-blocking callers' form, which must not read it on their own thread)."""
         if kind not in ("add", "contains"):
             raise ValueError(kind)
-        r = _Req(name, kind, int(size), int(k), list(elems))
+        return self._enqueue(_Req(name, kind, int(size), int(k), list(elems)))
+
+    def submit_task(self, fn) -> WaitFuture:
+        """Any other engine call on a filter (tryInit, the config read, count, delete): run by the completion thread
+        in its FIFO place, after every request queued before it, so it neither blocks the caller's thread on the
+        device nor overtakes a queued add / contains."""
+        return self._enqueue(_Req(None, "task", 0, 0, [], fn))
+
+    def _enqueue(self, r: _Req) -> WaitFuture:
         with self._cv:
             if self._stop:
                 raise RuntimeError("coalescer closed")
@@ -129,17 +140,32 @@ class BloomCoalescer:
 
     def _execute(self, run: List[_Req]):
         head = run[0]
+        if head.fn is not None:
+            try:
+                v = head.fn()
+            except Exception as e:  # noqa: BLE001 - the task's caller sees its error
+                head.future._fail(e)
+            else:
+                head.future._set(v)
+            if self.log is not None:
+                self.log.append(("task", [([], head.future)]))
+            self.calls += 1
+            self.requests += 1
+            return
         elems = [e for r in run for e in r.elems]
         fn = self.engine.bloom_add if head.kind == "add" else self.engine.bloom_contains
         try:
             from .engine import common_prefix
 
+            size, k = head.size, head.k
+            if size == 0:   # config read here, in FIFO order (submit's size = 0 form)
+                size, k = self.engine.bloom_config(head.name)[:2]
             plen = common_prefix(elems) if elems else 0
             if plen >= 8:   # a shared codec prefix: prefix form, only the suffixes cross the host link
-                res = self.engine.bloom_prefix(head.kind, head.name, head.size, head.k, bytes(elems[0])[:plen],
+                res = self.engine.bloom_prefix(head.kind, head.name, size, k, bytes(elems[0])[:plen],
                                                [bytes(e)[plen:] for e in elems])
             else:
-                res = fn(head.name, head.size, head.k, elems) if elems else []
+                res = fn(head.name, size, k, elems) if elems else []
         except Exception as e:  # noqa: BLE001 - every request of the run sees the engine's error
             for r in run:
                 r.future._fail(e)

@@ -1498,6 +1498,15 @@ int sk_hll_lookup(sk_ctx *c, uint32_t n, const uint64_t *off, const uint8_t *byt
 // out_changed.  A chunk of valid one-element commands (the RBatch of add)
 // ships the caller's ids, rebased offsets and bytes as they are; otherwise
 // the valid commands' elements are re-packed with a command index each.
+// distinct sketches of a batch: only the density heuristic of the non-default paths (pfadd_uses_sort) uses it, so
+// the default partition path skips the count
+static uint64_t pfadd_touched(const sk_ctx *c, const uint32_t *ids, uint64_t m) {
+    if (c->pfadd_path == 1) return 0;
+    std::vector<uint32_t> uniq(ids, ids + m);
+    std::sort(uniq.begin(), uniq.end());
+    return uint64_t(std::unique(uniq.begin(), uniq.end()) - uniq.begin());
+}
+
 static int pfadd_host_batch(sk_ctx *c, uint32_t n_cmds, const uint32_t *cmd_key, const uint8_t *valid,
                             const uint32_t *elem_counts, const uint64_t *elem_off, const uint8_t *elem_bytes,
                             uint8_t *out_changed) {
@@ -1589,12 +1598,7 @@ static int pfadd_host_batch(sk_ctx *c, uint32_t n_cmds, const uint32_t *cmd_key,
             if ((sr = stage_h2d(c, c->in_bytes.p, bytes_src, nbytes))) return sr;
             HIPCHK(c, hipMemsetAsync(c->in_bytes.as<uint8_t>() + nbytes, 0, 16, c->st)); // padding contract
             HIPCHK(c, hipMemsetAsync(c->out_u8.p, 0, c1 - c0, c->st));
-            uint64_t touched = 0; // distinct sketches: only the density heuristic of the non-default paths uses it
-            if (c->pfadd_path != 1) {
-                std::vector<uint32_t> uniq(ids_src, ids_src + m);
-                std::sort(uniq.begin(), uniq.end());
-                touched = uint64_t(std::unique(uniq.begin(), uniq.end()) - uniq.begin());
-            }
+            const uint64_t touched = pfadd_touched(c, ids_src, m);
             // long elements (addAll's Q1 element: the whole Jackson array) are hashed by one workgroup each
             const uint64_t *d_pre = nullptr;
             if (c->pfadd_path == 1 && nbytes >= sk::long_elem_bytes()) {
@@ -2903,8 +2907,9 @@ int sk_pfadd_ids_prefix(sk_ctx *c, uint32_t n, const uint32_t *key_ids, const ui
         if ((r = stage_h2d(c, c->in_ids.p, key_ids + c0, m * 4ull))) return r;
         if ((r = stage_prefixed(c, m, pre, soff + c0, sbytes))) return r;
         HIPCHK(c, hipMemsetAsync(c->out_u8.p, 0, m, c->st));
+        // the same path choice as sk_pfadd_ids for the same batch
         if ((r = pfadd_device(c, m, c->in_ids.as<uint32_t>(), c->in_off.as<uint64_t>(), c->in_bytes.as<uint8_t>(),
-                              nullptr, m, c->out_u8.as<uint8_t>(), 0)))
+                              nullptr, m, c->out_u8.as<uint8_t>(), pfadd_touched(c, key_ids + c0, m))))
             return r;
         HIPCHK(c, hipMemcpyAsync(out_changed + c0, c->out_u8.p, m, hipMemcpyDeviceToHost, c->st));
         if ((r = sync(c))) return r;
@@ -3076,21 +3081,25 @@ int sk_dev_free(sk_ctx *c, void *p) {
 }
 int sk_h2d(sk_ctx *c, void *dst, const void *src, uint64_t n) {
     std::lock_guard<std::mutex> g(c->mu);
+    ENTER(c); // after outstanding read-stream work (an async contains may still be writing the buffer)
     if (n) HIPCHK(c, hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, c->st));
     return sync(c);
 }
 int sk_d2h(sk_ctx *c, void *dst, const void *src, uint64_t n) {
     std::lock_guard<std::mutex> g(c->mu);
+    ENTER(c); // after outstanding read-stream work (an async contains may still be writing the buffer)
     if (n) HIPCHK(c, hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, c->st));
     return sync(c);
 }
 int sk_d2d(sk_ctx *c, void *dst, const void *src, uint64_t n) {
     std::lock_guard<std::mutex> g(c->mu);
+    ENTER(c); // after outstanding read-stream work (an async contains may still be writing the buffer)
     if (n) HIPCHK(c, hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToDevice, c->st));
     return sync(c);
 }
 int sk_dev_memset(sk_ctx *c, void *p, int v, uint64_t n) {
     std::lock_guard<std::mutex> g(c->mu);
+    ENTER(c); // after outstanding read-stream work (an async contains may still be writing the buffer)
     if (n) HIPCHK(c, hipMemsetAsync(p, v, n, c->st));
     return sync(c);
 }
@@ -3285,6 +3294,7 @@ int sk_alltoallv(sk_ctx *c, const void *d_send, const uint64_t *send_bytes, void
 // cross-GPU PFMERGE / countWith: register-wise max of 16384-byte arrays
 int sk_allreduce_max_u8(sk_ctx *c, uint8_t *d_buf, uint64_t n) {
     std::lock_guard<std::mutex> g(c->mu);
+    ENTER(c); // after outstanding read-stream work (an async contains may still be writing the buffer)
     if (!c->comm) return fail(c, SK_EINVAL, "sk_comm_init first");
     NCCLCHK(c, ncclAllReduce(d_buf, d_buf, n, ncclUint8, ncclMax, c->comm, c->st));
     return sync(c);
@@ -3292,6 +3302,7 @@ int sk_allreduce_max_u8(sk_ctx *c, uint8_t *d_buf, uint64_t n) {
 // BITCOUNT of a range-sharded bitset
 int sk_allreduce_sum_u64(sk_ctx *c, uint64_t *d_buf, uint64_t n) {
     std::lock_guard<std::mutex> g(c->mu);
+    ENTER(c); // after outstanding read-stream work (an async contains may still be writing the buffer)
     if (!c->comm) return fail(c, SK_EINVAL, "sk_comm_init first");
     NCCLCHK(c, ncclAllReduce(d_buf, d_buf, n, ncclUint64, ncclSum, c->comm, c->st));
     return sync(c);
@@ -3299,6 +3310,7 @@ int sk_allreduce_sum_u64(sk_ctx *c, uint64_t *d_buf, uint64_t n) {
 // key-sharded BITOP: gather the remote operands, then a local op
 int sk_allgather(sk_ctx *c, const void *d_send, void *d_recv, uint64_t bytes_per_rank) {
     std::lock_guard<std::mutex> g(c->mu);
+    ENTER(c); // after outstanding read-stream work (an async contains may still be writing the buffer)
     if (!c->comm) return fail(c, SK_EINVAL, "sk_comm_init first");
     NCCLCHK(c, ncclAllGather(d_send, d_recv, bytes_per_rank, ncclUint8, c->comm, c->st));
     return sync(c);

@@ -304,18 +304,27 @@ class RBloomFilter(RObject):
         self._size = 0
         self._k = 0
 
+    def _co(self):
+        return getattr(self._c, "bloom_coalescer", None)
+
+    def _call(self, fn):
+        """Every engine call of the filter: with group commit on, it runs on the coalescer's completion thread in
+        FIFO order with the queued add / contains requests, never on the caller's thread."""
+        co = self._co()
+        return co.submit_task(fn).get() if co is not None else fn()
+
     def _read_config(self):
-        size, k, _, _ = self._e.bloom_config(self._name)   # IllegalStateException if absent
+        size, k, _, _ = self._call(lambda: self._e.bloom_config(self._name))   # IllegalStateException if absent
         self._size, self._k = size, k
 
     def tryInit(self, expectedInsertions: int, falseProbability: float) -> bool:
-        ok = self._e.bloom_try_init(self._name, int(expectedInsertions), float(falseProbability))
+        ok = self._call(lambda: self._e.bloom_try_init(self._name, int(expectedInsertions), float(falseProbability)))
         self._read_config()
         return ok
 
     def _run(self, fn, objs):
         elems = [self.codec.encode(o) for o in objs]
-        co = getattr(self._c, "bloom_coalescer", None)
+        co = self._co()
         while True:
             if self._size == 0:
                 self._read_config()
@@ -342,25 +351,47 @@ class RBloomFilter(RObject):
     def containsAll(self, objs) -> List[bool]:
         return self._run(self._e.bloom_contains, list(objs))
 
+    def _async(self, kind, objs) -> Future:
+        """Non-blocking form (the Java twin's containsAllAsync, for event-loop callers): with group commit on, the
+        request carries no config and the completion thread reads it in FIFO order; the future completes from
+        that thread."""
+        elems = [self.codec.encode(o) for o in objs]
+        co = self._co()
+        if co is None:
+            return _completed(lambda: self._run(self._e.bloom_add if kind == "add" else self._e.bloom_contains, objs))
+        return co.submit(self._name, kind, 0, 0, elems)
+
+    def addAllAsync(self, objs) -> Future:
+        return self._async("add", list(objs))
+
+    def containsAllAsync(self, objs) -> Future:
+        return self._async("contains", list(objs))
+
     def count(self) -> int:
-        return self._e.bloom_count(self._name)
+        return self._call(lambda: self._e.bloom_count(self._name))
+
+    def _cfg(self, i):
+        return self._call(lambda: self._e.bloom_config(self._name))[i]
 
     def getExpectedInsertions(self) -> int:
-        return self._e.bloom_config(self._name)[2]
+        return self._cfg(2)
 
     def getFalseProbability(self) -> float:
-        return self._e.bloom_config(self._name)[3]
+        return self._cfg(3)
 
     def getSize(self) -> int:
-        return self._e.bloom_config(self._name)[0]
+        return self._cfg(0)
 
     def getHashIterations(self) -> int:
-        return self._e.bloom_config(self._name)[1]
+        return self._cfg(1)
 
     def deleteAsync(self) -> Future:
-        # DEL name {name}__config (:201-203)
+        # DEL name {name}__config (:201-203); with group commit on, completed by the coalescer's thread after every
+        # request queued before it
         cfg = "{" + self._name + "}__config"
-        return _completed(lambda: self._e.delete([self._name, cfg]) > 0)
+        fn = lambda: self._e.delete([self._name, cfg]) > 0   # noqa: E731
+        co = self._co()
+        return co.submit_task(fn) if co is not None else _completed(fn)
 
 
 # ------------------------------------------------------------------ batch

@@ -561,6 +561,14 @@ def run_bloom_shard(engine, rank, world, coll):
     out["empty"] = rb.contains([])                            # an empty batch on every rank
     out["bytes"] = rb.to_bytes()
     out["count"] = rb.count()
+    # Q6: a re-init replaces the config and keeps the one global bit string -- bit i stays bit i, both
+    # when the first shard layout still covers the new size and when a larger filter needs a wider layout
+    out["reinit_small"] = rb.try_init(2000, 0.01)
+    out["bytes_small"] = rb.to_bytes()
+    out["reinit_big"] = rb.try_init(200000, 0.01)
+    out["bytes_big"] = rb.to_bytes()
+    out["cfg_big"] = (rb.size, rb.k)
+    out["contains_big"] = gathered(rb.contains(mine(BLOOM_PROBE)))
     rp = ReplicatedBloom(engine, b"rpb:c3", rank, world, coll)
     rp.try_init(20000, 0.01)
     rp.add(BLOOM_ADDS[:1500])
@@ -586,6 +594,11 @@ def expected_bloom_shard():
     out["empty"] = []
     out["bytes"] = b.bytes()
     out["count"] = O.bloom_count(m, k, b.bitcount())
+    out["reinit_small"], out["bytes_small"] = False, b.bytes()
+    m2 = O.bloom_optimal_bits(200000, 0.01)
+    k2 = O.bloom_optimal_k(200000, m2)
+    out["reinit_big"], out["bytes_big"], out["cfg_big"] = False, b.bytes(), (m2, k2)
+    out["contains_big"] = [bool(x) for x in b.bloom_contains(m2, k2, BLOOM_PROBE)]
     r = O.BitString(16)
     r.bloom_add(m, k, BLOOM_ADDS[:1500])
     out["rep_contains_dev"] = [bool(x) for x in r.bloom_contains(m, k, BLOOM_PROBE)]

@@ -190,3 +190,92 @@ def test_rbloomfilter_coalesced_on_engine(O):
         assert r.engine.get("cbf") == ref.bytes()
     finally:
         r.shutdown()
+
+
+class _CfgBloomEngine(OracleBloomEngine):
+    """OracleBloomEngine plus the filter's other engine calls (tryInit / config / count / DEL), each recording the
+    thread it ran on."""
+
+    def __init__(self):
+        super().__init__()
+        self.threads = []
+
+    def _t(self, what):
+        self.threads.append((what, threading.current_thread().name))
+
+    def bloom_add(self, name, size, k, elems):
+        self._t("add")
+        return super().bloom_add(name, size, k, elems)
+
+    def bloom_contains(self, name, size, k, elems):
+        self._t("contains")
+        return super().bloom_contains(name, size, k, elems)
+
+    def bloom_try_init(self, name, n, p):
+        self._t("tryInit")
+        m = self.O.bloom_optimal_bits(n, p)
+        fresh = name not in self.cfg
+        self.cfg[name] = (m, self.O.bloom_optimal_k(n, m))
+        return fresh
+
+    def bloom_config(self, name):
+        self._t("config")
+        from redisson_amd.engine import IllegalStateException
+
+        if name not in self.cfg:
+            raise IllegalStateException("Bloom filter is not initialized!")
+        m, k = self.cfg[name]
+        return m, k, 0, 0.0
+
+    def bloom_count(self, name):
+        self._t("count")
+        m, k = self.cfg[name]
+        b = self.bits.get(name)
+        return self.O.bloom_count(m, k, b.bitcount() if b else 0)
+
+    def delete(self, keys):
+        self._t("delete")
+        n = 0
+        for key in keys:
+            n += self.bits.pop(key, None) is not None
+            n += self.cfg.pop(key, None) is not None
+        return n
+
+
+class _Client:
+    def __init__(self, eng, co):
+        from redisson_amd.redisson import Config
+
+        self.engine, self.bloom_coalescer, self.config = eng, co, Config()
+
+
+def test_filter_calls_run_on_the_fifo_worker_in_order():
+    """with group commit on, every engine call of RBloomFilter (tryInit, the config read, count,
+    getters, delete) runs on the coalescer's completion thread, and deleteAsync completes from it only after every
+    request queued before it -- a delete issued after a queued containsAllAsync never overtakes it."""
+    from redisson_amd.coalesce import BloomCoalescer
+    from redisson_amd.redisson import RBloomFilter
+
+    eng = _CfgBloomEngine()
+    co = BloomCoalescer(eng)
+    try:
+        bf = RBloomFilter(_Client(eng, co), "bf")
+        assert bf.tryInit(20000, 0.01) and not bf.tryInit(20000, 0.01)
+        elems = [_elem(1, i) for i in range(300)]
+        assert all(bf.addAll(elems))
+        m, k = eng.cfg["bf"]
+        assert (bf.getSize(), bf.getHashIterations()) == (m, k)
+        assert bf.count() > 250
+        with co.hold():
+            fc = bf.containsAllAsync(elems)     # queued: no config read or engine call on this thread
+            fd = bf.deleteAsync()               # queued behind the contains
+            fa = bf.containsAllAsync(elems[:5])   # after the delete: the filter is gone
+            assert not fc.isDone() and not fd.isDone()
+        assert fc.get(30) == [True] * len(elems)
+        assert fd.get(30) is True
+        with pytest.raises(Exception, match="not initialized"):
+            fa.get(30)
+        assert [w for w, _ in eng.threads][-3:] == ["contains", "delete", "config"]
+        assert {t for _, t in eng.threads} == {"sk-bloom-coalescer"}, eng.threads
+    finally:
+        co.close()

@@ -180,6 +180,44 @@ def test_range_sharded_bloom_rccl_world1(engine):
 
 
 @pytest.mark.gpu
+def test_replicated_bloom_contains_dev_async_rccl_world1(O):
+    """in async mode a contains runs on the read stream and returns before it finishes; the RCCL
+    all-gather of the reply pieces and the copy into d_out must wait for it (sk_allgather / sk_d2d enter like every
+    other call).  A region-schedule batch (3 M contains) under set_async(True) equals the oracle."""
+    from redisson_amd import SketchEngine
+    from redisson_amd.cluster import RcclCollective, ReplicatedBloom
+
+    eng = SketchEngine(device=0, max_batch=4 << 20)
+    try:
+        coll = RcclCollective(eng, 0, 1)
+        rp = ReplicatedBloom(eng, b"rpb:async", 0, 1, coll)
+        assert rp.try_init(4_000_000, 0.01)
+        size, k, _, _ = eng.bloom_config(b"rpb:async")
+        seed, n_add, n_q = 0x5EED7700, 1_000_000, 3 << 20
+        off, byt, tot = eng.gen_jackson_longs_dev(seed, n_add)
+        d_add = eng.alloc(n_add)
+        rp.add_dev(n_add, off, byt, tot, d_add)
+        rng = np.random.default_rng(7)
+        idx = np.where(rng.random(n_q) < 0.5, rng.integers(0, n_add, n_q, dtype=np.uint64),
+                       rng.integers(1 << 40, 1 << 41, n_q, dtype=np.uint64)).astype(np.uint64)
+        d_idx = eng.to_device(idx)
+        qoff, qbyt, qtot = eng.gen_jackson_longs_dev(seed, n_q, d_idx=d_idx)
+        d_out = eng.alloc(n_q)
+        eng.set_async(True)
+        try:
+            rp.contains_dev(n_q, qoff, qbyt, qtot, d_out)
+        finally:
+            eng.set_async(False)
+        got = d_out.download(np.uint8, n_q)
+        bits, ln = O.bloom_add_gen(size, k, seed, 0, n_add)
+        want = O.bloom_contains_gen(bits, ln, size, k, seed, idx)
+        assert np.array_equal(got, want), np.flatnonzero(got != want)[:8]
+        assert got[idx < n_add].all()
+    finally:
+        eng.close()
+
+
+@pytest.mark.gpu
 def test_routed_bitset_mixed_call_shapes_rccl_world1(engine):
     """The same call shapes through the engine's RCCL communicator at world 1 (sk_route_bits + sk_alltoallv)."""
     from redisson_amd.cluster import RcclCollective

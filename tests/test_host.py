@@ -212,3 +212,20 @@ def test_hot_path_kernels_use_no_scratch():
             assert k[".private_segment_fixed_size"] == 0, (k[".name"], k[".private_segment_fixed_size"])
             assert not k.get(".uses_dynamic_stack", False), k[".name"]
     assert seen >= 20, seen
+
+
+def test_java_bloom_filter_makes_no_jni_call_on_the_callers_thread():
+    """VERDICT r4 item 8 (source level, no JDK): every SketchNative call of GpuBloomFilter sits inside a
+    GpuBloomCoalescer.Task body (run by the coalescer's FIFO thread, with the task's ctx argument `c`), add /
+    contains go through coalescer.submit, and the coalescer runs tasks in their FIFO place."""
+    import re
+
+    src = open(os.path.join(ROOT, "java", "org", "redisson", "GpuBloomFilter.java")).read()
+    calls = re.findall(r"SketchNative\.(\w+)\((\w+)", src)
+    assert calls and all(arg == "c" for _, arg in calls), calls
+    bodies = re.findall(r"new GpuBloomCoalescer\.Task<\w+>\(\) \{(.*?)\n        \}", src, re.S)
+    assert sum(b.count("SketchNative.") for b in bodies) == len(calls)
+    assert "deleteAsync()" in src and "onWorker(new GpuBloomCoalescer.Task<Boolean>()" in src
+    co = open(os.path.join(ROOT, "java", "org", "redisson", "gpu", "GpuBloomCoalescer.java")).read()
+    assert "public <T> void submitTask(Task<T> task, Promise<T> promise)" in co
+    assert "if (head.task != null)" in co and "task == null && o.task == null" in co

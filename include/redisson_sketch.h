@@ -51,10 +51,13 @@ extern "C" {
                               whose registers do not decode) */
 #define SK_ESTALE (-11)    /* a caller-cached HLL slab id (sk_pfadd_ids / sk_pfcount_ids) whose key was deleted,
                               replaced or flushed: drop the cached id and resolve the key by name again */
+#define SK_EBUSYKEY (-12)  /* "BUSYKEY Target key name already exists." (RESTORE without REPLACE) */
+#define SK_EPAYLOAD (-13)  /* "ERR DUMP payload version or checksum are wrong" / a malformed RDB file */
 
 #define SK_TYPE_NONE 0
 #define SK_TYPE_HLL 1    /* string holding a HyperLogLog (PFADD/PFMERGE created it) */
 #define SK_TYPE_STRING 2 /* plain string: RBitSet / Bloom filter bit array */
+#define SK_TYPE_HASH 3   /* a Bloom filter config "{name}__config" (sk_type, sk_scan) */
 
 #define SK_BITOP_AND 0
 #define SK_BITOP_OR 1
@@ -328,6 +331,39 @@ int sk_prof_enable(sk_ctx *ctx, int on);
 int sk_prof_only(sk_ctx *ctx, const char *phase);
 int sk_prof_reset(sk_ctx *ctx);
 int sk_prof_read(sk_ctx *ctx, const char *phase, uint64_t *launches, double *total_ms);
+
+/* ---- persistence: redis-server's own formats (SURVEY 5 "Checkpoint / resume", 8(f) rank 1) ----
+ * Replaces redis-server's RDB persistence behind the keys the store holds (Redisson's tests drive it through
+ * RedisRunner's nosave / appendonly / dbfilename options, T:RedisRunner.java:68,174,339,497; the values are the GET /
+ * SET byte forms, M:RedissonBitSet.java:88-91,211-214, and the Bloom config hash, M:RedissonBloomFilter.java:
+ * 231-256).  Every value is written as redis-server 3.2 writes it (RDB_VERSION 7): HLLs and bit strings as strings
+ * (an HLL is its GET bytes: the dense `HYLL` encoding, or the sparse string in exact mode), a Bloom filter's
+ * "{name}__config" as a hash in HMSET order.  Reading accepts redis-server 3.2-5.0 output of those two types
+ * (integer- and LZF-encoded strings, ziplist hashes).  A restored string that is a Redis HLL becomes an HLL key at
+ * once when that leaves GET's bytes unchanged (exact mode, or the dense encoding with a stale cache: what this store
+ * writes), else on its first HLL command, as after SET. */
+
+/* SCAN: up to `count` keys from `cursor` (0 = start); *next_cursor = 0 when the scan is done.  Every key present
+ * for the whole scan is returned once.  names: the key bytes, name_off u64[*out_n + 1] into it (stops early rather
+ * than pass names_cap); types: SK_TYPE_HLL / SK_TYPE_STRING / SK_TYPE_HASH (a Bloom filter config). */
+int sk_scan(sk_ctx *ctx, uint64_t cursor, uint32_t count, uint64_t *next_cursor, uint32_t *out_n,
+            uint64_t *name_off, uint8_t *names, uint64_t names_cap, int32_t *types);
+/* DUMP key: the redis-server DUMP payload (type, value, RDB version, CRC64).  *out_len = its size (-1: no such
+ * key); at most cap bytes are copied (call with cap = 0 to size the buffer). */
+int sk_dump(sk_ctx *ctx, const uint8_t *key, uint64_t len, uint8_t *buf, uint64_t cap, int64_t *out_len);
+/* RESTORE key 0 payload [REPLACE]: SK_EBUSYKEY if the key exists and !replace, SK_EPAYLOAD for a bad payload. */
+int sk_restore(sk_ctx *ctx, const uint8_t *key, uint64_t len, const uint8_t *payload, uint64_t plen, int replace);
+/* SAVE: every key of the store into an RDB file at `path` (written in place; HLLs packed to their dense bodies
+ * on the GPU in bulk), plus n_extra caller-held keys: 2 * n_extra items in (off, bytes), key i then its DUMP
+ * payload (the RESP front-end's small hashes).  *out_keys = keys written. */
+int sk_save(sk_ctx *ctx, const char *path, uint32_t n_extra, const uint64_t *extra_off, const uint8_t *extra_bytes,
+            uint64_t *out_keys);
+/* Load an RDB file (this store's SAVE, or redis-server's dump.rdb holding strings and hashes) into the context;
+ * keys in the file replace existing ones.  take (optional): offered every hash value first as a DUMP payload;
+ * returning 1 keeps it out of the store (the RESP front-end holds its own hashes), 0 lets the store keep it (a
+ * Bloom filter config), < 0 fails the load.  Expire times in the file are ignored (no TTL is served). */
+typedef int (*sk_take_fn)(void *user, const uint8_t *key, uint64_t klen, const uint8_t *payload, uint64_t plen);
+int sk_load(sk_ctx *ctx, const char *path, sk_take_fn take, void *user, uint64_t *out_keys);
 
 /* ---- cross-GPU exchange: RCCL over xGMI (one context per GPU / process) ---- */
 int sk_comm_unique_id(uint8_t *out128);

@@ -25,6 +25,8 @@ SK_ESYNTAX = -8
 SK_ETOOBIG = -9
 SK_ECORRUPT = -10
 SK_ESTALE = -11
+SK_EBUSYKEY = -12
+SK_EPAYLOAD = -13
 
 SK_TYPE_NONE, SK_TYPE_HLL, SK_TYPE_STRING, SK_TYPE_HASH = 0, 1, 2, 3
 SK_BITOP = {"AND": 0, "OR": 1, "XOR": 2, "NOT": 3}
@@ -129,6 +131,12 @@ SIGNATURES = {
     "sk_allreduce_max_u8": (c_int, [P, P, c_uint64]),
     "sk_allreduce_sum_u64": (c_int, [P, P, c_uint64]),
     "sk_allgather": (c_int, [P, P, P, c_uint64]),
+    # persistence: SCAN / DUMP / RESTORE / SAVE / load (redis-server's formats)
+    "sk_scan": (c_int, [P, c_uint64, c_uint32, P, P, P, P, c_uint64, P]),
+    "sk_dump": (c_int, [P, _u8p, c_uint64, _u8p, c_uint64, _i64p]),
+    "sk_restore": (c_int, [P, _u8p, c_uint64, _u8p, c_uint64, c_int]),
+    "sk_save": (c_int, [P, c_char_p, c_uint32, P, P, P]),
+    "sk_load": (c_int, [P, c_char_p, P, P, P]),
     "sk_alltoallv": (c_int, [P, P, _u64p, P, _u64p]),
     "sk_route_bits": (c_int, [P, c_uint64, _u64p, _u8p, c_uint64, c_int32, _u64p, _u8p, _u32p, _u64p]),
     "sk_unroute_u8": (c_int, [P, c_uint64, _u32p, _u8p, _u8p]),

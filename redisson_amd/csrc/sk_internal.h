@@ -86,6 +86,9 @@ hipError_t sort_pairs(hipStream_t st, void *tmp, size_t tmp_bytes, const uint64_
 // per key: out[2k] = sum 2^(40 - r) over the registers, out[2k+1] = zeros | (a register >= 40) << 32 (PFCOUNT 3.x)
 hipError_t launch_hll_sum(hipStream_t st, uint64_t n, const uint32_t *ids, const uint8_t *arena, uint64_t *out);
 hipError_t launch_hll_hist(hipStream_t st, uint64_t n, const uint32_t *ids, const uint8_t *arena, uint32_t *hist);
+// Redis dense HLL bodies in bulk (SAVE / DUMP / snapshot restore): out / in hold n x 12,288 B (4-B aligned), n < 2^30
+hipError_t launch_hll_pack(hipStream_t st, uint64_t n, const uint32_t *ids, const uint8_t *arena, uint8_t *out);
+hipError_t launch_hll_unpack(hipStream_t st, uint64_t n, const uint32_t *ids, const uint8_t *in, uint8_t *arena);
 hipError_t launch_hll_union(hipStream_t st, uint64_t n, const uint32_t *ids, const uint8_t *arena, uint8_t *partial,
                             uint64_t max_groups, uint8_t *out, int include_out);
 // scratch: 16 B per element, used by the split schedule (sched 3) only

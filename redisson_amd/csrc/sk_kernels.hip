@@ -1652,6 +1652,49 @@ __global__ void __launch_bounds__(256) k_hll_union_final(uint64_t G, const uint8
     reinterpret_cast<uint4 *>(out)[lane16] = acc;
 }
 
+// ------------------------------------------------------------------ Redis dense HLL strings, in bulk
+// The dense encoding (HLL_DENSE_SET_REGISTER): register i in bits [6i, 6i + 6) of the 12,288-B body, LSB first, so
+// 16 registers are exactly 12 bytes.  One thread packs / unpacks one such group: a 16-B vector of u8 registers in,
+// three u32 words out (and back).  SAVE / DUMP of many HLLs and the bulk restore of a snapshot (sk_rdb.h) move the
+// dense bodies through these; a thread's group never straddles a key (1024 groups per key).
+__device__ __forceinline__ void pack16(uint4 r, uint32_t *w) {
+    const uint32_t b0 = r.x, b1 = r.y, b2 = r.z, b3 = r.w;
+    auto g = [](uint32_t v, int i) { return (v >> (8 * i)) & 63u; };
+    w[0] = g(b0, 0) | g(b0, 1) << 6 | g(b0, 2) << 12 | g(b0, 3) << 18 | g(b1, 0) << 24 | (g(b1, 1) & 3u) << 30;
+    w[1] = g(b1, 1) >> 2 | g(b1, 2) << 4 | g(b1, 3) << 10 | g(b2, 0) << 16 | g(b2, 1) << 22 | (g(b2, 2) & 15u) << 28;
+    w[2] = g(b2, 2) >> 4 | g(b2, 3) << 2 | g(b3, 0) << 8 | g(b3, 1) << 14 | g(b3, 2) << 20 | g(b3, 3) << 26;
+}
+__device__ __forceinline__ uint4 unpack16(uint32_t w0, uint32_t w1, uint32_t w2) {
+    auto q = [](uint32_t a, uint32_t b, uint32_t c, uint32_t d) { return a | b << 8 | c << 16 | d << 24; };
+    const uint32_t r0 = w0 & 63u, r1 = (w0 >> 6) & 63u, r2 = (w0 >> 12) & 63u, r3 = (w0 >> 18) & 63u;
+    const uint32_t r4 = (w0 >> 24) & 63u, r5 = (w0 >> 30) | ((w1 & 15u) << 2), r6 = (w1 >> 4) & 63u;
+    const uint32_t r7 = (w1 >> 10) & 63u, r8 = (w1 >> 16) & 63u, r9 = (w1 >> 22) & 63u;
+    const uint32_t r10 = (w1 >> 28) | ((w2 & 3u) << 4), r11 = (w2 >> 2) & 63u, r12 = (w2 >> 8) & 63u;
+    const uint32_t r13 = (w2 >> 14) & 63u, r14 = (w2 >> 20) & 63u, r15 = w2 >> 26;
+    return make_uint4(q(r0, r1, r2, r3), q(r4, r5, r6, r7), q(r8, r9, r10, r11), q(r12, r13, r14, r15));
+}
+// out[i * 12288 ..) = the dense body of slab ids[i] (generation bits masked off)
+__global__ void __launch_bounds__(256) k_hll_pack(uint64_t n, const uint32_t *__restrict__ ids,
+                                                  const uint8_t *__restrict__ arena, uint32_t *__restrict__ out) {
+    const uint64_t t = uint64_t(blockIdx.x) * 256 + threadIdx.x, key = t >> 10, grp = t & 1023;
+    if (key >= n) return;
+    const uint4 r = reinterpret_cast<const uint4 *>(arena + uint64_t(ids[key] & 0xffffffu) * 16384)[grp];
+    uint32_t w[3];
+    pack16(r, w);
+    uint32_t *o = out + key * 3072 + grp * 3;
+    o[0] = w[0];
+    o[1] = w[1];
+    o[2] = w[2];
+}
+// slab ids[i] = the registers of the dense body in[i * 12288 ..)
+__global__ void __launch_bounds__(256) k_hll_unpack(uint64_t n, const uint32_t *__restrict__ ids,
+                                                    const uint32_t *__restrict__ in, uint8_t *__restrict__ arena) {
+    const uint64_t t = uint64_t(blockIdx.x) * 256 + threadIdx.x, key = t >> 10, grp = t & 1023;
+    if (key >= n) return;
+    const uint32_t *w = in + key * 3072 + grp * 3;
+    reinterpret_cast<uint4 *>(arena + uint64_t(ids[key] & 0xffffffu) * 16384)[grp] = unpack16(w[0], w[1], w[2]);
+}
+
 // ------------------------------------------------------------------ Bloom
 __device__ __forceinline__ void bloom_hashes(const uint8_t *p, uint32_t len, uint64_t *h1, uint64_t *h2) {
     *h1 = xxh64(p, len);
@@ -3655,6 +3698,22 @@ hipError_t sort_pairs64(hipStream_t st, void *tmp, size_t tmp_bytes, const uint6
 hipError_t launch_hll_sum(hipStream_t st, uint64_t n, const uint32_t *ids, const uint8_t *arena, uint64_t *out) {
     if (!n) return hipSuccess;
     hipLaunchKernelGGL(k_hll_sum, dim3(grid_for((n + 3) / 4, 1, 4096)), dim3(256), 0, st, n, ids, arena, out);
+    SK_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+hipError_t launch_hll_pack(hipStream_t st, uint64_t n, const uint32_t *ids, const uint8_t *arena, uint8_t *out) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k_hll_pack, dim3(uint32_t(n * 4)), dim3(256), 0, st, n, ids, arena,
+                       reinterpret_cast<uint32_t *>(out));
+    SK_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+hipError_t launch_hll_unpack(hipStream_t st, uint64_t n, const uint32_t *ids, const uint8_t *in, uint8_t *arena) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k_hll_unpack, dim3(uint32_t(n * 4)), dim3(256), 0, st, n, ids,
+                       reinterpret_cast<const uint32_t *>(in), arena);
     SK_LAUNCH_CHECK();
     return hipSuccess;
 }

@@ -18,6 +18,7 @@
 // their body (tools/script_digests.py derives the digests), natively.
 #include "../../include/redisson_sketch.h"
 #include "sk_resp_parse.h"
+#include "sk_rdb.h"
 
 #include <arpa/inet.h>
 #include <errno.h>
@@ -27,6 +28,7 @@
 #include <signal.h>
 #include <sys/epoll.h>
 #include <sys/socket.h>
+#include <sys/stat.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -106,6 +108,53 @@ std::string lower(std::string s) {
     return s;
 }
 
+// glob-style pattern (KEYS / SCAN MATCH, redis util.c stringmatchlen): * ? [set] [^set] [a-z] and \ escapes
+bool glob_match(const char *p, const char *pe, const char *s, const char *se) {
+    while (p < pe) {
+        if (*p == '*') {
+            while (p + 1 < pe && p[1] == '*') p++;
+            if (p + 1 == pe) return true;
+            for (const char *t = s; t <= se; t++)
+                if (glob_match(p + 1, pe, t, se)) return true;
+            return false;
+        }
+        if (s == se) return false;
+        if (*p == '?') {
+            s++, p++;
+            continue;
+        }
+        if (*p == '[') {
+            const char *q = p + 1;
+            bool neg = q < pe && *q == '^', hit = false;
+            if (neg) q++;
+            for (; q < pe && *q != ']'; q++) {
+                if (*q == '\\' && q + 1 < pe) {
+                    q++;
+                    hit |= *q == *s;
+                } else if (q + 2 < pe && q[1] == '-' && q[2] != ']') {
+                    char a = q[0], b = q[2];
+                    if (a > b) std::swap(a, b);
+                    hit |= *s >= a && *s <= b;
+                    q += 2;
+                } else {
+                    hit |= *q == *s;
+                }
+            }
+            if (hit == neg) return false;
+            p = q < pe ? q + 1 : q;
+            s++;
+            continue;
+        }
+        if (*p == '\\' && p + 1 < pe) p++;
+        if (*p != *s) return false;
+        p++, s++;
+    }
+    return s == se;
+}
+bool glob_match(const std::string &pat, const std::string &s) {
+    return glob_match(pat.data(), pat.data() + pat.size(), s.data(), s.data() + s.size());
+}
+
 // (off u64[n+1], bytes) packing of byte strings for the C ABI
 struct Packed {
     std::vector<uint64_t> off{0};
@@ -125,6 +174,7 @@ enum KType { T_NONE = 0, T_HLL = 1, T_STR = 2, T_HASH = 10 };
 struct Server {
     sk_ctx *ctx = nullptr;
     uint64_t max_bit_offset = 1ull << 32;
+    std::string rdb_path = "dump.rdb"; // --dir / --dbfilename: SAVE writes it, startup loads it when present
     // small hashes, field order kept (Redis returns ziplist order for small hashes)
     std::unordered_map<std::string, std::vector<std::pair<std::string, std::string>>> hashes;
 
@@ -156,6 +206,44 @@ struct Server {
         if (!parse_ll(s, v) || v < 0 || uint64_t(v) >= max_bit_offset) return false;
         off = uint64_t(v);
         return true;
+    }
+
+    // ---- persistence (sk_rdb.h formats) ---------------------------------
+    // every key name: the engine's (a full SCAN) then this process's hashes
+    std::vector<std::string> all_keys() {
+        std::vector<std::string> out;
+        uint64_t cur = 0;
+        std::vector<uint64_t> off(1025);
+        std::vector<uint8_t> names(1 << 20);
+        std::vector<int32_t> types(1024);
+        do {
+            uint32_t n = 0;
+            if (sk_scan(ctx, cur, 1024, &cur, &n, off.data(), names.data(), names.size(), types.data()) != SK_OK) break;
+            for (uint32_t i = 0; i < n; i++)
+                out.emplace_back(reinterpret_cast<const char *>(names.data()) + off[i], off[i + 1] - off[i]);
+        } while (cur);
+        for (auto &kv : hashes) out.push_back(kv.first);
+        return out;
+    }
+    int save() {
+        Packed extra; // the hashes as (key, DUMP payload) pairs
+        for (auto &kv : hashes) {
+            extra.add(kv.first);
+            extra.add(sk_rdb::dump_hash(kv.second));
+        }
+        uint64_t n = 0;
+        return sk_save(ctx, rdb_path.c_str(), uint32_t(hashes.size()), extra.off.data(), extra.data(), &n);
+    }
+    // sk_load's `take`: every hash stays in this process (the EVAL scripts read the Bloom configs here)
+    static int take_hash(void *user, const uint8_t *key, uint64_t klen, const uint8_t *payload, uint64_t plen) {
+        sk_rdb::Value v;
+        if (!sk_rdb::load_payload(payload, plen, v).empty()) return -1;
+        static_cast<Server *>(user)->hashes[std::string(reinterpret_cast<const char *>(key), klen)] = v.fields;
+        return 1;
+    }
+    int load() {
+        uint64_t n = 0;
+        return sk_load(ctx, rdb_path.c_str(), &Server::take_hash, this, &n);
     }
 
     // ---- batched runs -------------------------------------------------
@@ -428,6 +516,104 @@ struct Server {
         } else if (name == "script") {
             if (c.size() == 3 && lower(c[1]) == "load") r_bulk(o, sha1_hex(c[2]));
             else r_error(o, "ERR SCRIPT supports only LOAD here");
+        } else if (name == "keys") {
+            if (!arity(2, false)) return true;
+            std::vector<std::string> ks;
+            for (auto &k : all_keys())
+                if (glob_match(c[1], k)) ks.push_back(k);
+            r_array(o, ks.size());
+            for (auto &k : ks) r_bulk(o, k);
+        } else if (name == "dbsize") {
+            if (arity(1, false)) r_int(o, (long long)all_keys().size());
+        } else if (name == "scan") {
+            // SCAN cursor [MATCH pattern] [COUNT n]: the engine's cursor, then one last step with this process's
+            // hashes (cursor kHashStep)
+            if (!arity(2, true)) return true;
+            const uint64_t kHashStep = 1ull << 62;
+            long long cur;
+            if (!parse_ll(c[1], cur) || cur < 0) return r_error(o, "ERR invalid cursor"), true;
+            std::string pat;
+            long long count = 10;
+            for (size_t i = 2; i < c.size(); i += 2) {
+                std::string opt = lower(c[i]);
+                if (i + 1 >= c.size()) return r_error(o, kSyntax), true;
+                if (opt == "match") pat = c[i + 1];
+                else if (opt == "count") {
+                    if (!parse_ll(c[i + 1], count) || count < 1) return r_error(o, kNotInt), true;
+                } else return r_error(o, kSyntax), true;
+            }
+            std::vector<std::string> ks;
+            uint64_t next = 0;
+            if (uint64_t(cur) != kHashStep) {
+                uint32_t n = 0;
+                const uint32_t want = uint32_t(std::min<long long>(count, 1 << 20));
+                std::vector<uint64_t> off(want + 1);
+                std::vector<uint8_t> names(1 << 20);
+                std::vector<int32_t> types(want);
+                if (sk_scan(ctx, uint64_t(cur), want, &next, &n, off.data(), names.data(), names.size(), types.data()) !=
+                    SK_OK)
+                    return r_error(o, engine_error()), true;
+                for (uint32_t i = 0; i < n; i++)
+                    ks.emplace_back(reinterpret_cast<const char *>(names.data()) + off[i], off[i + 1] - off[i]);
+                if (!next && !hashes.empty()) next = kHashStep;
+            } else {
+                for (auto &kv : hashes) ks.push_back(kv.first);
+            }
+            r_array(o, 2);
+            r_bulk(o, std::to_string(next));
+            std::vector<std::string> hit;
+            for (auto &k : ks)
+                if (pat.empty() || glob_match(pat, k)) hit.push_back(k);
+            r_array(o, hit.size());
+            for (auto &k : hit) r_bulk(o, k);
+        } else if (name == "dump") {
+            if (!arity(2, false)) return true;
+            auto h = hashes.find(c[1]);
+            if (h != hashes.end()) return r_bulk(o, sk_rdb::dump_hash(h->second)), true;
+            int64_t len = 0;
+            if (sk_dump(ctx, k1, c[1].size(), nullptr, 0, &len) != SK_OK) return r_error(o, engine_error()), true;
+            if (len < 0) return r_nil(o), true;
+            std::string v(size_t(len), '\0');
+            if (sk_dump(ctx, k1, c[1].size(), reinterpret_cast<uint8_t *>(&v[0]), v.size(), &len) != SK_OK)
+                return r_error(o, engine_error()), true;
+            r_bulk(o, v);
+        } else if (name == "restore") {
+            // RESTORE key ttl payload [REPLACE]; no TTL is served, so ttl must be 0
+            if (!arity(4, true)) return true;
+            bool replace = false;
+            for (size_t i = 4; i < c.size(); i++) {
+                if (lower(c[i]) == "replace") replace = true;
+                else return r_error(o, kSyntax), true;
+            }
+            long long ttl;
+            if (!parse_ll(c[2], ttl) || ttl < 0) return r_error(o, "ERR Invalid TTL value, must be >= 0"), true;
+            if (ttl) return r_error(o, "ERR a TTL is not served by this engine (RESTORE with ttl 0)"), true;
+            sk_rdb::Value v;
+            std::string why = sk_rdb::load_payload(reinterpret_cast<const uint8_t *>(c[3].data()), c[3].size(), v);
+            if (!why.empty()) return r_error(o, "ERR " + why), true;
+            if (!replace && type_of(c[1]) != T_NONE) return r_error(o, "BUSYKEY Target key name already exists."), true;
+            if (v.type == sk_rdb::kTypeHash) {
+                del_one(c[1]);
+                hashes[c[1]] = v.fields;
+                return r_simple(o, "OK"), true;
+            }
+            hashes.erase(c[1]);
+            int st = sk_restore(ctx, k1, c[1].size(), reinterpret_cast<const uint8_t *>(c[3].data()), c[3].size(), 1);
+            st == SK_OK ? r_simple(o, "OK") : r_error(o, engine_error());
+        } else if (name == "save" || name == "bgsave") {
+            if (!arity(1, false)) return true;
+            if (save() != SK_OK) return r_error(o, "ERR " + engine_error()), true;
+            name == "save" ? r_simple(o, "OK") : r_simple(o, "Background saving started");
+        } else if (name == "debug") {
+            // DEBUG RELOAD: save, empty the store, load the file back (what redis' persistence tests run)
+            if (c.size() == 2 && lower(c[1]) == "reload") {
+                if (save() != SK_OK) return r_error(o, "ERR " + engine_error()), true;
+                hashes.clear();
+                if (sk_flushall(ctx) != SK_OK || load() != SK_OK) return r_error(o, "ERR " + engine_error()), true;
+                r_simple(o, "OK");
+            } else {
+                r_error(o, "ERR DEBUG supports only RELOAD here");
+            }
         } else if (name == "pfadd" || name == "getbit" || name == "setbit") { // batched kinds with a bad arity
             r_error(o, "ERR wrong number of arguments for '" + name + "' command");
         } else {
@@ -517,6 +703,10 @@ int selftest() {
     std::string o;
     r_int(o, -3), r_nil(o), r_bulk(o, "hi"), r_simple(o, "OK"), r_error(o, "ERR x");
     check(o == ":-3\r\n$-1\r\n$2\r\nhi\r\n+OK\r\n-ERR x\r\n", "reply encoding");
+    check(glob_match("tenant:*:hll", "tenant:12:hll") && !glob_match("tenant:*:hll", "tenant:12:hl"), "glob *");
+    check(glob_match("h?llo", "hello") && glob_match("h[ae]llo", "hallo") && !glob_match("h[^e]llo", "hello"),
+          "glob ? and sets");
+    check(glob_match("h[a-c]x", "hbx") && glob_match("a\\*b", "a*b") && !glob_match("a\\*b", "axb"), "glob ranges, escapes");
     printf(bad ? "selftest: %d failure(s)\n" : "selftest: OK\n", bad);
     return bad ? 1 : 0;
 }
@@ -525,6 +715,7 @@ void usage() {
     fprintf(stderr,
             "usage: sk-resp-server [--bind ADDR] [--port P (0 = any)] [--device D] [--redis-major 3|5]\n"
             "                      [--max-bit-offset N] [--hll-capacity N] [--max-batch N] [--hll-exact-strings]\n"
+            "                      [--dir D] [--dbfilename F (RDB: SAVE writes it, startup loads it if present)]\n"
             "                      | --selftest\n");
 }
 
@@ -535,6 +726,7 @@ int main(int argc, char **argv) {
     int port = 6379;
     sk_config cfg = {0, 3, 0, 0, 0};
     bool exact = false;
+    std::string dir = ".", dbfile = "dump.rdb";
     for (int i = 1; i < argc; i++) {
         std::string a = argv[i];
         auto next = [&]() -> const char * {
@@ -550,6 +742,8 @@ int main(int argc, char **argv) {
         else if (a == "--hll-capacity") cfg.hll_capacity = strtoull(next(), nullptr, 10);
         else if (a == "--max-batch") cfg.max_batch = strtoull(next(), nullptr, 10);
         else if (a == "--hll-exact-strings") exact = true; // GET of an HLL: redis-server's sparse / dense bytes
+        else if (a == "--dir") dir = next();
+        else if (a == "--dbfilename") dbfile = next();
         else return usage(), 2;
     }
     Server srv;
@@ -562,6 +756,15 @@ int main(int argc, char **argv) {
     if (exact && (st = sk_hll_exact_strings(srv.ctx, 1)) != SK_OK) {
         fprintf(stderr, "sk-resp-server: %s\n", sk_strerror(st));
         return 1;
+    }
+    srv.rdb_path = dir + "/" + dbfile;
+    struct stat sst;
+    if (stat(srv.rdb_path.c_str(), &sst) == 0) { // redis-server loads its RDB file at startup
+        if (srv.load() != SK_OK) {
+            fprintf(stderr, "sk-resp-server: cannot load %s: %s\n", srv.rdb_path.c_str(), sk_last_error(srv.ctx));
+            sk_close(srv.ctx);
+            return 1;
+        }
     }
     int lfd = socket(AF_INET, SOCK_STREAM, 0);
     int one = 1;

@@ -16,6 +16,7 @@
 #include <condition_variable>
 #include <functional>
 #include <cmath>
+#include <cerrno>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -28,11 +29,15 @@
 #include <vector>
 
 #include <rccl/rccl.h>
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
 #include <unistd.h>
 
 #include "../../include/redisson_sketch.h"
 #include "sk_internal.h"
 #include "sk_hllstr.h"
+#include "sk_rdb.h"
 
 using namespace sk_hll;
 
@@ -168,6 +173,8 @@ struct BloomCfg {
     int32_t k;
     int64_t expected;
     double fpp;
+    sk_rdb::Fields fields; // the hash as stored (HMSET order and value strings), what DUMP / SAVE write
+    uint64_t seq = 0;      // its SCAN position: set once when the key is created, unique in the context
 };
 
 struct DBuf {
@@ -316,6 +323,7 @@ struct sk_ctx {
 
     std::unordered_map<std::string, KeyEnt> keys;
     std::unordered_map<std::string, BloomCfg> bloom; // keyed by "{name}__config"
+    uint64_t bloom_seq = 0;                          // next BloomCfg::seq
 
     // HLL arena: slab id -> arena + id*16 KiB; free slabs are kept zeroed
     uint8_t *arena = nullptr;
@@ -1200,6 +1208,8 @@ const char *sk_strerror(int s) {
     case SK_ETOOBIG: return "Bloom filter can't be greater than 4294967294";
     case SK_ECORRUPT: return "INVALIDOBJ Corrupted HLL object detected";
     case SK_ESTALE: return "stale HLL slab id: resolve the key again";
+    case SK_EBUSYKEY: return "BUSYKEY Target key name already exists.";
+    case SK_EPAYLOAD: return "ERR DUMP payload version or checksum are wrong";
     default: return "unknown";
     }
 }
@@ -2679,7 +2689,9 @@ int sk_bloom_try_init(sk_ctx *c, const uint8_t *name, uint64_t len, int64_t expe
     // that follows it still runs, so the new parameters replace the config,
     // and tryInit returns false after re-reading it (Q6).
     *out_ok = c->bloom.count(cfg) ? 0 : 1;
-    c->bloom[cfg] = BloomCfg{m, k, expected, fpp};
+    auto prev = c->bloom.find(cfg);
+    const uint64_t seq = prev != c->bloom.end() ? prev->second.seq : c->bloom_seq++; // a replaced config keeps it
+    c->bloom[cfg] = BloomCfg{m, k, expected, fpp, sk_rdb::bloom_config_fields(m, k, expected, fpp), seq};
     return SK_OK;
 }
 
@@ -3330,3 +3342,386 @@ extern "C" int sk_gen_jackson_longs_dev(sk_ctx *c, uint64_t seed, const uint64_t
                                      c->sort_tmp.cap, d_off, d_bytes));
     return sync(c);
 }
+
+// ================================================================== persistence (SURVEY 5 "Checkpoint / resume")
+// redis-server's own formats (sk_rdb.h): DUMP / RESTORE payloads, SCAN over the keys, and RDB files (SAVE / load).
+namespace {
+
+// GET's bytes of an HLL key (sk_get): the exact-mode sparse string, or the dense encoding (kept header in exact
+// mode, else "HYLL" + stale cache).  regs: the slab's registers, already on the host.
+void hll_string_of(const sk_ctx *c, uint32_t id, const uint8_t *regs, std::string &out) {
+    const HllStr *hx = c->hll_exact && id < c->hstr.size() ? &c->hstr[id] : nullptr;
+    if (hx && hx->sparse) {
+        out.assign(reinterpret_cast<const char *>(hx->hdr), 16);
+        out.append(reinterpret_cast<const char *>(hx->ops.data()), hx->ops.size());
+        return;
+    }
+    out.assign(SK_HLL_DENSE_SIZE, '\0');
+    hll_dense_encode(regs, hx ? hx->hdr : nullptr, reinterpret_cast<uint8_t *>(&out[0]));
+}
+
+// the value of key k as a DUMP payload (*found = false: no such key)
+int key_payload(sk_ctx *c, const std::string &k, std::string &out, bool *found) {
+    *found = false;
+    auto b = c->bloom.find(k);
+    if (b != c->bloom.end()) {
+        *found = true;
+        out = sk_rdb::dump_hash(b->second.fields);
+        return SK_OK;
+    }
+    auto it = c->keys.find(k);
+    if (it == c->keys.end()) return SK_OK;
+    *found = true;
+    std::string v;
+    if (it->second.type == SK_TYPE_HLL) {
+        std::vector<uint8_t> regs(kHllBytes);
+        HIPCHK(c, hipMemcpyAsync(regs.data(), c->arena + uint64_t(it->second.id) * kHllBytes, kHllBytes,
+                                 hipMemcpyDeviceToHost, c->st));
+        int r = sync(c);
+        if (r) return r;
+        hll_string_of(c, it->second.id, regs.data(), v);
+    } else {
+        uint64_t l;
+        int r = str_len(c, it->second.id, &l);
+        if (r) return r;
+        v.assign(l, '\0');
+        if (l) HIPCHK(c, hipMemcpyAsync(&v[0], c->strs[it->second.id].ptr, l, hipMemcpyDeviceToHost, c->st));
+        if ((r = sync(c))) return r;
+    }
+    out = sk_rdb::dump_string(v.data(), v.size());
+    return SK_OK;
+}
+
+// A restored string that is a Redis HLL is adopted at once when GET would return the same bytes afterwards: in
+// exact mode (header and sparse opcodes are kept), or for the dense encoding with a stale cache and no other header
+// bytes (what this store's GET writes).  Anything else stays a string until its first HLL command, as after SET.
+bool hll_eager(const sk_ctx *c, const std::string &v) {
+    const uint8_t *s = reinterpret_cast<const uint8_t *>(v.data());
+    if (v.size() < 16 || std::memcmp(s, "HYLL", 4) != 0) return false;
+    if (c->hll_exact) return s[4] <= 1;
+    if (v.size() != SK_HLL_DENSE_SIZE || s[4] != 0 || s[15] != 0x80) return false;
+    for (int i = 5; i < 15; i++)
+        if (s[i]) return false;
+    return true;
+}
+
+bool parse_i64(const std::string &s, int64_t *v) {
+    if (s.empty() || s.size() > 20) return false;
+    char *e = nullptr;
+    errno = 0;
+    long long x = std::strtoll(s.c_str(), &e, 10);
+    if (errno || *e) return false;
+    *v = x;
+    return true;
+}
+
+// a hash restored into the store: a Bloom filter config (size and hashIterations, M:RedissonBloomFilter.java:
+// 213-219; the other fields optional), kept with its fields as given
+int bloom_from_fields(sk_ctx *c, const sk_rdb::Fields &f, BloomCfg *out) {
+    const std::string *size = nullptr, *hi = nullptr, *ex = nullptr, *fp = nullptr;
+    for (auto &kv : f) {
+        if (kv.first == "size") size = &kv.second;
+        else if (kv.first == "hashIterations") hi = &kv.second;
+        else if (kv.first == "expectedInsertions") ex = &kv.second;
+        else if (kv.first == "falseProbability") fp = &kv.second;
+    }
+    int64_t sz, k, e = 0;
+    if (!size || !hi || !parse_i64(*size, &sz) || !parse_i64(*hi, &k) || (ex && !parse_i64(*ex, &e)))
+        return fail(c, SK_EINVAL,
+                    "ERR the sketch store keeps hashes only as Bloom filter configs (integer size and hashIterations)");
+    *out = BloomCfg{sz, int32_t(k), e, fp ? std::strtod(fp->c_str(), nullptr) : 0.0, f, 0};
+    return SK_OK;
+}
+
+// a staging area of dense HLL bodies adopted in bulk: registers unpacked into their slabs by k_hll_unpack
+struct HllBulk {
+    std::vector<uint32_t> ids;
+    std::vector<uint8_t> bodies; // 12,288 B per key
+};
+int hll_bulk_flush(sk_ctx *c, HllBulk &b) {
+    const uint64_t n = b.ids.size();
+    if (!n) return SK_OK;
+    HIPCHK(c, c->misc.ensure(n * 4));
+    HIPCHK(c, c->partial.ensure(n * 12288));
+    HIPCHK(c, hipMemcpyAsync(c->misc.p, b.ids.data(), n * 4, hipMemcpyHostToDevice, c->st));
+    HIPCHK(c, hipMemcpyAsync(c->partial.p, b.bodies.data(), n * 12288, hipMemcpyHostToDevice, c->st));
+    HIPCHK(c, sk::launch_hll_unpack(c->st, n, c->misc.as<uint32_t>(), c->partial.as<uint8_t>(), c->arena));
+    int r = sync(c);
+    b.ids.clear();
+    b.bodies.clear();
+    return r;
+}
+
+// the restored value of key k (already absent from the store); HLLs adopted at once go through `bulk`
+int restore_value(sk_ctx *c, const std::string &k, sk_rdb::Value &v, HllBulk &bulk) {
+    if (v.type == sk_rdb::kTypeHash) {
+        BloomCfg b;
+        int r = bloom_from_fields(c, v.fields, &b);
+        if (r) return r;
+        b.seq = c->bloom_seq++;
+        c->bloom[k] = std::move(b);
+        return SK_OK;
+    }
+    if (hll_eager(c, v.bytes)) {
+        const uint8_t *s = reinterpret_cast<const uint8_t *>(v.bytes.data());
+        std::vector<uint8_t> regs;
+        const bool dense = s[4] == 0 && v.bytes.size() == SK_HLL_DENSE_SIZE; // any dense body decodes
+        if (!dense) regs.resize(kHllBytes);
+        if (dense || hll_decode(s, v.bytes.size(), regs.data()) == SK_OK) {
+            uint32_t id;
+            int r = hll_alloc(c, &id);
+            if (r) return r;
+            c->keys[k] = KeyEnt{SK_TYPE_HLL, id};
+            if (c->hll_exact) {
+                HllStr &h = c->hstr[id];
+                std::memcpy(h.hdr, s, 16);
+                h.sparse = s[4] == 1;
+                if (h.sparse) h.ops.assign(s + 16, s + v.bytes.size());
+                else std::vector<uint8_t>().swap(h.ops);
+            }
+            const size_t at = bulk.bodies.size();
+            bulk.bodies.resize(at + 12288);
+            if (dense) {
+                std::memcpy(&bulk.bodies[at], s + 16, 12288);
+            } else { // sparse (exact mode): its registers in the dense layout
+                std::vector<uint8_t> d(SK_HLL_DENSE_SIZE);
+                hll_dense_encode(regs.data(), nullptr, d.data());
+                std::memcpy(&bulk.bodies[at], d.data() + 16, 12288);
+            }
+            bulk.ids.push_back(id);
+            return bulk.ids.size() >= 8192 ? hll_bulk_flush(c, bulk) : SK_OK;
+        }
+    }
+    uint32_t id;
+    int r = str_get(c, k, true, v.bytes.size(), &id);
+    if (r) return r;
+    if (!v.bytes.empty())
+        HIPCHK(c, hipMemcpyAsync(c->strs[id].ptr, v.bytes.data(), v.bytes.size(), hipMemcpyHostToDevice, c->st));
+    if ((r = sync(c))) return r;
+    return str_set_len(c, id, v.bytes.size());
+}
+
+} // namespace
+
+extern "C" {
+
+// SCAN: positions (type class << 56 | slab / string id / config sequence) are unique and stable while a key lives,
+// so the cursor is "the next position" (+ 1, 0 = start); a call returns the `count` keys of lowest position at or
+// after it
+int sk_scan(sk_ctx *c, uint64_t cursor, uint32_t count, uint64_t *next_cursor, uint32_t *out_n, uint64_t *name_off,
+            uint8_t *names, uint64_t names_cap, int32_t *types) {
+    std::lock_guard<std::mutex> g(c->mu);
+    ENTER(c);
+    *out_n = 0;
+    *next_cursor = 0;
+    name_off[0] = 0;
+    if (!count) return SK_OK;
+    const uint64_t from = cursor ? cursor - 1 : 0;
+    struct Ent {
+        uint64_t pos;
+        const std::string *name;
+        int type;
+    };
+    std::vector<Ent> all;
+    all.reserve(c->keys.size() + c->bloom.size());
+    for (auto &kv : c->keys) {
+        const uint64_t pos = (uint64_t(kv.second.type == SK_TYPE_HLL ? 0 : 1) << 56) | kv.second.id;
+        if (pos >= from) all.push_back(Ent{pos, &kv.first, kv.second.type});
+    }
+    for (auto &kv : c->bloom) {
+        const uint64_t pos = (2ull << 56) | kv.second.seq;
+        if (pos >= from) all.push_back(Ent{pos, &kv.first, SK_TYPE_HASH});
+    }
+    const size_t take = std::min<size_t>(count, all.size());
+    std::partial_sort(all.begin(), all.begin() + take, all.end(), [](const Ent &x, const Ent &y) { return x.pos < y.pos; });
+    uint64_t used = 0;
+    size_t n = 0;
+    for (; n < take; n++) {
+        const std::string &nm = *all[n].name;
+        if (used + nm.size() > names_cap) break;
+        std::memcpy(names + used, nm.data(), nm.size());
+        used += nm.size();
+        name_off[n + 1] = used;
+        types[n] = all[n].type;
+    }
+    if (n == 0 && take) return fail(c, SK_EINVAL, "sk_scan: names_cap %llu is too small for the next key",
+                                    (unsigned long long)names_cap);
+    *out_n = uint32_t(n);
+    if (n < all.size()) *next_cursor = all[n - 1].pos + 2;
+    return SK_OK;
+}
+
+int sk_dump(sk_ctx *c, const uint8_t *key, uint64_t len, uint8_t *buf, uint64_t cap, int64_t *out_len) {
+    std::lock_guard<std::mutex> g(c->mu);
+    ENTER(c);
+    std::string p;
+    bool found;
+    int r = key_payload(c, key_of(key, len), p, &found);
+    if (r) return r;
+    *out_len = found ? int64_t(p.size()) : -1;
+    if (found && cap) std::memcpy(buf, p.data(), std::min<uint64_t>(cap, p.size()));
+    return SK_OK;
+}
+
+int sk_restore(sk_ctx *c, const uint8_t *key, uint64_t len, const uint8_t *payload, uint64_t plen, int replace) {
+    std::lock_guard<std::mutex> g(c->mu);
+    ENTER(c);
+    const std::string k = key_of(key, len);
+    sk_rdb::Value v;
+    std::string why = sk_rdb::load_payload(payload, plen, v);
+    if (!why.empty())
+        return fail(c, SK_EPAYLOAD, "ERR %s", why.c_str());
+    if (!replace && (c->keys.count(k) || c->bloom.count(k)))
+        return fail(c, SK_EBUSYKEY, "BUSYKEY Target key name already exists.");
+    bool removed;
+    int r = del_key(c, k, &removed);
+    if (r) return r;
+    HllBulk bulk;
+    if ((r = restore_value(c, k, v, bulk))) return r;
+    if ((r = hll_bulk_flush(c, bulk))) return r;
+    return sync(c);
+}
+
+int sk_save(sk_ctx *c, const char *path, uint32_t n_extra, const uint64_t *extra_off, const uint8_t *extra_bytes,
+            uint64_t *out_keys) {
+    std::lock_guard<std::mutex> g(c->mu);
+    ENTER(c);
+    uint64_t nk = 0;
+    // the caller's records first checked, so a bad one fails before the file is touched
+    std::vector<sk_rdb::Value> extra(n_extra);
+    for (uint32_t i = 0; i < n_extra; i++) {
+        const uint64_t a = extra_off[2 * i + 1], b = extra_off[2 * i + 2];
+        std::string why = sk_rdb::load_payload(extra_bytes + a, b - a, extra[i]);
+        if (!why.empty()) return fail(c, SK_EPAYLOAD, "ERR extra record %u: %s", i, why.c_str());
+    }
+    sk_rdb::FileWriter w;
+    if (!w.open(path)) return fail(c, SK_EINVAL, "ERR cannot open %s: %s", path, strerror(errno));
+    std::vector<std::pair<uint32_t, const std::string *>> hlls, strs;
+    for (auto &kv : c->keys) (kv.second.type == SK_TYPE_HLL ? hlls : strs).emplace_back(kv.second.id, &kv.first);
+    std::sort(hlls.begin(), hlls.end());
+    std::sort(strs.begin(), strs.end());
+    // one pinned host buffer for every device read: HLL bodies in batches, strings in pieces
+    constexpr uint64_t kBatch = 4096, kPiece = kBatch * 12288;
+    uint8_t *pin = nullptr;
+    HIPCHK(c, hipHostMalloc(reinterpret_cast<void **>(&pin), kPiece, hipHostMallocDefault));
+    auto done = [&](int rc) {
+        (void)hipHostFree(pin);
+        return rc;
+    };
+    int r = SK_OK;
+    for (size_t b0 = 0; b0 < hlls.size() && !r; b0 += kBatch) {
+        const uint64_t n = std::min<uint64_t>(kBatch, hlls.size() - b0);
+        std::vector<uint32_t> ids(n);
+        for (uint64_t i = 0; i < n; i++) ids[i] = hlls[b0 + i].first;
+        if (c->misc.ensure(n * 4) != hipSuccess || c->partial.ensure(n * 12288) != hipSuccess)
+            return done(fail(c, SK_ENOMEM, "cannot allocate SAVE staging"));
+        if (hipMemcpyAsync(c->misc.p, ids.data(), n * 4, hipMemcpyHostToDevice, c->st) != hipSuccess ||
+            sk::launch_hll_pack(c->st, n, c->misc.as<uint32_t>(), c->arena, c->partial.as<uint8_t>()) != hipSuccess ||
+            hipMemcpyAsync(pin, c->partial.p, n * 12288, hipMemcpyDeviceToHost, c->st) != hipSuccess)
+            return done(fail(c, SK_EDEVICE, "HIP error during SAVE"));
+        if ((r = sync(c))) return done(r);
+        for (uint64_t i = 0; i < n; i++) {
+            const uint32_t id = ids[i];
+            const HllStr *hx = c->hll_exact && id < c->hstr.size() ? &c->hstr[id] : nullptr;
+            w.record_head(sk_rdb::kTypeString, *hlls[b0 + i].second);
+            std::string h;
+            if (hx && hx->sparse) { // the sparse string as GET returns it
+                sk_rdb::put_len(h, 16 + hx->ops.size());
+                h.append(reinterpret_cast<const char *>(hx->hdr), 16);
+                h.append(reinterpret_cast<const char *>(hx->ops.data()), hx->ops.size());
+                w.put(h);
+            } else {
+                sk_rdb::put_len(h, SK_HLL_DENSE_SIZE);
+                uint8_t hdr[16] = {'H', 'Y', 'L', 'L', 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0x80};
+                if (hx) std::memcpy(hdr, hx->hdr, 16);
+                h.append(reinterpret_cast<const char *>(hdr), 16);
+                w.put(h);
+                w.put(pin + i * 12288, 12288);
+            }
+            nk++;
+        }
+    }
+    for (auto &e : strs) {
+        uint64_t l;
+        if ((r = str_len(c, e.first, &l))) return done(r);
+        w.record_head(sk_rdb::kTypeString, *e.second);
+        std::string h;
+        sk_rdb::put_len(h, l);
+        w.put(h);
+        for (uint64_t o = 0; o < l; o += kPiece) {
+            const uint64_t m = std::min(kPiece, l - o);
+            if (hipMemcpyAsync(pin, c->strs[e.first].ptr + o, m, hipMemcpyDeviceToHost, c->st) != hipSuccess)
+                return done(fail(c, SK_EDEVICE, "HIP error during SAVE"));
+            if ((r = sync(c))) return done(r);
+            w.put(pin, m);
+        }
+        nk++;
+    }
+    std::vector<const std::string *> cfgs;
+    for (auto &kv : c->bloom) cfgs.push_back(&kv.first);
+    std::sort(cfgs.begin(), cfgs.end(), [](const std::string *a, const std::string *b) { return *a < *b; });
+    for (auto *k : cfgs) {
+        const sk_rdb::Fields &f = c->bloom[*k].fields;
+        w.record_head(sk_rdb::kTypeHash, *k);
+        std::string h;
+        sk_rdb::put_len(h, f.size());
+        for (auto &kv : f) sk_rdb::put_string(h, kv.first), sk_rdb::put_string(h, kv.second);
+        w.put(h);
+        nk++;
+    }
+    for (uint32_t i = 0; i < n_extra; i++) {
+        const uint64_t a = extra_off[2 * i], b = extra_off[2 * i + 1];
+        const uint8_t *p = extra_bytes + extra_off[2 * i + 1];
+        const uint64_t pl = extra_off[2 * i + 2] - extra_off[2 * i + 1];
+        w.record_head(p[0], std::string(reinterpret_cast<const char *>(extra_bytes + a), b - a));
+        w.put(p + 1, pl - 11); // the value: the payload without its type byte and 10-byte trailer
+        nk++;
+    }
+    if (!w.close()) return done(fail(c, SK_EINVAL, "ERR error writing %s: %s", path, strerror(errno)));
+    if (out_keys) *out_keys = nk;
+    return done(SK_OK);
+}
+
+int sk_load(sk_ctx *c, const char *path, sk_take_fn take, void *user, uint64_t *out_keys) {
+    std::lock_guard<std::mutex> g(c->mu);
+    ENTER(c);
+    const int fd = ::open(path, O_RDONLY);
+    if (fd < 0) return fail(c, SK_EINVAL, "ERR cannot open %s: %s", path, strerror(errno));
+    struct stat stt;
+    if (fstat(fd, &stt) != 0 || stt.st_size <= 0) {
+        ::close(fd);
+        return fail(c, SK_EPAYLOAD, "ERR %s is empty or unreadable", path);
+    }
+    const uint64_t n = uint64_t(stt.st_size);
+    void *m = mmap(nullptr, n, PROT_READ, MAP_PRIVATE, fd, 0);
+    ::close(fd);
+    if (m == MAP_FAILED) return fail(c, SK_ENOMEM, "ERR cannot map %s: %s", path, strerror(errno));
+    const uint8_t *img = static_cast<const uint8_t *>(m);
+    uint64_t nk = 0;
+    HllBulk bulk;
+    int rc = SK_OK;
+    std::string why = sk_rdb::parse_rdb(img, n, [&](const std::string &key, uint8_t type, sk_rdb::Reader &rd) {
+        sk_rdb::Value v;
+        std::string w = sk_rdb::load_value(rd, type, v);
+        if (!w.empty()) return w;
+        nk++;
+        if (v.type == sk_rdb::kTypeHash && take) {
+            const std::string p = sk_rdb::dump_hash(v.fields);
+            const int t = take(user, reinterpret_cast<const uint8_t *>(key.data()), key.size(),
+                               reinterpret_cast<const uint8_t *>(p.data()), p.size());
+            if (t < 0) return std::string("the caller refused the hash ") + key;
+            if (t == 1) return std::string();
+        }
+        bool removed;
+        if ((rc = del_key(c, key, &removed)) || (rc = restore_value(c, key, v, bulk)))
+            return std::string("store error: ") + c->err;
+        return std::string();
+    });
+    if (why.empty() && (rc = hll_bulk_flush(c, bulk))) why = "store error: " + c->err;
+    munmap(m, n);
+    if (!why.empty()) return rc ? rc : fail(c, SK_EPAYLOAD, "ERR %s: %s", path, why.c_str());
+    if (out_keys) *out_keys = nk;
+    return sync(c);
+}
+
+} // extern "C"

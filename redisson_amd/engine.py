@@ -9,6 +9,7 @@ client-side checks, M:RedissonBloomFilter.java:72-74,217,284).
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import Iterable, List, Sequence
 
 import numpy as np
@@ -555,6 +556,60 @@ class SketchEngine:
         k = _b(key)
         v = np.frombuffer(bytes(value) + b"\0", dtype=np.uint8)
         self._check(self.lib.sk_set(self.ctx, k, len(k), _addr(v), len(value)))
+
+    # ------------------------------------------------------------ persistence (redis-server's DUMP / RDB formats)
+    def scan(self, cursor: int = 0, count: int = 1000):
+        """SCAN: (next cursor, [(key bytes, SK_TYPE_*)]); next cursor 0 = done."""
+        cap = 1 << 20
+        nxt, n = ctypes.c_uint64(), ctypes.c_uint32()
+        off = np.zeros(count + 1, dtype=np.uint64)
+        names = np.zeros(cap, dtype=np.uint8)
+        types = np.zeros(max(count, 1), dtype=np.int32)
+        self._check(self.lib.sk_scan(self.ctx, int(cursor), int(count), ctypes.addressof(nxt), ctypes.addressof(n),
+                                     _addr(off), _addr(names), cap, _addr(types)))
+        raw = names.tobytes()
+        return nxt.value, [(raw[off[i]:off[i + 1]], int(types[i])) for i in range(n.value)]
+
+    def keys(self) -> List[tuple]:
+        """Every (key, type) of the store, by a full SCAN."""
+        out, cur = [], 0
+        while True:
+            cur, part = self.scan(cur, 4096)
+            out += part
+            if not cur:
+                return out
+
+    def dump(self, key):
+        """DUMP key: redis-server's payload (type, value, RDB version, CRC64), or None."""
+        k = _b(key)
+        ln = ctypes.c_int64()
+        self._check(self.lib.sk_dump(self.ctx, k, len(k), None, 0, ctypes.addressof(ln)))
+        if ln.value < 0:
+            return None
+        buf = np.zeros(max(ln.value, 1), dtype=np.uint8)
+        self._check(self.lib.sk_dump(self.ctx, k, len(k), _addr(buf), ln.value, ctypes.addressof(ln)))
+        return buf[: ln.value].tobytes()
+
+    def restore(self, key, payload: bytes, replace: bool = False):
+        """RESTORE key 0 payload [REPLACE]."""
+        k = _b(key)
+        v = np.frombuffer(bytes(payload) + b"\0", dtype=np.uint8)
+        self._check(self.lib.sk_restore(self.ctx, k, len(k), _addr(v), len(payload), int(replace)))
+
+    def save(self, path, extra=()) -> int:
+        """SAVE the whole store as an RDB file; extra: (key, DUMP payload) pairs written with it.  Keys written."""
+        items = [bytes(x) for kv in extra for x in (_b(kv[0]), kv[1])]
+        off, buf = pack(items) if items else (np.zeros(1, dtype=np.uint64), np.zeros(16, dtype=np.uint8))
+        n = ctypes.c_uint64()
+        self._check(self.lib.sk_save(self.ctx, os.fsencode(path), len(extra), _addr(off), _addr(buf),
+                                     ctypes.addressof(n)))
+        return n.value
+
+    def load(self, path) -> int:
+        """Load an RDB file (this store's SAVE or redis-server's dump.rdb of strings / hashes).  Keys read."""
+        n = ctypes.c_uint64()
+        self._check(self.lib.sk_load(self.ctx, os.fsencode(path), None, None, ctypes.addressof(n)))
+        return n.value
 
     def get_dev(self, key, d_buf, cap: int) -> int:
         """Copy a bit string into device memory (<= cap bytes); its length, or -1 if the key does not exist."""

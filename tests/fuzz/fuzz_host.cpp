@@ -17,9 +17,12 @@
 #include <string>
 #include <vector>
 
+#include <unistd.h>
+
 #include "../../oracle/sketch_oracle.h"
 #include "../../redisson_amd/csrc/sk_device.h"
 #include "../../redisson_amd/csrc/sk_hllstr.h"
+#include "../../redisson_amd/csrc/sk_rdb.h"
 #include "../../redisson_amd/csrc/sk_resp_parse.h"
 
 using namespace sk_hll;
@@ -310,6 +313,174 @@ void fuzz_hash(Rng &r, long it) {
 
 } // namespace
 
+// ---------------------------------------------------------------- redis persistence formats (sk_rdb.h)
+// known answers once, then random values through DUMP payloads and RDB file images, and mutated images that must be
+// refused or parsed without a memory error
+std::string bytes_of(std::initializer_list<int> b) {
+    std::string o;
+    for (int x : b) o.push_back(char(x));
+    return o;
+}
+
+void rdb_known(long it) {
+    check(sk_rdb::crc64(0, reinterpret_cast<const uint8_t *>("123456789"), 9) == 0xe9c6d914c4b8d9caull,
+          "crc64 check value", it);
+    // the Redis documentation's DUMP example: SET mykey 10 -> "\x00\xc0\n\t\x00\xbem\x06\x89Z(\x00\n" (RDB 9,
+    // the value integer-encoded)
+    const std::string doc = bytes_of({0x00, 0xc0, 0x0a, 0x09, 0x00, 0xbe, 0x6d, 0x06, 0x89, 0x5a, 0x28, 0x00, 0x0a});
+    sk_rdb::Value v;
+    std::string why = sk_rdb::load_payload(reinterpret_cast<const uint8_t *>(doc.data()), doc.size(), v);
+    check(why.empty() && v.type == sk_rdb::kTypeString && v.bytes == "10", "redis docs DUMP payload", it);
+    std::string bad = doc;
+    bad[2] = 0x0b;
+    check(!sk_rdb::load_payload(reinterpret_cast<const uint8_t *>(bad.data()), bad.size(), v).empty(),
+          "checksum mismatch refused", it);
+    // LZF: literal 'a', then a back reference of 9 bytes at distance 1 (ctrl 0xE0, length byte 0, offset 0)
+    const std::string lz = bytes_of({0x00, 'a', 0xe0, 0x00, 0x00});
+    std::string out(10, '\0');
+    check(sk_rdb::lzf_decompress(reinterpret_cast<const uint8_t *>(lz.data()), lz.size(),
+                                 reinterpret_cast<uint8_t *>(&out[0]), 10) && out == std::string(10, 'a'),
+          "lzf back reference", it);
+    // a ziplist hash as redis 3.2 stores a small HMSET: "size" -> 729 (int16), "hashIterations" -> 5 (immediate)
+    std::string ents;
+    std::vector<size_t> sizes;
+    auto entry = [&](const std::string &e) {
+        const size_t prev = sizes.empty() ? 0 : sizes.back();
+        std::string x(1, char(prev));
+        x += e;
+        sizes.push_back(x.size());
+        ents += x;
+    };
+    entry(bytes_of({0x04}) + "size");
+    entry(bytes_of({0xc0, 0xd9, 0x02}));
+    entry(bytes_of({0x0e}) + "hashIterations");
+    entry(bytes_of({0xf6}));
+    const uint32_t zlbytes = uint32_t(10 + ents.size() + 1), zltail = uint32_t(10 + ents.size() - sizes.back());
+    std::string zl(10, '\0');
+    std::memcpy(&zl[0], &zlbytes, 4);
+    std::memcpy(&zl[4], &zltail, 4);
+    zl[8] = 4;
+    zl += ents;
+    zl.push_back(char(0xff));
+    std::vector<std::string> e;
+    check(sk_rdb::ziplist_entries(zl, e) && e.size() == 4 && e[0] == "size" && e[1] == "729" &&
+              e[2] == "hashIterations" && e[3] == "5",
+          "ziplist hash", it);
+    // Redisson's falseProbability strings: BigDecimal.valueOf(d).toPlainString()
+    check(sk_rdb::java_plain_double(0.03) == "0.03", "plain 0.03", it);
+    check(sk_rdb::java_plain_double(0.008) == "0.008", "plain 0.008", it);
+    check(sk_rdb::java_plain_double(1e-6) == "0.0000010", "plain 1.0E-6", it);
+    check(sk_rdb::java_plain_double(1.5e-6) == "0.0000015", "plain 1.5E-6", it);
+    check(sk_rdb::java_plain_double(0.5) == "0.5", "plain 0.5", it);
+    check(sk_rdb::java_plain_double(1.0) == "1.0", "plain 1.0", it);
+    check(sk_rdb::java_plain_double(1e7) == "10000000", "plain 1.0E7", it);
+}
+
+std::string random_bytes(Rng &r, size_t n) {
+    std::string s(n, '\0');
+    for (auto &ch : s) ch = char(r.below(256));
+    return s;
+}
+
+void fuzz_rdb(Rng &r, long it) {
+    if (it == 0) rdb_known(it);
+    // a random value through a DUMP payload
+    sk_rdb::Value v, got;
+    std::string p;
+    if (r.below(3)) {
+        const uint32_t pick = r.below(4);
+        const size_t n = pick == 0 ? r.below(64) : pick == 1 ? 64 + r.below(16320) : pick == 2 ? r.below(20) : 16384 + r.below(70000);
+        v.bytes = random_bytes(r, n);
+        p = sk_rdb::dump_string(v.bytes.data(), v.bytes.size());
+    } else {
+        v.type = sk_rdb::kTypeHash;
+        for (uint32_t i = 0, nf = r.below(9); i < nf; i++)
+            v.fields.emplace_back(random_bytes(r, r.below(40)), random_bytes(r, r.below(r.below(8) ? 30 : 300)));
+        p = sk_rdb::dump_hash(v.fields);
+    }
+    {
+        std::vector<uint8_t> copy(p.begin(), p.end()); // exact length: reads past it are reported
+        std::string why = sk_rdb::load_payload(copy.data(), copy.size(), got);
+        check(why.empty() && got.type == v.type && got.bytes == v.bytes && got.fields == v.fields,
+              "DUMP payload round trip", it);
+    }
+    std::string m = p;
+    mutate(r, m);
+    {
+        std::vector<uint8_t> copy(m.begin(), m.end());
+        sk_rdb::Value x;
+        (void)sk_rdb::load_payload(copy.data(), copy.size(), x); // refused or decoded, never a memory error
+        // the CRC is bypassed: the decoder itself over mutated bytes
+        if (copy.size() > 1) {
+            sk_rdb::Reader rd{copy.data() + 1, copy.data() + copy.size()};
+            (void)sk_rdb::load_value(rd, copy[0], x);
+        }
+    }
+    std::string lz = random_bytes(r, r.below(40));
+    std::vector<uint8_t> lin(lz.begin(), lz.end()), lout(r.below(80));
+    (void)sk_rdb::lzf_decompress(lin.data(), lin.size(), lout.data(), lout.size());
+    std::vector<std::string> ze;
+    (void)sk_rdb::ziplist_entries(random_bytes(r, r.below(60)), ze);
+    // an RDB image of a few records, written through FileWriter and parsed back (every 64th iteration)
+    if (it % 64 == 0) {
+        char path[] = "/tmp/sk_fuzz_rdbXXXXXX";
+        const int fd = mkstemp(path);
+        if (fd < 0) return check(false, "mkstemp", it);
+        close(fd);
+        std::vector<std::pair<std::string, sk_rdb::Value>> recs;
+        sk_rdb::FileWriter w;
+        check(w.open(path), "rdb open", it);
+        for (uint32_t i = 0, n = r.below(6); i < n; i++) {
+            sk_rdb::Value x;
+            const std::string key = random_bytes(r, 1 + r.below(20));
+            if (r.below(2)) {
+                x.bytes = random_bytes(r, r.below(3000));
+                w.record_head(sk_rdb::kTypeString, key);
+                std::string h;
+                sk_rdb::put_string(h, x.bytes);
+                w.put(h);
+            } else {
+                x.type = sk_rdb::kTypeHash;
+                x.fields = sk_rdb::bloom_config_fields(r.below(1u << 30), int32_t(1 + r.below(9)), r.below(1u << 30),
+                                                       1.0 / (2 + r.below(1000)));
+                w.record_head(sk_rdb::kTypeHash, key);
+                std::string h;
+                sk_rdb::put_len(h, x.fields.size());
+                for (auto &kv : x.fields) sk_rdb::put_string(h, kv.first), sk_rdb::put_string(h, kv.second);
+                w.put(h);
+            }
+            recs.emplace_back(key, x);
+        }
+        check(w.close(), "rdb close", it);
+        FILE *f = fopen(path, "rb");
+        std::string img;
+        char buf[4096];
+        size_t k;
+        while (f && (k = fread(buf, 1, sizeof buf, f)) > 0) img.append(buf, k);
+        if (f) fclose(f);
+        unlink(path);
+        size_t at = 0;
+        auto parse = [&](const std::string &im) {
+            std::vector<uint8_t> copy(im.begin(), im.end());
+            at = 0;
+            return sk_rdb::parse_rdb(copy.data(), copy.size(), [&](const std::string &key, uint8_t t, sk_rdb::Reader &rd) {
+                sk_rdb::Value x;
+                std::string why = sk_rdb::load_value(rd, t, x);
+                if (!why.empty()) return why;
+                if (at < recs.size() && (recs[at].first != key || recs[at].second.bytes != x.bytes ||
+                                         recs[at].second.fields != x.fields))
+                    return std::string("record differs");
+                at++;
+                return std::string();
+            });
+        };
+        check(parse(img).empty() && at == recs.size(), "RDB file round trip", it);
+        std::string bad = img;
+        mutate(r, bad);
+        (void)parse(bad); // refused or parsed, never a memory error
+    }
+}
+
 int main(int argc, char **argv) {
     const long iters = argc > 1 ? atol(argv[1]) : 20000;
     Rng r{argc > 2 ? strtoull(argv[2], nullptr, 10) : 1};
@@ -317,6 +488,7 @@ int main(int argc, char **argv) {
         fuzz_hll(r, it);
         fuzz_resp(r, it);
         for (int j = 0; j < 8; j++) fuzz_hash(r, it);
+        fuzz_rdb(r, it);
     }
     printf("fuzz_host: %ld iterations, %ld failures\n", iters, g_fail);
     return g_fail ? 1 : 0;

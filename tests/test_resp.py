@@ -101,21 +101,30 @@ def test_server_fails_loudly_without_device():
     assert r.returncode != 0 and "sk_open failed" in r.stderr
 
 
-@pytest.fixture(scope="module")
-def server():
-    p = subprocess.Popen([SERVER, "--port", "0", "--device", "0"], stdout=subprocess.PIPE, stderr=subprocess.PIPE,
-                         text=True)
+def _start(*extra):
+    p = subprocess.Popen([SERVER, "--port", "0", "--device", "0", *extra], stdout=subprocess.PIPE,
+                         stderr=subprocess.PIPE, text=True)
     line = p.stdout.readline()
     if not line.startswith("ready"):
         p.kill()
         raise RuntimeError("server did not start: %s %s" % (line, p.stderr.read()))
-    port = int(line.split(":")[-1])
-    yield port
+    return p, int(line.split(":")[-1])
+
+
+def _stop(p):
     p.terminate()
     try:
         p.wait(30)
     except subprocess.TimeoutExpired:
         p.kill()
+
+
+@pytest.fixture(scope="module")
+def server(tmp_path_factory):
+    # its own --dir: a dump.rdb in the working directory is never loaded (redis-server loads it at startup)
+    p, port = _start("--dir", str(tmp_path_factory.mktemp("resp")))
+    yield port
+    _stop(p)
 
 
 @pytest.fixture()
@@ -263,3 +272,63 @@ def test_resp_protocol(server, cli):
     assert r[:5] == [1, 1, 1, 2, "OK"] and "invalid DB index" in str(r[5])
     assert cli.call("QUIT") == "OK"
     assert cli.s.recv(10) == b""
+
+
+@pytest.mark.gpu
+def test_resp_persistence(tmp_path, O):
+    """SURVEY 8(f) rank 1 / VERDICT r4 item 6 on the wire: KEYS / SCAN (MATCH, COUNT) / DUMP / RESTORE / SAVE, a
+    restart that loads the file (redis-server loads its dump.rdb at startup), and DEBUG RELOAD -- the HLLs, the
+    Bloom filter's bit array and "{name}__config" hash, and a bitset come back identical."""
+    from tests.test_gpu_persist import parse_payload
+
+    p, port = _start("--dir", str(tmp_path), "--dbfilename", "snap.rdb")
+    c = Client(port)
+    try:
+        elems = _jlongs(0x5EED7100, 4000)
+        c.pipeline([["PFADD", "t:%d" % (i % 9), e] for i, e in enumerate(elems)])
+        c.pipeline([["SETBIT", "bs", str(i * 131), "1"] for i in range(500)])
+        assert c.call("EVALSHA", SHA_BLOOM_INIT, 1, "{bf}__config", "729", "5") is None
+        c.call("HMSET", "{bf}__config", "size", "729", "hashIterations", "5", "expectedInsertions", "100",
+               "falseProbability", "0.03")
+        c.pipeline([["SETBIT", "bf", str(i * 7 % 729), "1"] for i in range(300)])
+        keys = {b"t:%d" % i for i in range(9)} | {b"bs", b"bf", b"{bf}__config"}
+        assert set(c.call("KEYS", "*")) == keys
+        assert set(c.call("KEYS", "t:*")) == {b"t:%d" % i for i in range(9)}
+        assert c.call("DBSIZE") == len(keys)
+        seen, cur = [], b"0"
+        while True:
+            cur, part = c.call("SCAN", cur, "COUNT", "2")
+            seen += part
+            if cur == b"0":
+                break
+        assert sorted(seen) == sorted(keys)
+        cur, part = c.call("SCAN", "0", "MATCH", "t:[0-3]", "COUNT", "1000")
+        assert set(part) <= {b"t:0", b"t:1", b"t:2", b"t:3"}
+        before = {k: c.call("DUMP", k) for k in keys}
+        t, f = parse_payload(before[b"{bf}__config"])
+        assert t == 4 and f[0] == (b"size", b"729")
+        gets = {k: c.call("GET", k) for k in keys if not k.startswith(b"{")}
+        counts = c.pipeline([["PFCOUNT", "t:%d" % i] for i in range(9)])
+        assert c.call("RESTORE", "copy", "0", before[b"t:4"]) == "OK"
+        assert c.call("GET", "copy") == gets[b"t:4"]
+        assert "BUSYKEY" in str(c.pipeline([["RESTORE", "copy", "0", before[b"bs"]]])[0])
+        assert c.call("RESTORE", "copy", "0", before[b"bs"], "REPLACE") == "OK"
+        assert c.call("GET", "copy") == gets[b"bs"]
+        assert c.call("RESTORE", "hcopy", "0", before[b"{bf}__config"]) == "OK"
+        assert c.call("HGETALL", "hcopy") == c.call("HGETALL", "{bf}__config")
+        c.call("DEL", "copy", "hcopy")
+        assert c.call("SAVE") == "OK"
+        c.close()
+        _stop(p)
+        p, port = _start("--dir", str(tmp_path), "--dbfilename", "snap.rdb")   # loads snap.rdb
+        c = Client(port)
+        assert set(c.call("KEYS", "*")) == keys
+        assert {k: c.call("DUMP", k) for k in keys} == before
+        assert {k: c.call("GET", k) for k in gets} == gets
+        assert c.pipeline([["PFCOUNT", "t:%d" % i] for i in range(9)]) == counts
+        assert c.call("EVALSHA", SHA_BLOOM_CHECK, 1, "{bf}__config", "729", "5") is None
+        assert c.call("DEBUG", "RELOAD") == "OK"
+        assert {k: c.call("DUMP", k) for k in keys} == before
+    finally:
+        c.close()
+        _stop(p)

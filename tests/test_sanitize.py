@@ -3,7 +3,9 @@
 tests/fuzz/fuzz_host.cpp is built with -fsanitize=address,undefined (no recovery: any report aborts the run) over
 the host-side code that parses caller or network input -- the Redis HLL string codec (sk_hllstr.h: dense / sparse
 decode of random and mutated strings, hllSparseSet replays compared byte for byte with the oracle's), the RESP
-request parser (sk_resp_parse.h: random streams, valid pipelines in random chunks, mutated pipelines) -- and the
+request parser (sk_resp_parse.h: random streams, valid pipelines in random chunks, mutated pipelines), the redis
+persistence formats (sk_rdb.h: CRC64 and the Redis documentation's DUMP example as known answers, LZF, ziplist hashes,
+DUMP payloads and RDB file images round-tripped and mutated) -- and the
 device hash code of sk_device.h compiled for the host (XXH64, farmhashuo, the shared-prefix path, BloomIdx against the
 oracle at every alignment)."""
 import os

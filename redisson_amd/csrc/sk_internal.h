@@ -155,6 +155,12 @@ hipError_t launch_setbit_void(hipStream_t st, uint64_t n, const uint64_t *offs, 
 uint32_t sbv_region_bits();
 hipError_t launch_setbit_void_regions(hipStream_t st, uint64_t n, const uint64_t *keys, uint64_t max_off,
                                       uint32_t *start, uint8_t *buf, uint64_t cap, uint32_t value);
+// dense SETBIT_VOID, hand-written region partition (k_sbv_part -> k_sbv_fine -> k_sbv_runs) in a scratch of
+// sbv_part_scratch_bytes(n, max_off) bytes; sbv_part_ok: the call's size fits the partition's tables
+uint64_t sbv_part_scratch_bytes(uint64_t n, uint64_t max_off);
+bool sbv_part_ok(uint64_t n, uint64_t max_off);
+hipError_t launch_setbit_void_part(hipStream_t st, uint64_t n, const uint64_t *offs, uint64_t max_off, void *scratch,
+                                   uint8_t *buf, uint64_t cap, uint32_t value);
 hipError_t launch_bit_range(hipStream_t st, uint8_t *buf, uint64_t from, uint64_t to, uint32_t value);
 hipError_t launch_max_u64(hipStream_t st, uint64_t n, const uint64_t *v, uint64_t *out);
 hipError_t launch_bitcount(hipStream_t st, const uint8_t *buf, uint64_t len, uint64_t *out);

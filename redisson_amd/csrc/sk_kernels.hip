@@ -3105,6 +3105,216 @@ __global__ void __launch_bounds__(SBV_TPB) k_sbv_apply(const uint64_t *__restric
     for (uint32_t v = threadIdx.x; v < nv; v += SBV_TPB) src[v] = reg4[v];
 }
 
+// Dense SETBIT_VOID without a library sort (r05).  The ops of one value commute, so the apply needs each 32 KiB
+// region's in-region bit offsets in any order, never a sorted op list.  Three passes of u32 records
+// rec = (region % SBV_G) << 18 | bit-in-region, each written once and read once (the rocPRIM radix sort moved the 8-B
+// offsets through two scatter passes and a histogram pass, ~45 % of the streaming rate):
+//   k_sbv_part   per block of SBV_E ops: coarse bucket = region / SBV_G (8 MiB of string), LDS counting sort,
+//                one coalesced chunk per block + S[bucket][block] = start | count << 16, tot[bucket][tile] += count
+//   k_sbv_fine   per (tile of T blocks, bucket): the bucket's segments of the tile sorted by region in LDS and
+//                stored as one piece at pbase[bucket][tile] with its region starts rs[bucket][tile][0..SBV_G]
+//   k_sbv_runs   per region: its run from every tile's piece of its bucket applied to the region staged in LDS
+#define SBV_E 16384   // ops per partition block (1024 threads x 16 in registers)
+#define SBV_PTPB 1024
+#define SBV_PPT (SBV_E / SBV_PTPB)
+#define SBV_G 256     // regions per coarse bucket (record: 8 + 18 bits)
+#define SBV_TMAX 256  // partition blocks per fine-sort tile (a call takes T = NC / 2: E * T / NC = 8 k records per
+                      // (tile, bucket) piece on average, whatever the string's size)
+#define SBV_FCAP 16384 // records a fine-sort workgroup places through LDS (more: placed by atomics, in pieces)
+#define SBV_NCMAX 4096 // coarse buckets (strings <= 2^38 bits)
+#define SBV_NTMAXR 256 // tiles per call
+static_assert(SBV_E <= 65535 && SBV_G * (1u << SBV_RB) <= (1ull << 32), "record and segment packing");
+
+__global__ void __launch_bounds__(SBV_PTPB) k_sbv_part(uint64_t n, const uint64_t *__restrict__ offs, uint32_t NC,
+                                                       uint32_t NB, uint32_t T, uint32_t ntile, uint32_t *__restrict__ chunks,
+                                                       uint32_t *__restrict__ S, uint32_t *__restrict__ tot) {
+    extern __shared__ uint32_t dyn32[];
+    uint32_t *hist = dyn32, *lrec = dyn32 + ((NC + 3) & ~3u);
+    __shared__ uint32_t wsum[SBV_PTPB / 64];
+    const uint32_t blk = blockIdx.x;
+    const uint64_t base = uint64_t(blk) * SBV_E;
+    for (uint32_t b = threadIdx.x; b < NC; b += SBV_PTPB) hist[b] = 0;
+    __syncthreads();
+    uint32_t rec[SBV_PPT], bk[SBV_PPT];
+#pragma unroll
+    for (int q = 0; q < SBV_PPT; q++) {
+        const uint64_t i = base + uint64_t(q) * SBV_PTPB + threadIdx.x;
+        bk[q] = 0xffffffffu;
+        if (i < n) {
+            const uint64_t o = offs[i];
+            const uint32_t r = uint32_t(o >> SBV_RB);
+            rec[q] = ((r % SBV_G) << SBV_RB) | uint32_t(o & ((1u << SBV_RB) - 1u));
+            const uint32_t b = r / SBV_G;
+            bk[q] = b | (atomicAdd(&hist[b], 1u) << 16); // rank < SBV_E
+        }
+    }
+    __syncthreads();
+    // bucket starts: consecutive buckets per thread
+    const uint32_t per = (NC + SBV_PTPB - 1) / SBV_PTPB;
+    uint32_t s4 = 0;
+    for (uint32_t k = 0; k < per; k++) {
+        const uint32_t b = threadIdx.x * per + k;
+        s4 += b < NC ? hist[b] : 0u;
+    }
+    uint32_t total;
+    uint32_t st = block_exscan<SBV_PTPB>(s4, wsum, &total);
+    for (uint32_t k = 0; k < per; k++) {
+        const uint32_t b = threadIdx.x * per + k;
+        if (b < NC) {
+            const uint32_t c = hist[b];
+            hist[b] = st;
+            S[uint64_t(b) * NB + blk] = st | (c << 16);
+            if (c) atomicAdd(&tot[uint64_t(b) * ntile + blk / T], c);
+            st += c;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < SBV_PPT; q++)
+        if (bk[q] != 0xffffffffu) lrec[hist[bk[q] & 0xffffu] + (bk[q] >> 16)] = rec[q];
+    __syncthreads();
+    uint32_t *dst = chunks + base;
+    for (uint32_t t = threadIdx.x; t < total; t += SBV_PTPB) dst[t] = lrec[t];
+}
+
+__global__ void __launch_bounds__(SBV_PTPB) k_sbv_fine(uint32_t NC, uint32_t NB, uint32_t T, uint32_t ntile,
+                                                       const uint32_t *__restrict__ chunks,
+                                                       const uint32_t *__restrict__ S,
+                                                       const uint32_t *__restrict__ tot, uint32_t *__restrict__ pbase,
+                                                       uint32_t *__restrict__ rs, uint32_t *__restrict__ out) {
+    __shared__ uint32_t segp[SBV_TMAX + 1], segs[SBV_TMAX], hist[SBV_G + 1], cur[SBV_G];
+    __shared__ uint32_t sorted[SBV_FCAP];
+    __shared__ uint32_t wsum[SBV_PTPB / 64];
+    const uint32_t t = blockIdx.x, g = blockIdx.y, b0 = t * T;
+    const uint32_t nb = (b0 + T < NB ? b0 + T : NB) - b0;
+    // the piece's base: every record of the tile's earlier blocks, then the tile's records of buckets before g
+    uint32_t acc = 0;
+    for (uint32_t gg = threadIdx.x; gg < g; gg += SBV_PTPB) acc += tot[uint64_t(gg) * ntile + t];
+    uint32_t pre;
+    block_exscan<SBV_PTPB>(acc, wsum, &pre);
+    const uint32_t base = t * T * SBV_E + pre; // < n < 2^32
+    uint32_t len = 0, st0 = 0;
+    if (threadIdx.x < nb) {
+        const uint32_t e = S[uint64_t(g) * NB + b0 + threadIdx.x];
+        st0 = e & 0xffffu;
+        len = e >> 16;
+    }
+    uint32_t m;
+    const uint32_t ex = block_exscan<SBV_PTPB>(len, wsum, &m);
+    if (threadIdx.x < nb) {
+        segp[threadIdx.x] = ex;
+        segs[threadIdx.x] = st0;
+    }
+    if (threadIdx.x == 0) {
+        segp[nb] = m;
+        pbase[uint64_t(g) * ntile + t] = base;
+    }
+    for (uint32_t x = threadIdx.x; x <= SBV_G; x += SBV_PTPB) hist[x] = 0;
+    __syncthreads();
+    auto rec_at = [&](uint32_t x) { // record x of the piece: segment lo with segp[lo] <= x < segp[lo + 1]
+        uint32_t lo = 0, hi = nb;
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (segp[mid] <= x) lo = mid;
+            else hi = mid;
+        }
+        return chunks[uint64_t(b0 + lo) * SBV_E + segs[lo] + (x - segp[lo])];
+    };
+    constexpr int RP = SBV_FCAP / SBV_PTPB;
+    uint32_t rv[RP], rk[RP];
+    const bool small = m <= SBV_FCAP;
+    if (small) {
+#pragma unroll
+        for (int q = 0; q < RP; q++) {
+            const uint32_t x = threadIdx.x + q * SBV_PTPB;
+            if (x < m) {
+                rv[q] = rec_at(x);
+                rk[q] = atomicAdd(&hist[rv[q] >> SBV_RB], 1u);
+            }
+        }
+    } else { // an oversized piece (skew): count first, place by atomics below
+        for (uint32_t x = threadIdx.x; x < m; x += SBV_PTPB) atomicAdd(&hist[rec_at(x) >> SBV_RB], 1u);
+    }
+    __syncthreads();
+    uint32_t tot2;
+    const uint32_t c = threadIdx.x < SBV_G ? hist[threadIdx.x] : 0u;
+    const uint32_t gs = block_exscan<SBV_PTPB>(c, wsum, &tot2);
+    uint32_t *rsp = rs + (uint64_t(g) * ntile + t) * (SBV_G + 1);
+    if (threadIdx.x < SBV_G) {
+        hist[threadIdx.x] = gs;
+        cur[threadIdx.x] = gs;
+        rsp[threadIdx.x] = gs;
+    }
+    if (threadIdx.x == 0) rsp[SBV_G] = m;
+    __syncthreads();
+    if (small) {
+#pragma unroll
+        for (int q = 0; q < RP; q++) {
+            const uint32_t x = threadIdx.x + q * SBV_PTPB;
+            if (x < m) sorted[hist[rv[q] >> SBV_RB] + rk[q]] = rv[q];
+        }
+        __syncthreads();
+        for (uint32_t x = threadIdx.x; x < m; x += SBV_PTPB) out[uint64_t(base) + x] = sorted[x];
+    } else {
+        for (uint32_t x = threadIdx.x; x < m; x += SBV_PTPB) {
+            const uint32_t r = rec_at(x);
+            out[uint64_t(base) + atomicAdd(&cur[r >> SBV_RB], 1u)] = r;
+        }
+    }
+}
+
+// one workgroup per region: its runs (one per tile) of its bucket's pieces, applied to the region in LDS
+__global__ void __launch_bounds__(SBV_TPB) k_sbv_runs(uint32_t ntile, const uint32_t *__restrict__ pbase,
+                                                      const uint32_t *__restrict__ rs,
+                                                      const uint32_t *__restrict__ recs, uint8_t *buf, uint64_t cap,
+                                                      uint32_t value) {
+    constexpr uint32_t RBYTES = 1u << (SBV_RB - 3), NV = RBYTES / 16, VPT = NV / SBV_TPB;
+    __shared__ uint4 reg4[NV];
+    __shared__ uint32_t rlo[SBV_NTMAXR], rn[SBV_NTMAXR + 1];
+    __shared__ uint32_t wsum[SBV_TPB / 64];
+    const uint32_t r = blockIdx.x, g = r / SBV_G, rr = r % SBV_G;
+    uint32_t lo = 0, c = 0;
+    if (threadIdx.x < ntile) {
+        const uint32_t *q = rs + (uint64_t(g) * ntile + threadIdx.x) * (SBV_G + 1) + rr;
+        lo = pbase[uint64_t(g) * ntile + threadIdx.x] + q[0];
+        c = q[1] - q[0];
+    }
+    uint32_t total;
+    const uint32_t ex = block_exscan<SBV_TPB>(c, wsum, &total);
+    if (total == 0) return; // uniform: no op in this region
+    if (threadIdx.x < ntile) {
+        rlo[threadIdx.x] = lo;
+        rn[threadIdx.x] = ex;
+    }
+    if (threadIdx.x == 0) rn[ntile] = total;
+    const uint64_t b0 = uint64_t(r) * RBYTES; // < cap: an op's byte lies in the region
+    uint4 *src = reinterpret_cast<uint4 *>(buf + b0);
+    const uint32_t nv = cap - b0 >= RBYTES ? NV : uint32_t((cap - b0) / 16); // cap is a multiple of 16
+    if (nv == NV) { // a whole region: every load issued before the first LDS store
+        uint4 tv[VPT];
+#pragma unroll
+        for (uint32_t q = 0; q < VPT; q++) tv[q] = src[threadIdx.x + q * SBV_TPB];
+#pragma unroll
+        for (uint32_t q = 0; q < VPT; q++) reg4[threadIdx.x + q * SBV_TPB] = tv[q];
+    } else {
+        for (uint32_t v = threadIdx.x; v < nv; v += SBV_TPB) reg4[v] = src[v];
+    }
+    __syncthreads();
+    uint32_t *w = reinterpret_cast<uint32_t *>(reg4);
+    for (uint32_t i = threadIdx.x; i < total; i += SBV_TPB) {
+        uint32_t t = 0; // the run of record i (ntile <= SBV_NTMAXR: fixed-step search)
+#pragma unroll
+        for (uint32_t step = SBV_NTMAXR / 2; step; step >>= 1)
+            if (t + step < ntile && rn[t + step] <= i) t += step;
+        const uint32_t lb = recs[rlo[t] + (i - rn[t])] & ((1u << SBV_RB) - 1u);
+        const uint32_t byte = lb >> 3, mask = 1u << ((byte & 3u) * 8u + (7u - (lb & 7u))); // bit_word's layout
+        if (value) atomicOr(&w[byte >> 2], mask);
+        else atomicAnd(&w[byte >> 2], ~mask);
+    }
+    __syncthreads();
+    for (uint32_t v = threadIdx.x; v < nv; v += SBV_TPB) src[v] = reg4[v];
+}
+
 // RBitSet.set(from, to) / clear(from, to) (M:RedissonBitSet.java:202-228:
 // one SETBIT_VOID per bit): bits [from, to) of an MSB-first string set to
 // `value`.  One lane per 16-B vector; vectors inside the range are stored
@@ -3974,6 +4184,47 @@ hipError_t launch_setbit_void_regions(hipStream_t st, uint64_t n, const uint64_t
     hipLaunchKernelGGL(k_sbv_starts, dim3(grid_for(n, 256)), dim3(256), 0, st, n, keys, NR, start);
     SK_LAUNCH_CHECK();
     hipLaunchKernelGGL(k_sbv_apply, dim3(NR), dim3(SBV_TPB), 0, st, keys, start, buf, cap, value);
+    SK_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+// dense SETBIT_VOID through the hand-written region partition: scratch = sbv_part_scratch_bytes(n, max_off) bytes
+static void sbv_dims(uint64_t n, uint64_t max_off, uint64_t *NR, uint64_t *NC, uint64_t *NB, uint64_t *T,
+                     uint64_t *ntile) {
+    *NR = (max_off >> SBV_RB) + 1;
+    *NC = (*NR + SBV_G - 1) / SBV_G;
+    *NB = (n + SBV_E - 1) / SBV_E;
+    *T = std::min<uint64_t>(SBV_TMAX, std::max<uint64_t>(1, *NC / 2));
+    *ntile = (*NB + *T - 1) / *T;
+}
+uint64_t sbv_part_scratch_bytes(uint64_t n, uint64_t max_off) {
+    uint64_t NR, NC, NB, T, ntile;
+    sbv_dims(n, max_off, &NR, &NC, &NB, &T, &ntile);
+    return 4 * (2 * NB * SBV_E + NC * NB + NC * ntile * (2 + SBV_G + 1)) + 64;
+}
+bool sbv_part_ok(uint64_t n, uint64_t max_off) {
+    uint64_t NR, NC, NB, T, ntile;
+    sbv_dims(n, max_off, &NR, &NC, &NB, &T, &ntile);
+    return n < (1ull << 32) && NC <= SBV_NCMAX && ntile <= SBV_NTMAXR;
+}
+hipError_t launch_setbit_void_part(hipStream_t st, uint64_t n, const uint64_t *offs, uint64_t max_off, void *scratch,
+                                   uint8_t *buf, uint64_t cap, uint32_t value) {
+    if (!n) return hipSuccess;
+    uint64_t NR_, NC_, NB_, T_, nt_;
+    sbv_dims(n, max_off, &NR_, &NC_, &NB_, &T_, &nt_);
+    const uint32_t NR = uint32_t(NR_), NC = uint32_t(NC_), NB = uint32_t(NB_), T = uint32_t(T_), ntile = uint32_t(nt_);
+    uint32_t *chunks = static_cast<uint32_t *>(scratch), *recs = chunks + uint64_t(NB) * SBV_E;
+    uint32_t *S = recs + uint64_t(NB) * SBV_E, *tot = S + uint64_t(NC) * NB, *pbase = tot + uint64_t(NC) * ntile;
+    uint32_t *rs = pbase + uint64_t(NC) * ntile;
+    hipError_t e = hipMemsetAsync(tot, 0, uint64_t(NC) * ntile * 4, st);
+    if (e != hipSuccess) return e;
+    const size_t lds = (((NC + 3) & ~3u) + SBV_E) * 4;
+    hipLaunchKernelGGL(k_sbv_part, dim3(NB), dim3(SBV_PTPB), lds, st, n, offs, NC, NB, T, ntile, chunks, S, tot);
+    SK_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_sbv_fine, dim3(ntile, NC), dim3(SBV_PTPB), 0, st, NC, NB, T, ntile, chunks, S, tot, pbase, rs,
+                       recs);
+    SK_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_sbv_runs, dim3(NR), dim3(SBV_TPB), 0, st, ntile, pbase, rs, recs, buf, cap, value);
     SK_LAUNCH_CHECK();
     return hipSuccess;
 }

@@ -372,6 +372,7 @@ struct sk_ctx {
     int pfadd_path = 1;         // 0 claim/commit, 1 partition, 2 sorted (SK_PFADD_PATH); dense batches use 2
     bool pfp_direct = true;     // partition path, one element per command: apply writes replies (SK_PFP_DIRECT)
     uint64_t sbv_min = 1u << 20; // SETBIT_VOID batches from which a dense one takes the region path (SK_SBV_MIN)
+    bool sbv_part = true;       // ... through the hand-written partition (SK_SBV_PART=0: the rocPRIM radix sort)
     int claim_all = 1;          // PFADD claim: 1 = every element claims (R0 from the atomic), 0 = load first, claim candidates (SK_PFADD_CLAIM)
     int read_stream = 1;        // async Bloom contains on the read stream st2 (SK_READ_STREAM=0: main stream)
     int bloom_sched = 0;        // contains kernel (SK_BLOOM_SCHED): 0 one element per thread; 1 probe queue, 4/lane; 3 split hash / probe passes
@@ -1245,6 +1246,7 @@ int sk_open(const sk_config *cfg, sk_ctx **out) {
     if (const char *e = getenv("SK_PFADD_PATH")) c->pfadd_path = atoi(e);
     if (const char *e = getenv("SK_PFP_DIRECT")) c->pfp_direct = atoi(e) != 0;
     if (const char *e = getenv("SK_SBV_MIN")) c->sbv_min = strtoull(e, nullptr, 10);
+    if (const char *e = getenv("SK_SBV_PART")) c->sbv_part = atoi(e) != 0;
     if (const char *e = getenv("SK_BLOOM_RC_MIN")) c->bloom_rc_min = strtoull(e, nullptr, 10);
     if (const char *e = getenv("SK_BLOOM_RA_MIN")) c->bloom_ra_min = strtoull(e, nullptr, 10);
     if (const char *e = getenv("SK_HLL_EXACT_STRINGS")) c->hll_exact = atoi(e) != 0;
@@ -2227,7 +2229,14 @@ int sk_setbit_dev(sk_ctx *c, const uint8_t *key, uint64_t len, uint64_t n, const
         // instead of one random atomic per op (k_sbv_apply); same bits, the ops of one value commute
         const unsigned rb = sk::sbv_region_bits(), eb = 64u - unsigned(__builtin_clzll(mx | 1));
         const uint64_t nr = (mx >> rb) + 1; // regions up to the highest op; >= 256 of them to fill the GPU
-        if (n >= c->sbv_min && n < (uint64_t(1) << 32) && n * 64 >= need && nr >= 256) {
+        if (n >= c->sbv_min && n < (uint64_t(1) << 32) && n * 64 >= need && nr >= 256 && c->sbv_part &&
+            sk::sbv_part_ok(n, mx)) { // the hand-written region partition (k_sbv_part / k_sbv_fine / k_sbv_runs)
+            HIPCHK(c, c->keys_b.ensure(sk::sbv_part_scratch_bytes(n, mx)));
+            Prof p_(c, 9);
+            HIPCHK(c, sk::launch_setbit_void_part(c->st, n, d_offsets, mx, c->keys_b.p, c->strs[id].ptr,
+                                                  c->strs[id].cap, value & 1));
+        } else if (n >= c->sbv_min && n < (uint64_t(1) << 32) && n * 64 >= need && nr >= 256) {
+            // the same through a radix sort of the offsets by region (SK_SBV_PART=0, or a call past the tables)
             const uint64_t *keys = d_offsets;
             HIPCHK(c, c->vals_a.ensure((nr + 1) * 4));
             Prof p_(c, 9);

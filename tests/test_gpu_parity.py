@@ -298,6 +298,43 @@ def test_dense_setbit_void_regions(engine):
     assert engine.bitcount(b"dense") == int(np.bitwise_count(want).sum(dtype=np.uint64))
 
 
+@pytest.mark.parametrize("part", ["1", "0"])
+def test_dense_setbit_void_partition_skew(O, part):
+    """The hand-written region partition of dense SETBIT_VOID (k_sbv_part / k_sbv_fine / k_sbv_runs; "0": the
+    rocPRIM radix-sort form it replaced) with 70 % of a 4 M-op call on one 32 KiB region: the fine-sort pieces of
+    that region's bucket overflow the LDS and take the atomic placement; the string ends mid-region; set, then
+    clear; the bytes equal numpy's."""
+    import os
+
+    from redisson_amd import SketchEngine
+
+    os.environ["SK_SBV_PART"] = part
+    try:
+        eng = SketchEngine(device=0, max_batch=8 << 20)
+    finally:
+        del os.environ["SK_SBV_PART"]
+    try:
+        rng = np.random.default_rng(81)
+        nbits = (1 << 28) + 777                       # 1025 regions, 5 coarse buckets, the last region partial
+        n = 4 << 20
+        offs = rng.integers(0, nbits, n).astype(np.uint64)
+        hot = rng.random(n) < 0.7
+        offs[hot] = (np.uint64(3) << np.uint64(18)) + rng.integers(0, 1 << 18, int(hot.sum())).astype(np.uint64)
+        offs[0] = nbits - 1
+        want = np.zeros((nbits + 7) // 8, dtype=np.uint8)
+        for key, val, ops in ((b"skew", 1, offs), (b"skew", 0, offs[::3])):
+            eng.setbit_dev(key, len(ops), eng.to_device(ops), val)
+            m = (np.uint8(1) << (np.uint8(7) - (ops & np.uint64(7)).astype(np.uint8))).astype(np.uint8)
+            if val:
+                np.bitwise_or.at(want, (ops >> np.uint64(3)).astype(np.int64), m)
+            else:
+                np.bitwise_and.at(want, (ops >> np.uint64(3)).astype(np.int64), ~m)
+            assert np.array_equal(np.frombuffer(eng.get(b"skew"), np.uint8), want)
+        assert eng.bitcount(b"skew") == int(np.bitwise_count(want).sum(dtype=np.uint64))
+    finally:
+        eng.close()
+
+
 def test_async_pfadd_and_read_stream(engine, O):
     """Async mode: PFADD batches (one overflowing the in-LDS conflict replay)
     interleaved with Bloom contains on the read stream and Bloom adds; the

@@ -10,8 +10,11 @@
 //     and parsed back exactly, and mutated pipelines;
 //   * the device hash code of redisson_amd/csrc/sk_device.h compiled for the CPU (hipstub/ stands in for the HIP
 //     header): XXH64, farmhashuo, the shared-prefix path bloom_hashes_pre and BloomIdx against the oracle, for keys of
-//     every length 0..200 at every byte alignment, so a wrong hash is caught before any GPU run.
+//     every length 0..200 at every byte alignment, so a wrong hash is caught before any GPU run;
+//   * the Bloom add hash block's per-thread arrays and their index expressions (window bounds, probe indexes, packed
+//     ranks, record layout) for one block at k = 2..PM, against the oracle's probes (fuzz_rc_block).
 // Usage: fuzz_host ITERATIONS SEED.  Exits non-zero on a wrong result; the sanitizers abort on any report.
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <string>
@@ -311,6 +314,102 @@ void fuzz_hash(Rng &r, long it) {
     }
 }
 
+// ------------------------------------------ the add hash block's per-thread indexing on the host
+// k_bloom_rc_hash<true, AEPB> (sk_kernels.hip, "probe p of round e") keeps, per thread, wb[ROUNDS + 1] window bounds
+// read at wb[e + 1] / wb[e + 2], and ix[ROUNDS][PM] / rk[ROUNDS][(PM + 1) / 2] (u16 ranks, two per word, rk[e][p >> 1])
+// across the block's rounds; the round-4 build that faulted held these in a runtime loop.  The same arrays and index
+// expressions run here for one block of AEPB elements (a partial block, ragged round counts, k = 2 a third of the
+// time), under UBSan's array-bounds checks and ASan; the block's records (bit-in-region << 13 | element << 1 | last
+// probe), laid out by the counting sort's segment starts, must be a permutation of the oracle's probes.
+template <uint32_t AEPB, uint32_t PM>
+void fuzz_rc_block(Rng &r, long it) {
+    constexpr uint32_t TPB = 1024, RB = 19;
+    constexpr int ROUNDS = int(AEPB / TPB);
+    const uint32_t P = r.below(3) == 0 ? 2u : 2u + r.below(PM - 1);          // k = 2..PM
+    const uint64_t size = r.below(3) ? 4271038538ull : 1u << 19 | r.below(~0u - (1u << 19));
+    const uint32_t NR = uint32_t((size + (1u << RB) - 1) >> RB);
+    const uint32_t n = r.below(4) == 0 ? AEPB : 1 + r.below(AEPB);          // elements of the block
+    std::vector<std::string> keys(n);
+    std::vector<uint64_t> off(n + 1, 0);
+    for (uint32_t i = 0; i < n; i++) {
+        keys[i] = "[\"java.lang.Long\"," + std::to_string(int64_t(r.next() >> r.below(64))) + "]";
+        off[i + 1] = off[i] + keys[i].size();
+    }
+    const int nr = int(std::min<uint64_t>((n + TPB - 1) / TPB, ROUNDS));
+    uint64_t wb[ROUNDS + 1];
+    for (int e = 0; e <= ROUNDS; e++) {
+        const uint64_t i0 = uint64_t(e) * TPB;
+        wb[e] = off[i0 < n ? i0 : n];
+    }
+    struct Thread {
+        uint32_t ix[ROUNDS][PM], rk[ROUNDS][(PM + 1) / 2];
+    };
+    std::vector<Thread> th(TPB);
+    std::vector<uint32_t> hist(NR, 0);
+    for (int e = 0; e < ROUNDS; e++) {
+        for (uint32_t t = 0; t < TPB; t++) {
+            Thread &T = th[t];
+            for (int q = 0; q < int(PM); q++) T.ix[e][q] = 0;
+            for (int q = 0; q < int(PM + 1) / 2; q++) T.rk[e][q] = 0;
+            if (e >= nr) continue;
+            if (e + 1 < nr) check(wb[e + 1] <= wb[e + 2], "window bounds ordered", it);
+            const uint64_t i = uint64_t(e) * TPB + t;
+            if (i >= n) continue;
+            check(off[i] >= wb[e] && off[i + 1] <= wb[e + 1], "element inside its round's window", it);
+            const uint32_t len = uint32_t(off[i + 1] - off[i]);
+            KeyBuf kb; // the device reads whole words: the key inside zero-padded words, as in the byte arena
+            const uint8_t *kp = kb.put(reinterpret_cast<const uint8_t *>(keys[i].data()), len, uint32_t(off[i] & 7u));
+            sk::BloomIdx32 bi(sk::xxh64(kp, len), sk::farm_uo64(kp, len), size, ~0ull / size);
+            for (int p = 0; p < int(PM); p++) {
+                if (uint32_t(p) >= P) break;
+                const uint32_t idx = uint32_t(bi.r);
+                T.ix[e][p] = idx;
+                const uint32_t rank = hist.at(idx >> RB)++;
+                T.rk[e][p >> 1] |= rank << ((p & 1) * 16);
+                bi.next(p);
+            }
+        }
+    }
+    std::vector<uint32_t> start(NR);
+    uint32_t tot = 0;
+    for (uint32_t q = 0; q < NR; q++) {
+        start[q] = tot;
+        tot += hist[q];
+    }
+    check(tot == n * P, "records == elements x probes", it);
+    std::vector<uint32_t> lrec(AEPB * PM, 0xffffffffu);
+    for (int e = 0; e < ROUNDS; e++)
+        for (uint32_t t = 0; t < TPB; t++) {
+            const uint64_t i = uint64_t(e) * TPB + t;
+            if (e >= nr || i >= n) continue;
+            for (int p = 0; p < int(PM); p++) {
+                if (uint32_t(p) >= P) break;
+                const uint32_t idx = th[t].ix[e][p], rank = (th[t].rk[e][p >> 1] >> ((p & 1) * 16)) & 0xffffu;
+                const uint32_t el = uint32_t(e) * TPB + t;
+                uint32_t &slot = lrec.at(start.at(idx >> RB) + rank);
+                check(slot == 0xffffffffu, "each record slot written once", it);
+                slot = (idx << 13) | (el << 1) | (uint32_t(p) + 1 == P ? 1u : 0u);
+            }
+        }
+    // decode by segment: (global bit, element, last) against the oracle's probes
+    std::vector<uint64_t> got, want;
+    for (uint32_t q = 0; q < NR; q++)
+        for (uint32_t s = start[q]; s < start[q] + hist[q]; s++) {
+            const uint32_t x = lrec[s];
+            got.push_back((uint64_t(q) << RB | (x >> 13)) << 14 | ((x >> 1) & 0xfffu) << 1 | (x & 1u));
+        }
+    int64_t w[16];
+    for (uint32_t i = 0; i < n; i++) {
+        or_bloom_indexes(reinterpret_cast<const uint8_t *>(keys[i].data()), uint32_t(keys[i].size()), int(P),
+                         int64_t(size), w);
+        for (uint32_t p = 0; p < P; p++)
+            want.push_back(uint64_t(w[p]) << 14 | uint64_t(i) << 1 | (p + 1 == P ? 1u : 0u));
+    }
+    std::sort(got.begin(), got.end());
+    std::sort(want.begin(), want.end());
+    check(got == want, "block records == oracle probes", it);
+}
+
 } // namespace
 
 // ---------------------------------------------------------------- redis persistence formats (sk_rdb.h)
@@ -489,6 +588,8 @@ int main(int argc, char **argv) {
         fuzz_resp(r, it);
         for (int j = 0; j < 8; j++) fuzz_hash(r, it);
         fuzz_rdb(r, it);
+        if (it % 40 == 0) fuzz_rc_block<4096, 7>(r, it);   // k <= RA_K4: 4096-element blocks
+        if (it % 40 == 20) fuzz_rc_block<2048, 8>(r, it);  // k = 8
     }
     printf("fuzz_host: %ld iterations, %ld failures\n", iters, g_fail);
     return g_fail ? 1 : 0;

@@ -512,7 +512,7 @@ struct BloomIdx {
 // then C is taken off modulo size.  Only the 63-bit m stays 64-bit.
 struct BloomIdx32 {
     uint64_t m, D1, D2;
-    uint32_t r, A1, A2, C, size;
+    uint32_t r, A1, A2, B1, B2, size; // B = (A - C) mod size: the step when m wraps past 2^63
     __device__ __forceinline__ BloomIdx32(uint64_t h1, uint64_t h2, uint64_t size_, uint64_t magic)
         : size(uint32_t(size_)) {
         const uint64_t MAXL = 0x7fffffffffffffffull;
@@ -521,20 +521,22 @@ struct BloomIdx32 {
         A1 = uint32_t(mod_invariant(D1, size_, magic));
         A2 = uint32_t(mod_invariant(D2, size_, magic));
         uint64_t c = mod_invariant(MAXL, size_, magic) + 1; // 2^63 mod size (uniform)
-        C = c == size_ ? 0u : uint32_t(c);
+        const uint32_t C = c == size_ ? 0u : uint32_t(c);
+        B1 = A1 >= C ? A1 - C : A1 - C + size;
+        B2 = A2 >= C ? A2 - C : A2 - C + size;
         m = D1;
         r = A1;
     }
+    // index += (D mod size) - [m + D >= 2^63] * (2^63 mod size), mod size: one step term chosen by the wrap, then
+    // one conditional subtraction (r + a < 2 * size; the carry out of 32 bits counts too)
     __device__ __forceinline__ void next(int p) {
         const uint64_t D = (p & 1) ? D1 : D2;
-        const uint32_t A = (p & 1) ? A1 : A2;
         const uint64_t s = m + D;
         const bool w = (s >> 63) != 0;
         m = s & 0x7fffffffffffffffull;
-        uint32_t x = r + A;
-        x = (x < r || x >= size) ? x - size : x; // (r + A) mod size
-        const uint32_t c = w ? C : 0u;
-        r = x >= c ? x - c : x - c + size;       // (x - c) mod size
+        const uint32_t a = w ? ((p & 1) ? B1 : B2) : ((p & 1) ? A1 : A2);
+        const uint32_t x = r + a;
+        r = (x < r || x >= size) ? x - size : x;
     }
 };
 

@@ -1921,7 +1921,8 @@ __global__ void __launch_bounds__(256) k_bloom_contains_q(uint64_t n, const uint
 // 8 no hash arithmetic, 16 no segment-table stores, 32 no record stores, 64 no add reply stores; of the add apply:
 // 128 records gathered from one contiguous run, 256 no windows (region and segment table only), 512 no chain walk;
 // 1024: the probe reads each (block, region) segment from a region-major position ((r * NB + j) * CH / NR words,
-// as a region-major record arena would place it: a wave's segments adjacent) -- a timing probe, results discarded
+// as a region-major record arena would place it: a wave's segments adjacent) -- a timing probe, results discarded;
+// of the probe's zero lists: 2048 no word tests, 4096 no scan or list entries, 8192 no list sort or write-back
 #define SK_RC_ABL 0
 #endif
 #ifndef SK_RC_STILE
@@ -2239,11 +2240,26 @@ __device__ __forceinline__ void rc_test_seg(const uint8_t *fb, const uint32_t *c
 #define RC_NG (RC_SMAX * RC_TPB / RC_GB) // reply groups per piece (<= 512)
 #define RC_ZCAP 7424                     // zero-list entries per region (LDS beside the 128 KiB region)
 static_assert((1u << (RC_RB - 3)) >= RC_ZCAP * 4, "the sorted list fits the region area");
+// SK_RC_TV: the probe's word tests without branches, and the wave scan of the zero-hit counts on DPP row shifts and
+// broadcasts (6 adds) instead of six shuffles through LDS
+#ifndef SK_RC_TV
+#define SK_RC_TV 1
+#endif
+// inclusive sum over the 64 lanes of a wave: row_shr 1, 2, 4, 8 inside each row of 16, then row_bcast 15 and 31
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
+    x += uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x111, 0xf, 0xf, false));
+    x += uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x112, 0xf, 0xf, false));
+    x += uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x114, 0xf, 0xf, false));
+    x += uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x118, 0xf, 0xf, false));
+    x += uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x142, 0xa, 0xf, false));
+    x += uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x143, 0xc, 0xf, false));
+    return x;
+}
 // the zero hits of one segment (the words the unrolled test found on 0 bits): the wave's counts are scanned, one
 // lane reserves the wave's slots, and every lane writes its entries; entries past the list's end store directly
 __device__ __forceinline__ void rc_test_seg_zl(const uint8_t *fb, const uint32_t *chunks, uint64_t CH, uint32_t j,
                                                uint32_t seg, const uint4 (&w)[RC_SEGV], uint8_t *out, uint32_t *zl,
-                                               uint32_t *zn) {
+                                               uint32_t *zn, uint32_t *gt_row) {
     const uint32_t st = seg & 0xffffu, cnt = seg >> 16, o = st & 3u;
     constexpr uint32_t NW = 4 * RC_SEGV;
     const uint32_t end = o + cnt < NW ? o + cnt : NW, inreg = end - o;
@@ -2252,6 +2268,23 @@ __device__ __forceinline__ void rc_test_seg_zl(const uint8_t *fb, const uint32_t
         return !((fb[bit >> 3] >> (7u - (bit & 7u))) & 1u);
     };
     uint32_t mask = 0;
+#if SK_RC_ABL & 2048
+    // timing probe: no word tests (the loads stay live; ~1 in 10 records reported zero)
+    (void)end;
+    (void)zero;
+    mask = ((w[0].x ^ w[1].y ^ w[2].z ^ w[3].w) % 10u == 0u ? 1u : 0u) << o;
+#elif SK_RC_TV
+    // every word tested without a branch (a word outside the segment reads some byte of the region: x >> 15 <
+    // 128 Ki), then masked to the segment's words [o, end)
+    auto zb = [&](uint32_t x) { return ((uint32_t(fb[x >> 15]) << ((x >> 12) & 7u)) & 0x80u) ^ 0x80u; };
+#pragma unroll
+    for (int q = 0; q < RC_SEGV; q++) {
+        const uint32_t t = 4u * uint32_t(q);
+        mask |= (zb(w[q].x) | zb(w[q].y) << 1 | zb(w[q].z) << 2 | zb(w[q].w) << 3) >> 7 << t;
+    }
+    mask &= ((1u << end) - 1u) & ~((1u << o) - 1u); // end <= 16
+    (void)zero;
+#else
 #pragma unroll
     for (int q = 0; q < RC_SEGV; q++) {
         const uint32_t t = 4u * uint32_t(q);
@@ -2260,7 +2293,45 @@ __device__ __forceinline__ void rc_test_seg_zl(const uint8_t *fb, const uint32_t
         if (t + 2 >= o && t + 2 < end && zero(w[q].z)) mask |= 4u << t;
         if (t + 3 >= o && t + 3 < end && zero(w[q].w)) mask |= 8u << t;
     }
-    const uint32_t k = __popc(mask), lane = threadIdx.x & 63u;
+#endif
+#if SK_RC_ABL & 4096
+    // timing probe: no zero-list scan or entries (the hits are folded into one word)
+    if (mask == (seg ^ 0x5bd1e995u)) zl[0] = j; // (a condition the compiler cannot fold away)
+    return;
+#endif
+    const uint32_t k = __popc(mask);
+#if SK_RC_TV
+    const uint32_t x = wave_incl_scan(k);
+    // the wave's total (uniform) reserved by lane 0 (every lane of the wave is active here)
+    const uint32_t tot = uint32_t(__builtin_amdgcn_readlane(int(x), 63));
+    uint32_t base = 0;
+    if (tot) {
+        if ((threadIdx.x & 63u) == 0u) base = atomicAdd(zn, tot);
+        base = uint32_t(__builtin_amdgcn_readlane(int(base), 0));
+    }
+    base += x - k;
+    {
+        // the wave's entries are in lane (= block) order and its 64 blocks are 4 whole reply groups (RC_GB = 16), so
+        // each group's entries are one run of the list: GT[region][group] = start | count << 16, clipped at the
+        // list's end (entries past it are stored directly)
+        static_assert(RC_GB == 16, "4 reply groups per wave");
+        const uint32_t lane = threadIdx.x & 63u;
+        const uint32_t g0 = uint32_t(__builtin_amdgcn_readlane(int(base), 0)),
+                       g1 = uint32_t(__builtin_amdgcn_readlane(int(base), 16)),
+                       g2 = uint32_t(__builtin_amdgcn_readlane(int(base), 32)),
+                       g3 = uint32_t(__builtin_amdgcn_readlane(int(base), 48)),
+                       ge = uint32_t(__builtin_amdgcn_readlane(int(base + k), 63));
+        if (lane < 4) {
+            uint32_t a = lane == 0 ? g0 : lane == 1 ? g1 : lane == 2 ? g2 : g3;
+            uint32_t b = lane == 0 ? g1 : lane == 1 ? g2 : lane == 2 ? g3 : ge;
+            a = a < RC_ZCAP ? a : RC_ZCAP;
+            b = b < RC_ZCAP ? b : RC_ZCAP;
+            gt_row[((j - lane) >> 4) + lane] = a | ((b - a) << 16);
+        }
+    }
+#else
+    (void)gt_row;
+    const uint32_t lane = threadIdx.x & 63u;
     uint32_t x = k;
 #pragma unroll
     for (int s2 = 1; s2 < 64; s2 <<= 1) {
@@ -2270,8 +2341,37 @@ __device__ __forceinline__ void rc_test_seg_zl(const uint8_t *fb, const uint32_t
     uint32_t base = 0;
     if (lane == 63 && x) base = atomicAdd(zn, x);
     base = __shfl(base, 63) + (x - k);
+#endif
     const uint32_t e0 = j * RC_EPB;
     uint8_t *ob = out + uint64_t(j) * RC_EPB;
+#if SK_RC_TV
+    if (tot == 0 || uint32_t(__builtin_amdgcn_readlane(int(base + k), 63)) <= RC_ZCAP) {
+        // uniform: all of the wave's entries fit (or there are none).  Every word is written, a hit to its list slot
+        // and a miss to the lane's spare slot past the list: no branches, and the 64 spare slots are distinct words
+        if (tot) {
+            const uint32_t spare = RC_ZCAP + (threadIdx.x & 63u);
+            uint32_t pos = base;
+            auto put1 = [&](uint32_t word, uint32_t t) {
+                const uint32_t hit = (mask >> t) & 1u;
+                zl[hit ? pos : spare] = (e0 & ~0xfffu) | (word & 0xfffu);
+                pos += hit;
+            };
+#pragma unroll
+            for (int q = 0; q < RC_SEGV; q++) {
+                const uint32_t t = 4u * uint32_t(q);
+                put1(w[q].x, t);
+                put1(w[q].y, t + 1);
+                put1(w[q].z, t + 2);
+                put1(w[q].w, t + 3);
+            }
+        }
+        if (cnt > inreg) { // long segment (rare): the rest word by word, direct stores
+            const uint32_t *cs = chunks + uint64_t(j) * CH + st;
+            for (uint32_t s2 = inreg; s2 < cnt; s2++) rc_test(fb, cs[s2], ob);
+        }
+        return;
+    }
+#endif
     auto put = [&](uint32_t word) {
         const uint32_t el = word & 0xfffu;
         if (base < RC_ZCAP) zl[base] = e0 + el;
@@ -2301,11 +2401,14 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_rc_probe(uint32_t NB, uint32_t
     const uint32_t r = rc_region(blockIdx.x, NR);
     if (r >= NR) return; // uniform
 #if SK_RC_ZL
-    __shared__ uint32_t zl[RC_ZCAP];
-    __shared__ uint32_t gcnt[RC_NG];
-    __shared__ uint32_t zn, wsum[RC_TPB / 64];
+    __shared__ uint32_t zl[RC_ZCAP + 64]; // + one spare word per lane (SK_RC_TV)
+    __shared__ uint32_t zn;
     if (threadIdx.x == 0) zn = 0;
+#if !SK_RC_TV
+    __shared__ uint32_t gcnt[RC_NG];
+    __shared__ uint32_t wsum[RC_TPB / 64];
     for (uint32_t g = threadIdx.x; g < RC_NG; g += RC_TPB) gcnt[g] = 0;
+#endif
 #else
     (void)Z;
     (void)GT;
@@ -2318,7 +2421,7 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_rc_probe(uint32_t NB, uint32_t
         for (uint32_t q = 0; q < VPT; q++) { // bytes past the buffer read as 0 (they are past the string)
             uint32_t v = threadIdx.x + q * RC_TPB;
 #if SK_RC_ABL & 4
-            fv[q] = make_uint4(v * 2654435761u, v, ~v, r);
+            fv[q] = make_uint4(~0u, ~((v * 2654435761u) & 0x01010101u), ~0u, ~(r & 0x10u)); // ~1 in 64 bits 0
             (void)src;
 #else
             fv[q] = b0 + uint64_t(v) * 16 < cap_bytes ? ld_nt(src + v) : make_uint4(0, 0, 0, 0);
@@ -2349,13 +2452,22 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_rc_probe(uint32_t NB, uint32_t
                 rc_load_seg(chunks, CH, threadIdx.x + (u + RC_PF - 1) * RC_TPB, seg0[u + RC_PF - 1],
                             w[(u + RC_PF - 1) % RC_PF], r, NB, NR);
 #if SK_RC_ZL
-            rc_test_seg_zl(fb, chunks, CH, threadIdx.x + u * RC_TPB, seg0[u], w[u % RC_PF], out, zl, &zn);
+            rc_test_seg_zl(fb, chunks, CH, threadIdx.x + u * RC_TPB, seg0[u], w[u % RC_PF], out, zl, &zn,
+                           GT + uint64_t(r) * RC_NG);
 #else
             rc_test_seg(fb, chunks, CH, threadIdx.x + u * RC_TPB, seg0[u], w[u % RC_PF], out);
 #endif
         }
     }
-#if SK_RC_ZL
+#if SK_RC_ABL & 8192
+    return; // timing probe: no zero-list sort or write-back
+#endif
+#if SK_RC_ZL && SK_RC_TV
+    __syncthreads(); // every test done: the list is complete, already in reply-group runs (GT written per wave)
+    const uint32_t nz = zn < RC_ZCAP ? zn : RC_ZCAP;
+    uint32_t *zdst = Z + uint64_t(r) * RC_ZCAP;
+    for (uint32_t i = threadIdx.x; i < nz; i += RC_TPB) zdst[i] = zl[i];
+#elif SK_RC_ZL
     __syncthreads(); // every test done: the list is complete and the region area is free
     const uint32_t nz = zn < RC_ZCAP ? zn : RC_ZCAP;
     constexpr uint32_t ZPT = (RC_ZCAP + RC_TPB - 1) / RC_TPB;

@@ -49,7 +49,7 @@ PMC_KERNELS = {"bloom_contains": "sk::k_bloom_contains", "pfadd_claim": "sk::k_p
                "pfp_reply": "sk::k_pfp_reply", "bloom_rc_hash": "sk::k_bloom_rc_hash<false>+sk::k_rc_stranspose",
                "pfl_hash": "sk::k_pfl_hash",
                "pfl_apply": "sk::k_pfl_fill+sk::k_pfl_plan+sk::k_pfl_apply", "pfl_part": "sk::k_pfl_tot+sk::k_pfl_region",
-               "bloom_rc_probe": "sk::k_bloom_rc_probe+sk::k_bloom_rc_zero"}
+               "bloom_rc_probe": "sk::k_bloom_rc_probe_p|sk::k_bloom_rc_probe+sk::k_bloom_rc_zero"}
 PHASES = HLL_KERNELS + ["pfadd_sort"] + BLOOM_KERNELS + CHAINS
 
 
@@ -419,7 +419,14 @@ def per_unit_bytes(mean_len_h, mean_len_b, k, size, CB, nr, tenants, group):
 
 
 def _summary_find(ks, k_):
-    """a kernel's entry in a summary; template kernels may carry more arguments in newer builds"""
+    """a kernel's entry in a summary; template kernels may carry more arguments in newer builds; "a|b": the first of
+    the alternatives the summary has (a kernel replaced by another form)"""
+    if "|" in k_:
+        for alt in k_.split("|"):
+            d = _summary_find(ks, alt)
+            if d:
+                return d
+        return None
     if k_ in ks:
         return ks[k_]
     stem = k_[:-1] + "," if k_.endswith(">") else k_ + "<"   # or a kernel that became a template

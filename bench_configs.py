@@ -266,7 +266,7 @@ def c5(eng, args):
           "setbit_cold_first_call_per_s": m0 / t_cold,
           "setbit_cold": "one %d-op call on a missing key: the 2 GiB string's creation and growth timed inside it" % m0,
           "setbit": "SETBIT_VOID (RBitSet.set(i)) in 64 M-op calls on the full-length string (created untimed); a dense "
-                    "call (>= 2 ops per 128-B line) takes the region path (radix sort by 32 KiB region + k_sbv_apply)",
+                    "call (>= 2 ops per 128-B line) takes the region path (partition by 32 KiB region: k_sbv_part + k_sbv_fine + k_sbv_runs)",
           "bitcount_GBps": nbytes / t_bc / 1e9, "bitop_and4_GBps": 5 * nbytes / t_and / 1e9,
           "bitop_or2_GBps": 3 * nbytes / t_or / 1e9,
           "device_GBps": {"bitcount": gbps(nbytes, d_bc), "bitop_and4": gbps(5 * nbytes, d_and),

@@ -2512,15 +2512,24 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_rc_probe(uint32_t NB, uint32_t
 #define SK_RC_PERSIST 1
 #endif
 #define RC_PSLOTS 32 // workgroups per XCD group (8 x 32 = 256 = one per CU)
-__global__ void __launch_bounds__(RC_TPB) k_bloom_rc_probe_p(uint32_t NB, uint32_t NR, const uint32_t *__restrict__ S,
-                                                             const uint32_t *__restrict__ chunks, uint32_t P,
-                                                             const uint8_t *__restrict__ bits, uint64_t cap_bytes,
-                                                             uint8_t *__restrict__ out, uint32_t *__restrict__ Z,
-                                                             uint32_t *__restrict__ GT) {
+#ifndef RC_PTPB
+#define RC_PTPB 1024 // threads per workgroup
+#endif
+#ifndef RC_PRING
+#define RC_PRING 2   // segment-vector sets in flight (3 at 512 threads)
+#endif
+// TPB threads (1024: 128 registers per lane, a ring of two; 512: 256 registers, a ring of three) per workgroup
+template <uint32_t TPB, int RING>
+__global__ void __launch_bounds__(TPB) k_bloom_rc_probe_p(uint32_t NB, uint32_t NR, const uint32_t *__restrict__ S,
+                                                          const uint32_t *__restrict__ chunks, uint32_t P,
+                                                          const uint8_t *__restrict__ bits, uint64_t cap_bytes,
+                                                          uint8_t *__restrict__ out, uint32_t *__restrict__ Z,
+                                                          uint32_t *__restrict__ GT) {
+    static_assert(RING == 2 || RING == 3, "segment-vector sets in flight");
     __shared__ uint4 filt[(1u << (RC_RB - 3)) / 16];
     __shared__ uint32_t zl[RC_ZCAP + 64]; // + one spare word per lane
     __shared__ uint32_t zn;
-    constexpr uint32_t NV = (1u << (RC_RB - 3)) / 16, VPT = NV / RC_TPB;
+    constexpr uint32_t NV = (1u << (RC_RB - 3)) / 16, VPT = NV / TPB;
     // XCD group x = blockIdx % 8 owns regions [x*q, (x+1)*q); its nslot workgroups take them interleaved, so the
     // ~32 regions an XCD works on at once are neighbours (their segments share lines of the block chunks)
     const uint32_t xg = blockIdx.x & 7u, slot = blockIdx.x >> 3, nslot = gridDim.x >> 3, q = (NR + 7) / 8;
@@ -2536,7 +2545,7 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_rc_probe_p(uint32_t NB, uint32
         const uint4 *src = reinterpret_cast<const uint4 *>(bits + b0);
 #pragma unroll
         for (uint32_t q2 = 0; q2 < VPT; q2++) { // bytes past the buffer read as 0 (they are past the string)
-            const uint32_t v = threadIdx.x + q2 * RC_TPB;
+            const uint32_t v = threadIdx.x + q2 * TPB;
             fv[q2] = b0 + uint64_t(v) * 16 < cap_bytes ? ld_nt(src + v) : make_uint4(0, 0, 0, 0);
         }
     };
@@ -2544,38 +2553,65 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_rc_probe_p(uint32_t NB, uint32
     if (threadIdx.x == 0) zn = 0;
     const uint64_t CH = uint64_t(RC_EPB) * P;
     const uint8_t *fb = reinterpret_cast<const uint8_t *>(filt);
-    const uint32_t nsteps = (NB + RC_TPB - 1) / RC_TPB; // NB <= RC_SMAX * RC_TPB
+    const uint32_t nsteps = (NB + TPB - 1) / TPB; // NB <= RC_SMAX * RC_TPB
     for (uint32_t i = 0; r < NR; i++) {
         const uint32_t *Srow = S + uint64_t(r) * NB;
         auto seg_of = [&](uint32_t u) -> uint32_t { // this thread's segment-table word of step u (0 past the end)
-            const uint32_t j = threadIdx.x + u * RC_TPB;
+            const uint32_t j = threadIdx.x + u * TPB;
             return u < nsteps && j < NB ? Srow[j] : 0u;
         };
-        uint32_t sc = seg_of(0), sn = seg_of(1);
+        auto ld = [&](uint32_t u, uint32_t sg, uint4 (&w)[RC_SEGV]) { // sg = 0 past the end: nothing read
+            rc_load_seg(chunks, CH, threadIdx.x + u * TPB, sg, w);
+        };
+        uint32_t *gt = GT + uint64_t(r) * RC_NG;
+        auto test = [&](uint32_t u, uint32_t sg, const uint4 (&w)[RC_SEGV]) {
+            if (u < nsteps) // uniform
+                rc_test_seg_zl(fb, chunks, CH, threadIdx.x + u * TPB, sg, w, out, zl, &zn, gt);
+        };
         uint4 wa[RC_SEGV], wb[RC_SEGV];
-        rc_load_seg(chunks, CH, threadIdx.x, sc, wa);
+        uint32_t sa = seg_of(0), sb = seg_of(1);
+        ld(0, sa, wa);
+        if constexpr (RING == 3) ld(1, sb, wb);
 #pragma unroll
-        for (uint32_t q2 = 0; q2 < VPT; q2++) filt[threadIdx.x + q2 * RC_TPB] = fv[q2];
+        for (uint32_t q2 = 0; q2 < VPT; q2++) filt[threadIdx.x + q2 * TPB] = fv[q2];
         const uint32_t rn = region(i + 1);
         if (rn < NR) load_bits(rn); // uniform: in flight while this region is tested
         __syncthreads();            // the region's bits staged; the list empty
-        uint32_t *gt = GT + uint64_t(r) * RC_NG;
+        if constexpr (RING == 2) {
 #pragma unroll 1
-        for (uint32_t u = 0; u < nsteps; u += 2) {
-            const uint32_t s2 = seg_of(u + 2);
-            rc_load_seg(chunks, CH, threadIdx.x + (u + 1) * RC_TPB, sn, wb); // sn = 0 past the end: nothing read
-            rc_test_seg_zl(fb, chunks, CH, threadIdx.x + u * RC_TPB, sc, wa, out, zl, &zn, gt);
-            const uint32_t s3 = seg_of(u + 3);
-            rc_load_seg(chunks, CH, threadIdx.x + (u + 2) * RC_TPB, s2, wa);
-            if (u + 1 < nsteps) // uniform
-                rc_test_seg_zl(fb, chunks, CH, threadIdx.x + (u + 1) * RC_TPB, sn, wb, out, zl, &zn, gt);
-            sc = s2;
-            sn = s3;
+            for (uint32_t u = 0; u < nsteps; u += 2) { // step u from wa, u + 1 from wb; loads one step ahead
+                const uint32_t s2 = seg_of(u + 2);
+                ld(u + 1, sb, wb);
+                test(u, sa, wa);
+                const uint32_t s3 = seg_of(u + 3);
+                ld(u + 2, s2, wa);
+                test(u + 1, sb, wb);
+                sa = s2;
+                sb = s3;
+            }
+        } else {
+            uint4 wc[RC_SEGV];
+            uint32_t sc = seg_of(2);
+#pragma unroll 1
+            for (uint32_t u = 0; u < nsteps; u += 3) { // steps u, u + 1, u + 2 from wa, wb, wc; loads two ahead
+                const uint32_t s3 = seg_of(u + 3);
+                ld(u + 2, sc, wc);
+                test(u, sa, wa);
+                const uint32_t s4 = seg_of(u + 4);
+                ld(u + 3, s3, wa);
+                test(u + 1, sb, wb);
+                const uint32_t s5 = seg_of(u + 5);
+                ld(u + 4, s4, wb);
+                test(u + 2, sc, wc);
+                sa = s3;
+                sb = s4;
+                sc = s5;
+            }
         }
         __syncthreads(); // every test done: the list complete (in reply-group runs), the bits free
         const uint32_t nz = zn < RC_ZCAP ? zn : RC_ZCAP;
         uint32_t *zdst = Z + uint64_t(r) * RC_ZCAP;
-        for (uint32_t t = threadIdx.x; t < nz; t += RC_TPB) zdst[t] = zl[t];
+        for (uint32_t t = threadIdx.x; t < nz; t += TPB) zdst[t] = zl[t];
         __syncthreads(); // every thread has read zn and the list
         if (threadIdx.x == 0) zn = 0;
         r = rn;
@@ -4277,8 +4313,8 @@ hipError_t launch_bloom_rc_probe(hipStream_t st, uint64_t n, uint64_t size, int 
     uint32_t NR = rc_regions(size), NB = rc_blocks(n);
 #if SK_RC_ZL && SK_RC_TV && SK_RC_PERSIST
     const uint32_t slots = std::min<uint32_t>(RC_PSLOTS, (NR + 7) / 8); // workgroups per XCD group
-    hipLaunchKernelGGL(k_bloom_rc_probe_p, dim3(8 * slots), dim3(RC_TPB), 0, st, NB, NR, S, recs, uint32_t(k - 1),
-                       bits, cap_bytes, out, Z, GT);
+    hipLaunchKernelGGL((k_bloom_rc_probe_p<RC_PTPB, RC_PRING>), dim3(8 * slots), dim3(RC_PTPB), 0, st, NB, NR, S,
+                       recs, uint32_t(k - 1), bits, cap_bytes, out, Z, GT);
 #else
     hipLaunchKernelGGL(k_bloom_rc_probe, dim3(8 * ((NR + 7) / 8)), dim3(RC_TPB), 0, st, NB, NR, S, recs,
                        uint32_t(k - 1), bits, cap_bytes, out, Z, GT);

@@ -1922,7 +1922,8 @@ __global__ void __launch_bounds__(256) k_bloom_contains_q(uint64_t n, const uint
 // 128 records gathered from one contiguous run, 256 no windows (region and segment table only), 512 no chain walk;
 // 1024: the probe reads each (block, region) segment from a region-major position ((r * NB + j) * CH / NR words,
 // as a region-major record arena would place it: a wave's segments adjacent) -- a timing probe, results discarded;
-// of the probe's zero lists: 2048 no word tests, 4096 no scan or list entries, 8192 no list sort or write-back
+// of the probe's zero lists: 2048 no word tests, 4096 no scan or list entries, 8192 no list sort or write-back;
+// of the hash: 16384 no per-round barrier
 #define SK_RC_ABL 0
 #endif
 #ifndef SK_RC_STILE
@@ -2071,7 +2072,9 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_rc_hash(uint64_t n, const uint
             }
         }
         if (pre) pfp_win_store(wb[e + 1], wb[e + 2], v, win[(e + 1) & 1]);
+#if !(SK_RC_ABL & 16384) // timing probe: no per-round barrier (keys read from a window that may not be staged)
         __syncthreads(); // window e+1 staged; window e free for round e+2
+#endif
     }
     // segment starts: RPT consecutive regions per thread
     uint32_t c4[RPT], s4 = 0;

@@ -378,9 +378,11 @@ def main():
                      "valu_frac": valu,
                      "note": "frac = PMC bytes of the chain per launch / avg_launch_ms / 8 TB/s.  avg_launch_ms = HIP "
                              "events around each launch of the chain on its stream inside the timed region (PFADD: "
-                             "the per-batch period); valu_frac = SQ_ACTIVE_INST_VALU / (SIMDs x dispatch cycles) of "
-                             "the chain's longest kernel from the newest profiles/*_sq_summary.json (that kernel is "
-                             "VALU-bound, not HBM-bound); line-level bytes per kernel: DESIGN.md kernel table"},
+                             "the per-batch period); valu_frac = SQ_ACTIVE_INST_VALU x 4 cycles / (SIMDs x dispatch "
+                             "cycles) of the chain's longest kernel from the newest profiles/*_sq_summary.json: an "
+                             "upper bound on its VALU busy share, since gfx950 issues a wave64 integer add in 2 cycles "
+                             "and a 32-bit multiply in ~3.5 (profiles/r05_mulrate.log); line-level bytes per kernel: "
+                             "DESIGN.md kernel table"},
         "kernels": kernels,
         "chains": chains,
         "cpu_baseline": cpu,

@@ -1934,6 +1934,21 @@ __global__ void __launch_bounds__(256) k_bloom_contains_q(uint64_t n, const uint
 // interleaved table cost the probe 0.15 ms).  1: the hash writes the rows itself, no transpose.
 #define SK_RC_STILE 32
 #endif
+#ifndef SK_RC_STAMP
+#define SK_RC_STAMP 0 // dev: s_memtime stamps of the contains hash blocks' phases (thread 0 of each block)
+#endif
+#if SK_RC_STAMP
+__device__ unsigned long long sk_rc_stamps[8192 * 8];
+#define RC_STAMP(k)                                                                                                    \
+    do {                                                                                                               \
+        if (!ADD && threadIdx.x == 0 && jb < 8192) sk_rc_stamps[jb * 8 + (k)] = __builtin_amdgcn_s_memtime();          \
+    } while (0)
+extern "C" hipError_t sk_rc_stamp_read(unsigned long long *out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(sk_rc_stamps), sizeof(sk_rc_stamps), 0, hipMemcpyDeviceToHost);
+}
+#else
+#define RC_STAMP(k) do { } while (0)
+#endif
 __host__ __device__ __forceinline__ uint64_t rc_sidx(uint32_t r, uint32_t j, uint32_t NB) {
     return (uint64_t(r / SK_RC_STILE) * NB + j) * SK_RC_STILE + (r % SK_RC_STILE);
 }
@@ -1981,6 +1996,7 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_rc_hash(uint64_t n, const uint
     // once write neighbouring words of each region's row of S and those lines fill in its L2
     const uint32_t jq = (NB + 7) / 8, jb = (blockIdx.x & 7u) * jq + (blockIdx.x >> 3);
     if (jb >= NB) return; // uniform
+    RC_STAMP(0);
     __shared__ uint32_t wsum[RC_TPB / 64];
     __shared__ uint64_t buf[ra_bufw(EPB, PM)]; // two key windows, then the block's records (EPB x PM u32)
     uint64_t *win[2] = {buf, buf + SK_PFP_WIN};
@@ -2012,6 +2028,7 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_rc_hash(uint64_t n, const uint
         pfp_win_store(wb[0], wb[1], v, win[0]);
     }
     __syncthreads(); // hist zeroed, window 0 staged
+    RC_STAMP(1);
 #if SK_BLOOM_PRE
     // the block's first element's 16 leading bytes: the shared-prefix pattern (bloom_hashes_pre)
     const BloomPre bpre = fit0 ? bloom_pre(LdsReader{win[0], uint32_t(wb[0] & 15u)}.u64(0),
@@ -2076,6 +2093,7 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_rc_hash(uint64_t n, const uint
         __syncthreads(); // window e+1 staged; window e free for round e+2
 #endif
     }
+    RC_STAMP(2);
     // segment starts: RPT consecutive regions per thread
     uint32_t c4[RPT], s4 = 0;
 #pragma unroll
@@ -2097,6 +2115,7 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_rc_hash(uint64_t n, const uint
         st += c4[q];
     }
     __syncthreads();
+    RC_STAMP(3);
 #pragma unroll
     for (int e = 0; e < ROUNDS; e++) {
         uint64_t i = base + uint64_t(e) * RC_TPB + threadIdx.x;
@@ -2111,10 +2130,12 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_rc_hash(uint64_t n, const uint
         }
     }
     __syncthreads();
+    RC_STAMP(4);
     uint4 *dst = reinterpret_cast<uint4 *>(chunks + uint64_t(jb) * EPB * P);
     const uint4 *src = reinterpret_cast<const uint4 *>(lrec);
     if (!(SK_RC_ABL & 32) || ADD)
         for (uint32_t t = threadIdx.x; t < (tot + 3) / 4; t += RC_TPB) dst[t] = src[t];
+    RC_STAMP(5);
 }
 
 // St (interleaved by SK_RC_STILE regions) -> S (region-major rows): one 128 x T tile of (block, region) entries per

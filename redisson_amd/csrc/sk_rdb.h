@@ -16,6 +16,8 @@
 #include <utility>
 #include <vector>
 
+#include <unistd.h>
+
 namespace sk_rdb {
 
 constexpr uint8_t kTypeString = 0, kTypeHash = 4, kTypeHashZiplist = 13;
@@ -316,13 +318,17 @@ inline std::string load_payload(const uint8_t *p, uint64_t n, Value &v) {
 }
 
 // ---------------------------------------------------------------- RDB file writer: streamed, CRC kept running
+// Written to "<path>.tmp-<pid>", flushed to disk, then renamed over <path> (as redis-server's rdbSave does), so a
+// failed or interrupted SAVE never leaves a torn file at <path>; the temporary is removed on failure.
 struct FileWriter {
     FILE *f = nullptr;
     uint64_t crc = 0;
     bool ok = true;
-    std::string buf;
+    std::string buf, final_path, tmp_path;
     bool open(const char *path) {
-        f = std::fopen(path, "wb");
+        final_path = path;
+        tmp_path = final_path + ".tmp-" + std::to_string(long(getpid()));
+        f = std::fopen(tmp_path.c_str(), "wb");
         if (!f) return ok = false;
         buf.reserve(1 << 20);
         put(reinterpret_cast<const uint8_t *>("REDIS0007"), 9);
@@ -360,12 +366,18 @@ struct FileWriter {
         uint8_t c8[8];
         for (int i = 0; i < 8; i++) c8[i] = uint8_t(crc >> (8 * i));
         if (std::fwrite(c8, 1, 8, f) != 8) ok = false;
+        if (std::fflush(f) != 0 || fsync(fileno(f)) != 0) ok = false;
         if (std::fclose(f) != 0) ok = false;
         f = nullptr;
+        if (ok && std::rename(tmp_path.c_str(), final_path.c_str()) != 0) ok = false;
+        if (!ok) std::remove(tmp_path.c_str());
         return ok;
     }
-    ~FileWriter() {
-        if (f) std::fclose(f);
+    ~FileWriter() { // abandoned (an error before close): no file at the path, no temporary left
+        if (f) {
+            std::fclose(f);
+            std::remove(tmp_path.c_str());
+        }
     }
 };
 

@@ -551,6 +551,19 @@ void fuzz_rdb(Rng &r, long it) {
             recs.emplace_back(key, x);
         }
         check(w.close(), "rdb close", it);
+        check(access(w.tmp_path.c_str(), F_OK) != 0, "rdb temporary renamed away", it);
+        {   // an abandoned writer (an error before close) leaves neither its temporary nor a file at its path
+            const std::string gone = std::string(path) + ".abandoned";
+            std::string tmp;
+            {
+                sk_rdb::FileWriter a;
+                check(a.open(gone.c_str()), "rdb open (abandoned)", it);
+                a.put(reinterpret_cast<const uint8_t *>("x"), 1);
+                tmp = a.tmp_path;
+            }
+            check(access(tmp.c_str(), F_OK) != 0 && access(gone.c_str(), F_OK) != 0, "abandoned rdb leaves nothing",
+                  it);
+        }
         FILE *f = fopen(path, "rb");
         std::string img;
         char buf[4096];

@@ -63,7 +63,7 @@ bool pfl_dims_ok(const PflDims &d);
 uint32_t pfl_max_slabs();
 hipError_t launch_pfl_hash(hipStream_t st, uint64_t n, const uint32_t *key_ids, const uint64_t *off,
                            const uint8_t *bytes, int v5, uint64_t *chunks, uint32_t *S, uint32_t *big_alloc);
-// region totals + region sort; C u32[c_words], rec2 u64[n]; dropped records (slab >= nslab) reply 0 in changed
+// region totals + region sort; C u32[c_words], rec2 u64[nblk * SK_PFP_EPB] (u64 records or the 6-B planes); dropped records (slab >= nslab) reply 0 in changed
 hipError_t launch_pfl_part(hipStream_t st, const PflDims &d, const uint64_t *chunks, const uint32_t *S, uint32_t *C,
                            uint64_t *rec2, uint8_t *changed);
 // replies pre-filled with the call's default reply (rc: u32[32] reply-mix counters, par: this call's parity)

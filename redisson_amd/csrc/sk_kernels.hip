@@ -374,6 +374,36 @@ __device__ __forceinline__ uint32_t pfl_slotb(uint64_t key) { // key = slab_low 
     return uint32_t(key >> 14) << SK_PFL_LB | (uint32_t(key) & ((1u << SK_PFL_LB) - 1));
 }
 
+#ifndef SK_PFL_C6
+#define SK_PFL_C6 0        // the line hash's block chunks as 6-B records too: measured slower (region pass 0.35 -> 0.445 ms)
+#endif
+// k_pfl_hash's records: slab << 32 | reg << 18 | rho << 12 | element-in-block, read back by the region pass with
+// reg's line bits zero in the 6-B form (the coarse bucket and the slab fix them).  6-B form: a u32 plane of the
+// low 32 bits with slab_low7 in bits 25..31, and a u16 plane of slab >> 7 (slab ids >= 2^23 kept as 2^23 - 1, which
+// is past every store's slab count, so those records are still dropped).
+struct PflChunk {
+    uint64_t *p;
+    uint64_t cap; // records: hash blocks x SK_PFP_EPB
+    __device__ __forceinline__ void put(uint64_t i, uint64_t r) const {
+        if (SK_PFL_C6) {
+            uint32_t slab = uint32_t(r >> 32);
+            slab = slab < (1u << 23) ? slab : (1u << 23) - 1u;
+            reinterpret_cast<uint32_t *>(p)[i] = (slab << 25) | (uint32_t(r) & ((1u << 25) - 1u));
+            reinterpret_cast<uint16_t *>(reinterpret_cast<uint32_t *>(p) + cap)[i] = uint16_t(slab >> 7);
+        } else {
+            p[i] = r;
+        }
+    }
+    __device__ __forceinline__ uint64_t get(uint64_t i) const {
+        if (SK_PFL_C6) {
+            const uint32_t lo = reinterpret_cast<const uint32_t *>(p)[i];
+            const uint32_t hi = reinterpret_cast<const uint16_t *>(reinterpret_cast<const uint32_t *>(p) + cap)[i];
+            return (uint64_t((hi << 7) | (lo >> 25)) << 32) | (lo & ((1u << 25) - 1u));
+        }
+        return p[i];
+    }
+};
+
 // NBK buckets; LINE = false: the partition path (records slot << 26 | seq << 6 | rho, pfp_bucket),
 // LINE = true: the line schedule (records slab << 32 | reg << 18 | rho << 12 | element-in-block, pfl_bucket)
 template <int NBK, bool LINE>
@@ -471,6 +501,11 @@ __device__ __forceinline__ void pfp_hash_impl(uint64_t n, const uint32_t *__rest
             if (pos) pos[base + uint64_t(e) * SK_PFP_TPB + threadIdx.x] = uint16_t(p);
         }
     __syncthreads();
+    if (LINE && SK_PFL_C6) {
+        const PflChunk ch{chunks, uint64_t(nblocks) * SK_PFP_EPB};
+        for (uint32_t t = threadIdx.x; t < tot; t += SK_PFP_TPB) ch.put(base + t, lrec[t]);
+        return;
+    }
     uint64_t *dst = chunks + base;
     for (uint32_t t = threadIdx.x; t < tot; t += SK_PFP_TPB) dst[t] = lrec[t];
 }
@@ -898,7 +933,7 @@ __global__ void __launch_bounds__(SK_PFP_ATPB) __attribute__((amdgpu_waves_per_e
 //   k_pfl_region   one workgroup per region: its segments into registers, counting-sorted in LDS by fine bucket
 //                  (b, p >> sh), written back as ONE contiguous region of rec2 (tile-major runs: region (b, t) holds
 //                  the runs (b, t, fine bucket) back to back) plus the region's fine-bucket starts C2[region][sub]
-//                  rec2 = slab_low << 46 | reg << 32 | rho << 26 | seq (26 bits)
+//                  rec2 = slab_low << 46 | reg << 32 | rho << 26 | seq (26 bits), stored as 6 B (PflRec)
 //   k_pfl_fill     replies pre-filled with the call's default (the majority reply of the previous call)
 //   k_pfl_apply    one workgroup per fine bucket: its 2^sh lines (one per sketch, 16 KiB) into LDS with its
 //                  records (one run per tile), the records chained per register in LDS, the sequential replies (rho
@@ -942,6 +977,36 @@ __global__ void __launch_bounds__(SK_PFP_ATPB) __attribute__((amdgpu_waves_per_e
 #ifndef SK_PFL_LDS
 #define SK_PFL_LDS (160 * 1024 - 9 * 1024) // dynamic LDS of a region workgroup: records + fine-bucket counts
 #endif
+#ifndef SK_PFL_R6
+#define SK_PFL_R6 1        // rec2 as 6-B records: a u32 plane (rho << 26 | seq) and a u16 plane (slab_low << 7 |
+                           // register in its line) instead of one u64 (SK_PFL_R6=0)
+#endif
+// rec2 record slot i.  The region pass writes the records sorted; the apply reads them back as the u64
+// slab_low << 46 | reg << 32 | rho << 26 | seq, with reg's line bits zero in the 6-B form (a fine bucket holds one
+// line of each of its sketches, so slab_low and the register's place in its line name the register).  The buffer
+// holds u64[cap] either way: the 6-B form keeps the u32 plane at [0, 4 cap) bytes and the u16 plane after it.
+struct PflRec {
+    uint64_t *p;
+    uint64_t cap; // records the planes hold (the call's hash blocks x SK_PFP_EPB)
+    __device__ __forceinline__ void put(uint64_t i, uint64_t r) const {
+        if (SK_PFL_R6) {
+            reinterpret_cast<uint32_t *>(p)[i] = uint32_t(r);
+            reinterpret_cast<uint16_t *>(reinterpret_cast<uint32_t *>(p) + cap)[i] =
+                uint16_t((uint32_t(r >> 46) << SK_PFL_LB) | (uint32_t(r >> 32) & ((1u << SK_PFL_LB) - 1)));
+        } else {
+            p[i] = r;
+        }
+    }
+    __device__ __forceinline__ uint64_t get(uint64_t i) const {
+        if (SK_PFL_R6) {
+            const uint32_t lo = reinterpret_cast<const uint32_t *>(p)[i];
+            const uint32_t hi = reinterpret_cast<const uint16_t *>(reinterpret_cast<const uint32_t *>(p) + cap)[i];
+            return (uint64_t(hi >> SK_PFL_LB) << 46) | (uint64_t(hi & ((1u << SK_PFL_LB) - 1)) << 32) | lo;
+        }
+        return p[i];
+    }
+};
+static_assert(SK_PFL_SH + SK_PFL_LB <= 16, "6-B records: slab_low and the register in its line fit 16 bits");
 __device__ __forceinline__ uint32_t pfl_ht(uint64_t key) {
     static_assert((SK_PFL_HT & (SK_PFL_HT - 1)) == 0, "power-of-two chain heads");
     return uint32_t((key * 0xC2B2AE3D27D4EB4Full) >> (64 - __builtin_ctz(SK_PFL_HT)));
@@ -971,7 +1036,7 @@ __global__ void __launch_bounds__(256) k_pfl_tot(const uint32_t *__restrict__ S,
 }
 
 // The region's record x: segment lo with segp[lo] <= x < segp[lo + 1] (binary search over the tile's prefix)
-__device__ __forceinline__ uint64_t pfl_region_rec(const uint64_t *__restrict__ chunks, const uint32_t *segp,
+__device__ __forceinline__ uint64_t pfl_region_rec(const PflChunk chunks, const uint32_t *segp,
                                                    const uint32_t *segs, uint32_t nb, uint32_t b0, uint32_t x,
                                                    uint32_t *blk) {
     uint32_t lo = 0, hi = nb;
@@ -981,7 +1046,7 @@ __device__ __forceinline__ uint64_t pfl_region_rec(const uint64_t *__restrict__ 
         else hi = mid;
     }
     *blk = b0 + lo;
-    return chunks[uint64_t(b0 + lo) * SK_PFP_EPB + segs[lo] + (x - segp[lo])];
+    return chunks.get(uint64_t(b0 + lo) * SK_PFP_EPB + segs[lo] + (x - segp[lo]));
 }
 
 // One workgroup per region g = b * ntile + t.  Dynamic LDS: cap records (u64) + nsub + 1 counts.
@@ -990,12 +1055,12 @@ __device__ __forceinline__ uint64_t pfl_region_rec(const uint64_t *__restrict__ 
 #ifndef SK_PFL_RWPE
 #define SK_PFL_RWPE 4      // region waves per SIMD the register budget is sized for (one 1024-thread workgroup per CU)
 #endif
-__global__ void __launch_bounds__(SK_PFL_RTPB) __attribute__((amdgpu_waves_per_eu(SK_PFL_RWPE))) k_pfl_region(const uint64_t *__restrict__ chunks,
+__global__ void __launch_bounds__(SK_PFL_RTPB) __attribute__((amdgpu_waves_per_eu(SK_PFL_RWPE))) k_pfl_region(const PflChunk chunks,
                                                             const uint32_t *__restrict__ S, uint32_t nblk, uint32_t tb,
                                                             uint32_t ntile, uint32_t nsub, uint32_t sh, PflPerm pm,
                                                             uint32_t cap, const uint32_t *__restrict__ tot,
                                                             uint32_t *__restrict__ rbase, uint32_t *__restrict__ C2,
-                                                            uint64_t *__restrict__ rec2,
+                                                            PflRec rec2,
                                                             uint8_t *__restrict__ changed, int probe) {
     extern __shared__ uint64_t dyn64[];
     uint64_t *sorted = dyn64;
@@ -1086,7 +1151,7 @@ __global__ void __launch_bounds__(SK_PFL_RTPB) __attribute__((amdgpu_waves_per_e
                     continue;
                 }
                 const uint32_t lo = seg_of[x];
-                r[q] = chunks[uint64_t(b0 + lo) * SK_PFP_EPB + segs[lo] + (x - segp[lo])];
+                r[q] = chunks.get(uint64_t(b0 + lo) * SK_PFP_EPB + segs[lo] + (x - segp[lo]));
                 rk[q] = b0 + lo;
             }
         }
@@ -1104,9 +1169,8 @@ __global__ void __launch_bounds__(SK_PFL_RTPB) __attribute__((amdgpu_waves_per_e
             if (r[q] != ~0ull) sorted[hist[rk[q] >> 14] + (rk[q] & 16383u)] = r[q];
         __syncthreads();
         const uint32_t kept = hist[nsub];
-        uint64_t *dst = rec2 + base;
         if (probe & 1024) return; // dev ablation: no write-out
-        for (uint32_t i = tid; i < kept; i += SK_PFL_RTPB) dst[i] = sorted[i];
+        for (uint32_t i = tid; i < kept; i += SK_PFL_RTPB) rec2.put(base + i, sorted[i]);
         return;
     }
     // swollen region (one element repeated in many blocks): count every piece, then place every piece; the runs
@@ -1133,7 +1197,7 @@ __global__ void __launch_bounds__(SK_PFL_RTPB) __attribute__((amdgpu_waves_per_e
             if (x >= m || x - p0 >= cap) continue;
             uint32_t blk, sub = 0;
             const uint64_t rr = conv(pfl_region_rec(chunks, segp, segs, nb, b0, x, &blk), blk, &sub);
-            if (rr != ~0ull) rec2[base + hist[sub] + atomicAdd(&lcnt[sub], 1u)] = rr;
+            if (rr != ~0ull) rec2.put(base + hist[sub] + atomicAdd(&lcnt[sub], 1u), rr);
         }
         __syncthreads();
         for (uint32_t x = tid; x < nsub; x += SK_PFL_RTPB) {
@@ -1236,7 +1300,7 @@ __global__ void __launch_bounds__(256) k_pfl_plan(const uint32_t *__restrict__ C
     if (heavy && base + ph < hmax) order[base + ph] = f; // hmax bounds the heavy buckets (n / (CAP + 1))
 }
 
-__global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const uint64_t *__restrict__ rec2,
+__global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const PflRec rec2,
                                                            const uint32_t *__restrict__ rbase,
                                                            const uint32_t *__restrict__ C2, uint32_t ntile,
                                                            uint32_t nsub, uint32_t sh, PflPerm pm, uint32_t nslab,
@@ -1309,11 +1373,11 @@ __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const uint64_t *__res
 #pragma unroll
         for (uint32_t step = 64; step; step >>= 1)
             if (lo + step < ntile && rp[lo + step] <= u) lo += step;
-        return rec2[rs[lo] + (u - rp[lo])];
+        return rec2.get(rs[lo] + (u - rp[lo]));
     };
     auto rec_one = [&](uint32_t u) -> uint64_t {
         const uint32_t t = run_of[u];
-        return rec2[rs[t] + (u - rp[t])];
+        return rec2.get(rs[t] + (u - rp[t]));
     };
     if (cnt <= SK_PFL_CAP && threadIdx.x < ntile)
         for (uint32_t u = ex; u < ex + len; u++) run_of[u] = uint8_t(threadIdx.x);
@@ -1381,7 +1445,8 @@ __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const uint64_t *__res
                 __syncthreads();
                 pfl_chunk(R, k, nxt, head, fin, reg, dirty, [] {}, put);
             } else { // one run larger than a chunk (t1 == t0 + 1), contiguous from rs[t0]
-                const uint64_t *run = rec2 + rs[t0];
+                const uint64_t run0 = rs[t0];
+                auto run = [&](uint32_t u) -> uint64_t { return rec2.get(run0 + u); };
                 // only records above their register can rise, and only they can stop a later record from rising:
                 // the rest reply 0 now; the candidates are resolved as a chunk when they fit (a hot sketch whose
                 // registers are already high has few), else with the (slot, rho) -> min seq table
@@ -1394,7 +1459,7 @@ __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const uint64_t *__res
 #pragma unroll
                     for (int q = 0; q < FU; q++) {
                         const uint32_t u = u0 + q * SK_PFL_ATPB + threadIdx.x;
-                        rr[q] = u < k ? run[u] : ~0ull;
+                        rr[q] = u < k ? run(u) : ~0ull;
                     }
 #pragma unroll
                     for (int q = 0; q < FU; q++) {
@@ -1429,13 +1494,13 @@ __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const uint64_t *__res
                     return ((r >> 26) & 63u) > reg[pfl_slotb(key)];
                 };
                 for (uint32_t u = threadIdx.x; u < k; u += SK_PFL_ATPB) {
-                    const uint64_t r = run[u];
+                    const uint64_t r = run(u);
                     if (cand(r)) T.insert(((r >> 32) << 6) | ((r >> 26) & 63u), uint32_t(r & 0x3ffffffu));
                 }
                 __threadfence();
                 __syncthreads();
                 for (uint32_t u = threadIdx.x; u < k; u += SK_PFL_ATPB) { // replies (registers only read)
-                    const uint64_t r = run[u], key = r >> 32;
+                    const uint64_t r = run(u), key = r >> 32;
                     if (!cand(r)) continue;
                     const uint32_t rho = uint32_t(r >> 26) & 63u, seq = uint32_t(r & 0x3ffffffu);
                     bool first = true;
@@ -1444,7 +1509,7 @@ __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const uint64_t *__res
                 }
                 __syncthreads();
                 for (uint32_t u = threadIdx.x; u < k; u += SK_PFL_ATPB) { // the register's writer: its top record
-                    const uint64_t r = run[u], key = r >> 32;
+                    const uint64_t r = run(u), key = r >> 32;
                     if (!cand(r)) continue;
                     const uint32_t rho = uint32_t(r >> 26) & 63u, seq = uint32_t(r & 0x3ffffffu);
                     if (T.find((key << 6) | rho) != seq) continue;
@@ -4075,8 +4140,10 @@ hipError_t launch_pfl_part(hipStream_t st, const PflDims &d, const uint64_t *chu
         attr = true;
     }
     static const int probe_flags = getenv("SK_PFL_PROBE") ? atoi(getenv("SK_PFL_PROBE")) : 0; // dev ablations
-    hipLaunchKernelGGL(k_pfl_region, dim3(d.nreg), dim3(SK_PFL_RTPB), lds, st, chunks, S, d.nblk, d.tb, d.ntile,
-                       d.nsub, d.sh, PflPerm{d.pa, d.pai, d.pm_mask, d.nslab}, d.rcap, tot, rbase, C2, rec2,
+    hipLaunchKernelGGL(k_pfl_region, dim3(d.nreg), dim3(SK_PFL_RTPB), lds, st,
+                       PflChunk{const_cast<uint64_t *>(chunks), uint64_t(d.nblk) * SK_PFP_EPB}, S, d.nblk, d.tb, d.ntile,
+                       d.nsub, d.sh, PflPerm{d.pa, d.pai, d.pm_mask, d.nslab}, d.rcap, tot, rbase, C2,
+                       PflRec{rec2, uint64_t(d.nblk) * SK_PFP_EPB},
                        changed, probe_flags);
     SK_LAUNCH_CHECK();
     return hipSuccess;
@@ -4105,7 +4172,8 @@ hipError_t launch_pfl_apply(hipStream_t st, const PflDims &d, const uint64_t *re
                            uint32_t(d.nf), hmax, big_alloc + 1, order);
         SK_LAUNCH_CHECK();
     }
-    hipLaunchKernelGGL(k_pfl_apply, dim3(uint32_t(d.nf) + hmax), dim3(SK_PFL_ATPB), 0, st, rec2, rbase, C2, d.ntile,
+    hipLaunchKernelGGL(k_pfl_apply, dim3(uint32_t(d.nf) + hmax), dim3(SK_PFL_ATPB), 0, st,
+                       PflRec{const_cast<uint64_t *>(rec2), uint64_t(d.nblk) * SK_PFP_EPB}, rbase, C2, d.ntile,
                        d.nsub, d.sh, PflPerm{d.pa, d.pai, d.pm_mask, d.nslab}, nslab, arena, changed, big_alloc,
                        big_keys, big_vals, flags | probe_flags, hmax, big_alloc + 1, order, rc, par);
     SK_LAUNCH_CHECK();

@@ -1054,7 +1054,7 @@ int pfadd_lines(sk_ctx *c, uint64_t n, const uint32_t *d_ids, const uint64_t *d_
     HIPCHK(c, c->pfl_chunks.ensure(d.chunk_bytes));
     HIPCHK(c, c->pfl_S.ensure(d.S_bytes));
     HIPCHK(c, c->pfl_C.ensure(d.c_words * 4));
-    HIPCHK(c, c->pfl_rec.ensure(n * 8));
+    HIPCHK(c, c->pfl_rec.ensure(d.chunk_bytes)); // records: u64 or 6-B planes per hash-block slot (SK_PFL_R6)
     HIPCHK(c, c->pfl_bk.ensure(2 * n * 8));
     HIPCHK(c, c->pfl_bv.ensure(2 * n * 4));
     HIPCHK(c, c->pfl_ovf.ensure(64));

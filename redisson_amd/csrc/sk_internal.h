@@ -123,7 +123,8 @@ uint64_t rc_group_table_words(uint64_t size);
 // Bloom add, region schedule: pieces of <= ra_piece() elements; k <= rc_max_probes()
 uint32_t ra_blocks(uint64_t n, int k);
 uint64_t rc_seg_words(uint32_t nb, uint32_t nr); // u32 words of a hash's interleaved segment table (nb blocks, nr regions)
-bool rc_seg_interleaved();                        // the hash writes an interleaved table (then launch_rc_stranspose)
+bool rc_seg_interleaved();
+bool rc_probe_reads_st();                        // the hash writes an interleaved table (then launch_rc_stranspose)
 hipError_t launch_rc_stranspose(hipStream_t st, uint32_t nb, uint32_t nr, const uint32_t *St, uint32_t *S);
 uint32_t ra_regions(uint64_t size);
 uint64_t ra_piece(int k);

@@ -1234,6 +1234,15 @@ __global__ void __launch_bounds__(256) k_pfl_fill(uint8_t *__restrict__ changed,
     if (i < ((n - head) & 15)) changed[head + nv * 16 + i] = uint8_t(v);
 }
 
+#ifndef SK_PFL_DG
+#define SK_PFL_DG 1        // 16-B words per dirty flag: the apply stores back the 16-B pieces of its lines that changed
+#endif
+#define PFL_DWORDS ((16384 / 16 / SK_PFL_DG + 31) / 32)
+__device__ __forceinline__ void pfl_mark(uint32_t *dirty, uint32_t slotb) { // register slotb of the LDS lines changed
+    const uint32_t piece = slotb / (16 * SK_PFL_DG);
+    atomicOr(&dirty[piece >> 5], 1u << (piece & 31u));
+}
+
 // one chunk of records R[0..cnt) (every record of its registers with a smaller seq is in this chunk or was
 // applied to `reg` before): chains per register, sequential replies, final register values into `reg` (LDS).
 // Caller syncs before (R loaded, heads cleared) and after; `fill` runs between the chain build and the walk (the
@@ -1241,7 +1250,7 @@ __global__ void __launch_bounds__(256) k_pfl_fill(uint8_t *__restrict__ changed,
 // reply (only those that differ from the call's default when the replies were pre-filled).
 template <class Fill, class Put>
 __device__ __forceinline__ void pfl_chunk(const uint64_t *R, uint32_t cnt, uint16_t *nxt, uint32_t *head,
-                                          uint8_t *fin, uint8_t *reg, uint8_t *dirty, Fill fill, Put put) {
+                                          uint8_t *fin, uint8_t *reg, uint32_t *dirty, Fill fill, Put put) {
     for (uint32_t u = threadIdx.x; u < cnt; u += SK_PFL_ATPB)
         nxt[u] = uint16_t(atomicExch(&head[pfl_ht(R[u] >> 32)], u));
     fill();
@@ -1271,7 +1280,7 @@ __device__ __forceinline__ void pfl_chunk(const uint64_t *R, uint32_t cnt, uint1
         if (fin[u]) {
             const uint64_t key = R[u] >> 32;
             reg[pfl_slotb(key)] = fin[u];
-            dirty[uint32_t(key >> 14)] = 1;
+            pfl_mark(dirty, pfl_slotb(key));
         }
 }
 
@@ -1317,7 +1326,7 @@ __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const PflRec rec2,
     constexpr uint32_t LW = (1u << SK_PFL_LB) / 16; // 16-B words per line
     __shared__ uint4 regs4[NL * LW];           // line of sketch slab0 + i at reg[i << SK_PFL_LB]
     __shared__ uint64_t work[(kWork + 7) / 8]; // chunk records, chains, final values (or the big-run table)
-    __shared__ uint8_t dirty[NL];
+    __shared__ uint32_t dirty[PFL_DWORDS]; // bit per SK_PFL_DG-word piece of the lines: changed, stored back
     __shared__ uint32_t rs[SK_PFL_NTMAX], rp[SK_PFL_NTMAX + 1]; // the fine bucket's run per tile: start, prefix
     __shared__ uint32_t wsum[SK_PFL_ATPB / 64];
     uint8_t *reg = reinterpret_cast<uint8_t *>(regs4);
@@ -1391,7 +1400,7 @@ __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const PflRec rec2,
             nones += rep;
         }
     };
-    for (uint32_t i = threadIdx.x; i < NL; i += SK_PFL_ATPB) dirty[i] = 0;
+    for (uint32_t i = threadIdx.x; i < PFL_DWORDS; i += SK_PFL_ATPB) dirty[i] = 0;
     for (uint32_t t = threadIdx.x; t < SK_PFL_HT; t += SK_PFL_ATPB) head[t] = 0xffffu;
     if (threadIdx.x == 0) rp[ntile] = cnt;
     __syncthreads();
@@ -1518,7 +1527,7 @@ __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const PflRec rec2,
                     const uint32_t slotb = pfl_slotb(key);
                     if (top && rho > reg[slotb]) {
                         reg[slotb] = uint8_t(rho);
-                        dirty[uint32_t(key >> 14)] = 1;
+                        pfl_mark(dirty, slotb);
                     }
                 }
                 }
@@ -1543,7 +1552,7 @@ __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const PflRec rec2,
     if (probe & 4) return;
     typedef unsigned int v4u __attribute__((ext_vector_type(4)));
     for (uint32_t q = threadIdx.x; q < nsl * LW; q += SK_PFL_ATPB)
-        if (dirty[q / LW]) {
+        if ((dirty[(q / SK_PFL_DG) >> 5] >> ((q / SK_PFL_DG) & 31u)) & 1u) {
             if (probe & 16) {
                 const uint4 x = regs4[q];
                 v4u y = {x.x, x.y, x.z, x.w};
@@ -2601,6 +2610,13 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_rc_probe(uint32_t NB, uint32_t
 #define SK_RC_PERSIST 1
 #endif
 #define RC_PSLOTS 32 // workgroups per XCD group (8 x 32 = 256 = one per CU)
+#ifndef SK_RC_PCOL
+// 1: the probe reads the hash blocks' interleaved segment table St itself (no k_rc_stranspose): an XCD group starts
+// on a multiple of SK_RC_STILE regions, so its 32 workgroups test one interleave group's regions at a time and the
+// group's lines of St (a block's entries for those regions, 128 B) are fetched into that XCD's L2 once.  Measured
+// slower (probe 0.684 -> 0.809 ms per 32 M for the transpose's ~0.03 ms, r05dg): 0 keeps the transpose
+#define SK_RC_PCOL 0
+#endif
 #ifndef RC_PTPB
 #define RC_PTPB 1024 // threads per workgroup
 #endif
@@ -2621,7 +2637,8 @@ __global__ void __launch_bounds__(TPB) k_bloom_rc_probe_p(uint32_t NB, uint32_t 
     constexpr uint32_t NV = (1u << (RC_RB - 3)) / 16, VPT = NV / TPB;
     // XCD group x = blockIdx % 8 owns regions [x*q, (x+1)*q); its nslot workgroups take them interleaved, so the
     // ~32 regions an XCD works on at once are neighbours (their segments share lines of the block chunks)
-    const uint32_t xg = blockIdx.x & 7u, slot = blockIdx.x >> 3, nslot = gridDim.x >> 3, q = (NR + 7) / 8;
+    const uint32_t xg = blockIdx.x & 7u, slot = blockIdx.x >> 3, nslot = gridDim.x >> 3;
+    const uint32_t q = SK_RC_PCOL ? ((NR + 7) / 8 + SK_RC_STILE - 1) / SK_RC_STILE * SK_RC_STILE : (NR + 7) / 8;
     auto region = [&](uint32_t i) -> uint32_t {
         const uint32_t t = slot + nslot * i, rr = xg * q + t;
         return t < q && rr < NR ? rr : NR;
@@ -2647,6 +2664,7 @@ __global__ void __launch_bounds__(TPB) k_bloom_rc_probe_p(uint32_t NB, uint32_t 
         const uint32_t *Srow = S + uint64_t(r) * NB;
         auto seg_of = [&](uint32_t u) -> uint32_t { // this thread's segment-table word of step u (0 past the end)
             const uint32_t j = threadIdx.x + u * TPB;
+            if (SK_RC_PCOL) return u < nsteps && j < NB ? S[rc_sidx(r, j, NB)] : 0u;
             return u < nsteps && j < NB ? Srow[j] : 0u;
         };
         auto ld = [&](uint32_t u, uint32_t sg, uint4 (&w)[RC_SEGV]) { // sg = 0 past the end: nothing read
@@ -4326,6 +4344,8 @@ uint64_t rc_seg_words(uint32_t nb, uint32_t nr) {
     return uint64_t(nb) * ((nr + SK_RC_STILE - 1) / SK_RC_STILE * SK_RC_STILE);
 }
 bool rc_seg_interleaved() { return SK_RC_STILE > 1; }
+// the contains probe reads the interleaved table itself (no transpose before it)
+bool rc_probe_reads_st() { return SK_RC_STILE > 1 && SK_RC_PCOL && SK_RC_ZL && SK_RC_TV && SK_RC_PERSIST; }
 hipError_t launch_rc_stranspose(hipStream_t st, uint32_t nb, uint32_t nr, const uint32_t *St, uint32_t *S) {
     if (SK_RC_STILE == 1) return hipSuccess;
     hipLaunchKernelGGL(k_rc_stranspose, dim3((nb + RC_STJ - 1) / RC_STJ, (nr + SK_RC_STILE - 1) / SK_RC_STILE), dim3(256), 0, st,

@@ -2830,9 +2830,11 @@ static int bloom_contains_launch(sk_ctx *c, hipStream_t s, uint32_t id, int64_t 
         { Prof q_(c, 18, s);
         HIPCHK(c, sk::launch_bloom_rc_hash(s, m, d_off + s0, d_bytes, usize, magic, k, St,
                                            c->rc_rec.as<uint32_t>(), d_out + s0));
-        HIPCHK(c, sk::launch_rc_stranspose(s, sk::rc_blocks(m), uint32_t(nr), St, c->rc_S.as<uint32_t>())); }
+        if (!sk::rc_probe_reads_st())
+            HIPCHK(c, sk::launch_rc_stranspose(s, sk::rc_blocks(m), uint32_t(nr), St, c->rc_S.as<uint32_t>())); }
         { Prof q_(c, 19, s);
-        HIPCHK(c, sk::launch_bloom_rc_probe(s, m, usize, k, c->rc_S.as<uint32_t>(), c->rc_rec.as<uint32_t>(),
+        HIPCHK(c, sk::launch_bloom_rc_probe(s, m, usize, k, sk::rc_probe_reads_st() ? St : c->rc_S.as<uint32_t>(),
+                                            c->rc_rec.as<uint32_t>(),
                                             c->strs[id].ptr, c->strs[id].cap, d_out + s0, c->rc_Z.as<uint32_t>(),
                                             c->rc_GT.as<uint32_t>())); }
     }

@@ -1238,6 +1238,9 @@ __global__ void __launch_bounds__(256) k_pfl_fill(uint8_t *__restrict__ changed,
 #define SK_PFL_DG 1        // 16-B words per dirty flag: the apply stores back the 16-B pieces of its lines that changed
 #endif
 #define PFL_DWORDS ((16384 / 16 / SK_PFL_DG + 31) / 32)
+#ifndef SK_PFL_TL
+#define SK_PFL_TL 1        // a one-chunk fine bucket loads only the 16-B line pieces its records read, after them
+#endif
 __device__ __forceinline__ void pfl_mark(uint32_t *dirty, uint32_t slotb) { // register slotb of the LDS lines changed
     const uint32_t piece = slotb / (16 * SK_PFL_DG);
     atomicOr(&dirty[piece >> 5], 1u << (piece & 31u));
@@ -1327,6 +1330,7 @@ __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const PflRec rec2,
     __shared__ uint4 regs4[NL * LW];           // line of sketch slab0 + i at reg[i << SK_PFL_LB]
     __shared__ uint64_t work[(kWork + 7) / 8]; // chunk records, chains, final values (or the big-run table)
     __shared__ uint32_t dirty[PFL_DWORDS]; // bit per SK_PFL_DG-word piece of the lines: changed, stored back
+    __shared__ uint32_t need[NL * LW / 32]; // SK_PFL_TL: bit per 16-B piece of the lines that a record reads
     __shared__ uint32_t rs[SK_PFL_NTMAX], rp[SK_PFL_NTMAX + 1]; // the fine bucket's run per tile: start, prefix
     __shared__ uint32_t wsum[SK_PFL_ATPB / 64];
     uint8_t *reg = reinterpret_cast<uint8_t *>(regs4);
@@ -1401,11 +1405,13 @@ __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const PflRec rec2,
         }
     };
     for (uint32_t i = threadIdx.x; i < PFL_DWORDS; i += SK_PFL_ATPB) dirty[i] = 0;
+    if (SK_PFL_TL)
+        for (uint32_t i = threadIdx.x; i < NL * LW / 32; i += SK_PFL_ATPB) need[i] = 0;
     for (uint32_t t = threadIdx.x; t < SK_PFL_HT; t += SK_PFL_ATPB) head[t] = 0xffffu;
     if (threadIdx.x == 0) rp[ntile] = cnt;
     __syncthreads();
     if (cnt <= SK_PFL_CAP) { // the whole fine bucket is one chunk: records and lines in one round trip
-        load_lines();
+        if (!SK_PFL_TL) load_lines();
         constexpr int RU = SK_PFL_CAP / SK_PFL_ATPB; // every record load in flight at once
         uint64_t rv[RU];
 #pragma unroll
@@ -1416,16 +1422,31 @@ __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const PflRec rec2,
 #pragma unroll
         for (int q = 0; q < RU; q++) {
             const uint32_t u = q * SK_PFL_ATPB + threadIdx.x;
-            if (u < cnt) R[u] = rv[q];
+            if (u < cnt) {
+                R[u] = rv[q];
+                if (SK_PFL_TL) {
+                    const uint32_t w = pfl_slotb(rv[q] >> 32) >> 4;
+                    atomicOr(&need[w >> 5], 1u << (w & 31u));
+                }
+            }
         }
+        auto needed = [&](uint32_t q) { return !SK_PFL_TL || ((need[q >> 5] >> (q & 31u)) & 1u); };
         auto fill_lines = [&] {
 #pragma unroll
             for (int j = 0; j < LQ; j++) {
                 const uint32_t q = threadIdx.x + j * SK_PFL_ATPB;
-                if (q < nsl * LW && pm.inv(slab0 + q / LW) < nslab) regs4[q] = lv[j];
+                if (q < nsl * LW && pm.inv(slab0 + q / LW) < nslab && needed(q)) regs4[q] = lv[j];
             }
         };
         __syncthreads();
+        if (SK_PFL_TL) { // only the 16-B pieces of the lines that records read (about half of them at 64 M)
+#pragma unroll
+            for (int j = 0; j < LQ; j++) {
+                const uint32_t q = threadIdx.x + j * SK_PFL_ATPB;
+                if (q < nsl * LW && pm.inv(slab0 + q / LW) < nslab && needed(q))
+                    lv[j] = (probe & 4) ? make_uint4(0, 0, 0, 0) : line(q / LW)[q % LW];
+            }
+        }
         if (probe & 128) return; // dev ablation: run table, lines and records loaded, nothing applied
         pfl_chunk(R, cnt, nxt, head, fin, reg, dirty, fill_lines, put);
     } else {

@@ -978,32 +978,50 @@ __global__ void __launch_bounds__(SK_PFP_ATPB) __attribute__((amdgpu_waves_per_e
 #define SK_PFL_LDS (160 * 1024 - 9 * 1024) // dynamic LDS of a region workgroup: records + fine-bucket counts
 #endif
 #ifndef SK_PFL_R6
-#define SK_PFL_R6 1        // rec2 as 6-B records: a u32 plane (rho << 26 | seq) and a u16 plane (slab_low << 7 |
-                           // register in its line) instead of one u64 (SK_PFL_R6=0)
+#define SK_PFL_R6 2        // rec2 as 6-B records packed back to back (0: u64)
 #endif
 // rec2 record slot i.  The region pass writes the records sorted; the apply reads them back as the u64
-// slab_low << 46 | reg << 32 | rho << 26 | seq, with reg's line bits zero in the 6-B form (a fine bucket holds one
-// line of each of its sketches, so slab_low and the register's place in its line name the register).  The buffer
-// holds u64[cap] either way: the 6-B form keeps the u32 plane at [0, 4 cap) bytes and the u16 plane after it.
+// slab_low << 46 | reg << 32 | rho << 26 | seq, with reg's line bits zero in the 6-B forms (a fine bucket holds one
+// line of each of its sketches, so slab_low and the register's place in its line name the register): lo = the low
+// 32 bits, hi = slab_low << 7 | register in its line.  The buffer holds u64[cap] in every form.
+//   2: record i at bytes [6i, 6i + 6): lo then hi for even i, hi then lo for odd i, so both are aligned loads and
+//      a fine bucket's run (~16 records) spans as few 128-B lines as its 96 bytes allow;
+//   (a u32 plane and a u16 plane instead, tried first: a run then touches lines of both planes, and r05req counted
+//   17 % more read requests in the apply than with u64 records; packed, 4 % fewer.)
 struct PflRec {
     uint64_t *p;
-    uint64_t cap; // records the planes hold (the call's hash blocks x SK_PFP_EPB)
+    uint64_t cap; // records the buffer holds (the call's hash blocks x SK_PFP_EPB)
     __device__ __forceinline__ void put(uint64_t i, uint64_t r) const {
-        if (SK_PFL_R6) {
-            reinterpret_cast<uint32_t *>(p)[i] = uint32_t(r);
-            reinterpret_cast<uint16_t *>(reinterpret_cast<uint32_t *>(p) + cap)[i] =
-                uint16_t((uint32_t(r >> 46) << SK_PFL_LB) | (uint32_t(r >> 32) & ((1u << SK_PFL_LB) - 1)));
+        const uint32_t lo = uint32_t(r);
+        const uint16_t hi = uint16_t((uint32_t(r >> 46) << SK_PFL_LB) | (uint32_t(r >> 32) & ((1u << SK_PFL_LB) - 1)));
+        if (SK_PFL_R6 == 2) {
+            const uint64_t odd = i & 1u;
+            reinterpret_cast<uint32_t *>(p)[(3 * i + odd) >> 1] = lo;
+            reinterpret_cast<uint16_t *>(p)[3 * i + 2 * (1 - odd)] = hi;
         } else {
             p[i] = r;
         }
     }
+    // SK_PFL_R6 == 2: records 2P and 2P + 1 as three whole words (lo, hi | hi' << 16, lo')
+    __device__ __forceinline__ void put_pair(uint64_t P, uint64_t r0, uint64_t r1) const {
+        auto hi = [](uint64_t r) {
+            return (uint32_t(r >> 46) << SK_PFL_LB) | (uint32_t(r >> 32) & ((1u << SK_PFL_LB) - 1));
+        };
+        uint32_t *w = reinterpret_cast<uint32_t *>(p) + 3 * P;
+        w[0] = uint32_t(r0);
+        w[1] = hi(r0) | (hi(r1) << 16);
+        w[2] = uint32_t(r1);
+    }
     __device__ __forceinline__ uint64_t get(uint64_t i) const {
-        if (SK_PFL_R6) {
-            const uint32_t lo = reinterpret_cast<const uint32_t *>(p)[i];
-            const uint32_t hi = reinterpret_cast<const uint16_t *>(reinterpret_cast<const uint32_t *>(p) + cap)[i];
-            return (uint64_t(hi >> SK_PFL_LB) << 46) | (uint64_t(hi & ((1u << SK_PFL_LB) - 1)) << 32) | lo;
+        uint32_t lo, hi;
+        if (SK_PFL_R6 == 2) {
+            const uint64_t odd = i & 1u;
+            lo = reinterpret_cast<const uint32_t *>(p)[(3 * i + odd) >> 1];
+            hi = reinterpret_cast<const uint16_t *>(p)[3 * i + 2 * (1 - odd)];
+        } else {
+            return p[i];
         }
-        return p[i];
+        return (uint64_t(hi >> SK_PFL_LB) << 46) | (uint64_t(hi & ((1u << SK_PFL_LB) - 1)) << 32) | lo;
     }
 };
 static_assert(SK_PFL_SH + SK_PFL_LB <= 16, "6-B records: slab_low and the register in its line fit 16 bits");
@@ -1170,7 +1188,17 @@ __global__ void __launch_bounds__(SK_PFL_RTPB) __attribute__((amdgpu_waves_per_e
         __syncthreads();
         const uint32_t kept = hist[nsub];
         if (probe & 1024) return; // dev ablation: no write-out
-        for (uint32_t i = tid; i < kept; i += SK_PFL_RTPB) rec2.put(base + i, sorted[i]);
+        if (SK_PFL_R6 != 2) {
+            for (uint32_t i = tid; i < kept; i += SK_PFL_RTPB) rec2.put(base + i, sorted[i]);
+            return;
+        }
+        // packed records: whole pairs as three words each; an odd first or last record alone (its pair is shared
+        // with the neighbouring region)
+        const uint64_t a = base, e = uint64_t(base) + kept, a2 = a + (a & 1u), e2 = e - (e & 1u);
+        if (kept && (a & 1u) && tid == 0) rec2.put(a, sorted[0]);
+        if (kept && (e & 1u) && e - 1 >= a2 && tid == 1) rec2.put(e - 1, sorted[e - 1 - a]);
+        for (uint64_t P = a2 / 2 + tid; P < e2 / 2; P += SK_PFL_RTPB)
+            rec2.put_pair(P, sorted[2 * P - a], sorted[2 * P + 1 - a]);
         return;
     }
     // swollen region (one element repeated in many blocks): count every piece, then place every piece; the runs
@@ -1238,9 +1266,6 @@ __global__ void __launch_bounds__(256) k_pfl_fill(uint8_t *__restrict__ changed,
 #define SK_PFL_DG 1        // 16-B words per dirty flag: the apply stores back the 16-B pieces of its lines that changed
 #endif
 #define PFL_DWORDS ((16384 / 16 / SK_PFL_DG + 31) / 32)
-#ifndef SK_PFL_TL
-#define SK_PFL_TL 1        // a one-chunk fine bucket loads only the 16-B line pieces its records read, after them
-#endif
 __device__ __forceinline__ void pfl_mark(uint32_t *dirty, uint32_t slotb) { // register slotb of the LDS lines changed
     const uint32_t piece = slotb / (16 * SK_PFL_DG);
     atomicOr(&dirty[piece >> 5], 1u << (piece & 31u));
@@ -1330,7 +1355,6 @@ __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const PflRec rec2,
     __shared__ uint4 regs4[NL * LW];           // line of sketch slab0 + i at reg[i << SK_PFL_LB]
     __shared__ uint64_t work[(kWork + 7) / 8]; // chunk records, chains, final values (or the big-run table)
     __shared__ uint32_t dirty[PFL_DWORDS]; // bit per SK_PFL_DG-word piece of the lines: changed, stored back
-    __shared__ uint32_t need[NL * LW / 32]; // SK_PFL_TL: bit per 16-B piece of the lines that a record reads
     __shared__ uint32_t rs[SK_PFL_NTMAX], rp[SK_PFL_NTMAX + 1]; // the fine bucket's run per tile: start, prefix
     __shared__ uint32_t wsum[SK_PFL_ATPB / 64];
     uint8_t *reg = reinterpret_cast<uint8_t *>(regs4);
@@ -1405,13 +1429,11 @@ __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const PflRec rec2,
         }
     };
     for (uint32_t i = threadIdx.x; i < PFL_DWORDS; i += SK_PFL_ATPB) dirty[i] = 0;
-    if (SK_PFL_TL)
-        for (uint32_t i = threadIdx.x; i < NL * LW / 32; i += SK_PFL_ATPB) need[i] = 0;
     for (uint32_t t = threadIdx.x; t < SK_PFL_HT; t += SK_PFL_ATPB) head[t] = 0xffffu;
     if (threadIdx.x == 0) rp[ntile] = cnt;
     __syncthreads();
     if (cnt <= SK_PFL_CAP) { // the whole fine bucket is one chunk: records and lines in one round trip
-        if (!SK_PFL_TL) load_lines();
+        load_lines();
         constexpr int RU = SK_PFL_CAP / SK_PFL_ATPB; // every record load in flight at once
         uint64_t rv[RU];
 #pragma unroll
@@ -1422,31 +1444,16 @@ __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const PflRec rec2,
 #pragma unroll
         for (int q = 0; q < RU; q++) {
             const uint32_t u = q * SK_PFL_ATPB + threadIdx.x;
-            if (u < cnt) {
-                R[u] = rv[q];
-                if (SK_PFL_TL) {
-                    const uint32_t w = pfl_slotb(rv[q] >> 32) >> 4;
-                    atomicOr(&need[w >> 5], 1u << (w & 31u));
-                }
-            }
+            if (u < cnt) R[u] = rv[q];
         }
-        auto needed = [&](uint32_t q) { return !SK_PFL_TL || ((need[q >> 5] >> (q & 31u)) & 1u); };
         auto fill_lines = [&] {
 #pragma unroll
             for (int j = 0; j < LQ; j++) {
                 const uint32_t q = threadIdx.x + j * SK_PFL_ATPB;
-                if (q < nsl * LW && pm.inv(slab0 + q / LW) < nslab && needed(q)) regs4[q] = lv[j];
+                if (q < nsl * LW && pm.inv(slab0 + q / LW) < nslab) regs4[q] = lv[j];
             }
         };
         __syncthreads();
-        if (SK_PFL_TL) { // only the 16-B pieces of the lines that records read (about half of them at 64 M)
-#pragma unroll
-            for (int j = 0; j < LQ; j++) {
-                const uint32_t q = threadIdx.x + j * SK_PFL_ATPB;
-                if (q < nsl * LW && pm.inv(slab0 + q / LW) < nslab && needed(q))
-                    lv[j] = (probe & 4) ? make_uint4(0, 0, 0, 0) : line(q / LW)[q % LW];
-            }
-        }
         if (probe & 128) return; // dev ablation: run table, lines and records loaded, nothing applied
         pfl_chunk(R, cnt, nxt, head, fin, reg, dirty, fill_lines, put);
     } else {

@@ -1012,6 +1012,21 @@ struct PflRec {
         w[1] = hi(r0) | (hi(r1) << 16);
         w[2] = uint32_t(r1);
     }
+    // records 2P and 2P + 1
+    __device__ __forceinline__ void get_pair(uint64_t P, uint64_t *r0, uint64_t *r1) const {
+        if (SK_PFL_R6 == 2) {
+            const uint32_t *w = reinterpret_cast<const uint32_t *>(p) + 3 * P;
+            const uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
+            *r0 = unpack(w0, w1 & 0xffffu);
+            *r1 = unpack(w2, w1 >> 16);
+        } else {
+            *r0 = p[2 * P];
+            *r1 = p[2 * P + 1];
+        }
+    }
+    __device__ __forceinline__ static uint64_t unpack(uint32_t lo, uint32_t hi) {
+        return (uint64_t(hi >> SK_PFL_LB) << 46) | (uint64_t(hi & ((1u << SK_PFL_LB) - 1)) << 32) | lo;
+    }
     __device__ __forceinline__ uint64_t get(uint64_t i) const {
         uint32_t lo, hi;
         if (SK_PFL_R6 == 2) {
@@ -1021,7 +1036,7 @@ struct PflRec {
         } else {
             return p[i];
         }
-        return (uint64_t(hi >> SK_PFL_LB) << 46) | (uint64_t(hi & ((1u << SK_PFL_LB) - 1)) << 32) | lo;
+        return unpack(lo, hi);
     }
 };
 static_assert(SK_PFL_SH + SK_PFL_LB <= 16, "6-B records: slab_low and the register in its line fit 16 bits");
@@ -1490,16 +1505,22 @@ __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const PflRec rec2,
                 __shared__ uint32_t ncand;
                 if (threadIdx.x == 0) ncand = 0;
                 __syncthreads();
-                constexpr int FU = 8; // records in flight per thread
-                for (uint32_t u0 = 0; u0 < k; u0 += FU * SK_PFL_ATPB) {
-                    uint64_t rr[FU];
+                // records in pairs (a packed pair is three aligned words: one load), FU of them in flight per
+                // thread; the run's slots [run0, run0 + k) may start and end inside a pair
+                constexpr int FU = 4;
+                const uint64_t pe0 = run0 >> 1, pe1 = (run0 + k + 1) >> 1;
+                for (uint64_t p0 = pe0; p0 < pe1; p0 += FU * SK_PFL_ATPB) {
+                    uint64_t rr[2 * FU];
 #pragma unroll
                     for (int q = 0; q < FU; q++) {
-                        const uint32_t u = u0 + q * SK_PFL_ATPB + threadIdx.x;
-                        rr[q] = u < k ? run(u) : ~0ull;
+                        const uint64_t P = p0 + q * SK_PFL_ATPB + threadIdx.x;
+                        rr[2 * q] = rr[2 * q + 1] = ~0ull;
+                        if (P < pe1) rec2.get_pair(P, &rr[2 * q], &rr[2 * q + 1]);
+                        if (2 * P < run0) rr[2 * q] = ~0ull;
+                        if (2 * P + 1 >= run0 + k) rr[2 * q + 1] = ~0ull;
                     }
 #pragma unroll
-                    for (int q = 0; q < FU; q++) {
+                    for (int q = 0; q < 2 * FU; q++) {
                         const uint64_t r = rr[q], key = r >> 32;
                         if (r == ~0ull) continue;
                         if (((r >> 26) & 63u) > reg[pfl_slotb(key)]) {

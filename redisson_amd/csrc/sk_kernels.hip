@@ -2075,11 +2075,17 @@ extern "C" hipError_t sk_rc_stamp_read(unsigned long long *out) {
 __host__ __device__ __forceinline__ uint64_t rc_sidx(uint32_t r, uint32_t j, uint32_t NB) {
     return (uint64_t(r / SK_RC_STILE) * NB + j) * SK_RC_STILE + (r % SK_RC_STILE);
 }
+#ifndef RC_RB
 #define RC_RB 20                      // region = 2^20 bits = 128 KiB
+#endif
 #define RC_TPB 1024
 #define RC_EPB 4096                   // elements per hash block (12-bit element-in-block)
+#ifndef RC_PMAX
 #define RC_PMAX 8                     // probes per element handled here (k <= 9)
+#endif
+#ifndef RC_NRMAX
 #define RC_NRMAX 4096                 // regions (bit arrays <= 2^32 bits)
+#endif
 #define RC_ROUNDS (RC_EPB / RC_TPB)
 // add: elements per hash block.  4096 while the block's records (4096 x k u32) fit LDS beside the key windows and
 // the region counts (k <= RA_K4), else 2048: twice the records per (block, region) segment and half the segment
@@ -2385,7 +2391,9 @@ __device__ __forceinline__ void rc_test_seg(const uint8_t *fb, const uint32_t *c
 #endif
 #define RC_GB 16                         // hash blocks per reply group: 64 Ki replies, a 64 KiB LDS map
 #define RC_NG (RC_SMAX * RC_TPB / RC_GB) // reply groups per piece (<= 512)
+#ifndef RC_ZCAP
 #define RC_ZCAP 7424                     // zero-list entries per region (LDS beside the 128 KiB region)
+#endif
 static_assert((1u << (RC_RB - 3)) >= RC_ZCAP * 4, "the sorted list fits the region area");
 // SK_RC_TV: the probe's word tests without branches, and the wave scan of the zero-hit counts on DPP row shifts and
 // broadcasts (6 adds) instead of six shuffles through LDS
@@ -2658,7 +2666,9 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_rc_probe(uint32_t NB, uint32_t
 #ifndef SK_RC_PERSIST
 #define SK_RC_PERSIST 1
 #endif
+#ifndef RC_PSLOTS
 #define RC_PSLOTS 32 // workgroups per XCD group (8 x 32 = 256 = one per CU)
+#endif
 #ifndef SK_RC_PCOL
 // 1: the probe reads the hash blocks' interleaved segment table St itself (no k_rc_stranspose): an XCD group starts
 // on a multiple of SK_RC_STILE regions, so its 32 workgroups test one interleave group's regions at a time and the

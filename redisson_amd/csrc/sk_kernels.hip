@@ -2275,7 +2275,7 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_rc_hash(uint64_t n, const uint
 __global__ void __launch_bounds__(256) k_rc_stranspose(const uint32_t *__restrict__ St, uint32_t *__restrict__ S,
                                                        uint32_t NB, uint32_t NR) {
     constexpr uint32_t T = SK_RC_STILE, TJ = RC_STJ;
-    static_assert(T % 4 == 0 && TJ % 4 == 0, "16-B vectors on both sides");
+    static_assert(T == 1 || (T % 4 == 0 && TJ % 4 == 0), "16-B vectors on both sides"); // T = 1: never launched
     __shared__ uint32_t tile[TJ][T + 1];
     const uint32_t j0 = blockIdx.x * TJ, rt = blockIdx.y;
     for (uint32_t e = threadIdx.x; e < TJ * T / 4; e += 256) {

@@ -977,6 +977,12 @@ __global__ void __launch_bounds__(SK_PFP_ATPB) __attribute__((amdgpu_waves_per_e
 #ifndef SK_PFL_LDS
 #define SK_PFL_LDS (160 * 1024 - 9 * 1024) // dynamic LDS of a region workgroup: records + fine-bucket counts
 #endif
+#ifndef SK_PFL_WFU
+#define SK_PFL_WFU 4       // wave-loaded pair steps in flight per thread
+#endif
+#ifndef SK_PFL_WAVELD
+#define SK_PFL_WAVELD 1    // the apply's big runs: a wave's packed pairs as three coalesced word loads + ds_bpermute
+#endif
 #ifndef SK_PFL_R6
 #define SK_PFL_R6 2        // rec2 as 6-B records packed back to back (0: u64)
 #endif
@@ -1013,7 +1019,7 @@ struct PflRec {
         w[2] = uint32_t(r1);
     }
     // records 2P and 2P + 1
-    __device__ __forceinline__ void get_pair(uint64_t P, uint64_t *r0, uint64_t *r1) const {
+    __device__ __forceinline__ void get_pair(uint32_t P, uint64_t *r0, uint64_t *r1) const { // slots < 2^26
         if (SK_PFL_R6 == 2) {
             const uint32_t *w = reinterpret_cast<const uint32_t *>(p) + 3 * P;
             const uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
@@ -1507,29 +1513,65 @@ __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const PflRec rec2,
                 __syncthreads();
                 // records in pairs (a packed pair is three aligned words: one load), FU of them in flight per
                 // thread; the run's slots [run0, run0 + k) may start and end inside a pair
-                constexpr int FU = 4;
-                const uint64_t pe0 = run0 >> 1, pe1 = (run0 + k + 1) >> 1;
-                for (uint64_t p0 = pe0; p0 < pe1; p0 += FU * SK_PFL_ATPB) {
+                constexpr int FU = SK_PFL_R6 == 2 && SK_PFL_WAVELD ? SK_PFL_WFU : 4;
+                auto consider = [&](uint64_t r) { // a record of the run: a candidate, or its reply is 0 now
+                    if (r == ~0ull) return;
+                    const uint64_t key = r >> 32;
+                    if (((r >> 26) & 63u) > reg[pfl_slotb(key)]) {
+                        const uint32_t i = atomicAdd(&ncand, 1u);
+                        if (i < SK_PFL_CAP) R[i] = r;
+                    } else {
+                        put(uint32_t(r & 0x3ffffffu), 0u);
+                    }
+                };
+                const uint32_t r0s = rs[t0], r1s = r0s + k, pe0 = r0s >> 1, pe1 = (r1s + 1) >> 1; // slots < 2^26
+                for (uint32_t p0 = pe0; p0 < pe1; p0 += FU * SK_PFL_ATPB) {
+#if SK_PFL_R6 == 2 && SK_PFL_WAVELD
+                    // packed: each wave reads its 64 pairs (192 words) as three coalesced word loads, and every lane
+                    // gathers its pair's three words from the holders (ds_bpermute)
+                    const uint32_t lane = threadIdx.x & 63u;
+                    uint32_t a[FU][3];
+#pragma unroll
+                    for (int q = 0; q < FU; q++) {
+                        const uint32_t Pq = p0 + q * SK_PFL_ATPB + (threadIdx.x - lane); // the wave's first pair
+                        const uint32_t lim = pe1 > Pq ? 3 * (pe1 - Pq) : 0u;             // its words in the run
+                        const uint32_t *wb = reinterpret_cast<const uint32_t *>(rec2.p) + 3 * uint64_t(Pq);
+#pragma unroll
+                        for (int j = 0; j < 3; j++) a[q][j] = lane + 64 * j < lim ? wb[lane + 64 * j] : 0u;
+                    }
+#pragma unroll
+                    for (int q = 0; q < FU; q++) {
+                        // lane l takes the wave's records l and 64 + l (consecutive lanes, consecutive records)
+                        auto take = [&](uint32_t d) -> uint32_t { // word d of the wave's 192
+                            const int src = int(d & 63u) << 2;
+                            const uint32_t x0 = __builtin_amdgcn_ds_bpermute(src, int(a[q][0])),
+                                           x1 = __builtin_amdgcn_ds_bpermute(src, int(a[q][1])),
+                                           x2 = __builtin_amdgcn_ds_bpermute(src, int(a[q][2]));
+                            return d < 64 ? x0 : d < 128 ? x1 : x2;
+                        };
+                        const uint32_t Pq = p0 + q * SK_PFL_ATPB + (threadIdx.x - lane), odd = lane & 1u;
+#pragma unroll
+                        for (int m = 0; m < 2; m++) {
+                            const uint32_t pr = (lane >> 1) + 32u * m;           // the record's pair in the wave
+                            const uint32_t lo = take(3 * pr + 2 * odd), hw = take(3 * pr + 1);
+                            const uint32_t slot = 2 * (Pq + pr) + odd;
+                            if (Pq + pr < pe1 && slot >= r0s && slot < r1s)
+                                consider(PflRec::unpack(lo, odd ? hw >> 16 : hw & 0xffffu));
+                        }
+                    }
+#else
                     uint64_t rr[2 * FU];
 #pragma unroll
                     for (int q = 0; q < FU; q++) {
-                        const uint64_t P = p0 + q * SK_PFL_ATPB + threadIdx.x;
+                        const uint32_t P = p0 + q * SK_PFL_ATPB + threadIdx.x;
                         rr[2 * q] = rr[2 * q + 1] = ~0ull;
                         if (P < pe1) rec2.get_pair(P, &rr[2 * q], &rr[2 * q + 1]);
-                        if (2 * P < run0) rr[2 * q] = ~0ull;
-                        if (2 * P + 1 >= run0 + k) rr[2 * q + 1] = ~0ull;
+                        if (2 * P < r0s) rr[2 * q] = ~0ull;
+                        if (2 * P + 1 >= r1s) rr[2 * q + 1] = ~0ull;
                     }
 #pragma unroll
-                    for (int q = 0; q < 2 * FU; q++) {
-                        const uint64_t r = rr[q], key = r >> 32;
-                        if (r == ~0ull) continue;
-                        if (((r >> 26) & 63u) > reg[pfl_slotb(key)]) {
-                            const uint32_t i = atomicAdd(&ncand, 1u);
-                            if (i < SK_PFL_CAP) R[i] = r;
-                        } else {
-                            put(uint32_t(r & 0x3ffffffu), 0u);
-                        }
-                    }
+                    for (int q = 0; q < 2 * FU; q++) consider(rr[q]);
+#endif
                 }
                 __syncthreads();
                 const uint32_t nc = ncand;

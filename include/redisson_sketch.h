@@ -321,7 +321,8 @@ int sk_timer_elapsed(sk_ctx *ctx, int slot_a, int slot_b, float *ms);
  * "setbit", "getbit", "bitcount", "bitop", "pfadd_claim", "pfadd_commit",
  * "pfp_hash", "pfp_apply", "pfp_reply", "bloom_rc_hash", "bloom_rc_probe",
  * "pfadd_long", "bloom_ra_hash", "bloom_ra_apply", "pfl_hash", "pfl_part",
- * "pfl_apply", "hll_sum";
+ * "pfl_apply" (k_pfl_plan + k_pfl_apply), "hll_sum", "pfl_fill" (the
+ * line schedule's default-reply fill);
  * chains: "bloom_contains" (every kernel of one contains call), "pfadd" (every
  * kernel of one sk_pfadd_dev batch).  "pfadd_long_fallback" is a count, not a
  * time: calls whose long elements (>= 64 KiB) were re-hashed per thread because
@@ -344,10 +345,14 @@ int sk_prof_read(sk_ctx *ctx, const char *phase, uint64_t *launches, double *tot
  * writes), else on its first HLL command, as after SET. */
 
 /* SCAN: up to `count` keys from `cursor` (0 = start); *next_cursor = 0 when the scan is done.  Every key present
- * for the whole scan is returned once.  names: the key bytes, name_off u64[*out_n + 1] into it (stops early rather
+ * for the whole scan is returned once: a key's position is a hash of its name, so it holds across type changes
+ * (a string adopted as an HLL) and replacement; keys sharing a position are never split between calls (a call may
+ * then return fewer than `count`).  names: the key bytes, name_off u64[*out_n + 1] into it (stops early rather
  * than pass names_cap); types: SK_TYPE_HLL / SK_TYPE_STRING / SK_TYPE_HASH (a Bloom filter config). */
 int sk_scan(sk_ctx *ctx, uint64_t cursor, uint32_t count, uint64_t *next_cursor, uint32_t *out_n,
             uint64_t *name_off, uint8_t *names, uint64_t names_cap, int32_t *types);
+/* DBSIZE: the number of keys the store holds (HLLs, strings, Bloom filter configs), O(1) */
+int sk_dbsize(sk_ctx *ctx, uint64_t *out);
 /* DUMP key: the redis-server DUMP payload (type, value, RDB version, CRC64).  *out_len = its size (-1: no such
  * key); at most cap bytes are copied (call with cap = 0 to size the buffer). */
 int sk_dump(sk_ctx *ctx, const uint8_t *key, uint64_t len, uint8_t *buf, uint64_t cap, int64_t *out_len);

@@ -18,6 +18,7 @@
  * is order-free (register max, bit OR) or per-owner ordered (PFADD replies).
  */
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 #include <pthread.h>
 #include <stdint.h>
@@ -37,13 +38,17 @@ typedef struct {
     uint64_t strlen_bytes;
     int64_t size;
     int32_t k;
+    /* PFADD: the commands of owner t are own[own_start[t] .. own_start[t + 1]) (routed once, in batch order) */
+    const uint32_t *own, *own_start;
 } mt_arg;
+
+#define OR_MT_MAX_THREADS 1024
 
 static void *pfadd_owned(void *p) {
     mt_arg *a = (mt_arg *)p;
-    for (uint32_t c = 0; c < a->n; c++) {
+    for (uint32_t j = a->own_start[a->t]; j < a->own_start[a->t + 1]; j++) {
+        uint32_t c = a->own[j];
         uint32_t key = a->key_ids[c];
-        if ((int)(key % (uint32_t)a->T) != a->t) continue;
         uint8_t *regs = a->regs_base + (uint64_t)key * OR_HLL_REGISTERS;
         int updated = 0;
         if (!a->exists[key]) {
@@ -67,10 +72,8 @@ static void *contains_range(void *p) {
 }
 
 static void run(int T, mt_arg *base, void *(*fn)(void *)) {
-    pthread_t th[256];
-    mt_arg args[256];
-    if (T > 256) T = 256;
-    if (T < 1) T = 1;
+    pthread_t *th = (pthread_t *)malloc(sizeof(pthread_t) * (size_t)T);
+    mt_arg *args = (mt_arg *)malloc(sizeof(mt_arg) * (size_t)T);
     for (int t = 0; t < T; t++) {
         args[t] = *base;
         args[t].t = t;
@@ -78,7 +81,10 @@ static void run(int T, mt_arg *base, void *(*fn)(void *)) {
         pthread_create(&th[t], NULL, fn, &args[t]);
     }
     for (int t = 0; t < T; t++) pthread_join(th[t], NULL);
+    free(th);
+    free(args);
 }
+static int clampMT(int T) { return T < 1 ? 1 : (T > OR_MT_MAX_THREADS ? OR_MT_MAX_THREADS : T); }
 
 /* one element per command; regs_base: n_keys x 16384 registers, exists: n_keys flags */
 void or_pfadd_owned_mt(uint8_t *regs_base, uint8_t *exists, uint32_t n, const uint32_t *key_ids,
@@ -93,7 +99,21 @@ void or_pfadd_owned_mt(uint8_t *regs_base, uint8_t *exists, uint32_t n, const ui
     a.off = elem_off;
     a.bytes = elem_bytes;
     a.redis_major = redis_major;
-    run(nthreads, &a, pfadd_owned);
+    /* client-side routing (key id % T), once per batch: each owner's commands in batch order */
+    int T = clampMT(nthreads);
+    uint32_t *start = (uint32_t *)calloc((size_t)T + 1, sizeof(uint32_t));
+    uint32_t *own = (uint32_t *)malloc(sizeof(uint32_t) * ((size_t)n + 1));
+    for (uint32_t c = 0; c < n; c++) start[key_ids[c] % (uint32_t)T + 1]++;
+    for (int t = 0; t < T; t++) start[t + 1] += start[t];
+    uint32_t *pos = (uint32_t *)malloc(sizeof(uint32_t) * (size_t)T);
+    memcpy(pos, start, sizeof(uint32_t) * (size_t)T);
+    for (uint32_t c = 0; c < n; c++) own[pos[key_ids[c] % (uint32_t)T]++] = c;
+    a.own = own;
+    a.own_start = start;
+    run(T, &a, pfadd_owned);
+    free(pos);
+    free(own);
+    free(start);
 }
 
 void or_bloom_contains_mt(const uint8_t *buf, uint64_t strlen_bytes, int64_t size, int32_t k, uint32_t n,
@@ -107,7 +127,7 @@ void or_bloom_contains_mt(const uint8_t *buf, uint64_t strlen_bytes, int64_t siz
     a.off = elem_off;
     a.bytes = elem_bytes;
     a.out = out;
-    run(nthreads, &a, contains_range);
+    run(clampMT(nthreads), &a, contains_range);
 }
 
 

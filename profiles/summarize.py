@@ -21,6 +21,21 @@ def main(src, tag, into=None):
     out = into or os.path.dirname(os.path.abspath(__file__))
     os.makedirs(out, exist_ok=True)
     shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(out, f"{tag}_kernel_stats.csv"))
+    # per-kernel dispatch durations from the trace: mean, the mean without each kernel's first dispatch (the bench's
+    # warm-up call: cold TLBs / L2 after the setup), median -- the bench's own per-kernel timing skips its warm-up
+    tr = os.path.join(src, "trace", "run_kernel_trace.csv")
+    if os.path.exists(tr):
+        durs = defaultdict(list)
+        for r in csv.DictReader(open(tr)):
+            nm = r["Kernel_Name"].split("(")[0].replace("void ", "")
+            durs[nm].append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]) - int(r["Start_Timestamp"])))
+        steady = {}
+        for nm, v in durs.items():
+            d = [x[1] for x in sorted(v)]
+            rest = d[1:] or d
+            steady[nm] = {"dispatches": len(d), "mean_ns": sum(d) / len(d), "mean_ns_after_first": sum(rest) / len(rest),
+                          "median_ns": sorted(d)[len(d) // 2], "first_ns": d[0]}
+        json.dump({"source": src, "kernels": steady}, open(os.path.join(out, f"{tag}_kernel_steady.json"), "w"), indent=1)
     res = defaultdict(dict)
     for sub, ctr in [("pmc_fetch", "FETCH_SIZE"), ("pmc_write", "WRITE_SIZE")]:
         acc = defaultdict(list)

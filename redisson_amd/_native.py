@@ -133,6 +133,7 @@ SIGNATURES = {
     "sk_allgather": (c_int, [P, P, P, c_uint64]),
     # persistence: SCAN / DUMP / RESTORE / SAVE / load (redis-server's formats)
     "sk_scan": (c_int, [P, c_uint64, c_uint32, P, P, P, P, c_uint64, P]),
+    "sk_dbsize": (c_int, [P, P]),
     "sk_dump": (c_int, [P, _u8p, c_uint64, _u8p, c_uint64, _i64p]),
     "sk_restore": (c_int, [P, _u8p, c_uint64, _u8p, c_uint64, c_int]),
     "sk_save": (c_int, [P, c_char_p, c_uint32, P, P, P]),

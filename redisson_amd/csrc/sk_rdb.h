@@ -196,6 +196,10 @@ inline bool load_string(Reader &r, std::string &out) {
             const uint64_t clen = r.plain_len(), ulen = r.plain_len();
             const uint8_t *c;
             if (!r.ok || !r.take(clen, &c)) return false;
+            // bound the allocation by what clen can decompress to: the longest LZF back-reference (3 bytes) yields
+            // 264 bytes, literal runs never expand, so ulen <= 88 * clen; and no string past 4 GiB (the engine's
+            // largest bit string is 2 GiB at max_bit_offset 2^34)
+            if (ulen > clen * 88 || ulen > (uint64_t(1) << 32)) return r.ok = false;
             out.assign(ulen, '\0');
             return lzf_decompress(c, clen, reinterpret_cast<uint8_t *>(&out[0]), ulen) || (r.ok = false);
         } else {

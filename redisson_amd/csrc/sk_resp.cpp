@@ -212,13 +212,17 @@ struct Server {
     // every key name: the engine's (a full SCAN) then this process's hashes
     std::vector<std::string> all_keys() {
         std::vector<std::string> out;
-        uint64_t cur = 0;
-        std::vector<uint64_t> off(1025);
-        std::vector<uint8_t> names(1 << 20);
-        std::vector<int32_t> types(1024);
+        uint64_t cur = 0, nk = 0;
+        if (sk_dbsize(ctx, &nk) != SK_OK) return out;
+        // one SCAN call for the whole keyspace (a second only if the names outgrow the buffer): O(N log N), not a
+        // full pass per 1024 keys
+        const uint32_t want = uint32_t(std::min<uint64_t>(nk + 64, 0xfffffff0u));
+        std::vector<uint64_t> off(want + 1);
+        std::vector<uint8_t> names(std::max<uint64_t>(1 << 20, nk * 48));
+        std::vector<int32_t> types(want);
         do {
             uint32_t n = 0;
-            if (sk_scan(ctx, cur, 1024, &cur, &n, off.data(), names.data(), names.size(), types.data()) != SK_OK) break;
+            if (sk_scan(ctx, cur, want, &cur, &n, off.data(), names.data(), names.size(), types.data()) != SK_OK) break;
             for (uint32_t i = 0; i < n; i++)
                 out.emplace_back(reinterpret_cast<const char *>(names.data()) + off[i], off[i + 1] - off[i]);
         } while (cur);
@@ -524,7 +528,11 @@ struct Server {
             r_array(o, ks.size());
             for (auto &k : ks) r_bulk(o, k);
         } else if (name == "dbsize") {
-            if (arity(1, false)) r_int(o, (long long)all_keys().size());
+            uint64_t nk = 0;
+            if (arity(1, false)) {
+                if (sk_dbsize(ctx, &nk) != SK_OK) return r_error(o, engine_error()), true;
+                r_int(o, (long long)(nk + hashes.size()));
+            }
         } else if (name == "scan") {
             // SCAN cursor [MATCH pattern] [COUNT n]: the engine's cursor, then one last step with this process's
             // hashes (cursor kHashStep)

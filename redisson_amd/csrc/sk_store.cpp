@@ -492,8 +492,9 @@ const char *kPhaseNames[] = {"pfadd_hash",  "pfadd_sort",   "pfadd_apply", "hll_
                              "getbit",      "bitcount",     "bitop",       "pfadd_claim", "pfadd_commit",
                              "pfp_hash",    "pfp_apply",    "pfp_reply",   "bloom_rc_hash", "bloom_rc_probe", "pfadd",
                              "pfadd_long",  "bloom_ra_hash", "bloom_ra_apply", "pfl_hash",   "pfl_part",
-                             "pfl_apply",   "hll_sum"};
+                             "pfl_apply",   "hll_sum",      "pfl_fill"};
 constexpr int kNumPhases = sizeof(kPhaseNames) / sizeof(kPhaseNames[0]);
+static_assert(kNumPhases <= 32, "prof_ms / prof_n / prof_mask hold 32 phases");
 
 hipEvent_t ev_get(sk_ctx *c) {
     if (!c->ev_pool.empty()) {
@@ -1072,7 +1073,7 @@ int pfadd_lines(sk_ctx *c, uint64_t n, const uint32_t *d_ids, const uint64_t *d_
     // (slab id >= nslab: no register, reply 0), so the default never overwrites those.
     const uint32_t par = c->pfl_par;
     c->pfl_par ^= 1;
-    { Prof p_(c, 26);
+    { Prof p_(c, 28);
     if (c->pfl_zero) HIPCHK(c, sk::launch_pfl_fill(c->st, d_changed, n, c->pfl_rc.as<uint32_t>(), par)); }
     { Prof p_(c, 25);
     HIPCHK(c, sk::launch_pfl_part(c->st, d, c->pfl_chunks.as<uint64_t>(), c->pfl_S.as<uint32_t>(),
@@ -3440,6 +3441,11 @@ int bloom_from_fields(sk_ctx *c, const sk_rdb::Fields &f, BloomCfg *out) {
     if (!size || !hi || !parse_i64(*size, &sz) || !parse_i64(*hi, &k) || (ex && !parse_i64(*ex, &e)))
         return fail(c, SK_EINVAL,
                     "ERR the sketch store keeps hashes only as Bloom filter configs (integer size and hashIterations)");
+    // what tryInit can produce (M:RedissonBloomFilter.java:52,72-74): the probe kernels index bits in 32-bit words
+    // (sizes < 2^32), and readConfig's Integer.valueOf refuses a hashIterations past int range (:217)
+    if (sz < 1 || sz > kBloomMaxSize || k < 1 || k > INT32_MAX)
+        return fail(c, SK_EINVAL, "ERR Bloom filter config out of range: size %lld (1..%lld), hashIterations %lld",
+                    (long long)sz, (long long)kBloomMaxSize, (long long)k);
     *out = BloomCfg{sz, int32_t(k), e, fp ? std::strtod(fp->c_str(), nullptr) : 0.0, f, 0};
     return SK_OK;
 }
@@ -3463,62 +3469,107 @@ int hll_bulk_flush(sk_ctx *c, HllBulk &b) {
     return r;
 }
 
-// the restored value of key k (already absent from the store); HLLs adopted at once go through `bulk`
-int restore_value(sk_ctx *c, const std::string &k, sk_rdb::Value &v, HllBulk &bulk) {
+// a restored value, everything it needs already allocated, so that RESTORE ... REPLACE / load delete the old key
+// only once the new value is certain to go in (redis-server decodes the object before it deletes the old key)
+struct Restored {
+    int kind = 0; // 1 Bloom config, 2 HLL, 3 string
+    BloomCfg b;
+    uint32_t id = kNoId;
+    std::vector<uint8_t> body; // HLL: its 12,288-B dense body
+};
+int restore_prepare(sk_ctx *c, sk_rdb::Value &v, Restored &p) {
     if (v.type == sk_rdb::kTypeHash) {
-        BloomCfg b;
-        int r = bloom_from_fields(c, v.fields, &b);
-        if (r) return r;
-        b.seq = c->bloom_seq++;
-        c->bloom[k] = std::move(b);
-        return SK_OK;
+        p.kind = 1;
+        return bloom_from_fields(c, v.fields, &p.b);
     }
     if (hll_eager(c, v.bytes)) {
         const uint8_t *s = reinterpret_cast<const uint8_t *>(v.bytes.data());
-        std::vector<uint8_t> regs;
         const bool dense = s[4] == 0 && v.bytes.size() == SK_HLL_DENSE_SIZE; // any dense body decodes
+        std::vector<uint8_t> regs;
         if (!dense) regs.resize(kHllBytes);
         if (dense || hll_decode(s, v.bytes.size(), regs.data()) == SK_OK) {
-            uint32_t id;
-            int r = hll_alloc(c, &id);
-            if (r) return r;
-            c->keys[k] = KeyEnt{SK_TYPE_HLL, id};
-            if (c->hll_exact) {
-                HllStr &h = c->hstr[id];
-                std::memcpy(h.hdr, s, 16);
-                h.sparse = s[4] == 1;
-                if (h.sparse) h.ops.assign(s + 16, s + v.bytes.size());
-                else std::vector<uint8_t>().swap(h.ops);
-            }
-            const size_t at = bulk.bodies.size();
-            bulk.bodies.resize(at + 12288);
+            p.body.resize(12288);
             if (dense) {
-                std::memcpy(&bulk.bodies[at], s + 16, 12288);
+                std::memcpy(p.body.data(), s + 16, 12288);
             } else { // sparse (exact mode): its registers in the dense layout
                 std::vector<uint8_t> d(SK_HLL_DENSE_SIZE);
                 hll_dense_encode(regs.data(), nullptr, d.data());
-                std::memcpy(&bulk.bodies[at], d.data() + 16, 12288);
+                std::memcpy(p.body.data(), d.data() + 16, 12288);
             }
-            bulk.ids.push_back(id);
-            return bulk.ids.size() >= 8192 ? hll_bulk_flush(c, bulk) : SK_OK;
+            p.kind = 2;
+            return hll_alloc(c, &p.id);
         }
     }
-    uint32_t id;
-    int r = str_get(c, k, true, v.bytes.size(), &id);
-    if (r) return r;
+    p.kind = 3;
+    return str_alloc(c, v.bytes.size(), &p.id);
+}
+// undo a prepare whose key could not be installed
+void restore_release(sk_ctx *c, Restored &p) {
+    if (p.kind == 2 && p.id != kNoId) {
+        c->hll_live[p.id] = 0;
+        c->hll_free.push_back(p.id);
+    } else if (p.kind == 3 && p.id != kNoId) {
+        (void)str_free(c, p.id);
+    }
+    p.kind = 0;
+}
+// install the prepared value as key k (already absent from the store); HLL bodies go through `bulk`
+int restore_commit(sk_ctx *c, const std::string &k, sk_rdb::Value &v, Restored &p, HllBulk &bulk) {
+    if (p.kind == 1) {
+        p.b.seq = c->bloom_seq++;
+        c->bloom[k] = std::move(p.b);
+        return SK_OK;
+    }
+    if (p.kind == 2) {
+        c->keys[k] = KeyEnt{SK_TYPE_HLL, p.id};
+        if (c->hll_exact) {
+            const uint8_t *s = reinterpret_cast<const uint8_t *>(v.bytes.data());
+            HllStr &h = c->hstr[p.id];
+            std::memcpy(h.hdr, s, 16);
+            h.sparse = s[4] == 1;
+            if (h.sparse) h.ops.assign(s + 16, s + v.bytes.size());
+            else std::vector<uint8_t>().swap(h.ops);
+        }
+        bulk.bodies.insert(bulk.bodies.end(), p.body.begin(), p.body.end());
+        bulk.ids.push_back(p.id);
+        return bulk.ids.size() >= 8192 ? hll_bulk_flush(c, bulk) : SK_OK;
+    }
+    c->keys[k] = KeyEnt{SK_TYPE_STRING, p.id};
     if (!v.bytes.empty())
-        HIPCHK(c, hipMemcpyAsync(c->strs[id].ptr, v.bytes.data(), v.bytes.size(), hipMemcpyHostToDevice, c->st));
-    if ((r = sync(c))) return r;
-    return str_set_len(c, id, v.bytes.size());
+        HIPCHK(c, hipMemcpyAsync(c->strs[p.id].ptr, v.bytes.data(), v.bytes.size(), hipMemcpyHostToDevice, c->st));
+    int r = sync(c);
+    if (r) return r;
+    return str_set_len(c, p.id, v.bytes.size());
+}
+// prepare, then delete the old key, then install
+int restore_replace(sk_ctx *c, const std::string &k, sk_rdb::Value &v, HllBulk &bulk) {
+    Restored p;
+    int r = restore_prepare(c, v, p);
+    if (r) {
+        restore_release(c, p);
+        return r;
+    }
+    bool removed;
+    if ((r = del_key(c, k, &removed))) {
+        restore_release(c, p);
+        return r;
+    }
+    return restore_commit(c, k, v, p, bulk);
 }
 
 } // namespace
 
 extern "C" {
 
-// SCAN: positions (type class << 56 | slab / string id / config sequence) are unique and stable while a key lives,
-// so the cursor is "the next position" (+ 1, 0 = start); a call returns the `count` keys of lowest position at or
-// after it
+// SCAN: a key's position is a 61-bit hash of its name (FNV-1a), so it does not move when the key changes type (a
+// string adopted as an HLL, SET over an HLL) or is replaced; the cursor is "the next position" (+ 1, 0 = start).  A call
+// returns up to `count` keys of lowest position at or after it, and never splits keys of one position between calls
+// (a 61-bit collision), so every key present for the whole scan is returned once.
+static uint64_t scan_pos(const std::string &k) {
+    uint64_t h = 0xcbf29ce484222325ull;
+    for (unsigned char ch : k) h = (h ^ ch) * 0x100000001b3ull;
+    return h >> 3;
+}
 int sk_scan(sk_ctx *c, uint64_t cursor, uint32_t count, uint64_t *next_cursor, uint32_t *out_n, uint64_t *name_off,
             uint8_t *names, uint64_t names_cap, int32_t *types) {
     std::lock_guard<std::mutex> g(c->mu);
@@ -3536,15 +3587,22 @@ int sk_scan(sk_ctx *c, uint64_t cursor, uint32_t count, uint64_t *next_cursor, u
     std::vector<Ent> all;
     all.reserve(c->keys.size() + c->bloom.size());
     for (auto &kv : c->keys) {
-        const uint64_t pos = (uint64_t(kv.second.type == SK_TYPE_HLL ? 0 : 1) << 56) | kv.second.id;
+        const uint64_t pos = scan_pos(kv.first);
         if (pos >= from) all.push_back(Ent{pos, &kv.first, kv.second.type});
     }
     for (auto &kv : c->bloom) {
-        const uint64_t pos = (2ull << 56) | kv.second.seq;
+        const uint64_t pos = scan_pos(kv.first);
         if (pos >= from) all.push_back(Ent{pos, &kv.first, SK_TYPE_HASH});
     }
-    const size_t take = std::min<size_t>(count, all.size());
-    std::partial_sort(all.begin(), all.begin() + take, all.end(), [](const Ent &x, const Ent &y) { return x.pos < y.pos; });
+    auto lt = [](const Ent &x, const Ent &y) { return x.pos < y.pos || (x.pos == y.pos && *x.name < *y.name); };
+    size_t take = std::min<size_t>(count, all.size());
+    std::partial_sort(all.begin(), all.begin() + take, all.end(), lt);
+    if (take && take < all.size()) { // a position's keys stay together (a hash collision): the last one's wait
+        const uint64_t last = all[take - 1].pos;
+        if (std::any_of(all.begin() + take, all.end(), [&](const Ent &e) { return e.pos == last; }))
+            while (take > 0 && all[take - 1].pos == last) take--;
+        if (!take) return fail(c, SK_EINVAL, "sk_scan: count %u is too small for the keys of one position", count);
+    }
     uint64_t used = 0;
     size_t n = 0;
     for (; n < take; n++) {
@@ -3555,10 +3613,18 @@ int sk_scan(sk_ctx *c, uint64_t cursor, uint32_t count, uint64_t *next_cursor, u
         name_off[n + 1] = used;
         types[n] = all[n].type;
     }
-    if (n == 0 && take) return fail(c, SK_EINVAL, "sk_scan: names_cap %llu is too small for the next key",
+    // a stop for names_cap must not split one position's keys either
+    while (n > 0 && n < take && all[n].pos == all[n - 1].pos) n--;
+    if (n == 0 && take) return fail(c, SK_EINVAL, "sk_scan: names_cap %llu is too small for the next keys",
                                     (unsigned long long)names_cap);
     *out_n = uint32_t(n);
     if (n < all.size()) *next_cursor = all[n - 1].pos + 2;
+    return SK_OK;
+}
+
+int sk_dbsize(sk_ctx *c, uint64_t *out) {
+    std::lock_guard<std::mutex> g(c->mu);
+    *out = uint64_t(c->keys.size() + c->bloom.size());
     return SK_OK;
 }
 
@@ -3584,11 +3650,9 @@ int sk_restore(sk_ctx *c, const uint8_t *key, uint64_t len, const uint8_t *paylo
         return fail(c, SK_EPAYLOAD, "ERR %s", why.c_str());
     if (!replace && (c->keys.count(k) || c->bloom.count(k)))
         return fail(c, SK_EBUSYKEY, "BUSYKEY Target key name already exists.");
-    bool removed;
-    int r = del_key(c, k, &removed);
-    if (r) return r;
     HllBulk bulk;
-    if ((r = restore_value(c, k, v, bulk))) return r;
+    int r = restore_replace(c, k, v, bulk);
+    if (r) return r;
     if ((r = hll_bulk_flush(c, bulk))) return r;
     return sync(c);
 }
@@ -3723,9 +3787,7 @@ int sk_load(sk_ctx *c, const char *path, sk_take_fn take, void *user, uint64_t *
             if (t < 0) return std::string("the caller refused the hash ") + key;
             if (t == 1) return std::string();
         }
-        bool removed;
-        if ((rc = del_key(c, key, &removed)) || (rc = restore_value(c, key, v, bulk)))
-            return std::string("store error: ") + c->err;
+        if ((rc = restore_replace(c, key, v, bulk))) return std::string("store error: ") + c->err;
         return std::string();
     });
     if (why.empty() && (rc = hll_bulk_flush(c, bulk))) why = "store error: " + c->err;

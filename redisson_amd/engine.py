@@ -570,6 +570,12 @@ class SketchEngine:
         raw = names.tobytes()
         return nxt.value, [(raw[off[i]:off[i + 1]], int(types[i])) for i in range(n.value)]
 
+    def dbsize(self) -> int:
+        """DBSIZE: keys in the store (HLLs, strings, Bloom filter configs)."""
+        n = ctypes.c_uint64()
+        self._check(self.lib.sk_dbsize(self.ctx, ctypes.addressof(n)))
+        return n.value
+
     def keys(self) -> List[tuple]:
         """Every (key, type) of the store, by a full SCAN."""
         out, cur = [], 0

@@ -440,6 +440,17 @@ void rdb_known(long it) {
     check(sk_rdb::lzf_decompress(reinterpret_cast<const uint8_t *>(lz.data()), lz.size(),
                                  reinterpret_cast<uint8_t *>(&out[0]), 10) && out == std::string(10, 'a'),
           "lzf back reference", it);
+    // an LZF string claiming a huge uncompressed length: refused before any allocation, valid CRC
+    for (uint64_t ulen : {uint64_t(1) << 40, uint64_t(1) << 33, uint64_t(5) * 88 + 1}) {
+        std::string pl(1, char(sk_rdb::kTypeString));
+        pl.push_back(char(0xc3));
+        sk_rdb::put_len(pl, 5);
+        sk_rdb::put_len(pl, ulen);
+        pl += bytes_of({0x00, 'a', 0xe0, 0xff, 0x00});
+        sk_rdb::finish_payload(pl);
+        check(!sk_rdb::load_payload(reinterpret_cast<const uint8_t *>(pl.data()), pl.size(), v).empty(),
+              "huge LZF ulen refused", it);
+    }
     // a ziplist hash as redis 3.2 stores a small HMSET: "size" -> 729 (int16), "hashIterations" -> 5 (immediate)
     std::string ents;
     std::vector<size_t> sizes;

@@ -126,6 +126,60 @@ def test_dump_restore_scan_every_type(O, tmp_path):
         eng.close()
 
 
+def _hash_payload(fields):
+    """a DUMP payload of a hash (RDB type 4, plain encoding) with a valid CRC64"""
+    def ln(n):
+        return bytes([n]) if n < 64 else bytes([0x40 | (n >> 8), n & 0xFF])
+    body = bytes([4]) + ln(len(fields))
+    for f, v in fields:
+        body += ln(len(f)) + f + ln(len(v)) + v
+    body += bytes([7, 0])
+    return body + crc64(body).to_bytes(8, "little")
+
+
+def test_restore_refuses_bad_bloom_configs_and_keeps_the_old_key(O):
+    """a restored Bloom config must be one tryInit can make (1 <= size <= 4,294,967,294, hashIterations in
+    int range: the probe kernels index in 32-bit words); RESTORE ... REPLACE that fails leaves the old key alone
+    (redis-server decodes the object before it deletes the old key); DBSIZE counts every key; SCAN returns a key
+    once across its change of type (a string adopted as an HLL on its first PFADD)."""
+    from redisson_amd.engine import RedisException
+
+    eng = _engine()
+    try:
+        assert eng.bloom_try_init(b"bf", 100, 0.03)
+        eng.setbit([b"bits"], [9], [1])
+        good = eng.dump(b"{bf}__config")
+        assert parse_payload(_hash_payload([(b"size", b"729"), (b"hashIterations", b"5")]))[0] == 4
+        eng.restore(b"{ok}__config", _hash_payload([(b"size", b"729"), (b"hashIterations", b"5")]))
+        for size, k in ((b"4294967301", b"5"), (b"4294967295", b"5"), (b"0", b"5"), (b"729", b"4294967301"),
+                        (b"729", b"0"), (b"-3", b"5")):
+            with pytest.raises(RedisException, match="out of range"):
+                eng.restore(b"{bad}__config", _hash_payload([(b"size", size), (b"hashIterations", k)]))
+            with pytest.raises(RedisException, match="out of range"):
+                eng.restore(b"bits", _hash_payload([(b"size", size), (b"hashIterations", k)]), replace=True)
+            assert eng.get(b"bits") == b"\x00\x40", "a failed REPLACE deleted the old key"
+        assert eng.dump(b"{bad}__config") is None and eng.dump(b"{bf}__config") == good
+        n = eng.dbsize()
+        assert n == len(eng.keys()) == 3   # {bf}__config, bits, {ok}__config
+        # a string holding a dense HLL becomes an HLL on its first PFADD: its SCAN position holds
+        eng.pfadd([b"h"], [[b"x"]])
+        eng.set(b"s", eng.get(b"h"))
+        eng.delete([b"h"])
+        seen, cur, first = [], 0, True
+        while True:
+            cur, part = eng.scan(cur, 1)
+            seen += [k for k, _ in part]
+            if first:
+                eng.pfadd([b"s"], [[b"y"]])   # adopted between SCAN calls
+                first = False
+            if not cur:
+                break
+        assert sorted(seen) == sorted(set(seen)) and b"s" in seen and len(seen) == eng.dbsize() == 4
+        assert dict(eng.keys())[b"s"] == 1
+    finally:
+        eng.close()
+
+
 def test_exact_mode_sparse_strings_survive_save_load(O, tmp_path):
     """Exact HLL strings (redis-server's sparse bytes, sk_hll_exact_strings): SAVE / load keeps every GET byte for
     byte and the registers; in the default mode a sparse string from a redis-server file stays a string until its

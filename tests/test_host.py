@@ -229,3 +229,26 @@ def test_java_bloom_filter_makes_no_jni_call_on_the_callers_thread():
     co = open(os.path.join(ROOT, "java", "org", "redisson", "gpu", "GpuBloomCoalescer.java")).read()
     assert "public <T> void submitTask(Task<T> task, Promise<T> promise)" in co
     assert "if (head.task != null)" in co and "task == null && o.task == null" in co
+
+
+def test_newest_bench_record_is_physical():
+    """the newest committed bench line (profiles/*_bench.json) reports no per-kernel rate above the
+    8 TB/s HBM peak, every timed phase is one kernel family launched once per unit it names (the line schedule's
+    reply fill has its own phase), and the roofline fraction is <= 1."""
+    import glob
+    import json
+    import os
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    files = sorted(glob.glob(os.path.join(root, "profiles", "*_bench.json")))
+    assert files, "no committed bench record"
+    d = json.load(open(files[-1]))
+    for name, k in d["kernels"].items():
+        for f in ("GBps_isolated", "pmc_GBps_isolated"):
+            assert k.get(f) is None or k[f] <= 8000.0, (files[-1], name, f, k[f])
+    if "pfl_apply" in d["kernels"]:
+        assert d["kernels"]["pfl_apply"]["launches_per_step"] == 1, files[-1]
+    assert 0 < d["roofline"]["frac"] <= 1.0
+    cpu = d.get("cpu_baseline")
+    if cpu and "host" in cpu:
+        assert cpu["host"]["nproc"] and cpu["cores"] >= 1

@@ -243,6 +243,36 @@ def c5(eng, args):
                 t_set += dt
                 t_get += timed(eng, lambda: eng.getbit_dev(key, m, d_off, d_out))
             d_off.free()
+    # the C ABI the Java executors call: one 64 M-op RBatch run by key name from host buffers --
+    # SETBIT_VOID (no reply array), SETBIT with replies, GETBIT -- host-timed (key scan, pageable H2D, kernels, replies)
+    m = min(chunk, n)
+    h_off = rng.integers(0, bits, m, dtype=np.uint64)
+    kb_ = keys[0]
+    koff = np.arange(m + 1, dtype=np.uint64) * np.uint64(len(kb_))
+    kbuf = np.frombuffer(kb_ * m + b"\0" * 16, dtype=np.uint8)
+    ones = np.ones(m, dtype=np.uint8)
+    h_rep = np.zeros(m, dtype=np.uint8)
+    eng.setbit_packed(koff, kbuf, h_off[:1024], ones[:1024])                      # warm the paths
+    eng.setbit_packed(koff, kbuf, h_off[:1024], ones[:1024], h_rep[:1024])
+    eng.prof_reset()
+    eng.prof_enable(True)
+    t_hv = timed(eng, lambda: eng.setbit_packed(koff, kbuf, h_off, ones))
+    eng.prof_enable(False)
+    k_, ms_ = eng.prof_read("setbit")
+    hv_dev = ms_ / k_ if k_ else None
+    eng.prof_reset()
+    eng.prof_enable(True)
+    t_hr = timed(eng, lambda: eng.setbit_packed(koff, kbuf, h_off, ones, h_rep))
+    eng.prof_enable(False)
+    k_, ms_ = eng.prof_read("setbit")
+    hr_dev = ms_ / k_ if k_ else None
+    t_hg = timed(eng, lambda: eng.getbit_packed(koff, kbuf, h_off, h_rep))
+    host_path = {"ops_per_call": m, "setbit_void_per_s": m / t_hv, "setbit_void_device_per_s": m / (hv_dev * 1e-3)
+                 if hv_dev else None, "setbit_replies_per_s": m / t_hr,
+                 "setbit_replies_device_per_s": m / (hr_dev * 1e-3) if hr_dev else None, "getbit_per_s": m / t_hg,
+                 "note": "sk_setbit / sk_getbit by key name from pageable host buffers (what SketchNative.setbit / getbit "
+                         "pass): one key scan, the offsets' H2D, the kernels (SETBIT_VOID: k_sbv_part/fine/runs; with "
+                         "replies: k_sbv_part<u64>/k_sbv_fine<u64>/k_sbr_runs), the replies' D2H; no library sort"}
     for key in keys[1:]:     # make every bitset full length (2^34 bits)
         eng.setbit([key], [bits - 1], [1])
     # host-timed (the call, its launch and the reply copy) and device-timed (HIP events around the kernel)
@@ -261,7 +291,7 @@ def c5(eng, args):
     line({"metric": "C5 RBitSet 2^%d bits: SETBIT+GETBIT ops/sec" % args.c5_log2_bits,
           "value": 2 * n / (t_set + t_get), "unit": "ops/s",
           "config": {"workload": "c5", "bits": bits, "ops": n},
-          "setbit_per_s": n / t_set, "getbit_per_s": n / t_get,
+          "setbit_per_s": n / t_set, "getbit_per_s": n / t_get, "host_path": host_path,
           "setbit_device_per_s": n / (set_dev_ms * 1e-3) if set_dev_ms else None,
           "setbit_cold_first_call_per_s": m0 / t_cold,
           "setbit_cold": "one %d-op call on a missing key: the 2 GiB string's creation and growth timed inside it" % m0,

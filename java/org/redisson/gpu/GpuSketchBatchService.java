@@ -379,8 +379,14 @@ public class GpuSketchBatchService extends CommandBatchService {
                         vals[c] = (byte) Integer.parseInt(run.get(c).params[2].toString());
                     }
                 }
+                // SETBIT_VOID (RBitSet.set(i), M:RedissonBitSet.java:79-81) owes no reply: a null reply array lets
+                // the engine take the SETBIT_VOID kernels (sk_setbit, the dense region path for dense runs)
+                boolean allVoid = true;
+                for (Cmd c : run) {
+                    allVoid &= c.command == RedisCommands.SETBIT_VOID;
+                }
                 SketchDispatch.check(ctx, "SETBIT".equals(kind)
-                        ? SketchNative.setbit(ctx, k.off, k.bytes, offs, vals, out)
+                        ? SketchNative.setbit(ctx, k.off, k.bytes, offs, vals, allVoid ? null : out)
                         : SketchNative.getbit(ctx, k.off, k.bytes, offs, out));
             }
             for (int c = 0; c < n; c++) {

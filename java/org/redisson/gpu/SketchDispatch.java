@@ -19,6 +19,7 @@ import java.util.concurrent.ThreadFactory;
 import org.redisson.client.RedisException;
 import org.redisson.client.codec.Codec;
 import org.redisson.client.protocol.RedisCommand;
+import org.redisson.client.protocol.RedisCommands;
 
 public final class SketchDispatch {
     private SketchDispatch() {
@@ -313,7 +314,8 @@ public final class SketchDispatch {
                     check(ctx, SketchNative.getbit(ctx, k.off, k.bytes, offs, out));
                 } else {
                     byte[] vals = {(byte) Integer.parseInt(params[2].toString())};
-                    check(ctx, SketchNative.setbit(ctx, k.off, k.bytes, offs, vals, out));
+                    check(ctx, SketchNative.setbit(ctx, k.off, k.bytes, offs, vals,
+                            command == RedisCommands.SETBIT_VOID ? null : out));
                 }
                 return Long.valueOf(out[0]);
             }

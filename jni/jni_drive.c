@@ -171,6 +171,17 @@ int main(void) {
     const char *gk[] = {"jd:s", "jd:s", "jd:t", "jd:s"};
     packed(4, gk, &ko, &kb);
     pr_u8("getbit", Java_org_redisson_gpu_SketchNative_getbit(env, cls, ctx, ko, kb, jlongs(4, go), gb), gb);
+    /* SETBIT_VOID as the Java executors send it: no reply array */
+    const char *wk[] = {"jd:w", "jd:w", "jd:w"};
+    int64_t wo[] = {3, 3, 9};
+    packed(3, wk, &ko, &kb);
+    jbyteArray wv = f_newbytes(env, 3);
+    D(wv)[0] = 1, D(wv)[1] = 1, D(wv)[2] = 1;
+    jint wst = Java_org_redisson_gpu_SketchNative_setbit(env, cls, ctx, ko, kb, jlongs(3, wo), wv, NULL);
+    int64_t wg[] = {3, 9, 4};
+    jbyteArray wb = f_newbytes(env, 3);
+    jint wgs = Java_org_redisson_gpu_SketchNative_getbit(env, cls, ctx, ko, kb, jlongs(3, wg), wb);
+    pr_u8("void_getbit", wst ? wst : wgs, wb);
     jlongArray o1 = jlongs(1, NULL);
     pr_i64("bitcount", Java_org_redisson_gpu_SketchNative_bitcount(env, cls, ctx, jbytes("jd:s"), o1), o1);
     pr_i64("strlen", Java_org_redisson_gpu_SketchNative_strlen(env, cls, ctx, jbytes("jd:s"), o1), o1);

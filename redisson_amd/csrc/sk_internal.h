@@ -162,6 +162,20 @@ uint64_t sbv_part_scratch_bytes(uint64_t n, uint64_t max_off);
 bool sbv_part_ok(uint64_t n, uint64_t max_off);
 hipError_t launch_setbit_void_part(hipStream_t st, uint64_t n, const uint64_t *offs, uint64_t max_off, void *scratch,
                                    uint8_t *buf, uint64_t cap, uint32_t value);
+// SETBIT with replies (and SETBIT_VOID of several keys or values) through the region partition with u64 records
+// (k_sbv_part<u64> -> k_sbv_fine<u64> -> k_sbr_runs): op i sets bit offs[i] of the key whose virtual regions start at
+// vrb[i] (nullptr: one key at 0; 0xffffffff: op skipped) to vals[i] (nullptr: value_all), replying the bit before it
+// in batch order into out[i] (nullptr: none).  seg: SbrSeg[nseg] {u64 rb, u8 *ptr, u64 cap} sorted by rb.
+struct SbrSegH {
+    uint64_t rb;
+    uint8_t *ptr;
+    uint64_t cap;
+};
+uint64_t sbr_scratch_bytes(uint64_t n, uint64_t NRv);
+bool sbr_ok(uint64_t n, uint64_t NRv);
+hipError_t launch_setbit_regions(hipStream_t st, uint64_t n, const uint64_t *offs, const uint32_t *vrb,
+                                 const uint8_t *vals, uint32_t value_all, uint64_t NRv, const void *seg, uint32_t nseg,
+                                 void *scratch, uint8_t *out);
 hipError_t launch_bit_range(hipStream_t st, uint8_t *buf, uint64_t from, uint64_t to, uint32_t value);
 hipError_t launch_max_u64(hipStream_t st, uint64_t n, const uint64_t *v, uint64_t *out);
 hipError_t launch_bitcount(hipStream_t st, const uint8_t *buf, uint64_t len, uint64_t *out);

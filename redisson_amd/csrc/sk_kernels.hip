@@ -3562,27 +3562,46 @@ __global__ void __launch_bounds__(SBV_TPB) k_sbv_apply(const uint64_t *__restric
 #define SBV_NTMAXR 256 // tiles per call
 static_assert(SBV_E <= 65535 && SBV_G * (1u << SBV_RB) <= (1ull << 32), "record and segment packing");
 
-__global__ void __launch_bounds__(SBV_PTPB) k_sbv_part(uint64_t n, const uint64_t *__restrict__ offs, uint32_t NC,
-                                                       uint32_t NB, uint32_t T, uint32_t ntile, uint32_t *__restrict__ chunks,
-                                                       uint32_t *__restrict__ S, uint32_t *__restrict__ tot) {
+// Records: u32 rec = (region % SBV_G) << 18 | bit-in-region (SETBIT_VOID: the ops of one value commute), or u64 with
+// that word on top and seq << 1 | value below (SETBIT with replies, k_sbr_runs: the seq orders one bit's ops; the
+// partition need not be stable).  `vrb` (optional): per-op base of the op's key in the call's virtual region space
+// (0xffffffff: an op that failed validation, dropped); `vals` (optional): per-op values, else `value_all`.
+template <typename R> __device__ __forceinline__ uint32_t sbv_key(R r) { return uint32_t(uint64_t(r) >> (sizeof(R) == 8 ? 32 : 0)); }
+template <typename R> constexpr uint32_t sbv_fcap() { return sizeof(R) == 8 ? SBV_FCAP / 2 : SBV_FCAP; } // 64 KiB of LDS
+
+template <typename R>
+__global__ void __launch_bounds__(SBV_PTPB) k_sbv_part(uint64_t n, const uint64_t *__restrict__ offs,
+                                                       const uint32_t *__restrict__ vrb, const uint8_t *__restrict__ vals,
+                                                       uint32_t value_all, uint32_t NC, uint32_t NB, uint32_t T,
+                                                       uint32_t ntile, R *__restrict__ chunks, uint32_t *__restrict__ S,
+                                                       uint32_t *__restrict__ tot) {
     extern __shared__ uint32_t dyn32[];
-    uint32_t *hist = dyn32, *lrec = dyn32 + ((NC + 3) & ~3u);
+    uint32_t *hist = dyn32;
+    R *lrec = reinterpret_cast<R *>(dyn32 + ((NC + 3) & ~3u));
     __shared__ uint32_t wsum[SBV_PTPB / 64];
     const uint32_t blk = blockIdx.x;
     const uint64_t base = uint64_t(blk) * SBV_E;
     for (uint32_t b = threadIdx.x; b < NC; b += SBV_PTPB) hist[b] = 0;
     __syncthreads();
-    uint32_t rec[SBV_PPT], bk[SBV_PPT];
+    R rec[SBV_PPT];
+    uint32_t bk[SBV_PPT];
 #pragma unroll
     for (int q = 0; q < SBV_PPT; q++) {
         const uint64_t i = base + uint64_t(q) * SBV_PTPB + threadIdx.x;
         bk[q] = 0xffffffffu;
         if (i < n) {
             const uint64_t o = offs[i];
-            const uint32_t r = uint32_t(o >> SBV_RB);
-            rec[q] = ((r % SBV_G) << SBV_RB) | uint32_t(o & ((1u << SBV_RB) - 1u));
-            const uint32_t b = r / SBV_G;
-            bk[q] = b | (atomicAdd(&hist[b], 1u) << 16); // rank < SBV_E
+            const uint32_t vb = vrb ? vrb[i] : 0u;
+            if (vb != 0xffffffffu) {
+                const uint32_t r = vb + uint32_t(o >> SBV_RB);
+                const uint32_t key = ((r % SBV_G) << SBV_RB) | uint32_t(o & ((1u << SBV_RB) - 1u));
+                if constexpr (sizeof(R) == 8)
+                    rec[q] = (uint64_t(key) << 32) | (uint32_t(i) << 1) | (vals ? vals[i] & 1u : value_all);
+                else
+                    rec[q] = key;
+                const uint32_t b = r / SBV_G;
+                bk[q] = b | (atomicAdd(&hist[b], 1u) << 16); // rank < SBV_E
+            }
         }
     }
     __syncthreads();
@@ -3610,17 +3629,19 @@ __global__ void __launch_bounds__(SBV_PTPB) k_sbv_part(uint64_t n, const uint64_
     for (int q = 0; q < SBV_PPT; q++)
         if (bk[q] != 0xffffffffu) lrec[hist[bk[q] & 0xffffu] + (bk[q] >> 16)] = rec[q];
     __syncthreads();
-    uint32_t *dst = chunks + base;
+    R *dst = chunks + base;
     for (uint32_t t = threadIdx.x; t < total; t += SBV_PTPB) dst[t] = lrec[t];
 }
 
+template <typename R>
 __global__ void __launch_bounds__(SBV_PTPB) k_sbv_fine(uint32_t NC, uint32_t NB, uint32_t T, uint32_t ntile,
-                                                       const uint32_t *__restrict__ chunks,
+                                                       const R *__restrict__ chunks,
                                                        const uint32_t *__restrict__ S,
                                                        const uint32_t *__restrict__ tot, uint32_t *__restrict__ pbase,
-                                                       uint32_t *__restrict__ rs, uint32_t *__restrict__ out) {
+                                                       uint32_t *__restrict__ rs, R *__restrict__ out) {
+    constexpr uint32_t FCAP = sbv_fcap<R>();
     __shared__ uint32_t segp[SBV_TMAX + 1], segs[SBV_TMAX], hist[SBV_G + 1], cur[SBV_G];
-    __shared__ uint32_t sorted[SBV_FCAP];
+    __shared__ R sorted[FCAP];
     __shared__ uint32_t wsum[SBV_PTPB / 64];
     const uint32_t t = blockIdx.x, g = blockIdx.y, b0 = t * T;
     const uint32_t nb = (b0 + T < NB ? b0 + T : NB) - b0;
@@ -3657,20 +3678,21 @@ __global__ void __launch_bounds__(SBV_PTPB) k_sbv_fine(uint32_t NC, uint32_t NB,
         }
         return chunks[uint64_t(b0 + lo) * SBV_E + segs[lo] + (x - segp[lo])];
     };
-    constexpr int RP = SBV_FCAP / SBV_PTPB;
-    uint32_t rv[RP], rk[RP];
-    const bool small = m <= SBV_FCAP;
+    constexpr int RP = FCAP / SBV_PTPB;
+    R rv[RP];
+    uint32_t rk[RP];
+    const bool small = m <= FCAP;
     if (small) {
 #pragma unroll
         for (int q = 0; q < RP; q++) {
             const uint32_t x = threadIdx.x + q * SBV_PTPB;
             if (x < m) {
                 rv[q] = rec_at(x);
-                rk[q] = atomicAdd(&hist[rv[q] >> SBV_RB], 1u);
+                rk[q] = atomicAdd(&hist[sbv_key(rv[q]) >> SBV_RB], 1u);
             }
         }
     } else { // an oversized piece (skew): count first, place by atomics below
-        for (uint32_t x = threadIdx.x; x < m; x += SBV_PTPB) atomicAdd(&hist[rec_at(x) >> SBV_RB], 1u);
+        for (uint32_t x = threadIdx.x; x < m; x += SBV_PTPB) atomicAdd(&hist[sbv_key(rec_at(x)) >> SBV_RB], 1u);
     }
     __syncthreads();
     uint32_t tot2;
@@ -3688,14 +3710,14 @@ __global__ void __launch_bounds__(SBV_PTPB) k_sbv_fine(uint32_t NC, uint32_t NB,
 #pragma unroll
         for (int q = 0; q < RP; q++) {
             const uint32_t x = threadIdx.x + q * SBV_PTPB;
-            if (x < m) sorted[hist[rv[q] >> SBV_RB] + rk[q]] = rv[q];
+            if (x < m) sorted[hist[sbv_key(rv[q]) >> SBV_RB] + rk[q]] = rv[q];
         }
         __syncthreads();
         for (uint32_t x = threadIdx.x; x < m; x += SBV_PTPB) out[uint64_t(base) + x] = sorted[x];
     } else {
         for (uint32_t x = threadIdx.x; x < m; x += SBV_PTPB) {
-            const uint32_t r = rec_at(x);
-            out[uint64_t(base) + atomicAdd(&cur[r >> SBV_RB], 1u)] = r;
+            const R r = rec_at(x);
+            out[uint64_t(base) + atomicAdd(&cur[sbv_key(r) >> SBV_RB], 1u)] = r;
         }
     }
 }
@@ -3750,6 +3772,175 @@ __global__ void __launch_bounds__(SBV_TPB) k_sbv_runs(uint32_t ntile, const uint
     }
     __syncthreads();
     for (uint32_t v = threadIdx.x; v < nv; v += SBV_TPB) src[v] = reg4[v];
+}
+
+// SETBIT with replies (M:RedissonBitSet.java:79-81 with a reply, RBatch SETBIT; the reference's pipeline executes
+// the ops in batch order, each replying the bit before it) over the same region partition, u64 records carrying the
+// op's seq and value.  One workgroup per 32 KiB region of the call's virtual region space (every key touched gets a
+// range of regions, `seg`): the region's bits staged in LDS, its records sorted by (bit, seq) in LDS (bitonic), then
+// each op replies the value of the op before it on the same bit -- or the bit as the batch found it -- and the last
+// op of each bit leaves its value.  A region with more than SBR_RCAP ops (a skewed batch) sorts them in global memory
+// first: LDS-sorted chunks, then merge-path passes, through the partition's free chunk buffer at the same slots.
+#define SBR_TPB 1024
+#define SBR_RCAP 4096
+struct SbrSeg { // a key's range of virtual regions: [rb, next seg's rb) -> its string
+    uint64_t rb;
+    uint8_t *ptr;
+    uint64_t cap;
+};
+__device__ __forceinline__ void lds_bitonic_u64(uint64_t *a, uint32_t P) {
+    for (uint32_t k = 2; k <= P; k <<= 1)
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t t = threadIdx.x; t < P / 2; t += SBR_TPB) {
+                const uint32_t i = ((t & ~(j - 1u)) << 1) | (t & (j - 1u)), l = i + j;
+                const bool up = (i & k) == 0;
+                const uint64_t x = a[i], y = a[l];
+                if ((x > y) == up) {
+                    a[i] = y;
+                    a[l] = x;
+                }
+            }
+            __syncthreads();
+        }
+}
+__global__ void __launch_bounds__(SBR_TPB) k_sbr_runs(uint32_t ntile, const uint32_t *__restrict__ pbase,
+                                                      const uint32_t *__restrict__ rs, uint64_t *recs, uint64_t *scr,
+                                                      const SbrSeg *__restrict__ seg, uint32_t nseg,
+                                                      uint8_t *__restrict__ out) {
+    constexpr uint32_t RBYTES = 1u << (SBV_RB - 3), NV = RBYTES / 16, VPT = NV / SBR_TPB;
+    constexpr uint64_t KMASK = 0x0003ffffffffffffull; // bit-in-region << 32 | seq << 1 | value
+    __shared__ uint4 reg4[NV];
+    __shared__ uint64_t key[SBR_RCAP + 2];
+    __shared__ uint32_t rlo[SBV_NTMAXR], rn[SBV_NTMAXR + 1];
+    __shared__ uint32_t wsum[SBR_TPB / 64];
+    const uint32_t r = blockIdx.x, g = r / SBV_G, rr = r % SBV_G;
+    uint32_t lo = 0, c = 0;
+    if (threadIdx.x < ntile) {
+        const uint32_t *q = rs + (uint64_t(g) * ntile + threadIdx.x) * (SBV_G + 1) + rr;
+        lo = pbase[uint64_t(g) * ntile + threadIdx.x] + q[0];
+        c = q[1] - q[0];
+    }
+    uint32_t total;
+    const uint32_t ex = block_exscan<SBR_TPB>(c, wsum, &total);
+    if (total == 0) return; // uniform: no op in this region
+    if (threadIdx.x < ntile) {
+        rlo[threadIdx.x] = lo;
+        rn[threadIdx.x] = ex;
+    }
+    if (threadIdx.x == 0) rn[ntile] = total;
+    // the key this region belongs to (largest rb <= r)
+    uint32_t sl = 0, sh = nseg;
+    while (sh - sl > 1) {
+        const uint32_t mid = (sl + sh) >> 1;
+        if (seg[mid].rb <= r) sl = mid;
+        else sh = mid;
+    }
+    const uint64_t srb = seg[sl].rb, scap = seg[sl].cap;
+    uint8_t *const sptr = seg[sl].ptr;
+    const uint64_t b0 = (uint64_t(r) - srb) * RBYTES; // < cap: an op's byte lies in the region
+    uint4 *src = reinterpret_cast<uint4 *>(sptr + b0);
+    const uint32_t nv = scap - b0 >= RBYTES ? NV : uint32_t((scap - b0) / 16); // cap is a multiple of 16
+    if (nv == NV) { // a whole region: both loads issued before the LDS stores
+        static_assert(VPT == 2, "two 16-B vectors per thread");
+        const uint4 t0 = src[threadIdx.x], t1 = src[threadIdx.x + SBR_TPB];
+        reg4[threadIdx.x] = t0;
+        reg4[threadIdx.x + SBR_TPB] = t1;
+    } else {
+        for (uint32_t v = threadIdx.x; v < nv; v += SBR_TPB) reg4[v] = src[v];
+    }
+    __syncthreads();
+    uint32_t *w = reinterpret_cast<uint32_t *>(reg4);
+    auto slot = [=](uint32_t i) __attribute__((always_inline)) -> uint64_t { // the partition slot of the region's record i (its tile's run)
+        uint32_t t = 0;
+#pragma unroll
+        for (uint32_t step = SBV_NTMAXR / 2; step; step >>= 1)
+            if (t + step < ntile && rn[t + step] <= i) t += step;
+        return uint64_t(rlo[t]) + (i - rn[t]);
+    };
+    auto bit_of = [](uint32_t lb) __attribute__((always_inline)) { // LDS word and mask of bit lb (bit_word's layout)
+        const uint32_t byte = lb >> 3;
+        return 1u << ((byte & 3u) * 8u + (7u - (lb & 7u)));
+    };
+    // replies and final bits of sorted records key[1 .. m] (key[0] = the record before them or ~0, key[m + 1] the one
+    // after or ~0): phase A reads the bits as the batch found them, phase B writes each bit's last value
+    auto apply_sorted = [=](uint32_t m) __attribute__((always_inline)) {
+        for (uint32_t i = threadIdx.x; i < m; i += SBR_TPB) {
+            const uint64_t k = key[i + 1], kp = key[i];
+            const uint32_t lb = uint32_t(k >> 32);
+            const uint32_t rep = (kp >> 32) == lb ? uint32_t(kp) & 1u : (w[lb >> 5] & bit_of(lb)) ? 1u : 0u;
+            if (out) out[uint32_t(k) >> 1] = uint8_t(rep);
+        }
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < m; i += SBR_TPB) {
+            const uint64_t k = key[i + 1], kn = key[i + 2];
+            const uint32_t lb = uint32_t(k >> 32);
+            if ((kn >> 32) != lb) {
+                if (uint32_t(k) & 1u) atomicOr(&w[lb >> 5], bit_of(lb));
+                else atomicAnd(&w[lb >> 5], ~bit_of(lb));
+            }
+        }
+        __syncthreads();
+    };
+    if (total <= SBR_RCAP) {
+        uint32_t P = 2;
+        while (P < total) P <<= 1;
+        for (uint32_t i = threadIdx.x; i < P; i += SBR_TPB) key[i + 1] = i < total ? recs[slot(i)] & KMASK : ~0ull;
+        if (threadIdx.x == 0) key[0] = ~0ull;
+        __syncthreads();
+        lds_bitonic_u64(key + 1, P);
+        if (threadIdx.x == 0) key[total + 1] = ~0ull;
+        __syncthreads();
+        apply_sorted(total);
+    } else {
+        // 1) LDS-sorted chunks of SBR_RCAP: recs -> scr
+        for (uint32_t c0 = 0; c0 < total; c0 += SBR_RCAP) {
+            const uint32_t m = total - c0 < SBR_RCAP ? total - c0 : SBR_RCAP;
+            uint32_t P = 2;
+            while (P < m) P <<= 1;
+            for (uint32_t i = threadIdx.x; i < P; i += SBR_TPB) key[i + 1] = i < m ? recs[slot(c0 + i)] & KMASK : ~0ull;
+            __syncthreads();
+            lds_bitonic_u64(key + 1, P);
+            for (uint32_t i = threadIdx.x; i < m; i += SBR_TPB) scr[slot(c0 + i)] = key[i + 1];
+            __syncthreads();
+        }
+        // 2) merge passes (merge path per thread), src <-> dst
+        uint64_t *a = scr, *b = recs;
+        for (uint32_t wd = SBR_RCAP; wd < total; wd <<= 1) {
+            for (uint32_t p0 = 0; p0 < total; p0 += 2 * wd) {
+                const uint32_t a1 = p0 + wd < total ? p0 + wd : total, b1 = p0 + 2 * wd < total ? p0 + 2 * wd : total;
+                const uint32_t la = a1 - p0, lb = b1 - a1, len = la + lb;
+                const uint32_t d0 = uint32_t(uint64_t(len) * threadIdx.x / SBR_TPB);
+                const uint32_t d1 = uint32_t(uint64_t(len) * (threadIdx.x + 1) / SBR_TPB);
+                uint32_t x = d0 > lb ? d0 - lb : 0u, y = d0 < la ? d0 : la; // A items taken before output d0
+                while (x < y) {
+                    const uint32_t mid = (x + y) >> 1;
+                    if (a[slot(p0 + mid)] < a[slot(a1 + (d0 - 1 - mid))]) x = mid + 1;
+                    else y = mid;
+                }
+                uint32_t i = x, j = d0 - x;
+                for (uint32_t d = d0; d < d1; d++) {
+                    const bool ta = j >= lb || (i < la && a[slot(p0 + i)] < a[slot(a1 + j)]);
+                    b[slot(p0 + d)] = ta ? a[slot(p0 + i)] : a[slot(a1 + j)];
+                    i += ta ? 1u : 0u;
+                    j += ta ? 0u : 1u;
+                }
+            }
+            __syncthreads();
+            uint64_t *t_ = a;
+            a = b;
+            b = t_;
+        }
+        // 3) the sorted records, chunk by chunk, with their neighbours across chunk ends
+        for (uint32_t c0 = 0; c0 < total; c0 += SBR_RCAP) {
+            const uint32_t m = total - c0 < SBR_RCAP ? total - c0 : SBR_RCAP;
+            for (uint32_t i = threadIdx.x; i < m; i += SBR_TPB) key[i + 1] = a[slot(c0 + i)];
+            if (threadIdx.x == 0) key[0] = c0 ? a[slot(c0 - 1)] : ~0ull;
+            if (threadIdx.x == 1) key[m + 1] = c0 + m < total ? a[slot(c0 + m)] : ~0ull;
+            __syncthreads();
+            apply_sorted(m);
+        }
+    }
+    for (uint32_t v = threadIdx.x; v < nv; v += SBR_TPB) src[v] = reg4[v];
 }
 
 // RBitSet.set(from, to) / clear(from, to) (M:RedissonBitSet.java:202-228:
@@ -4667,12 +4858,57 @@ hipError_t launch_setbit_void_part(hipStream_t st, uint64_t n, const uint64_t *o
     hipError_t e = hipMemsetAsync(tot, 0, uint64_t(NC) * ntile * 4, st);
     if (e != hipSuccess) return e;
     const size_t lds = (((NC + 3) & ~3u) + SBV_E) * 4;
-    hipLaunchKernelGGL(k_sbv_part, dim3(NB), dim3(SBV_PTPB), lds, st, n, offs, NC, NB, T, ntile, chunks, S, tot);
+    hipLaunchKernelGGL(k_sbv_part<uint32_t>, dim3(NB), dim3(SBV_PTPB), lds, st, n, offs, nullptr, nullptr, 0u, NC, NB,
+                       T, ntile, chunks, S, tot);
     SK_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_sbv_fine, dim3(ntile, NC), dim3(SBV_PTPB), 0, st, NC, NB, T, ntile, chunks, S, tot, pbase, rs,
-                       recs);
+    hipLaunchKernelGGL(k_sbv_fine<uint32_t>, dim3(ntile, NC), dim3(SBV_PTPB), 0, st, NC, NB, T, ntile, chunks, S, tot,
+                       pbase, rs, recs);
     SK_LAUNCH_CHECK();
     hipLaunchKernelGGL(k_sbv_runs, dim3(NR), dim3(SBV_TPB), 0, st, ntile, pbase, rs, recs, buf, cap, value);
+    SK_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+// SETBIT with replies over the region partition (u64 records): NRv virtual regions, segments sorted by rb
+uint64_t sbr_scratch_bytes(uint64_t n, uint64_t NRv) {
+    uint64_t NR, NC, NB, T, ntile;
+    sbv_dims(n, (NRv << SBV_RB) - 1, &NR, &NC, &NB, &T, &ntile);
+    return 8 * (2 * NB * SBV_E) + 4 * (NC * NB + NC * ntile * (2 + SBV_G + 1)) + 64;
+}
+bool sbr_ok(uint64_t n, uint64_t NRv) {
+    uint64_t NR, NC, NB, T, ntile;
+    if (!NRv || NRv > (uint64_t(SBV_NCMAX) * SBV_G)) return false;
+    sbv_dims(n, (NRv << SBV_RB) - 1, &NR, &NC, &NB, &T, &ntile);
+    return n <= (1ull << 30) && NC <= SBV_NCMAX && ntile <= SBV_NTMAXR;
+}
+hipError_t launch_setbit_regions(hipStream_t st, uint64_t n, const uint64_t *offs, const uint32_t *vrb,
+                                 const uint8_t *vals, uint32_t value_all, uint64_t NRv, const void *seg, uint32_t nseg,
+                                 void *scratch, uint8_t *out) {
+    if (!n) return hipSuccess;
+    uint64_t NR_, NC_, NB_, T_, nt_;
+    sbv_dims(n, (NRv << SBV_RB) - 1, &NR_, &NC_, &NB_, &T_, &nt_);
+    const uint32_t NR = uint32_t(NR_), NC = uint32_t(NC_), NB = uint32_t(NB_), T = uint32_t(T_), ntile = uint32_t(nt_);
+    uint64_t *chunks = static_cast<uint64_t *>(scratch), *recs = chunks + uint64_t(NB) * SBV_E;
+    uint32_t *S = reinterpret_cast<uint32_t *>(recs + uint64_t(NB) * SBV_E), *tot = S + uint64_t(NC) * NB;
+    uint32_t *pbase = tot + uint64_t(NC) * ntile, *rs = pbase + uint64_t(NC) * ntile;
+    hipError_t e = hipMemsetAsync(tot, 0, uint64_t(NC) * ntile * 4, st);
+    if (e != hipSuccess) return e;
+    const size_t lds = ((NC + 3) & ~3u) * 4 + size_t(SBV_E) * 8;
+    static bool attr = false;
+    if (!attr) {
+        e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_sbv_part<uint64_t>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, int(((SBV_NCMAX + 3) & ~3u) * 4 + SBV_E * 8));
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
+    hipLaunchKernelGGL(k_sbv_part<uint64_t>, dim3(NB), dim3(SBV_PTPB), lds, st, n, offs, vrb, vals, value_all & 1u, NC,
+                       NB, T, ntile, chunks, S, tot);
+    SK_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_sbv_fine<uint64_t>, dim3(ntile, NC), dim3(SBV_PTPB), 0, st, NC, NB, T, ntile, chunks, S, tot,
+                       pbase, rs, recs);
+    SK_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_sbr_runs, dim3(NR), dim3(SBR_TPB), 0, st, ntile, pbase, rs, recs, chunks,
+                       static_cast<const SbrSeg *>(seg), nseg, out);
     SK_LAUNCH_CHECK();
     return hipSuccess;
 }

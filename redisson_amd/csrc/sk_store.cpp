@@ -2092,112 +2092,295 @@ int sk_hll_registers(sk_ctx *c, const uint8_t *key, uint64_t len, uint8_t *out) 
 // ============================================================== bit strings
 extern "C" {
 
+} // extern "C"
+
+namespace {
+// The keys of a bit batch, each distinct key resolved once (RBatch SETBIT / GETBIT runs name one bitset over and over:
+// a run of equal keys is found by comparing bytes, other repeats through a map of the batch's own key bytes)
+struct BitKeys {
+    bool single = true;           // every op names key 0
+    std::vector<uint32_t> kid;    // per op (multi-key): its key's index
+    std::vector<uint64_t> first;  // per key: an op naming it (its bytes)
+};
+// one parallel pass over a bit batch: does every op name op 0's key, are all offsets below `lim`, do all values
+// equal values[0] (values may be null), the largest valid offset
+struct BitScan {
+    bool single = true, all_valid = true, one_value = true, any_valid = false;
+    uint64_t mx = 0;
+};
+BitScan bit_scan(uint64_t n, const uint64_t *key_off, const uint8_t *key_bytes, const uint64_t *offs,
+                 const uint8_t *values, uint64_t lim) {
+    BitScan S;
+    std::mutex mu;
+    const uint64_t l0 = key_off[1] - key_off[0];
+    const uint8_t v0 = values ? values[0] & 1u : 0u;
+    host_for(n, 1u << 18, [&](uint64_t i0, uint64_t i1) {
+        BitScan L;
+        for (uint64_t i = i0; i < i1; i++) {
+            L.single &= key_off[i + 1] - key_off[i] == l0 &&
+                        std::memcmp(key_bytes + key_off[i], key_bytes + key_off[0], l0) == 0;
+            if (values) L.one_value &= (values[i] & 1u) == v0;
+            if (offs[i] >= lim) {
+                L.all_valid = false;
+            } else {
+                L.mx = L.any_valid ? std::max(L.mx, offs[i]) : offs[i];
+                L.any_valid = true;
+            }
+        }
+        std::lock_guard<std::mutex> g(mu);
+        S.single &= L.single;
+        S.all_valid &= L.all_valid;
+        S.one_value &= L.one_value;
+        if (L.any_valid) S.mx = S.any_valid ? std::max(S.mx, L.mx) : L.mx;
+        S.any_valid |= L.any_valid;
+    });
+    return S;
+}
+void bit_keys(uint64_t n, const uint64_t *key_off, const uint8_t *key_bytes, BitKeys &K, bool single) {
+    K.single = single;
+    K.first.assign(1, 0);
+    if (K.single) return;
+    K.kid.assign(n, 0);
+    std::unordered_map<std::string_view, uint32_t> ix;
+    auto view = [&](uint64_t i) {
+        return std::string_view(reinterpret_cast<const char *>(key_bytes + key_off[i]), key_off[i + 1] - key_off[i]);
+    };
+    ix.emplace(view(0), 0u);
+    for (uint64_t i = 1; i < n; i++) {
+        if (key_off[i + 1] - key_off[i] == key_off[i] - key_off[i - 1] &&
+            std::memcmp(key_bytes + key_off[i], key_bytes + key_off[i - 1], key_off[i + 1] - key_off[i]) == 0) {
+            K.kid[i] = K.kid[i - 1]; // the same key as the op before
+            continue;
+        }
+        auto it = ix.emplace(view(i), uint32_t(K.first.size()));
+        if (it.second) K.first.push_back(i);
+        K.kid[i] = it.first->second;
+    }
+}
+
+// dense / sparse SETBIT_VOID of one value on string `id` (device offsets, max offset mx already validated and the
+// string grown): a dense batch streams the string through LDS region by region (k_sbv_part / k_sbv_fine /
+// k_sbv_runs) instead of one random atomic per op (k_setbit_void); the ops of one value commute
+int setbit_void_device(sk_ctx *c, uint32_t id, uint64_t n, const uint64_t *d_offsets, uint64_t mx, uint8_t value) {
+    const uint64_t need = (mx >> 3) + 1;
+    const unsigned rb = sk::sbv_region_bits(), eb = 64u - unsigned(__builtin_clzll(mx | 1));
+    const uint64_t nr = (mx >> rb) + 1; // regions up to the highest op; >= 256 of them to fill the GPU
+    if (n >= c->sbv_min && n < (uint64_t(1) << 32) && n * 64 >= need && nr >= 256 && c->sbv_part &&
+        sk::sbv_part_ok(n, mx)) { // the hand-written region partition
+        HIPCHK(c, c->keys_b.ensure(sk::sbv_part_scratch_bytes(n, mx)));
+        Prof p_(c, 9);
+        HIPCHK(c, sk::launch_setbit_void_part(c->st, n, d_offsets, mx, c->keys_b.p, c->strs[id].ptr, c->strs[id].cap,
+                                              value & 1));
+    } else if (n >= c->sbv_min && n < (uint64_t(1) << 32) && n * 64 >= need && nr >= 256) {
+        // the same through a radix sort of the offsets by region (SK_SBV_PART=0, or a call past the tables)
+        const uint64_t *keys = d_offsets;
+        HIPCHK(c, c->vals_a.ensure((nr + 1) * 4));
+        Prof p_(c, 9);
+        if (eb > rb) { // more than one region: group the ops by region
+            size_t tmp;
+            HIPCHK(c, sk::sort_keys_size(n, rb, eb, &tmp));
+            HIPCHK(c, c->sort_tmp.ensure(tmp));
+            HIPCHK(c, c->keys_b.ensure(n * 8));
+            HIPCHK(c, sk::sort_keys(c->st, c->sort_tmp.p, c->sort_tmp.cap, d_offsets, c->keys_b.as<uint64_t>(), n, rb,
+                                    eb));
+            keys = c->keys_b.as<uint64_t>();
+        }
+        HIPCHK(c, sk::launch_setbit_void_regions(c->st, n, keys, mx, c->vals_a.as<uint32_t>(), c->strs[id].ptr,
+                                                 c->strs[id].cap, value & 1));
+    } else {
+        Prof p_(c, 9);
+        HIPCHK(c, sk::launch_setbit_void(c->st, n, d_offsets, c->strs[id].ptr, value & 1));
+    }
+    return SK_OK;
+}
+
+// SETBIT through the region partition with u64 records, in pieces of <= 2^30 ops run one after another (an op's
+// seq is 31 bits; later pieces see earlier ones' bits, as batch order does).  seg (device) holds nseg SbrSeg.
+int setbit_regions(sk_ctx *c, uint64_t n, const uint64_t *d_off, const uint32_t *d_vrb, const uint8_t *d_vals,
+                   uint8_t value, uint64_t NRv, const void *d_seg, uint32_t nseg, uint8_t *d_out) {
+    constexpr uint64_t kPiece = uint64_t(1) << 30;
+    for (uint64_t s0 = 0; s0 < n; s0 += kPiece) {
+        const uint64_t m = std::min(kPiece, n - s0);
+        if (!sk::sbr_ok(m, NRv))
+            return fail(c, SK_EINVAL, "SETBIT batch of %llu ops over %llu regions of 2^%u bits is past the region tables",
+                        (unsigned long long)m, (unsigned long long)NRv, sk::sbv_region_bits());
+        HIPCHK(c, c->keys_b.ensure(sk::sbr_scratch_bytes(m, NRv)));
+        Prof p_(c, 9);
+        HIPCHK(c, sk::launch_setbit_regions(c->st, m, d_off + s0, d_vrb ? d_vrb + s0 : nullptr,
+                                            d_vals ? d_vals + s0 : nullptr, value & 1u, NRv, d_seg, nseg, c->keys_b.p,
+                                            d_out ? d_out + s0 : nullptr));
+    }
+    return SK_OK;
+}
+// the same for one string (device batches): one segment
+int setbit_regions_one(sk_ctx *c, uint32_t id, uint64_t n, const uint64_t *d_off, const uint8_t *d_vals, uint8_t value,
+                       uint64_t mx, uint8_t *d_out) {
+    const sk::SbrSegH one{0, c->strs[id].ptr, c->strs[id].cap};
+    HIPCHK(c, c->ptrs.ensure(sizeof one));
+    HIPCHK(c, hipMemcpyAsync(c->ptrs.p, &one, sizeof one, hipMemcpyHostToDevice, c->st));
+    int r = setbit_regions(c, n, d_off, nullptr, d_vals, value, (mx >> sk::sbv_region_bits()) + 1, c->ptrs.p, 1, d_out);
+    if (r) return r;
+    return sync(c); // `one` is a stack variable
+}
+
+// grow string `id` to hold bit mx (capacity and length: SETBIT's sdsgrowzero)
+int str_grow_bits(sk_ctx *c, uint32_t id, uint64_t mx) {
+    const uint64_t need = (mx >> 3) + 1;
+    uint64_t cur;
+    int r = str_reserve(c, id, need);
+    if (!r) r = str_len(c, id, &cur);
+    if (!r && need > cur) r = str_set_len(c, id, need);
+    return r;
+}
+} // namespace
+
+extern "C" {
+
+// SETBIT batch by key name (RBatch runs, RBitSet.set with a reply; M:RedissonBitSet.java:79-81,202-228).  Each
+// distinct key is resolved once.  out_old == NULL is SETBIT_VOID (RBitSet.set(i), the Java executors pass no reply
+// array for it): a batch of one key and one value takes the SETBIT_VOID kernels (the dense region path for a dense
+// batch); everything else -- replies, several keys, mixed values -- the region partition with u64 records
+// (k_sbv_part<u64> -> k_sbv_fine<u64> -> k_sbr_runs), whose replies are the bits as batch order finds them.  An op
+// with a bad offset or on a key of another type fails alone (reply 0) and the call reports the error, as a pipeline.
 int sk_setbit(sk_ctx *c, uint32_t n, const uint64_t *key_off, const uint8_t *key_bytes, const uint64_t *offsets,
               const uint8_t *values, uint8_t *out_old) {
     std::lock_guard<std::mutex> g(c->mu);
     ENTER(c);
     if (!n) return SK_OK;
-    std::vector<uint8_t> ok;
-    int status = check_offsets(c, n, offsets, ok);
-    // resolve / create keys, find per-key max offset (capacity + new length)
-    std::vector<uint32_t> sid(n);
-    std::unordered_map<uint32_t, uint64_t> maxoff;
-    for (uint32_t i = 0; i < n; i++) {
-        if (!ok[i]) {
-            sid[i] = kNoId;
-            continue;
+    if (out_old) std::memset(out_old, 0, n);
+    int status = SK_OK;
+    const BitScan B = bit_scan(n, key_off, key_bytes, offsets, values, c->max_bit_offset);
+    BitKeys K;
+    bit_keys(n, key_off, key_bytes, K, B.single);
+    const size_t nk = K.first.size();
+    // per key: max valid offset
+    std::vector<uint64_t> mx(nk, 0);
+    std::vector<uint8_t> has(nk, 0);
+    bool all_valid = B.all_valid;
+    const bool one_value = B.one_value;
+    const uint8_t v0 = values[0] & 1u;
+    if (!all_valid) status = fail(c, SK_ERANGE, "%s", kRange);
+    if (K.single) {
+        mx[0] = B.mx;
+        has[0] = B.any_valid;
+    } else {
+        for (uint32_t i = 0; i < n; i++) {
+            const uint32_t k = K.kid[i];
+            if (offsets[i] >= c->max_bit_offset) continue;
+            mx[k] = has[k] ? std::max(mx[k], offsets[i]) : offsets[i];
+            has[k] = 1;
         }
-        int r = str_get(c, key_at(key_off, key_bytes, i), true, (offsets[i] >> 3) + 1, &sid[i]);
+    }
+    // resolve / create each key once, grow its string; the call's virtual region space: one range per key
+    std::vector<uint32_t> sid(nk, kNoId);
+    std::vector<sk::SbrSegH> seg;
+    std::vector<uint32_t> rbase(nk, 0xffffffffu);
+    uint64_t NRv = 0;
+    const unsigned RB = sk::sbv_region_bits();
+    for (size_t k = 0; k < nk; k++) {
+        if (!has[k]) continue;
+        int r = str_get(c, key_at(key_off, key_bytes, K.first[k]), true, (mx[k] >> 3) + 1, &sid[k]);
         if (r == SK_EWRONGTYPE) {
-            ok[i] = 0;
-            sid[i] = kNoId;
+            sid[k] = kNoId;
+            all_valid = false;
             status = r;
             continue;
         }
-        if (r) return r;
-        auto it = maxoff.find(sid[i]);
-        if (it == maxoff.end() || it->second < offsets[i]) maxoff[sid[i]] = offsets[i];
+        if (r || (r = str_grow_bits(c, sid[k], mx[k]))) return r;
+        rbase[k] = uint32_t(std::min<uint64_t>(NRv, 0xfffffffeu));
+        seg.push_back(sk::SbrSegH{NRv, c->strs[sid[k]].ptr, c->strs[sid[k]].cap});
+        NRv += (mx[k] >> RB) + 1;
     }
-    for (auto &kv : maxoff) {
-        uint64_t need = (kv.second >> 3) + 1, len;
-        int r = str_reserve(c, kv.first, need);
+    if (seg.empty()) return status;
+    HIPCHK(c, c->in_off.ensure(uint64_t(n) * 8));
+    HIPCHK(c, hipMemcpyAsync(c->in_off.p, offsets, uint64_t(n) * 8, hipMemcpyHostToDevice, c->st));
+    if (!out_old && seg.size() == 1 && all_valid && one_value) { // SETBIT_VOID of one key and one value
+        const uint32_t k = 0;
+        int r = setbit_void_device(c, sid[k], n, c->in_off.as<uint64_t>(), mx[k], v0);
         if (r) return r;
-        r = str_len(c, kv.first, &len);
-        if (r) return r;
-        if (need > len && (r = str_set_len(c, kv.first, need))) return r;
+        r = sync(c);
+        return r ? r : status;
     }
-    // compact the valid ops (order kept)
-    std::vector<uint32_t> vs;
-    std::vector<uint64_t> vo;
-    std::vector<uint8_t> vv;
-    std::vector<uint32_t> vidx;
-    for (uint32_t i = 0; i < n; i++)
-        if (ok[i]) {
-            vs.push_back(sid[i]);
-            vo.push_back(offsets[i]);
-            vv.push_back(values[i] & 1);
-            vidx.push_back(i);
+    // per-op key bases (several keys, or ops to drop) and values (unless one value)
+    const uint32_t *d_vrb = nullptr;
+    const uint8_t *d_vals = nullptr;
+    std::vector<uint32_t> vrb;
+    if (!K.single || !all_valid) {
+        vrb.resize(n);
+        for (uint32_t i = 0; i < n; i++) {
+            const uint32_t k = K.single ? 0u : K.kid[i];
+            vrb[i] = offsets[i] < c->max_bit_offset && sid[k] != kNoId ? rbase[k] : 0xffffffffu;
         }
-    uint64_t m = vs.size();
-    if (out_old) std::memset(out_old, 0, n);
-    if (!m) return status;
-    unsigned sid_bits = bits_for(c->strs.size() ? c->strs.size() - 1 : 0);
-    if (36 + sid_bits > 64) return fail(c, SK_EINVAL, "too many strings");
-    HIPCHK(c, c->in_ids.ensure(m * 4));
-    HIPCHK(c, c->in_off.ensure(m * 8));
-    HIPCHK(c, c->in_bytes.ensure(m));
-    HIPCHK(c, c->out_u8.ensure(m));
-    HIPCHK(c, c->keys_a.ensure(m * 8));
-    HIPCHK(c, c->keys_b.ensure(m * 8));
-    HIPCHK(c, c->vals_a.ensure(m * 4));
-    HIPCHK(c, c->vals_b.ensure(m * 4));
-    size_t tmp;
-    HIPCHK(c, sk::sort_pairs_size(m, 0, 36 + sid_bits, &tmp));
-    HIPCHK(c, c->sort_tmp.ensure(tmp));
-    HIPCHK(c, hipMemcpyAsync(c->in_ids.p, vs.data(), m * 4, hipMemcpyHostToDevice, c->st));
-    HIPCHK(c, hipMemcpyAsync(c->in_off.p, vo.data(), m * 8, hipMemcpyHostToDevice, c->st));
-    HIPCHK(c, hipMemcpyAsync(c->in_bytes.p, vv.data(), m, hipMemcpyHostToDevice, c->st));
-    HIPCHK(c, sk::launch_setbit_keys(c->st, m, c->in_ids.as<uint32_t>(), c->in_off.as<uint64_t>(),
-                                     c->keys_a.as<uint64_t>(), c->vals_a.as<uint32_t>()));
-    HIPCHK(c, sk::sort_pairs(c->st, c->sort_tmp.p, c->sort_tmp.cap, c->keys_a.as<uint64_t>(), c->keys_b.as<uint64_t>(),
-                             c->vals_a.as<uint32_t>(), c->vals_b.as<uint32_t>(), m, 0, 36 + sid_bits));
-    HIPCHK(c, sk::launch_setbit_apply(c->st, m, c->keys_b.as<uint64_t>(), c->vals_b.as<uint32_t>(),
-                                      c->in_bytes.as<uint8_t>(), 0, c->d_dir, c->out_u8.as<uint8_t>()));
-    std::vector<uint8_t> old(m);
-    HIPCHK(c, hipMemcpyAsync(old.data(), c->out_u8.p, m, hipMemcpyDeviceToHost, c->st));
-    int r = sync(c);
-    if (r) return r;
-    if (out_old)
-        for (uint64_t j = 0; j < m; j++) out_old[vidx[j]] = old[j];
-    return status;
+        HIPCHK(c, c->in_ids.ensure(uint64_t(n) * 4));
+        HIPCHK(c, hipMemcpyAsync(c->in_ids.p, vrb.data(), uint64_t(n) * 4, hipMemcpyHostToDevice, c->st));
+        d_vrb = c->in_ids.as<uint32_t>();
+    }
+    if (!one_value) {
+        HIPCHK(c, c->in_bytes.ensure(n));
+        HIPCHK(c, hipMemcpyAsync(c->in_bytes.p, values, n, hipMemcpyHostToDevice, c->st));
+        d_vals = c->in_bytes.as<uint8_t>();
+    }
+    HIPCHK(c, c->ptrs.ensure(seg.size() * sizeof(sk::SbrSegH)));
+    HIPCHK(c, hipMemcpyAsync(c->ptrs.p, seg.data(), seg.size() * sizeof(sk::SbrSegH), hipMemcpyHostToDevice, c->st));
+    uint8_t *d_out = nullptr;
+    if (out_old) {
+        HIPCHK(c, c->out_u8.ensure(n));
+        HIPCHK(c, hipMemsetAsync(c->out_u8.p, 0, n, c->st));
+        d_out = c->out_u8.as<uint8_t>();
+    }
+    int rr = setbit_regions(c, n, c->in_off.as<uint64_t>(), d_vrb, d_vals, v0, NRv, c->ptrs.p, uint32_t(seg.size()),
+                            d_out);
+    if (rr) {
+        (void)sync(c);
+        return rr;
+    }
+    if (out_old) HIPCHK(c, hipMemcpyAsync(out_old, d_out, n, hipMemcpyDeviceToHost, c->st));
+    int r = sync(c); // vrb / offsets are host buffers
+    return r ? r : status;
 }
 
+// GETBIT batch by key name: each distinct key resolved once; one key -> k_getbit_single on its string, several ->
+// k_getbit_multi over per-op string ids.  Missing keys and bad offsets reply 0 (a bad offset also fails the call).
 int sk_getbit(sk_ctx *c, uint32_t n, const uint64_t *key_off, const uint8_t *key_bytes, const uint64_t *offsets,
               uint8_t *out) {
     std::lock_guard<std::mutex> g(c->mu);
     ENTER(c);
     if (!n) return SK_OK;
-    std::vector<uint8_t> ok;
-    int status = check_offsets(c, n, offsets, ok);
-    std::vector<uint32_t> sid(n);
-    for (uint32_t i = 0; i < n; i++) {
-        sid[i] = kNoId;
-        if (!ok[i]) continue;
-        int r = str_get(c, key_at(key_off, key_bytes, i), false, 0, &sid[i]);
+    int status = SK_OK;
+    const BitScan B = bit_scan(n, key_off, key_bytes, offsets, nullptr, c->max_bit_offset);
+    if (!B.all_valid) status = fail(c, SK_ERANGE, "%s", kRange); // such an op reads past the string: 0
+    BitKeys K;
+    bit_keys(n, key_off, key_bytes, K, B.single);
+    std::vector<uint32_t> sid(K.first.size(), kNoId);
+    for (size_t k = 0; k < K.first.size(); k++) {
+        int r = str_get(c, key_at(key_off, key_bytes, K.first[k]), false, 0, &sid[k]);
         if (r == SK_EWRONGTYPE) {
-            sid[i] = kNoId;
+            sid[k] = kNoId;
             status = r;
             continue;
         }
         if (r) return r;
     }
-    HIPCHK(c, c->in_ids.ensure(n * 4));
-    HIPCHK(c, c->in_off.ensure(n * 8));
+    HIPCHK(c, c->in_off.ensure(uint64_t(n) * 8));
     HIPCHK(c, c->out_u8.ensure(n));
-    HIPCHK(c, hipMemcpyAsync(c->in_ids.p, sid.data(), n * 4, hipMemcpyHostToDevice, c->st));
-    HIPCHK(c, hipMemcpyAsync(c->in_off.p, offsets, n * 8ull, hipMemcpyHostToDevice, c->st));
-    HIPCHK(c, sk::launch_getbit_multi(c->st, n, c->in_ids.as<uint32_t>(), c->in_off.as<uint64_t>(), c->d_dir,
-                                      c->out_u8.as<uint8_t>()));
+    if (K.single && sid[0] == kNoId) {
+        std::memset(out, 0, n);
+        return status;
+    }
+    HIPCHK(c, hipMemcpyAsync(c->in_off.p, offsets, uint64_t(n) * 8, hipMemcpyHostToDevice, c->st));
+    if (K.single) {
+        Prof p_(c, 10);
+        HIPCHK(c, sk::launch_getbit_single(c->st, n, c->in_off.as<uint64_t>(), c->strs[sid[0]].ptr,
+                                           &c->d_dir[sid[0]].len, c->out_u8.as<uint8_t>()));
+    } else {
+        std::vector<uint32_t> ops(n);
+        for (uint32_t i = 0; i < n; i++) ops[i] = sid[K.kid[i]];
+        HIPCHK(c, c->in_ids.ensure(uint64_t(n) * 4));
+        HIPCHK(c, hipMemcpyAsync(c->in_ids.p, ops.data(), uint64_t(n) * 4, hipMemcpyHostToDevice, c->st));
+        Prof p_(c, 10);
+        HIPCHK(c, sk::launch_getbit_multi(c->st, n, c->in_ids.as<uint32_t>(), c->in_off.as<uint64_t>(), c->d_dir,
+                                          c->out_u8.as<uint8_t>()));
+    }
     HIPCHK(c, hipMemcpyAsync(out, c->out_u8.p, n, hipMemcpyDeviceToHost, c->st));
     int r = sync(c);
     return r ? r : status;
@@ -2226,56 +2409,11 @@ int sk_setbit_dev(sk_ctx *c, const uint8_t *key, uint64_t len, uint64_t n, const
     if ((r = str_len(c, id, &cur))) return r;
     if (need > cur && (r = str_set_len(c, id, need))) return r;
     if (!d_out_old) {
-        // a dense batch (>= 2 ops per 128-B line of the string) streams the string through LDS region by region
-        // instead of one random atomic per op (k_sbv_apply); same bits, the ops of one value commute
-        const unsigned rb = sk::sbv_region_bits(), eb = 64u - unsigned(__builtin_clzll(mx | 1));
-        const uint64_t nr = (mx >> rb) + 1; // regions up to the highest op; >= 256 of them to fill the GPU
-        if (n >= c->sbv_min && n < (uint64_t(1) << 32) && n * 64 >= need && nr >= 256 && c->sbv_part &&
-            sk::sbv_part_ok(n, mx)) { // the hand-written region partition (k_sbv_part / k_sbv_fine / k_sbv_runs)
-            HIPCHK(c, c->keys_b.ensure(sk::sbv_part_scratch_bytes(n, mx)));
-            Prof p_(c, 9);
-            HIPCHK(c, sk::launch_setbit_void_part(c->st, n, d_offsets, mx, c->keys_b.p, c->strs[id].ptr,
-                                                  c->strs[id].cap, value & 1));
-        } else if (n >= c->sbv_min && n < (uint64_t(1) << 32) && n * 64 >= need && nr >= 256) {
-            // the same through a radix sort of the offsets by region (SK_SBV_PART=0, or a call past the tables)
-            const uint64_t *keys = d_offsets;
-            HIPCHK(c, c->vals_a.ensure((nr + 1) * 4));
-            Prof p_(c, 9);
-            if (eb > rb) { // more than one region: group the ops by region
-                size_t tmp;
-                HIPCHK(c, sk::sort_keys_size(n, rb, eb, &tmp));
-                HIPCHK(c, c->sort_tmp.ensure(tmp));
-                HIPCHK(c, c->keys_b.ensure(n * 8));
-                HIPCHK(c, sk::sort_keys(c->st, c->sort_tmp.p, c->sort_tmp.cap, d_offsets, c->keys_b.as<uint64_t>(), n,
-                                        rb, eb));
-                keys = c->keys_b.as<uint64_t>();
-            }
-            HIPCHK(c, sk::launch_setbit_void_regions(c->st, n, keys, mx, c->vals_a.as<uint32_t>(), c->strs[id].ptr,
-                                                     c->strs[id].cap, value & 1));
-        } else {
-            Prof p_(c, 9);
-            HIPCHK(c, sk::launch_setbit_void(c->st, n, d_offsets, c->strs[id].ptr, value & 1));
-        }
+        if ((r = setbit_void_device(c, id, n, d_offsets, mx, value))) return r;
         return sync(c);
     }
-    size_t tmp;
-    HIPCHK(c, sk::sort_pairs_size(n, 0, 36, &tmp));
-    HIPCHK(c, c->sort_tmp.ensure(tmp));
-    HIPCHK(c, c->keys_a.ensure(n * 8));
-    HIPCHK(c, c->keys_b.ensure(n * 8));
-    HIPCHK(c, c->vals_a.ensure(n * 4));
-    HIPCHK(c, c->vals_b.ensure(n * 4));
-    // single key: string id bits are zero in the sort key, the apply kernel reads dir[0]
-    // through a one-entry directory view of this key
-    DirEnt one{c->strs[id].ptr, 0, c->strs[id].cap};
-    HIPCHK(c, c->ptrs.ensure(sizeof(DirEnt)));
-    HIPCHK(c, hipMemcpyAsync(c->ptrs.p, &one, sizeof one, hipMemcpyHostToDevice, c->st));
-    HIPCHK(c, sk::launch_setbit_keys(c->st, n, nullptr, d_offsets, c->keys_a.as<uint64_t>(), c->vals_a.as<uint32_t>()));
-    HIPCHK(c, sk::sort_pairs(c->st, c->sort_tmp.p, c->sort_tmp.cap, c->keys_a.as<uint64_t>(), c->keys_b.as<uint64_t>(),
-                             c->vals_a.as<uint32_t>(), c->vals_b.as<uint32_t>(), n, 0, 36));
-    HIPCHK(c, sk::launch_setbit_apply(c->st, n, c->keys_b.as<uint64_t>(), c->vals_b.as<uint32_t>(), nullptr,
-                                      value & 1, c->ptrs.p, d_out_old));
-    return sync(c);
+    // replies: the region partition with the ops' seq (no library sort)
+    return setbit_regions_one(c, id, n, d_offsets, nullptr, value, mx, d_out_old);
 }
 
 // Range-sharded RBitSet routing (cluster.py ShardedBitSet.set_dev / get_dev): a device batch of logical bit offsets
@@ -2361,22 +2499,7 @@ int sk_setbit_values_dev(sk_ctx *c, const uint8_t *key, uint64_t len, uint64_t n
     if ((r = str_reserve(c, id, need))) return r;
     if ((r = str_len(c, id, &cur))) return r;
     if (need > cur && (r = str_set_len(c, id, need))) return r;
-    size_t tmp;
-    HIPCHK(c, sk::sort_pairs_size(n, 0, 36, &tmp));
-    HIPCHK(c, c->sort_tmp.ensure(tmp));
-    HIPCHK(c, c->keys_a.ensure(n * 8));
-    HIPCHK(c, c->keys_b.ensure(n * 8));
-    HIPCHK(c, c->vals_a.ensure(n * 4));
-    HIPCHK(c, c->vals_b.ensure(n * 4));
-    DirEnt one{c->strs[id].ptr, 0, c->strs[id].cap};
-    HIPCHK(c, c->ptrs.ensure(sizeof(DirEnt)));
-    HIPCHK(c, hipMemcpyAsync(c->ptrs.p, &one, sizeof one, hipMemcpyHostToDevice, c->st));
-    HIPCHK(c, sk::launch_setbit_keys(c->st, n, nullptr, d_offsets, c->keys_a.as<uint64_t>(), c->vals_a.as<uint32_t>()));
-    HIPCHK(c, sk::sort_pairs(c->st, c->sort_tmp.p, c->sort_tmp.cap, c->keys_a.as<uint64_t>(), c->keys_b.as<uint64_t>(),
-                             c->vals_a.as<uint32_t>(), c->vals_b.as<uint32_t>(), n, 0, 36));
-    HIPCHK(c, sk::launch_setbit_apply(c->st, n, c->keys_b.as<uint64_t>(), c->vals_b.as<uint32_t>(), d_values, 0,
-                                      c->ptrs.p, d_out_old));
-    return sync(c);
+    return setbit_regions_one(c, id, n, d_offsets, d_values, 0, mx, d_out_old);
 }
 
 // RBitSet.set(from, to) / clear(from, to): the reference sends one SETBIT_VOID

@@ -474,6 +474,19 @@ class SketchEngine:
         self._check(self.lib.sk_getbit(self.ctx, n, _addr(koff), _addr(kbuf), _addr(offs), _addr(out)))
         return [int(x) for x in out]
 
+    def setbit_packed(self, koff, kbuf, offsets, values, out=None):
+        """sk_setbit over caller-packed key names (koff u64[n + 1] into kbuf) and host arrays, as the JNI shim passes
+        them; out: u8[n] for the old bits, None for SETBIT_VOID."""
+        offs = np.ascontiguousarray(offsets, dtype=np.uint64)
+        vals = np.ascontiguousarray(values, dtype=np.uint8)
+        self._check(self.lib.sk_setbit(self.ctx, len(offs), _addr(koff), _addr(kbuf), _addr(offs), _addr(vals),
+                                       _addr(out)))
+
+    def getbit_packed(self, koff, kbuf, offsets, out):
+        """sk_getbit over caller-packed key names and host arrays (out: u8[n])."""
+        offs = np.ascontiguousarray(offsets, dtype=np.uint64)
+        self._check(self.lib.sk_getbit(self.ctx, len(offs), _addr(koff), _addr(kbuf), _addr(offs), _addr(out)))
+
     def setbit_dev(self, key, n: int, d_offsets, value: int, d_out_old=None):
         k = _b(key)
         self._check(self.lib.sk_setbit_dev(self.ctx, k, len(k), n, _addr(d_offsets), value, _addr(d_out_old)))

@@ -204,7 +204,7 @@ def test_hot_path_kernels_use_no_scratch():
         notes = subprocess.run([f"{llvm}/llvm-readelf", "--notes", co], check=True, capture_output=True,
                                text=True).stdout
     meta = yaml.safe_load(notes[notes.index("---"):notes.rindex("...")])
-    hot = re.compile(r"k_(bloom_rc|bloom_ra|pfl_|pfp_|hll_sum|hll_hist|hll_union|getbit|setbit|sbv_|bitcount|bitop)")
+    hot = re.compile(r"k_(bloom_rc|bloom_ra|pfl_|pfp_|hll_sum|hll_hist|hll_union|getbit|setbit|sbv_|sbr_|bitcount|bitop)")
     seen = 0
     for k in meta["amdhsa.kernels"]:
         if hot.search(k[".name"]):

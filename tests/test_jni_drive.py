@@ -53,6 +53,7 @@ def test_jni_drive_every_entry_point(O):
     assert out["pfmerge_count"] == ["0", str(ref.count([b"jd:m"]))]
     assert out["setbit"] == ["0", "0", "0", "1", "0"]
     assert out["getbit"] == ["0", "0", "1", "1", "0"]
+    assert out["void_getbit"] == ["0", "1", "1", "0"]   # SETBIT_VOID with a null reply array
     assert out["bitcount"] == ["0", "1"] and out["strlen"] == ["0", "13"]
     s = bytearray(13)
     s[100 >> 3] |= 0x80 >> (100 & 7)

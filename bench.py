@@ -277,7 +277,7 @@ def main():
     lines = 128.0 * len(mine)
     touched = lines * (1.0 - math.exp(-(G * B) / lines))
     piece = min(CB, 32 << 20)                         # contains pieces of <= 32 M elements (sk_store.cpp)
-    own = {"pfadd": mean_len_h + 8 + 4 + 1 + 4 * 8 + 2 * 128 * touched / (G * B),
+    own = {"pfadd": mean_len_h + 8 + 4 + 1 + 4 * 8 + 2 * 96 * touched / (G * B),
            "bloom_contains": mean_len_b + 8 + 1 + 2 * 4 * (k - 1) + 2 * 4.0 * nr / 4096 + (size / 8.0) / piece}
     # PMC bytes per dispatch x dispatches of each kernel per launch of the chain (a 64 M contains call is two
     # 32 M pieces)
@@ -400,13 +400,13 @@ def per_unit_bytes(mean_len_h, mean_len_b, k, size, CB, nr, tenants, group):
     priced at one 64-B sector; streamed data at its bytes."""
     P = k - 1
     seg = 4.0 * nr / 4096            # segment table entry per hash block, per element
-    lines = 128.0 * tenants          # 128-B register lines of the arena; a group of `group` elements touches
+    lines = 128.0 * tenants          # 128-register lines (96 B packed) of the arena; a group of `group` elements touches
     touched = lines * (1.0 - math.exp(-group / lines))   # this many of them (uniform tenants)
     return {
         "pfl_hash": mean_len_h + 8 + 4 + 8,            # key bytes + offset + slab id in, record out
         "pfl_part": 8 + 8,                             # records read once and written once (tile-major region sort)
         "pfl_fill": 1,                                 # the default reply, streamed
-        "pfl_apply": 6 + 2 * 128 * touched / group,    # 6-B record + each touched line in and out once
+        "pfl_apply": 6 + 2 * 96 * touched / group,     # 6-B record + each touched 96-B packed line in and out once
         "pfp_hash": mean_len_h + 8 + 4 + 8,            # key bytes + offset + slab id in, record out
         "pfp_apply": 8 + 64 + 64 + 1,                  # record + register sector load (R0) + store + reply
         "pfp_reply": 1 + 2 + 1,                        # chunk-order reply + chunk slot in, reply out

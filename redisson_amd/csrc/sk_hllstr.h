@@ -143,16 +143,30 @@ inline int hll_sparse_set(HllStr &h, uint32_t index, uint8_t count) {
 // value 1..32)).  Returns SK_OK, SK_EWRONGTYPE (not an HLL string: what
 // isHLLObjectOrReply rejects) or SK_ECORRUPT (sparse opcodes that do not cover
 // exactly 16384 registers).
+// the 12,288-B dense register body (HLL_DENSE_GET_REGISTER / _SET_REGISTER: 6 bits at bit 6*i, LSB first) <-> 16384
+// u8 registers.  The engine's HBM arena holds exactly these bodies.
+inline void hll_body_unpack(const uint8_t *body, uint8_t *regs) {
+    for (int i = 0; i < 16384; i++) {
+        unsigned bit = unsigned(i) * 6, byte = bit >> 3, fb = bit & 7;
+        unsigned v = unsigned(body[byte]) >> fb;
+        if (fb > 2) v |= unsigned(body[byte + 1]) << (8 - fb);
+        regs[i] = uint8_t(v & 63);
+    }
+}
+inline void hll_body_pack(const uint8_t *regs, uint8_t *body) {
+    std::memset(body, 0, 12288);
+    for (int i = 0; i < 16384; i++) {
+        unsigned byte = unsigned(i * 6) / 8, fb = unsigned(i * 6) & 7, v = regs[i] & 63;
+        body[byte] |= uint8_t(v << fb);
+        if (fb > 2) body[byte + 1] |= uint8_t(v >> (8 - fb));
+    }
+}
+
 inline int hll_decode(const uint8_t *s, uint64_t len, uint8_t *regs) {
     if (len < 16 || std::memcmp(s, "HYLL", 4) != 0 || s[4] > 1) return SK_EWRONGTYPE;
     if (s[4] == 0) { // dense
         if (len != SK_HLL_DENSE_SIZE) return SK_EWRONGTYPE;
-        for (int i = 0; i < 16384; i++) {
-            unsigned bit = unsigned(i) * 6, byte = bit >> 3, fb = bit & 7;
-            unsigned v = unsigned(s[16 + byte]) >> fb;
-            if (fb > 2) v |= unsigned(s[16 + byte + 1]) << (8 - fb);
-            regs[i] = uint8_t(v & 63);
-        }
+        hll_body_unpack(s + 16, regs);
         return SK_OK;
     }
     uint64_t idx = 0;
@@ -179,11 +193,7 @@ inline void hll_dense_encode(const uint8_t *regs, const uint8_t *hdr, uint8_t *o
     std::memcpy(out, "HYLL", 4);
     out[15] = 0x80;
     if (hdr) std::memcpy(out, hdr, 16);
-    for (int i = 0; i < 16384; i++) {
-        unsigned byte = unsigned(i * 6) / 8, fb = unsigned(i * 6) & 7, v = regs[i] & 63;
-        out[16 + byte] |= uint8_t(v << fb);
-        if (fb > 2) out[16 + byte + 1] |= uint8_t(v >> (8 - fb));
-    }
+    hll_body_pack(regs, out + 16);
 }
 
 } // namespace sk_hll

@@ -6,22 +6,7 @@
 
 namespace sk {
 
-hipError_t launch_pfadd_hash(hipStream_t st, uint64_t n, const uint32_t *key_ids, const uint64_t *off,
-                             const uint8_t *bytes, const uint32_t *cmd_of, int v5, unsigned slot_shift,
-                             uint64_t *out_keys);
-hipError_t launch_pfadd_apply(hipStream_t st, uint64_t n, const uint64_t *keys, unsigned slot_shift, uint64_t cmd_mask,
-                              uint8_t *arena, uint8_t *changed);
-hipError_t launch_pfadd_claim(hipStream_t st, uint64_t n, const uint32_t *key_ids, const uint64_t *off,
-                              const uint8_t *bytes, int v5, uint8_t *arena, uint64_t *rec, uint8_t *changed_i,
-                              uint32_t *conf_count, int claim_all);
-hipError_t launch_pfadd_conflicts(hipStream_t st, const uint64_t *conf_keys, const uint64_t *conf_vals,
-                                  const uint32_t *conf_count, uint8_t *arena, uint8_t *changed, uint32_t *host_count);
-hipError_t launch_pfadd_commit(hipStream_t st, uint64_t n, const uint64_t *rec, const uint32_t *cmd_of, uint8_t *arena,
-                               uint8_t *changed, uint64_t *conf_keys, uint64_t *conf_vals, uint32_t *conf_count,
-                               uint32_t conf_cap);
-hipError_t launch_pfadd_conflicts_sorted(hipStream_t st, uint64_t cnt, const uint64_t *K, const uint64_t *V,
-                                         uint8_t *arena, uint8_t *changed);
-uint32_t pfadd_conflict_lds_capacity();
+
 uint32_t pfp_blocks(uint64_t n);
 uint32_t pfp_buckets();
 uint32_t pfp_epb();
@@ -85,12 +70,16 @@ hipError_t sort_pairs(hipStream_t st, void *tmp, size_t tmp_bytes, const uint64_
                       const uint32_t *vin, uint32_t *vout, uint64_t n, unsigned begin_bit, unsigned end_bit);
 // per key: out[2k] = sum 2^(40 - r) over the registers, out[2k+1] = zeros | (a register >= 40) << 32 (PFCOUNT 3.x)
 hipError_t launch_hll_sum(hipStream_t st, uint64_t n, const uint32_t *ids, const uint8_t *arena, uint64_t *out);
-hipError_t launch_hll_hist(hipStream_t st, uint64_t n, const uint32_t *ids, const uint8_t *arena, uint32_t *hist);
-// Redis dense HLL bodies in bulk (SAVE / DUMP / snapshot restore): out / in hold n x 12,288 B (4-B aligned), n < 2^30
+// 64-bin register histograms: slabs ids[] of the packed arena (packed), or u8 register arrays (ids[k] = 0)
+hipError_t launch_hll_hist(hipStream_t st, uint64_t n, const uint32_t *ids, const uint8_t *arena, uint32_t *hist,
+                           int packed);
+// Redis dense HLL bodies in bulk (SAVE / DUMP / snapshot restore): out / in hold n x 12,288 B (16-B aligned), n < 2^30
 hipError_t launch_hll_pack(hipStream_t st, uint64_t n, const uint32_t *ids, const uint8_t *arena, uint8_t *out);
 hipError_t launch_hll_unpack(hipStream_t st, uint64_t n, const uint32_t *ids, const uint8_t *in, uint8_t *arena);
-hipError_t launch_hll_union(hipStream_t st, uint64_t n, const uint32_t *ids, const uint8_t *arena, uint8_t *partial,
-                            uint64_t max_groups, uint8_t *out, int include_out);
+// out = max over sources (include_out: and out): sources are slabs ids[] of the packed arena (src_packed) or u8
+// register arrays (ids null: consecutive 16 KiB arrays); out is a packed slab (out_packed) or 16384 u8 registers
+hipError_t launch_hll_union(hipStream_t st, uint64_t n, const uint32_t *ids, const uint8_t *src, uint8_t *partial,
+                            uint64_t max_groups, uint8_t *out, int include_out, int src_packed, int out_packed);
 // scratch: 16 B per element, used by the split schedule (sched 3) only
 hipError_t launch_bloom_contains(hipStream_t st, uint64_t n, const uint64_t *off, const uint8_t *bytes,
                                  const uint8_t *bits, const uint64_t *d_len, uint64_t size, uint64_t magic, int k,

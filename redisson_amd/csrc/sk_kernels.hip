@@ -1,8 +1,8 @@
 // sk_kernels.hip -- CDNA4 (gfx950) kernels of the sketch engine.
 //
 // Layout in HBM (see DESIGN.md "Data layout"):
-//   HLL arena   : u8 registers, 16384 per slab, slab id -> arena + id*16 KiB
-//                 (unpacked; the 6-bit Redis dense form is produced on GET).
+//   HLL arena   : Redis's dense register bodies, 12,288 B (16384 x 6 bits) per slab,
+//                 slab id -> arena + id * 12288 (SK_SLAB_BYTES; GET copies it).
 //   bit strings : one buffer per key, Redis MSB-first bytes, capacity a
 //                 multiple of 16 B, bytes in [len, cap) kept zero; a device
 //                 directory {ptr, len, cap} per string id, len grown by
@@ -32,6 +32,75 @@ static inline unsigned grid_for(uint64_t n, unsigned block, unsigned cap = 0x7ff
     return g > cap ? cap : unsigned(g);
 }
 
+// ------------------------------------------------------------------ the HLL arena: Redis's dense registers
+// A slab is the 12,288-B register body of Redis's dense encoding (HLL_DENSE_GET/SET_REGISTER, hyperloglog.c):
+// register i in bits [6i, 6i + 6) of the body, LSB first.  So 16 registers are exactly 12 bytes (three u32 words) and
+// a 128-register line exactly 96 bytes; GET / DUMP / SAVE copy the body as it is.  The arena ends with 16 B of
+// padding (a field read takes the byte after its own).
+#define SK_SLAB_BYTES 12288u
+__device__ __forceinline__ uint8_t *slab_at(uint8_t *arena, uint64_t slab) { return arena + slab * SK_SLAB_BYTES; }
+__device__ __forceinline__ const uint8_t *slab_at(const uint8_t *arena, uint64_t slab) {
+    return arena + slab * SK_SLAB_BYTES;
+}
+// the slab of a caller's handle (slab | generation << 24).  The empty asm keeps the mask: hipcc (ROCm 7.2) compiles
+// `(h & 0xffffff) * 12288` into one v_mad_u64_u32 of the UNMASKED h, so a handle with a nonzero generation addressed
+// 12288 x 2^24 x gen bytes past its slab (a memory aperture violation on the GPU, round 6; tools/micro: the 4-line
+// reproducer in DESIGN "The packed arena").  With the barrier the AND is materialised before the multiply.
+__device__ __forceinline__ uint64_t slab_of(uint32_t handle) {
+    uint32_t s = handle & SK_SLAB_MASK;
+    __asm__ volatile("" : "+v"(s));
+    return s;
+}
+// register r of a slab (two byte loads: the field may straddle a byte boundary)
+__device__ __forceinline__ uint32_t reg_get(const uint8_t *slab, uint32_t r) {
+    const uint32_t bit = 6u * r, by = bit >> 3;
+    return ((uint32_t(slab[by]) | (uint32_t(slab[by + 1]) << 8)) >> (bit & 7u)) & 63u;
+}
+// register r of a slab from `old` to old ^ x: device-scope XORs on its aligned word(s).  Other registers of the same
+// words may change at the same time (their own XORs commute with this one); the caller is this register's only
+// writer and knows its value.
+__device__ __forceinline__ void reg_xor(uint8_t *slab, uint32_t r, uint32_t x) {
+    if (!x) return;
+    uint32_t *w = reinterpret_cast<uint32_t *>(slab);
+    const uint32_t bit = 6u * r, wi = bit >> 5, sh = bit & 31u;
+    atomicXor(&w[wi], x << sh);
+    if (sh > 26u) atomicXor(&w[wi + 1], x >> (32u - sh));
+}
+// 16 registers <-> their 12 bytes: a 16-B vector of u8 registers <-> three u32 words
+__device__ __forceinline__ void pack16(uint4 r, uint32_t *w) {
+    const uint32_t b0 = r.x, b1 = r.y, b2 = r.z, b3 = r.w;
+    auto g = [](uint32_t v, int i) { return (v >> (8 * i)) & 63u; };
+    w[0] = g(b0, 0) | g(b0, 1) << 6 | g(b0, 2) << 12 | g(b0, 3) << 18 | g(b1, 0) << 24 | (g(b1, 1) & 3u) << 30;
+    w[1] = g(b1, 1) >> 2 | g(b1, 2) << 4 | g(b1, 3) << 10 | g(b2, 0) << 16 | g(b2, 1) << 22 | (g(b2, 2) & 15u) << 28;
+    w[2] = g(b2, 2) >> 4 | g(b2, 3) << 2 | g(b3, 0) << 8 | g(b3, 1) << 14 | g(b3, 2) << 20 | g(b3, 3) << 26;
+}
+__device__ __forceinline__ uint4 unpack16(uint32_t w0, uint32_t w1, uint32_t w2) {
+    auto q = [](uint32_t a, uint32_t b, uint32_t c, uint32_t d) { return a | b << 8 | c << 16 | d << 24; };
+    const uint32_t r0 = w0 & 63u, r1 = (w0 >> 6) & 63u, r2 = (w0 >> 12) & 63u, r3 = (w0 >> 18) & 63u;
+    const uint32_t r4 = (w0 >> 24) & 63u, r5 = (w0 >> 30) | ((w1 & 15u) << 2), r6 = (w1 >> 4) & 63u;
+    const uint32_t r7 = (w1 >> 10) & 63u, r8 = (w1 >> 16) & 63u, r9 = (w1 >> 22) & 63u;
+    const uint32_t r10 = (w1 >> 28) | ((w2 & 3u) << 4), r11 = (w2 >> 2) & 63u, r12 = (w2 >> 8) & 63u;
+    const uint32_t r13 = (w2 >> 14) & 63u, r14 = (w2 >> 20) & 63u, r15 = w2 >> 26;
+    return make_uint4(q(r0, r1, r2, r3), q(r4, r5, r6, r7), q(r8, r9, r10, r11), q(r12, r13, r14, r15));
+}
+// group g (16 registers) of a packed body: three word loads (nontemporal: streamed once)
+__device__ __forceinline__ uint4 grp_load_nt(const uint8_t *body, uint32_t g) {
+    const uint32_t *w = reinterpret_cast<const uint32_t *>(body) + 3 * g;
+    return unpack16(__builtin_nontemporal_load(w), __builtin_nontemporal_load(w + 1), __builtin_nontemporal_load(w + 2));
+}
+__device__ __forceinline__ uint4 grp_load(const uint8_t *body, uint32_t g) {
+    const uint32_t *w = reinterpret_cast<const uint32_t *>(body) + 3 * g;
+    return unpack16(w[0], w[1], w[2]);
+}
+__device__ __forceinline__ void grp_store(uint8_t *body, uint32_t g, uint4 r) {
+    uint32_t p[3];
+    pack16(r, p);
+    uint32_t *w = reinterpret_cast<uint32_t *>(body) + 3 * g;
+    w[0] = p[0];
+    w[1] = p[1];
+    w[2] = p[2];
+}
+
 // ------------------------------------------------------------------ PFADD
 // hllPatLen: register index = low 14 bits; rho = 1 + trailing zeros of
 // bits 14.. with the version's sentinel (3.2: bit 63 -> rho <= 50,
@@ -40,222 +109,6 @@ __device__ __forceinline__ void hll_pat(uint64_t h, int v5, uint32_t *reg, uint3
     *reg = uint32_t(h & 16383u);
     uint64_t x = (h >> 14) | (v5 ? (1ull << 50) : (1ull << 49));
     *rho = 1u + uint32_t(__builtin_ctzll(x));
-}
-
-__global__ void __launch_bounds__(256) k_pfadd_hash(uint64_t n, const uint32_t *__restrict__ key_ids,
-                                                    const uint64_t *__restrict__ off,
-                                                    const uint8_t *__restrict__ bytes,
-                                                    const uint32_t *__restrict__ cmd_of, int v5,
-                                                    unsigned slot_shift, uint64_t *__restrict__ out_keys) {
-    uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    uint64_t o = off[i];
-    uint32_t len = uint32_t(off[i + 1] - o);
-    uint64_t h = murmur64a(bytes + o, len, 0xadc83b19ull);
-    uint32_t reg, rho;
-    hll_pat(h, v5, &reg, &rho);
-    uint64_t cmd = cmd_of ? cmd_of[i] : i;
-    uint64_t slot = (uint64_t(key_ids[i] & SK_SLAB_MASK) << 14) | reg;
-    out_keys[i] = (slot << slot_shift) | (cmd << 6) | rho;
-}
-
-// One thread per sorted element; the first element of each (slab, register)
-// segment walks the segment in batch order: exact PFADD replies, one store.
-__global__ void __launch_bounds__(256) k_pfadd_apply(uint64_t n, const uint64_t *__restrict__ keys,
-                                                     unsigned slot_shift, uint64_t cmd_mask,
-                                                     uint8_t *__restrict__ arena, uint8_t *__restrict__ changed) {
-    uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    uint64_t k = keys[i];
-    uint64_t slot = k >> slot_shift;
-    if (i > 0 && (keys[i - 1] >> slot_shift) == slot) return;
-    uint8_t *r = arena + slot; // slot = id*16384 + reg
-    uint32_t R0 = *r, R = R0;
-    for (uint64_t j = i; j < n; j++) {
-        uint64_t kk = (j == i) ? k : keys[j];
-        if ((kk >> slot_shift) != slot) break;
-        uint32_t rho = uint32_t(kk & 63u);
-        if (rho > R) {
-            changed[(kk >> 6) & cmd_mask] = 1;
-            R = rho;
-        }
-    }
-    if (R != R0) *r = uint8_t(R);
-}
-
-
-// ----------------------------------------------------- PFADD, sparse path
-// For batches that touch many registers thinly (C2: 1M elements over
-// 100k x 16384 registers) the sort is replaced by a claim / commit protocol
-// that uses the two spare bits of every register byte (values <= 51 < 64):
-//   bit 7 CLAIMED  -- some candidate of this batch targets the register
-//   bit 6 CONFLICT -- at least two candidates target it
-// A candidate is an element whose rho exceeds the pre-batch value R0 (the
-// value bits never change during the claim pass).  A register with a single
-// candidate is raised by it and that command replies 1 -- exactly the
-// sequential result, because non-candidates change nothing.  Registers with
-// several candidates (rare: ~n^2/2R pairs) are replayed in batch order by
-// k_pfadd_conflicts.  Flags are cleared by the commit that writes the value.
-#define SK_CLAIMED 0x80u
-#define SK_CONFLICT 0x40u
-
-template <bool ALL>
-__global__ void __launch_bounds__(256) k_pfadd_claim(uint64_t n, const uint32_t *__restrict__ key_ids,
-                                                     const uint64_t *__restrict__ off,
-                                                     const uint8_t *__restrict__ bytes, int v5, uint8_t *arena,
-                                                     uint64_t *__restrict__ rec, uint8_t *__restrict__ changed_i,
-                                                     uint32_t *conf_count) {
-    __shared__ uint64_t lds[SK_STAGE_WORDS];
-    uint64_t e0 = uint64_t(blockIdx.x) * blockDim.x, e1 = e0 + blockDim.x < n ? e0 + blockDim.x : n;
-    uint64_t lo = off[e0], hi = off[e1];
-    bool staged = stage_fits(lo, hi); // uniform per workgroup
-    uint32_t wbase = staged ? stage_keys(bytes, lo, hi, lds) : 0u;
-    uint64_t i = e0 + threadIdx.x;
-    if (i == 0) *conf_count = 0; // consumed by k_pfadd_commit, which runs after this kernel
-    if (i >= n) return;
-    if (changed_i) changed_i[i] = 0; // one element per command: replies start at 0
-    uint64_t o = off[i];
-    uint32_t len = uint32_t(off[i + 1] - o);
-    uint64_t h = staged ? murmur64a_r(LdsReader{lds, wbase + uint32_t(o - lo)}, len, 0xadc83b19ull)
-                        : murmur64a(bytes + o, len, 0xadc83b19ull);
-    uint32_t reg, rho;
-    hll_pat(h, v5, &reg, &rho);
-    uint64_t slot = (uint64_t(key_ids[i] & SK_SLAB_MASK) << 14) | reg;
-    uint8_t *p = arena + slot;
-    uint32_t sh = uint32_t(slot & 3) * 8u;
-    uint32_t *w = reinterpret_cast<uint32_t *>(arena + (slot & ~uint64_t(3)));
-    uint64_t r = 0;
-    if (ALL) {
-        // every element claims; the atomic's old value is also R0 (one random op, no load)
-        uint32_t old = atomicOr(w, SK_CLAIMED << sh);
-        uint32_t b = (old >> sh) & 0xffu;
-        if (b & SK_CLAIMED) atomicOr(w, SK_CONFLICT << sh);
-        uint32_t cand = rho > (b & 63u);
-        r = (slot << 8) | (uint64_t(cand) << 7) | (uint64_t(rho) << 1) | 1u;
-    } else if (rho > (uint32_t(*p) & 63u)) { // candidates only: load, then claim
-        uint32_t old = atomicOr(w, SK_CLAIMED << sh);
-        if ((old >> sh) & SK_CLAIMED) atomicOr(w, SK_CONFLICT << sh);
-        r = (slot << 8) | (1u << 7) | (uint64_t(rho) << 1) | 1u;
-    }
-    rec[i] = r;
-}
-
-__global__ void __launch_bounds__(256) k_pfadd_commit(uint64_t n, const uint64_t *__restrict__ rec,
-                                                      const uint32_t *__restrict__ cmd_of, uint8_t *arena,
-                                                      uint8_t *__restrict__ changed, uint64_t *conf_keys,
-                                                      uint64_t *conf_vals, uint32_t *conf_count, uint32_t conf_cap) {
-    uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    uint64_t r = rec[i];
-    if (!(r & 1u)) return;
-    uint64_t slot = r >> 8;
-    uint32_t rho = uint32_t(r >> 1) & 63u;
-    bool cand = (r >> 7) & 1u;
-    uint32_t cmd = cmd_of ? cmd_of[i] : uint32_t(i);
-    uint8_t *p = arena + slot;
-    uint32_t b = *p;
-    if (!(b & SK_CONFLICT)) { // the only claimer of this register
-        if (cand) {
-            *p = uint8_t(rho); // raise and clear the flags
-            changed[cmd] = 1;
-        } else {
-            *p = uint8_t(b & 63u); // non-candidate claimer: just clear the flag
-        }
-        return;
-    }
-    uint32_t k = atomicAdd(conf_count, 1u);
-    if (k < conf_cap) {
-        conf_keys[k] = (slot << 26) | i; // batch order inside a register
-        // R0: the value bits are untouched until the replay writes the register
-        conf_vals[k] = (uint64_t(cmd) << 16) | (uint64_t(b & 63u) << 8) | rho;
-    }
-}
-
-// Conflict replay.  Every conflict entry carries (slot, seq) as its key and
-// (cmd, R0, rho) as its value.  Entry t is raised iff its rho beats R0 and the
-// rho of every earlier (lower seq) entry of its register; the earliest entry
-// of a register writes max(R0, every rho) and so clears the flags.  One
-// 1024-thread workgroup loads up to SK_CONF_MAX entries into LDS and chains
-// them by register in an LDS hash table (atomicExch on bucket heads), so each
-// entry visits only the entries of its own register.  Longer lists are left
-// to the host (rocPRIM sort + k_pfadd_conflicts_sorted).
-#define SK_CONF_TPB 1024
-#define SK_CONF_MAX 4096
-#define SK_CONF_BUCKETS 4096
-__global__ void __launch_bounds__(SK_CONF_TPB) k_pfadd_conflicts(const uint64_t *__restrict__ conf_keys,
-                                                                 const uint64_t *__restrict__ conf_vals,
-                                                                 const uint32_t *__restrict__ conf_count,
-                                                                 uint8_t *arena, uint8_t *__restrict__ changed,
-                                                                 uint32_t *host_count) {
-    __shared__ uint64_t K[SK_CONF_MAX];
-    __shared__ uint64_t V[SK_CONF_MAX];
-    __shared__ uint32_t head[SK_CONF_BUCKETS];
-    __shared__ uint32_t nxt[SK_CONF_MAX];
-    uint32_t cnt = *conf_count;
-    if (threadIdx.x == 0) *host_count = cnt; // zero-copy: read after the stream sync
-    if (cnt == 0 || cnt > SK_CONF_MAX) return;
-    constexpr int PER = SK_CONF_MAX / SK_CONF_TPB;
-    uint64_t kr[PER], vr[PER];
-#pragma unroll
-    for (int q = 0; q < PER; q++) { // every global load issued before the LDS stores
-        uint32_t t = threadIdx.x + q * SK_CONF_TPB;
-        kr[q] = t < cnt ? conf_keys[t] : 0;
-        vr[q] = t < cnt ? conf_vals[t] : 0;
-    }
-    for (uint32_t b = threadIdx.x; b < SK_CONF_BUCKETS; b += SK_CONF_TPB) head[b] = 0xffffffffu;
-    __syncthreads();
-#pragma unroll
-    for (int q = 0; q < PER; q++) {
-        uint32_t t = threadIdx.x + q * SK_CONF_TPB;
-        if (t < cnt) {
-            K[t] = kr[q];
-            V[t] = vr[q];
-            uint32_t bkt = uint32_t(((kr[q] >> 26) * 0x9E3779B97F4A7C15ull) >> 52);
-            nxt[t] = atomicExch(&head[bkt], t);
-        }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int q = 0; q < PER; q++) {
-        uint32_t t = threadIdx.x + q * SK_CONF_TPB;
-        if (t >= cnt) continue;
-        uint64_t kt = kr[q], vt = vr[q];
-        uint64_t slot = kt >> 26;
-        uint32_t rho = uint32_t(vt & 63u), R0 = uint32_t(vt >> 8) & 63u;
-        uint32_t mx = rho, pm = 0, nearlier = 0;
-        uint32_t bkt = uint32_t((slot * 0x9E3779B97F4A7C15ull) >> 52);
-        for (uint32_t u = head[bkt]; u != 0xffffffffu; u = nxt[u]) {
-            uint64_t ku = K[u];
-            if ((ku >> 26) != slot) continue;
-            uint32_t ru = uint32_t(V[u] & 63u);
-            mx = ru > mx ? ru : mx;
-            if (ku < kt) {
-                nearlier++;
-                pm = ru > pm ? ru : pm;
-            }
-        }
-        if (rho > (R0 > pm ? R0 : pm)) changed[vt >> 16] = 1;
-        if (nearlier == 0) arena[slot] = uint8_t(R0 > mx ? R0 : mx);
-    }
-}
-
-// host fallback for long conflict lists: same replay over a rocPRIM-sorted list
-__global__ void __launch_bounds__(256) k_pfadd_conflicts_sorted(uint64_t cnt, const uint64_t *__restrict__ K,
-                                                                const uint64_t *__restrict__ V, uint8_t *arena,
-                                                                uint8_t *__restrict__ changed) {
-    uint64_t t = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-    if (t >= cnt) return;
-    uint64_t slot = K[t] >> 26;
-    if (t > 0 && (K[t - 1] >> 26) == slot) return;
-    uint32_t R = uint32_t(V[t] >> 8) & 63u; // R0
-    for (uint64_t u = t; u < cnt && (K[u] >> 26) == slot; u++) {
-        uint32_t rho = uint32_t(V[u] & 63u);
-        if (rho > R) {
-            changed[V[u] >> 16] = 1;
-            R = rho;
-        }
-    }
-    arena[slot] = uint8_t(R);
 }
 
 // Bloom add: the string length follows the largest probed bit = the last sorted key
@@ -286,6 +139,9 @@ __global__ void k_len_from_last_key(const uint64_t *keys, uint64_t m, uint64_t *
 #define SK_PFP_TPB 1024   // threads per hash workgroup (16 waves: one per CU hides the latency)
 #define SK_PFP_EPB 4096   // elements per hash workgroup = max blocks 256 for n <= 2^20
 #define SK_PFP_ATPB 1024  // threads per apply workgroup (4 per block segment)
+#ifndef SK_PFP_BYTEW
+#define SK_PFP_BYTEW 0    // the apply's register writes as byte stores where no neighbour shares the bytes (else XORs)
+#endif
 #define SK_PFP_CAP 4096   // records one apply workgroup holds in LDS
 #define SK_PFP_HT 4096    // LDS hash-chain heads
 #define SK_PFP_STAGE (4 * SK_STAGE_WORDS) // LDS key window (u64 words) for SK_PFP_TPB elements
@@ -817,7 +673,7 @@ __device__ void pfp_big_resolve(const uint64_t *seg, uint32_t t0, uint32_t seg_c
     for (uint32_t t = t0; t < seg_cnt; t += 4) { // replies (the arena is only read)
         uint64_t r = seg[t], slot = r >> 26;
         uint32_t rho = uint32_t(r & 63u), seq = uint32_t((r >> 6) & 0xfffffu);
-        bool first = rho > (uint32_t(arena[slot]) & 63u);
+        bool first = rho > reg_get(slab_at(arena, slot >> 14), uint32_t(slot) & 16383u);
         // v = rho: no earlier equal rho; v > rho: no earlier larger one
         for (uint32_t v = rho; v < 52 && first; v++) first = T.find((slot << 6) | v) >= seq;
         if (first) pfp_event(ev, ev_n, r);
@@ -831,7 +687,10 @@ __device__ void pfp_big_resolve(const uint64_t *seg, uint32_t t0, uint32_t seg_c
         if (T.find((slot << 6) | rho) != seq) continue;
         bool top = true;
         for (uint32_t v = rho + 1; v < 52 && top; v++) top = T.find((slot << 6) | v) == 0xffffffffu;
-        if (top && rho > (uint32_t(arena[slot]) & 63u)) arena[slot] = uint8_t(rho);
+        if (!top) continue;
+        uint8_t *sl = slab_at(arena, slot >> 14);
+        const uint32_t cur = reg_get(sl, uint32_t(slot) & 16383u); // this thread is the register's only writer
+        if (rho > cur) reg_xor(sl, uint32_t(slot) & 16383u, cur ^ rho);
     }
 }
 
@@ -876,16 +735,17 @@ __global__ void __launch_bounds__(SK_PFP_ATPB) __attribute__((amdgpu_waves_per_e
     uint32_t t = sub;
     for (; t + 4 < c; t += 8) { // two records per step: both loads, then both register loads, in flight
         uint64_t ra = seg[t], rb = seg[t + 4];
-        uint8_t va = arena[ra >> 26], vb = arena[rb >> 26];
+        const uint32_t va = reg_get(slab_at(arena, ra >> 40), uint32_t(ra >> 26) & 16383u);
+        const uint32_t vb = reg_get(slab_at(arena, rb >> 40), uint32_t(rb >> 26) & 16383u);
         R[dst + t] = ra;
         R[dst + t + 4] = rb;
-        r0[dst + t] = va & 63u;
-        r0[dst + t + 4] = vb & 63u;
+        r0[dst + t] = uint8_t(va);
+        r0[dst + t + 4] = uint8_t(vb);
     }
     if (t < c) {
         uint64_t ra = seg[t];
         R[dst + t] = ra;
-        r0[dst + t] = arena[ra >> 26] & 63u;
+        r0[dst + t] = uint8_t(reg_get(slab_at(arena, ra >> 40), uint32_t(ra >> 26) & 16383u));
     }
     __syncthreads();
     for (uint32_t u = threadIdx.x; u < cnt; u += SK_PFP_ATPB)
@@ -916,7 +776,30 @@ __global__ void __launch_bounds__(SK_PFP_ATPB) __attribute__((amdgpu_waves_per_e
         if (reply) pfp_event(ev, ev_n, rt);
         if (changed) changed[seq] = reply; // one element per command: straight to batch order
         else r0[tq] = reply;               // the reply replaces R0 (read by this thread only)
-        if (earliest && m > R0) arena[slot] = uint8_t(m);
+        if (earliest && m > R0) {
+            uint8_t *sl = slab_at(arena, slot >> 14);
+            const uint32_t r = uint32_t(slot) & 16383u;
+#if SK_PFP_BYTEW
+            // byte stores when no register sharing the field's bytes has a record in this batch (no other writer
+            // of those bytes: runs of 32 registers are 24 whole bytes, owned by this workgroup); else XORs
+            auto has = [&](uint64_t sl2) {
+                for (uint32_t v = head[pfp_ht(sl2)]; v != 0xffffu; v = nxt[v])
+                    if ((R[v] >> 26) == sl2) return true;
+                return false;
+            };
+            const bool lo_shared = (r & 3u) != 0, hi_shared = (r & 3u) != 3;
+            if (!(lo_shared && (r & 31u) != 0 && has(slot - 1)) && !(hi_shared && (r & 31u) != 31 && has(slot + 1))) {
+                const uint32_t bit = 6u * r, by = bit >> 3, sh = bit & 7u;
+                const uint32_t v16 = (uint32_t(sl[by]) | (uint32_t(sl[by + 1]) << 8)) ^ ((R0 ^ m) << sh);
+                sl[by] = uint8_t(v16);
+                if (sh > 2u) sl[by + 1] = uint8_t(v16 >> 8);
+            } else {
+                reg_xor(sl, r, R0 ^ m);
+            }
+#else
+            reg_xor(sl, r, R0 ^ m);
+#endif
+        }
     }
     if (changed) return;
     __syncthreads();
@@ -1389,22 +1272,35 @@ __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const PflRec rec2,
         if (blockIdx.x >= order_n[0]) return; // uniform
         f = order[blockIdx.x];
     } else {
-        f = blockIdx.x - hmax;
+        // XCD-aware order (hmax is a multiple of 8, so j % 8 is the workgroup's XCD): the 128 coarse buckets of one
+        // group of fine buckets run back to back on one XCD, so the 96-B packed lines of neighbouring buckets -- which
+        // share 128-B cache lines for line % 4 in {1, 2} -- meet in that XCD's L2 and each cache line is read once
+        const uint32_t j = blockIdx.x - hmax, jj = j >> 3, sub_ = (jj / SK_PFL_NB) * 8u + (j & 7u);
+        if (sub_ >= nsub) return;
+        f = (jj % SK_PFL_NB) * nsub + sub_;
     }
     const uint32_t b = f / nsub, sub = f % nsub;
     const uint32_t slab0 = sub << sh, nsl = 1u << sh; // permuted ids slab0 + i, i < nsl
-    auto line = [&](uint32_t i) -> uint4 * {
+    // line i of the bucket: the 96 packed bytes of registers (b - rot(s)) * 128 .. + 127 of sketch s; LDS word q of the
+    // lines (16 u8 registers) <-> packed group q % LW (12 B) of line q / LW
+    auto line = [&](uint32_t i) -> uint8_t * {
         const uint32_t s = pm.inv(slab0 + i);
-        return reinterpret_cast<uint4 *>(arena + (uint64_t(s) << 14) + (((b - pfl_rot(s)) & (SK_PFL_NB - 1)) << SK_PFL_LB));
+        return slab_at(arena, s) + ((b - pfl_rot(s)) & (SK_PFL_NB - 1)) * (SK_SLAB_BYTES / SK_PFL_NB);
     };
     constexpr int LQ = (NL * LW + SK_PFL_ATPB - 1) / SK_PFL_ATPB;
-    uint4 lv[LQ];
+    uint4 lv[LQ]; // the packed group's three words (w unused) until fill_lines unpacks them
     auto load_lines = [&] {
 #pragma unroll
         for (int j = 0; j < LQ; j++) {
             const uint32_t q = threadIdx.x + j * SK_PFL_ATPB;
-            if (q < nsl * LW && pm.inv(slab0 + q / LW) < nslab)
-                lv[j] = (probe & 4) ? make_uint4(0, 0, 0, 0) : line(q / LW)[q % LW];
+            if (q < nsl * LW && pm.inv(slab0 + q / LW) < nslab) {
+                if (probe & 4) {
+                    lv[j] = make_uint4(0, 0, 0, 0);
+                } else {
+                    const uint32_t *w = reinterpret_cast<const uint32_t *>(line(q / LW)) + 3 * (q % LW);
+                    lv[j] = make_uint4(w[0], w[1], w[2], 0);
+                }
+            }
         }
     };
     uint32_t st = 0, len = 0;
@@ -1471,7 +1367,7 @@ __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const PflRec rec2,
 #pragma unroll
             for (int j = 0; j < LQ; j++) {
                 const uint32_t q = threadIdx.x + j * SK_PFL_ATPB;
-                if (q < nsl * LW && pm.inv(slab0 + q / LW) < nslab) regs4[q] = lv[j];
+                if (q < nsl * LW && pm.inv(slab0 + q / LW) < nslab) regs4[q] = unpack16(lv[j].x, lv[j].y, lv[j].z);
             }
         };
         __syncthreads();
@@ -1479,7 +1375,7 @@ __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const PflRec rec2,
         pfl_chunk(R, cnt, nxt, head, fin, reg, dirty, fill_lines, put);
     } else {
         for (uint32_t q = threadIdx.x; q < nsl * LW; q += SK_PFL_ATPB)
-            if (pm.inv(slab0 + q / LW) < nslab) regs4[q] = line(q / LW)[q % LW];
+            if (pm.inv(slab0 + q / LW) < nslab) regs4[q] = grp_load(line(q / LW), q % LW);
         __syncthreads();
         uint32_t t0 = 0;
         while (t0 < ntile) { // uniform: chunks of whole runs, in tile (= batch) order
@@ -1641,17 +1537,8 @@ __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const PflRec rec2,
         }
     }
     if (probe & 4) return;
-    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
-    for (uint32_t q = threadIdx.x; q < nsl * LW; q += SK_PFL_ATPB)
-        if ((dirty[(q / SK_PFL_DG) >> 5] >> ((q / SK_PFL_DG) & 31u)) & 1u) {
-            if (probe & 16) {
-                const uint4 x = regs4[q];
-                v4u y = {x.x, x.y, x.z, x.w};
-                __builtin_nontemporal_store(y, reinterpret_cast<v4u *>(line(q / LW) + (q % LW)));
-            } else {
-                line(q / LW)[q % LW] = regs4[q];
-            }
-        }
+    for (uint32_t q = threadIdx.x; q < nsl * LW; q += SK_PFL_ATPB) // the changed 16-register groups, packed
+        if ((dirty[(q / SK_PFL_DG) >> 5] >> ((q / SK_PFL_DG) & 31u)) & 1u) grp_store(line(q / LW), q % LW, regs4[q]);
 }
 
 // streamed-once 16-B load with the nontemporal hint (native vector type for the builtin)
@@ -1665,7 +1552,7 @@ __device__ __forceinline__ uint4 ld_nt(const uint4 *p) {
 // The 3.x estimator needs only E = sum 2^-r[j] and the zero count (hllDenseSum).  With every register <= 39 each
 // partial sum of E is exact in double (multiples of 2^-39 below 2^14), so E = S * 2^-40 with the integer
 // S = sum 2^(40 - r[j]) (< 2^55) is bit-identical to Redis's sum in any order.  One wave per key, no LDS: a lane sums
-// 256 registers (16 x 16-B loads in flight), the wave reduces with shuffles.  out[2k] = S, out[2k + 1] = zeros |
+// 256 registers (16 packed 12-B groups in flight, unpacked in registers), the wave reduces with shuffles.  out[2k] = S, out[2k + 1] = zeros |
 // (a register >= 40) << 32: the host then takes Redis's register-order sum instead (S is not used).
 // Per byte: extract, 40 - r (the 64-bit shift takes it mod 64: garbage only for r > 40, which the flag catches),
 // a 64-bit shift and add; per word the zero count and the >= 40 test (r + 24 reaches bit 6 iff r >= 40, r <= 63).
@@ -1673,15 +1560,19 @@ __global__ void __launch_bounds__(256) k_hll_sum(uint64_t n, const uint32_t *__r
                                                  const uint8_t *__restrict__ arena, uint64_t *__restrict__ out) {
     const uint32_t lane = threadIdx.x & 63u;
     for (uint64_t key = uint64_t(blockIdx.x) * 4 + (threadIdx.x >> 6); key < n; key += uint64_t(gridDim.x) * 4) {
-        const uint4 *base = reinterpret_cast<const uint4 *>(arena + (uint64_t(ids[key] & SK_SLAB_MASK) << 14));
-        uint4 v[16];
+        // the key's 1024 packed groups (12 B = 16 registers): a lane reads groups it * 64 + lane, 16 in flight
+        const uint32_t *base = reinterpret_cast<const uint32_t *>(slab_at(arena, slab_of(ids[key])));
+        uint32_t v[16][3];
 #pragma unroll
-        for (int it = 0; it < 16; it++) v[it] = ld_nt(base + it * 64 + lane);
+        for (int it = 0; it < 16; it++)
+#pragma unroll
+            for (int q = 0; q < 3; q++) v[it][q] = __builtin_nontemporal_load(base + 3 * (it * 64 + lane) + q);
         uint64_t S = 0;
         uint32_t zeros = 0, ge40 = 0;
 #pragma unroll
         for (int it = 0; it < 16; it++) {
-            const uint32_t ws[4] = {v[it].x, v[it].y, v[it].z, v[it].w};
+            const uint4 u = unpack16(v[it][0], v[it][1], v[it][2]);
+            const uint32_t ws[4] = {u.x, u.y, u.z, u.w};
 #pragma unroll
             for (int w = 0; w < 4; w++) {
                 const uint32_t x = ws[w] & 0x3f3f3f3fu;
@@ -1713,6 +1604,9 @@ __global__ void __launch_bounds__(256) k_hll_sum(uint64_t n, const uint32_t *__r
 // land after this key's reads.  The next key's 16 KiB loads while the table is summed (a second key in registers,
 // loading while this one is counted, measured the same).  10 waves per CU (the LDS): 48 % of wave cycles parked,
 // LDS array 39 % busy, VALU 27 % (profiles/r03j_hist_sq_summary.json).
+// PK: slabs ids[k] of the packed arena; else u8 register arrays (ids[k] = 0 with the array as `arena`: a union's
+// temporary registers, sk_hll_count_registers_dev)
+template <bool PK>
 __global__ void __launch_bounds__(64) k_hll_hist(uint64_t n, const uint32_t *__restrict__ ids,
                                                    const uint8_t *__restrict__ arena, uint32_t *__restrict__ hist) {
     __shared__ uint4 h4[64 * 16];
@@ -1720,17 +1614,30 @@ __global__ void __launch_bounds__(64) k_hll_hist(uint64_t n, const uint32_t *__r
     const uint32_t lane = threadIdx.x;
 #pragma unroll
     for (int j = 0; j < 16; j++) h4[lane + 64 * j] = make_uint4(0, 0, 0, 0);
-    auto load = [&](uint64_t key, uint4 (&v)[16]) {
-        const uint4 *base = reinterpret_cast<const uint4 *>(arena + (uint64_t(ids[key] & SK_SLAB_MASK) << 14));
+    // a lane's 16 groups of 16 registers: groups it * 64 + lane (packed: three words each; u8: one 16-B vector)
+    auto load = [&](uint64_t key, uint32_t (&v)[16][4]) {
+        if constexpr (PK) {
+            const uint32_t *base = reinterpret_cast<const uint32_t *>(slab_at(arena, slab_of(ids[key])));
 #pragma unroll
-        for (int it = 0; it < 16; it++) v[it] = ld_nt(base + it * 64 + lane);
+            for (int it = 0; it < 16; it++)
+#pragma unroll
+                for (int q = 0; q < 3; q++) v[it][q] = __builtin_nontemporal_load(base + 3 * (it * 64 + lane) + q);
+        } else {
+            const uint4 *base = reinterpret_cast<const uint4 *>(arena + (uint64_t(ids[key] & SK_SLAB_MASK) << 14));
+#pragma unroll
+            for (int it = 0; it < 16; it++) {
+                const uint4 x = ld_nt(base + it * 64 + lane);
+                v[it][0] = x.x, v[it][1] = x.y, v[it][2] = x.z, v[it][3] = x.w;
+            }
+        }
     };
-    auto count = [&](uint64_t key, const uint4 (&v)[16]) {
+    auto count = [&](uint64_t key, const uint32_t (&v)[16][4]) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
 #pragma unroll
         for (int it = 0; it < 16; it++) {
-            const uint32_t ws[4] = {v[it].x, v[it].y, v[it].z, v[it].w};
+            const uint4 u = PK ? unpack16(v[it][0], v[it][1], v[it][2]) : make_uint4(v[it][0], v[it][1], v[it][2], v[it][3]);
+            const uint32_t ws[4] = {u.x, u.y, u.z, u.w};
 #pragma unroll
             for (int w = 0; w < 4; w++)
 #pragma unroll
@@ -1751,7 +1658,7 @@ __global__ void __launch_bounds__(64) k_hll_hist(uint64_t n, const uint32_t *__r
         hist[key * 64 + lane] = c;
     };
     const uint64_t G = gridDim.x;
-    uint4 v[16];
+    uint32_t v[16][4];
     uint64_t key = blockIdx.x;
     if (key < n) load(key, v);
     for (; key < n; key += G) {
@@ -1774,90 +1681,74 @@ __device__ __forceinline__ uint4 bytemax4(uint4 a, uint4 b) {
     return make_uint4(bytemax(a.x, b.x), bytemax(a.y, b.y), bytemax(a.z, b.z), bytemax(a.w, b.w));
 }
 
-// grid (4, G): block (x, g) covers 4096 registers (256 lanes x 16 B) of the
-// union of sources [g*per, (g+1)*per) and writes partial[g].  Sources are
-// slabs ids[k] of `base`, or (ids == null) consecutive 16 KiB arrays -- the
-// form the next tree level reads.
+// grid (4, G): block (x, g) covers 4096 registers (256 lanes x 16 registers) of the union of sources
+// [g*per, (g+1)*per) and writes partial[g] as u8 registers.  Sources are slabs ids[k] of the packed arena (PK: 12-B
+// groups, unpacked in registers), or consecutive u8 register arrays of 16 KiB (ids == null: the form the next tree
+// level reads; or one caller array, sk_hll_merge_registers_dev).
+template <bool PK>
 __global__ void __launch_bounds__(256) k_hll_union_partial(uint64_t n, const uint32_t *__restrict__ ids,
                                                            const uint8_t *__restrict__ base, uint64_t per,
                                                            uint8_t *__restrict__ partial) {
-    unsigned lane16 = blockIdx.x * 256 + threadIdx.x; // uint4 index within 16 KiB
+    unsigned lane16 = blockIdx.x * 256 + threadIdx.x; // group of 16 registers within the key
     uint64_t g = blockIdx.y, k0 = g * per, k1 = k0 + per;
     if (k1 > n) k1 = n;
     uint4 acc = make_uint4(0, 0, 0, 0);
     uint64_t k = k0;
     // the next step's slab ids are loaded while this step's 8 vectors are in flight (the id loads used to sit in
     // front of every step's vector loads)
-    auto idof = [&](uint64_t kk) -> uint64_t { return ids ? uint64_t(ids[kk] & SK_SLAB_MASK) : kk; };
-    auto src = [&](uint64_t id) { return reinterpret_cast<const uint4 *>(base + (id << 14)) + lane16; };
+    auto idof = [&](uint64_t kk) -> uint64_t { return ids ? slab_of(ids[kk]) : kk; };
+    auto ld = [&](uint64_t id) -> uint4 {
+        if constexpr (PK) return grp_load_nt(slab_at(base, id), lane16);
+        else return ld_nt(reinterpret_cast<const uint4 *>(base + (id << 14)) + lane16);
+    };
     uint64_t idn[8];
     if (k + 8 <= k1)
 #pragma unroll
         for (int j = 0; j < 8; j++) idn[j] = idof(k + j);
-    for (; k + 8 <= k1; k += 8) { // 8 independent 16 B loads in flight per lane
+    for (; k + 8 <= k1; k += 8) { // 8 independent loads in flight per lane
         uint4 a[8];
 #pragma unroll
-        for (int j = 0; j < 8; j++) a[j] = ld_nt(src(idn[j]));
+        for (int j = 0; j < 8; j++) a[j] = ld(idn[j]);
         if (k + 16 <= k1)
 #pragma unroll
             for (int j = 0; j < 8; j++) idn[j] = idof(k + 8 + j);
         acc = bytemax4(acc, bytemax4(bytemax4(bytemax4(a[0], a[1]), bytemax4(a[2], a[3])),
                                      bytemax4(bytemax4(a[4], a[5]), bytemax4(a[6], a[7]))));
     }
-    for (; k < k1; k++) acc = bytemax4(acc, *src(idof(k)));
+    for (; k < k1; k++) acc = bytemax4(acc, ld(idof(k)));
     reinterpret_cast<uint4 *>(partial + g * 16384)[lane16] = acc;
 }
 
-// out = max(include_out ? out : 0, partial[0..G)) for a small G (the tree root)
+// out = max(include_out ? out : 0, partial[0..G)) for a small G (the tree root); PKOUT: out is a packed slab (the
+// PFMERGE destination), else u8 registers
+template <bool PKOUT>
 __global__ void __launch_bounds__(256) k_hll_union_final(uint64_t G, const uint8_t *__restrict__ partial,
                                                          uint8_t *__restrict__ out, int include_out) {
     unsigned lane16 = blockIdx.x * 256 + threadIdx.x;
-    uint4 acc = include_out ? reinterpret_cast<const uint4 *>(out)[lane16] : make_uint4(0, 0, 0, 0);
+    uint4 acc = make_uint4(0, 0, 0, 0);
+    if (include_out) acc = PKOUT ? grp_load(out, lane16) : reinterpret_cast<const uint4 *>(out)[lane16];
     for (uint64_t g = 0; g < G; g++) acc = bytemax4(acc, reinterpret_cast<const uint4 *>(partial + g * 16384)[lane16]);
-    reinterpret_cast<uint4 *>(out)[lane16] = acc;
+    if (PKOUT) grp_store(out, lane16, acc);
+    else reinterpret_cast<uint4 *>(out)[lane16] = acc;
 }
 
-// ------------------------------------------------------------------ Redis dense HLL strings, in bulk
-// The dense encoding (HLL_DENSE_SET_REGISTER): register i in bits [6i, 6i + 6) of the 12,288-B body, LSB first, so
-// 16 registers are exactly 12 bytes.  One thread packs / unpacks one such group: a 16-B vector of u8 registers in,
-// three u32 words out (and back).  SAVE / DUMP of many HLLs and the bulk restore of a snapshot (sk_rdb.h) move the
-// dense bodies through these; a thread's group never straddles a key (1024 groups per key).
-__device__ __forceinline__ void pack16(uint4 r, uint32_t *w) {
-    const uint32_t b0 = r.x, b1 = r.y, b2 = r.z, b3 = r.w;
-    auto g = [](uint32_t v, int i) { return (v >> (8 * i)) & 63u; };
-    w[0] = g(b0, 0) | g(b0, 1) << 6 | g(b0, 2) << 12 | g(b0, 3) << 18 | g(b1, 0) << 24 | (g(b1, 1) & 3u) << 30;
-    w[1] = g(b1, 1) >> 2 | g(b1, 2) << 4 | g(b1, 3) << 10 | g(b2, 0) << 16 | g(b2, 1) << 22 | (g(b2, 2) & 15u) << 28;
-    w[2] = g(b2, 2) >> 4 | g(b2, 3) << 2 | g(b3, 0) << 8 | g(b3, 1) << 14 | g(b3, 2) << 20 | g(b3, 3) << 26;
-}
-__device__ __forceinline__ uint4 unpack16(uint32_t w0, uint32_t w1, uint32_t w2) {
-    auto q = [](uint32_t a, uint32_t b, uint32_t c, uint32_t d) { return a | b << 8 | c << 16 | d << 24; };
-    const uint32_t r0 = w0 & 63u, r1 = (w0 >> 6) & 63u, r2 = (w0 >> 12) & 63u, r3 = (w0 >> 18) & 63u;
-    const uint32_t r4 = (w0 >> 24) & 63u, r5 = (w0 >> 30) | ((w1 & 15u) << 2), r6 = (w1 >> 4) & 63u;
-    const uint32_t r7 = (w1 >> 10) & 63u, r8 = (w1 >> 16) & 63u, r9 = (w1 >> 22) & 63u;
-    const uint32_t r10 = (w1 >> 28) | ((w2 & 3u) << 4), r11 = (w2 >> 2) & 63u, r12 = (w2 >> 8) & 63u;
-    const uint32_t r13 = (w2 >> 14) & 63u, r14 = (w2 >> 20) & 63u, r15 = w2 >> 26;
-    return make_uint4(q(r0, r1, r2, r3), q(r4, r5, r6, r7), q(r8, r9, r10, r11), q(r12, r13, r14, r15));
-}
+// The arena holds Redis's dense bodies, so SAVE / DUMP of many HLLs and the bulk restore of a snapshot (sk_rdb.h) are
+// gathers / scatters of 12,288-B bodies: 768 16-B vectors per key, one per thread.
 // out[i * 12288 ..) = the dense body of slab ids[i] (generation bits masked off)
 __global__ void __launch_bounds__(256) k_hll_pack(uint64_t n, const uint32_t *__restrict__ ids,
                                                   const uint8_t *__restrict__ arena, uint32_t *__restrict__ out) {
-    const uint64_t t = uint64_t(blockIdx.x) * 256 + threadIdx.x, key = t >> 10, grp = t & 1023;
+    const uint64_t t = uint64_t(blockIdx.x) * 256 + threadIdx.x, key = t / 768, v = t % 768;
     if (key >= n) return;
-    const uint4 r = reinterpret_cast<const uint4 *>(arena + uint64_t(ids[key] & 0xffffffu) * 16384)[grp];
-    uint32_t w[3];
-    pack16(r, w);
-    uint32_t *o = out + key * 3072 + grp * 3;
-    o[0] = w[0];
-    o[1] = w[1];
-    o[2] = w[2];
+    reinterpret_cast<uint4 *>(out)[key * 768 + v] =
+        reinterpret_cast<const uint4 *>(slab_at(arena, slab_of(ids[key])))[v];
 }
-// slab ids[i] = the registers of the dense body in[i * 12288 ..)
+// slab ids[i] = the dense body in[i * 12288 ..)
 __global__ void __launch_bounds__(256) k_hll_unpack(uint64_t n, const uint32_t *__restrict__ ids,
                                                     const uint32_t *__restrict__ in, uint8_t *__restrict__ arena) {
-    const uint64_t t = uint64_t(blockIdx.x) * 256 + threadIdx.x, key = t >> 10, grp = t & 1023;
+    const uint64_t t = uint64_t(blockIdx.x) * 256 + threadIdx.x, key = t / 768, v = t % 768;
     if (key >= n) return;
-    const uint32_t *w = in + key * 3072 + grp * 3;
-    reinterpret_cast<uint4 *>(arena + uint64_t(ids[key] & 0xffffffu) * 16384)[grp] = unpack16(w[0], w[1], w[2]);
+    reinterpret_cast<uint4 *>(slab_at(arena, slab_of(ids[key])))[v] =
+        reinterpret_cast<const uint4 *>(in)[key * 768 + v];
 }
 
 // ------------------------------------------------------------------ Bloom
@@ -2091,6 +1982,11 @@ __global__ void __launch_bounds__(256) k_bloom_contains_q(uint64_t n, const uint
 // of the hash: 16384 no per-round barrier
 #define SK_RC_ABL 0
 #endif
+#ifndef SK_RC_LATERANK
+// contains hash: 1 = the hashing rounds only count each probe's region (return-less LDS adds), and the records take
+// their places with returning adds on the region cursors after the scan (the ranks leave the rounds' critical path)
+#define SK_RC_LATERANK 0
+#endif
 #ifndef SK_RC_STILE
 // The hash blocks write their segment entries interleaved by SK_RC_STILE regions, St[(r / T * NB + block) * T + r % T]:
 // a block's entries for T consecutive regions are one 128-B line (coalesced stores; a region-major row per region
@@ -2254,8 +2150,12 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_rc_hash(uint64_t n, const uint
                 if (uint32_t(p) >= P) break;
                 uint32_t idx = uint32_t(bi.r);
                 ix[e][p] = idx;
-                uint32_t rank = atomicAdd(&hist[idx >> RB], 1u);
-                rk[e][p >> 1] |= rank << ((p & 1) * 16);
+                if (!ADD && SK_RC_LATERANK) { // a count only (a return-less LDS add): ranks come at placement
+                    atomicAdd(&hist[idx >> RB], 1u);
+                } else {
+                    uint32_t rank = atomicAdd(&hist[idx >> RB], 1u);
+                    rk[e][p >> 1] |= rank << ((p & 1) * 16);
+                }
                 bi.next(p);
             }
         }
@@ -2296,6 +2196,10 @@ __global__ void __launch_bounds__(RC_TPB) k_bloom_rc_hash(uint64_t n, const uint
             if (uint32_t(p) >= P) break;
             uint32_t idx = ix[e][p], rank = (rk[e][p >> 1] >> ((p & 1) * 16)) & 0xffffu;
             const uint32_t el = uint32_t(e) * RC_TPB + threadIdx.x;
+            if (!ADD && SK_RC_LATERANK) { // contains: a segment's order is free (the probe ANDs)
+                lrec[atomicAdd(&hist[idx >> RB], 1u)] = (idx << 12) | el;
+                continue;
+            }
             lrec[hist[idx >> RB] + rank] =
                 ADD ? (idx << 13) | (el << 1) | (uint32_t(p) + 1 == P ? 1u : 0u) : (idx << 12) | el;
         }
@@ -4266,68 +4170,7 @@ __global__ void __launch_bounds__(256) k_unroute(uint64_t n, const uint32_t *__r
         if (e__ != hipSuccess) return e__;                                                                             \
     } while (0)
 
-hipError_t launch_pfadd_hash(hipStream_t st, uint64_t n, const uint32_t *key_ids, const uint64_t *off,
-                             const uint8_t *bytes, const uint32_t *cmd_of, int v5, unsigned slot_shift,
-                             uint64_t *out_keys) {
-    if (!n) return hipSuccess;
-    hipLaunchKernelGGL(k_pfadd_hash, dim3(grid_for(n, 256)), dim3(256), 0, st, n, key_ids, off, bytes, cmd_of, v5,
-                       slot_shift, out_keys);
-    SK_LAUNCH_CHECK();
-    return hipSuccess;
-}
 
-hipError_t launch_pfadd_apply(hipStream_t st, uint64_t n, const uint64_t *keys, unsigned slot_shift, uint64_t cmd_mask,
-                              uint8_t *arena, uint8_t *changed) {
-    if (!n) return hipSuccess;
-    hipLaunchKernelGGL(k_pfadd_apply, dim3(grid_for(n, 256)), dim3(256), 0, st, n, keys, slot_shift, cmd_mask, arena,
-                       changed);
-    SK_LAUNCH_CHECK();
-    return hipSuccess;
-}
-
-
-hipError_t launch_pfadd_claim(hipStream_t st, uint64_t n, const uint32_t *key_ids, const uint64_t *off,
-                              const uint8_t *bytes, int v5, uint8_t *arena, uint64_t *rec, uint8_t *changed_i,
-                              uint32_t *conf_count, int claim_all) {
-    if (!n) return hipSuccess;
-    if (claim_all)
-        hipLaunchKernelGGL(k_pfadd_claim<true>, dim3(grid_for(n, 256)), dim3(256), 0, st, n, key_ids, off, bytes, v5,
-                           arena, rec, changed_i, conf_count);
-    else
-        hipLaunchKernelGGL(k_pfadd_claim<false>, dim3(grid_for(n, 256)), dim3(256), 0, st, n, key_ids, off, bytes, v5,
-                           arena, rec, changed_i, conf_count);
-    SK_LAUNCH_CHECK();
-    return hipSuccess;
-}
-
-hipError_t launch_pfadd_commit(hipStream_t st, uint64_t n, const uint64_t *rec, const uint32_t *cmd_of, uint8_t *arena,
-                               uint8_t *changed, uint64_t *conf_keys, uint64_t *conf_vals, uint32_t *conf_count,
-                               uint32_t conf_cap) {
-    if (!n) return hipSuccess;
-    hipLaunchKernelGGL(k_pfadd_commit, dim3(grid_for(n, 256)), dim3(256), 0, st, n, rec, cmd_of, arena, changed,
-                       conf_keys, conf_vals, conf_count, conf_cap);
-    SK_LAUNCH_CHECK();
-    return hipSuccess;
-}
-
-hipError_t launch_pfadd_conflicts(hipStream_t st, const uint64_t *conf_keys, const uint64_t *conf_vals,
-                                  const uint32_t *conf_count, uint8_t *arena, uint8_t *changed, uint32_t *host_count) {
-    hipLaunchKernelGGL(k_pfadd_conflicts, dim3(1), dim3(SK_CONF_TPB), 0, st, conf_keys, conf_vals, conf_count, arena,
-                       changed, host_count);
-    SK_LAUNCH_CHECK();
-    return hipSuccess;
-}
-
-hipError_t launch_pfadd_conflicts_sorted(hipStream_t st, uint64_t cnt, const uint64_t *K, const uint64_t *V,
-                                         uint8_t *arena, uint8_t *changed) {
-    if (!cnt) return hipSuccess;
-    hipLaunchKernelGGL(k_pfadd_conflicts_sorted, dim3(grid_for(cnt, 256)), dim3(256), 0, st, cnt, K, V, arena,
-                       changed);
-    SK_LAUNCH_CHECK();
-    return hipSuccess;
-}
-
-uint32_t pfadd_conflict_lds_capacity() { return SK_CONF_MAX; }
 
 
 uint64_t long_elem_bytes() { return SK_LONG_ELEM; }
@@ -4482,10 +4325,11 @@ hipError_t launch_pfl_apply(hipStream_t st, const PflDims &d, const uint64_t *re
                            uint32_t(d.nf), hmax, big_alloc + 1, order);
         SK_LAUNCH_CHECK();
     }
-    hipLaunchKernelGGL(k_pfl_apply, dim3(uint32_t(d.nf) + hmax), dim3(SK_PFL_ATPB), 0, st,
+    const uint32_t hmax8 = (hmax + 7u) & ~7u, nsubx = uint32_t((d.nsub + 7) / 8 * 8); // see k_pfl_apply's XCD order
+    hipLaunchKernelGGL(k_pfl_apply, dim3(uint32_t(SK_PFL_NB) * nsubx + hmax8), dim3(SK_PFL_ATPB), 0, st,
                        PflRec{const_cast<uint64_t *>(rec2), uint64_t(d.nblk) * SK_PFP_EPB}, rbase, C2, d.ntile,
                        d.nsub, d.sh, PflPerm{d.pa, d.pai, d.pm_mask, d.nslab}, nslab, arena, changed, big_alloc,
-                       big_keys, big_vals, flags | probe_flags, hmax, big_alloc + 1, order, rc, par);
+                       big_keys, big_vals, flags | probe_flags, hmax8, big_alloc + 1, order, rc, par);
     SK_LAUNCH_CHECK();
     return hipSuccess;
 }
@@ -4545,7 +4389,7 @@ hipError_t launch_hll_sum(hipStream_t st, uint64_t n, const uint32_t *ids, const
 
 hipError_t launch_hll_pack(hipStream_t st, uint64_t n, const uint32_t *ids, const uint8_t *arena, uint8_t *out) {
     if (!n) return hipSuccess;
-    hipLaunchKernelGGL(k_hll_pack, dim3(uint32_t(n * 4)), dim3(256), 0, st, n, ids, arena,
+    hipLaunchKernelGGL(k_hll_pack, dim3(uint32_t(n * 3)), dim3(256), 0, st, n, ids, arena,
                        reinterpret_cast<uint32_t *>(out));
     SK_LAUNCH_CHECK();
     return hipSuccess;
@@ -4553,15 +4397,19 @@ hipError_t launch_hll_pack(hipStream_t st, uint64_t n, const uint32_t *ids, cons
 
 hipError_t launch_hll_unpack(hipStream_t st, uint64_t n, const uint32_t *ids, const uint8_t *in, uint8_t *arena) {
     if (!n) return hipSuccess;
-    hipLaunchKernelGGL(k_hll_unpack, dim3(uint32_t(n * 4)), dim3(256), 0, st, n, ids,
+    hipLaunchKernelGGL(k_hll_unpack, dim3(uint32_t(n * 3)), dim3(256), 0, st, n, ids,
                        reinterpret_cast<const uint32_t *>(in), arena);
     SK_LAUNCH_CHECK();
     return hipSuccess;
 }
 
-hipError_t launch_hll_hist(hipStream_t st, uint64_t n, const uint32_t *ids, const uint8_t *arena, uint32_t *hist) {
+hipError_t launch_hll_hist(hipStream_t st, uint64_t n, const uint32_t *ids, const uint8_t *arena, uint32_t *hist,
+                           int packed) {
     if (!n) return hipSuccess;
-    hipLaunchKernelGGL(k_hll_hist, dim3(grid_for(n, 1, 8192)), dim3(64), 0, st, n, ids, arena, hist);
+    if (packed)
+        hipLaunchKernelGGL(k_hll_hist<true>, dim3(grid_for(n, 1, 8192)), dim3(64), 0, st, n, ids, arena, hist);
+    else
+        hipLaunchKernelGGL(k_hll_hist<false>, dim3(grid_for(n, 1, 8192)), dim3(64), 0, st, n, ids, arena, hist);
     SK_LAUNCH_CHECK();
     return hipSuccess;
 }
@@ -4570,37 +4418,47 @@ hipError_t launch_hll_hist(hipStream_t st, uint64_t n, const uint32_t *ids, cons
 // (>= 64 sources per workgroup column), each further level reduces 64:1 until
 // <= 64 remain, and the root folds them (and `out` when include_out) into out.
 // `partial` holds max_groups + max_groups/64 + 1 arrays of 16 KiB.
-hipError_t launch_hll_union(hipStream_t st, uint64_t n, const uint32_t *ids, const uint8_t *arena, uint8_t *partial,
-                            uint64_t max_groups, uint8_t *out, int include_out) {
+hipError_t launch_hll_union(hipStream_t st, uint64_t n, const uint32_t *ids, const uint8_t *src, uint8_t *partial,
+                            uint64_t max_groups, uint8_t *out, int include_out, int src_packed, int out_packed) {
     if (!n) {
-        if (!include_out) return hipMemsetAsync(out, 0, 16384, st);
+        if (!include_out) return hipMemsetAsync(out, 0, out_packed ? SK_SLAB_BYTES : 16384u, st);
         return hipSuccess;
     }
     const uint32_t *cur_ids = ids;
-    const uint8_t *cur = arena;
+    const uint8_t *cur = src;
     uint64_t cur_n = n;
+    bool pk = src_packed != 0;
     uint8_t *bufs[2] = {partial, partial + max_groups * 16384};
     int which = 0;
+    auto partial_pass = [&](uint64_t per, uint64_t G) {
+        if (pk)
+            hipLaunchKernelGGL(k_hll_union_partial<true>, dim3(4, unsigned(G)), dim3(256), 0, st, cur_n, cur_ids, cur,
+                               per, bufs[which]);
+        else
+            hipLaunchKernelGGL(k_hll_union_partial<false>, dim3(4, unsigned(G)), dim3(256), 0, st, cur_n, cur_ids, cur,
+                               per, bufs[which]);
+        cur = bufs[which];
+        cur_ids = nullptr;
+        pk = false; // the partials are u8
+        which ^= 1;
+    };
     while (cur_n > 64) {
         uint64_t per = (cur_n + max_groups - 1) / max_groups;
         if (per < 64) per = 64;
         uint64_t G = (cur_n + per - 1) / per;
-        hipLaunchKernelGGL(k_hll_union_partial, dim3(4, unsigned(G)), dim3(256), 0, st, cur_n, cur_ids, cur, per,
-                           bufs[which]);
+        partial_pass(per, G);
         SK_LAUNCH_CHECK();
-        cur = bufs[which];
-        cur_ids = nullptr;
         cur_n = G;
-        which ^= 1;
     }
-    if (cur_ids) { // n <= 64 slabs: one partial, then the root
-        hipLaunchKernelGGL(k_hll_union_partial, dim3(4, 1), dim3(256), 0, st, cur_n, cur_ids, cur, cur_n,
-                           bufs[which]);
+    if (cur_ids || pk) { // n <= 64 sources not yet in u8 partial form: one partial, then the root
+        partial_pass(cur_n, 1);
         SK_LAUNCH_CHECK();
-        cur = bufs[which];
         cur_n = 1;
     }
-    hipLaunchKernelGGL(k_hll_union_final, dim3(4), dim3(256), 0, st, cur_n, cur, out, include_out);
+    if (out_packed)
+        hipLaunchKernelGGL(k_hll_union_final<true>, dim3(4), dim3(256), 0, st, cur_n, cur, out, include_out);
+    else
+        hipLaunchKernelGGL(k_hll_union_final<false>, dim3(4), dim3(256), 0, st, cur_n, cur, out, include_out);
     SK_LAUNCH_CHECK();
     return hipSuccess;
 }

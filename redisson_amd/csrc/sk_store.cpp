@@ -153,7 +153,8 @@ void host_for(uint64_t n, uint64_t min_per_thread, const std::function<void(uint
     p.run(T, [&](unsigned t) { fn(n * t / T, n * (t + 1) / T); });
 }
 
-constexpr uint64_t kHllBytes = 16384;
+constexpr uint64_t kHllBytes = 16384;   // registers per HLL: the u8 register arrays (host side, union buffers)
+constexpr uint64_t kSlabBytes = 12288;  // a slab of the HBM arena: Redis's dense register body (SK_SLAB_BYTES)
 constexpr int64_t kBloomMaxSize = 2LL * 2147483647LL; // M:RedissonBloomFilter.java:52
 constexpr uint32_t kNoId = 0xffffffffu;
 
@@ -369,11 +370,10 @@ struct sk_ctx {
     uint32_t stage_bufs = 4;    // pinned buffers in the ring (SK_STAGE_BUFS, <= 8)
 
     bool async_dev = false;     // sk_set_async: _dev calls return without a final sync
-    int pfadd_path = 1;         // 0 claim/commit, 1 partition, 2 sorted (SK_PFADD_PATH); dense batches use 2
+    int pfadd_path = 1;         // 1: the partition path + line schedule (the only one since round 6)
     bool pfp_direct = true;     // partition path, one element per command: apply writes replies (SK_PFP_DIRECT)
     uint64_t sbv_min = 1u << 20; // SETBIT_VOID batches from which a dense one takes the region path (SK_SBV_MIN)
     bool sbv_part = true;       // ... through the hand-written partition (SK_SBV_PART=0: the rocPRIM radix sort)
-    int claim_all = 1;          // PFADD claim: 1 = every element claims (R0 from the atomic), 0 = load first, claim candidates (SK_PFADD_CLAIM)
     int read_stream = 1;        // async Bloom contains on the read stream st2 (SK_READ_STREAM=0: main stream)
     int bloom_sched = 0;        // contains kernel (SK_BLOOM_SCHED): 0 one element per thread; 1 probe queue, 4/lane; 3 split hash / probe passes
     // async PFADD: the conflict count of the last sparse batch is checked ("settled")
@@ -547,11 +547,12 @@ int hll_grow(sk_ctx *c, uint64_t need) {
     if (need <= c->hll_cap) return SK_OK;
     uint64_t nc = std::max<uint64_t>(need, c->hll_cap * 2);
     uint8_t *na = nullptr;
-    if (hipMalloc(&na, nc * kHllBytes) != hipSuccess)
+    // + 16 B: a register read takes the byte after its field (the last slab's last register included)
+    if (hipMalloc(&na, nc * kSlabBytes + 16) != hipSuccess)
         return fail(c, SK_ENOMEM, "cannot allocate %llu HLL slabs", (unsigned long long)nc);
-    HIPCHK(c, hipMemsetAsync(na + c->hll_cap * kHllBytes, 0, (nc - c->hll_cap) * kHllBytes, c->st));
+    HIPCHK(c, hipMemsetAsync(na + c->hll_cap * kSlabBytes, 0, (nc - c->hll_cap) * kSlabBytes + 16, c->st));
     if (c->arena) {
-        HIPCHK(c, hipMemcpyAsync(na, c->arena, c->hll_cap * kHllBytes, hipMemcpyDeviceToDevice, c->st));
+        HIPCHK(c, hipMemcpyAsync(na, c->arena, c->hll_cap * kSlabBytes, hipMemcpyDeviceToDevice, c->st));
         HIPCHK(c, hipStreamSynchronize(c->st));
         HIPCHK(c, hipFree(c->arena));
     }
@@ -715,7 +716,9 @@ int hll_adopt_string(sk_ctx *c, const std::string &k, KeyEnt &e, uint32_t *id) {
         if (h.sparse) h.ops.assign(s.begin() + 16, s.end());
         else std::vector<uint8_t>().swap(h.ops);
     }
-    HIPCHK(c, hipMemcpyAsync(c->arena + uint64_t(hid) * kHllBytes, regs.data(), kHllBytes, hipMemcpyHostToDevice,
+    std::vector<uint8_t> body(kSlabBytes);
+    hll_body_pack(regs.data(), body.data());
+    HIPCHK(c, hipMemcpyAsync(c->arena + uint64_t(hid) * kSlabBytes, body.data(), kSlabBytes, hipMemcpyHostToDevice,
                              c->st));
     if ((r = sync(c))) return r;
     if ((r = str_free(c, e.id))) return r;
@@ -855,7 +858,7 @@ int del_key(sk_ctx *c, const std::string &k, bool *removed) {
     c->keys.erase(it);
     *removed = true;
     if (e.type == SK_TYPE_HLL) {
-        HIPCHK(c, hipMemsetAsync(c->arena + uint64_t(e.id) * kHllBytes, 0, kHllBytes, c->st));
+        HIPCHK(c, hipMemsetAsync(c->arena + uint64_t(e.id) * kSlabBytes, 0, kSlabBytes, c->st));
         c->hll_live[e.id] = 0;
         c->hll_epoch++;
         c->hll_gen[e.id] = uint8_t(c->hll_gen[e.id] + 1);
@@ -868,84 +871,13 @@ int del_key(sk_ctx *c, const std::string &k, bool *removed) {
 }
 
 // ------------------------------------------------------------ PFADD core
-// Device batch: n elements with per-element slab id and command index.
-// Two exact paths (same replies, same registers):
-//  * sparse (few elements per touched sketch, C2): claim / commit on the
-//    spare register bits, conflicts replayed in batch order (sk_kernels.hip);
-//  * dense (many elements per sketch, C1): hash -> stable radix sort on
-//    (slab, register) -> segment heads walk in batch order.
-int pfadd_sorted(sk_ctx *c, uint64_t n, const uint32_t *d_ids, const uint64_t *d_off, const uint8_t *d_bytes,
-                 const uint32_t *d_cmd, uint64_t n_cmds, uint8_t *d_changed) {
-    unsigned id_bits = bits_for(c->hll_next ? c->hll_next - 1 : 0);
-    unsigned cmd_bits = bits_for(n_cmds ? n_cmds - 1 : 0);
-    if (6 + cmd_bits + 14 + id_bits > 64) return fail(c, SK_EINVAL, "PFADD batch too large for key packing");
-    unsigned slot_shift = 6 + cmd_bits;
-    uint64_t cmd_mask = (cmd_bits >= 64) ? ~0ull : ((1ull << cmd_bits) - 1);
-    HIPCHK(c, c->keys_a.ensure(n * 8));
-    HIPCHK(c, c->keys_b.ensure(n * 8));
-    size_t tmp = 0;
-    HIPCHK(c, sk::sort_keys_size(n, slot_shift, slot_shift + 14 + id_bits, &tmp));
-    HIPCHK(c, c->sort_tmp.ensure(tmp));
-    { Prof p_(c, 0);
-    HIPCHK(c, sk::launch_pfadd_hash(c->st, n, d_ids, d_off, d_bytes, d_cmd, c->redis_major >= 5, slot_shift,
-                                    c->keys_a.as<uint64_t>())); }
-    { Prof p_(c, 1);
-    HIPCHK(c, sk::sort_keys(c->st, c->sort_tmp.p, c->sort_tmp.cap, c->keys_a.as<uint64_t>(), c->keys_b.as<uint64_t>(),
-                            n, slot_shift, slot_shift + 14 + id_bits)); }
-    { Prof p_(c, 2);
-    HIPCHK(c, sk::launch_pfadd_apply(c->st, n, c->keys_b.as<uint64_t>(), slot_shift, cmd_mask, c->arena, d_changed)); }
-    return SK_OK;
-}
-
-int pfadd_sparse(sk_ctx *c, uint64_t n, const uint32_t *d_ids, const uint64_t *d_off, const uint8_t *d_bytes,
-                 const uint32_t *d_cmd, uint8_t *d_changed) {
-    if (n >= (1ull << 26) || c->hll_next >= (1ull << 24)) return fail(c, SK_EINVAL, "PFADD batch too large");
-    HIPCHK(c, c->keys_a.ensure(n * 8)); // claim records
-    HIPCHK(c, c->keys_b.ensure(n * 8)); // conflict keys
-    HIPCHK(c, c->vals_a.ensure(n * 8)); // conflict values (cmd, R0, rho)
-    uint32_t *d_cnt = reinterpret_cast<uint32_t *>(c->misc.as<uint8_t>() + 256);
-    { Prof p_(c, 13);
-    // one element per command (d_cmd == null): the claim pass also zeroes the replies
-    HIPCHK(c, sk::launch_pfadd_claim(c->st, n, d_ids, d_off, d_bytes, c->redis_major >= 5, c->arena,
-                                     c->keys_a.as<uint64_t>(), d_cmd ? nullptr : d_changed, d_cnt, c->claim_all)); }
-    { Prof p_(c, 14);
-    HIPCHK(c, sk::launch_pfadd_commit(c->st, n, c->keys_a.as<uint64_t>(), d_cmd, c->arena, d_changed,
-                                      c->keys_b.as<uint64_t>(), c->vals_a.as<uint64_t>(), d_cnt, uint32_t(n)));
-    HIPCHK(c, sk::launch_pfadd_conflicts(c->st, c->keys_b.as<uint64_t>(), c->vals_a.as<uint64_t>(), d_cnt, c->arena,
-                                         d_changed, c->d_h_cnt)); }
-    c->pf_pending = true;
-    c->pf_changed = d_changed;
-    if (c->async_dev) return SK_OK; // settled by the next call that needs the HLL arena
-    return pfadd_settle(c);
-}
-
-// the conflict count of the last sparse batch decides whether the long-list path is needed
-
-int pfadd_settle(sk_ctx *c) {
+// Device batch: n elements with per-element slab id and command index.  Two schedules, same replies and registers:
+// the partition path (k_pfp_hash / k_pfp_apply, <= 1 M elements per launch, any density) and, for a large group of
+// one-element commands, the line schedule (k_pfl_*).  (Rounds 1-5 also kept a claim / commit path on the registers'
+// spare bits and a radix-sorted path; the packed 6-bit arena has no spare bits, and both were retired in round 6.)
+int pfadd_settle(sk_ctx *c) { // nothing is left pending by the current paths
     c->pf_pending = false;
-    HIPCHK(c, hipStreamSynchronize(c->st));
-    uint32_t cnt = *c->h_cnt;
-    if (cnt > sk::pfadd_conflict_lds_capacity()) { // long conflict list: rocPRIM sort + replay
-        HIPCHK(c, c->vals_b.ensure(uint64_t(cnt) * 8));
-        size_t tmp;
-        HIPCHK(c, sk::sort_pairs64_size(cnt, &tmp));
-        HIPCHK(c, c->sort_tmp.ensure(tmp));
-        HIPCHK(c, sk::sort_pairs64(c->st, c->sort_tmp.p, c->sort_tmp.cap, c->keys_b.as<uint64_t>(),
-                                   c->keys_a.as<uint64_t>(), c->vals_a.as<uint64_t>(), c->vals_b.as<uint64_t>(), cnt));
-        HIPCHK(c, sk::launch_pfadd_conflicts_sorted(c->st, cnt, c->keys_a.as<uint64_t>(), c->vals_b.as<uint64_t>(),
-                                                    c->arena, c->pf_changed));
-        HIPCHK(c, hipStreamSynchronize(c->st));
-    }
     return SK_OK;
-}
-
-// Path choice.  Partition (default): any density.  Claim/commit: expected
-// conflicting fraction ~ (n / touched) / 32768, used while that is small, else
-// the sorted path.
-bool pfadd_uses_sort(sk_ctx *c, uint64_t n, uint64_t touched_keys) {
-    if (c->pfadd_path == 1) return false;
-    if (c->pfadd_path == 2) return true;
-    return !(touched_keys && n <= 2048 * touched_keys && n < (1ull << 26));
 }
 
 // partition path (sk_kernels.hip "PFADD, partition path"); n <= 2^20 per launch.
@@ -1127,31 +1059,34 @@ int pfadd_device(sk_ctx *c, uint64_t n, const uint32_t *d_ids, const uint64_t *d
         }
         return SK_OK;
     }
-    if (!pfadd_uses_sort(c, n, touched_keys)) return pfadd_sparse(c, n, d_ids, d_off, d_bytes, d_cmd, d_changed);
-    return pfadd_sorted(c, n, d_ids, d_off, d_bytes, d_cmd, n_cmds, d_changed);
+    return fail(c, SK_EINVAL, "PFADD path %d is retired (the partition path is 1)", c->pfadd_path);
 }
 
+// base: the packed arena (slab ids), or a u8 register array (d_ids = d_zero)
 int hll_histograms(sk_ctx *c, uint64_t n, const uint32_t *d_ids, const uint8_t *base, std::vector<uint32_t> &h) {
     HIPCHK(c, c->hist.ensure(n * 64 * 4));
     { Prof p_(c, 3);
-    HIPCHK(c, sk::launch_hll_hist(c->st, n, d_ids, base, c->hist.as<uint32_t>())); }
+    HIPCHK(c, sk::launch_hll_hist(c->st, n, d_ids, base, c->hist.as<uint32_t>(), base == c->arena ? 1 : 0)); }
     h.resize(n * 64);
     HIPCHK(c, hipMemcpyAsync(h.data(), c->hist.p, n * 64 * 4, hipMemcpyDeviceToHost, c->st));
     return sync(c);
 }
 
-int union_into(sk_ctx *c, const std::vector<uint32_t> &ids, uint8_t *d_out, int include_out) {
+// register max of slabs `ids` into d_out: u8 registers, or a packed slab of the arena (out_slab)
+int union_into(sk_ctx *c, const std::vector<uint32_t> &ids, uint8_t *d_out, int include_out, int out_slab) {
     HIPCHK(c, c->in_ids.ensure(std::max<size_t>(ids.size(), 1) * 4));
     if (!ids.empty())
         HIPCHK(c, hipMemcpyAsync(c->in_ids.p, ids.data(), ids.size() * 4, hipMemcpyHostToDevice, c->st));
     const uint64_t max_groups = 4096;
     HIPCHK(c, c->partial.ensure((max_groups + max_groups / 64 + 2) * kHllBytes));
     HIPCHK(c, sk::launch_hll_union(c->st, ids.size(), c->in_ids.as<uint32_t>(), c->arena, c->partial.as<uint8_t>(),
-                                   max_groups, d_out, include_out));
+                                   max_groups, d_out, include_out, 1, out_slab));
     return sync(c); // ids is a host vector
 }
 
-uint64_t estimate_host(sk_ctx *c, const uint32_t *hist, const uint8_t *d_regs, bool raw_order, int *rc) {
+// d_regs: u8 registers on the device, or (packed) a slab of the arena
+uint64_t estimate_host(sk_ctx *c, const uint32_t *hist, const uint8_t *d_regs, bool raw_order, int *rc,
+                       bool packed = false) {
     *rc = SK_OK;
     if (c->redis_major >= 5) return estimate_v5(hist);
     if (hist_exact_v3(hist)) {
@@ -1160,11 +1095,13 @@ uint64_t estimate_host(sk_ctx *c, const uint32_t *hist, const uint8_t *d_regs, b
         return estimate_v3(E, int(hist[0]));
     }
     // a register >= 40: the summation order matters -> redo it in Redis order
-    std::vector<uint8_t> regs(kHllBytes);
-    if (hipMemcpy(regs.data(), d_regs, kHllBytes, hipMemcpyDeviceToHost) != hipSuccess) {
+    std::vector<uint8_t> regs(kHllBytes), body(packed ? kSlabBytes : 0);
+    if (hipMemcpy(packed ? body.data() : regs.data(), d_regs, packed ? kSlabBytes : kHllBytes, hipMemcpyDeviceToHost) !=
+        hipSuccess) {
         *rc = fail(c, SK_EDEVICE, "register readback failed");
         return 0;
     }
+    if (packed) hll_body_unpack(body.data(), regs.data());
     int ez;
     double E = raw_order ? raw_sum(regs.data(), &ez) : dense_sum(regs.data(), &ez);
     return estimate_v3(E, ez);
@@ -1243,7 +1180,6 @@ int sk_open(const sk_config *cfg, sk_ctx **out) {
     }
     if (const char *e = getenv("SK_BLOOM_SCHED")) c->bloom_sched = atoi(e);
     if (const char *e = getenv("SK_READ_STREAM")) c->read_stream = atoi(e);
-    if (const char *e = getenv("SK_PFADD_CLAIM")) c->claim_all = atoi(e);
     if (const char *e = getenv("SK_PFADD_PATH")) c->pfadd_path = atoi(e);
     if (const char *e = getenv("SK_PFP_DIRECT")) c->pfp_direct = atoi(e) != 0;
     if (const char *e = getenv("SK_SBV_MIN")) c->sbv_min = strtoull(e, nullptr, 10);
@@ -1764,11 +1700,8 @@ int sk_pfadd_dev(sk_ctx *c, uint64_t n, const uint32_t *d_ids, const uint64_t *d
     }
     for (uint64_t s = 0; s < n; s += max_cmds) {
         uint64_t m = std::min(max_cmds, n - s);
-        uint64_t live = c->hll_next - c->hll_free.size() - c->hll_retired; // slabs in use bounds the touched sketches
-        if (pfadd_uses_sort(c, m, live))
-            HIPCHK(c, hipMemsetAsync(d_changed + s, 0, m, c->st)); // the sorted path sets only the 1s
         Prof p_(c, 20); // the whole PFADD chain of this batch
-        int r = pfadd_device(c, m, d_ids + s, d_off + s, d_bytes, nullptr, m, d_changed + s, live);
+        int r = pfadd_device(c, m, d_ids + s, d_off + s, d_bytes, nullptr, m, d_changed + s, 0);
         if (r) return r;
     }
     return c->async_dev ? SK_OK : sync(c);
@@ -1787,7 +1720,7 @@ int sk_hll_histogram_dev(sk_ctx *c, uint64_t n, const uint32_t *d_ids, uint32_t 
     std::lock_guard<std::mutex> g(c->mu);
     ENTER(c);
     { Prof p_(c, 3);
-    HIPCHK(c, sk::launch_hll_hist(c->st, n, d_ids, c->arena, d_hist)); }
+    HIPCHK(c, sk::launch_hll_hist(c->st, n, d_ids, c->arena, d_hist, 1)); }
     return sync(c);
 }
 
@@ -1805,9 +1738,10 @@ static int estimate_many_sums(sk_ctx *c, uint64_t n, const uint64_t *s2, const u
     host_for(n, 32768, work);
     for (uint64_t i = 0; i < n; i++) {
         if (!slow[i]) continue;
-        std::vector<uint8_t> regs(kHllBytes);
-        HIPCHK(c, hipMemcpy(regs.data(), c->arena + uint64_t(ids[i] & kSlabMask) * kHllBytes, kHllBytes,
+        std::vector<uint8_t> regs(kHllBytes), body(kSlabBytes);
+        HIPCHK(c, hipMemcpy(body.data(), c->arena + uint64_t(ids[i] & kSlabMask) * kSlabBytes, kSlabBytes,
                             hipMemcpyDeviceToHost));
+        hll_body_unpack(body.data(), regs.data());
         int ez;
         const double E = dense_sum(regs.data(), &ez);
         out[i] = int64_t(estimate_v3(E, ez));
@@ -1846,7 +1780,8 @@ static int estimate_many(sk_ctx *c, uint64_t n, const uint32_t *h, const uint32_
     for (uint64_t i = 0; i < n; i++) {
         if (!slow[i]) continue;
         int rc;
-        out[i] = int64_t(estimate_host(c, h + i * 64, c->arena + uint64_t(ids[i] & kSlabMask) * kHllBytes, false, &rc));
+        out[i] = int64_t(
+            estimate_host(c, h + i * 64, c->arena + uint64_t(ids[i] & kSlabMask) * kSlabBytes, false, &rc, true));
         if (rc) return rc;
     }
     return SK_OK;
@@ -1956,7 +1891,7 @@ int sk_pfcount(sk_ctx *c, uint32_t n_cmds, const uint32_t *nkeys, const uint64_t
     HIPCHK(c, c->misc.ensure(4096));
     for (uint32_t cmd = 0; cmd < n_cmds; cmd++) {
         if (!is_multi[cmd]) continue;
-        int r = union_into(c, multi[cmd], c->uni.as<uint8_t>(), 0);
+        int r = union_into(c, multi[cmd], c->uni.as<uint8_t>(), 0, 0);
         if (r) return r;
         r = hll_histograms(c, 1, c->d_zero, c->uni.as<uint8_t>(), h);
         if (r) return r;
@@ -1986,7 +1921,7 @@ int sk_hll_union_dev(sk_ctx *c, uint64_t n, const uint32_t *d_ids, uint8_t *d_ou
     const uint64_t max_groups = 4096;
     HIPCHK(c, c->partial.ensure((max_groups + max_groups / 64 + 2) * kHllBytes));
     { Prof p_(c, 4);
-    HIPCHK(c, sk::launch_hll_union(c->st, n, d_ids, c->arena, c->partial.as<uint8_t>(), max_groups, d_out, 0)); }
+    HIPCHK(c, sk::launch_hll_union(c->st, n, d_ids, c->arena, c->partial.as<uint8_t>(), max_groups, d_out, 0, 1, 0)); }
     return sync(c);
 }
 
@@ -2035,7 +1970,7 @@ int sk_hll_union_keys(sk_ctx *c, uint32_t n, const uint64_t *off, const uint8_t 
     HIPCHK(c, c->partial.ensure((max_groups + max_groups / 64 + 2) * kHllBytes));
     { Prof p_(c, 4);
     HIPCHK(c, sk::launch_hll_union(c->st, k, c->in_ids.as<uint32_t>(), c->arena, c->partial.as<uint8_t>(), max_groups,
-                                   d_out, 0)); }
+                                   d_out, 0, 1, 0)); }
     return sync(c); // ids is a host vector
 }
 
@@ -2055,7 +1990,7 @@ int sk_pfmerge(sk_ctx *c, const uint8_t *dest, uint64_t dest_len, uint32_t n_src
     int r = hll_get(c, key_of(dest, dest_len), true, &did, nullptr);
     if (r) return r;
     hll_str_merged(c, did);
-    return union_into(c, ids, c->arena + uint64_t(did) * kHllBytes, 1);
+    return union_into(c, ids, c->arena + uint64_t(did) * kSlabBytes, 1, 1);
 }
 
 int sk_hll_merge_registers_dev(sk_ctx *c, const uint8_t *key, uint64_t len, const uint8_t *d_regs) {
@@ -2069,7 +2004,7 @@ int sk_hll_merge_registers_dev(sk_ctx *c, const uint8_t *key, uint64_t len, cons
     const uint64_t max_groups = 4096;
     HIPCHK(c, c->partial.ensure((max_groups + max_groups / 64 + 2) * kHllBytes));
     HIPCHK(c, sk::launch_hll_union(c->st, 1, c->d_zero, d_regs, c->partial.as<uint8_t>(), max_groups,
-                                   c->arena + uint64_t(did) * kHllBytes, 1));
+                                   c->arena + uint64_t(did) * kSlabBytes, 1, 0, 1));
     return sync(c);
 }
 
@@ -2083,8 +2018,11 @@ int sk_hll_registers(sk_ctx *c, const uint8_t *key, uint64_t len, uint8_t *out) 
         std::memset(out, 0, kHllBytes);
         return SK_OK;
     }
-    HIPCHK(c, hipMemcpyAsync(out, c->arena + uint64_t(id) * kHllBytes, kHllBytes, hipMemcpyDeviceToHost, c->st));
-    return sync(c);
+    std::vector<uint8_t> body(kSlabBytes);
+    HIPCHK(c, hipMemcpyAsync(body.data(), c->arena + uint64_t(id) * kSlabBytes, kSlabBytes, hipMemcpyDeviceToHost, c->st));
+    int rr = sync(c);
+    if (!rr) hll_body_unpack(body.data(), out);
+    return rr;
 }
 
 } // extern "C"
@@ -2677,11 +2615,6 @@ int sk_get(sk_ctx *c, const uint8_t *key, uint64_t len, uint8_t *buf, uint64_t c
         return SK_OK;
     }
     if (it->second.type == SK_TYPE_HLL) {
-        std::vector<uint8_t> regs(kHllBytes);
-        HIPCHK(c, hipMemcpyAsync(regs.data(), c->arena + uint64_t(it->second.id) * kHllBytes, kHllBytes,
-                                 hipMemcpyDeviceToHost, c->st));
-        int r = sync(c);
-        if (r) return r;
         const HllStr *hx = c->hll_exact && it->second.id < c->hstr.size() ? &c->hstr[it->second.id] : nullptr;
         if (hx && hx->sparse) { // the sparse string as redis-server keeps it
             *out_len = int64_t(16 + hx->ops.size());
@@ -2689,8 +2622,15 @@ int sk_get(sk_ctx *c, const uint8_t *key, uint64_t len, uint8_t *buf, uint64_t c
             if (cap > 16) std::memcpy(buf + 16, hx->ops.data(), std::min<uint64_t>(cap - 16, hx->ops.size()));
             return SK_OK;
         }
+        // the slab is the dense body itself: header + one copy
         std::vector<uint8_t> s(SK_HLL_DENSE_SIZE, 0);
-        hll_dense_encode(regs.data(), hx ? hx->hdr : nullptr, s.data());
+        std::memcpy(s.data(), "HYLL", 4);
+        s[15] = 0x80;
+        if (hx) std::memcpy(s.data(), hx->hdr, 16);
+        HIPCHK(c, hipMemcpyAsync(s.data() + 16, c->arena + uint64_t(it->second.id) * kSlabBytes, kSlabBytes,
+                                 hipMemcpyDeviceToHost, c->st));
+        int r = sync(c);
+        if (r) return r;
         *out_len = int64_t(s.size());
         if (cap) std::memcpy(buf, s.data(), std::min<uint64_t>(cap, s.size()));
         return SK_OK;
@@ -3483,8 +3423,8 @@ extern "C" int sk_gen_jackson_longs_dev(sk_ctx *c, uint64_t seed, const uint64_t
 namespace {
 
 // GET's bytes of an HLL key (sk_get): the exact-mode sparse string, or the dense encoding (kept header in exact
-// mode, else "HYLL" + stale cache).  regs: the slab's registers, already on the host.
-void hll_string_of(const sk_ctx *c, uint32_t id, const uint8_t *regs, std::string &out) {
+// mode, else "HYLL" + stale cache).  body: the slab (the dense register body), already on the host.
+void hll_string_of(const sk_ctx *c, uint32_t id, const uint8_t *body, std::string &out) {
     const HllStr *hx = c->hll_exact && id < c->hstr.size() ? &c->hstr[id] : nullptr;
     if (hx && hx->sparse) {
         out.assign(reinterpret_cast<const char *>(hx->hdr), 16);
@@ -3492,7 +3432,9 @@ void hll_string_of(const sk_ctx *c, uint32_t id, const uint8_t *regs, std::strin
         return;
     }
     out.assign(SK_HLL_DENSE_SIZE, '\0');
-    hll_dense_encode(regs, hx ? hx->hdr : nullptr, reinterpret_cast<uint8_t *>(&out[0]));
+    uint8_t hdr[16] = {'H', 'Y', 'L', 'L', 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0x80};
+    std::memcpy(&out[0], hx ? hx->hdr : hdr, 16);
+    std::memcpy(&out[16], body, kSlabBytes);
 }
 
 // the value of key k as a DUMP payload (*found = false: no such key)
@@ -3509,12 +3451,12 @@ int key_payload(sk_ctx *c, const std::string &k, std::string &out, bool *found) 
     *found = true;
     std::string v;
     if (it->second.type == SK_TYPE_HLL) {
-        std::vector<uint8_t> regs(kHllBytes);
-        HIPCHK(c, hipMemcpyAsync(regs.data(), c->arena + uint64_t(it->second.id) * kHllBytes, kHllBytes,
+        std::vector<uint8_t> body(kSlabBytes);
+        HIPCHK(c, hipMemcpyAsync(body.data(), c->arena + uint64_t(it->second.id) * kSlabBytes, kSlabBytes,
                                  hipMemcpyDeviceToHost, c->st));
         int r = sync(c);
         if (r) return r;
-        hll_string_of(c, it->second.id, regs.data(), v);
+        hll_string_of(c, it->second.id, body.data(), v);
     } else {
         uint64_t l;
         int r = str_len(c, it->second.id, &l);

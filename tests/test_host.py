@@ -252,3 +252,31 @@ def test_newest_bench_record_is_physical():
     cpu = d.get("cpu_baseline")
     if cpu and "host" in cpu:
         assert cpu["host"]["nproc"] and cpu["cores"] >= 1
+
+
+def test_handle_indexed_kernels_mask_the_generation():
+    """Kernels that index the packed arena by caller handles (slab | generation << 24) mask the generation off before
+    the 12,288-B slab multiply.  hipcc (ROCm 7.2) folds `(h & 0xffffff) * 12288` into one v_mad_u64_u32 of the
+    unmasked handle (a GPU memory aperture violation in round 6); sk_kernels.hip's slab_of() keeps the AND behind an
+    empty asm.  Checked on the built gfx950 code object's disassembly (no GPU)."""
+    import re
+    import subprocess
+    import tempfile
+
+    obj = os.path.join(ROOT, "build", "obj", "sk_kernels.o")
+    if not os.path.exists(obj):
+        pytest.skip("engine not built")
+    llvm = "/opt/rocm/lib/llvm/bin"
+    with tempfile.TemporaryDirectory() as d:
+        fb, co = os.path.join(d, "fb.bin"), os.path.join(d, "k.co")
+        subprocess.run([f"{llvm}/llvm-objcopy", f"--dump-section=.hip_fatbin={fb}", obj, os.path.join(d, "x.o")],
+                       check=True)
+        subprocess.run([f"{llvm}/clang-offload-bundler", "--unbundle", "--type=o", f"--input={fb}",
+                        "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"], check=True)
+        dis = subprocess.run([f"{llvm}/llvm-objdump", "-d", co], check=True, capture_output=True, text=True).stdout
+    funcs = re.split(r"\n(?=[0-9a-f]+ <_Z)", dis)
+    want = ["k_hll_sum", "k_hll_histILb1E", "k_hll_pack", "k_hll_unpack", "k_hll_union_partialILb1E"]
+    for w in want:
+        body = [f for f in funcs if re.match(r"[0-9a-f]+ <_ZN2sk\d+" + w, f)]
+        assert len(body) == 1, w
+        assert "0xffffff" in body[0], "%s: the slab mask was folded away" % w

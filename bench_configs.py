@@ -50,6 +50,9 @@ def line(d):
     print(json.dumps(d), flush=True)
 
 
+SLAB = 12288   # bytes a PFCOUNT / union kernel reads per key: the arena's packed 6-bit register body
+
+
 def timed(eng, fn, reps=1):
     eng.sync()
     t0 = time.perf_counter()
@@ -118,6 +121,43 @@ def c1(eng, args):
                         eng.pfcount([[b"hll:c1q"]])[0]}})
 
 
+def c2u(eng, args):
+    """C2 as one RBatch per call (RedissonBatch.execute -> one device call, M:RedissonBatch.java:226-228): 1M-command
+    PFADD batches over 100k uniform tenants, each its own sk_pfadd_dev call (the partition path: k_pfp_hash +
+    k_pfp_apply), device-timed (HIP events around each call's chain) and host-timed."""
+    B, steps, nt = 1 << 20, 20, 100_000
+    names = [b"tenant:%d:hll" % t for t in range(nt)]
+    ids = eng.hll_resolve(names)
+    rng = np.random.default_rng(23)
+    kid = rng.integers(0, nt, B * (steps + 2))
+    d_ids = eng.to_device(ids[kid].astype(np.uint32))
+    off, byt, tot = eng.gen_jackson_longs_dev(0x5EED0023, B * (steps + 2))
+    d_out = eng.alloc(B)
+    for s in range(2):   # warm
+        eng.pfadd_dev(B, d_ids.ptr + s * B * 4, off.ptr + s * B * 8, byt, tot, d_out)
+    eng.prof_reset()
+    eng.prof_enable(True)
+    eng.prof_only("pfadd,pfp_hash,pfp_apply")
+    eng.set_async(True)
+    t = timed(eng, lambda: [eng.pfadd_dev(B, d_ids.ptr + s * B * 4, off.ptr + s * B * 8, byt, tot, d_out)
+                            for s in range(2, steps + 2)])
+    eng.set_async(False)
+    eng.prof_enable(False)
+    eng.prof_only(None)
+    n_c, ms_c = eng.prof_read("pfadd")
+    k = {p: eng.prof_read(p) for p in ("pfp_hash", "pfp_apply")}
+    t_sync = timed(eng, lambda: [eng.pfadd_dev(B, d_ids.ptr + s * B * 4, off.ptr + s * B * 8, byt, tot, d_out)
+                                 for s in range(2, steps + 2)])
+    line({"metric": "C2 PFADD inserts/sec, one 1M-command RBatch per device call (100k uniform tenants)",
+          "value": B * steps / t, "unit": "inserts/s",
+          "config": {"workload": "c2u", "batch": B, "tenants": nt, "calls": steps},
+          "device_inserts_per_s": B / (ms_c / n_c * 1e-3) if n_c else None,
+          "device_ms_per_call": ms_c / n_c if n_c else None,
+          "kernel_ms": {p: (v[1] / v[0] if v[0] else None) for p, v in k.items()},
+          "synchronous_calls_inserts_per_s": B * steps / t_sync,
+          "note": "value: back-to-back async calls host-timed; device: HIP events around each call's PFADD chain"})
+
+
 def c2zipf(eng, args):
     """SURVEY 8d C2 variant: 1M-command PFADD batches with Zipf(1.1) tenants (device-resident)."""
     B, steps, nt, G = 1 << 20, 10, 100_000, 64
@@ -162,7 +202,7 @@ def c2zipf(eng, args):
     s_ms = ms_s / max(n_s, 1)
     t_c = timed(eng, lambda: eng.pfcount([[nm] for nm in names]))
     t_ci = timed(eng, lambda: eng.pfcount_ids(ids))                  # slab ids cached by the caller
-    gbs = nt * 16384 / (k_ms * 1e-3) / 1e9
+    gbs = nt * SLAB / (k_ms * 1e-3) / 1e9
     line({"metric": "C2 Zipf(1.1) PFADD inserts/sec (1M-command batches, 100k tenants)", "value": B * steps / t,
           "unit": "inserts/s", "config": {"workload": "c2zipf", "batch": B, "tenants": nt, "zipf_s": 1.1,
                                           "hottest_tenant_share": top},
@@ -174,8 +214,8 @@ def c2zipf(eng, args):
           "hll_hist": {"achieved_GBps": gbs, "frac": gbs / PEAK, "avg_launch_ms": k_ms,
                        "note": "64-bin histograms (sk_hll_histogram_dev; the redis >= 5 estimator's input)"},
           "roofline": {"kernel": "hll_sum (PFCOUNT, redis 3.x: exact register sums)", "bound": "hbm",
-                       "achieved": nt * 16384 / (s_ms * 1e-3) / 1e9, "peak": PEAK, "unit": "GB/s",
-                       "frac": nt * 16384 / (s_ms * 1e-3) / 1e9 / PEAK, "bytes_per_unit": 16384,
+                       "achieved": nt * SLAB / (s_ms * 1e-3) / 1e9, "peak": PEAK, "unit": "GB/s",
+                       "frac": nt * SLAB / (s_ms * 1e-3) / 1e9 / PEAK, "bytes_per_unit": SLAB,
                        "avg_launch_ms": s_ms}})
 
 
@@ -203,12 +243,12 @@ def c4(eng, args):
     k_ms = ms / max(n_l, 1)
     eng.hll_merge_registers_dev(b"t4:union", d_u)
     est = eng.pfcount([[b"t4:union"]])[0]
-    gbs = nk * 16384 / (k_ms * 1e-3) / 1e9
+    gbs = nk * SLAB / (k_ms * 1e-3) / 1e9
     line({"metric": "C4 global union (countWith/PFMERGE) sources/sec, one GPU's shard", "value": nk / t_u,
           "unit": "sources/s", "config": {"workload": "c4", "keys": nk, "elements_per_key": per},
           "pfadd_inserts_per_s": total / t_add, "union_estimate": est,
           "roofline": {"kernel": "hll_union", "bound": "hbm", "achieved": gbs, "peak": PEAK, "unit": "GB/s",
-                       "frac": gbs / PEAK, "bytes_per_unit": 16384, "avg_launch_ms": k_ms}})
+                       "frac": gbs / PEAK, "bytes_per_unit": SLAB, "avg_launch_ms": k_ms}})
 
 
 def c5(eng, args):
@@ -592,7 +632,7 @@ def host(eng, args):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--configs", default="c1,c2zipf,c4,c5,host")
+    ap.add_argument("--configs", default="c1,c2u,c2zipf,c4,c5,host")
     ap.add_argument("--c1-n", type=int, default=1 << 20)
     ap.add_argument("--c4-keys", type=int, default=125_000)       # 1M keys / 8 GPUs
     ap.add_argument("--c4-per-key", type=int, default=1000)
@@ -607,7 +647,7 @@ def main():
     eng = SketchEngine(device=int(os.environ.get("LOCAL_RANK", "0")), max_bit_offset=1 << 36,
                        hll_capacity=cap, max_batch=1 << 24)
     for c in cfgs:
-        {"c1": c1, "c2zipf": c2zipf, "c4": c4, "c5": c5, "host": host, "c4mr": c4mr, "c5mr": c5mr}[c](eng, args)
+        {"c1": c1, "c2u": c2u, "c2zipf": c2zipf, "c4": c4, "c5": c5, "host": host, "c4mr": c4mr, "c5mr": c5mr}[c](eng, args)
     eng.close()
 
 

@@ -860,6 +860,9 @@ __global__ void __launch_bounds__(SK_PFP_ATPB) __attribute__((amdgpu_waves_per_e
 #ifndef SK_PFL_LDS
 #define SK_PFL_LDS (160 * 1024 - 9 * 1024) // dynamic LDS of a region workgroup: records + fine-bucket counts
 #endif
+#ifndef SK_PFL_XORD
+#define SK_PFL_XORD 8      // the apply's XCD order: fine buckets per XCD block (0: bucket-major, the round-5 order)
+#endif
 #ifndef SK_PFL_WFU
 #define SK_PFL_WFU 4       // wave-loaded pair steps in flight per thread
 #endif
@@ -1170,6 +1173,21 @@ __global__ void __launch_bounds__(256) k_pfl_fill(uint8_t *__restrict__ changed,
 #define SK_PFL_DG 1        // 16-B words per dirty flag: the apply stores back the 16-B pieces of its lines that changed
 #endif
 #define PFL_DWORDS ((16384 / 16 / SK_PFL_DG + 31) / 32)
+// The apply's lines stay packed in LDS (Redis's layout, 24 words per 128-register line, line i at word 24 i): a
+// chunk touches ~600 of the 16384 registers it holds, so reading and writing those fields costs less than unpacking
+// every line to bytes and packing the changed ones back.  Register slotb = line << 7 | register-in-line.
+__device__ __forceinline__ uint32_t lds_reg_get(const uint32_t *lw, uint32_t slotb) {
+    const uint32_t bit = 6u * (slotb & 127u), w = (slotb >> 7) * 24u + (bit >> 5), sh = bit & 31u;
+    uint32_t v = lw[w] >> sh;
+    if (sh > 26u) v |= lw[w + 1] << (32u - sh);
+    return v & 63u;
+}
+// field slotb from `old` to old ^ x (LDS XORs: neighbours of the same words may change at the same time)
+__device__ __forceinline__ void lds_reg_xor(uint32_t *lw, uint32_t slotb, uint32_t x) {
+    const uint32_t bit = 6u * (slotb & 127u), w = (slotb >> 7) * 24u + (bit >> 5), sh = bit & 31u;
+    atomicXor(&lw[w], x << sh);
+    if (sh > 26u) atomicXor(&lw[w + 1], x >> (32u - sh));
+}
 __device__ __forceinline__ void pfl_mark(uint32_t *dirty, uint32_t slotb) { // register slotb of the LDS lines changed
     const uint32_t piece = slotb / (16 * SK_PFL_DG);
     atomicOr(&dirty[piece >> 5], 1u << (piece & 31u));
@@ -1182,7 +1200,7 @@ __device__ __forceinline__ void pfl_mark(uint32_t *dirty, uint32_t slotb) { // r
 // reply (only those that differ from the call's default when the replies were pre-filled).
 template <class Fill, class Put>
 __device__ __forceinline__ void pfl_chunk(const uint64_t *R, uint32_t cnt, uint16_t *nxt, uint32_t *head,
-                                          uint8_t *fin, uint8_t *reg, uint32_t *dirty, Fill fill, Put put) {
+                                          uint8_t *fin, uint32_t *lw, uint32_t *dirty, Fill fill, Put put) {
     for (uint32_t u = threadIdx.x; u < cnt; u += SK_PFL_ATPB)
         nxt[u] = uint16_t(atomicExch(&head[pfl_ht(R[u] >> 32)], u));
     fill();
@@ -1203,16 +1221,16 @@ __device__ __forceinline__ void pfl_chunk(const uint64_t *R, uint32_t cnt, uint1
             }
         }
         const uint32_t slotb = pfl_slotb(key);
-        const uint32_t R0 = reg[slotb];
+        const uint32_t R0 = lds_reg_get(lw, slotb);
         put(uint32_t(seq), uint32_t(rho > (R0 > p ? R0 : p)));
-        fin[u] = earliest && m > R0 ? uint8_t(m) : uint8_t(0);
+        fin[u] = earliest && m > R0 ? uint8_t(m ^ R0) : uint8_t(0); // the register's change, as an XOR
     }
     __syncthreads();
     for (uint32_t u = threadIdx.x; u < cnt; u += SK_PFL_ATPB)
         if (fin[u]) {
-            const uint64_t key = R[u] >> 32;
-            reg[pfl_slotb(key)] = fin[u];
-            pfl_mark(dirty, pfl_slotb(key));
+            const uint32_t slotb = pfl_slotb(R[u] >> 32);
+            lds_reg_xor(lw, slotb, fin[u]);
+            pfl_mark(dirty, slotb);
         }
 }
 
@@ -1241,7 +1259,10 @@ __global__ void __launch_bounds__(256) k_pfl_plan(const uint32_t *__restrict__ C
     if (heavy && base + ph < hmax) order[base + ph] = f; // hmax bounds the heavy buckets (n / (CAP + 1))
 }
 
-__global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const PflRec rec2,
+#ifndef SK_PFL_AWPE
+#define SK_PFL_AWPE 6      // apply waves per SIMD the register budget allows (6: <= 80 VGPRs; 7 needs <= 72)
+#endif
+__global__ void __launch_bounds__(SK_PFL_ATPB) __attribute__((amdgpu_waves_per_eu(SK_PFL_AWPE))) k_pfl_apply(const PflRec rec2,
                                                            const uint32_t *__restrict__ rbase,
                                                            const uint32_t *__restrict__ C2, uint32_t ntile,
                                                            uint32_t nsub, uint32_t sh, PflPerm pm, uint32_t nslab,
@@ -1256,12 +1277,11 @@ __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const PflRec rec2,
     constexpr uint32_t kBigL = 512;        // LDS slots of the big-run table
     static_assert(kWork >= kBigL * 12, "the big-run table shares the chunk LDS");
     constexpr uint32_t LW = (1u << SK_PFL_LB) / 16; // 16-B words per line
-    __shared__ uint4 regs4[NL * LW];           // line of sketch slab0 + i at reg[i << SK_PFL_LB]
+    __shared__ uint32_t lw[NL * 24];           // packed line of sketch slab0 + i at lw[24 i] (12-B group q at 3q)
     __shared__ uint64_t work[(kWork + 7) / 8]; // chunk records, chains, final values (or the big-run table)
     __shared__ uint32_t dirty[PFL_DWORDS]; // bit per SK_PFL_DG-word piece of the lines: changed, stored back
     __shared__ uint32_t rs[SK_PFL_NTMAX], rp[SK_PFL_NTMAX + 1]; // the fine bucket's run per tile: start, prefix
     __shared__ uint32_t wsum[SK_PFL_ATPB / 64];
-    uint8_t *reg = reinterpret_cast<uint8_t *>(regs4);
     uint64_t *R = work;
     uint16_t *nxt = reinterpret_cast<uint16_t *>(R + SK_PFL_CAP);
     uint32_t *head = reinterpret_cast<uint32_t *>(nxt + SK_PFL_CAP);
@@ -1275,9 +1295,20 @@ __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const PflRec rec2,
         // XCD-aware order (hmax is a multiple of 8, so j % 8 is the workgroup's XCD): the 128 coarse buckets of one
         // group of fine buckets run back to back on one XCD, so the 96-B packed lines of neighbouring buckets -- which
         // share 128-B cache lines for line % 4 in {1, 2} -- meet in that XCD's L2 and each cache line is read once
-        const uint32_t j = blockIdx.x - hmax, jj = j >> 3, sub_ = (jj / SK_PFL_NB) * 8u + (j & 7u);
+        const uint32_t j = blockIdx.x - hmax;
+#if SK_PFL_XORD == 0
+        f = j; // bucket-major: f = b * nsub + sub
+        if (f >= SK_PFL_NB * nsub) return;
+#else
+        // XCD x takes blocks of SK_PFL_XORD consecutive fine buckets of each coarse bucket; on it, b advances every
+        // SK_PFL_XORD workgroups: the block's record runs lie side by side in each region (shared record lines) and a
+        // sketch's neighbouring lines come SK_PFL_XORD workgroups apart (shared packed-line lines in its L2)
+        constexpr uint32_t SB = SK_PFL_XORD;
+        const uint32_t x = j & 7u, jj = j >> 3, grp = jj / (SK_PFL_NB * SB), w = jj % (SK_PFL_NB * SB);
+        const uint32_t sub_ = (grp * 8u + x) * SB + w % SB;
         if (sub_ >= nsub) return;
-        f = (jj % SK_PFL_NB) * nsub + sub_;
+        f = (w / SB) * nsub + sub_;
+#endif
     }
     const uint32_t b = f / nsub, sub = f % nsub;
     const uint32_t slab0 = sub << sh, nsl = 1u << sh; // permuted ids slab0 + i, i < nsl
@@ -1367,15 +1398,24 @@ __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const PflRec rec2,
 #pragma unroll
             for (int j = 0; j < LQ; j++) {
                 const uint32_t q = threadIdx.x + j * SK_PFL_ATPB;
-                if (q < nsl * LW && pm.inv(slab0 + q / LW) < nslab) regs4[q] = unpack16(lv[j].x, lv[j].y, lv[j].z);
+                if (q < nsl * LW && pm.inv(slab0 + q / LW) < nslab) {
+                    lw[3 * q] = lv[j].x;
+                    lw[3 * q + 1] = lv[j].y;
+                    lw[3 * q + 2] = lv[j].z;
+                }
             }
         };
         __syncthreads();
         if (probe & 128) return; // dev ablation: run table, lines and records loaded, nothing applied
-        pfl_chunk(R, cnt, nxt, head, fin, reg, dirty, fill_lines, put);
+        pfl_chunk(R, cnt, nxt, head, fin, lw, dirty, fill_lines, put);
     } else {
         for (uint32_t q = threadIdx.x; q < nsl * LW; q += SK_PFL_ATPB)
-            if (pm.inv(slab0 + q / LW) < nslab) regs4[q] = grp_load(line(q / LW), q % LW);
+            if (pm.inv(slab0 + q / LW) < nslab) {
+                const uint32_t *w = reinterpret_cast<const uint32_t *>(line(q / LW)) + 3 * (q % LW);
+                lw[3 * q] = w[0];
+                lw[3 * q + 1] = w[1];
+                lw[3 * q + 2] = w[2];
+            }
         __syncthreads();
         uint32_t t0 = 0;
         while (t0 < ntile) { // uniform: chunks of whole runs, in tile (= batch) order
@@ -1397,7 +1437,7 @@ __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const PflRec rec2,
                     if (u < k) R[u] = rr[q];
                 }
                 __syncthreads();
-                pfl_chunk(R, k, nxt, head, fin, reg, dirty, [] {}, put);
+                pfl_chunk(R, k, nxt, head, fin, lw, dirty, [] {}, put);
             } else { // one run larger than a chunk (t1 == t0 + 1), contiguous from rs[t0]
                 const uint64_t run0 = rs[t0];
                 auto run = [&](uint32_t u) -> uint64_t { return rec2.get(run0 + u); };
@@ -1413,7 +1453,7 @@ __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const PflRec rec2,
                 auto consider = [&](uint64_t r) { // a record of the run: a candidate, or its reply is 0 now
                     if (r == ~0ull) return;
                     const uint64_t key = r >> 32;
-                    if (((r >> 26) & 63u) > reg[pfl_slotb(key)]) {
+                    if (((r >> 26) & 63u) > lds_reg_get(lw, pfl_slotb(key))) {
                         const uint32_t i = atomicAdd(&ncand, 1u);
                         if (i < SK_PFL_CAP) R[i] = r;
                     } else {
@@ -1472,7 +1512,7 @@ __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const PflRec rec2,
                 __syncthreads();
                 const uint32_t nc = ncand;
                 if (nc <= SK_PFL_CAP) {
-                    pfl_chunk(R, nc, nxt, head, fin, reg, dirty, [] {}, put);
+                    pfl_chunk(R, nc, nxt, head, fin, lw, dirty, [] {}, put);
                 } else {
                 __shared__ uint32_t gbase;
                 unsigned long long *lk = reinterpret_cast<unsigned long long *>(work);
@@ -1487,7 +1527,7 @@ __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const PflRec rec2,
                 __syncthreads();
                 auto cand = [&](uint64_t r) {
                     const uint64_t key = r >> 32;
-                    return ((r >> 26) & 63u) > reg[pfl_slotb(key)];
+                    return ((r >> 26) & 63u) > lds_reg_get(lw, pfl_slotb(key));
                 };
                 for (uint32_t u = threadIdx.x; u < k; u += SK_PFL_ATPB) {
                     const uint64_t r = run(u);
@@ -1512,8 +1552,9 @@ __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const PflRec rec2,
                     bool top = true;
                     for (uint32_t v = rho + 1; v < 52 && top; v++) top = T.find((key << 6) | v) == 0xffffffffu;
                     const uint32_t slotb = pfl_slotb(key);
-                    if (top && rho > reg[slotb]) {
-                        reg[slotb] = uint8_t(rho);
+                    const uint32_t cur = lds_reg_get(lw, slotb); // this thread is the register's only writer
+                    if (top && rho > cur) {
+                        lds_reg_xor(lw, slotb, cur ^ rho);
                         pfl_mark(dirty, slotb);
                     }
                 }
@@ -1537,8 +1578,13 @@ __global__ void __launch_bounds__(SK_PFL_ATPB) k_pfl_apply(const PflRec rec2,
         }
     }
     if (probe & 4) return;
-    for (uint32_t q = threadIdx.x; q < nsl * LW; q += SK_PFL_ATPB) // the changed 16-register groups, packed
-        if ((dirty[(q / SK_PFL_DG) >> 5] >> ((q / SK_PFL_DG) & 31u)) & 1u) grp_store(line(q / LW), q % LW, regs4[q]);
+    for (uint32_t q = threadIdx.x; q < nsl * LW; q += SK_PFL_ATPB) // the changed 16-register groups (12 B each)
+        if ((dirty[(q / SK_PFL_DG) >> 5] >> ((q / SK_PFL_DG) & 31u)) & 1u) {
+            uint32_t *w = reinterpret_cast<uint32_t *>(line(q / LW)) + 3 * (q % LW);
+            w[0] = lw[3 * q];
+            w[1] = lw[3 * q + 1];
+            w[2] = lw[3 * q + 2];
+        }
 }
 
 // streamed-once 16-B load with the nontemporal hint (native vector type for the builtin)
@@ -4325,7 +4371,9 @@ hipError_t launch_pfl_apply(hipStream_t st, const PflDims &d, const uint64_t *re
                            uint32_t(d.nf), hmax, big_alloc + 1, order);
         SK_LAUNCH_CHECK();
     }
-    const uint32_t hmax8 = (hmax + 7u) & ~7u, nsubx = uint32_t((d.nsub + 7) / 8 * 8); // see k_pfl_apply's XCD order
+    // see k_pfl_apply's XCD order: heavy slots a multiple of 8, the fine buckets padded to whole XCD blocks
+    const uint32_t sbx = SK_PFL_XORD ? 8u * SK_PFL_XORD : 1u;
+    const uint32_t hmax8 = (hmax + 7u) & ~7u, nsubx = uint32_t((d.nsub + sbx - 1) / sbx * sbx);
     hipLaunchKernelGGL(k_pfl_apply, dim3(uint32_t(SK_PFL_NB) * nsubx + hmax8), dim3(SK_PFL_ATPB), 0, st,
                        PflRec{const_cast<uint64_t *>(rec2), uint64_t(d.nblk) * SK_PFP_EPB}, rbase, C2, d.ntile,
                        d.nsub, d.sh, PflPerm{d.pa, d.pai, d.pm_mask, d.nslab}, nslab, arena, changed, big_alloc,

@@ -1596,12 +1596,12 @@ __device__ __forceinline__ uint4 ld_nt(const uint4 *p) {
 
 // -------------------------------------------------------------- exact register sums (PFCOUNT, redis 3.x)
 // The 3.x estimator needs only E = sum 2^-r[j] and the zero count (hllDenseSum).  With every register <= 39 each
-// partial sum of E is exact in double (multiples of 2^-39 below 2^14), so E = S * 2^-40 with the integer
-// S = sum 2^(40 - r[j]) (< 2^55) is bit-identical to Redis's sum in any order.  One wave per key, no LDS: a lane sums
-// 256 registers (16 packed 12-B groups in flight, unpacked in registers), the wave reduces with shuffles.  out[2k] = S, out[2k + 1] = zeros |
-// (a register >= 40) << 32: the host then takes Redis's register-order sum instead (S is not used).
-// Per byte: extract, 40 - r (the 64-bit shift takes it mod 64: garbage only for r > 40, which the flag catches),
-// a 64-bit shift and add; per word the zero count and the >= 40 test (r + 24 reaches bit 6 iff r >= 40, r <= 63).
+// partial sum of E is exact in double (multiples of 2^-39 below 2^14: 53 significant bits), so E summed in any order
+// -- and S = E * 2^40, an integer < 2^55 -- is bit-identical to Redis's sum.  One wave per key, no LDS: a lane sums
+// 256 registers (16 packed 12-B groups in flight), reading each 6-bit field straight from the packed words (one bit
+// field extract; two fields of a group straddle words), then 2^-r by v_ldexp_f64 and one f64 add; the wave reduces
+// with shuffles.  out[2k] = S, out[2k + 1] = zeros | (a register >= 40) << 32: the host then takes Redis's
+// register-order sum instead (S is not used).
 __global__ void __launch_bounds__(256) k_hll_sum(uint64_t n, const uint32_t *__restrict__ ids,
                                                  const uint8_t *__restrict__ arena, uint64_t *__restrict__ out) {
     const uint32_t lane = threadIdx.x & 63u;
@@ -1613,30 +1613,35 @@ __global__ void __launch_bounds__(256) k_hll_sum(uint64_t n, const uint32_t *__r
         for (int it = 0; it < 16; it++)
 #pragma unroll
             for (int q = 0; q < 3; q++) v[it][q] = __builtin_nontemporal_load(base + 3 * (it * 64 + lane) + q);
-        uint64_t S = 0;
-        uint32_t zeros = 0, ge40 = 0;
+        double E = 0.0;
+        uint32_t zeros = 0, rmax = 0;
 #pragma unroll
         for (int it = 0; it < 16; it++) {
-            const uint4 u = unpack16(v[it][0], v[it][1], v[it][2]);
-            const uint32_t ws[4] = {u.x, u.y, u.z, u.w};
+            const uint32_t w0 = v[it][0], w1 = v[it][1], w2 = v[it][2];
 #pragma unroll
-            for (int w = 0; w < 4; w++) {
-                const uint32_t x = ws[w] & 0x3f3f3f3fu;
-                zeros += __popc(~(((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x | 0x7f7f7f7fu));
-                ge40 |= (x + 0x18181818u) & 0x40404040u;
-#pragma unroll
-                for (int b = 0; b < 4; b++) S += 1ull << ((40u - ((x >> (8 * b)) & 63u)) & 63u);
+            for (int j = 0; j < 16; j++) { // register j of the group: bits [6j, 6j + 6) of w0 | w1 << 32 | w2 << 64
+                const int bit = 6 * j;
+                uint32_t r;
+                if (bit + 6 <= 32) r = (w0 >> bit) & 63u;
+                else if (bit < 32) r = __builtin_amdgcn_alignbit(w1, w0, bit) & 63u;
+                else if (bit + 6 <= 64) r = (w1 >> (bit - 32)) & 63u;
+                else if (bit < 64) r = __builtin_amdgcn_alignbit(w2, w1, bit - 32) & 63u;
+                else r = (w2 >> (bit - 64)) & 63u;
+                zeros += r == 0u ? 1u : 0u;
+                rmax = r > rmax ? r : rmax;
+                E += __builtin_amdgcn_ldexp(1.0, -int(r));
             }
         }
 #pragma unroll
         for (int o = 32; o; o >>= 1) {
-            S += __shfl_xor(S, o);
+            E += __shfl_xor(E, o);
             zeros += __shfl_xor(zeros, o);
-            ge40 |= __shfl_xor(ge40, o);
+            const uint32_t m = __shfl_xor(rmax, o);
+            rmax = m > rmax ? m : rmax;
         }
         if (lane == 0) {
-            out[2 * key] = S;
-            out[2 * key + 1] = uint64_t(zeros) | (uint64_t(ge40 ? 1u : 0u) << 32);
+            out[2 * key] = rmax < 40u ? uint64_t(E * 1099511627776.0) : 0ull; // E * 2^40, exact below 40
+            out[2 * key + 1] = uint64_t(zeros) | (uint64_t(rmax >= 40u ? 1u : 0u) << 32);
         }
     }
 }

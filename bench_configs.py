@@ -129,25 +129,43 @@ def c2u(eng, args):
     names = [b"tenant:%d:hll" % t for t in range(nt)]
     ids = eng.hll_resolve(names)
     rng = np.random.default_rng(23)
-    kid = rng.integers(0, nt, B * (steps + 2))
+    nb = 2 + 4 * steps   # warm, then fresh batches for each timing pass (a re-applied batch raises no register)
+    kid = rng.integers(0, nt, B * nb)
     d_ids = eng.to_device(ids[kid].astype(np.uint32))
-    off, byt, tot = eng.gen_jackson_longs_dev(0x5EED0023, B * (steps + 2))
+    off, byt, tot = eng.gen_jackson_longs_dev(0x5EED0023, B * nb)
     d_out = eng.alloc(B)
     for s in range(2):   # warm
         eng.pfadd_dev(B, d_ids.ptr + s * B * 4, off.ptr + s * B * 8, byt, tot, d_out)
-    eng.prof_reset()
-    eng.prof_enable(True)
-    eng.prof_only("pfadd,pfp_hash,pfp_apply")
+    def calls(first):
+        for s in range(first, first + steps):
+            eng.pfadd_dev(B, d_ids.ptr + s * B * 4, off.ptr + s * B * 8, byt, tot, d_out)
+    # back to back, no host waits: host-timed, and device-timed by two HIP events around the whole run
     eng.set_async(True)
-    t = timed(eng, lambda: [eng.pfadd_dev(B, d_ids.ptr + s * B * 4, off.ptr + s * B * 8, byt, tot, d_out)
-                            for s in range(2, steps + 2)])
+    eng.sync()
+    t0 = time.perf_counter()
+    eng.timer_record(0)
+    calls(2)
+    eng.timer_record(1)
+    eng.sync()
+    t = time.perf_counter() - t0
     eng.set_async(False)
+    dev_ms = eng.timer_elapsed_ms(0, 1)
+    t_sync = timed(eng, lambda: calls(2 + steps))       # each call waits for its replies
+    sync_dev = 0.0                              # ... and its device time: two HIP events around each call
+    for s_ in range(2 + 2 * steps, 2 + 3 * steps):
+        eng.timer_record(2)
+        eng.pfadd_dev(B, d_ids.ptr + s_ * B * 4, off.ptr + s_ * B * 8, byt, tot, d_out)
+        eng.timer_record(3)
+        sync_dev += eng.timer_elapsed_ms(2, 3)
+    eng.prof_reset()                            # per-kernel times (events around each launch), a separate pass
+    eng.prof_enable(True)
+    eng.prof_only("pfp_hash,pfp_apply")
+    calls(2 + 3 * steps)
+    eng.sync()
     eng.prof_enable(False)
     eng.prof_only(None)
-    n_c, ms_c = eng.prof_read("pfadd")
     k = {p: eng.prof_read(p) for p in ("pfp_hash", "pfp_apply")}
-    t_sync = timed(eng, lambda: [eng.pfadd_dev(B, d_ids.ptr + s * B * 4, off.ptr + s * B * 8, byt, tot, d_out)
-                                 for s in range(2, steps + 2)])
+    n_c, ms_c = steps, dev_ms
     line({"metric": "C2 PFADD inserts/sec, one 1M-command RBatch per device call (100k uniform tenants)",
           "value": B * steps / t, "unit": "inserts/s",
           "config": {"workload": "c2u", "batch": B, "tenants": nt, "calls": steps},
@@ -155,7 +173,9 @@ def c2u(eng, args):
           "device_ms_per_call": ms_c / n_c if n_c else None,
           "kernel_ms": {p: (v[1] / v[0] if v[0] else None) for p, v in k.items()},
           "synchronous_calls_inserts_per_s": B * steps / t_sync,
-          "note": "value: back-to-back async calls host-timed; device: HIP events around each call's PFADD chain"})
+          "synchronous_calls_device_inserts_per_s": B * steps / (sync_dev * 1e-3),
+          "note": "value: back-to-back async calls host-timed; device: two HIP events around the same run / calls; "
+                  "kernel_ms: events around each launch in a separate pass"})
 
 
 def c2zipf(eng, args):
@@ -207,6 +227,7 @@ def c2zipf(eng, args):
           "unit": "inserts/s", "config": {"workload": "c2zipf", "batch": B, "tenants": nt, "zipf_s": 1.1,
                                           "hottest_tenant_share": top},
           "synchronous_calls_inserts_per_s": B * steps / t_sync,
+          "synchronous_calls_device_inserts_per_s": B * steps / (sync_dev * 1e-3),
           "group_commit_inserts_per_s": B * G / t_g, "group_commit_kernel_ms": g_ms,
           "group_commit_device_inserts_per_s": B * G / (sum(g_ms.values()) * 1e-3) if all(g_ms.values()) else None,
           "group_commit": "%d fresh 1M batches as one call (line schedule), host-timed after a warm group" % G,

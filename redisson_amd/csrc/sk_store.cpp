@@ -409,7 +409,7 @@ struct sk_ctx {
         bool used = false;
     } pfs[2];
     int pf_par = 0;
-    bool pfp_pipe = true;
+    bool pfp_pipe = false;      // SK_PFP_PIPE=1: the next 1 M batch hashes on a second stream while one applies (round 6 A/B: 10.4 vs 11.4 G/s without, packed arena)
     bool pf_dev_call = false;   // inside sk_pfadd_dev: inputs are caller-owned device memory, no host staging
     hipStream_t st3 = nullptr;
     // Redis HLL strings byte for byte (sk_hll_exact_strings; off by default): per slab header + sparse opcodes,

@@ -431,15 +431,15 @@ def test_edge_cases(engine, O):
     assert engine.get(b"edge:none") is None
 
 
-@pytest.mark.parametrize("direct", ["1", "0"])
-def test_pfadd_paths_agree(O, direct):
+@pytest.mark.parametrize("direct,pipe", [("1", "0"), ("0", "0"), ("1", "1")])
+def test_pfadd_paths_agree(O, direct, pipe):
     """The partition path (replies stored by k_pfp_apply, or restored by k_pfp_reply) on the packed 6-bit arena gives
     the oracle's registers and replies, dense and sparse, with intra-batch collisions (neighbouring registers of one
     word rising in one batch: the packed writes are XORs on shared words) and an oversized partition bucket.  (The
     claim / commit and sorted paths of rounds 1-5 were retired with the u8 arena.)"""
     import os
     from redisson_amd import SketchEngine
-    env = {"SK_PFP_DIRECT": direct}
+    env = {"SK_PFP_DIRECT": direct, "SK_PFP_PIPE": pipe}   # pipe: device batches hashed on a second stream
     os.environ.update(env)
     try:
         e = SketchEngine(device=0)

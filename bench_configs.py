@@ -227,7 +227,6 @@ def c2zipf(eng, args):
           "unit": "inserts/s", "config": {"workload": "c2zipf", "batch": B, "tenants": nt, "zipf_s": 1.1,
                                           "hottest_tenant_share": top},
           "synchronous_calls_inserts_per_s": B * steps / t_sync,
-          "synchronous_calls_device_inserts_per_s": B * steps / (sync_dev * 1e-3),
           "group_commit_inserts_per_s": B * G / t_g, "group_commit_kernel_ms": g_ms,
           "group_commit_device_inserts_per_s": B * G / (sum(g_ms.values()) * 1e-3) if all(g_ms.values()) else None,
           "group_commit": "%d fresh 1M batches as one call (line schedule), host-timed after a warm group" % G,

@@ -139,9 +139,6 @@ __global__ void k_len_from_last_key(const uint64_t *keys, uint64_t m, uint64_t *
 #define SK_PFP_TPB 1024   // threads per hash workgroup (16 waves: one per CU hides the latency)
 #define SK_PFP_EPB 4096   // elements per hash workgroup = max blocks 256 for n <= 2^20
 #define SK_PFP_ATPB 1024  // threads per apply workgroup (4 per block segment)
-#ifndef SK_PFP_BYTEW
-#define SK_PFP_BYTEW 0    // the apply's register writes as byte stores where no neighbour shares the bytes (else XORs)
-#endif
 #define SK_PFP_CAP 4096   // records one apply workgroup holds in LDS
 #define SK_PFP_HT 4096    // LDS hash-chain heads
 #define SK_PFP_STAGE (4 * SK_STAGE_WORDS) // LDS key window (u64 words) for SK_PFP_TPB elements
@@ -752,8 +749,12 @@ __global__ void __launch_bounds__(SK_PFP_ATPB) __attribute__((amdgpu_waves_per_e
         nxt[u] = uint16_t(atomicExch(&head[pfp_ht(R[u] >> 26)], u));
     __syncthreads();
     constexpr int PER = SK_PFP_CAP / SK_PFP_ATPB;
+    uint64_t wslot[PER];
+    uint32_t wx[PER];
 #pragma unroll
     for (int q = 0; q < PER; q++) {
+        wx[q] = 0;
+        wslot[q] = 0;
         uint32_t tq = threadIdx.x + q * SK_PFP_ATPB;
         if (tq >= cnt) continue;
         uint64_t rt = R[tq], slot = rt >> 26, seq = (rt >> 6) & 0xfffffu;
@@ -776,31 +777,17 @@ __global__ void __launch_bounds__(SK_PFP_ATPB) __attribute__((amdgpu_waves_per_e
         if (reply) pfp_event(ev, ev_n, rt);
         if (changed) changed[seq] = reply; // one element per command: straight to batch order
         else r0[tq] = reply;               // the reply replaces R0 (read by this thread only)
-        if (earliest && m > R0) {
-            uint8_t *sl = slab_at(arena, slot >> 14);
-            const uint32_t r = uint32_t(slot) & 16383u;
-#if SK_PFP_BYTEW
-            // byte stores when no register sharing the field's bytes has a record in this batch (no other writer
-            // of those bytes: runs of 32 registers are 24 whole bytes, owned by this workgroup); else XORs
-            auto has = [&](uint64_t sl2) {
-                for (uint32_t v = head[pfp_ht(sl2)]; v != 0xffffu; v = nxt[v])
-                    if ((R[v] >> 26) == sl2) return true;
-                return false;
-            };
-            const bool lo_shared = (r & 3u) != 0, hi_shared = (r & 3u) != 3;
-            if (!(lo_shared && (r & 31u) != 0 && has(slot - 1)) && !(hi_shared && (r & 31u) != 31 && has(slot + 1))) {
-                const uint32_t bit = 6u * r, by = bit >> 3, sh = bit & 7u;
-                const uint32_t v16 = (uint32_t(sl[by]) | (uint32_t(sl[by + 1]) << 8)) ^ ((R0 ^ m) << sh);
-                sl[by] = uint8_t(v16);
-                if (sh > 2u) sl[by + 1] = uint8_t(v16 >> 8);
-            } else {
-                reg_xor(sl, r, R0 ^ m);
-            }
-#else
-            reg_xor(sl, r, R0 ^ m);
-#endif
+        if (earliest && m > R0) {          // the slot's one writer: register R0 -> m
+            wslot[q] = slot;
+            wx[q] = R0 ^ m;
         }
     }
+    // the slots' writes: device-scope XORs on the fields' words (neighbouring slots share words; XORs commute).
+    // Merging them per word in LDS and storing whole words was slower: apply 82.8 vs 74.1 us per 1 M (C2, one RBatch
+    // per call, profiles/r06_ab/r06k_ab_*)
+#pragma unroll
+    for (int q = 0; q < PER; q++)
+        if (wx[q]) reg_xor(slab_at(arena, wslot[q] >> 14), uint32_t(wslot[q]) & 16383u, wx[q]);
     if (changed) return;
     __syncthreads();
     uint8_t *rs = rep + uint64_t(j) * SK_PFP_EPB + lo; // replies as runs, in the chunk's order
@@ -1595,53 +1582,68 @@ __device__ __forceinline__ uint4 ld_nt(const uint4 *p) {
 }
 
 // -------------------------------------------------------------- exact register sums (PFCOUNT, redis 3.x)
-// The 3.x estimator needs only E = sum 2^-r[j] and the zero count (hllDenseSum).  With every register <= 39 each
-// partial sum of E is exact in double (multiples of 2^-39 below 2^14: 53 significant bits), so E summed in any order
-// -- and S = E * 2^40, an integer < 2^55 -- is bit-identical to Redis's sum.  One wave per key, no LDS: a lane sums
-// 256 registers (16 packed 12-B groups in flight), reading each 6-bit field straight from the packed words (one bit
-// field extract; two fields of a group straddle words), then 2^-r by v_ldexp_f64 and one f64 add; the wave reduces
-// with shuffles.  out[2k] = S, out[2k + 1] = zeros | (a register >= 40) << 32: the host then takes Redis's
-// register-order sum instead (S is not used).
+// The 3.x estimator needs only E = sum 2^-r[j] and the zero count (hllDenseSum).  With every register <= 39,
+// S = E * 2^40 = sum 2^(40 - r[j]) is an integer < 2^55, and the host's E = S * 2^-40 is bit-identical to Redis's
+// register-order double sum (every partial sum is a multiple of 2^-39 below 2^14: exact in 53 bits).
+// One wave per key, 12 fully coalesced 16-B loads per lane: lane l holds chunks c = it * 64 + l of the 12,288-B body.
+// Chunk c holds the registers whose 6-bit fields start in its bits: 22 of them when c % 3 == 0 (the 22nd straddles
+// into chunk c + 1, whose first word comes from the next lane, or for lane 63 from lane 0's next chunk), else 21
+// starting 4 (c % 3 == 1) or 2 (c % 3 == 2) bits in.  Registers are taken two at a time: the 12-bit pair indexes a
+// 4,160-entry u64 table in LDS (built by each workgroup once) holding 2^(40 - a) + 2^(40 - b) in bits [0, 48), the
+// pair's zero count at bit 48 and its count of registers >= 40 at bit 56 (entries 4096 + r: one register, the odd
+// one of a 21-register chunk).  So a pair costs one extract, one LDS read and one 64-bit add.  Two accumulators (even
+// and odd chunks, <= 132 registers each) keep the three fields from carrying into each other.
+// out[2k] = S (0 when a register is >= 40), out[2k + 1] = zeros | (a register >= 40) << 32: the host then takes
+// Redis's register-order sum instead.
+#define SK_SUM_LUT (4096 + 64)
+__device__ __forceinline__ uint64_t sum_term(uint32_t r) {
+    return (r < 40u ? (1ull << (40u - r)) : 0ull) + (uint64_t(r == 0u) << 48) + (uint64_t(r >= 40u) << 56);
+}
 __global__ void __launch_bounds__(256) k_hll_sum(uint64_t n, const uint32_t *__restrict__ ids,
                                                  const uint8_t *__restrict__ arena, uint64_t *__restrict__ out) {
-    const uint32_t lane = threadIdx.x & 63u;
+    __shared__ uint64_t lut[SK_SUM_LUT];
+    for (uint32_t i = threadIdx.x; i < SK_SUM_LUT; i += 256)
+        lut[i] = i < 4096u ? sum_term(i & 63u) + sum_term(i >> 6) : sum_term(i - 4096u);
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63u, l3 = lane % 3u;
     for (uint64_t key = uint64_t(blockIdx.x) * 4 + (threadIdx.x >> 6); key < n; key += uint64_t(gridDim.x) * 4) {
-        // the key's 1024 packed groups (12 B = 16 registers): a lane reads groups it * 64 + lane, 16 in flight
-        const uint32_t *base = reinterpret_cast<const uint32_t *>(slab_at(arena, slab_of(ids[key])));
-        uint32_t v[16][3];
+        const uint4 *base = reinterpret_cast<const uint4 *>(slab_at(arena, slab_of(ids[key])));
+        uint4 v[12];
 #pragma unroll
-        for (int it = 0; it < 16; it++)
+        for (int it = 0; it < 12; it++) v[it] = ld_nt(base + it * 64 + lane);
+        uint64_t acc[2] = {0ull, 0ull};
 #pragma unroll
-            for (int q = 0; q < 3; q++) v[it][q] = __builtin_nontemporal_load(base + 3 * (it * 64 + lane) + q);
-        double E = 0.0;
-        uint32_t zeros = 0, rmax = 0;
+        for (int it = 0; it < 12; it++) {
+            const uint32_t m3 = (uint32_t(it) + l3) % 3u; // chunk % 3 (64 = 1 mod 3)
+            const uint32_t o = m3 == 0u ? 0u : (m3 == 1u ? 4u : 2u);
+            const uint32_t nx_same = uint32_t(__shfl(int(v[it].x), int((lane + 1u) & 63u)));
+            const uint32_t nx_next = it + 1 < 12 ? __builtin_amdgcn_readfirstlane(v[it + 1 < 12 ? it + 1 : it].x) : 0u;
+            const uint32_t w4 = lane == 63u ? nx_next : nx_same;
+            // the chunk's 160-bit window shifted so that its first register starts at bit 0
+            const uint32_t s[5] = {__builtin_amdgcn_alignbit(v[it].y, v[it].x, o),
+                                   __builtin_amdgcn_alignbit(v[it].z, v[it].y, o),
+                                   __builtin_amdgcn_alignbit(v[it].w, v[it].z, o),
+                                   __builtin_amdgcn_alignbit(w4, v[it].w, o), w4 >> o};
 #pragma unroll
-        for (int it = 0; it < 16; it++) {
-            const uint32_t w0 = v[it][0], w1 = v[it][1], w2 = v[it][2];
-#pragma unroll
-            for (int j = 0; j < 16; j++) { // register j of the group: bits [6j, 6j + 6) of w0 | w1 << 32 | w2 << 64
-                const int bit = 6 * j;
-                uint32_t r;
-                if (bit + 6 <= 32) r = (w0 >> bit) & 63u;
-                else if (bit < 32) r = __builtin_amdgcn_alignbit(w1, w0, bit) & 63u;
-                else if (bit + 6 <= 64) r = (w1 >> (bit - 32)) & 63u;
-                else if (bit < 64) r = __builtin_amdgcn_alignbit(w2, w1, bit - 32) & 63u;
-                else r = (w2 >> (bit - 64)) & 63u;
-                zeros += r == 0u ? 1u : 0u;
-                rmax = r > rmax ? r : rmax;
-                E += __builtin_amdgcn_ldexp(1.0, -int(r));
+            for (int p = 0; p < 11; p++) {
+                const int bit = 12 * p, q = bit >> 5, sh = bit & 31;
+                uint32_t x = (sh <= 20 ? (s[q] >> sh) : __builtin_amdgcn_alignbit(s[q + 1], s[q], sh)) & 0xfffu;
+                if (p == 10) x = o == 0u ? x : 4096u + (x & 63u); // register 20 alone
+                acc[it & 1] += lut[x];
             }
         }
+        uint64_t S = (acc[0] & 0xffffffffffffull) + (acc[1] & 0xffffffffffffull);
+        uint32_t zeros = uint32_t((acc[0] >> 48) & 255u) + uint32_t((acc[1] >> 48) & 255u);
+        uint32_t big = uint32_t(acc[0] >> 56) + uint32_t(acc[1] >> 56);
 #pragma unroll
         for (int o = 32; o; o >>= 1) {
-            E += __shfl_xor(E, o);
+            S += __shfl_xor(S, o);
             zeros += __shfl_xor(zeros, o);
-            const uint32_t m = __shfl_xor(rmax, o);
-            rmax = m > rmax ? m : rmax;
+            big += __shfl_xor(big, o);
         }
         if (lane == 0) {
-            out[2 * key] = rmax < 40u ? uint64_t(E * 1099511627776.0) : 0ull; // E * 2^40, exact below 40
-            out[2 * key + 1] = uint64_t(zeros) | (uint64_t(rmax >= 40u ? 1u : 0u) << 32);
+            out[2 * key] = big ? 0ull : S;
+            out[2 * key + 1] = uint64_t(zeros) | (uint64_t(big ? 1u : 0u) << 32);
         }
     }
 }
@@ -4435,7 +4437,7 @@ hipError_t sort_pairs64(hipStream_t st, void *tmp, size_t tmp_bytes, const uint6
 
 hipError_t launch_hll_sum(hipStream_t st, uint64_t n, const uint32_t *ids, const uint8_t *arena, uint64_t *out) {
     if (!n) return hipSuccess;
-    hipLaunchKernelGGL(k_hll_sum, dim3(grid_for((n + 3) / 4, 1, 4096)), dim3(256), 0, st, n, ids, arena, out);
+    hipLaunchKernelGGL(k_hll_sum, dim3(grid_for((n + 3) / 4, 1, 1024)), dim3(256), 0, st, n, ids, arena, out);
     SK_LAUNCH_CHECK();
     return hipSuccess;
 }

@@ -1659,14 +1659,18 @@ __global__ void __launch_bounds__(256) k_hll_sum(uint64_t n, const uint32_t *__r
 // LDS array 39 % busy, VALU 27 % (profiles/r03j_hist_sq_summary.json).
 // PK: slabs ids[k] of the packed arena; else u8 register arrays (ids[k] = 0 with the array as `arena`: a union's
 // temporary registers, sk_hll_count_registers_dev)
+#ifndef SK_HH16
+#define SK_HH16 1 // 16-bit counters, two bins per LDS word: 8 KiB per wave, 20 waves per CU instead of 10
+#endif
 template <bool PK>
 __global__ void __launch_bounds__(64) k_hll_hist(uint64_t n, const uint32_t *__restrict__ ids,
                                                    const uint8_t *__restrict__ arena, uint32_t *__restrict__ hist) {
-    __shared__ uint4 h4[64 * 16];
+    constexpr int ROWS = SK_HH16 ? 32 : 64; // SK_HH16: bins 2i and 2i + 1 as the halves of row i's words
+    __shared__ uint4 h4[ROWS * 16];
     uint32_t *h = reinterpret_cast<uint32_t *>(h4);
     const uint32_t lane = threadIdx.x;
 #pragma unroll
-    for (int j = 0; j < 16; j++) h4[lane + 64 * j] = make_uint4(0, 0, 0, 0);
+    for (int j = 0; j < ROWS / 4; j++) h4[lane + 64 * j] = make_uint4(0, 0, 0, 0);
     // a lane's 16 groups of 16 registers: groups it * 64 + lane (packed: three words each; u8: one 16-B vector)
     auto load = [&](uint64_t key, uint32_t (&v)[16][4]) {
         if constexpr (PK) {
@@ -1694,19 +1698,38 @@ __global__ void __launch_bounds__(64) k_hll_hist(uint64_t n, const uint32_t *__r
 #pragma unroll
             for (int w = 0; w < 4; w++)
 #pragma unroll
-                for (int b = 0; b < 4; b++)
-                    __hip_atomic_fetch_add(&h[((ws[w] >> (8 * b)) & 63u) * 64 + lane], 1u, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_WAVEFRONT);
+                for (int b = 0; b < 4; b++) {
+                    const uint32_t r = (ws[w] >> (8 * b)) & 63u;
+                    if (SK_HH16)
+                        __hip_atomic_fetch_add(&h[(r >> 1) * 64 + lane], 1u << ((r & 1u) << 4), __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_WAVEFRONT);
+                    else
+                        __hip_atomic_fetch_add(&h[r * 64 + lane], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+                }
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
         __builtin_amdgcn_wave_barrier();
         uint32_t c = 0;
+        if (SK_HH16) {
+            // lanes 2i and 2i + 1 sum the two halves of row i (64 lanes x <= 256 registers per bin: no carry out of
+            // a 16-bit half), then add each other's: bin 2i in the low half, 2i + 1 in the high half
 #pragma unroll
-        for (int j = 0; j < 16; j++) {
-            const uint32_t q = lane * 16 + ((j + lane) & 15u);
-            const uint4 x = h4[q];
-            c += x.x + x.y + x.z + x.w;
-            h4[q] = make_uint4(0, 0, 0, 0);
+            for (int j = 0; j < 8; j++) {
+                const uint32_t q = (lane >> 1) * 16 + (lane & 1u) * 8 + ((j + (lane >> 1)) & 7u);
+                const uint4 x = h4[q];
+                c += x.x + x.y + x.z + x.w;
+                h4[q] = make_uint4(0, 0, 0, 0);
+            }
+            c += __shfl_xor(c, 1);
+            c = (lane & 1u) ? c >> 16 : c & 0xffffu;
+        } else {
+#pragma unroll
+            for (int j = 0; j < 16; j++) {
+                const uint32_t q = lane * 16 + ((j + lane) & 15u);
+                const uint4 x = h4[q];
+                c += x.x + x.y + x.z + x.w;
+                h4[q] = make_uint4(0, 0, 0, 0);
+            }
         }
         hist[key * 64 + lane] = c;
     };

@@ -1761,6 +1761,15 @@ __device__ __forceinline__ uint4 bytemax4(uint4 a, uint4 b) {
 // [g*per, (g+1)*per) and writes partial[g] as u8 registers.  Sources are slabs ids[k] of the packed arena (PK: 12-B
 // groups, unpacked in registers), or consecutive u8 register arrays of 16 KiB (ids == null: the form the next tree
 // level reads; or one caller array, sk_hll_merge_registers_dev).
+// PK keeps the running max as 8 pairs of u16 lanes (registers 2j, 2j + 1 of the group: one v_pk_max_u16 each), each
+// source's 12 bytes going straight into that form (two field extracts and a shift-or per pair), and converts to u8 once
+__device__ __forceinline__ void grp_pairs(uint32_t w0, uint32_t w1, uint32_t w2, us2 (&p)[8]) {
+    const uint32_t x[8] = {w0, w0 >> 12, __builtin_amdgcn_alignbit(w1, w0, 24), w1 >> 4,
+                           w1 >> 16, __builtin_amdgcn_alignbit(w2, w1, 28), w2 >> 8, w2 >> 20};
+#pragma unroll
+    for (int j = 0; j < 8; j++)
+        p[j] = __builtin_bit_cast(us2, (x[j] & 63u) | (((x[j] >> 6) & 63u) << 16));
+}
 template <bool PK>
 __global__ void __launch_bounds__(256) k_hll_union_partial(uint64_t n, const uint32_t *__restrict__ ids,
                                                            const uint8_t *__restrict__ base, uint64_t per,
@@ -1768,31 +1777,67 @@ __global__ void __launch_bounds__(256) k_hll_union_partial(uint64_t n, const uin
     unsigned lane16 = blockIdx.x * 256 + threadIdx.x; // group of 16 registers within the key
     uint64_t g = blockIdx.y, k0 = g * per, k1 = k0 + per;
     if (k1 > n) k1 = n;
-    uint4 acc = make_uint4(0, 0, 0, 0);
     uint64_t k = k0;
     // the next step's slab ids are loaded while this step's 8 vectors are in flight (the id loads used to sit in
     // front of every step's vector loads)
     auto idof = [&](uint64_t kk) -> uint64_t { return ids ? slab_of(ids[kk]) : kk; };
-    auto ld = [&](uint64_t id) -> uint4 {
-        if constexpr (PK) return grp_load_nt(slab_at(base, id), lane16);
-        else return ld_nt(reinterpret_cast<const uint4 *>(base + (id << 14)) + lane16);
-    };
     uint64_t idn[8];
     if (k + 8 <= k1)
 #pragma unroll
         for (int j = 0; j < 8; j++) idn[j] = idof(k + j);
-    for (; k + 8 <= k1; k += 8) { // 8 independent loads in flight per lane
-        uint4 a[8];
+    if constexpr (PK) {
+        us2 acc[8];
 #pragma unroll
-        for (int j = 0; j < 8; j++) a[j] = ld(idn[j]);
-        if (k + 16 <= k1)
+        for (int j = 0; j < 8; j++) acc[j] = us2{0, 0};
+        auto fold = [&](uint32_t w0, uint32_t w1, uint32_t w2) {
+            us2 p[8];
+            grp_pairs(w0, w1, w2, p);
 #pragma unroll
-            for (int j = 0; j < 8; j++) idn[j] = idof(k + 8 + j);
-        acc = bytemax4(acc, bytemax4(bytemax4(bytemax4(a[0], a[1]), bytemax4(a[2], a[3])),
-                                     bytemax4(bytemax4(a[4], a[5]), bytemax4(a[6], a[7]))));
+            for (int j = 0; j < 8; j++) acc[j] = __builtin_elementwise_max(acc[j], p[j]);
+        };
+        auto wp = [&](uint64_t id) { return reinterpret_cast<const uint32_t *>(slab_at(base, id)) + 3 * lane16; };
+        for (; k + 8 <= k1; k += 8) { // 8 independent groups in flight per lane
+            uint32_t a[8][3];
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                const uint32_t *w = wp(idn[j]);
+                a[j][0] = __builtin_nontemporal_load(w);
+                a[j][1] = __builtin_nontemporal_load(w + 1);
+                a[j][2] = __builtin_nontemporal_load(w + 2);
+            }
+            if (k + 16 <= k1)
+#pragma unroll
+                for (int j = 0; j < 8; j++) idn[j] = idof(k + 8 + j);
+#pragma unroll
+            for (int j = 0; j < 8; j++) fold(a[j][0], a[j][1], a[j][2]);
+        }
+        for (; k < k1; k++) {
+            const uint32_t *w = wp(idof(k));
+            fold(__builtin_nontemporal_load(w), __builtin_nontemporal_load(w + 1), __builtin_nontemporal_load(w + 2));
+        }
+        uint32_t o[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) { // bytes 0 and 2 of pair 2q (registers 4q, 4q + 1), then of pair 2q + 1
+            const uint32_t lo = __builtin_bit_cast(uint32_t, acc[2 * q]), hi = __builtin_bit_cast(uint32_t, acc[2 * q + 1]);
+            o[q] = __builtin_amdgcn_perm(hi, lo, 0x06040200u);
+        }
+        reinterpret_cast<uint4 *>(partial + g * 16384)[lane16] = make_uint4(o[0], o[1], o[2], o[3]);
+    } else {
+        uint4 acc = make_uint4(0, 0, 0, 0);
+        auto ld = [&](uint64_t id) -> uint4 { return ld_nt(reinterpret_cast<const uint4 *>(base + (id << 14)) + lane16); };
+        for (; k + 8 <= k1; k += 8) { // 8 independent loads in flight per lane
+            uint4 a[8];
+#pragma unroll
+            for (int j = 0; j < 8; j++) a[j] = ld(idn[j]);
+            if (k + 16 <= k1)
+#pragma unroll
+                for (int j = 0; j < 8; j++) idn[j] = idof(k + 8 + j);
+            acc = bytemax4(acc, bytemax4(bytemax4(bytemax4(a[0], a[1]), bytemax4(a[2], a[3])),
+                                         bytemax4(bytemax4(a[4], a[5]), bytemax4(a[6], a[7]))));
+        }
+        for (; k < k1; k++) acc = bytemax4(acc, ld(idof(k)));
+        reinterpret_cast<uint4 *>(partial + g * 16384)[lane16] = acc;
     }
-    for (; k < k1; k++) acc = bytemax4(acc, ld(idof(k)));
-    reinterpret_cast<uint4 *>(partial + g * 16384)[lane16] = acc;
 }
 
 // out = max(include_out ? out : 0, partial[0..G)) for a small G (the tree root); PKOUT: out is a packed slab (the
@@ -1803,7 +1848,16 @@ __global__ void __launch_bounds__(256) k_hll_union_final(uint64_t G, const uint8
     unsigned lane16 = blockIdx.x * 256 + threadIdx.x;
     uint4 acc = make_uint4(0, 0, 0, 0);
     if (include_out) acc = PKOUT ? grp_load(out, lane16) : reinterpret_cast<const uint4 *>(out)[lane16];
-    for (uint64_t g = 0; g < G; g++) acc = bytemax4(acc, reinterpret_cast<const uint4 *>(partial + g * 16384)[lane16]);
+    const uint4 *pp = reinterpret_cast<const uint4 *>(partial) + lane16;
+    uint64_t g = 0;
+    for (; g + 8 <= G; g += 8) { // 8 partials in flight (one at a time took 12 us for 31 partials at C4)
+        uint4 a[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) a[j] = pp[(g + j) * 1024];
+        acc = bytemax4(acc, bytemax4(bytemax4(bytemax4(a[0], a[1]), bytemax4(a[2], a[3])),
+                                     bytemax4(bytemax4(a[4], a[5]), bytemax4(a[6], a[7]))));
+    }
+    for (; g < G; g++) acc = bytemax4(acc, pp[g * 1024]);
     if (PKOUT) grp_store(out, lane16, acc);
     else reinterpret_cast<uint4 *>(out)[lane16] = acc;
 }

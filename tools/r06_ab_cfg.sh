@@ -6,9 +6,9 @@ T=$1; VARS=$2; CF=${3:-c1,c2zipf}
 R=$(pwd); O=$R/gpurun_out/$T; mkdir -p $O
 for rep in 1 2; do
   for v in $VARS; do
-    E=""  # "e_NAME=VALUE": the base build with that environment setting
+    E=""  # "e_NAME=VALUE[+NAME2=VALUE2]": the base build with those environment settings
     if [ "$v" = base ]; then L=$R/redisson_amd/libredisson_sketch.so
-    elif [ "${v#e_}" != "$v" ]; then L=$R/redisson_amd/libredisson_sketch.so; E=${v#e_}
+    elif [ "${v#e_}" != "$v" ]; then L=$R/redisson_amd/libredisson_sketch.so; E=${v#e_}; E=${E//+/ }
     else L=$R/redisson_amd/var_$v.so; fi
     env $E SK_LIB_PATH=$L timeout -k 10 300 python3 -u bench_configs.py --configs $CF > $O/$v.$rep.jsonl 2> $O/$v.$rep.err || { echo "$v failed"; tail $O/$v.$rep.err; exit 1; }
     python3 - $O/$v.$rep.jsonl $v <<'PY'

@@ -135,7 +135,9 @@ __global__ void k_len_from_last_key(const uint64_t *keys, uint64_t m, uint64_t *
 //   rec = slot << 26 | seq << 6 | rho   (slot <= 38 bits, seq < 2^20)
 // Buckets larger than SK_PFP_CAP (hot registers, skew) are resolved by the
 // same workgroup from a (slot, rho) -> min seq table (pfp_big_resolve).
+#ifndef SK_PFP_NB
 #define SK_PFP_NB 512     // buckets (~n/512 records each; ~8 records = one 64-B line per block segment)
+#endif
 #define SK_PFP_TPB 1024   // threads per hash workgroup (16 waves: one per CU hides the latency)
 #define SK_PFP_EPB 4096   // elements per hash workgroup = max blocks 256 for n <= 2^20
 #define SK_PFP_ATPB 1024  // threads per apply workgroup (4 per block segment)
@@ -149,10 +151,11 @@ static_assert(SK_PFP_CAP < 0xffff, "u16 chain links");
 // bucket then read their registers from one 32-B piece, so a wave's register loads coalesce into one request.
 // Run g of sketch s goes to bucket (g + hash(s)) % 512: the 512 runs of every sketch cover the 512 buckets once
 // each (one hot sketch fills every bucket evenly), and sketches are rotated against each other.
-static_assert(SK_PFP_NB == 512, "16384 registers = 512 runs of 32");
+static_assert(SK_PFP_NB == 512 || SK_PFP_NB == 1024, "16384 registers = 512 runs of 32 (or 1024 of 16)");
 __device__ __forceinline__ uint32_t pfp_bucket(uint64_t slot) {
-    const uint32_t run = uint32_t(slot >> 5) & 511u, rot = (uint32_t(slot >> 14) * 0x9E3779B1u) >> 23;
-    return (run + rot) & 511u;
+    constexpr uint32_t LNB = SK_PFP_NB == 512 ? 9 : 10, RB = 14 - LNB;
+    const uint32_t run = uint32_t(slot >> RB) & (SK_PFP_NB - 1u), rot = (uint32_t(slot >> 14) * 0x9E3779B1u) >> (32 - LNB);
+    return (run + rot) & (SK_PFP_NB - 1u);
 }
 __device__ __forceinline__ uint32_t pfp_ht(uint64_t slot) {
     return uint32_t((slot * 0xC2B2AE3D27D4EB4Full) >> 52); // 12 bits

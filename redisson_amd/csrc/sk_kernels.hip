@@ -139,12 +139,17 @@ __global__ void k_len_from_last_key(const uint64_t *keys, uint64_t m, uint64_t *
 #define SK_PFP_NB 512     // buckets (~n/512 records each; ~8 records = one 64-B line per block segment)
 #endif
 #define SK_PFP_TPB 1024   // threads per hash workgroup (16 waves: one per CU hides the latency)
-#define SK_PFP_EPB 4096   // elements per hash workgroup = max blocks 256 for n <= 2^20
+#define SK_PFP_EPB 4096   // elements per line-schedule hash workgroup (12-bit element-in-block)
+#ifndef SK_PFQ_EPB
+#define SK_PFQ_EPB 4096   // elements per partition-path hash workgroup (2048, two per CU: slower, r06s)
+#endif
+#define SK_PFQ_TPS (SK_PFP_ATPB * SK_PFQ_EPB >> 20) // apply threads per hash block (n <= 2^20)
 #define SK_PFP_ATPB 1024  // threads per apply workgroup (4 per block segment)
 #define SK_PFP_CAP 4096   // records one apply workgroup holds in LDS
 #define SK_PFP_HT 4096    // LDS hash-chain heads
 #define SK_PFP_STAGE (4 * SK_STAGE_WORDS) // LDS key window (u64 words) for SK_PFP_TPB elements
-static_assert(SK_PFP_ATPB / 4 * SK_PFP_EPB >= (1 << 20), "4 apply threads per hash block");
+static_assert(SK_PFQ_TPS >= 1 && (SK_PFQ_TPS & (SK_PFQ_TPS - 1)) == 0 && SK_PFQ_TPS <= 64 &&
+              SK_PFP_ATPB / SK_PFQ_TPS * SK_PFQ_EPB >= (1 << 20), "apply threads per hash block");
 static_assert(SK_PFP_NB <= SK_PFP_TPB, "one bucket per hash thread in the start scan");
 static_assert(SK_PFP_CAP < 0xffff, "u16 chain links");
 // a bucket takes whole runs of 32 registers of a sketch: the records of a hot sketch (C1, a Zipf head) in one
@@ -262,7 +267,7 @@ struct PflChunk {
 
 // NBK buckets; LINE = false: the partition path (records slot << 26 | seq << 6 | rho, pfp_bucket),
 // LINE = true: the line schedule (records slab << 32 | reg << 18 | rho << 12 | element-in-block, pfl_bucket)
-template <int NBK, bool LINE>
+template <int NBK, bool LINE, int EPB>
 __device__ __forceinline__ void pfp_hash_impl(uint64_t n, const uint32_t *__restrict__ key_ids,
                                               const uint64_t *__restrict__ off, const uint8_t *__restrict__ bytes,
                                               int v5, uint64_t *__restrict__ chunks, uint32_t *__restrict__ S,
@@ -270,18 +275,23 @@ __device__ __forceinline__ void pfp_hash_impl(uint64_t n, const uint32_t *__rest
                                               uint32_t *__restrict__ big_alloc, const uint64_t *__restrict__ pre_h) {
     // the block's records reuse the key windows' LDS once the last round is hashed: 98 KiB in all, so a hash
     // workgroup (the next batch, on the third stream) fits on a CU beside an apply workgroup (61.5 KiB)
-    __shared__ uint32_t h[NBK];
-    __shared__ uint32_t wsum[SK_PFP_TPB / 64];
+    // bucket counts and starts as u16 (<= EPB): counted with u32 adds on the pairs' words; the scan's wave sums sit
+    // at the end of the second key window (free once the last round is hashed).  80 KiB in all: two hash workgroups
+    // per CU.
+    __shared__ uint32_t h32[NBK / 2];
     __shared__ uint64_t win[2][SK_PFP_WIN];
-    static_assert(SK_PFP_EPB <= 2 * SK_PFP_WIN, "records fit the windows");
+    static_assert(EPB <= 2 * SK_PFP_WIN && EPB <= 0xffff && NBK % 2 == 0, "records fit the windows");
+    uint16_t *h = reinterpret_cast<uint16_t *>(h32);
+    uint32_t *wsum = reinterpret_cast<uint32_t *>(&win[1][SK_PFP_WIN - SK_PFP_TPB / 128]);
+    static_assert(EPB * 8 <= SK_PFP_WIN * 8 * 2 - SK_PFP_TPB / 16, "records clear of the wave sums");
     uint64_t *lrec = &win[0][0];
-    for (uint32_t b = threadIdx.x; b < NBK; b += SK_PFP_TPB) h[b] = 0;
+    for (uint32_t b = threadIdx.x; b < NBK / 2; b += SK_PFP_TPB) h32[b] = 0;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         big_alloc[0] = 0;
         if (LINE) big_alloc[1] = big_alloc[2] = 0; // the line plan's heavy / light counters
     }
-    constexpr int PER = SK_PFP_EPB / SK_PFP_TPB;
-    const uint64_t base = uint64_t(blockIdx.x) * SK_PFP_EPB;
+    constexpr int PER = EPB / SK_PFP_TPB;
+    const uint64_t base = uint64_t(blockIdx.x) * EPB;
     const uint64_t rounds = (n - base + SK_PFP_TPB - 1) / SK_PFP_TPB;
     const int nr = rounds < PER ? int(rounds) : PER;
     uint64_t wb[PER + 1], oa[PER], ob[PER];
@@ -335,7 +345,8 @@ __device__ __forceinline__ void pfp_hash_impl(uint64_t n, const uint32_t *__rest
                 r[e] = (slot << 26) | (i << 6) | rho;
                 bk[e] = pfp_bucket(slot);
             }
-            rk[e] = atomicAdd(&h[bk[e]], 1u);
+            const uint32_t hs = (bk[e] & 1u) << 4;
+            rk[e] = (atomicAdd(&h32[bk[e] >> 1], 1u << hs) >> hs) & 0xffffu;
         }
         if (pre) pfp_win_store(wb[e + 1], wb[e + 2], v, win[(e + 1) & 1]);
         __syncthreads(); // window e+1 staged; window e free for round e+2
@@ -358,7 +369,7 @@ __device__ __forceinline__ void pfp_hash_impl(uint64_t n, const uint32_t *__rest
         }
     __syncthreads();
     if (LINE && SK_PFL_C6) {
-        const PflChunk ch{chunks, uint64_t(nblocks) * SK_PFP_EPB};
+        const PflChunk ch{chunks, uint64_t(nblocks) * EPB};
         for (uint32_t t = threadIdx.x; t < tot; t += SK_PFP_TPB) ch.put(base + t, lrec[t]);
         return;
     }
@@ -373,14 +384,14 @@ __global__ void __launch_bounds__(SK_PFP_TPB) k_pfp_hash(uint64_t n, const uint3
                                                          uint32_t nblocks, uint16_t *__restrict__ pos,
                                                          uint32_t *__restrict__ big_alloc,
                                                          const uint64_t *__restrict__ pre_h) {
-    pfp_hash_impl<SK_PFP_NB, false>(n, key_ids, off, bytes, v5, chunks, S, nblocks, pos, big_alloc, pre_h);
+    pfp_hash_impl<SK_PFP_NB, false, SK_PFQ_EPB>(n, key_ids, off, bytes, v5, chunks, S, nblocks, pos, big_alloc, pre_h);
 }
 __global__ void __launch_bounds__(SK_PFP_TPB) k_pfl_hash(uint64_t n, const uint32_t *__restrict__ key_ids,
                                                          const uint64_t *__restrict__ off,
                                                          const uint8_t *__restrict__ bytes, int v5,
                                                          uint64_t *__restrict__ chunks, uint32_t *__restrict__ S,
                                                          uint32_t nblocks, uint32_t *__restrict__ big_alloc) {
-    pfp_hash_impl<SK_PFL_NB, true>(n, key_ids, off, bytes, v5, chunks, S, nblocks, nullptr, big_alloc, nullptr);
+    pfp_hash_impl<SK_PFL_NB, true, SK_PFP_EPB>(n, key_ids, off, bytes, v5, chunks, S, nblocks, nullptr, big_alloc, nullptr);
 }
 
 // Replies back to batch order: rep holds them in chunk order (written by
@@ -389,9 +400,9 @@ __global__ void __launch_bounds__(SK_PFP_TPB) k_pfp_reply(uint64_t n, const uint
                                                           const uint16_t *__restrict__ pos,
                                                           const uint32_t *__restrict__ cmd_of,
                                                           uint8_t *__restrict__ changed) {
-    __shared__ uint8_t lr[SK_PFP_EPB];
-    const uint64_t base = uint64_t(blockIdx.x) * SK_PFP_EPB;
-    const uint32_t m = uint32_t(n - base < SK_PFP_EPB ? n - base : SK_PFP_EPB);
+    __shared__ uint8_t lr[SK_PFQ_EPB];
+    const uint64_t base = uint64_t(blockIdx.x) * SK_PFQ_EPB;
+    const uint32_t m = uint32_t(n - base < SK_PFQ_EPB ? n - base : SK_PFQ_EPB);
     for (uint32_t t = threadIdx.x; t < m; t += SK_PFP_TPB) lr[t] = rep[base + t];
     __syncthreads();
     for (uint32_t t = threadIdx.x; t < m; t += SK_PFP_TPB) {
@@ -664,13 +675,13 @@ __device__ void pfp_big_resolve(const uint64_t *seg, uint32_t t0, uint32_t seg_c
     for (uint32_t s = threadIdx.x; s < T.S; s += blockDim.x) T.gk[s] = SK_BIG_EMPTY, T.gv[s] = 0xffffffffu;
     __threadfence();
     __syncthreads();
-    for (uint32_t t = t0; t < seg_cnt; t += 4) {
+    for (uint32_t t = t0; t < seg_cnt; t += SK_PFQ_TPS) {
         uint64_t r = seg[t];
         T.insert(((r >> 26) << 6) | (r & 63u), uint32_t((r >> 6) & 0xfffffu));
     }
     __threadfence();
     __syncthreads();
-    for (uint32_t t = t0; t < seg_cnt; t += 4) { // replies (the arena is only read)
+    for (uint32_t t = t0; t < seg_cnt; t += SK_PFQ_TPS) { // replies (the arena is only read)
         uint64_t r = seg[t], slot = r >> 26;
         uint32_t rho = uint32_t(r & 63u), seq = uint32_t((r >> 6) & 0xfffffu);
         bool first = rho > reg_get(slab_at(arena, slot >> 14), uint32_t(slot) & 16383u);
@@ -681,7 +692,7 @@ __device__ void pfp_big_resolve(const uint64_t *seg, uint32_t t0, uint32_t seg_c
         else rep_seg[t] = first ? 1 : 0;
     }
     __syncthreads();
-    for (uint32_t t = t0; t < seg_cnt; t += 4) { // the slot's writer
+    for (uint32_t t = t0; t < seg_cnt; t += SK_PFQ_TPS) { // the slot's writer
         uint64_t r = seg[t], slot = r >> 26;
         uint32_t rho = uint32_t(r & 63u), seq = uint32_t((r >> 6) & 0xfffffu);
         if (T.find((slot << 6) | rho) != seq) continue;
@@ -715,7 +726,7 @@ __global__ void __launch_bounds__(SK_PFP_ATPB) __attribute__((amdgpu_waves_per_e
     uint16_t *nxt = reinterpret_cast<uint16_t *>(R + SK_PFP_CAP);
     uint32_t *head = reinterpret_cast<uint32_t *>(nxt + SK_PFP_CAP);
     uint8_t *r0 = reinterpret_cast<uint8_t *>(head + SK_PFP_HT);
-    uint32_t b = blockIdx.x, j = threadIdx.x >> 2, sub = threadIdx.x & 3u;
+    uint32_t b = blockIdx.x, j = threadIdx.x / SK_PFQ_TPS, sub = threadIdx.x % SK_PFQ_TPS;
     uint32_t lo = 0, c = 0;
     if (j < nblocks) {
         lo = S[uint64_t(b) * nblocks + j];
@@ -723,24 +734,24 @@ __global__ void __launch_bounds__(SK_PFP_ATPB) __attribute__((amdgpu_waves_per_e
     }
     uint32_t cnt;
     uint32_t dst = block_exscan<SK_PFP_ATPB>(sub ? 0u : c, wsum, &cnt);
-    dst = __shfl(dst, int((threadIdx.x & 63u) & ~3u)); // the group's start (from its sub 0 lane)
+    dst = __shfl(dst, int((threadIdx.x & 63u) & ~(SK_PFQ_TPS - 1u))); // the group's start (from its sub 0 lane)
     if (cnt == 0) return; // uniform
-    const uint64_t *seg = chunks + uint64_t(j) * SK_PFP_EPB + lo;
+    const uint64_t *seg = chunks + uint64_t(j) * SK_PFQ_EPB + lo;
     if (cnt > SK_PFP_CAP) {
         pfp_big_resolve(seg, sub, c, cnt, smem, big_alloc, big_keys, big_vals, arena,
-                        rep + uint64_t(j) * SK_PFP_EPB + lo, changed, ev, ev_n);
+                        rep + uint64_t(j) * SK_PFQ_EPB + lo, changed, ev, ev_n);
         return;
     }
     for (uint32_t t = threadIdx.x; t < SK_PFP_HT; t += SK_PFP_ATPB) head[t] = 0xffffu;
     uint32_t t = sub;
-    for (; t + 4 < c; t += 8) { // two records per step: both loads, then both register loads, in flight
-        uint64_t ra = seg[t], rb = seg[t + 4];
+    for (; t + SK_PFQ_TPS < c; t += 2 * SK_PFQ_TPS) { // two records per step: both loads, then both register loads
+        uint64_t ra = seg[t], rb = seg[t + SK_PFQ_TPS];
         const uint32_t va = reg_get(slab_at(arena, ra >> 40), uint32_t(ra >> 26) & 16383u);
         const uint32_t vb = reg_get(slab_at(arena, rb >> 40), uint32_t(rb >> 26) & 16383u);
         R[dst + t] = ra;
-        R[dst + t + 4] = rb;
+        R[dst + t + SK_PFQ_TPS] = rb;
         r0[dst + t] = uint8_t(va);
-        r0[dst + t + 4] = uint8_t(vb);
+        r0[dst + t + SK_PFQ_TPS] = uint8_t(vb);
     }
     if (t < c) {
         uint64_t ra = seg[t];
@@ -793,8 +804,8 @@ __global__ void __launch_bounds__(SK_PFP_ATPB) __attribute__((amdgpu_waves_per_e
         if (wx[q]) reg_xor(slab_at(arena, wslot[q] >> 14), uint32_t(wslot[q]) & 16383u, wx[q]);
     if (changed) return;
     __syncthreads();
-    uint8_t *rs = rep + uint64_t(j) * SK_PFP_EPB + lo; // replies as runs, in the chunk's order
-    for (uint32_t u = sub; u < c; u += 4) rs[u] = r0[dst + u];
+    uint8_t *rs = rep + uint64_t(j) * SK_PFQ_EPB + lo; // replies as runs, in the chunk's order
+    for (uint32_t u = sub; u < c; u += SK_PFQ_TPS) rs[u] = r0[dst + u];
 }
 
 // ---------------------------------------------------------------- PFADD, line schedule (group apply)
@@ -4328,9 +4339,10 @@ hipError_t launch_murmur_long(hipStream_t st, uint32_t n_long, uint32_t n_wg, co
     return hipSuccess;
 }
 
-uint32_t pfp_blocks(uint64_t n) { return uint32_t((n + SK_PFP_EPB - 1) / SK_PFP_EPB); }
+uint32_t pfp_blocks(uint64_t n) { return uint32_t((n + SK_PFQ_EPB - 1) / SK_PFQ_EPB); } // partition path
 uint32_t pfp_buckets() { return SK_PFP_NB; }
-uint32_t pfp_epb() { return SK_PFP_EPB; }
+uint32_t pfp_epb() { return SK_PFQ_EPB; }
+static uint32_t pfl_blocks(uint64_t n) { return uint32_t((n + SK_PFP_EPB - 1) / SK_PFP_EPB); } // line schedule
 
 
 // hash + block-local bucket sort -> per-bucket LDS resolve; one launcher per stage so each is timed
@@ -4364,7 +4376,7 @@ hipError_t launch_pfp_reply(hipStream_t st, uint64_t n, const uint8_t *rep, cons
 // line schedule: layout of one call's scratch (PflDims) and its stages
 PflDims pfl_dims(uint64_t n, uint32_t nslab, uint32_t tile_blocks) {
     PflDims d;
-    d.nblk = pfp_blocks(n);
+    d.nblk = pfl_blocks(n);
     // permutation over 2^pk >= nslab ids (>= one fine bucket); a fine bucket = 2^sh consecutive permuted ids, of which
     // nslab / 2^pk are live: it expects n * 2^sh / (128 * 2^pk) records.  Keep that <= ~600 (one chunk of
     // SK_PFL_CAP with margin), within the LDS lines (2^SK_PFL_SH) and the region's fine-bucket counts (MAXSUB)
@@ -4403,7 +4415,7 @@ uint32_t pfl_max_slabs() { return (SK_PFL_MAXSUB << SK_PFL_SH) / 2; } // the per
 
 hipError_t launch_pfl_hash(hipStream_t st, uint64_t n, const uint32_t *key_ids, const uint64_t *off,
                            const uint8_t *bytes, int v5, uint64_t *chunks, uint32_t *S, uint32_t *big_alloc) {
-    uint32_t nb = pfp_blocks(n);
+    uint32_t nb = pfl_blocks(n);
     hipLaunchKernelGGL(k_pfl_hash, dim3(nb), dim3(SK_PFP_TPB), 0, st, n, key_ids, off, bytes, v5, chunks, S, nb,
                        big_alloc);
     SK_LAUNCH_CHECK();

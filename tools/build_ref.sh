@@ -6,7 +6,7 @@ R=$(cd "$(dirname "$0")/.." && pwd)
 NAME=$1; REF=${2:-HEAD}; DEFS=${3:-}
 O=$R/build/ref_$NAME; rm -rf $O; mkdir -p $O/redisson_amd/csrc $O/include
 for f in redisson_amd/csrc/sk_kernels.hip redisson_amd/csrc/sk_store.cpp redisson_amd/csrc/sk_device.h \
-         redisson_amd/csrc/sk_internal.h redisson_amd/csrc/sk_hllstr.h include/redisson_sketch.h; do
+         redisson_amd/csrc/sk_internal.h redisson_amd/csrc/sk_hllstr.h redisson_amd/csrc/sk_rdb.h include/redisson_sketch.h; do
   git -C $R show $REF:$f > $O/$f
 done
 cd $O/redisson_amd/csrc

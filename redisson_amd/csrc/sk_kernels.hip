@@ -3851,6 +3851,32 @@ __device__ __forceinline__ void lds_bitonic_u64(uint64_t *a, uint32_t P) {
             __syncthreads();
         }
 }
+// The same sort for P <= SBR_TPB keys held one per thread (threads >= P hold ~0 and only ever pair with each other):
+// the exchange stages within a wave (j < 64) go through shuffles with no barrier, the wider ones through two
+// alternating LDS buffers (one barrier each) -- 10 barriers for 1024 keys instead of 55
+__device__ __forceinline__ uint64_t bitonic_regs_u64(uint64_t x, uint32_t P, uint64_t *buf) {
+    const uint32_t t = threadIdx.x;
+    uint32_t nb = 0;
+    for (uint32_t k = 2; k <= P; k <<= 1)
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            uint64_t y;
+            if (j >= 64) { // uniform
+                uint64_t *b = buf + nb * SBR_TPB;
+                nb ^= 1u;
+                b[t] = x;
+                __syncthreads();
+                y = b[t ^ j];
+            } else {
+                const uint32_t hi = uint32_t(__shfl_xor(int(uint32_t(x >> 32)), int(j)));
+                const uint32_t lo = uint32_t(__shfl_xor(int(uint32_t(x)), int(j)));
+                y = (uint64_t(hi) << 32) | lo;
+            }
+            const bool up = (t & k) == 0, lower = (t & j) == 0;
+            const uint64_t mn = x < y ? x : y, mx = x < y ? y : x;
+            x = lower == up ? mn : mx;
+        }
+    return x;
+}
 __global__ void __launch_bounds__(SBR_TPB) k_sbr_runs(uint32_t ntile, const uint32_t *__restrict__ pbase,
                                                       const uint32_t *__restrict__ rs, uint64_t *recs, uint64_t *scr,
                                                       const SbrSeg *__restrict__ seg, uint32_t nseg,
@@ -3929,7 +3955,20 @@ __global__ void __launch_bounds__(SBR_TPB) k_sbr_runs(uint32_t ntile, const uint
         }
         __syncthreads();
     };
-    if (total <= SBR_RCAP) {
+    if (total <= SBR_TPB) { // one key per thread: sorted in registers and shuffles
+        uint32_t P = 2;
+        while (P < total) P <<= 1;
+        uint64_t x = threadIdx.x < total ? recs[slot(threadIdx.x)] & KMASK : ~0ull;
+        static_assert(2 * SBR_TPB <= SBR_RCAP + 2, "two exchange buffers in key[]");
+        x = bitonic_regs_u64(x, P, key);
+        __syncthreads(); // the exchange buffers read
+        if (threadIdx.x < P) key[threadIdx.x + 1] = x;
+        if (threadIdx.x == 0) key[0] = ~0ull;
+        __syncthreads();
+        if (threadIdx.x == 0) key[total + 1] = ~0ull;
+        __syncthreads();
+        apply_sorted(total);
+    } else if (total <= SBR_RCAP) {
         uint32_t P = 2;
         while (P < total) P <<= 1;
         for (uint32_t i = threadIdx.x; i < P; i += SBR_TPB) key[i + 1] = i < total ? recs[slot(i)] & KMASK : ~0ull;

@@ -1673,18 +1673,20 @@ __global__ void __launch_bounds__(256) k_hll_sum(uint64_t n, const uint32_t *__r
 // LDS array 39 % busy, VALU 27 % (profiles/r03j_hist_sq_summary.json).
 // PK: slabs ids[k] of the packed arena; else u8 register arrays (ids[k] = 0 with the array as `arena`: a union's
 // temporary registers, sk_hll_count_registers_dev)
-#ifndef SK_HH16
-#define SK_HH16 1 // 16-bit counters, two bins per LDS word: 8 KiB per wave, 20 waves per CU instead of 10
-#endif
+// Round 6: 16-bit halves of 8 KiB per wave (20 waves per CU): row r & 31 of lane l counts bin r in its low half and
+// bin r + 32 in its high half.  Registers >= 32 need 31 leading zero bits of a hash, so a lane whose 16-register
+// group holds none (one test of the fields' bit 5 per group) adds a constant 1 at row (r & 31) -- a 5-bit field
+// extract and one shift-or per register -- and only a group with one takes the per-register increment.  Lanes 2 x
+// 32 then sum the two halves of each row.  (u32 counters, 64 rows at 16 KiB per wave: 0.290 ms per 100 k keys;
+// bins 2i / 2i + 1 in the halves with a computed increment per register: 0.276 ms.)
 template <bool PK>
 __global__ void __launch_bounds__(64) k_hll_hist(uint64_t n, const uint32_t *__restrict__ ids,
                                                    const uint8_t *__restrict__ arena, uint32_t *__restrict__ hist) {
-    constexpr int ROWS = SK_HH16 ? 32 : 64; // SK_HH16: bins 2i and 2i + 1 as the halves of row i's words
-    __shared__ uint4 h4[ROWS * 16];
+    __shared__ uint4 h4[32 * 16];
     uint32_t *h = reinterpret_cast<uint32_t *>(h4);
-    const uint32_t lane = threadIdx.x;
+    const uint32_t lane = threadIdx.x, l4 = lane * 4u;
 #pragma unroll
-    for (int j = 0; j < ROWS / 4; j++) h4[lane + 64 * j] = make_uint4(0, 0, 0, 0);
+    for (int j = 0; j < 8; j++) h4[lane + 64 * j] = make_uint4(0, 0, 0, 0);
     // a lane's 16 groups of 16 registers: groups it * 64 + lane (packed: three words each; u8: one 16-B vector)
     auto load = [&](uint64_t key, uint32_t (&v)[16][4]) {
         if constexpr (PK) {
@@ -1702,50 +1704,56 @@ __global__ void __launch_bounds__(64) k_hll_hist(uint64_t n, const uint32_t *__r
             }
         }
     };
+    auto add = [&](uint32_t byteaddr, uint32_t inc) {
+        __hip_atomic_fetch_add(reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(h) + byteaddr), inc,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    };
     auto count = [&](uint64_t key, const uint32_t (&v)[16][4]) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
 #pragma unroll
         for (int it = 0; it < 16; it++) {
-            const uint4 u = PK ? unpack16(v[it][0], v[it][1], v[it][2]) : make_uint4(v[it][0], v[it][1], v[it][2], v[it][3]);
-            const uint32_t ws[4] = {u.x, u.y, u.z, u.w};
+            uint32_t src[16], pos[16];
+            bool big;
+            if constexpr (PK) {
+                const uint32_t w0 = v[it][0], w1 = v[it][1], w2 = v[it][2];
+                // bit 5 of fields 0-4 / 6-9 (+ field 5's) / 10-15: any register >= 32 in the group
+                big = ((w0 & 0x20820820u) | (w1 & 0x08208208u) | (w2 & 0x82082082u)) != 0u;
+                const uint32_t x5 = __builtin_amdgcn_alignbit(w1, w0, 30), x10 = __builtin_amdgcn_alignbit(w2, w1, 28);
+                const uint32_t sw[16] = {w0, w0, w0, w0, w0, x5, w1, w1, w1, w1, x10, w2, w2, w2, w2, w2};
+                const uint32_t sp[16] = {0, 6, 12, 18, 24, 0, 4, 10, 16, 22, 0, 2, 8, 14, 20, 26};
 #pragma unroll
-            for (int w = 0; w < 4; w++)
+                for (int j = 0; j < 16; j++) src[j] = sw[j], pos[j] = sp[j];
+            } else {
+                big = ((v[it][0] | v[it][1] | v[it][2] | v[it][3]) & 0x20202020u) != 0u;
 #pragma unroll
-                for (int b = 0; b < 4; b++) {
-                    const uint32_t r = (ws[w] >> (8 * b)) & 63u;
-                    if (SK_HH16)
-                        __hip_atomic_fetch_add(&h[(r >> 1) * 64 + lane], 1u << ((r & 1u) << 4), __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_WAVEFRONT);
-                    else
-                        __hip_atomic_fetch_add(&h[r * 64 + lane], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+                for (int j = 0; j < 16; j++) src[j] = v[it][j >> 2], pos[j] = 8u * (j & 3);
+            }
+            if (!big) { // row = the field's low 5 bits, +1 in the low half
+#pragma unroll
+                for (int j = 0; j < 16; j++) add((__builtin_amdgcn_ubfe(src[j], pos[j], 5) << 8) | l4, 1u);
+            } else {
+#pragma unroll
+                for (int j = 0; j < 16; j++) {
+                    const uint32_t r = __builtin_amdgcn_ubfe(src[j], pos[j], 6);
+                    add(((r & 31u) << 8) | l4, (r & 32u) ? 65536u : 1u);
                 }
+            }
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
         __builtin_amdgcn_wave_barrier();
+        // lanes b and b + 32 sum the two halves of row b & 31, then add each other's: bin b in the low half, b + 32 in
+        // the high (64 lanes x <= 256 registers per bin: no carry out of a half)
         uint32_t c = 0;
-        if (SK_HH16) {
-            // lanes 2i and 2i + 1 sum the two halves of row i (64 lanes x <= 256 registers per bin: no carry out of
-            // a 16-bit half), then add each other's: bin 2i in the low half, 2i + 1 in the high half
 #pragma unroll
-            for (int j = 0; j < 8; j++) {
-                const uint32_t q = (lane >> 1) * 16 + (lane & 1u) * 8 + ((j + (lane >> 1)) & 7u);
-                const uint4 x = h4[q];
-                c += x.x + x.y + x.z + x.w;
-                h4[q] = make_uint4(0, 0, 0, 0);
-            }
-            c += __shfl_xor(c, 1);
-            c = (lane & 1u) ? c >> 16 : c & 0xffffu;
-        } else {
-#pragma unroll
-            for (int j = 0; j < 16; j++) {
-                const uint32_t q = lane * 16 + ((j + lane) & 15u);
-                const uint4 x = h4[q];
-                c += x.x + x.y + x.z + x.w;
-                h4[q] = make_uint4(0, 0, 0, 0);
-            }
+        for (int j = 0; j < 8; j++) {
+            const uint32_t q = (lane & 31u) * 16 + (lane >> 5) * 8 + ((j + lane) & 7u);
+            const uint4 x = h4[q];
+            c += x.x + x.y + x.z + x.w;
+            h4[q] = make_uint4(0, 0, 0, 0);
         }
-        hist[key * 64 + lane] = c;
+        c += __shfl_xor(c, 32);
+        hist[key * 64 + lane] = lane < 32u ? c & 0xffffu : c >> 16;
     };
     const uint64_t G = gridDim.x;
     uint32_t v[16][4];

@@ -154,6 +154,50 @@ def test_hll_histogram_many_keys(engine, O):
     np.testing.assert_array_equal(h, want)
 
 
+def test_hll_histogram_high_registers(engine, O):
+    """k_hll_hist counts a register r at row r & 31 (+1 in the low half, +65536 for r >= 32 in the high half) and takes
+    the per-register increment only in 16-register groups holding a register >= 32: keys whose every group has one
+    (registers uniform over 0..63), keys with a few high registers (single groups on the slow path), and keys with
+    none; packed arena rows (k_hll_hist<true>) equal np.bincount, and the u8 form (k_hll_hist<false>, PFCOUNT of a
+    raw register array, registers clamped to Redis's 0..51) gives the oracle's redis >= 5 count, whose q + 1 bin (51)
+    weighs on the estimate."""
+    from redisson_amd import SketchEngine
+    rng = np.random.default_rng(78)
+    regs = []
+    for i in range(24):
+        kind = i % 3
+        if kind == 0:
+            r = rng.integers(0, 64, 16384, dtype=np.uint8)
+        elif kind == 1:
+            r = rng.integers(0, 32, 16384, dtype=np.uint8)
+            hot = rng.integers(0, 16384, 1 + i)
+            r[hot] = rng.integers(32, 64, len(hot), dtype=np.uint8)
+            r[hot[:1]] = 51
+        else:
+            r = rng.integers(0, 32, 16384, dtype=np.uint8)
+        regs.append(r)
+    names = [b"hh64:%d" % i for i in range(len(regs))]
+    ids = engine.hll_resolve(names)
+    for nm, r in zip(names, regs):
+        d = engine.to_device(r)
+        engine.hll_merge_registers_dev(nm, d)
+        d.free()
+    d_hist = engine.alloc(len(regs) * 64 * 4)
+    engine.hll_histogram_dev(len(regs), engine.to_device(ids), d_hist)
+    h = d_hist.download(np.uint32).reshape(len(regs), 64)
+    want = np.stack([np.bincount(r, minlength=64) for r in regs]).astype(np.uint32)
+    np.testing.assert_array_equal(h, want)
+    e5 = SketchEngine(device=0, redis_major=5)
+    try:
+        for r in regs:
+            r = np.minimum(r, 51).astype(np.uint8)   # registers a redis >= 5 histogram holds (q + 2 = 52 bins)
+            d = e5.to_device(r)
+            assert e5.hll_count_registers_dev(d) == O.count_regs(r, 1, 5)
+            d.free()
+    finally:
+        e5.close()
+
+
 # ------------------------------------------------------------------- Bloom
 @pytest.mark.parametrize("n_exp,p", [(100, 0.03), (20000, 0.01), (5000, 0.5)])
 def test_bloom_add_contains(engine, O, n_exp, p):
